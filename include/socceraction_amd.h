@@ -1,0 +1,183 @@
+/*
+ * socceraction_amd.h — C ABI of the MI355X (gfx950) valuation-path library
+ * (libsocceraction_amd.so).  Plain pointers and sizes only: every array pointer
+ * below is a *device* pointer (HBM) unless marked [host]; streams are hipStream_t
+ * passed as void*.  All calls are asynchronous on the given stream unless noted.
+ *
+ * The reference (rtelmore/socceraction) is pure Python/pandas and has no native
+ * FFI.  Each entry point below replaces the pandas implementation of one
+ * reference function on the hot path; the Python drop-in layer
+ * (socceraction_amd/_native.py) binds them with ctypes exactly as INTEGRATION.md
+ * shows.  Reference citations are file:line into /root/reference.
+ *
+ * Conventions
+ *  - return 0 on success, a negative SA_E* code on failure; sa_last_error()
+ *    returns a thread-local message.  No C++ exception crosses this ABI.
+ *  - the caller owns every buffer.  Output blocks are column-major [cols][ld]
+ *    (one contiguous run of `ld` elements per feature column, matching pandas'
+ *    2-D block layout); ld % 16 == 0 and ld >= round_up(n, 16).  Rows n..ld-1 of
+ *    every output column are scratch (may be overwritten).
+ *  - input columns are length-n arrays, 16-byte aligned.
+ *  - ids are uint8 (SPADL type 0-22, result 0-5, bodypart 0-3, period 1-5; atomic
+ *    type 0-32); team ids are int32 codes whose equality equals the equality of
+ *    the original team ids (a factorisation); coordinates and times are float64.
+ */
+#ifndef SOCCERACTION_AMD_H
+#define SOCCERACTION_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SA_ABI_VERSION 1
+#define SA_MAX_FRAMES 8 /* max nb_prev_actions (window frames) */
+
+enum sa_status {
+  SA_OK = 0,
+  SA_EINVAL = -1,   /* bad argument (maps to ValueError) */
+  SA_EHIP = -2,     /* HIP runtime error */
+  SA_EDATA = -3,    /* input data error, e.g. non-finite xT coordinates (ValueError) */
+  SA_ENOMEM = -4,   /* scratch allocation failed */
+};
+
+/* One frame of action columns.  SPADL: c0..c3 = start_x, start_y, end_x, end_y.
+ * Atomic-SPADL: c0..c3 = x, y, dx, dy.  result_id is ignored for atomic. */
+typedef struct sa_frame {
+  const double* c0;
+  const double* c1;
+  const double* c2;
+  const double* c3;
+  const double* time_seconds;
+  const uint8_t* type_id;
+  const uint8_t* result_id;
+  const uint8_t* bodypart_id;
+  const uint8_t* period_id;
+  const int32_t* team;
+} sa_frame;
+
+/* A batch of actions split into segments (games).
+ *  - n_frames == 1: "windowed" mode, the batched game-state path.  Game-state
+ *    window i of action j is row max(j - i, segment start) of frames[0]
+ *    (reference vaep/features.py:62-88 gamestates), and if home_team != NULL the
+ *    coordinates of every window row are flipped when team[j] != home_team[seg]
+ *    (vaep/features.py:91-116 play_left_to_right, keyed on the *current* action).
+ *  - n_frames == k > 1: "explicit" mode for the module-level transformers that
+ *    receive a user-built list of k frames: window i of row j is row j of
+ *    frames[i]; no flip (the frames are already flipped).  n_segments must be 1.
+ * Module-level reference functions treat a whole frame as ONE segment. */
+typedef struct sa_actions {
+  int64_t n;
+  int64_t n_segments;
+  const int64_t* seg_off;   /* [n_segments + 1], seg_off[0] = 0, seg_off[n_segments] = n */
+  const int32_t* home_team; /* [n_segments] team code of the home team, or NULL (no flip) */
+  int32_t n_frames;
+  int32_t atomic;           /* 0 = SPADL, 1 = Atomic-SPADL */
+  sa_frame frames[SA_MAX_FRAMES];
+} sa_actions;
+
+/* Feature transformers (reference vaep/features.py, atomic/vaep/features.py). */
+enum sa_xfn {
+  SA_XFN_ACTIONTYPE = 0,            /* features.py:151-165        i64 x k   */
+  SA_XFN_ACTIONTYPE_ONEHOT,         /* features.py:168-186 (atomic: atomic/vaep/features.py:114-132) bool */
+  SA_XFN_RESULT,                    /* features.py:189-203        i64 x k   */
+  SA_XFN_RESULT_ONEHOT,             /* features.py:206-224        bool 6k   */
+  SA_XFN_ACTIONTYPE_RESULT_ONEHOT,  /* features.py:227-247        bool 138k */
+  SA_XFN_BODYPART,                  /* features.py:250-264        i64 x k   */
+  SA_XFN_BODYPART_ONEHOT,           /* features.py:267-285        bool 4k   */
+  SA_XFN_TIME,                      /* features.py:288-314        i64 k + f64 2k */
+  SA_XFN_STARTLOCATION,             /* features.py:317-331        f64 2k    */
+  SA_XFN_ENDLOCATION,               /* features.py:334-348        f64 2k    */
+  SA_XFN_STARTPOLAR,                /* features.py:355-377        f64 2k    */
+  SA_XFN_ENDPOLAR,                  /* features.py:380-402        f64 2k    */
+  SA_XFN_MOVEMENT,                  /* features.py:405-424        f64 3k    */
+  SA_XFN_TEAM,                      /* features.py:430-452        bool k-1  */
+  SA_XFN_TIME_DELTA,                /* features.py:455-473        f64 k-1   */
+  SA_XFN_SPACE_DELTA,               /* features.py:476-499        f64 3(k-1) */
+  SA_XFN_GOALSCORE,                 /* features.py:505-539 (atomic: atomic/vaep/features.py:229-260) i64 3 */
+  SA_XFN_LOCATION,                  /* atomic/vaep/features.py:135-149  f64 2k */
+  SA_XFN_POLAR,                     /* atomic/vaep/features.py:152-178  f64 2k */
+  SA_XFN_MOVEMENT_POLAR,            /* atomic/vaep/features.py:181-200  f64 2k */
+  SA_XFN_DIRECTION,                 /* atomic/vaep/features.py:203-226  f64 2k */
+  SA_XFN_COUNT
+};
+
+/* Where each requested transformer writes: first column index inside the bool,
+ * f64 and i64 output blocks (-1 = not requested / no columns of that dtype). */
+typedef struct sa_feature_plan {
+  int32_t nb_prev_actions;            /* k, 1..SA_MAX_FRAMES */
+  int32_t bool_col[SA_XFN_COUNT];
+  int32_t f64_col[SA_XFN_COUNT];
+  int32_t i64_col[SA_XFN_COUNT];
+} sa_feature_plan;
+
+/* ---- VAEP / Atomic-VAEP ------------------------------------------------------
+ * Replaces VAEP.compute_features (vaep/base.py:97-116): gamestates + flip + the
+ * transformers of `plan`, for every segment of `a` at once.  Blocks may be NULL
+ * when the plan writes no column of that dtype. */
+int sa_vaep_features(const sa_actions* a, const sa_feature_plan* plan, uint8_t* bool_out,
+                     double* f64_out, int64_t* i64_out, int64_t ld, void* stream);
+
+/* Replaces labels.scores / concedes / goal_from_shot (vaep/labels.py:9-116;
+ * atomic/vaep/labels.py:9-107): look-ahead of nr_actions (>=1) clamped at each
+ * segment's last row.  Any output may be NULL.  Outputs are length-ld bool bytes. */
+int sa_vaep_labels(const sa_actions* a, int32_t nr_actions, uint8_t* scores, uint8_t* concedes,
+                   uint8_t* goal_from_shot, int64_t ld, void* stream);
+
+/* Replaces formula.value (vaep/formula.py:116-151; atomic/vaep/formula.py:116-141)
+ * with float64 probabilities; outputs offensive, defensive, vaep (length ld). */
+int sa_vaep_formula_f64(const sa_actions* a, const double* p_scores, const double* p_concedes,
+                        double* off, double* def, double* val, void* stream);
+/* Same with float32 probabilities (the reference keeps the probability dtype). */
+int sa_vaep_formula_f32(const sa_actions* a, const float* p_scores, const float* p_concedes,
+                        float* off, float* def, float* val, void* stream);
+
+/* ---- Expected Threat (xthreat.py) --------------------------------------------
+ * Count pass over SPADL actions (frames[0] of `a`; segments ignored):
+ * shot[c] += shots (type 11) by start cell, goal[c] += successful shots,
+ * move[c] += moves (type pass/dribble/cross, any result) by start cell,
+ * trans[s*C+e] += successful moves s->e  (xthreat.py:40-67, 74-98, 144-218).
+ * Accumulates into the caller's zeroed buffers (RCCL-reducible), C = l*w.
+ * NaN start coordinates are dropped from shot/goal/move counts (`_count`); a
+ * non-finite coordinate that the reference would cast to int64 sets a bit in
+ * *err_flags (device int32): 1 = non-finite shot start, 2 = non-finite move coord. */
+int sa_xt_count(const sa_actions* a, int32_t l, int32_t w, int64_t* shot, int64_t* goal,
+                int64_t* move, int32_t* trans, int32_t* err_flags, void* stream);
+
+/* Normalise the counts into the reference's matrices and run the value iteration
+ * x <- s*p_shot + p_move * (T x) until no cell changes by more than eps
+ * (xthreat.py:278-345).  Writes (all float64, device):
+ *   mats[4*C] = scoring_prob | shot_prob | move_prob | xT  (row-major w x l each)
+ *   trans_t[C*C] = transition matrix TRANSPOSED (trans_t[e*C+s] = T[s,e])
+ *   heatmaps[(max_iter+1)*C] = x after 0..n_iter iterations
+ * *n_iter [host] receives the iteration count (-1: max_iter reached first).
+ * Synchronises the stream. */
+int sa_xt_solve(const int64_t* shot, const int64_t* goal, const int64_t* move,
+                const int32_t* trans, int32_t l, int32_t w, double eps, int32_t max_iter,
+                double* mats, double* trans_t, double* heatmaps, int32_t* n_iter, void* stream);
+
+/* Interpolated surface for ExpectedThreat.rate(use_interpolation=True)
+ * (xthreat.py:347-378, 443-451): grid[r*L + h] = bilinear(xT; xs[h], ys[r]) over
+ * cell centres cx[l], cy[w] ([device] f64), clamped to the centre hull, with
+ * xs = linspace(0,105,L), ys = linspace(0,68,W). */
+int sa_xt_interp_grid(const double* xT, const double* cx, const double* cy, int32_t l, int32_t w,
+                      int32_t L, int32_t W, double* grid, void* stream);
+
+/* ExpectedThreat.rate (xthreat.py:408-465): out[j] = grid[W-1-yj(end), xi(end)] -
+ * grid[W-1-yj(start), xi(start)] for successful moves, NaN otherwise.  A non-finite
+ * coordinate of a successful move (the reference's int64 cast raises) sets bit 4 in
+ * *err_flags (device int32, may be NULL). */
+int sa_xt_rate(const sa_actions* a, const double* grid, int32_t L, int32_t W, double* out,
+               int32_t* err_flags, void* stream);
+
+/* ---- misc -------------------------------------------------------------------- */
+int sa_abi_version(void);
+const char* sa_last_error(void);
+/* Device-side timing of the last launch of each kernel family is not kept here;
+ * benchmarks time with HIP events on the caller's stream. */
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SOCCERACTION_AMD_H */

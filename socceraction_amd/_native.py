@@ -1,0 +1,115 @@
+"""ctypes binding of ``libsocceraction_amd.so`` (the C ABI in ``include/socceraction_amd.h``).
+
+This module is the *only* way the Python layer reaches the HIP kernels. There is no
+CPU fallback: if the shared library is missing or no ROCm GPU is visible, every
+compute entry point raises. The library is built in-tree by
+``python -m socceraction_amd.build`` (or ``__graft_entry__.build()``).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, '_lib', 'libsocceraction_amd.so')
+
+SA_MAX_FRAMES = 8
+SA_OK, SA_EINVAL, SA_EHIP, SA_EDATA, SA_ENOMEM = 0, -1, -2, -3, -4
+
+# enum sa_xfn (order matters: mirrors include/socceraction_amd.h)
+XFN_NAMES = [
+    'actiontype', 'actiontype_onehot', 'result', 'result_onehot', 'actiontype_result_onehot',
+    'bodypart', 'bodypart_onehot', 'time', 'startlocation', 'endlocation', 'startpolar',
+    'endpolar', 'movement', 'team', 'time_delta', 'space_delta', 'goalscore', 'location',
+    'polar', 'movement_polar', 'direction',
+]
+XFN = {name: i for i, name in enumerate(XFN_NAMES)}
+SA_XFN_COUNT = len(XFN_NAMES)
+
+_p = ctypes.c_void_p
+
+
+class SaFrame(ctypes.Structure):
+    _fields_ = [('c0', _p), ('c1', _p), ('c2', _p), ('c3', _p), ('time_seconds', _p),
+                ('type_id', _p), ('result_id', _p), ('bodypart_id', _p), ('period_id', _p),
+                ('team', _p)]
+
+
+class SaActions(ctypes.Structure):
+    _fields_ = [('n', ctypes.c_int64), ('n_segments', ctypes.c_int64), ('seg_off', _p),
+                ('home_team', _p), ('n_frames', ctypes.c_int32), ('atomic', ctypes.c_int32),
+                ('frames', SaFrame * SA_MAX_FRAMES)]
+
+
+class SaFeaturePlan(ctypes.Structure):
+    _fields_ = [('nb_prev_actions', ctypes.c_int32),
+                ('bool_col', ctypes.c_int32 * SA_XFN_COUNT),
+                ('f64_col', ctypes.c_int32 * SA_XFN_COUNT),
+                ('i64_col', ctypes.c_int32 * SA_XFN_COUNT)]
+
+
+# name -> (restype, argtypes)
+_SIGNATURES = {
+    'sa_vaep_features': (ctypes.c_int, [ctypes.POINTER(SaActions), ctypes.POINTER(SaFeaturePlan),
+                                        _p, _p, _p, ctypes.c_int64, _p]),
+    'sa_vaep_labels': (ctypes.c_int, [ctypes.POINTER(SaActions), ctypes.c_int32, _p, _p, _p,
+                                      ctypes.c_int64, _p]),
+    'sa_vaep_formula_f64': (ctypes.c_int, [ctypes.POINTER(SaActions), _p, _p, _p, _p, _p, _p]),
+    'sa_vaep_formula_f32': (ctypes.c_int, [ctypes.POINTER(SaActions), _p, _p, _p, _p, _p, _p]),
+    'sa_xt_count': (ctypes.c_int, [ctypes.POINTER(SaActions), ctypes.c_int32, ctypes.c_int32,
+                                   _p, _p, _p, _p, _p, _p]),
+    'sa_xt_solve': (ctypes.c_int, [_p, _p, _p, _p, ctypes.c_int32, ctypes.c_int32,
+                                   ctypes.c_double, ctypes.c_int32, _p, _p, _p,
+                                   ctypes.POINTER(ctypes.c_int32), _p]),
+    'sa_xt_interp_grid': (ctypes.c_int, [_p, _p, _p, ctypes.c_int32, ctypes.c_int32,
+                                         ctypes.c_int32, ctypes.c_int32, _p, _p]),
+    'sa_xt_rate': (ctypes.c_int, [ctypes.POINTER(SaActions), _p, ctypes.c_int32, ctypes.c_int32,
+                                  _p, _p, _p]),
+    'sa_abi_version': (ctypes.c_int, []),
+    'sa_last_error': (ctypes.c_char_p, []),
+}
+EXPORTED_SYMBOLS = tuple(_SIGNATURES)
+
+_lib: Optional[ctypes.CDLL] = None
+
+
+class NativeError(RuntimeError):
+    """A HIP runtime failure inside libsocceraction_amd."""
+
+
+def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
+    """dlopen the library and declare every signature (no GPU needed)."""
+    global _lib
+    if _lib is not None and path == LIB_PATH:
+        return _lib
+    if not os.path.exists(path):
+        raise ImportError(
+            f'{path} is missing: build the HIP library first '
+            '(python -m socceraction_amd.build). socceraction_amd has no CPU fallback.')
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in _SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.sa_abi_version() != 1:
+        raise ImportError('libsocceraction_amd ABI version mismatch')
+    if path == LIB_PATH:
+        _lib = lib
+    return lib
+
+
+def lib() -> ctypes.CDLL:
+    return load_library()
+
+
+def check(rc: int) -> None:
+    """Map a C-ABI status to the reference's exception types."""
+    if rc == SA_OK:
+        return
+    msg = (lib().sa_last_error() or b'').decode(errors='replace')
+    if rc in (SA_EINVAL, SA_EDATA):
+        raise ValueError(msg)
+    if rc == SA_ENOMEM:
+        raise MemoryError(msg)
+    raise NativeError(f'libsocceraction_amd error {rc}: {msg}')

@@ -1,0 +1,438 @@
+// Expected Threat (xT) kernels for gfx950: binning + counts, normalisation, value
+// iteration, interpolated surface and rate.  Reference: socceraction/xthreat.py.
+//
+// Binning reproduces `_get_cell_indexes` bit for bit: (x / 105) * l in f64 (divide
+// THEN multiply), truncation toward zero like numpy's int64 cast, clip to [0, l-1].
+// The value iteration keeps the reference's summation order exactly: for each cell r
+// total = sum_{c=0}^{C-1} T[r,c] * x[c], accumulated left to right in f64 with
+// separate multiply and add (xthreat.py:306-312), so iterates and the iteration count
+// are bit-identical to the pandas path.  T is kept transposed (Tt[c*C + r]) so that at
+// step c the lanes of a wave read one contiguous run of rows (coalesced).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <vector>
+
+#include "sa_common.h"
+#include "sa_internal.h"
+
+namespace sa {
+
+// numpy float64 -> int64 cast (x86 cvttsd2si: NaN / out of range -> INT64_MIN), then clip.
+__device__ __forceinline__ int cell_index(double v, int l) {
+  long long c = (v >= -9.2233720368547758e18 && v < 9.2233720368547758e18) ? (long long)v
+                                                                             : (long long)INT64_MIN;
+  return c < 0 ? 0 : (c > l - 1 ? l - 1 : (int)c);
+}
+
+__device__ __forceinline__ int flat_index(double x, double y, int l, int w) {
+  int xi = cell_index(x / FIELD_L * (double)l, l);
+  int yj = cell_index(y / FIELD_W * (double)w, w);
+  return (w - 1 - yj) * l + xi;
+}
+
+__device__ __forceinline__ bool is_move(int t) { return t == T_PASS || t == T_DRIBBLE || t == T_CROSS; }
+
+// ---------------------------------------------------------------------------------------------
+// Count pass.  SMALL: per-workgroup LDS histograms (u32 for the three C-vectors, the C x C
+// transition counts packed two u16 per word), flushed with one global atomic per non-zero
+// bin; a workgroup handles <= 65535 actions so a u16 bin cannot overflow.  Otherwise global
+// atomics straight into the caller's buffers.
+constexpr int XT_THREADS = 256;
+constexpr int XT_SMALL_ACTS = 32768;  // actions per workgroup in the LDS-privatised form
+
+template <bool SMALL>
+__global__ __launch_bounds__(XT_THREADS) void xt_count_kernel(sa_actions A, int l, int w,
+                                                             unsigned long long* __restrict__ shot,
+                                                             unsigned long long* __restrict__ goal,
+                                                             unsigned long long* __restrict__ move,
+                                                             int32_t* __restrict__ trans,
+                                                             int32_t* __restrict__ err) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  const int C = l * w;
+  const int64_t n = A.n;
+  const sa_frame& F = A.frames[0];
+  uint32_t* hs = lds;          // [C]
+  uint32_t* hg = lds + C;      // [C]
+  uint32_t* hm = lds + 2 * C;  // [C]
+  uint32_t* ht = lds + 3 * C;  // [(C*C+1)/2] packed u16 pairs
+  int64_t begin, end, stride;
+  if (SMALL) {
+    const int tw = (C * C + 1) / 2;
+    for (int k = threadIdx.x; k < 3 * C + tw; k += blockDim.x) lds[k] = 0;
+    __syncthreads();
+    begin = (int64_t)blockIdx.x * XT_SMALL_ACTS + threadIdx.x;
+    end = min(n, (int64_t)(blockIdx.x + 1) * XT_SMALL_ACTS);
+    stride = blockDim.x;
+  } else {
+    begin = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    end = n;
+    stride = (int64_t)gridDim.x * blockDim.x;
+  }
+  int32_t bad = 0;
+  for (int64_t j = begin; j < end; j += stride) {
+    const int t = F.type_id[j];
+    const bool shot_t = t == T_SHOT, move_t = is_move(t);
+    if (!shot_t && !move_t) continue;
+    const double sx = F.c0[j], sy = F.c1[j];
+    const int r = F.result_id[j];
+    if (shot_t) {
+      if (isnan(sx) || isnan(sy)) continue;  // _count drops NaN rows (xthreat.py:60-61)
+      if (!isfinite(sx) || !isfinite(sy)) {
+        bad |= 1;
+        continue;
+      }
+      const int c = flat_index(sx, sy, l, w);
+      if (SMALL) {
+        atomicAdd(&hs[c], 1u);
+        if (r == R_SUCCESS) atomicAdd(&hg[c], 1u);
+      } else {
+        atomicAdd(&shot[c], 1ull);
+        if (r == R_SUCCESS) atomicAdd(&goal[c], 1ull);
+      }
+    } else {
+      const double ex = F.c2[j], ey = F.c3[j];
+      if (!isfinite(sx) || !isfinite(sy) || !isfinite(ex) || !isfinite(ey)) {
+        bad |= 2;  // move_transition_matrix casts every move coordinate to int64
+        continue;
+      }
+      const int cs = flat_index(sx, sy, l, w);
+      if (SMALL)
+        atomicAdd(&hm[cs], 1u);
+      else
+        atomicAdd(&move[cs], 1ull);
+      if (r == R_SUCCESS) {
+        const int ce = flat_index(ex, ey, l, w);
+        const int64_t k = (int64_t)cs * C + ce;
+        if (SMALL)
+          atomicAdd(&ht[k >> 1], (k & 1) ? 0x10000u : 1u);
+        else
+          atomicAdd(&trans[k], 1);
+      }
+    }
+  }
+  if (bad) atomicOr(err, bad);
+  if (SMALL) {
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+      if (hs[c]) atomicAdd(&shot[c], (unsigned long long)hs[c]);
+      if (hg[c]) atomicAdd(&goal[c], (unsigned long long)hg[c]);
+      if (hm[c]) atomicAdd(&move[c], (unsigned long long)hm[c]);
+    }
+    const int tw = (C * C + 1) / 2;
+    for (int k = threadIdx.x; k < tw; k += blockDim.x) {
+      const uint32_t v = ht[k];
+      if (v & 0xFFFFu) atomicAdd(&trans[2 * k], (int32_t)(v & 0xFFFFu));
+      if (v >> 16) atomicAdd(&trans[2 * k + 1], (int32_t)(v >> 16));
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Normalisation (xthreat.py:70-98, 144-174, 177-218).
+__global__ void xt_prob_kernel(const unsigned long long* __restrict__ shot,
+                               const unsigned long long* __restrict__ goal,
+                               const unsigned long long* __restrict__ move, int C,
+                               double* __restrict__ mats, double* __restrict__ gs,
+                               double* __restrict__ pmove) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const double s = (double)shot[c], g = (double)goal[c], m = (double)move[c];
+  const double tot = m + s;
+  const double ps = s != 0.0 ? g / s : 0.0;  // _safe_divide
+  const double pshot = tot != 0.0 ? s / tot : 0.0;
+  const double pm = tot != 0.0 ? m / tot : 0.0;
+  mats[c] = ps;
+  mats[C + c] = pshot;
+  mats[2 * C + c] = pm;
+  gs[c] = ps * pshot;
+  pmove[c] = pm;
+}
+
+// Tt[e*C + s] = trans[s*C + e] / move[s]  (32x32 LDS-tiled transpose; rows with no moves stay 0)
+__global__ __launch_bounds__(256) void xt_transpose_kernel(const int32_t* __restrict__ trans,
+                                                           const unsigned long long* __restrict__ move,
+                                                           int C, double* __restrict__ Tt) {
+  __shared__ double tile[32][33];
+  const int s0 = blockIdx.y * 32, e0 = blockIdx.x * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+  for (int k = ty; k < 32; k += 8) {
+    const int s = s0 + k, e = e0 + tx;
+    double v = 0.0;
+    if (s < C && e < C) {
+      const int32_t cnt = trans[(int64_t)s * C + e];
+      v = cnt != 0 ? (double)cnt / (double)move[s] : 0.0;
+    }
+    tile[k][tx] = v;
+  }
+  __syncthreads();
+  for (int k = ty; k < 32; k += 8) {
+    const int e = e0 + k, s = s0 + tx;
+    if (s < C && e < C) Tt[(int64_t)e * C + s] = tile[tx][k];
+  }
+}
+
+// One value-iteration step for C rows; row r = one lane, sequential sum over c.
+__device__ __forceinline__ double row_payoff(const double* __restrict__ Tt, const double* __restrict__ x,
+                                             int C, int r) {
+  double acc = 0.0;
+  int c = 0;
+  for (; c + 8 <= C; c += 8) {
+    double tv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) tv[u] = Tt[(int64_t)(c + u) * C + r];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const double p = tv[u] * x[c + u];
+      acc = acc + p;
+    }
+  }
+  for (; c < C; ++c) {
+    const double p = Tt[(int64_t)c * C + r] * x[c];
+    acc = acc + p;
+  }
+  return acc;
+}
+
+// Small grids: one persistent workgroup runs every iteration; x lives in LDS.
+constexpr int XT_SOLVE_MAX_C = 1024;
+
+__global__ __launch_bounds__(1024) void xt_solve_small_kernel(const double* __restrict__ Tt,
+                                                              const double* __restrict__ gs,
+                                                              const double* __restrict__ pmove, int C,
+                                                              double eps, int max_iter,
+                                                              double* __restrict__ heat,
+                                                              double* __restrict__ xT_out,
+                                                              int32_t* __restrict__ n_iter) {
+  __shared__ double xs[XT_SOLVE_MAX_C];
+  const int r = threadIdx.x;
+  if (r < C) {
+    xs[r] = 0.0;
+    heat[r] = 0.0;
+  }
+  __syncthreads();
+  int it = 0;
+  bool cont = true;
+  while (cont && it < max_iter) {
+    double nx = 0.0;
+    int flag = 0;
+    if (r < C) {
+      const double tot = row_payoff(Tt, xs, C, r);
+      const double mv = pmove[r] * tot;
+      nx = gs[r] + mv;
+      const double diff = nx - xs[r];
+      flag = diff > eps;  // np.any(diff > eps): NaN compares False
+      heat[(int64_t)(it + 1) * C + r] = nx;
+    }
+    cont = __syncthreads_or(flag);
+    if (r < C) xs[r] = nx;
+    __syncthreads();
+    ++it;
+  }
+  if (r < C) xT_out[r] = xs[r];
+  if (r == 0) *n_iter = cont ? -1 : it;
+}
+
+// Large grids: one launch per iteration, one wave per 64 rows.  flags[it] != 0 <=> some cell
+// of iteration it changed by more than eps; a launch whose predecessor converged is a no-op.
+__global__ __launch_bounds__(64) void xt_iter_kernel(const double* __restrict__ Tt,
+                                                     const double* __restrict__ gs,
+                                                     const double* __restrict__ pmove, int C, double eps,
+                                                     int it, double* __restrict__ heat,
+                                                     int32_t* __restrict__ flags) {
+  if (it > 0 && __hip_atomic_load(&flags[it - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
+    return;
+  const int r = blockIdx.x * 64 + threadIdx.x;
+  const double* x = heat + (int64_t)it * C;
+  int flag = 0;
+  if (r < C) {
+    const double tot = row_payoff(Tt, x, C, r);
+    const double mv = pmove[r] * tot;
+    const double nx = gs[r] + mv;
+    heat[(int64_t)(it + 1) * C + r] = nx;
+    flag = (nx - x[r]) > eps;
+  }
+  if (__any(flag) && (threadIdx.x == 0)) atomicOr(&flags[it], 1);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Interpolated surface: grid[r*L + h] = B(xs[h], ys[r]) — piecewise bilinear through the cell
+// centres (interp2d kind='linear' on a regular grid), clamped to the centre hull.
+__device__ __forceinline__ void bracket(const double* __restrict__ c, int m, double q, int& i, double& t) {
+  q = q < c[0] ? c[0] : (q > c[m - 1] ? c[m - 1] : q);
+  int lo = 0, hi = m - 1;  // c[lo] <= q <= c[hi]
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (c[mid] <= q)
+      lo = mid;
+    else
+      hi = mid;
+  }
+  i = lo;
+  t = (q - c[lo]) / (c[lo + 1] - c[lo]);
+}
+
+__global__ void xt_interp_kernel(const double* __restrict__ xT, const double* __restrict__ cx,
+                                 const double* __restrict__ cy, int l, int w, int L, int W,
+                                 double* __restrict__ grid) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= (int64_t)L * W) return;
+  const int r = (int)(k / L), h = (int)(k % L);
+  // numpy.linspace(0, stop, num): i * (stop / (num - 1)), last node exactly `stop`
+  const double xq = (h == L - 1) ? FIELD_L : (double)h * (FIELD_L / (double)(L - 1));
+  const double yq = (r == W - 1) ? FIELD_W : (double)r * (FIELD_W / (double)(W - 1));
+  int i, j;
+  double tx, ty;
+  bracket(cx, l, xq, i, tx);
+  bracket(cy, w, yq, j, ty);
+  const double z00 = xT[j * l + i], z01 = xT[j * l + i + 1];
+  const double z10 = xT[(j + 1) * l + i], z11 = xT[(j + 1) * l + i + 1];
+  const double ux = 1.0 - tx, uy = 1.0 - ty;
+  grid[k] = (ux * z00 + tx * z01) * uy + (ux * z10 + tx * z11) * ty;
+}
+
+// rate (xthreat.py:408-465): successful moves get grid[end] - grid[start], others NaN.
+__global__ __launch_bounds__(256) void xt_rate_kernel(sa_actions A, const double* __restrict__ grid,
+                                                      int L, int W, double* __restrict__ out,
+                                                      int32_t* __restrict__ err) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= A.n) return;
+  const sa_frame& F = A.frames[0];
+  const int t = F.type_id[j];
+  double v = __builtin_nan("");
+  if (is_move(t) && F.result_id[j] == R_SUCCESS) {
+    const double sx = F.c0[j], sy = F.c1[j], ex = F.c2[j], ey = F.c3[j];
+    if (!isfinite(sx) || !isfinite(sy) || !isfinite(ex) || !isfinite(ey)) {
+      if (err) atomicOr(err, 4);
+    } else {
+      const int s = flat_index(sx, sy, L, W), e = flat_index(ex, ey, L, W);
+      v = grid[e] - grid[s];
+    }
+  }
+  out[j] = v;
+}
+
+}  // namespace sa
+
+// ================================== C ABI =================================================
+using namespace sa;
+
+extern "C" int sa_xt_count(const sa_actions* a, int32_t l, int32_t w, int64_t* shot, int64_t* goal,
+                           int64_t* move, int32_t* trans, int32_t* err_flags, void* stream) {
+  if (!a || a->n < 0) return fail(SA_EINVAL, "bad sa_actions");
+  if (l < 1 || w < 1) return fail(SA_EINVAL, "l and w must be >= 1");
+  if ((int64_t)l * w > 46340) return fail(SA_EINVAL, "grid too large (C*C must fit int32 indexing)");
+  if (!shot || !goal || !move || !trans || !err_flags) return fail(SA_EINVAL, "null output");
+  const sa_frame& F = a->frames[0];
+  if (a->n > 0 && (!F.type_id || !F.result_id || !F.c0 || !F.c1 || !F.c2 || !F.c3))
+    return fail(SA_EINVAL, "null input column");
+  if (a->n == 0) return SA_OK;
+  const int C = l * w;
+  const size_t small_lds = (size_t)(3 * C + (C * C + 1) / 2) * 4;
+  hipStream_t st = (hipStream_t)stream;
+  auto* us = reinterpret_cast<unsigned long long*>(shot);
+  auto* ug = reinterpret_cast<unsigned long long*>(goal);
+  auto* um = reinterpret_cast<unsigned long long*>(move);
+  if (small_lds <= 80 * 1024) {
+    const unsigned blocks = (unsigned)((a->n + XT_SMALL_ACTS - 1) / XT_SMALL_ACTS);
+    hipLaunchKernelGGL((xt_count_kernel<true>), dim3(blocks), dim3(XT_THREADS), small_lds, st, *a, l, w,
+                       us, ug, um, trans, err_flags);
+  } else {
+    int64_t blocks = (a->n + XT_THREADS - 1) / XT_THREADS;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL((xt_count_kernel<false>), dim3((unsigned)blocks), dim3(XT_THREADS), 0, st, *a, l,
+                       w, us, ug, um, trans, err_flags);
+  }
+  return check_launch("xt_count_kernel");
+}
+
+extern "C" int sa_xt_solve(const int64_t* shot, const int64_t* goal, const int64_t* move,
+                           const int32_t* trans, int32_t l, int32_t w, double eps, int32_t max_iter,
+                           double* mats, double* trans_t, double* heatmaps, int32_t* n_iter,
+                           void* stream) {
+  if (l < 1 || w < 1 || max_iter < 0) return fail(SA_EINVAL, "bad l, w or max_iter");
+  if (!shot || !goal || !move || !trans || !mats || !trans_t || !heatmaps || !n_iter)
+    return fail(SA_EINVAL, "null pointer");
+  const int C = l * w;
+  hipStream_t st = (hipStream_t)stream;
+  auto* us = reinterpret_cast<const unsigned long long*>(shot);
+  auto* ug = reinterpret_cast<const unsigned long long*>(goal);
+  auto* um = reinterpret_cast<const unsigned long long*>(move);
+  double* gs = nullptr;
+  int32_t* dflags = nullptr;
+  int rc = check_hip(hipMallocAsync((void**)&gs, sizeof(double) * 2 * C, st), "hipMallocAsync");
+  if (rc) return rc;
+  double* pm = gs + C;
+  int32_t iters = -1;
+  hipLaunchKernelGGL(xt_prob_kernel, dim3((C + 255) / 256), dim3(256), 0, st, us, ug, um, C, mats, gs, pm);
+  const dim3 tgrid((C + 31) / 32, (C + 31) / 32);
+  hipLaunchKernelGGL(xt_transpose_kernel, tgrid, dim3(256), 0, st, trans, um, C, trans_t);
+  rc = check_launch("xt normalise");
+  if (!rc && C <= XT_SOLVE_MAX_C) {
+    int32_t* dn = nullptr;
+    rc = check_hip(hipMallocAsync((void**)&dn, sizeof(int32_t), st), "hipMallocAsync");
+    if (!rc) {
+      const int threads = ((C + 63) / 64) * 64;
+      hipLaunchKernelGGL(xt_solve_small_kernel, dim3(1), dim3(threads), 0, st, trans_t, gs, pm, C, eps,
+                         max_iter, heatmaps, mats + 3 * C, dn);
+      rc = check_launch("xt_solve_small_kernel");
+      if (!rc) rc = check_hip(hipMemcpyAsync(&iters, dn, sizeof(int32_t), hipMemcpyDeviceToHost, st),
+                              "copy n_iter");
+      if (!rc) rc = check_hip(hipStreamSynchronize(st), "hipStreamSynchronize");
+      (void)hipFreeAsync(dn, st);
+    }
+  } else if (!rc) {
+    rc = check_hip(hipMallocAsync((void**)&dflags, sizeof(int32_t) * (max_iter + 1), st), "hipMallocAsync");
+    if (!rc) rc = check_hip(hipMemsetAsync(dflags, 0, sizeof(int32_t) * (max_iter + 1), st), "memset");
+    if (!rc) rc = check_hip(hipMemsetAsync(heatmaps, 0, sizeof(double) * C, st), "memset");
+    std::vector<int32_t> hflags(max_iter + 1, 0);
+    const int batch = 8;
+    for (int it0 = 0; !rc && it0 < max_iter && iters < 0; it0 += batch) {
+      const int it1 = it0 + batch < max_iter ? it0 + batch : max_iter;
+      for (int it = it0; it < it1; ++it)
+        hipLaunchKernelGGL(xt_iter_kernel, dim3((C + 63) / 64), dim3(64), 0, st, trans_t, gs, pm, C, eps,
+                           it, heatmaps, dflags);
+      rc = check_launch("xt_iter_kernel");
+      if (!rc) rc = check_hip(hipMemcpyAsync(hflags.data() + it0, dflags + it0,
+                                             sizeof(int32_t) * (it1 - it0), hipMemcpyDeviceToHost, st),
+                              "copy flags");
+      if (!rc) rc = check_hip(hipStreamSynchronize(st), "hipStreamSynchronize");
+      for (int it = it0; !rc && it < it1; ++it)
+        if (hflags[it] == 0) {
+          iters = it + 1;
+          break;
+        }
+    }
+    if (!rc) {
+      const int last = iters < 0 ? max_iter : iters;
+      rc = check_hip(hipMemcpyAsync(mats + 3 * C, heatmaps + (int64_t)last * C, sizeof(double) * C,
+                                    hipMemcpyDeviceToDevice, st),
+                     "copy xT");
+      if (!rc) rc = check_hip(hipStreamSynchronize(st), "hipStreamSynchronize");
+    }
+    (void)hipFreeAsync(dflags, st);
+  }
+  (void)hipFreeAsync(gs, st);
+  if (!rc) rc = check_hip(hipStreamSynchronize(st), "hipStreamSynchronize");
+  *n_iter = iters;
+  return rc;
+}
+
+extern "C" int sa_xt_interp_grid(const double* xT, const double* cx, const double* cy, int32_t l,
+                                 int32_t w, int32_t L, int32_t W, double* grid, void* stream) {
+  if (l < 2 || w < 2) return fail(SA_EINVAL, "interpolation needs at least 2 cells per axis");
+  if (L < 2 || W < 2 || !xT || !cx || !cy || !grid) return fail(SA_EINVAL, "bad interpolation args");
+  const int64_t total = (int64_t)L * W;
+  hipLaunchKernelGGL(xt_interp_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, xT, cx, cy, l, w, L, W, grid);
+  return check_launch("xt_interp_kernel");
+}
+
+extern "C" int sa_xt_rate(const sa_actions* a, const double* grid, int32_t L, int32_t W, double* out,
+                          int32_t* err_flags, void* stream) {
+  if (!a || a->n < 0 || !grid || !out || L < 1 || W < 1) return fail(SA_EINVAL, "bad xt_rate args");
+  if (a->n == 0) return SA_OK;
+  hipLaunchKernelGGL(xt_rate_kernel, dim3((unsigned)((a->n + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, *a, grid, L, W, out, err_flags);
+  return check_launch("xt_rate_kernel");
+}

@@ -1,0 +1,211 @@
+"""Device-level operations: allocate HBM outputs and launch the C-ABI kernels.
+
+Everything here works on :class:`~socceraction_amd.batch.ActionBatch` objects and
+returns torch tensors that stay on the GPU; the pandas-facing drop-in modules
+(``vaep``, ``atomic.vaep``, ``xthreat``) are thin wrappers around these calls.
+Kernels run on torch's current stream.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from . import _native
+from .batch import ActionBatch, stream_handle
+from .catalog import FeaturePlan, assemble_frame, build_plan
+
+
+def _ld(n: int) -> int:
+    return max(16, (n + 15) // 16 * 16)
+
+
+@dataclass
+class FeatureBlocks:
+    """Column-major feature blocks in HBM: ``[n_cols, ld]`` each (rows >= n are scratch)."""
+
+    plan: FeaturePlan
+    n: int
+    ld: int
+    bool_block: torch.Tensor
+    f64_block: torch.Tensor
+    i64_block: torch.Tensor
+
+    def to_frame(self, index=None):
+        """Copy to host and build the reference-shaped DataFrame."""
+        b = self.bool_block.cpu().numpy()
+        f = self.f64_block.cpu().numpy()
+        i = self.i64_block.cpu().numpy()
+        return assemble_frame(self.plan, b, f, i, self.n, index)
+
+
+def alloc_feature_blocks(plan: FeaturePlan, n: int, dev) -> FeatureBlocks:
+    ld = _ld(n)
+    return FeatureBlocks(plan, n, ld,
+                         torch.empty((plan.n_bool, ld), dtype=torch.uint8, device=dev),
+                         torch.empty((plan.n_f64, ld), dtype=torch.float64, device=dev),
+                         torch.empty((plan.n_i64, ld), dtype=torch.int64, device=dev))
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return t.data_ptr() if (t is not None and t.numel()) else None
+
+
+def features_into(s: _native.SaActions, out: FeatureBlocks) -> None:
+    lib = _native.lib()
+    _native.check(lib.sa_vaep_features(ctypes.byref(s), ctypes.byref(out.plan.struct),
+                                       _ptr(out.bool_block), _ptr(out.f64_block),
+                                       _ptr(out.i64_block), out.ld, stream_handle()))
+
+
+def features(batch: ActionBatch, xfns: Sequence[str], k: int, flip: bool = True,
+             out: Optional[FeatureBlocks] = None) -> FeatureBlocks:
+    """Game-state features of every segment of ``batch`` (windowed mode)."""
+    plan = out.plan if out is not None else build_plan(xfns, k, batch.atomic)
+    out = out or alloc_feature_blocks(plan, batch.n, batch.device)
+    features_into(batch.struct(flip=flip), out)
+    return out
+
+
+def features_explicit(frames: Sequence[ActionBatch], xfns: Sequence[str]) -> FeatureBlocks:
+    """Features of a user-built list of game-state frames (module-level transformers)."""
+    plan = build_plan(xfns, len(frames), frames[0].atomic)
+    out = alloc_feature_blocks(plan, frames[0].n, frames[0].device)
+    features_into(ActionBatch.explicit_struct(frames), out)
+    return out
+
+
+@dataclass
+class LabelBlocks:
+    n: int
+    scores: torch.Tensor
+    concedes: torch.Tensor
+    goal_from_shot: torch.Tensor
+
+
+def labels(batch: ActionBatch, nr_actions: int = 10, out: Optional[LabelBlocks] = None) -> LabelBlocks:
+    ld = _ld(batch.n)
+    if out is None:
+        buf = torch.empty((3, ld), dtype=torch.uint8, device=batch.device)
+        out = LabelBlocks(batch.n, buf[0], buf[1], buf[2])
+    s = batch.struct()
+    _native.check(_native.lib().sa_vaep_labels(ctypes.byref(s), int(nr_actions), _ptr(out.scores),
+                                               _ptr(out.concedes), _ptr(out.goal_from_shot), ld,
+                                               stream_handle()))
+    return out
+
+
+def formula(batch: ActionBatch, p_scores: torch.Tensor, p_concedes: torch.Tensor,
+            out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """offensive / defensive / vaep value as a ``[3, ld]`` tensor of the probability dtype."""
+    dt = p_scores.dtype
+    if dt not in (torch.float32, torch.float64) or p_concedes.dtype != dt:
+        raise TypeError('probabilities must both be float32 or both float64')
+    if p_scores.numel() < batch.n or p_concedes.numel() < batch.n:
+        raise ValueError('one probability per action is required')
+    ps, pc = p_scores.contiguous(), p_concedes.contiguous()
+    if out is None:
+        out = torch.empty((3, _ld(batch.n)), dtype=dt, device=batch.device)
+    s = batch.struct()
+    fn = _native.lib().sa_vaep_formula_f64 if dt == torch.float64 else \
+        _native.lib().sa_vaep_formula_f32
+    _native.check(fn(ctypes.byref(s), _ptr(ps), _ptr(pc), _ptr(out[0]), _ptr(out[1]),
+                     _ptr(out[2]), stream_handle()))
+    return out
+
+
+# ------------------------------------------------------------------------------- xT
+@dataclass
+class XTCounts:
+    l: int
+    w: int
+    shot: torch.Tensor   # int64 [C]
+    goal: torch.Tensor   # int64 [C]
+    move: torch.Tensor   # int64 [C]
+    trans: torch.Tensor  # int32 [C*C]
+    err: torch.Tensor    # int32 [1]
+
+    @property
+    def C(self) -> int:
+        return self.l * self.w
+
+
+def xt_zero_counts(l: int, w: int, dev) -> XTCounts:
+    C = l * w
+    vec = torch.zeros((3, C), dtype=torch.int64, device=dev)
+    return XTCounts(l, w, vec[0], vec[1], vec[2],
+                    torch.zeros(C * C, dtype=torch.int32, device=dev),
+                    torch.zeros(1, dtype=torch.int32, device=dev))
+
+
+def xt_count(batch: ActionBatch, l: int, w: int, acc: Optional[XTCounts] = None) -> XTCounts:
+    acc = acc or xt_zero_counts(l, w, batch.device)
+    s = batch.struct()
+    _native.check(_native.lib().sa_xt_count(ctypes.byref(s), l, w, _ptr(acc.shot), _ptr(acc.goal),
+                                            _ptr(acc.move), _ptr(acc.trans), _ptr(acc.err),
+                                            stream_handle()))
+    return acc
+
+
+def xt_check_errors(acc: XTCounts) -> None:
+    e = int(acc.err.item())
+    if e & 1:
+        raise ValueError('Cannot convert non-finite values (NA or inf) to integer '
+                         '(shot start coordinates)')
+    if e & 2:
+        raise ValueError('Cannot convert non-finite values (NA or inf) to integer '
+                         '(move coordinates)')
+
+
+@dataclass
+class XTSolution:
+    mats: torch.Tensor      # f64 [4, C]: scoring, shot, move, xT
+    trans_t: torch.Tensor   # f64 [C, C] transposed transition matrix
+    heatmaps: torch.Tensor  # f64 [n_iter + 1, C]
+    n_iter: int
+
+
+def xt_solve(acc: XTCounts, eps: float = 1e-5, max_iter: int = 1000) -> XTSolution:
+    C = acc.C
+    dev = acc.shot.device
+    mats = torch.empty((4, C), dtype=torch.float64, device=dev)
+    tt = torch.empty((C, C), dtype=torch.float64, device=dev)
+    heat = torch.empty((max_iter + 1, C), dtype=torch.float64, device=dev)
+    n_iter = ctypes.c_int32(0)
+    _native.check(_native.lib().sa_xt_solve(_ptr(acc.shot), _ptr(acc.goal), _ptr(acc.move),
+                                            _ptr(acc.trans), acc.l, acc.w, float(eps),
+                                            int(max_iter), _ptr(mats), _ptr(tt), _ptr(heat),
+                                            ctypes.byref(n_iter), stream_handle()))
+    if n_iter.value < 0:
+        raise RuntimeError(f'xT value iteration did not converge within {max_iter} iterations')
+    return XTSolution(mats, tt, heat[:n_iter.value + 1], n_iter.value)
+
+
+def _centres(extent: float, cells: int) -> np.ndarray:
+    """Cell centres exactly as the reference (xthreat.py:372-376)."""
+    size = extent / cells
+    return np.arange(0.0, extent, size) + 0.5 * size
+
+
+def xt_interp_grid(xT: torch.Tensor, l: int, w: int, L: int = 1050, W: int = 680) -> torch.Tensor:
+    cx, cy = _centres(105.0, l), _centres(68.0, w)
+    if len(cx) != l or len(cy) != w:
+        raise ValueError('x and y must have the lengths of the xT surface')  # interp2d would
+    dev = xT.device
+    c = torch.from_numpy(np.concatenate([cx, cy])).to(dev)
+    grid = torch.empty((W, L), dtype=torch.float64, device=dev)
+    _native.check(_native.lib().sa_xt_interp_grid(_ptr(xT.contiguous()), _ptr(c[:l]), _ptr(c[l:]),
+                                                  l, w, L, W, _ptr(grid), stream_handle()))
+    return grid
+
+
+def xt_rate(batch: ActionBatch, grid: torch.Tensor, L: int, W: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    out = torch.empty(max(batch.n, 1), dtype=torch.float64, device=batch.device)
+    err = torch.zeros(1, dtype=torch.int32, device=batch.device)
+    s = batch.struct()
+    _native.check(_native.lib().sa_xt_rate(ctypes.byref(s), _ptr(grid.contiguous()), L, W,
+                                           _ptr(out), _ptr(err), stream_handle()))
+    return out[:batch.n], err

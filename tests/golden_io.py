@@ -1,0 +1,57 @@
+"""Load the golden fixtures of tests/golden (written by tests/golden/make_golden.py)."""
+import glob
+import os
+
+import numpy as np
+import pandas as pd
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
+
+SPADL_IN = ['game_id', 'period_id', 'time_seconds', 'team_id', 'start_x', 'start_y', 'end_x',
+            'end_y', 'type_id', 'result_id', 'bodypart_id']
+ATOMIC_IN = ['game_id', 'period_id', 'time_seconds', 'team_id', 'x', 'y', 'dx', 'dy', 'type_id',
+             'bodypart_id']
+
+
+def cases(prefix):
+    """Names of the golden cases with a given prefix ('spadl', 'atomic', 'xt')."""
+    return sorted(os.path.basename(p)[len(prefix) + 1:-4]
+                  for p in glob.glob(os.path.join(GOLDEN, f'{prefix}_*.npz')))
+
+
+def load(prefix, name):
+    with np.load(os.path.join(GOLDEN, f'{prefix}_{name}.npz'), allow_pickle=False) as z:
+        return {k: z[k] for k in z.files}
+
+
+def inputs(g, atomic=False):
+    """Input columns of a case as a dict of numpy arrays (raw reference dtypes)."""
+    return {c: g['in_' + c] for c in (ATOMIC_IN if atomic else SPADL_IN)}
+
+
+def frame(g, atomic=False):
+    """The case's input as a reference-shaped DataFrame."""
+    cols = inputs(g, atomic)
+    df = pd.DataFrame(cols)
+    df.insert(1, 'original_event_id', None)
+    df.insert(2, 'action_id', np.arange(len(df)))
+    df.insert(6, 'player_id', 0)
+    return df
+
+
+def ks(g):
+    return sorted(int(k[1:k.index('_')]) for k in g if k.startswith('k') and k.endswith('_names_all'))
+
+
+def assert_close(a, b, name=''):
+    """float parity bar: |a-b| <= 1e-6*|b| + 1e-12, NaNs in the same places."""
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    assert a.shape == b.shape, (name, a.shape, b.shape)
+    na, nb = np.isnan(a), np.isnan(b)
+    assert (na == nb).all(), f'{name}: NaN pattern differs'
+    ok = ~nb
+    err = np.abs(a[ok] - b[ok])
+    tol = 1e-6 * np.abs(b[ok]) + 1e-12
+    bad = err > tol
+    assert not bad.any(), f'{name}: {bad.sum()} mismatches, max err {err.max()}'

@@ -1,0 +1,82 @@
+"""The CPU oracle reproduces the reference's goldens (CPU only, no GPU)."""
+import numpy as np
+import pytest
+
+from golden_io import assert_close, cases, inputs, ks, load
+from oracle import vaep_oracle as vo
+from oracle import xt_oracle as xo
+
+
+def _check_features(got, g, k):
+    names = list(g[f'k{k}_names_all'])
+    assert [c[0] for c in got] == names
+    kinds = list(g[f'k{k}_kinds_all'])
+    assert [c[1] for c in got] == kinds
+    for kind in 'bfi':
+        ref = g[f'k{k}_feat_{kind}']
+        mine = [c[2] for c in got if c[1] == kind]
+        if not mine:
+            assert ref.shape[1] == 0
+            continue
+        M = np.stack(mine, axis=1)
+        if kind == 'f':
+            assert_close(M, ref, f'k{k} float features')
+        else:
+            np.testing.assert_array_equal(M.astype(ref.dtype), ref)
+
+
+@pytest.mark.parametrize('name', cases('spadl'))
+def test_spadl_oracle(name):
+    g = load('spadl', name)
+    cols = inputs(g)
+    home = [g['home_team_id'][0]]
+    for k in ks(g):
+        _check_features(vo.features(cols, k, vo.SPADL_DEFAULT, home=home), g, k)
+    lab = vo.labels(cols)
+    np.testing.assert_array_equal(lab['scores'], g['scores'].astype(bool))
+    np.testing.assert_array_equal(lab['concedes'], g['concedes'].astype(bool))
+    np.testing.assert_array_equal(lab['goal_from_shot'], g['goal_from_shot'].astype(bool))
+    for tag, dt in (('64', np.float64), ('32', np.float32)):
+        v = vo.formula(cols, g['ps'].astype(dt), g['pc'].astype(dt))
+        for c in ('offensive_value', 'defensive_value', 'vaep_value'):
+            assert v[c].dtype == dt
+            if dt == np.float64:
+                assert_close(v[c], g[f'{c}_{tag}'], c)
+            else:
+                np.testing.assert_array_equal(v[c], g[f'{c}_{tag}'])
+
+
+@pytest.mark.parametrize('name', cases('atomic'))
+def test_atomic_oracle(name):
+    g = load('atomic', name)
+    cols = inputs(g, atomic=True)
+    home = [g['home_team_id'][0]]
+    for k in ks(g):
+        _check_features(vo.features(cols, k, vo.ATOMIC_DEFAULT, atomic=True, home=home), g, k)
+    lab = vo.labels(cols, atomic=True)
+    np.testing.assert_array_equal(lab['scores'], g['scores'].astype(bool))
+    np.testing.assert_array_equal(lab['concedes'], g['concedes'].astype(bool))
+    np.testing.assert_array_equal(lab['goal_from_shot'], g['goal_from_shot'].astype(bool))
+    for tag, dt in (('64', np.float64), ('32', np.float32)):
+        v = vo.formula(cols, g['ps'].astype(dt), g['pc'].astype(dt), atomic=True)
+        for c in ('offensive_value', 'defensive_value', 'vaep_value'):
+            np.testing.assert_allclose(v[c], g[f'{c}_{tag}'], rtol=1e-6, atol=1e-12)
+
+
+@pytest.mark.parametrize('name', cases('xt'))
+def test_xt_oracle(name):
+    g = load('xt', name)
+    cols = inputs(g)
+    grids = sorted({k.split('_')[0] for k in g if k[0].isdigit()})
+    for tag in grids:
+        l, w = map(int, tag.split('x'))
+        f = xo.fit(cols, l, w)
+        np.testing.assert_array_equal(f['scoring_prob'], g[f'{tag}_scoring_prob'])
+        np.testing.assert_array_equal(f['shot_prob'], g[f'{tag}_shot_prob'])
+        np.testing.assert_array_equal(f['move_prob'], g[f'{tag}_move_prob'])
+        np.testing.assert_array_equal(f['transition'], g[f'{tag}_transition'])
+        assert f['heatmaps'].shape == g[f'{tag}_heatmaps'].shape  # same iteration count
+        np.testing.assert_array_equal(f['xT'], g[f'{tag}_xT'])  # bit-exact summation order
+        assert_close(xo.rate(cols, g[f'{tag}_xT']), g[f'{tag}_rate'], 'rate')
+        if f'{tag}_rate_interp' in g:
+            assert_close(xo.rate(cols, g[f'{tag}_xT'], True), g[f'{tag}_rate_interp'], 'interp')
