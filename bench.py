@@ -1,0 +1,185 @@
+#!/usr/bin/env python
+"""Benchmark: SPADL actions/s valued (VAEP features + labels + formula) on MI355X.
+
+One *step* = one pass of the valuation hot path over one batch: the reference's
+``VAEP.compute_features`` (k=3, default xfns: 568 columns) + ``compute_labels``
+(scores, concedes) + ``formula.value`` (f64 probabilities) for every game of the
+batch, all kernels on device-resident inputs (synthetic data, cfg2 of BASELINE.json:
+10k games, ~16M actions per GPU).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--games G]
+
+N > 1 runs one rank per GPU under torch.distributed.run; each rank values its own
+10k games (weak scaling, no data-path collective) and rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import copy
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from socceraction_amd import batch as B  # noqa: E402
+from socceraction_amd import catalog, ops, synthetic  # noqa: E402
+from socceraction_amd._native import XFN  # noqa: E402
+
+SPADL_DEFAULT = ['actiontype_onehot', 'result_onehot', 'actiontype_result_onehot',
+                 'bodypart_onehot', 'time', 'startlocation', 'endlocation', 'startpolar',
+                 'endpolar', 'movement', 'team', 'time_delta', 'space_delta', 'goalscore']
+
+# algorithmic bytes per action of each kernel (inputs read once + outputs written once)
+BYTES = {'features': 48 + 515 + 47 * 8 + 3 * 8,  # 963
+         'goalscore': 6 + 24, 'labels': 6 + 2, 'formula': 30 + 24}
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def _dist():
+    ws = int(os.environ.get('WORLD_SIZE', '1'))
+    if ws > 1:
+        import torch.distributed as dist
+        lr = int(os.environ.get('LOCAL_RANK', '0'))
+        torch.cuda.set_device(lr)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', lr))
+        return dist, dist.get_rank(), ws
+    return None, 0, 1
+
+
+def cpu_baseline(d, seconds: float) -> dict:
+    """The oracle port (numpy, 1 thread) on the GPU box's host, over whole games."""
+    from oracle import vaep_oracle as vo
+    p = synthetic.probabilities(int(d['game_off'][-1]))
+    off = d['game_off']
+    names = ('period_id', 'time_seconds', 'team_id', 'start_x', 'start_y', 'end_x', 'end_y',
+             'type_id', 'result_id', 'bodypart_id')
+    done, games, t0 = 0, 0, time.perf_counter()
+    while games < len(off) - 1 and time.perf_counter() - t0 < seconds:
+        s, e = int(off[games]), int(off[games + 1])
+        cols = {c: d[c][s:e] for c in names}
+        vo.features(cols, 3, vo.SPADL_DEFAULT, home=[d['home_team_id'][games]])
+        vo.labels(cols)
+        vo.formula(cols, p['scores'][s:e], p['concedes'][s:e])
+        done += e - s
+        games += 1
+    dt = time.perf_counter() - t0
+    return {'value': round(done / dt, 1), 'unit': 'actions/s', 'cores': 1, 'kind': 'port',
+            'sample': f'{games} synthetic games ({done} actions) of the same workload, '
+                      f'numpy oracle, 1 thread, {dt:.1f} s'}
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--warmup', type=int, default=3)
+    ap.add_argument('--games', type=int, default=10000, help='games per GPU (cfg2: 10k)')
+    ap.add_argument('--cpu-seconds', type=float, default=15.0)
+    ap.add_argument('--no-cpu', action='store_true')
+    args = ap.parse_args()
+
+    dist, rank, world = _dist()
+    dev = B.device()
+    d = synthetic.spadl_games(args.games, game_id0=rank * args.games)
+    ab = B.ActionBatch.from_columns(d, dev=dev)
+    n = ab.n
+    plan = catalog.build_plan(SPADL_DEFAULT, 3)
+    out = ops.alloc_feature_blocks(plan, n, dev)
+    fplan = copy.copy(plan)  # features call without goalscore: timed as its own launch
+    fplan.struct = copy.deepcopy(plan.struct)
+    fplan.struct.i64_col[XFN['goalscore']] = -1
+    fout = ops.FeatureBlocks(fplan, n, out.ld, out.bool_block, out.f64_block, out.i64_block)
+    p = synthetic.probabilities(n)
+    ps = torch.from_numpy(p['scores']).to(dev)
+    pc = torch.from_numpy(p['concedes']).to(dev)
+    lab_buf = torch.empty((3, out.ld), dtype=torch.uint8, device=dev)
+    lab = ops.LabelBlocks(n, lab_buf[0], lab_buf[1], None)
+    val = torch.empty((3, out.ld), dtype=torch.float64, device=dev)
+    s_act = ab.struct()
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record()
+        ops.features_into(s_act, fout)
+        if ev is not None:
+            ev[1].record()
+        ops.goalscore_into(ab, out)
+        if ev is not None:
+            ev[2].record()
+        ops.labels(ab, 10, lab)
+        if ev is not None:
+            ev[3].record()
+        ops.formula(ab, ps, pc, val)
+        if ev is not None:
+            ev[4].record()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(5)] for _ in range(args.steps)]
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(evs[k])
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    kern = {name: float(np.mean([e[i].elapsed_time(e[i + 1]) for e in evs]))
+            for i, name in enumerate(('features', 'goalscore', 'labels', 'formula'))}
+    total_actions = n
+    if dist:
+        t = torch.tensor([wall], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall = float(t.item())
+        c = torch.tensor([n], dtype=torch.int64, device=dev)
+        dist.all_reduce(c)
+        total_actions = int(c.item())
+    if rank != 0:
+        if dist:
+            dist.destroy_process_group()
+        return
+    ms_per_step = wall / args.steps * 1e3
+    value = total_actions * args.steps / wall
+    feat_ms = kern['features']
+    achieved = BYTES['features'] * n / (feat_ms * 1e-3) / 1e9
+    traffic = None
+    pmc = os.path.join(ROOT, 'profiles', 'pmc_features_kernel.json')
+    if os.path.exists(pmc):
+        with open(pmc) as f:
+            traffic = json.load(f).get('hbm_bytes_per_launch_per_action')
+        if traffic is not None:
+            traffic = round(traffic * n)
+    line = {
+        'metric': 'SPADL actions/sec valued (VAEP feat+labels+formula, xT fit+rate) at 1/2/4/8 GPUs',
+        'value': round(value, 1), 'unit': 'actions/s', 'n_gpus': world, 'steps': args.steps,
+        'warmup': args.warmup, 'ms_per_step': round(ms_per_step, 4), 'higher_is_better': True,
+        'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f64',
+        'data': 'synthetic (seeded SPADL games, BASELINE cfg2 shape; inputs resident in HBM)',
+        'config': {'workload': 'cfg2: 10k-game synthetic SPADL per GPU, VAEP compute_features '
+                               '(k=3, default xfns, 568 cols) + compute_labels + formula.value (f64)',
+                   'games_per_gpu': args.games, 'actions_per_gpu': n,
+                   'parallelism': f'games sharded over {world} GPU(s)'},
+        'kernels_ms': {k: round(v, 4) for k, v in kern.items()},
+        'roofline': {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS,
+                     'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 4),
+                     'traffic': traffic, 'kernel': 'features_kernel',
+                     'bytes_per_action': BYTES['features']},
+    }
+    if not args.no_cpu:
+        line['cpu_baseline'] = cpu_baseline(d, args.cpu_seconds)
+    print(json.dumps(line), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

@@ -119,6 +119,11 @@ typedef struct sa_feature_plan {
 int sa_vaep_features(const sa_actions* a, const sa_feature_plan* plan, uint8_t* bool_out,
                      double* f64_out, int64_t* i64_out, int64_t ld, void* stream);
 
+/* goalscore alone (vaep/features.py:505-539; atomic/vaep/features.py:313-344): writes the
+ * goalscore_team / _opponent / _diff columns at out[0], out[ld], out[2*ld].  Also launched by
+ * sa_vaep_features when the plan requests SA_XFN_GOALSCORE. */
+int sa_vaep_goalscore(const sa_actions* a, int64_t* out, int64_t ld, void* stream);
+
 /* Replaces labels.scores / concedes / goal_from_shot (vaep/labels.py:9-116;
  * atomic/vaep/labels.py:9-107): look-ahead of nr_actions (>=1) clamped at each
  * segment's last row.  Any output may be NULL.  Outputs are length-ld bool bytes. */

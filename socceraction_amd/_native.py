@@ -53,6 +53,7 @@ class SaFeaturePlan(ctypes.Structure):
 _SIGNATURES = {
     'sa_vaep_features': (ctypes.c_int, [ctypes.POINTER(SaActions), ctypes.POINTER(SaFeaturePlan),
                                         _p, _p, _p, ctypes.c_int64, _p]),
+    'sa_vaep_goalscore': (ctypes.c_int, [ctypes.POINTER(SaActions), _p, ctypes.c_int64, _p]),
     'sa_vaep_labels': (ctypes.c_int, [ctypes.POINTER(SaActions), ctypes.c_int32, _p, _p, _p,
                                       ctypes.c_int64, _p]),
     'sa_vaep_formula_f64': (ctypes.c_int, [ctypes.POINTER(SaActions), _p, _p, _p, _p, _p, _p]),

@@ -1,0 +1,53 @@
+"""Build libsocceraction_amd.so in-tree with hipcc for gfx950.
+
+    python -m socceraction_amd.build [--force]
+
+Flags: ``-O3 --offload-arch=gfx950 -ffp-contract=off``.  ``-ffp-contract=off`` is a
+parity requirement: numpy evaluates ``dx**2 + dy**2`` and the xT dot products with a
+separately rounded multiply and add, so the kernels must not fuse them into FMAs.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, 'csrc')
+OUT = os.path.join(HERE, '_lib', 'libsocceraction_amd.so')
+SOURCES = ['sa_api.hip', 'sa_vaep.hip', 'sa_xt.hip']
+HEADERS = ['sa_common.h', 'sa_internal.h', os.path.join('..', '..', 'include', 'socceraction_amd.h')]
+FLAGS = ['-O3', '--offload-arch=gfx950', '-ffp-contract=off', '-fPIC', '-shared', '-std=c++17',
+         '-Wall']
+
+
+def hipcc() -> str:
+    for c in (os.environ.get('HIPCC'), '/opt/rocm/bin/hipcc', 'hipcc'):
+        if c and (os.path.sep not in c or os.path.exists(c)):
+            return c
+    raise RuntimeError('hipcc not found')
+
+
+def _stale() -> bool:
+    if not os.path.exists(OUT):
+        return True
+    t = os.path.getmtime(OUT)
+    deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS]
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(force: bool = False, verbose: bool = True) -> str:
+    if not force and not _stale():
+        return OUT
+    os.makedirs(os.path.dirname(OUT), exist_ok=True)
+    tmp = OUT + '.tmp'
+    cmd = [hipcc()] + FLAGS + [os.path.join(CSRC, s) for s in SOURCES] + ['-o', tmp]
+    if verbose:
+        print(' '.join(cmd), flush=True)
+    subprocess.run(cmd, check=True, cwd=CSRC)
+    os.replace(tmp, OUT)
+    return OUT
+
+
+if __name__ == '__main__':
+    print(build(force='--force' in sys.argv))

@@ -745,17 +745,24 @@ extern "C" int sa_vaep_features(const sa_actions* a, const sa_feature_plan* plan
   rc = check_launch("features_kernel");
   if (rc) return rc;
   const int gc = plan->i64_col[SA_XFN_GOALSCORE];
-  if (gc >= 0) {
-    sa_actions a1 = *a;  // goalscore reads a0 only (frames[0])
-    if (a->atomic)
-      hipLaunchKernelGGL((goalscore_kernel<true>), dim3((unsigned)a->n_segments), dim3(GS_THREADS), 0,
-                         st, a1, i64_out + (int64_t)gc * ld, ld);
-    else
-      hipLaunchKernelGGL((goalscore_kernel<false>), dim3((unsigned)a->n_segments), dim3(GS_THREADS), 0,
-                         st, a1, i64_out + (int64_t)gc * ld, ld);
-    rc = check_launch("goalscore_kernel");
-  }
+  if (gc >= 0) rc = sa_vaep_goalscore(a, i64_out + (int64_t)gc * ld, ld, stream);
   return rc;
+}
+
+extern "C" int sa_vaep_goalscore(const sa_actions* a, int64_t* out, int64_t ld, void* stream) {
+  int rc = check_actions(a, true);
+  if (rc) return rc;
+  if (!out) return fail(SA_EINVAL, "null goalscore output");
+  if (ld < a->n) return fail(SA_EINVAL, "ld < n");
+  if (a->n == 0) return SA_OK;
+  hipStream_t st = (hipStream_t)stream;
+  if (a->atomic)
+    hipLaunchKernelGGL((goalscore_kernel<true>), dim3((unsigned)a->n_segments), dim3(GS_THREADS), 0, st,
+                       *a, out, ld);
+  else
+    hipLaunchKernelGGL((goalscore_kernel<false>), dim3((unsigned)a->n_segments), dim3(GS_THREADS), 0,
+                       st, *a, out, ld);
+  return check_launch("goalscore_kernel");
 }
 
 extern "C" int sa_vaep_labels(const sa_actions* a, int32_t nr_actions, uint8_t* scores,

@@ -209,3 +209,14 @@ def xt_rate(batch: ActionBatch, grid: torch.Tensor, L: int, W: int) -> Tuple[tor
     _native.check(_native.lib().sa_xt_rate(ctypes.byref(s), _ptr(grid.contiguous()), L, W,
                                            _ptr(out), _ptr(err), stream_handle()))
     return out[:batch.n], err
+
+
+def goalscore_into(batch: ActionBatch, out: FeatureBlocks) -> None:
+    """Launch only the goalscore scan into the plan's goalscore columns."""
+    from ._native import XFN
+    gc = out.plan.struct.i64_col[XFN['goalscore']]
+    if gc < 0:
+        raise ValueError('plan has no goalscore columns')
+    s = batch.struct()
+    _native.check(_native.lib().sa_vaep_goalscore(ctypes.byref(s), out.i64_block[gc].data_ptr(),
+                                                  out.ld, stream_handle()))

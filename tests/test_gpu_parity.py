@@ -1,0 +1,223 @@
+"""GPU parity: the HIP kernels (through the C ABI) against the reference goldens and the oracle.
+
+Bar: bit-exact for ids, one-hots, labels, goal scores and counts; floats within
+|a-b| <= 1e-6*|ref| + 1e-12 (see golden_io.assert_close).
+"""
+import numpy as np
+import pytest
+
+from golden_io import assert_close, cases, frame, inputs, ks, load
+from oracle import vaep_oracle as vo
+from oracle import xt_oracle as xo
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip('torch')
+
+
+@pytest.fixture(scope='module')
+def sa():
+    from socceraction_amd import _native, batch, catalog, ops, synthetic
+    _native.load_library()
+    return dict(batch=batch, catalog=catalog, ops=ops, synthetic=synthetic)
+
+
+def _blocks_match(fb, g, k, n):
+    names = list(g[f'k{k}_names_all'])
+    assert fb.plan.names == names
+    b = fb.bool_block.cpu().numpy()
+    f = fb.f64_block.cpu().numpy()
+    i = fb.i64_block.cpu().numpy()
+    blocks = {'b': b, 'f': f, 'i': i}
+    got = {'b': [], 'f': [], 'i': []}
+    for name, kind, col in fb.plan.order:
+        got[kind].append(blocks[kind][col, :n])
+    for kind in 'bfi':
+        ref = g[f'k{k}_feat_{kind}']
+        if not got[kind]:
+            assert ref.shape[1] == 0
+            continue
+        M = np.stack(got[kind], axis=1)
+        if kind == 'f':
+            assert_close(M, ref, f'k{k} f64 block')
+        else:
+            np.testing.assert_array_equal(M.astype(ref.dtype), ref, err_msg=f'k{k} {kind} block')
+
+
+@pytest.mark.parametrize('atomic', [False, True])
+def test_features_labels_formula_goldens(sa, atomic):
+    B, ops = sa['batch'], sa['ops']
+    default = vo.ATOMIC_DEFAULT if atomic else vo.SPADL_DEFAULT
+    prefix = 'atomic' if atomic else 'spadl'
+    for name in cases(prefix):
+        g = load(prefix, name)
+        df = frame(g, atomic)
+        n = len(df)
+        ab = B.ActionBatch.from_frame(df, atomic=atomic, home_team_id=g['home_team_id'][0])
+        for k in ks(g):
+            fb = ops.features(ab, default, k)
+            _blocks_match(fb, g, k, n)
+        lb = ops.labels(ab)
+        np.testing.assert_array_equal(lb.scores[:n].cpu().numpy(), g['scores'], err_msg=name)
+        np.testing.assert_array_equal(lb.concedes[:n].cpu().numpy(), g['concedes'], err_msg=name)
+        np.testing.assert_array_equal(lb.goal_from_shot[:n].cpu().numpy(), g['goal_from_shot'],
+                                      err_msg=name)
+        for tag, dt in (('64', torch.float64), ('32', torch.float32)):
+            ps = torch.tensor(g['ps'], dtype=dt, device=ab.device)
+            pc = torch.tensor(g['pc'], dtype=dt, device=ab.device)
+            v = ops.formula(ab, ps, pc).cpu().numpy()[:, :n]
+            for r, c in enumerate(('offensive_value', 'defensive_value', 'vaep_value')):
+                if dt == torch.float32:
+                    np.testing.assert_allclose(v[r], g[f'{c}_{tag}'], rtol=1e-6, atol=1e-7,
+                                               err_msg=f'{name} {c}')
+                else:
+                    assert_close(v[r], g[f'{c}_{tag}'], f'{name} {c}')
+
+
+@pytest.mark.parametrize('atomic', [False, True])
+def test_batched_segments_match_per_game(sa, atomic):
+    """Many games in one batch (one segment each) == per-game reference outputs."""
+    B, ops = sa['batch'], sa['ops']
+    prefix = 'atomic' if atomic else 'spadl'
+    default = vo.ATOMIC_DEFAULT if atomic else vo.SPADL_DEFAULT
+    names = [c for c in cases(prefix) if c != 'concat2']
+    gs = [load(prefix, c) for c in names]
+    import pandas as pd
+    dfs = []
+    for idx, g in enumerate(gs):
+        d = frame(g, atomic).copy()
+        d['game_id'] = idx  # one contiguous run per case
+        dfs.append(d)
+    df = pd.concat(dfs, ignore_index=True)
+    homes = [g['home_team_id'][0] for g in gs]
+    ab = B.ActionBatch.from_frame(df, atomic=atomic, home_team_id=homes, segments='game')
+    assert ab.n_segments == len(gs)
+    fb = ops.features(ab, default, 3)
+    lb = ops.labels(ab)
+    ps = torch.tensor(np.concatenate([g['ps'] for g in gs]), device=ab.device)
+    pc = torch.tensor(np.concatenate([g['pc'] for g in gs]), device=ab.device)
+    v = ops.formula(ab, ps, pc).cpu().numpy()
+    b, f, i = (fb.bool_block.cpu().numpy(), fb.f64_block.cpu().numpy(),
+               fb.i64_block.cpu().numpy())
+    o = 0
+    for g in gs:
+        n = len(g['type_id'] if 'type_id' in g else g['in_type_id'])
+        sl = slice(o, o + n)
+        blocks = {'b': b[:, sl], 'f': f[:, sl], 'i': i[:, sl]}
+        for kind in 'bfi':
+            cols = [blocks[kind][col] for _, kk, col in fb.plan.order if kk == kind]
+            M = np.stack(cols, axis=1)
+            ref = g[f'k3_feat_{kind}']
+            if kind == 'f':
+                assert_close(M, ref, 'batched f64')
+            else:
+                np.testing.assert_array_equal(M.astype(ref.dtype), ref)
+        np.testing.assert_array_equal(lb.scores[sl].cpu().numpy(), g['scores'])
+        np.testing.assert_array_equal(lb.concedes[sl].cpu().numpy(), g['concedes'])
+        np.testing.assert_array_equal(lb.goal_from_shot[sl].cpu().numpy(), g['goal_from_shot'])
+        for r, c in enumerate(('offensive_value', 'defensive_value', 'vaep_value')):
+            assert_close(v[r, sl], g[f'{c}_64'], c)
+        o += n
+
+
+def test_explicit_frames_match_windowed(sa):
+    """Explicit-frame mode (module-level transformers) == windowed mode on the same states."""
+    B, ops = sa['batch'], sa['ops']
+    g = load('spadl', 'full0')
+    df = frame(g)
+    n = len(df)
+    k = 3
+    home = g['home_team_id'][0]
+    cols = inputs(g)
+    # build the k game-state frames like gamestates + play_left_to_right on the host
+    frames = []
+    away = cols['team_id'] != home
+    for i in range(k):
+        rows = np.maximum(np.arange(n) - i, 0)
+        d = df.iloc[rows].reset_index(drop=True).copy()
+        for c, ext in (('start_x', 105.0), ('end_x', 105.0), ('start_y', 68.0), ('end_y', 68.0)):
+            d.loc[away, c] = ext - d.loc[away, c].to_numpy()
+        frames.append(d)
+    fbs = B.frames_batches(frames, atomic=False)
+    fb = ops.features_explicit(fbs, vo.SPADL_DEFAULT)
+    _blocks_match(fb, g, k, n)
+
+
+def test_xt_goldens(sa):
+    B, ops = sa['batch'], sa['ops']
+    for name in cases('xt'):
+        g = load('xt', name)
+        df = frame(g)
+        ab = B.ActionBatch.from_frame(df)
+        grids = sorted({k.split('_')[0] for k in g if k[0].isdigit()})
+        for tag in grids:
+            l, w = map(int, tag.split('x'))
+            acc = ops.xt_count(ab, l, w)
+            ops.xt_check_errors(acc)
+            sol = ops.xt_solve(acc)
+            C = l * w
+            m = sol.mats.cpu().numpy()
+            np.testing.assert_array_equal(m[0].reshape(w, l), g[f'{tag}_scoring_prob'])
+            np.testing.assert_array_equal(m[1].reshape(w, l), g[f'{tag}_shot_prob'])
+            np.testing.assert_array_equal(m[2].reshape(w, l), g[f'{tag}_move_prob'])
+            np.testing.assert_array_equal(sol.trans_t.cpu().numpy().T, g[f'{tag}_transition'])
+            assert sol.n_iter + 1 == len(g[f'{tag}_heatmaps']), (name, tag)
+            np.testing.assert_array_equal(m[3].reshape(w, l), g[f'{tag}_xT'])
+            np.testing.assert_array_equal(sol.heatmaps.cpu().numpy().reshape(-1, w, l),
+                                          g[f'{tag}_heatmaps'])
+            xT = sol.mats[3].reshape(w, l)
+            r, err = ops.xt_rate(ab, xT, l, w)
+            assert int(err.item()) == 0
+            assert_close(r.cpu().numpy(), g[f'{tag}_rate'], f'{name} {tag} rate')
+            if f'{tag}_rate_interp' in g:
+                grid = ops.xt_interp_grid(xT, l, w)
+                assert_close(grid.cpu().numpy(), xo.interp_grid(g[f'{tag}_xT']), 'interp grid')
+                r, _ = ops.xt_rate(ab, grid, 1050, 680)
+                assert_close(r.cpu().numpy(), g[f'{tag}_rate_interp'], f'{name} {tag} interp rate')
+
+
+def test_full_size_sampled_games_vs_oracle(sa):
+    """cfg2-sized batch (10k games, ~16M actions): sampled games checked against the oracle,
+    plus size-independent invariants over the whole batch (one-hot rows sum to 1)."""
+    B, ops, syn = sa['batch'], sa['ops'], sa['synthetic']
+    d = syn.spadl_games(10000)
+    ab = B.ActionBatch.from_columns(d)
+    fb = ops.features(ab, vo.SPADL_DEFAULT, 3)
+    lb = ops.labels(ab)
+    p = syn.probabilities(ab.n)
+    ps = torch.from_numpy(p['scores']).to(ab.device)
+    pc = torch.from_numpy(p['concedes']).to(ab.device)
+    val = ops.formula(ab, ps, pc)
+    torch.cuda.synchronize()
+    n = ab.n
+    # invariant: each window's type x result one-hot has exactly one True per action
+    plan = fb.plan
+    tr = [col for name, kind, col in plan.order if name.startswith('type_') and '_result_' in name]
+    assert len(tr) == 414
+    for i in range(3):
+        s = fb.bool_block[tr[i * 138]:tr[i * 138] + 138, :n].sum(dim=0, dtype=torch.int32)
+        assert bool((s == 1).all())
+    rng = np.random.default_rng(0)
+    off = d['game_off']
+    names = plan.names
+    for g in rng.choice(len(off) - 1, 12, replace=False):
+        s, e = int(off[g]), int(off[g + 1])
+        cols = {c: d[c][s:e] for c in ('period_id', 'time_seconds', 'team_id', 'start_x',
+                                       'start_y', 'end_x', 'end_y', 'type_id', 'result_id',
+                                       'bodypart_id')}
+        ref = vo.features(cols, 3, vo.SPADL_DEFAULT, home=[d['home_team_id'][g]])
+        assert [c[0] for c in ref] == names
+        blocks = {'b': fb.bool_block[:, s:e].cpu().numpy(), 'f': fb.f64_block[:, s:e].cpu().numpy(),
+                  'i': fb.i64_block[:, s:e].cpu().numpy()}
+        for (name, kind, col), (_, _, rv) in zip(plan.order, ref):
+            got = blocks[kind][col]
+            if kind == 'f':
+                assert_close(got, rv, name)
+            else:
+                np.testing.assert_array_equal(got.astype(np.int64), rv.astype(np.int64), err_msg=name)
+        lab = vo.labels(cols)
+        np.testing.assert_array_equal(lb.scores[s:e].cpu().numpy().astype(bool), lab['scores'])
+        np.testing.assert_array_equal(lb.concedes[s:e].cpu().numpy().astype(bool), lab['concedes'])
+        fo = vo.formula(cols, p['scores'][s:e], p['concedes'][s:e])
+        for r, c in enumerate(('offensive_value', 'defensive_value', 'vaep_value')):
+            assert_close(val[r, s:e].cpu().numpy(), fo[c], c)
