@@ -162,12 +162,20 @@ int sa_xt_solve(const int64_t* shot, const int64_t* goal, const int64_t* move,
                 const int32_t* trans, int32_t l, int32_t w, double eps, int32_t max_iter,
                 double* mats, double* trans_t, double* heatmaps, int32_t* n_iter, void* stream);
 
-/* Interpolated surface for ExpectedThreat.rate(use_interpolation=True)
- * (xthreat.py:347-378, 443-451): grid[r*L + h] = bilinear(xT; xs[h], ys[r]) over
- * cell centres cx[l], cy[w] ([device] f64), clamped to the centre hull, with
- * xs = linspace(0,105,L), ys = linspace(0,68,W). */
+/* Normalisation only (scoring_prob, action_prob, move_transition_matrix of
+ * xthreat.py:74-218): mats[3*C] = scoring_prob | shot_prob | move_prob, trans_t as in
+ * sa_xt_solve.  Asynchronous. */
+int sa_xt_normalize(const int64_t* shot, const int64_t* goal, const int64_t* move,
+                    const int32_t* trans, int32_t l, int32_t w, double* mats, double* trans_t,
+                    void* stream);
+
+/* interp2d(x=cx, y=cy, z=xT, kind='linear')(xs, ys) of ExpectedThreat.interpolator
+ * (xthreat.py:347-378): grid[r*L + h] = bilinear(xT; xs[h], ys[r]) through the cell
+ * centres cx[l], cy[w], clamped to the centre hull (FITPACK evaluation clamps).  All
+ * arrays are device f64; xs (length L) and ys (length W) sorted ascending. */
 int sa_xt_interp_grid(const double* xT, const double* cx, const double* cy, int32_t l, int32_t w,
-                      int32_t L, int32_t W, double* grid, void* stream);
+                      const double* xs, int32_t L, const double* ys, int32_t W, double* grid,
+                      void* stream);
 
 /* ExpectedThreat.rate (xthreat.py:408-465): out[j] = grid[W-1-yj(end), xi(end)] -
  * grid[W-1-yj(start), xi(start)] for successful moves, NaN otherwise.  A non-finite

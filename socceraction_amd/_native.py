@@ -63,8 +63,10 @@ _SIGNATURES = {
     'sa_xt_solve': (ctypes.c_int, [_p, _p, _p, _p, ctypes.c_int32, ctypes.c_int32,
                                    ctypes.c_double, ctypes.c_int32, _p, _p, _p,
                                    ctypes.POINTER(ctypes.c_int32), _p]),
-    'sa_xt_interp_grid': (ctypes.c_int, [_p, _p, _p, ctypes.c_int32, ctypes.c_int32,
-                                         ctypes.c_int32, ctypes.c_int32, _p, _p]),
+    'sa_xt_normalize': (ctypes.c_int, [_p, _p, _p, _p, ctypes.c_int32, ctypes.c_int32, _p, _p,
+                                       _p]),
+    'sa_xt_interp_grid': (ctypes.c_int, [_p, _p, _p, ctypes.c_int32, ctypes.c_int32, _p,
+                                         ctypes.c_int32, _p, ctypes.c_int32, _p, _p]),
     'sa_xt_rate': (ctypes.c_int, [ctypes.POINTER(SaActions), _p, ctypes.c_int32, ctypes.c_int32,
                                   _p, _p, _p]),
     'sa_abi_version': (ctypes.c_int, []),

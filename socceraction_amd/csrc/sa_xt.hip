@@ -273,14 +273,13 @@ __device__ __forceinline__ void bracket(const double* __restrict__ c, int m, dou
 }
 
 __global__ void xt_interp_kernel(const double* __restrict__ xT, const double* __restrict__ cx,
-                                 const double* __restrict__ cy, int l, int w, int L, int W,
-                                 double* __restrict__ grid) {
+                                 const double* __restrict__ cy, int l, int w,
+                                 const double* __restrict__ xs, int L, const double* __restrict__ ys,
+                                 int W, double* __restrict__ grid) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= (int64_t)L * W) return;
   const int r = (int)(k / L), h = (int)(k % L);
-  // numpy.linspace(0, stop, num): i * (stop / (num - 1)), last node exactly `stop`
-  const double xq = (h == L - 1) ? FIELD_L : (double)h * (FIELD_L / (double)(L - 1));
-  const double yq = (r == W - 1) ? FIELD_W : (double)r * (FIELD_W / (double)(W - 1));
+  const double xq = xs[h], yq = ys[r];
   int i, j;
   double tx, ty;
   bracket(cx, l, xq, i, tx);
@@ -419,13 +418,37 @@ extern "C" int sa_xt_solve(const int64_t* shot, const int64_t* goal, const int64
 }
 
 extern "C" int sa_xt_interp_grid(const double* xT, const double* cx, const double* cy, int32_t l,
-                                 int32_t w, int32_t L, int32_t W, double* grid, void* stream) {
+                                 int32_t w, const double* xs, int32_t L, const double* ys, int32_t W,
+                                 double* grid, void* stream) {
   if (l < 2 || w < 2) return fail(SA_EINVAL, "interpolation needs at least 2 cells per axis");
-  if (L < 2 || W < 2 || !xT || !cx || !cy || !grid) return fail(SA_EINVAL, "bad interpolation args");
+  if (L < 1 || W < 1 || !xT || !cx || !cy || !xs || !ys || !grid)
+    return fail(SA_EINVAL, "bad interpolation args");
   const int64_t total = (int64_t)L * W;
   hipLaunchKernelGGL(xt_interp_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
-                     (hipStream_t)stream, xT, cx, cy, l, w, L, W, grid);
+                     (hipStream_t)stream, xT, cx, cy, l, w, xs, L, ys, W, grid);
   return check_launch("xt_interp_kernel");
+}
+
+extern "C" int sa_xt_normalize(const int64_t* shot, const int64_t* goal, const int64_t* move,
+                               const int32_t* trans, int32_t l, int32_t w, double* mats,
+                               double* trans_t, void* stream) {
+  if (l < 1 || w < 1) return fail(SA_EINVAL, "bad l or w");
+  if (!shot || !goal || !move || !trans || !mats || !trans_t) return fail(SA_EINVAL, "null pointer");
+  const int C = l * w;
+  hipStream_t st = (hipStream_t)stream;
+  auto* us = reinterpret_cast<const unsigned long long*>(shot);
+  auto* ug = reinterpret_cast<const unsigned long long*>(goal);
+  auto* um = reinterpret_cast<const unsigned long long*>(move);
+  double* gs = nullptr;
+  int rc = check_hip(hipMallocAsync((void**)&gs, sizeof(double) * 2 * C, st), "hipMallocAsync");
+  if (rc) return rc;
+  hipLaunchKernelGGL(xt_prob_kernel, dim3((C + 255) / 256), dim3(256), 0, st, us, ug, um, C, mats, gs,
+                     gs + C);
+  const dim3 tgrid((C + 31) / 32, (C + 31) / 32);
+  hipLaunchKernelGGL(xt_transpose_kernel, tgrid, dim3(256), 0, st, trans, um, C, trans_t);
+  rc = check_launch("xt normalise");
+  (void)hipFreeAsync(gs, st);
+  return rc;
 }
 
 extern "C" int sa_xt_rate(const sa_actions* a, const double* grid, int32_t L, int32_t W, double* out,

@@ -190,16 +190,40 @@ def _centres(extent: float, cells: int) -> np.ndarray:
     return np.arange(0.0, extent, size) + 0.5 * size
 
 
-def xt_interp_grid(xT: torch.Tensor, l: int, w: int, L: int = 1050, W: int = 680) -> torch.Tensor:
+def xt_interp_grid(xT: torch.Tensor, l: int, w: int, xs: Optional[np.ndarray] = None,
+                   ys: Optional[np.ndarray] = None, L: int = 1050, W: int = 680) -> torch.Tensor:
+    """Bilinear xT surface on the nodes xs x ys (default: the reference's 1050 x 680
+    ``linspace`` grid of ExpectedThreat.rate, xthreat.py:443-451) as a ``[W, L]`` tensor."""
     cx, cy = _centres(105.0, l), _centres(68.0, w)
     if len(cx) != l or len(cy) != w:
         raise ValueError('x and y must have the lengths of the xT surface')  # interp2d would
+    if xs is None:
+        xs = np.linspace(0, 105.0, L)
+    if ys is None:
+        ys = np.linspace(0, 68.0, W)
+    xs = np.sort(np.asarray(xs, np.float64).reshape(-1))
+    ys = np.sort(np.asarray(ys, np.float64).reshape(-1))
+    L, W = len(xs), len(ys)
     dev = xT.device
-    c = torch.from_numpy(np.concatenate([cx, cy])).to(dev)
+    c = torch.from_numpy(np.concatenate([cx, cy, xs, ys])).to(dev)
     grid = torch.empty((W, L), dtype=torch.float64, device=dev)
-    _native.check(_native.lib().sa_xt_interp_grid(_ptr(xT.contiguous()), _ptr(c[:l]), _ptr(c[l:]),
-                                                  l, w, L, W, _ptr(grid), stream_handle()))
+    o = l + w
+    _native.check(_native.lib().sa_xt_interp_grid(_ptr(xT.contiguous()), _ptr(c[:l]), _ptr(c[l:o]),
+                                                  l, w, _ptr(c[o:o + L]), L, _ptr(c[o + L:]), W,
+                                                  _ptr(grid), stream_handle()))
     return grid
+
+
+def xt_normalize(acc: XTCounts) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(mats [3, C] scoring/shot/move probabilities, trans_t [C, C]) on device."""
+    C = acc.C
+    dev = acc.shot.device
+    mats = torch.empty((3, C), dtype=torch.float64, device=dev)
+    tt = torch.empty((C, C), dtype=torch.float64, device=dev)
+    _native.check(_native.lib().sa_xt_normalize(_ptr(acc.shot), _ptr(acc.goal), _ptr(acc.move),
+                                                _ptr(acc.trans), acc.l, acc.w, _ptr(mats), _ptr(tt),
+                                                stream_handle()))
+    return mats, tt
 
 
 def xt_rate(batch: ActionBatch, grid: torch.Tensor, L: int, W: int) -> Tuple[torch.Tensor, torch.Tensor]:

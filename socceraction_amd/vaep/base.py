@@ -18,7 +18,7 @@ import pandas as pd
 from sklearn.exceptions import NotFittedError
 from sklearn.metrics import brier_score_loss, roc_auc_score
 
-from .. import ops
+from .. import catalog, ops
 from .. import spadl as spadlcfg
 from ..batch import ActionBatch
 from . import features as fs
@@ -116,7 +116,8 @@ class VAEP:
             if i in parts:
                 frames.append(parts[i])
             else:
-                ncols = len(self._fs.xfn_columns_for(f, self.nb_prev_actions, self._atomic))
+                ncols = len(catalog.xfn_columns(self._fs.xfn_name(f, self._atomic),
+                                                self.nb_prev_actions, self._atomic))
                 frames.append(kdf.iloc[:, pos:pos + ncols])
                 pos += ncols
         return pd.concat(frames, axis=1)

@@ -1,0 +1,348 @@
+"""CPU-only tests: C-ABI library surface, host-side logic (catalogue, plans, batches,
+sharding) and the host helpers the reference's own tests pin. No GPU needed."""
+import json
+import os
+import re
+
+import numpy as np
+import pandas as pd
+import pytest
+
+from golden_io import cases, inputs, ks, load
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+# ----------------------------------------------------------------------------- C ABI
+def _declared_functions():
+    with open(os.path.join(ROOT, 'include', 'socceraction_amd.h')) as f:
+        src = f.read()
+    src = re.sub(r'/\*.*?\*/', '', src, flags=re.S)
+    return sorted(set(re.findall(r'\b(sa_[a-z0-9_]+)\s*\(', src)))
+
+
+def test_library_builds_and_exports_every_declared_symbol():
+    from socceraction_amd import _native, build
+    build.build(force=False, verbose=False)
+    lib = _native.load_library()
+    declared = _declared_functions()
+    assert 'sa_vaep_features' in declared and 'sa_xt_solve' in declared
+    for sym in declared:
+        assert hasattr(lib, sym), sym
+    assert set(declared) == set(_native.EXPORTED_SYMBOLS)
+    assert lib.sa_abi_version() == 1
+
+
+def test_ctypes_struct_layout_matches_header():
+    """Struct sizes the kernels see: sa_frame = 10 pointers, sa_actions = 40 B + 8 frames."""
+    import ctypes
+
+    from socceraction_amd import _native
+    assert ctypes.sizeof(_native.SaFrame) == 80
+    assert ctypes.sizeof(_native.SaActions) == 40 + 8 * 80
+    assert ctypes.sizeof(_native.SaFeaturePlan) == 4 * (1 + 3 * _native.SA_XFN_COUNT)
+    with open(os.path.join(ROOT, 'include', 'socceraction_amd.h')) as f:
+        enum = f.read().split('enum sa_xfn {')[1].split('};')[0]
+    names = re.findall(r'SA_XFN_([A-Z_]+)', enum)
+    assert [n.lower() for n in names[:-1]] == _native.XFN_NAMES and names[-1] == 'COUNT'
+
+
+def test_invalid_arguments_are_rejected_without_a_gpu():
+    """Argument validation happens before any HIP call (returns SA_EINVAL)."""
+    import ctypes
+
+    from socceraction_amd import _native
+    lib = _native.load_library()
+    s = _native.SaActions()
+    s.n, s.n_segments, s.n_frames = 10, 1, 0
+    plan = _native.SaFeaturePlan()
+    rc = lib.sa_vaep_features(ctypes.byref(s), ctypes.byref(plan), None, None, None, 16, None)
+    assert rc == _native.SA_EINVAL
+    assert b'n_frames' in lib.sa_last_error()
+    with pytest.raises(ValueError):
+        _native.check(rc)
+
+
+# ----------------------------------------------------------------------------- catalogue
+@pytest.mark.parametrize('prefix', ['spadl', 'atomic'])
+def test_catalogue_names_match_reference(prefix):
+    from socceraction_amd import catalog
+    from socceraction_amd.atomic.vaep import base as abase
+    from socceraction_amd.vaep import base as vbase
+    atomic = prefix == 'atomic'
+    xfns = [f._sa_xfn for f in (abase.xfns_default if atomic else vbase.xfns_default)]
+    for name in cases(prefix):
+        g = load(prefix, name)
+        for k in ks(g):
+            plan = catalog.build_plan(xfns, k, atomic)
+            assert plan.names == list(g[f'k{k}_names_all'])
+            assert [c[1] for c in plan.order] == list(g[f'k{k}_kinds_all'])
+
+
+def test_default_plan_block_sizes():
+    from socceraction_amd import catalog
+    from socceraction_amd.atomic.vaep import base as abase
+    from socceraction_amd.vaep import base as vbase
+    p = catalog.build_plan([f._sa_xfn for f in vbase.xfns_default], 3)
+    assert (p.n_bool, p.n_f64, p.n_i64) == (515, 47, 6)
+    p = catalog.build_plan([f._sa_xfn for f in abase.xfns_default], 3, atomic=True)
+    assert (p.n_bool, p.n_f64, p.n_i64) == (110, 32, 12)
+    with pytest.raises(ValueError):
+        catalog.build_plan(['location'], 3, atomic=False)
+    with pytest.raises(ValueError):
+        catalog.build_plan(['movement'], 3, atomic=True)
+    with pytest.raises(ValueError):
+        catalog.build_plan(['time'], 9)
+
+
+def test_feature_column_names_with_user_transformer():
+    from socceraction_amd.vaep import base as vbase
+    from socceraction_amd.vaep import features as fs
+
+    @fs.simple
+    def myfeat(actions):
+        return pd.DataFrame({'double_x': actions['start_x'] * 2})
+
+    names = fs.feature_column_names(vbase.xfns_default + [myfeat], 2)
+    assert names[-2:] == ['double_x_a0', 'double_x_a1']
+    g = load('spadl', 'fixture')
+    assert fs.feature_column_names(vbase.xfns_default, 3) == list(g['k3_names_all'])
+
+
+def test_host_gamestates_and_flip_match_oracle():
+    from oracle import vaep_oracle as vo
+    from socceraction_amd.vaep import features as fs
+    g = load('spadl', 'n40')
+    cols = inputs(g)
+    df = pd.DataFrame(cols)
+    gs = fs.play_left_to_right(fs.gamestates(df, 3), g['home_team_id'][0])
+    for i, a in enumerate(gs):
+        rows = vo.window_rows(len(df), np.array([0, len(df)]), i)
+        away = cols['team_id'] != g['home_team_id'][0]
+        exp = np.where(away, 105.0 - cols['start_x'][rows], cols['start_x'][rows])
+        np.testing.assert_array_equal(a['start_x'].to_numpy(), exp)
+
+
+# ----------------------------------------------------------------------------- batches
+def test_encode_teams_preserves_equality():
+    from socceraction_amd.batch import encode_teams
+    ids = np.array(['b', 'a', 'b', 'c'], dtype=object)
+    codes, home = encode_teams(ids, ['c', 'zz'])
+    assert (codes[0] == codes[2]) and len(set(codes.tolist())) == 3
+    assert home[0] == codes[3] and home[1] == -1
+    big = np.array([2**40, 5, 2**40])
+    codes, home = encode_teams(big, [5])
+    assert codes[0] == codes[2] != codes[1] and home[0] == codes[1]
+    with pytest.raises(ValueError):
+        encode_teams(np.array([1.0, np.nan]))
+
+
+def test_encode_columns_validates_like_the_schema():
+    from socceraction_amd.batch import encode_columns
+    g = load('spadl', 'fixture')
+    df = pd.DataFrame(inputs(g))
+    cols = encode_columns(df, atomic=False)
+    assert cols['type_id'].dtype == np.uint8 and cols['c0'].dtype == np.float64
+    bad = df.copy()
+    bad.loc[3, 'type_id'] = 23
+    with pytest.raises(ValueError):
+        encode_columns(bad, atomic=False)
+    bad = df.copy()
+    bad.loc[3, 'result_id'] = 6
+    with pytest.raises(ValueError):
+        encode_columns(bad, atomic=False)
+    names = df.drop(columns=['type_id']).assign(type_name=['pass'] * len(df))
+    assert (encode_columns(names, atomic=False)['type_id'] == 0).all()
+
+
+def test_segment_offsets():
+    from socceraction_amd.batch import segment_offsets
+    np.testing.assert_array_equal(segment_offsets(np.array([7, 7, 3, 3, 3, 9])), [0, 2, 5, 6])
+    np.testing.assert_array_equal(segment_offsets(np.array([], dtype=np.int64)), [0])
+
+
+# ----------------------------------------------------------------------------- sharding
+def test_partition_games_covers_every_game_once():
+    from socceraction_amd import shard, synthetic
+    d = synthetic.spadl_games(101)
+    off = d['game_off']
+    for world in (1, 2, 3, 4, 8):
+        parts = shard.partition_games(off, world)
+        assert parts[0][0] == 0 and parts[-1][1] == 101
+        assert all(a[1] == b[0] for a, b in zip(parts, parts[1:]))
+        sizes = [off[b] - off[a] for a, b in parts]
+        assert max(sizes) - min(sizes) <= 2 * 2000  # within two games of balance
+
+
+def _gloo_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+
+    from oracle import xt_oracle as xo
+    from socceraction_amd import shard, synthetic
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    d = synthetic.spadl_games(6, seed=9)
+    off = d['game_off']
+    g0, g1 = shard.partition_games(off, world)[rank]
+    s, e = int(off[g0]), int(off[g1])
+    l, w = 8, 6
+    C = l * w
+    cols = {c: d[c][s:e] for c in ('start_x', 'start_y', 'end_x', 'end_y', 'type_id', 'result_id')}
+    t = cols['type_id']
+    shot = t == 11
+    move = (t == 0) | (t == 21) | (t == 1)
+    succ = move & (cols['result_id'] == 1)
+    cnt = lambda m, x, y: np.bincount(xo.flat_indexes(x[m], y[m], l, w), minlength=C)  # noqa: E731
+    sh = torch.tensor(cnt(shot, cols['start_x'], cols['start_y']), dtype=torch.int64)
+    go = torch.tensor(cnt(shot & (cols['result_id'] == 1), cols['start_x'], cols['start_y']),
+                      dtype=torch.int64)
+    mv = torch.tensor(cnt(move, cols['start_x'], cols['start_y']), dtype=torch.int64)
+    tr = np.zeros(C * C, np.int32)
+    np.add.at(tr, xo.flat_indexes(cols['start_x'][succ], cols['start_y'][succ], l, w) * C +
+              xo.flat_indexes(cols['end_x'][succ], cols['end_y'][succ], l, w), 1)
+    tr = torch.tensor(tr)
+    err = torch.tensor([rank], dtype=torch.int32)
+    shard.allreduce_xt_counts(sh, go, mv, tr, err)
+    if rank == 0:
+        q.put((sh.numpy(), go.numpy(), mv.numpy(), tr.numpy(), int(err.item())))
+    dist.destroy_process_group()
+
+
+def test_xt_count_allreduce_gloo_world2():
+    """World-size-2 gloo run of the xT exchange step: sharded counts sum to the global ones."""
+    import multiprocessing as mp
+    import socket
+
+    from oracle import xt_oracle as xo
+    from socceraction_amd import synthetic
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_gloo_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    sh, go, mv, tr, err = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert err == 1
+    d = synthetic.spadl_games(6, seed=9)
+    f = xo.fit({c: d[c] for c in ('start_x', 'start_y', 'end_x', 'end_y', 'type_id',
+                                  'result_id')}, 8, 6)
+    total = mv.astype(np.float64) + sh
+    np.testing.assert_array_equal(np.divide(sh, total, out=np.zeros(48), where=total != 0),
+                                  f['shot_prob'].reshape(-1))
+    T = np.zeros((48, 48))
+    t2 = tr.reshape(48, 48)
+    nz = t2 != 0
+    T[nz] = t2[nz] / mv.astype(np.float64)[np.nonzero(nz)[0]]
+    np.testing.assert_array_equal(T, f['transition'])
+
+
+# ----------------------------------------------------------------------------- synthetic data
+def test_synthetic_generator_shape_and_determinism():
+    from socceraction_amd import synthetic
+    a = synthetic.spadl_games(20)
+    b = synthetic.spadl_games(20)
+    for k in a:
+        np.testing.assert_array_equal(a[k], b[k])
+    sizes = np.diff(a['game_off'])
+    assert sizes.min() >= 1200 and sizes.max() <= 2000
+    assert a['start_x'].min() >= 0 and a['start_x'].max() <= 105
+    assert a['end_y'].min() >= 0 and a['end_y'].max() <= 68
+    df = synthetic.to_frame(a)
+    assert len(df) == a['game_off'][-1] and df['type_id'].dtype == np.int64
+    gaps = df.groupby('game_id').time_seconds.diff().dropna()
+    assert 0.01 < (gaps.abs() > 10).mean() < 0.2
+    at = synthetic.atomic_games(3)
+    assert (at['type_id'] == 27).any() and at['type_id'].max() <= 32
+
+
+# ----------------------------------------------------------------------------- xT host helpers
+class TestGridCount:
+    """Known-answer tests of reference tests/test_xthreat.py:44-78 (host index helpers)."""
+
+    N = 2
+    M = 2
+
+    def test_get_cell_indexes(self):
+        from socceraction_amd import xthreat as xt
+        x = pd.Series([0, 105 / 2 - 1, 105.0])
+        y = pd.Series([0, 68 / 2 + 1, 68.0])
+        xi, yi = xt._get_cell_indexes(x, y, self.N, self.M)
+        pd.testing.assert_series_equal(xi, pd.Series([0, 0, 1]))
+        pd.testing.assert_series_equal(yi, pd.Series([0, 1, 1]))
+
+    def test_get_cell_indexes_out_of_bounds(self):
+        from socceraction_amd import xthreat as xt
+        xi, yi = xt._get_cell_indexes(pd.Series([-10.0, 115.0]), pd.Series([-10.0, 78.0]),
+                                      self.N, self.M)
+        pd.testing.assert_series_equal(xi, pd.Series([0, 1]))
+        pd.testing.assert_series_equal(yi, pd.Series([0, 1]))
+
+    def test_get_flat_indexes(self):
+        from socceraction_amd import xthreat as xt
+        x = pd.Series([0, 105 / 2 - 1, 105 / 2 + 1, 105.0])
+        y = pd.Series([0, 68 / 2 + 1, 68 / 2 - 1, 68.0])
+        pd.testing.assert_series_equal(xt._get_flat_indexes(x, y, self.N, self.M),
+                                       pd.Series([2, 0, 3, 1]))
+
+
+class TestModelPersistency:
+    """reference tests/test_xthreat.py:88-129 (host JSON I/O, NotFittedError)."""
+
+    def test_save_and_load_model(self, tmp_path):
+        from socceraction_amd import xthreat as xt
+        p = tmp_path / 'xt_model.json'
+        model = xt.ExpectedThreat()
+        model.xT = np.ones((model.w, model.l))
+        model.save_model(str(p))
+        assert p.read_text() == json.dumps(model.xT.tolist())
+        p.write_text(json.dumps([[0.1, 0.2], [0.1, 0.0]]))
+        m2 = xt.load_model(str(p))
+        assert (m2.w, m2.l) == (2, 2)
+        np.testing.assert_array_equal(m2.xT, [[0.1, 0.2], [0.1, 0.0]])
+
+    def test_save_model_not_fitted_and_exists(self, tmp_path):
+        from sklearn.exceptions import NotFittedError
+
+        from socceraction_amd import xthreat as xt
+        p = tmp_path / 'xt_model.json'
+        model = xt.ExpectedThreat()
+        with pytest.raises(NotFittedError):
+            model.save_model(str(p))
+        p.write_text('create file')
+        model.xT = np.ones((model.w, model.l))
+        with pytest.raises(ValueError):
+            model.save_model(str(p), overwrite=False)
+        model.save_model(str(p), overwrite=True)
+
+    def test_init_and_rate_not_fitted(self):
+        from sklearn.exceptions import NotFittedError
+
+        from socceraction_amd import xthreat as xt
+        m = xt.ExpectedThreat(l=8, w=6, eps=1e-3)
+        assert (m.l, m.w, m.eps) == (8, 6, 1e-3) and np.sum(m.xT) == 0
+        assert m.transition_matrix is None and len(m.heatmaps) == 0
+        with pytest.raises(NotFittedError):
+            m.rate(pd.DataFrame({'type_id': [0]}))
+
+    def test_interpolate_without_interp2d(self, monkeypatch):
+        from socceraction_amd import xthreat as xt
+        monkeypatch.setattr(xt, 'interp2d', None)
+        with pytest.raises(ImportError, match='Interpolation requires scipy to be installed.'):
+            xt.ExpectedThreat().interpolator()
+
+
+def test_move_filters_on_reference_fixture():
+    """reference tests/test_xthreat.py:132-154 (pandas filters)."""
+    from socceraction_amd import xthreat as xt
+    g = load('spadl', 'fixture')
+    df = pd.DataFrame(inputs(g))
+    mv = xt.get_move_actions(df)
+    assert mv.type_id.isin([0, 21, 1]).all() and len(mv) > 0
+    sm = xt.get_successful_move_actions(df)
+    assert (sm.result_id == 1).all()
