@@ -1,0 +1,50 @@
+"""Copy rocprofv3 results of one profiling round into profiles/ and derive HBM traffic.
+
+    python scripts/summarize_profile.py r01 [N_ACTIONS]
+
+Reads gpurun_out/prof_<tag>_{trace,fetch,write}/ (see scripts/profile_round.sh) and writes
+  profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary
+  profiles/<tag>_pmc.csv            per-kernel mean FETCH_SIZE / WRITE_SIZE (KiB) + HBM bytes
+  profiles/pmc_features_kernel.json features_kernel HBM bytes per action (read by bench.py)
+HBM bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024: on gfx950 FETCH_SIZE reports half the
+bytes of wide streaming reads (MI355X_MICROARCH.md, HBM section); WRITE_SIZE is exact for
+16-byte-per-lane streaming stores.
+"""
+import json
+import os
+import shutil
+import sys
+
+import pandas as pd
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def main(tag: str, n_actions: int) -> None:
+    out = os.path.join(ROOT, 'profiles')
+    src = os.path.join(ROOT, 'gpurun_out')
+    shutil.copy(os.path.join(src, f'prof_{tag}_trace', 'run_kernel_stats.csv'),
+                os.path.join(out, f'{tag}_kernel_stats.csv'))
+    rows = {}
+    for kind in ('fetch', 'write'):
+        p = os.path.join(src, f'prof_{tag}_{kind}', 'run_counter_collection.csv')
+        t = pd.read_csv(p)
+        for (k, c), v in t.groupby(['Kernel_Name', 'Counter_Name']).Counter_Value.mean().items():
+            rows.setdefault(k, {})[c] = v
+    df = pd.DataFrame.from_dict(rows, orient='index')
+    df['hbm_bytes'] = (2 * df['FETCH_SIZE'] + df['WRITE_SIZE']) * 1024
+    df['hbm_bytes_per_action'] = df['hbm_bytes'] / n_actions
+    df.index.name = 'kernel'
+    df.to_csv(os.path.join(out, f'{tag}_pmc.csv'))
+    feat = [k for k in df.index if 'features_kernel' in k][0]
+    with open(os.path.join(out, 'pmc_features_kernel.json'), 'w') as f:
+        json.dump({'tag': tag, 'kernel': feat, 'n_actions': n_actions,
+                   'fetch_kib': float(df.loc[feat, 'FETCH_SIZE']),
+                   'write_kib': float(df.loc[feat, 'WRITE_SIZE']),
+                   'hbm_bytes_per_launch_per_action': float(df.loc[feat, 'hbm_bytes_per_action'])},
+                  f, indent=1)
+    print(df.to_string())
+
+
+if __name__ == '__main__':
+    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 15992198)
