@@ -35,9 +35,12 @@ SPADL_DEFAULT = ['actiontype_onehot', 'result_onehot', 'actiontype_result_onehot
                  'bodypart_onehot', 'time', 'startlocation', 'endlocation', 'startpolar',
                  'endpolar', 'movement', 'team', 'time_delta', 'space_delta', 'goalscore']
 
-# algorithmic bytes per action of each kernel (inputs read once + outputs written once)
-BYTES = {'features': 48 + 515 + 47 * 8 + 3 * 8,  # 963
+# algorithmic bytes per action of each kernel (its inputs read once + outputs written once;
+# DESIGN.md "Kernels and rooflines")
+BYTES = {'bool_features': 7 + 515,             # type/result/bodypart u8 + team i32 -> 515 bools
+         'num_features': 48 + 47 * 8 + 3 * 8,  # 5 f64 + 4 u8 + team -> 47 f64 + 3 i64
          'goalscore': 6 + 24, 'labels': 6 + 2, 'formula': 30 + 24}
+KERNELS = ('bool_features', 'num_features', 'goalscore', 'labels', 'formula')
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 
@@ -91,10 +94,20 @@ def main() -> None:
     n = ab.n
     plan = catalog.build_plan(SPADL_DEFAULT, 3)
     out = ops.alloc_feature_blocks(plan, n, dev)
-    fplan = copy.copy(plan)  # features call without goalscore: timed as its own launch
-    fplan.struct = copy.deepcopy(plan.struct)
-    fplan.struct.i64_col[XFN['goalscore']] = -1
-    fout = ops.FeatureBlocks(fplan, n, out.ld, out.bool_block, out.f64_block, out.i64_block)
+
+    def sub(keep):  # the same block layout with only some column families launched
+        q = copy.copy(plan)
+        q.struct = copy.deepcopy(plan.struct)
+        for x in range(len(q.struct.bool_col)):
+            if 'b' not in keep:
+                q.struct.bool_col[x] = -1
+            if 'f' not in keep:
+                q.struct.f64_col[x] = -1
+            if 'i' not in keep or x == XFN['goalscore']:
+                q.struct.i64_col[x] = -1
+        return ops.FeatureBlocks(q, n, out.ld, out.bool_block, out.f64_block, out.i64_block)
+
+    bool_out, num_out = sub('b'), sub('fi')
     p = synthetic.probabilities(n)
     ps = torch.from_numpy(p['scores']).to(dev)
     pc = torch.from_numpy(p['concedes']).to(dev)
@@ -102,27 +115,25 @@ def main() -> None:
     lab = ops.LabelBlocks(n, lab_buf[0], lab_buf[1], None)
     val = torch.empty((3, out.ld), dtype=torch.float64, device=dev)
     s_act = ab.struct()
+    calls = (lambda: ops.features_into(s_act, bool_out),
+             lambda: ops.features_into(s_act, num_out),
+             lambda: ops.goalscore_into(ab, out),
+             lambda: ops.labels(ab, 10, lab),
+             lambda: ops.formula(ab, ps, pc, val))
 
     def step(ev=None):
+        for i, call in enumerate(calls):
+            if ev is not None:
+                ev[i].record()
+            call()
         if ev is not None:
-            ev[0].record()
-        ops.features_into(s_act, fout)
-        if ev is not None:
-            ev[1].record()
-        ops.goalscore_into(ab, out)
-        if ev is not None:
-            ev[2].record()
-        ops.labels(ab, 10, lab)
-        if ev is not None:
-            ev[3].record()
-        ops.formula(ab, ps, pc, val)
-        if ev is not None:
-            ev[4].record()
+            ev[len(calls)].record()
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(5)] for _ in range(args.steps)]
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(len(calls) + 1)]
+           for _ in range(args.steps)]
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -134,7 +145,7 @@ def main() -> None:
         dist.barrier()
     wall = time.perf_counter() - t0
     kern = {name: float(np.mean([e[i].elapsed_time(e[i + 1]) for e in evs]))
-            for i, name in enumerate(('features', 'goalscore', 'labels', 'formula'))}
+            for i, name in enumerate(KERNELS)}
     total_actions = n
     if dist:
         t = torch.tensor([wall], dtype=torch.float64, device=dev)
@@ -149,15 +160,18 @@ def main() -> None:
         return
     ms_per_step = wall / args.steps * 1e3
     value = total_actions * args.steps / wall
-    feat_ms = kern['features']
-    achieved = BYTES['features'] * n / (feat_ms * 1e-3) / 1e9
+    dom = max(KERNELS, key=lambda k: BYTES[k])  # dominant kernel by algorithmic bytes
+    achieved = BYTES[dom] * n / (kern[dom] * 1e-3) / 1e9
+    per_kernel = {k: {'ms': round(kern[k], 4), 'bytes_per_action': BYTES[k],
+                      'achieved_GBs': round(BYTES[k] * n / (kern[k] * 1e-3) / 1e9, 1)}
+                  for k in KERNELS}
     traffic = None
-    pmc = os.path.join(ROOT, 'profiles', 'pmc_features_kernel.json')
+    pmc = os.path.join(ROOT, 'profiles', 'pmc_dominant_kernel.json')
     if os.path.exists(pmc):
         with open(pmc) as f:
-            traffic = json.load(f).get('hbm_bytes_per_launch_per_action')
-        if traffic is not None:
-            traffic = round(traffic * n)
+            rec = json.load(f)
+        if dom in rec.get('kernel', ''):
+            traffic = round(rec['hbm_bytes_per_launch_per_action'] * n)
     line = {
         'metric': 'SPADL actions/sec valued (VAEP feat+labels+formula, xT fit+rate) at 1/2/4/8 GPUs',
         'value': round(value, 1), 'unit': 'actions/s', 'n_gpus': world, 'steps': args.steps,
@@ -168,11 +182,11 @@ def main() -> None:
                                '(k=3, default xfns, 568 cols) + compute_labels + formula.value (f64)',
                    'games_per_gpu': args.games, 'actions_per_gpu': n,
                    'parallelism': f'games sharded over {world} GPU(s)'},
-        'kernels_ms': {k: round(v, 4) for k, v in kern.items()},
+        'kernels': per_kernel,
         'roofline': {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS,
                      'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 4),
-                     'traffic': traffic, 'kernel': 'features_kernel',
-                     'bytes_per_action': BYTES['features']},
+                     'traffic': traffic, 'kernel': f'{dom}_kernel',
+                     'bytes_per_action': BYTES[dom]},
     }
     if not args.no_cpu:
         line['cpu_baseline'] = cpu_baseline(d, args.cpu_seconds)

@@ -5,7 +5,7 @@
 Reads gpurun_out/prof_<tag>_{trace,fetch,write}/ (see scripts/profile_round.sh) and writes
   profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary
   profiles/<tag>_pmc.csv            per-kernel mean FETCH_SIZE / WRITE_SIZE (KiB) + HBM bytes
-  profiles/pmc_features_kernel.json features_kernel HBM bytes per action (read by bench.py)
+  profiles/pmc_dominant_kernel.json HBM bytes per action of the dominant kernel (read by bench.py)
 HBM bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024: on gfx950 FETCH_SIZE reports half the
 bytes of wide streaming reads (MI355X_MICROARCH.md, HBM section); WRITE_SIZE is exact for
 16-byte-per-lane streaming stores.
@@ -20,7 +20,7 @@ import pandas as pd
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def main(tag: str, n_actions: int) -> None:
+def main(tag: str, n_actions: int, dominant: str = 'bool_features_kernel') -> None:
     out = os.path.join(ROOT, 'profiles')
     src = os.path.join(ROOT, 'gpurun_out')
     shutil.copy(os.path.join(src, f'prof_{tag}_trace', 'run_kernel_stats.csv'),
@@ -36,8 +36,8 @@ def main(tag: str, n_actions: int) -> None:
     df['hbm_bytes_per_action'] = df['hbm_bytes'] / n_actions
     df.index.name = 'kernel'
     df.to_csv(os.path.join(out, f'{tag}_pmc.csv'))
-    feat = [k for k in df.index if 'features_kernel' in k][0]
-    with open(os.path.join(out, 'pmc_features_kernel.json'), 'w') as f:
+    feat = [k for k in df.index if dominant in k][0]
+    with open(os.path.join(out, 'pmc_dominant_kernel.json'), 'w') as f:
         json.dump({'tag': tag, 'kernel': feat, 'n_actions': n_actions,
                    'fetch_kib': float(df.loc[feat, 'FETCH_SIZE']),
                    'write_kib': float(df.loc[feat, 'WRITE_SIZE']),
@@ -47,4 +47,5 @@ def main(tag: str, n_actions: int) -> None:
 
 
 if __name__ == '__main__':
-    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 15992198)
+    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 15992198,
+         sys.argv[3] if len(sys.argv) > 3 else 'bool_features_kernel')

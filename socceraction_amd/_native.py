@@ -12,7 +12,7 @@ import os
 from typing import Optional
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, '_lib', 'libsocceraction_amd.so')
+LIB_PATH = os.environ.get('SOCCERACTION_AMD_LIB') or os.path.join(HERE, '_lib', 'libsocceraction_amd.so')
 
 SA_MAX_FRAMES = 8
 SA_OK, SA_EINVAL, SA_EHIP, SA_EDATA, SA_ENOMEM = 0, -1, -2, -3, -4

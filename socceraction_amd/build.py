@@ -36,18 +36,23 @@ def _stale() -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = True) -> str:
-    if not force and not _stale():
-        return OUT
-    os.makedirs(os.path.dirname(OUT), exist_ok=True)
-    tmp = OUT + '.tmp'
-    cmd = [hipcc()] + FLAGS + [os.path.join(CSRC, s) for s in SOURCES] + ['-o', tmp]
+def build(force: bool = False, verbose: bool = True, defines=(), out: str = OUT) -> str:
+    """Compile the library; ``defines`` (e.g. ``['SA_NT_STORES=0']``) build A/B variants."""
+    if out == OUT and not defines and not force and not _stale():
+        return out
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    tmp = out + '.tmp'
+    cmd = [hipcc()] + FLAGS + [f'-D{d}' for d in defines] + \
+        [os.path.join(CSRC, s) for s in SOURCES] + ['-o', tmp]
     if verbose:
         print(' '.join(cmd), flush=True)
     subprocess.run(cmd, check=True, cwd=CSRC)
-    os.replace(tmp, OUT)
-    return OUT
+    os.replace(tmp, out)
+    return out
 
 
 if __name__ == '__main__':
-    print(build(force='--force' in sys.argv))
+    defs = [a[2:] for a in sys.argv[1:] if a.startswith('-D')]
+    variant = [a.split('=', 1)[1] for a in sys.argv[1:] if a.startswith('--variant=')]
+    target = OUT if not variant else os.path.join(HERE, '_lib', f'libsocceraction_amd_{variant[0]}.so')
+    print(build(force='--force' in sys.argv, defines=defs, out=target))

@@ -1,16 +1,20 @@
 // VAEP / Atomic-VAEP hot-path kernels for gfx950 (MI355X).
 //
-//   features_kernel   gamestates + play_left_to_right + every known transformer,
-//                     fused; writes column-major bool / f64 / i64 blocks.
-//   goalscore_kernel  segmented exclusive scan (one workgroup per segment).
-//   labels_kernel     scores / concedes / goal_from_shot look-ahead.
-//   formula_kernel    offensive / defensive / vaep value (f64 or f32).
+//   bool_features_kernel  one-hot + team features (gamestates + flip fused in), bool block
+//   num_features_kernel   time / location / polar / movement / deltas / ids, f64 + i64 blocks
+//   goalscore_kernel      segmented exclusive scan (one workgroup per segment)
+//   labels_kernel         scores / concedes / goal_from_shot look-ahead
+//   formula_kernel        offensive / defensive / vaep value (f64 or f32)
 //
-// All of it is HBM-bound byte/int/f64 streaming: nothing here is GEMM-shaped.
-// Layout: one wave owns 1024 consecutive actions.  Bool columns
-// are written with lane-owns-16-actions (one 16-B store per lane = 1 KiB per wave
-// instruction); f64/i64 columns with lane-owns-2-actions (again 1 KiB per wave
-// instruction).  Per-action window metadata passes between the two phases in LDS.
+// All of it is HBM-bound byte/int/f64 streaming; nothing here is GEMM-shaped.  The output
+// is ~94 % of the traffic, so the kernels are built around full-width stores:
+//  * bool columns: a lane owns 16 consecutive actions and writes one 16-B word per column,
+//    so one store instruction writes 1 KiB of one column;
+//  * f64 / i64 columns: a lane owns 2 consecutive actions (one 16-B store), so one store
+//    instruction writes 1 KiB of one column.
+// Long runs per column per wave matter (see bool_features_kernel).  Game-state windows
+// never leave registers: window i of action j is row j - min(i, j - segment_start)
+// (vaep/features.py:83-88), built with funnel shifts from the lane's rows j0-8 .. j0+15.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -18,12 +22,21 @@
 #include "sa_common.h"
 #include "sa_internal.h"
 
+#ifndef SA_NT_STORES
+#define SA_NT_STORES 1
+#endif
+
 namespace sa {
 
 constexpr int WAVE = 64;
 constexpr int LANE_ACTS = 16;
-constexpr int WAVE_ACTS = WAVE * LANE_ACTS;  // 1024
+#ifndef SA_NUM_PAIRS
+#define SA_NUM_PAIRS 8
+#endif
 constexpr int BLOCK_WAVES = 4;
+constexpr int NUM_PAIRS = SA_NUM_PAIRS;         // 2-action pairs per lane in num_features_kernel
+constexpr int WAVE_ACTS = 128 * NUM_PAIRS;      // actions per wave in num_features_kernel
+constexpr int BLOCK_ACTS = WAVE_ACTS * BLOCK_WAVES;
 
 struct FeatArgs {
   sa_actions a;
@@ -34,252 +47,338 @@ struct FeatArgs {
   int64_t ld;
 };
 
-__device__ __forceinline__ uint32_t pick6(const uint32_t (&W)[6], int idx) {
-  uint32_t r = W[0];
-#pragma unroll
-  for (int k = 1; k < 6; ++k) r = (idx == k) ? W[k] : r;
-  return r;
+// ------------------------------------------------------------------------------ helpers
+struct SegCursor {
+  int64_t g, s, e;  // segment index, start, end (exclusive)
+};
+
+__device__ __forceinline__ SegCursor seg_at(const sa_actions& A, int64_t j) {
+  SegCursor c;
+  c.g = find_segment(A.seg_off, A.n_segments, j);
+  c.s = A.seg_off[c.g];
+  c.e = A.seg_off[c.g + 1];
+  return c;
 }
 
-// byte at position B (0..23) of the 24-byte window W
-__device__ __forceinline__ uint32_t byte24(const uint32_t (&W)[6], int B) {
-  return (pick6(W, B >> 2) >> (8 * (B & 3))) & 0xFFu;
-}
-
-__device__ __forceinline__ int32_t pick24(const int32_t (&T)[24], int idx) {
-  int32_t r = T[0];
-#pragma unroll
-  for (int k = 1; k < 24; ++k) r = (idx == k) ? T[k] : r;
-  return r;
-}
-
-// Word q (bytes 4q..4q+3 of the lane's 16 actions) of game-state window i, where the
-// lane's rows j0-8 .. j0+15 sit in W (byte 8 = row j0) and d[m] = min(j - seg_start, 15).
-__device__ __forceinline__ uint32_t window_word(const uint32_t (&W)[6], const uint32_t (&dw)[4],
-                                                int q, int i, bool slow) {
-  int B = 8 + 4 * q - i;  // 0 <= B <= 20
-  uint32_t v = funnel_bytes(pick6(W, B >> 2), pick6(W, (B >> 2) + 1), B & 3);
-  if (slow) {
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      int d = (int)byte_of(dw[q], b);
-      if (d < i) {  // window row clamps to the segment start: row j - d
-        uint32_t x = byte24(W, 8 + 4 * q + b - d);
-        v = (v & ~(0xFFu << (8 * b))) | (x << (8 * b));
-      }
-    }
+__device__ __forceinline__ void seg_advance(const sa_actions& A, SegCursor& c, int64_t j) {
+  while (j >= c.e) {
+    ++c.g;
+    c.s = c.e;
+    c.e = A.seg_off[c.g + 1];
   }
-  return v;
+}
+
+// Game-state windows of a lane's 16 actions, kept as 16 bytes (4 words) per id column.
+// R[0..5] holds rows j0-8 .. j0+15 (byte 8 = row j0).  Window i+1 is the window-i rows
+// shifted by one row, except for actions whose row already reached the segment start
+// (d = j - seg_start < i+1): they keep their window-i byte (vaep/features.py:83-88 clamps
+// the shifted frames at the first row).  Everything stays in registers (static indices).
+__device__ __forceinline__ void shift_rows(uint32_t (&R)[6]) {
+#pragma unroll
+  for (int k = 5; k > 0; --k) R[k] = funnel_bytes(R[k - 1], R[k], 3);  // (R[k] << 8) | R[k-1] >> 24
+  R[0] <<= 8;
+}
+
+// 0xFF in every byte whose d (0..15) is >= i (1..15); all-ones when i == 0
+__device__ __forceinline__ uint32_t ge_mask(uint32_t dw, int i) {
+  const uint32_t x = (dw + (uint32_t)(16 - i) * 0x01010101u) & 0x10101010u;
+  return (x >> 4) * 0xFFu;
+}
+
+template <typename V, typename P>
+__device__ __forceinline__ void st16(P* p, V v) {
+#if SA_NT_STORES
+  __builtin_nontemporal_store(v, reinterpret_cast<V*>(p));
+#else
+  *reinterpret_cast<V*>(p) = v;
+#endif
 }
 
 __device__ __forceinline__ void st_bool16(uint8_t* __restrict__ base, int64_t col, int64_t ld,
                                           int64_t j0, uint32_t w0, uint32_t w1, uint32_t w2,
                                           uint32_t w3) {
   u32x4 v = {w0, w1, w2, w3};
-  __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(base + col * ld + j0));
+  st16(base + col * ld + j0, v);
 }
 
 __device__ __forceinline__ void st_f64x2(double* __restrict__ base, int64_t col, int64_t ld,
                                          int64_t j, double v0, double v1) {
   f64x2 v = {v0, v1};
-  __builtin_nontemporal_store(v, reinterpret_cast<f64x2*>(base + col * ld + j));
+  st16(base + col * ld + j, v);
 }
 
 __device__ __forceinline__ void st_i64x2(int64_t* __restrict__ base, int64_t col, int64_t ld,
                                          int64_t j, int64_t v0, int64_t v1) {
   i64x2 v = {(long long)v0, (long long)v1};
-  __builtin_nontemporal_store(v, reinterpret_cast<i64x2*>(base + col * ld + j));
+  st16(base + col * ld + j, v);
 }
 
-// nan_to_num(arctan(dy / dx)) of vaep/features.py:376 (atan of +-inf is +-pi/2, 0/0 -> 0)
+// nan_to_num(arctan(dy / dx)) of vaep/features.py:376 (atan(+-inf) = +-pi/2, 0/0 -> 0)
 __device__ __forceinline__ double polar_angle(double dy, double dx) {
-  double a = atan(dy / dx);
+  const double a = atan(dy / dx);
   return isnan(a) ? 0.0 : a;
 }
 
+// 0x01-per-byte mask -> 4 bits
+__device__ __forceinline__ uint32_t pack4(uint32_t x) {
+  return (x & 1u) | ((x >> 7) & 2u) | ((x >> 14) & 4u) | ((x >> 21) & 8u);
+}
+
+// goal / owngoal bytes of a word of type / result bytes (vaep/labels.py:28-33;
+// atomic/vaep/labels.py:27-28)
+__device__ __forceinline__ void goal_bytes(uint32_t tw, uint32_t rw, bool atomic, uint32_t& g,
+                                           uint32_t& o) {
+  if (atomic) {
+    g = bytes_eq(tw, AT_GOAL);
+    o = bytes_eq(tw, AT_OWNGOAL);
+  } else {
+    const uint32_t shot = bytes_eq(tw, T_SHOT) | bytes_eq(tw, T_SHOT_PENALTY) |
+                          bytes_eq(tw, T_SHOT_FREEKICK);
+    g = shot & bytes_eq(rw, R_SUCCESS);
+    o = shot & bytes_eq(rw, R_OWNGOAL);
+  }
+}
+
+// ------------------------------------------------------------------------------ bool block
+// actiontype_onehot, result_onehot, actiontype_result_onehot, bodypart_onehot, team.
+// A wave owns BOOL_G runs of 1024 consecutive actions; lane l owns actions 16l .. 16l+15 of
+// every run, so one store instruction writes 1 KiB of one column and the wave writes
+// BOOL_G KiB of each column back to back (long runs per column keep HBM rows open: the
+// column-major layout otherwise scatters a wave's output over 515 streams 16 MB apart).
+#ifndef SA_BOOL_G
+#define SA_BOOL_G 1
+#endif
+constexpr int BOOL_G = SA_BOOL_G;
+constexpr int BOOL_WAVE_ACTS = 1024 * BOOL_G;
+constexpr int BOOL_BLOCK_ACTS = BOOL_WAVE_ACTS * BLOCK_WAVES;
+
 template <bool ATOMIC, bool EXPLICIT>
-__global__ __launch_bounds__(256) void features_kernel(FeatArgs args) {
-  __shared__ __attribute__((aligned(16))) uint8_t info[BLOCK_WAVES][WAVE_ACTS];
+__global__ __launch_bounds__(256) void bool_features_kernel(FeatArgs args) {
+  __shared__ int32_t team_lds[BLOCK_WAVES][BOOL_WAVE_ACTS + 8];
   const int lane = threadIdx.x & (WAVE - 1);
   const int wv = threadIdx.x / WAVE;
   const sa_actions& A = args.a;
   const sa_feature_plan& P = args.p;
   const int64_t n = A.n;
   const int K = P.nb_prev_actions;
-  const int64_t wave_base = ((int64_t)blockIdx.x * BLOCK_WAVES + wv) * WAVE_ACTS;
-  const int64_t j0 = wave_base + (int64_t)lane * LANE_ACTS;
   const int64_t ld = args.ld;
+  const int64_t wave_base = ((int64_t)blockIdx.x * BLOCK_WAVES + wv) * BOOL_WAVE_ACTS;
   const sa_frame& F0 = A.frames[0];
-
-  // ---------------- per-action window metadata: d = min(j - seg_start, 15), away -------------
-  uint32_t dw[4] = {0, 0, 0, 0};  // rows >= n keep d = 0 (window rows stay in range)
-  uint32_t aw[4] = {0, 0, 0, 0};
-  int dmin = 15;
-  if (!EXPLICIT && j0 < n) {
-    int64_t g = find_segment(A.seg_off, A.n_segments, j0);
-    int64_t s = A.seg_off[g], e = A.seg_off[g + 1];
+  const int tcol = P.bool_col[SA_XFN_TEAM];
+  const bool need_team = tcol >= 0 && K > 1;
+  int64_t j0[BOOL_G];
 #pragma unroll
-    for (int m = 0; m < LANE_ACTS; ++m) {
-      int64_t j = j0 + m;
-      if (j < n) {
-        while (j >= e) {
-          ++g;
-          s = e;
-          e = A.seg_off[g + 1];
+  for (int g = 0; g < BOOL_G; ++g) j0[g] = wave_base + g * 1024 + (int64_t)lane * LANE_ACTS;
+
+  // d = min(j - seg_start, 15) per action; rows >= n keep d = 0 (windows stay in range)
+  uint32_t dw[BOOL_G][4];
+#pragma unroll
+  for (int g = 0; g < BOOL_G; ++g) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) dw[g][q] = 0;
+    if (!EXPLICIT && j0[g] < n) {
+      SegCursor c = seg_at(A, j0[g]);
+#pragma unroll
+      for (int m = 0; m < LANE_ACTS; ++m) {
+        const int64_t j = j0[g] + m;
+        if (j < n) {
+          seg_advance(A, c, j);
+          const int64_t dd = j - c.s;
+          const int d = dd > 15 ? 15 : (int)dd;
+          dw[g][m >> 2] |= (uint32_t)d << (8 * (m & 3));
         }
-        int64_t dd = j - s;
-        int d = dd > 15 ? 15 : (int)dd;
-        dmin = d < dmin ? d : dmin;
-        uint32_t away = (A.home_team != nullptr && F0.team[j] != A.home_team[g]) ? 1u : 0u;
-        dw[m >> 2] = (dw[m >> 2] & ~(0xFFu << (8 * (m & 3)))) | ((uint32_t)d << (8 * (m & 3)));
-        aw[m >> 2] |= away << (8 * (m & 3));
       }
     }
   }
-  {  // publish (d | away << 4) for phase B of this wave
-    u32x4 v = {dw[0] | (aw[0] << 4), dw[1] | (aw[1] << 4), dw[2] | (aw[2] << 4),
-               dw[3] | (aw[3] << 4)};
-    *reinterpret_cast<u32x4*>(&info[wv][lane * LANE_ACTS]) = v;
+  if (!EXPLICIT && need_team) {  // team codes of rows wave_base-8 .. wave_base+1024G-1 -> LDS
+    int32_t* tl = team_lds[wv];
+#pragma unroll
+    for (int g = 0; g < BOOL_G; ++g) {
+#pragma unroll
+      for (int m = 0; m < LANE_ACTS; ++m)
+        tl[8 + g * 1024 + lane * LANE_ACTS + m] = ld_or0(F0.team, j0[g] + m, n);
+    }
+    if (lane < 8) tl[lane] = ld_or0(F0.team, wave_base - 8 + lane, n);
   }
-
-  // ---------------- phase A: bool columns, lane owns 16 consecutive actions -------------------
-  const bool any_bool = P.bool_col[SA_XFN_ACTIONTYPE_ONEHOT] >= 0 ||
-                        P.bool_col[SA_XFN_RESULT_ONEHOT] >= 0 ||
-                        P.bool_col[SA_XFN_ACTIONTYPE_RESULT_ONEHOT] >= 0 ||
-                        P.bool_col[SA_XFN_BODYPART_ONEHOT] >= 0 || P.bool_col[SA_XFN_TEAM] >= 0;
-  if (any_bool && j0 < n) {
-    const int64_t wbase = j0 / 4 - 2;  // word index of row j0-8
-    uint32_t TW[6], RW[6], BW[6];
-    int32_t TM[24];
-    const bool need_team = P.bool_col[SA_XFN_TEAM] >= 0;
-    if (!EXPLICIT) {
+  __syncthreads();
+  if (j0[0] >= n) return;
+  uint32_t TR[BOOL_G][6], RR[BOOL_G][6], BR[BOOL_G][6];  // rows j0-8 .. j0+15, shifted per window
+  uint32_t tw[BOOL_G][4], rw[BOOL_G][4], bw[BOOL_G][4];  // window i of the lane's actions
+  if (!EXPLICIT) {
+#pragma unroll
+    for (int g = 0; g < BOOL_G; ++g) {
+      const int64_t wbase = j0[g] / 4 - 2;  // word index of row j0-8
 #pragma unroll
       for (int k = 0; k < 6; ++k) {
-        TW[k] = ld_u8x4(F0.type_id, wbase + k, n);
-        RW[k] = ATOMIC ? 0u : ld_u8x4(F0.result_id, wbase + k, n);
-        BW[k] = ld_u8x4(F0.bodypart_id, wbase + k, n);
-      }
-      if (need_team) {
-#pragma unroll
-        for (int k = 0; k < 24; ++k) TM[k] = ld_or0(F0.team, j0 - 8 + k, n);
+        TR[g][k] = ld_u8x4(F0.type_id, wbase + k, n);
+        RR[g][k] = ATOMIC ? 0u : ld_u8x4(F0.result_id, wbase + k, n);
+        BR[g][k] = ld_u8x4(F0.bodypart_id, wbase + k, n);
       }
     }
-    const bool slow = dmin < K - 1;
-    for (int i = 0; i < K; ++i) {
-      uint32_t tw[4], rw[4], bw[4];
+  }
+  const int c_type = P.bool_col[SA_XFN_ACTIONTYPE_ONEHOT];
+  const int c_res = ATOMIC ? -1 : P.bool_col[SA_XFN_RESULT_ONEHOT];
+  const int c_tr = ATOMIC ? -1 : P.bool_col[SA_XFN_ACTIONTYPE_RESULT_ONEHOT];
+  const int c_bp = P.bool_col[SA_XFN_BODYPART_ONEHOT];
+  for (int i = 0; i < K; ++i) {
+#pragma unroll
+    for (int g = 0; g < BOOL_G; ++g) {
       if (EXPLICIT) {
         const sa_frame& Fi = A.frames[i];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          tw[q] = ld_u8x4(Fi.type_id, j0 / 4 + q, n);
-          rw[q] = ATOMIC ? 0u : ld_u8x4(Fi.result_id, j0 / 4 + q, n);
-          bw[q] = ld_u8x4(Fi.bodypart_id, j0 / 4 + q, n);
+          tw[g][q] = ld_u8x4(Fi.type_id, j0[g] / 4 + q, n);
+          rw[g][q] = ATOMIC ? 0u : ld_u8x4(Fi.result_id, j0[g] / 4 + q, n);
+          bw[g][q] = ld_u8x4(Fi.bodypart_id, j0[g] / 4 + q, n);
         }
-      } else {
+      } else if (i == 0) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          tw[q] = window_word(TW, dw, q, i, slow);
-          rw[q] = ATOMIC ? 0u : window_word(RW, dw, q, i, slow);
-          bw[q] = window_word(BW, dw, q, i, slow);
+          tw[g][q] = TR[g][2 + q];
+          rw[g][q] = RR[g][2 + q];
+          bw[g][q] = BR[g][2 + q];
+        }
+      } else {
+        shift_rows(TR[g]);
+        if (!ATOMIC) shift_rows(RR[g]);
+        shift_rows(BR[g]);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint32_t mk = ge_mask(dw[g][q], i);  // actions whose window i is a new row
+          tw[g][q] = (TR[g][2 + q] & mk) | (tw[g][q] & ~mk);
+          rw[g][q] = (RR[g][2 + q] & mk) | (rw[g][q] & ~mk);
+          bw[g][q] = (BR[g][2 + q] & mk) | (bw[g][q] & ~mk);
         }
       }
-      int c = P.bool_col[SA_XFN_ACTIONTYPE_ONEHOT];
-      if (c >= 0) {
-        if (!ATOMIC) {
-          for (int t = 0; t < N_TYPES; ++t)
-            st_bool16(args.bout, c + i * N_TYPES + t, ld, j0, bytes_eq(tw[0], t), bytes_eq(tw[1], t),
-                      bytes_eq(tw[2], t), bytes_eq(tw[3], t));
-        } else {
-          // 33 atomic names, 32 unique: 'interception' (ids 10 and 24) is one column that is
-          // true for both ids (atomic/vaep/features.py:114-132 + atomic/spadl/config.py:25-36)
-          for (int u = 0; u < N_ATOMIC_NAMES; ++u) {
-            uint32_t id = u <= 23 ? (uint32_t)u : (uint32_t)u + 1;
-            uint32_t m0 = bytes_eq(tw[0], id), m1 = bytes_eq(tw[1], id), m2 = bytes_eq(tw[2], id),
-                     m3 = bytes_eq(tw[3], id);
+    }
+    if (c_type >= 0) {
+      if (!ATOMIC) {
+        for (int t = 0; t < N_TYPES; ++t) {
+#pragma unroll
+          for (int g = 0; g < BOOL_G; ++g)
+            st_bool16(args.bout, c_type + i * N_TYPES + t, ld, j0[g], bytes_eq(tw[g][0], t),
+                      bytes_eq(tw[g][1], t), bytes_eq(tw[g][2], t), bytes_eq(tw[g][3], t));
+        }
+      } else {
+        // 33 atomic names, 32 unique: 'interception' (ids 10 and 24) is ONE column true for
+        // both ids (atomic/vaep/features.py:114-132 + atomic/spadl/config.py:25-36)
+        for (int u = 0; u < N_ATOMIC_NAMES; ++u) {
+          const uint32_t id = u <= 23 ? (uint32_t)u : (uint32_t)u + 1;
+#pragma unroll
+          for (int g = 0; g < BOOL_G; ++g) {
+            uint32_t m0 = bytes_eq(tw[g][0], id), m1 = bytes_eq(tw[g][1], id),
+                     m2 = bytes_eq(tw[g][2], id), m3 = bytes_eq(tw[g][3], id);
             if (u == 10) {
-              m0 |= bytes_eq(tw[0], AT_INTERCEPTION2);
-              m1 |= bytes_eq(tw[1], AT_INTERCEPTION2);
-              m2 |= bytes_eq(tw[2], AT_INTERCEPTION2);
-              m3 |= bytes_eq(tw[3], AT_INTERCEPTION2);
+              m0 |= bytes_eq(tw[g][0], AT_INTERCEPTION2);
+              m1 |= bytes_eq(tw[g][1], AT_INTERCEPTION2);
+              m2 |= bytes_eq(tw[g][2], AT_INTERCEPTION2);
+              m3 |= bytes_eq(tw[g][3], AT_INTERCEPTION2);
             }
-            st_bool16(args.bout, c + i * N_ATOMIC_NAMES + u, ld, j0, m0, m1, m2, m3);
+            st_bool16(args.bout, c_type + i * N_ATOMIC_NAMES + u, ld, j0[g], m0, m1, m2, m3);
           }
         }
       }
-      c = P.bool_col[SA_XFN_RESULT_ONEHOT];
-      if (!ATOMIC && c >= 0) {
-        for (int r = 0; r < N_RESULTS; ++r)
-          st_bool16(args.bout, c + i * N_RESULTS + r, ld, j0, bytes_eq(rw[0], r), bytes_eq(rw[1], r),
-                    bytes_eq(rw[2], r), bytes_eq(rw[3], r));
-      }
-      c = P.bool_col[SA_XFN_ACTIONTYPE_RESULT_ONEHOT];
-      if (!ATOMIC && c >= 0) {
-        // code = type*6 + result per byte (type <= 22, result <= 5: no carries between bytes)
-        uint32_t cw[4];
+    }
+    if (c_res >= 0) {
+      for (int r = 0; r < N_RESULTS; ++r) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) cw[q] = (tw[q] << 2) + (tw[q] << 1) + rw[q];
-        const int64_t cb = c + (int64_t)i * N_TYPES * N_RESULTS;
-        for (int code = 0; code < N_TYPES * N_RESULTS; ++code)
-          st_bool16(args.bout, cb + code, ld, j0, bytes_eq(cw[0], code), bytes_eq(cw[1], code),
-                    bytes_eq(cw[2], code), bytes_eq(cw[3], code));
+        for (int g = 0; g < BOOL_G; ++g)
+          st_bool16(args.bout, c_res + i * N_RESULTS + r, ld, j0[g], bytes_eq(rw[g][0], r),
+                    bytes_eq(rw[g][1], r), bytes_eq(rw[g][2], r), bytes_eq(rw[g][3], r));
       }
-      c = P.bool_col[SA_XFN_BODYPART_ONEHOT];
-      if (c >= 0) {
-        for (int b = 0; b < N_BODYPARTS; ++b)
-          st_bool16(args.bout, c + i * N_BODYPARTS + b, ld, j0, bytes_eq(bw[0], b),
-                    bytes_eq(bw[1], b), bytes_eq(bw[2], b), bytes_eq(bw[3], b));
+    }
+    if (c_tr >= 0) {
+      // code = type*6 + result per byte (type <= 22, result <= 5: no carry between bytes)
+      uint32_t cw[BOOL_G][4];
+#pragma unroll
+      for (int g = 0; g < BOOL_G; ++g) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) cw[g][q] = (tw[g][q] << 2) + (tw[g][q] << 1) + rw[g][q];
       }
-      c = P.bool_col[SA_XFN_TEAM];
-      if (c >= 0 && i >= 1) {  // team_i = team[a_i] == team[a0] (features.py:430-452)
+      const int64_t cb = c_tr + (int64_t)i * N_TYPES * N_RESULTS;
+      for (int code = 0; code < N_TYPES * N_RESULTS; ++code) {
+#pragma unroll
+        for (int g = 0; g < BOOL_G; ++g)
+          st_bool16(args.bout, cb + code, ld, j0[g], bytes_eq(cw[g][0], code),
+                    bytes_eq(cw[g][1], code), bytes_eq(cw[g][2], code), bytes_eq(cw[g][3], code));
+      }
+    }
+    if (c_bp >= 0) {
+      for (int b = 0; b < N_BODYPARTS; ++b) {
+#pragma unroll
+        for (int g = 0; g < BOOL_G; ++g)
+          st_bool16(args.bout, c_bp + i * N_BODYPARTS + b, ld, j0[g], bytes_eq(bw[g][0], b),
+                    bytes_eq(bw[g][1], b), bytes_eq(bw[g][2], b), bytes_eq(bw[g][3], b));
+      }
+    }
+    if (need_team && i >= 1) {  // team_i = team[a_i] == team[a0] (features.py:448-452)
+#pragma unroll
+      for (int g = 0; g < BOOL_G; ++g) {
         uint32_t m[4] = {0, 0, 0, 0};
 #pragma unroll
         for (int mm = 0; mm < LANE_ACTS; ++mm) {
           int32_t t0, ti;
           if (EXPLICIT) {
-            t0 = ld_or0(A.frames[0].team, j0 + mm, n);
-            ti = ld_or0(A.frames[i].team, j0 + mm, n);
+            t0 = ld_or0(A.frames[0].team, j0[g] + mm, n);
+            ti = ld_or0(A.frames[i].team, j0[g] + mm, n);
           } else {
-            int d = (int)byte_of(dw[mm >> 2], mm & 3);
-            int s = d < i ? d : i;
-            t0 = TM[8 + mm];
-            ti = pick24(TM, 8 + mm - s);
+            const int d = (int)byte_of(dw[g][mm >> 2], mm & 3);
+            const int s = d < i ? d : i;
+            const int32_t* tl = team_lds[wv] + 8 + g * 1024 + lane * LANE_ACTS + mm;
+            t0 = tl[0];
+            ti = tl[-s];
           }
           m[mm >> 2] |= (uint32_t)(t0 == ti) << (8 * (mm & 3));
         }
-        st_bool16(args.bout, c + (i - 1), ld, j0, m[0], m[1], m[2], m[3]);
+        st_bool16(args.bout, tcol + (i - 1), ld, j0[g], m[0], m[1], m[2], m[3]);
       }
     }
   }
-  __syncthreads();
+}
 
-  // ---------------- phase B: f64 / i64 columns, lane owns 2 consecutive actions ---------------
-  const bool any_num =
-      P.i64_col[SA_XFN_ACTIONTYPE] >= 0 || P.i64_col[SA_XFN_RESULT] >= 0 ||
-      P.i64_col[SA_XFN_BODYPART] >= 0 || P.i64_col[SA_XFN_TIME] >= 0 ||
-      P.f64_col[SA_XFN_TIME] >= 0 || P.f64_col[SA_XFN_STARTLOCATION] >= 0 ||
-      P.f64_col[SA_XFN_ENDLOCATION] >= 0 || P.f64_col[SA_XFN_STARTPOLAR] >= 0 ||
-      P.f64_col[SA_XFN_ENDPOLAR] >= 0 || P.f64_col[SA_XFN_MOVEMENT] >= 0 ||
-      P.f64_col[SA_XFN_TIME_DELTA] >= 0 || P.f64_col[SA_XFN_SPACE_DELTA] >= 0 ||
-      P.f64_col[SA_XFN_LOCATION] >= 0 || P.f64_col[SA_XFN_POLAR] >= 0 ||
-      P.f64_col[SA_XFN_MOVEMENT_POLAR] >= 0 || P.f64_col[SA_XFN_DIRECTION] >= 0;
-  if (!any_num || wave_base >= n) return;
+// ------------------------------------------------------------------------------ f64/i64 block
+template <bool ATOMIC, bool EXPLICIT>
+__global__ __launch_bounds__(256) void num_features_kernel(FeatArgs args) {
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int wv = threadIdx.x / WAVE;
+  const sa_actions& A = args.a;
+  const sa_feature_plan& P = args.p;
+  const int64_t n = A.n;
+  const int K = P.nb_prev_actions;
+  const int64_t ld = args.ld;
+  const int64_t wave_base = ((int64_t)blockIdx.x * BLOCK_WAVES + wv) * WAVE_ACTS;
+  const sa_frame& F0 = A.frames[0];
+  if (wave_base + 2 * lane >= n) return;
+  SegCursor cur = {0, 0, 0};
+  if (!EXPLICIT) cur = seg_at(A, wave_base + 2 * lane);
+  const int c_at = P.i64_col[SA_XFN_ACTIONTYPE], c_re = P.i64_col[SA_XFN_RESULT],
+            c_bi = P.i64_col[SA_XFN_BODYPART], c_ti = P.i64_col[SA_XFN_TIME],
+            c_tf = P.f64_col[SA_XFN_TIME], c_sl = P.f64_col[SA_XFN_STARTLOCATION],
+            c_el = P.f64_col[SA_XFN_ENDLOCATION], c_sp = P.f64_col[SA_XFN_STARTPOLAR],
+            c_ep = P.f64_col[SA_XFN_ENDPOLAR], c_mv = P.f64_col[SA_XFN_MOVEMENT],
+            c_td = P.f64_col[SA_XFN_TIME_DELTA], c_sd = P.f64_col[SA_XFN_SPACE_DELTA],
+            c_lo = P.f64_col[SA_XFN_LOCATION], c_po = P.f64_col[SA_XFN_POLAR],
+            c_mp = P.f64_col[SA_XFN_MOVEMENT_POLAR], c_di = P.f64_col[SA_XFN_DIRECTION];
 
-  for (int pr = 0; pr < LANE_ACTS / 2; ++pr) {
-    const int rel = pr * 2 * WAVE + 2 * lane;  // 0..1022, even
-    const int64_t jb = wave_base + rel;
+  for (int pr = 0; pr < NUM_PAIRS; ++pr) {
+    const int64_t jb = wave_base + pr * 2 * WAVE + 2 * lane;
     if (jb >= n) break;
     int64_t jr[2];
     int dd[2];
     bool away[2];
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
-      int64_t j = jb + e;
-      jr[e] = j < n ? j : n - 1;  // padded tail rows recompute the last row
-      uint32_t inf = info[wv][rel + e];
-      dd[e] = (int)(inf & 0x0F);
-      away[e] = (inf >> 4) & 1;
+      const int64_t j = jb + e < n ? jb + e : n - 1;  // padded tail rows recompute row n-1
+      jr[e] = j;
+      dd[e] = 0;
+      away[e] = false;
+      if (!EXPLICIT) {
+        seg_advance(A, cur, j);
+        const int64_t d = j - cur.s;
+        dd[e] = d > 15 ? 15 : (int)d;
+        away[e] = A.home_team != nullptr && F0.team[j] != A.home_team[cur.g];
+      }
     }
-    // a0 values kept for the state features
     double sx0[2], sy0[2], t0[2];
     for (int i = 0; i < K; ++i) {
       const sa_frame& Fi = EXPLICIT ? A.frames[i] : F0;
@@ -287,7 +386,7 @@ __global__ __launch_bounds__(256) void features_kernel(FeatArgs args) {
       int32_t per[2], typ[2], res[2], bp[2];
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
-        int64_t r = EXPLICIT ? jr[e] : jr[e] - (dd[e] < i ? dd[e] : i);
+        const int64_t r = EXPLICIT ? jr[e] : jr[e] - (dd[e] < i ? dd[e] : i);
         c0[e] = Fi.c0[r];
         c1[e] = Fi.c1[r];
         c2[e] = Fi.c2[r];
@@ -297,7 +396,7 @@ __global__ __launch_bounds__(256) void features_kernel(FeatArgs args) {
         typ[e] = Fi.type_id[r];
         res[e] = ATOMIC ? 0 : Fi.result_id[r];
         bp[e] = Fi.bodypart_id[r];
-        if (!EXPLICIT && away[e]) {  // play_left_to_right, keyed on the current action
+        if (!EXPLICIT && away[e]) {  // play_left_to_right, keyed on the CURRENT action
           c0[e] = FIELD_L - c0[e];
           c1[e] = FIELD_W - c1[e];
           if (ATOMIC) {
@@ -314,49 +413,48 @@ __global__ __launch_bounds__(256) void features_kernel(FeatArgs args) {
           t0[e] = ts[e];
         }
       }
-      int c;
-      if ((c = P.i64_col[SA_XFN_ACTIONTYPE]) >= 0) st_i64x2(args.iout, c + i, ld, jb, typ[0], typ[1]);
-      if ((c = P.i64_col[SA_XFN_RESULT]) >= 0) st_i64x2(args.iout, c + i, ld, jb, res[0], res[1]);
-      if ((c = P.i64_col[SA_XFN_BODYPART]) >= 0) st_i64x2(args.iout, c + i, ld, jb, bp[0], bp[1]);
-      if ((c = P.i64_col[SA_XFN_TIME]) >= 0) st_i64x2(args.iout, c + i, ld, jb, per[0], per[1]);
-      if ((c = P.f64_col[SA_XFN_TIME]) >= 0) {
-        st_f64x2(args.fout, c + 2 * i, ld, jb, ts[0], ts[1]);
+      if (c_at >= 0) st_i64x2(args.iout, c_at + i, ld, jb, typ[0], typ[1]);
+      if (c_re >= 0) st_i64x2(args.iout, c_re + i, ld, jb, res[0], res[1]);
+      if (c_bi >= 0) st_i64x2(args.iout, c_bi + i, ld, jb, bp[0], bp[1]);
+      if (c_ti >= 0) st_i64x2(args.iout, c_ti + i, ld, jb, per[0], per[1]);
+      if (c_tf >= 0) {
+        st_f64x2(args.fout, c_tf + 2 * i, ld, jb, ts[0], ts[1]);
         // ((period_id - 1) * 45 * 60) + time_seconds   (features.py:313)
-        st_f64x2(args.fout, c + 2 * i + 1, ld, jb, (double)((per[0] - 1) * 2700) + ts[0],
+        st_f64x2(args.fout, c_tf + 2 * i + 1, ld, jb, (double)((per[0] - 1) * 2700) + ts[0],
                  (double)((per[1] - 1) * 2700) + ts[1]);
       }
       if (!ATOMIC) {
-        if ((c = P.f64_col[SA_XFN_STARTLOCATION]) >= 0) {
-          st_f64x2(args.fout, c + 2 * i, ld, jb, c0[0], c0[1]);
-          st_f64x2(args.fout, c + 2 * i + 1, ld, jb, c1[0], c1[1]);
+        if (c_sl >= 0) {
+          st_f64x2(args.fout, c_sl + 2 * i, ld, jb, c0[0], c0[1]);
+          st_f64x2(args.fout, c_sl + 2 * i + 1, ld, jb, c1[0], c1[1]);
         }
-        if ((c = P.f64_col[SA_XFN_ENDLOCATION]) >= 0) {
-          st_f64x2(args.fout, c + 2 * i, ld, jb, c2[0], c2[1]);
-          st_f64x2(args.fout, c + 2 * i + 1, ld, jb, c3[0], c3[1]);
+        if (c_el >= 0) {
+          st_f64x2(args.fout, c_el + 2 * i, ld, jb, c2[0], c2[1]);
+          st_f64x2(args.fout, c_el + 2 * i + 1, ld, jb, c3[0], c3[1]);
         }
-        if ((c = P.f64_col[SA_XFN_STARTPOLAR]) >= 0) {
+        if (c_sp >= 0) {
           double dist[2], ang[2];
 #pragma unroll
           for (int e = 0; e < 2; ++e) {
-            double dx = fabs(FIELD_L - c0[e]), dy = fabs(GOAL_Y - c1[e]);
+            const double dx = fabs(FIELD_L - c0[e]), dy = fabs(GOAL_Y - c1[e]);
             dist[e] = sqrt(dx * dx + dy * dy);
             ang[e] = polar_angle(dy, dx);
           }
-          st_f64x2(args.fout, c + 2 * i, ld, jb, dist[0], dist[1]);
-          st_f64x2(args.fout, c + 2 * i + 1, ld, jb, ang[0], ang[1]);
+          st_f64x2(args.fout, c_sp + 2 * i, ld, jb, dist[0], dist[1]);
+          st_f64x2(args.fout, c_sp + 2 * i + 1, ld, jb, ang[0], ang[1]);
         }
-        if ((c = P.f64_col[SA_XFN_ENDPOLAR]) >= 0) {
+        if (c_ep >= 0) {
           double dist[2], ang[2];
 #pragma unroll
           for (int e = 0; e < 2; ++e) {
-            double dx = fabs(FIELD_L - c2[e]), dy = fabs(GOAL_Y - c3[e]);
+            const double dx = fabs(FIELD_L - c2[e]), dy = fabs(GOAL_Y - c3[e]);
             dist[e] = sqrt(dx * dx + dy * dy);
             ang[e] = polar_angle(dy, dx);
           }
-          st_f64x2(args.fout, c + 2 * i, ld, jb, dist[0], dist[1]);
-          st_f64x2(args.fout, c + 2 * i + 1, ld, jb, ang[0], ang[1]);
+          st_f64x2(args.fout, c_ep + 2 * i, ld, jb, dist[0], dist[1]);
+          st_f64x2(args.fout, c_ep + 2 * i + 1, ld, jb, ang[0], ang[1]);
         }
-        if ((c = P.f64_col[SA_XFN_MOVEMENT]) >= 0) {
+        if (c_mv >= 0) {
           double mdx[2], mdy[2], mv[2];
 #pragma unroll
           for (int e = 0; e < 2; ++e) {
@@ -364,11 +462,11 @@ __global__ __launch_bounds__(256) void features_kernel(FeatArgs args) {
             mdy[e] = c3[e] - c1[e];
             mv[e] = sqrt(mdx[e] * mdx[e] + mdy[e] * mdy[e]);
           }
-          st_f64x2(args.fout, c + 3 * i, ld, jb, mdx[0], mdx[1]);
-          st_f64x2(args.fout, c + 3 * i + 1, ld, jb, mdy[0], mdy[1]);
-          st_f64x2(args.fout, c + 3 * i + 2, ld, jb, mv[0], mv[1]);
+          st_f64x2(args.fout, c_mv + 3 * i, ld, jb, mdx[0], mdx[1]);
+          st_f64x2(args.fout, c_mv + 3 * i + 1, ld, jb, mdy[0], mdy[1]);
+          st_f64x2(args.fout, c_mv + 3 * i + 2, ld, jb, mv[0], mv[1]);
         }
-        if (i >= 1 && (c = P.f64_col[SA_XFN_SPACE_DELTA]) >= 0) {
+        if (i >= 1 && c_sd >= 0) {  // space_delta: a_i end - a0 start (features.py:491-499)
           double sdx[2], sdy[2], sm[2];
 #pragma unroll
           for (int e = 0; e < 2; ++e) {
@@ -376,57 +474,58 @@ __global__ __launch_bounds__(256) void features_kernel(FeatArgs args) {
             sdy[e] = c3[e] - sy0[e];
             sm[e] = sqrt(sdx[e] * sdx[e] + sdy[e] * sdy[e]);
           }
-          st_f64x2(args.fout, c + 3 * (i - 1), ld, jb, sdx[0], sdx[1]);
-          st_f64x2(args.fout, c + 3 * (i - 1) + 1, ld, jb, sdy[0], sdy[1]);
-          st_f64x2(args.fout, c + 3 * (i - 1) + 2, ld, jb, sm[0], sm[1]);
+          st_f64x2(args.fout, c_sd + 3 * (i - 1), ld, jb, sdx[0], sdx[1]);
+          st_f64x2(args.fout, c_sd + 3 * (i - 1) + 1, ld, jb, sdy[0], sdy[1]);
+          st_f64x2(args.fout, c_sd + 3 * (i - 1) + 2, ld, jb, sm[0], sm[1]);
         }
       } else {
-        if ((c = P.f64_col[SA_XFN_LOCATION]) >= 0) {
-          st_f64x2(args.fout, c + 2 * i, ld, jb, c0[0], c0[1]);
-          st_f64x2(args.fout, c + 2 * i + 1, ld, jb, c1[0], c1[1]);
+        if (c_lo >= 0) {
+          st_f64x2(args.fout, c_lo + 2 * i, ld, jb, c0[0], c0[1]);
+          st_f64x2(args.fout, c_lo + 2 * i + 1, ld, jb, c1[0], c1[1]);
         }
-        if ((c = P.f64_col[SA_XFN_POLAR]) >= 0) {
+        if (c_po >= 0) {
           double dist[2], ang[2];
 #pragma unroll
           for (int e = 0; e < 2; ++e) {
-            double dx = fabs(FIELD_L - c0[e]), dy = fabs(GOAL_Y - c1[e]);
+            const double dx = fabs(FIELD_L - c0[e]), dy = fabs(GOAL_Y - c1[e]);
             dist[e] = sqrt(dx * dx + dy * dy);
             ang[e] = polar_angle(dy, dx);
           }
-          st_f64x2(args.fout, c + 2 * i, ld, jb, dist[0], dist[1]);
-          st_f64x2(args.fout, c + 2 * i + 1, ld, jb, ang[0], ang[1]);
+          st_f64x2(args.fout, c_po + 2 * i, ld, jb, dist[0], dist[1]);
+          st_f64x2(args.fout, c_po + 2 * i + 1, ld, jb, ang[0], ang[1]);
         }
-        if ((c = P.f64_col[SA_XFN_MOVEMENT_POLAR]) >= 0) {
+        if (c_mp >= 0) {  // atomic/vaep/features.py:279-284
           double md[2], ma[2];
 #pragma unroll
           for (int e = 0; e < 2; ++e) {
             md[e] = sqrt(c2[e] * c2[e] + c3[e] * c3[e]);
-            ma[e] = (c3[e] == 0.0) ? 0.0 : atan2(c3[e], c2[e]);  // atomic/vaep/features.py:181-200
+            ma[e] = (c3[e] == 0.0) ? 0.0 : atan2(c3[e], c2[e]);
           }
-          st_f64x2(args.fout, c + 2 * i, ld, jb, md[0], md[1]);
-          st_f64x2(args.fout, c + 2 * i + 1, ld, jb, ma[0], ma[1]);
+          st_f64x2(args.fout, c_mp + 2 * i, ld, jb, md[0], md[1]);
+          st_f64x2(args.fout, c_mp + 2 * i + 1, ld, jb, ma[0], ma[1]);
         }
-        if ((c = P.f64_col[SA_XFN_DIRECTION]) >= 0) {
+        if (c_di >= 0) {  // atomic/vaep/features.py:302-310
           double ox[2], oy[2];
 #pragma unroll
           for (int e = 0; e < 2; ++e) {
-            double td = sqrt(c2[e] * c2[e] + c3[e] * c3[e]);
-            ox[e] = td > 0.0 ? c2[e] / td : c2[e];  // atomic/vaep/features.py:203-226
+            const double td = sqrt(c2[e] * c2[e] + c3[e] * c3[e]);
+            ox[e] = td > 0.0 ? c2[e] / td : c2[e];
             oy[e] = td > 0.0 ? c3[e] / td : c3[e];
           }
-          st_f64x2(args.fout, c + 2 * i, ld, jb, ox[0], ox[1]);
-          st_f64x2(args.fout, c + 2 * i + 1, ld, jb, oy[0], oy[1]);
+          st_f64x2(args.fout, c_di + 2 * i, ld, jb, ox[0], ox[1]);
+          st_f64x2(args.fout, c_di + 2 * i + 1, ld, jb, oy[0], oy[1]);
         }
       }
-      if (i >= 1 && (c = P.f64_col[SA_XFN_TIME_DELTA]) >= 0)
-        st_f64x2(args.fout, c + (i - 1), ld, jb, t0[0] - ts[0], t0[1] - ts[1]);
+      if (i >= 1 && c_td >= 0)  // time_delta: a0 time - a_i time (features.py:469-473)
+        st_f64x2(args.fout, c_td + (i - 1), ld, jb, t0[0] - ts[0], t0[1] - ts[1]);
     }
   }
 }
 
-// ------------------------------------------------------------------------------------------
-// goalscore (features.py:505-539 / atomic/vaep/features.py:313-344): per segment, teamA =
-// team of the segment's first row, exclusive cumsum of goals for A and B.
+// ------------------------------------------------------------------------------ goalscore
+// features.py:505-539 / atomic/vaep/features.py:313-344: per segment, teamA = team of the
+// segment's first row, exclusive cumsum of goals for A and for B.  One workgroup per
+// segment; each iteration covers 1024 rows (4 per thread, word-aligned loads).
 constexpr int GS_THREADS = 256;
 
 template <bool ATOMIC>
@@ -436,44 +535,34 @@ __global__ __launch_bounds__(GS_THREADS) void goalscore_kernel(sa_actions A, int
   const int64_t g = blockIdx.x;
   const int64_t s = A.seg_off[g], e = A.seg_off[g + 1];
   if (s >= e) return;
+  const int64_t n = A.n;
   const sa_frame& F = A.frames[0];
   const int32_t teamA = F.team[s];
   const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
-  uint64_t carry = 0;  // low 32: goals team A so far, high 32: goals team B so far
-  for (int64_t base = s; base < e; base += 2 * GS_THREADS) {
-    int64_t jj[2];
-    uint64_t inc[2];
-    bool isA[2];
+  uint64_t carry = 0;  // low 32 bits: goals of team A so far; high 32 bits: team B
+  for (int64_t base = s & ~(int64_t)3; base < e; base += 4 * GS_THREADS) {
+    const int64_t j0 = base + 4 * threadIdx.x;
+    const uint32_t tw = ld_u8x4(F.type_id, j0 / 4, n);
+    const uint32_t rw = ATOMIC ? 0u : ld_u8x4(F.result_id, j0 / 4, n);
+    uint32_t gb, ob;
+    goal_bytes(tw, rw, ATOMIC, gb, ob);
+    uint64_t inc[4];
+    bool isA[4], valid[4];
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      int64_t j = base + 2 * threadIdx.x + q;
-      jj[q] = j;
-      inc[q] = 0;
-      isA[q] = false;
-      if (j < e) {
-        int t = F.type_id[j];
-        bool goal, og;
-        if (ATOMIC) {
-          goal = t == AT_GOAL;
-          og = t == AT_OWNGOAL;
-        } else {
-          bool shot = t == T_SHOT || t == T_SHOT_PENALTY || t == T_SHOT_FREEKICK;
-          int r = F.result_id[j];
-          goal = shot && r == R_SUCCESS;
-          og = shot && r == R_OWNGOAL;
-        }
-        isA[q] = F.team[j] == teamA;
-        bool gA = (goal && isA[q]) || (og && !isA[q]);
-        bool gB = (goal && !isA[q]) || (og && isA[q]);
-        inc[q] = (uint64_t)gA | ((uint64_t)gB << 32);
-      }
+    for (int q = 0; q < 4; ++q) {
+      const int64_t j = j0 + q;
+      valid[q] = j >= s && j < e;
+      isA[q] = valid[q] && F.team[j] == teamA;
+      const bool goal = valid[q] && byte_of(gb, q), og = valid[q] && byte_of(ob, q);
+      const bool gA = (goal && isA[q]) || (og && !isA[q]);
+      const bool gB = (goal && !isA[q]) || (og && isA[q]);
+      inc[q] = (uint64_t)gA | ((uint64_t)gB << 32);
     }
-    // block exclusive scan of (inc0 + inc1)
-    uint64_t x = inc[0] + inc[1];
+    const uint64_t x = inc[0] + inc[1] + inc[2] + inc[3];
     uint64_t incl = x;
 #pragma unroll
     for (int off = 1; off < WAVE; off <<= 1) {
-      uint64_t y = __shfl_up(incl, off, WAVE);
+      const uint64_t y = __shfl_up(incl, off, WAVE);
       if (lane >= off) incl += y;
     }
     if (lane == WAVE - 1) wsum[wv] = incl;
@@ -481,20 +570,21 @@ __global__ __launch_bounds__(GS_THREADS) void goalscore_kernel(sa_actions A, int
     uint64_t wpre = 0, total = 0;
 #pragma unroll
     for (int k = 0; k < GS_THREADS / WAVE; ++k) {
-      uint64_t v = wsum[k];
-      if (k < wv) wpre += v;
+      const uint64_t v = wsum[k];
+      wpre += k < wv ? v : 0;
       total += v;
     }
     __syncthreads();
     uint64_t excl = carry + wpre + incl - x;
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      if (jj[q] < e) {
-        int64_t cA = (int64_t)(excl & 0xFFFFFFFFull), cB = (int64_t)(excl >> 32);
-        int64_t tm = isA[q] ? cA : cB, op = isA[q] ? cB : cA;
-        out[jj[q]] = tm;
-        out[ld + jj[q]] = op;
-        out[2 * ld + jj[q]] = tm - op;
+    for (int q = 0; q < 4; ++q) {
+      if (valid[q]) {
+        const int64_t j = j0 + q;
+        const int64_t cA = (int64_t)(excl & 0xFFFFFFFFull), cB = (int64_t)(excl >> 32);
+        const int64_t tm = isA[q] ? cA : cB, op = isA[q] ? cB : cA;
+        out[j] = tm;
+        out[ld + j] = op;
+        out[2 * ld + j] = tm - op;
       }
       excl += inc[q];
     }
@@ -502,10 +592,12 @@ __global__ __launch_bounds__(GS_THREADS) void goalscore_kernel(sa_actions A, int
   }
 }
 
-// ------------------------------------------------------------------------------------------
-// labels (vaep/labels.py:9-116, atomic/vaep/labels.py:9-107).  Lane owns 16 consecutive
-// actions; rows j0 .. j0+31 are held as goal/owngoal bit masks + team codes, so the
-// look-ahead of nr_actions <= 17 needs no further loads.
+// ------------------------------------------------------------------------------ labels
+// vaep/labels.py:9-116, atomic/vaep/labels.py:9-107.  A lane owns 16 consecutive actions
+// and holds rows j0 .. j0+31 as goal / owngoal bit masks plus team codes, so a look-ahead of
+// nr_actions <= 17 needs no further loads.  The look-ahead clamps at the segment's last row,
+// which only repeats a row already in the window, so the window is rows j+1 .. min(j+nr-1,
+// last).
 template <bool ATOMIC>
 __global__ __launch_bounds__(256) void labels_kernel(sa_actions A, int nr, uint8_t* __restrict__ sc,
                                                      uint8_t* __restrict__ co,
@@ -514,157 +606,183 @@ __global__ __launch_bounds__(256) void labels_kernel(sa_actions A, int nr, uint8
   const int64_t j0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * LANE_ACTS;
   if (j0 >= n) return;
   const sa_frame& F = A.frames[0];
-  int64_t g = find_segment(A.seg_off, A.n_segments, j0);
-  int64_t e = A.seg_off[g + 1];
-  uint32_t gm = 0, om = 0, sm = 0;  // goal / owngoal / shot(type 11, atomic gfs) bits
-  int32_t tm[32];
-  uint32_t t27 = 0;                 // atomic: type == goal bits
+  uint32_t gm = 0, om = 0, shm = 0;  // goal / owngoal / shot(type 11) row bits
 #pragma unroll
-  for (int r = 0; r < 32; ++r) {
-    int64_t j = j0 + r;
-    int t = 0, res = 0;
-    int32_t te = 0;
-    if (j < n) {
-      t = F.type_id[j];
-      res = ATOMIC ? 0 : F.result_id[j];
-      te = F.team[j];
-    }
-    bool goal, og;
-    if (ATOMIC) {
-      goal = t == AT_GOAL;
-      og = t == AT_OWNGOAL;
-    } else {
-      bool shot = t == T_SHOT || t == T_SHOT_PENALTY || t == T_SHOT_FREEKICK;
-      goal = shot && res == R_SUCCESS;
-      og = shot && res == R_OWNGOAL;
-    }
-    gm |= (uint32_t)goal << r;
-    om |= (uint32_t)og << r;
-    sm |= (uint32_t)(t == T_SHOT) << r;
-    t27 |= (uint32_t)(t == AT_GOAL) << r;
-    tm[r] = te;
+  for (int q = 0; q < 8; ++q) {
+    const uint32_t tw = ld_u8x4(F.type_id, j0 / 4 + q, n);
+    const uint32_t rw = ATOMIC ? 0u : ld_u8x4(F.result_id, j0 / 4 + q, n);
+    uint32_t g, o;
+    goal_bytes(tw, rw, ATOMIC, g, o);
+    gm |= pack4(g) << (4 * q);
+    om |= pack4(o) << (4 * q);
+    if (ATOMIC) shm |= pack4(bytes_eq(tw, T_SHOT)) << (4 * q);
   }
+  int32_t tm[32];
+  if (j0 + 32 <= n) {
+    const int4* tp = reinterpret_cast<const int4*>(F.team + j0);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int4 v = tp[q];
+      tm[4 * q] = v.x;
+      tm[4 * q + 1] = v.y;
+      tm[4 * q + 2] = v.z;
+      tm[4 * q + 3] = v.w;
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < 32; ++r) tm[r] = ld_or0(F.team, j0 + r, n);
+  }
+  SegCursor cur = seg_at(A, j0);
   uint32_t s_out[4] = {0, 0, 0, 0}, c_out[4] = {0, 0, 0, 0}, g_out[4] = {0, 0, 0, 0};
 #pragma unroll
   for (int m = 0; m < LANE_ACTS; ++m) {
-    int64_t j = j0 + m;
-    if (j >= n) break;
-    while (j >= e) {
-      ++g;
-      e = A.seg_off[g + 1];
-    }
-    const int64_t last = e - 1;  // segment's last row: look-ahead clamps here
-    bool scores, concedes;
-    const bool goal_j = (gm >> m) & 1, og_j = (om >> m) & 1;
-    if (nr <= 17) {
-      int64_t hi = j + nr - 1 < last ? j + nr - 1 : last;  // rows j+1 .. hi
-      int span = (int)(hi - j);                            // 0 .. 16
-      uint32_t win = span > 0 ? (((1u << span) - 1u) << (m + 1)) : 0u;
-      uint32_t same = 0;
+    const int64_t j = j0 + m;
+    if (j < n) {
+      seg_advance(A, cur, j);
+      const int64_t last = cur.e - 1;
+      bool scores, concedes;
+      const bool goal_j = (gm >> m) & 1, og_j = (om >> m) & 1;
+      if (nr <= 17) {
+        const int64_t hi = j + nr - 1 < last ? j + nr - 1 : last;
+        const int span = (int)(hi - j);  // 0 .. 16
+        const uint32_t win = span > 0 ? (((1u << span) - 1u) << (m + 1)) : 0u;
+        uint32_t same = 0;
 #pragma unroll
-      for (int r = 0; r < 32; ++r) same |= (uint32_t)(tm[r] == tm[m]) << r;
-      scores = goal_j || (((gm & same) | (om & ~same)) & win) != 0;
-      concedes = og_j || (((gm & ~same) | (om & same)) & win) != 0;
-    } else {
-      scores = goal_j;
-      concedes = og_j;
-      const int32_t tj = tm[m];
-      for (int i = 1; i < nr; ++i) {
-        int64_t c = j + i < last ? j + i : last;
-        int t = F.type_id[c];
-        bool goal, og;
-        if (ATOMIC) {
-          goal = t == AT_GOAL;
-          og = t == AT_OWNGOAL;
-        } else {
-          bool shot = t == T_SHOT || t == T_SHOT_PENALTY || t == T_SHOT_FREEKICK;
-          int res = F.result_id[c];
-          goal = shot && res == R_SUCCESS;
-          og = shot && res == R_OWNGOAL;
+        for (int r = 0; r < 32; ++r) same |= (uint32_t)(tm[r] == tm[m]) << r;
+        scores = goal_j || (((gm & same) | (om & ~same)) & win) != 0;
+        concedes = og_j || (((gm & ~same) | (om & same)) & win) != 0;
+      } else {
+        scores = goal_j;
+        concedes = og_j;
+        const int32_t tj = tm[m];
+        for (int i = 1; i < nr; ++i) {
+          const int64_t c = j + i < last ? j + i : last;
+          const int t = F.type_id[c];
+          bool goal, og;
+          if (ATOMIC) {
+            goal = t == AT_GOAL;
+            og = t == AT_OWNGOAL;
+          } else {
+            const bool shot = t == T_SHOT || t == T_SHOT_PENALTY || t == T_SHOT_FREEKICK;
+            const int res = F.result_id[c];
+            goal = shot && res == R_SUCCESS;
+            og = shot && res == R_OWNGOAL;
+          }
+          const bool same = F.team[c] == tj;
+          scores |= (goal && same) || (og && !same);
+          concedes |= (goal && !same) || (og && same);
         }
-        bool same = F.team[c] == tj;
-        scores |= (goal && same) || (og && !same);
-        concedes |= (goal && !same) || (og && same);
       }
+      bool gf;
+      if (ATOMIC)  // shot followed by goal; the segment's last row compares NaN -> False
+        gf = ((shm >> m) & 1) && j < last && ((gm >> (m + 1)) & 1);
+      else
+        gf = goal_j;
+      s_out[m >> 2] |= (uint32_t)scores << (8 * (m & 3));
+      c_out[m >> 2] |= (uint32_t)concedes << (8 * (m & 3));
+      g_out[m >> 2] |= (uint32_t)gf << (8 * (m & 3));
     }
-    bool gf;
-    if (ATOMIC)  // shot followed by goal; the segment's last row compares with NaN -> False
-      gf = ((sm >> m) & 1) && j < last && ((t27 >> (m + 1)) & 1);
-    else
-      gf = goal_j;
-    s_out[m >> 2] |= (uint32_t)scores << (8 * (m & 3));
-    c_out[m >> 2] |= (uint32_t)concedes << (8 * (m & 3));
-    g_out[m >> 2] |= (uint32_t)gf << (8 * (m & 3));
   }
-  if (sc) *reinterpret_cast<uint4*>(sc + j0) = make_uint4(s_out[0], s_out[1], s_out[2], s_out[3]);
-  if (co) *reinterpret_cast<uint4*>(co + j0) = make_uint4(c_out[0], c_out[1], c_out[2], c_out[3]);
-  if (gfs) *reinterpret_cast<uint4*>(gfs + j0) = make_uint4(g_out[0], g_out[1], g_out[2], g_out[3]);
+  if (sc) st16(sc + j0, u32x4{s_out[0], s_out[1], s_out[2], s_out[3]});
+  if (co) st16(co + j0, u32x4{c_out[0], c_out[1], c_out[2], c_out[3]});
+  if (gfs) st16(gfs + j0, u32x4{g_out[0], g_out[1], g_out[2], g_out[3]});
 }
 
-// ------------------------------------------------------------------------------------------
-// formula (vaep/formula.py:8-151, atomic/vaep/formula.py:8-141).  Arithmetic stays in the
-// probability dtype and mirrors the reference's pandas expression tree operation by operation.
+// ------------------------------------------------------------------------------ formula
+// vaep/formula.py:8-151, atomic/vaep/formula.py:8-141.  Arithmetic stays in the probability
+// dtype and mirrors the pandas expression tree operation by operation.  A lane owns V
+// consecutive actions (16-B stores); the previous row's values come from the same lane or,
+// for the lane's first action, from the neighbouring lane by a wave shuffle.
 template <bool ATOMIC, typename T>
 __global__ __launch_bounds__(256) void formula_kernel(sa_actions A, const T* __restrict__ ps,
                                                       const T* __restrict__ pc, T* __restrict__ off,
                                                       T* __restrict__ def, T* __restrict__ val) {
   constexpr int V = 16 / sizeof(T);
   const int64_t n = A.n;
+  const int lane = threadIdx.x & (WAVE - 1);
   const int64_t j0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * V;
-  if (j0 >= n) return;
+  const bool active = j0 < n;
   const sa_frame& F = A.frames[0];
-  int64_t g = find_segment(A.seg_off, A.n_segments, j0);
-  int64_t s = A.seg_off[g], e = A.seg_off[g + 1];
-  T vo[V], vd[V], vv[V];
+  T s_[V], c_[V];
+  double t_[V];
+  int32_t tm_[V], ty_[V], rs_[V];
+#pragma unroll
+  for (int q = 0; q < V; ++q) {  // own rows j0 .. j0+V-1 (clamped to n-1 in the tail)
+    const int64_t j = active ? (j0 + q < n ? j0 + q : n - 1) : 0;
+    s_[q] = ps[j];
+    c_[q] = pc[j];
+    t_[q] = F.time_seconds[j];
+    tm_[q] = F.team[j];
+    ty_[q] = F.type_id[j];
+    rs_[q] = ATOMIC ? 0 : F.result_id[j];
+  }
+  // row j0-1 comes from the previous lane (lane 0 loads it itself)
+  T sp = __shfl_up(s_[V - 1], 1, WAVE), cp = __shfl_up(c_[V - 1], 1, WAVE);
+  double tp = __shfl_up(t_[V - 1], 1, WAVE);
+  int32_t tmp = __shfl_up(tm_[V - 1], 1, WAVE), typ = __shfl_up(ty_[V - 1], 1, WAVE),
+          rsp = __shfl_up(rs_[V - 1], 1, WAVE);
+  if (!active) return;
+  if (lane == 0 && j0 > 0) {
+    const int64_t p = j0 - 1;
+    sp = ps[p];
+    cp = pc[p];
+    tp = F.time_seconds[p];
+    tmp = F.team[p];
+    typ = F.type_id[p];
+    rsp = ATOMIC ? 0 : F.result_id[p];
+  }
+  SegCursor cur = seg_at(A, j0);
+  typedef T vec_t __attribute__((ext_vector_type(V)));
+  vec_t vo, vd, vv;
 #pragma unroll
   for (int q = 0; q < V; ++q) {
-    int64_t j = j0 + q;
-    if (j >= n) j = n - 1;
-    while (j >= e) {
-      ++g;
-      s = e;
-      e = A.seg_off[g + 1];
+    const int64_t j = j0 + q < n ? j0 + q : n - 1;
+    seg_advance(A, cur, j);
+    const bool first = j == cur.s;  // _prev of a segment's first row is the row itself
+    T Sp = q ? s_[q - 1] : sp, Cp = q ? c_[q - 1] : cp;
+    double Tp = q ? t_[q - 1] : tp;
+    int32_t TMp = q ? tm_[q - 1] : tmp, TYp = q ? ty_[q - 1] : typ, RSp = q ? rs_[q - 1] : rsp;
+    if (first) {
+      Sp = s_[q];
+      Cp = c_[q];
+      Tp = t_[q];
+      TMp = tm_[q];
+      TYp = ty_[q];
+      RSp = rs_[q];
     }
-    const int64_t p = j > s ? j - 1 : j;  // _prev: shift(1) with row 0 = itself
     const T one = T(1), zero = T(0);
-    const bool same = F.team[p] == F.team[j];
+    const bool same = TMp == tm_[q];
     const T fs = same ? one : zero, fn = same ? zero : one;
-    T prev_s = ps[p] * fs + pc[p] * fn;
-    T prev_c = pc[p] * fs + ps[p] * fn;
-    const int tp = F.type_id[p], tj = F.type_id[j];
+    T prev_s = Sp * fs + Cp * fn;  // _prev(scores) * sameteam + _prev(concedes) * ~sameteam
+    T prev_c = Cp * fs + Sp * fn;
     bool prevgoal;
     if (ATOMIC) {
-      prevgoal = tp == AT_GOAL || tp == AT_OWNGOAL;
+      prevgoal = TYp == AT_GOAL || TYp == AT_OWNGOAL;
     } else {
-      const bool toolong = fabs(F.time_seconds[j] - F.time_seconds[p]) > 10.0;  // _samephase_nb
-      if (toolong) {
+      if (fabs(t_[q] - Tp) > 10.0) {  // _samephase_nb
         prev_s = zero;
         prev_c = zero;
       }
-      prevgoal = (tp == T_SHOT || tp == T_SHOT_PENALTY || tp == T_SHOT_FREEKICK) &&
-                 F.result_id[p] == R_SUCCESS;
+      prevgoal = (TYp == T_SHOT || TYp == T_SHOT_PENALTY || TYp == T_SHOT_FREEKICK) &&
+                 RSp == R_SUCCESS;
     }
     if (prevgoal) {
       prev_s = zero;
       prev_c = zero;
     }
     if (!ATOMIC) {
-      if (tj == T_SHOT_PENALTY) prev_s = T(0.792453);
-      if (tj == T_CORNER_CROSSED || tj == T_CORNER_SHORT) prev_s = T(0.046500);
+      if (ty_[q] == T_SHOT_PENALTY) prev_s = T(0.792453);
+      if (ty_[q] == T_CORNER_CROSSED || ty_[q] == T_CORNER_SHORT) prev_s = T(0.046500);
     }
-    vo[q] = ps[j] - prev_s;
-    vd[q] = -(pc[j] - prev_c);
-    vv[q] = vo[q] + vd[q];
+    const T o = s_[q] - prev_s;
+    const T d = -(c_[q] - prev_c);
+    vo[q] = o;
+    vd[q] = d;
+    vv[q] = o + d;
   }
-  if (sizeof(T) == 8) {
-    *reinterpret_cast<double2*>(off + j0) = *reinterpret_cast<double2*>(vo);
-    *reinterpret_cast<double2*>(def + j0) = *reinterpret_cast<double2*>(vd);
-    *reinterpret_cast<double2*>(val + j0) = *reinterpret_cast<double2*>(vv);
-  } else {
-    *reinterpret_cast<float4*>(off + j0) = *reinterpret_cast<float4*>(vo);
-    *reinterpret_cast<float4*>(def + j0) = *reinterpret_cast<float4*>(vd);
-    *reinterpret_cast<float4*>(val + j0) = *reinterpret_cast<float4*>(vv);
-  }
+  st16(off + j0, vo);
+  st16(def + j0, vd);
+  st16(val + j0, vv);
 }
 
 }  // namespace sa
@@ -687,8 +805,9 @@ static int check_actions(const sa_actions* a, bool allow_explicit) {
     if (!F.type_id || !F.team || !F.bodypart_id || !F.period_id || !F.time_seconds || !F.c0 ||
         !F.c1 || !F.c2 || !F.c3 || (!a->atomic && !F.result_id))
       return fail(SA_EINVAL, "frame %d has a null column", f);
-    if (!aligned16(F.type_id) || !aligned16(F.result_id) || !aligned16(F.bodypart_id))
-      return fail(SA_EINVAL, "frame %d: id columns must be 16-byte aligned", f);
+    if (!aligned16(F.type_id) || !aligned16(F.result_id) || !aligned16(F.bodypart_id) ||
+        !aligned16(F.team))
+      return fail(SA_EINVAL, "frame %d: id and team columns must be 16-byte aligned", f);
   }
   return SA_OK;
 }
@@ -704,14 +823,18 @@ extern "C" int sa_vaep_features(const sa_actions* a, const sa_feature_plan* plan
     return fail(SA_EINVAL, "explicit mode needs n_frames == nb_prev_actions");
   if (ld % 16 != 0 || ld < ((a->n + 15) / 16) * 16)
     return fail(SA_EINVAL, "ld must be a multiple of 16 and >= round_up(n, 16)");
-  bool wb = false, wf = false, wi = false;
+  if (!aligned16(bool_out) || !aligned16(f64_out) || !aligned16(i64_out))
+    return fail(SA_EINVAL, "output blocks must be 16-byte aligned");
+  bool wb = false, wn = false;
   for (int x = 0; x < SA_XFN_COUNT; ++x) {
     wb |= plan->bool_col[x] >= 0;
-    wf |= plan->f64_col[x] >= 0;
-    wi |= plan->i64_col[x] >= 0;
+    wn |= plan->f64_col[x] >= 0 || (plan->i64_col[x] >= 0 && x != SA_XFN_GOALSCORE);
   }
-  if ((wb && !bool_out) || (wf && !f64_out) || (wi && !i64_out))
-    return fail(SA_EINVAL, "plan writes a block whose pointer is null");
+  for (int x = 0; x < SA_XFN_COUNT; ++x) {
+    if ((plan->bool_col[x] >= 0 && !bool_out) || (plan->f64_col[x] >= 0 && !f64_out) ||
+        (plan->i64_col[x] >= 0 && !i64_out))
+      return fail(SA_EINVAL, "plan writes a block whose pointer is null");
+  }
   if (a->atomic) {
     const int spadl_only[] = {SA_XFN_RESULT, SA_XFN_RESULT_ONEHOT, SA_XFN_ACTIONTYPE_RESULT_ONEHOT,
                               SA_XFN_STARTLOCATION, SA_XFN_ENDLOCATION, SA_XFN_STARTPOLAR,
@@ -728,22 +851,39 @@ extern "C" int sa_vaep_features(const sa_actions* a, const sa_feature_plan* plan
   if (a->n == 0) return SA_OK;
   hipStream_t st = (hipStream_t)stream;
   FeatArgs args{*a, *plan, bool_out, f64_out, i64_out, ld};
-  const int64_t waves = (a->n + WAVE_ACTS - 1) / WAVE_ACTS;
-  const dim3 grid((unsigned)((waves + BLOCK_WAVES - 1) / BLOCK_WAVES)), block(BLOCK_WAVES * WAVE);
+  const dim3 grid((unsigned)((a->n + BLOCK_ACTS - 1) / BLOCK_ACTS)), block(BLOCK_WAVES * WAVE);
+  const dim3 bgrid((unsigned)((a->n + BOOL_BLOCK_ACTS - 1) / BOOL_BLOCK_ACTS));
   const bool expl = a->n_frames > 1;
-  if (a->atomic) {
-    if (expl)
-      hipLaunchKernelGGL((features_kernel<true, true>), grid, block, 0, st, args);
-    else
-      hipLaunchKernelGGL((features_kernel<true, false>), grid, block, 0, st, args);
-  } else {
-    if (expl)
-      hipLaunchKernelGGL((features_kernel<false, true>), grid, block, 0, st, args);
-    else
-      hipLaunchKernelGGL((features_kernel<false, false>), grid, block, 0, st, args);
+  if (wb) {
+    if (a->atomic) {
+      if (expl)
+        hipLaunchKernelGGL((bool_features_kernel<true, true>), bgrid, block, 0, st, args);
+      else
+        hipLaunchKernelGGL((bool_features_kernel<true, false>), bgrid, block, 0, st, args);
+    } else {
+      if (expl)
+        hipLaunchKernelGGL((bool_features_kernel<false, true>), bgrid, block, 0, st, args);
+      else
+        hipLaunchKernelGGL((bool_features_kernel<false, false>), bgrid, block, 0, st, args);
+    }
+    rc = check_launch("bool_features_kernel");
+    if (rc) return rc;
   }
-  rc = check_launch("features_kernel");
-  if (rc) return rc;
+  if (wn) {
+    if (a->atomic) {
+      if (expl)
+        hipLaunchKernelGGL((num_features_kernel<true, true>), grid, block, 0, st, args);
+      else
+        hipLaunchKernelGGL((num_features_kernel<true, false>), grid, block, 0, st, args);
+    } else {
+      if (expl)
+        hipLaunchKernelGGL((num_features_kernel<false, true>), grid, block, 0, st, args);
+      else
+        hipLaunchKernelGGL((num_features_kernel<false, false>), grid, block, 0, st, args);
+    }
+    rc = check_launch("num_features_kernel");
+    if (rc) return rc;
+  }
   const int gc = plan->i64_col[SA_XFN_GOALSCORE];
   if (gc >= 0) rc = sa_vaep_goalscore(a, i64_out + (int64_t)gc * ld, ld, stream);
   return rc;
