@@ -85,6 +85,8 @@ def main() -> None:
     ap.add_argument('--games', type=int, default=10000, help='games per GPU (cfg2: 10k)')
     ap.add_argument('--cpu-seconds', type=float, default=15.0)
     ap.add_argument('--no-cpu', action='store_true')
+    ap.add_argument('--tile-rows', type=int, default=1024,
+                    help='rows per output tile (0 = one tile: plain column-major blocks)')
     args = ap.parse_args()
 
     dist, rank, world = _dist()
@@ -93,7 +95,8 @@ def main() -> None:
     ab = B.ActionBatch.from_columns(d, dev=dev)
     n = ab.n
     plan = catalog.build_plan(SPADL_DEFAULT, 3)
-    out = ops.alloc_feature_blocks(plan, n, dev)
+    out = ops.alloc_feature_blocks(plan, n, dev, tile_rows=args.tile_rows or None)
+    ld = (n + 15) // 16 * 16
 
     def sub(keep):  # the same block layout with only some column families launched
         q = copy.copy(plan)
@@ -105,15 +108,15 @@ def main() -> None:
                 q.struct.f64_col[x] = -1
             if 'i' not in keep or x == XFN['goalscore']:
                 q.struct.i64_col[x] = -1
-        return ops.FeatureBlocks(q, n, out.ld, out.bool_block, out.f64_block, out.i64_block)
+        return ops.FeatureBlocks(q, n, out.R, out.bool_block, out.f64_block, out.i64_block)
 
     bool_out, num_out = sub('b'), sub('fi')
     p = synthetic.probabilities(n)
     ps = torch.from_numpy(p['scores']).to(dev)
     pc = torch.from_numpy(p['concedes']).to(dev)
-    lab_buf = torch.empty((3, out.ld), dtype=torch.uint8, device=dev)
+    lab_buf = torch.empty((3, ld), dtype=torch.uint8, device=dev)
     lab = ops.LabelBlocks(n, lab_buf[0], lab_buf[1], None)
-    val = torch.empty((3, out.ld), dtype=torch.float64, device=dev)
+    val = torch.empty((3, ld), dtype=torch.float64, device=dev)
     s_act = ab.struct()
     calls = (lambda: ops.features_into(s_act, bool_out),
              lambda: ops.features_into(s_act, num_out),
@@ -181,6 +184,7 @@ def main() -> None:
         'config': {'workload': 'cfg2: 10k-game synthetic SPADL per GPU, VAEP compute_features '
                                '(k=3, default xfns, 568 cols) + compute_labels + formula.value (f64)',
                    'games_per_gpu': args.games, 'actions_per_gpu': n,
+                   'feature_layout': f'tiled column-major, {out.R} rows per tile',
                    'parallelism': f'games sharded over {world} GPU(s)'},
         'kernels': per_kernel,
         'roofline': {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS,

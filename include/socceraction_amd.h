@@ -13,10 +13,15 @@
  * Conventions
  *  - return 0 on success, a negative SA_E* code on failure; sa_last_error()
  *    returns a thread-local message.  No C++ exception crosses this ABI.
- *  - the caller owns every buffer.  Output blocks are column-major [cols][ld]
- *    (one contiguous run of `ld` elements per feature column, matching pandas'
- *    2-D block layout); ld % 16 == 0 and ld >= round_up(n, 16).  Rows n..ld-1 of
- *    every output column are scratch (may be overwritten).
+ *  - the caller owns every buffer.  Feature output blocks (one per dtype: bool, f64,
+ *    i64) are TILED column-major: rows are grouped in tiles of R = tile_rows rows and
+ *    element (row j, column c) of a block with C columns lives at
+ *        (j / R) * (C * R) + c * R + (j % R)
+ *    i.e. each tile is a [C][R] column-major slab ("record batch").  With
+ *    R >= round_up(n, 16) there is one tile and the block is plain column-major with
+ *    leading dimension R (pandas' 2-D block layout).  R must be a multiple of 16 and
+ *    either a multiple of SA_TILE_QUANTUM or >= round_up(n, 16).  A block holds
+ *    ceil(n / R) * C * R elements; rows n.. of the last tile are scratch.
  *  - input columns are length-n arrays, 16-byte aligned.
  *  - ids are uint8 (SPADL type 0-22, result 0-5, bodypart 0-3, period 1-5; atomic
  *    type 0-32); team ids are int32 codes whose equality equals the equality of
@@ -33,6 +38,7 @@ extern "C" {
 
 #define SA_ABI_VERSION 1
 #define SA_MAX_FRAMES 8 /* max nb_prev_actions (window frames) */
+#define SA_TILE_QUANTUM 1024 /* tiled layouts: tile_rows must be a multiple of this */
 
 enum sa_status {
   SA_OK = 0,
@@ -110,6 +116,7 @@ typedef struct sa_feature_plan {
   int32_t bool_col[SA_XFN_COUNT];
   int32_t f64_col[SA_XFN_COUNT];
   int32_t i64_col[SA_XFN_COUNT];
+  int32_t n_bool, n_f64, n_i64;       /* total columns C of each block (tile stride) */
 } sa_feature_plan;
 
 /* ---- VAEP / Atomic-VAEP ------------------------------------------------------
@@ -117,21 +124,25 @@ typedef struct sa_feature_plan {
  * transformers of `plan`, for every segment of `a` at once.  Blocks may be NULL
  * when the plan writes no column of that dtype. */
 int sa_vaep_features(const sa_actions* a, const sa_feature_plan* plan, uint8_t* bool_out,
-                     double* f64_out, int64_t* i64_out, int64_t ld, void* stream);
+                     double* f64_out, int64_t* i64_out, int64_t tile_rows, void* stream);
 
 /* goalscore alone (vaep/features.py:505-539; atomic/vaep/features.py:313-344): writes the
- * goalscore_team / _opponent / _diff columns at out[0], out[ld], out[2*ld].  Also launched by
- * sa_vaep_features when the plan requests SA_XFN_GOALSCORE. */
-int sa_vaep_goalscore(const sa_actions* a, int64_t* out, int64_t ld, void* stream);
+ * goalscore_team / _opponent / _diff columns col, col+1, col+2 of the tiled i64 block
+ * `block` (n_cols columns, tile_rows rows per tile).  Also launched by sa_vaep_features
+ * when the plan requests SA_XFN_GOALSCORE. */
+int sa_vaep_goalscore(const sa_actions* a, int64_t* block, int32_t n_cols, int32_t col,
+                      int64_t tile_rows, void* stream);
 
 /* Replaces labels.scores / concedes / goal_from_shot (vaep/labels.py:9-116;
  * atomic/vaep/labels.py:9-107): look-ahead of nr_actions (>=1) clamped at each
- * segment's last row.  Any output may be NULL.  Outputs are length-ld bool bytes. */
+ * segment's last row.  Any output may be NULL.  Outputs are bool-byte vectors of length
+ * >= ld, 16-byte aligned (ld % 16 == 0, ld >= round_up(n, 16)). */
 int sa_vaep_labels(const sa_actions* a, int32_t nr_actions, uint8_t* scores, uint8_t* concedes,
                    uint8_t* goal_from_shot, int64_t ld, void* stream);
 
 /* Replaces formula.value (vaep/formula.py:116-151; atomic/vaep/formula.py:116-141)
- * with float64 probabilities; outputs offensive, defensive, vaep (length ld). */
+ * with float64 probabilities; outputs offensive, defensive, vaep: vectors of length
+ * >= round_up(n, 4), 16-byte aligned. */
 int sa_vaep_formula_f64(const sa_actions* a, const double* p_scores, const double* p_concedes,
                         double* off, double* def, double* val, void* stream);
 /* Same with float32 probabilities (the reference keeps the probability dtype). */

@@ -2,6 +2,8 @@
 
     python scripts/ab_sweep.py ROUNDS variant1 variant2 ...   ('default' = the main library)
 
+A variant may carry bench arguments after '@', e.g. 'default@--tile-rows=0' (plain layout).
+
 Each run is a fresh process with SOCCERACTION_AMD_LIB pointing at
 socceraction_amd/_lib/libsocceraction_amd_<variant>.so; results go to gpurun_out/ab.json.
 """
@@ -18,22 +20,24 @@ def main():
     variants = sys.argv[2:]
     res = {v: [] for v in variants}
     for r in range(rounds):
-        for v in variants:
+        for spec in variants:
+            v, _, extra = spec.partition('@')
             env = dict(os.environ)
             if v != 'default':
                 env['SOCCERACTION_AMD_LIB'] = os.path.join(
                     ROOT, 'socceraction_amd', '_lib', f'libsocceraction_amd_{v}.so')
-            out = subprocess.run([sys.executable, 'bench.py', '--steps', '20', '--warmup', '3',
-                                  '--no-cpu'], cwd=ROOT, env=env, capture_output=True, text=True,
+            args = [sys.executable, 'bench.py', '--steps', '20', '--warmup', '3', '--no-cpu']
+            args += [a for a in extra.split(',') if a]
+            out = subprocess.run(args, cwd=ROOT, env=env, capture_output=True, text=True,
                                  timeout=300)
             line = [ln for ln in out.stdout.splitlines() if ln.startswith('{')]
             if out.returncode != 0 or not line:
-                print(v, 'FAILED', out.returncode, out.stderr[-2000:], flush=True)
+                print(spec, 'FAILED', out.returncode, out.stderr[-2000:], flush=True)
                 sys.exit(out.returncode or 1)
             d = json.loads(line[0])
             ks = {k: x['ms'] for k, x in d['kernels'].items()}
-            res[v].append({'ms_per_step': d['ms_per_step'], 'kernels': ks})
-            print(r, v, d['ms_per_step'], ks, flush=True)
+            res[spec].append({'ms_per_step': d['ms_per_step'], 'kernels': ks})
+            print(r, spec, d['ms_per_step'], ks, flush=True)
     os.makedirs(os.path.join(ROOT, 'gpurun_out'), exist_ok=True)
     with open(os.path.join(ROOT, 'gpurun_out', 'ab.json'), 'w') as f:
         json.dump(res, f, indent=1)

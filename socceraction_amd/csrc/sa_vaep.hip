@@ -44,8 +44,15 @@ struct FeatArgs {
   uint8_t* bout;
   double* fout;
   int64_t* iout;
-  int64_t ld;
+  int64_t R;  // rows per tile (see include/socceraction_amd.h: tiled column-major blocks)
 };
+
+// Element offset of (row j, column c) in a tiled column-major block with C columns.  A
+// lane's 16 (or 2) rows never straddle a tile because R % 16 == 0.
+__device__ __forceinline__ int64_t tile_off(int64_t j, int64_t c, int64_t C, int64_t R) {
+  const int64_t t = j / R;
+  return t * C * R + c * R + (j - t * R);
+}
 
 // ------------------------------------------------------------------------------ helpers
 struct SegCursor {
@@ -94,23 +101,24 @@ __device__ __forceinline__ void st16(P* p, V v) {
 #endif
 }
 
-__device__ __forceinline__ void st_bool16(uint8_t* __restrict__ base, int64_t col, int64_t ld,
-                                          int64_t j0, uint32_t w0, uint32_t w1, uint32_t w2,
-                                          uint32_t w3) {
+// Stores into tiled blocks: `base` already points at the lane's (tile, row) position of
+// column 0, so column c is c * R elements further.
+__device__ __forceinline__ void st_bool16(uint8_t* __restrict__ base, int64_t col, int64_t R,
+                                          uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
   u32x4 v = {w0, w1, w2, w3};
-  st16(base + col * ld + j0, v);
+  st16(base + col * R, v);
 }
 
-__device__ __forceinline__ void st_f64x2(double* __restrict__ base, int64_t col, int64_t ld,
-                                         int64_t j, double v0, double v1) {
+__device__ __forceinline__ void st_f64x2(double* __restrict__ base, int64_t col, int64_t R,
+                                         double v0, double v1) {
   f64x2 v = {v0, v1};
-  st16(base + col * ld + j, v);
+  st16(base + col * R, v);
 }
 
-__device__ __forceinline__ void st_i64x2(int64_t* __restrict__ base, int64_t col, int64_t ld,
-                                         int64_t j, int64_t v0, int64_t v1) {
+__device__ __forceinline__ void st_i64x2(int64_t* __restrict__ base, int64_t col, int64_t R,
+                                         int64_t v0, int64_t v1) {
   i64x2 v = {(long long)v0, (long long)v1};
-  st16(base + col * ld + j, v);
+  st16(base + col * R, v);
 }
 
 // nan_to_num(arctan(dy / dx)) of vaep/features.py:376 (atan(+-inf) = +-pi/2, 0/0 -> 0)
@@ -161,14 +169,18 @@ __global__ __launch_bounds__(256) void bool_features_kernel(FeatArgs args) {
   const sa_feature_plan& P = args.p;
   const int64_t n = A.n;
   const int K = P.nb_prev_actions;
-  const int64_t ld = args.ld;
+  const int64_t R = args.R;
   const int64_t wave_base = ((int64_t)blockIdx.x * BLOCK_WAVES + wv) * BOOL_WAVE_ACTS;
   const sa_frame& F0 = A.frames[0];
   const int tcol = P.bool_col[SA_XFN_TEAM];
   const bool need_team = tcol >= 0 && K > 1;
   int64_t j0[BOOL_G];
+  uint8_t* bb[BOOL_G];  // column 0 of the lane's 16 rows in the tiled bool block
 #pragma unroll
-  for (int g = 0; g < BOOL_G; ++g) j0[g] = wave_base + g * 1024 + (int64_t)lane * LANE_ACTS;
+  for (int g = 0; g < BOOL_G; ++g) {
+    j0[g] = wave_base + g * 1024 + (int64_t)lane * LANE_ACTS;
+    bb[g] = args.bout + tile_off(j0[g], 0, P.n_bool, R);
+  }
 
   // d = min(j - seg_start, 15) per action; rows >= n keep d = 0 (windows stay in range)
   uint32_t dw[BOOL_G][4];
@@ -256,7 +268,7 @@ __global__ __launch_bounds__(256) void bool_features_kernel(FeatArgs args) {
         for (int t = 0; t < N_TYPES; ++t) {
 #pragma unroll
           for (int g = 0; g < BOOL_G; ++g)
-            st_bool16(args.bout, c_type + i * N_TYPES + t, ld, j0[g], bytes_eq(tw[g][0], t),
+            st_bool16(bb[g], c_type + i * N_TYPES + t, R, bytes_eq(tw[g][0], t),
                       bytes_eq(tw[g][1], t), bytes_eq(tw[g][2], t), bytes_eq(tw[g][3], t));
         }
       } else {
@@ -274,7 +286,7 @@ __global__ __launch_bounds__(256) void bool_features_kernel(FeatArgs args) {
               m2 |= bytes_eq(tw[g][2], AT_INTERCEPTION2);
               m3 |= bytes_eq(tw[g][3], AT_INTERCEPTION2);
             }
-            st_bool16(args.bout, c_type + i * N_ATOMIC_NAMES + u, ld, j0[g], m0, m1, m2, m3);
+            st_bool16(bb[g], c_type + i * N_ATOMIC_NAMES + u, R, m0, m1, m2, m3);
           }
         }
       }
@@ -283,7 +295,7 @@ __global__ __launch_bounds__(256) void bool_features_kernel(FeatArgs args) {
       for (int r = 0; r < N_RESULTS; ++r) {
 #pragma unroll
         for (int g = 0; g < BOOL_G; ++g)
-          st_bool16(args.bout, c_res + i * N_RESULTS + r, ld, j0[g], bytes_eq(rw[g][0], r),
+          st_bool16(bb[g], c_res + i * N_RESULTS + r, R, bytes_eq(rw[g][0], r),
                     bytes_eq(rw[g][1], r), bytes_eq(rw[g][2], r), bytes_eq(rw[g][3], r));
       }
     }
@@ -299,7 +311,7 @@ __global__ __launch_bounds__(256) void bool_features_kernel(FeatArgs args) {
       for (int code = 0; code < N_TYPES * N_RESULTS; ++code) {
 #pragma unroll
         for (int g = 0; g < BOOL_G; ++g)
-          st_bool16(args.bout, cb + code, ld, j0[g], bytes_eq(cw[g][0], code),
+          st_bool16(bb[g], cb + code, R, bytes_eq(cw[g][0], code),
                     bytes_eq(cw[g][1], code), bytes_eq(cw[g][2], code), bytes_eq(cw[g][3], code));
       }
     }
@@ -307,7 +319,7 @@ __global__ __launch_bounds__(256) void bool_features_kernel(FeatArgs args) {
       for (int b = 0; b < N_BODYPARTS; ++b) {
 #pragma unroll
         for (int g = 0; g < BOOL_G; ++g)
-          st_bool16(args.bout, c_bp + i * N_BODYPARTS + b, ld, j0[g], bytes_eq(bw[g][0], b),
+          st_bool16(bb[g], c_bp + i * N_BODYPARTS + b, R, bytes_eq(bw[g][0], b),
                     bytes_eq(bw[g][1], b), bytes_eq(bw[g][2], b), bytes_eq(bw[g][3], b));
       }
     }
@@ -330,7 +342,7 @@ __global__ __launch_bounds__(256) void bool_features_kernel(FeatArgs args) {
           }
           m[mm >> 2] |= (uint32_t)(t0 == ti) << (8 * (mm & 3));
         }
-        st_bool16(args.bout, tcol + (i - 1), ld, j0[g], m[0], m[1], m[2], m[3]);
+        st_bool16(bb[g], tcol + (i - 1), R, m[0], m[1], m[2], m[3]);
       }
     }
   }
@@ -345,7 +357,7 @@ __global__ __launch_bounds__(256) void num_features_kernel(FeatArgs args) {
   const sa_feature_plan& P = args.p;
   const int64_t n = A.n;
   const int K = P.nb_prev_actions;
-  const int64_t ld = args.ld;
+  const int64_t R = args.R;
   const int64_t wave_base = ((int64_t)blockIdx.x * BLOCK_WAVES + wv) * WAVE_ACTS;
   const sa_frame& F0 = A.frames[0];
   if (wave_base + 2 * lane >= n) return;
@@ -363,6 +375,8 @@ __global__ __launch_bounds__(256) void num_features_kernel(FeatArgs args) {
   for (int pr = 0; pr < NUM_PAIRS; ++pr) {
     const int64_t jb = wave_base + pr * 2 * WAVE + 2 * lane;
     if (jb >= n) break;
+    double* fb = args.fout + tile_off(jb, 0, P.n_f64, R);      // column 0 of rows jb, jb+1
+    int64_t* ib = args.iout + tile_off(jb, 0, P.n_i64, R);
     int64_t jr[2];
     int dd[2];
     bool away[2];
@@ -413,24 +427,24 @@ __global__ __launch_bounds__(256) void num_features_kernel(FeatArgs args) {
           t0[e] = ts[e];
         }
       }
-      if (c_at >= 0) st_i64x2(args.iout, c_at + i, ld, jb, typ[0], typ[1]);
-      if (c_re >= 0) st_i64x2(args.iout, c_re + i, ld, jb, res[0], res[1]);
-      if (c_bi >= 0) st_i64x2(args.iout, c_bi + i, ld, jb, bp[0], bp[1]);
-      if (c_ti >= 0) st_i64x2(args.iout, c_ti + i, ld, jb, per[0], per[1]);
+      if (c_at >= 0) st_i64x2(ib, c_at + i, R, typ[0], typ[1]);
+      if (c_re >= 0) st_i64x2(ib, c_re + i, R, res[0], res[1]);
+      if (c_bi >= 0) st_i64x2(ib, c_bi + i, R, bp[0], bp[1]);
+      if (c_ti >= 0) st_i64x2(ib, c_ti + i, R, per[0], per[1]);
       if (c_tf >= 0) {
-        st_f64x2(args.fout, c_tf + 2 * i, ld, jb, ts[0], ts[1]);
+        st_f64x2(fb, c_tf + 2 * i, R, ts[0], ts[1]);
         // ((period_id - 1) * 45 * 60) + time_seconds   (features.py:313)
-        st_f64x2(args.fout, c_tf + 2 * i + 1, ld, jb, (double)((per[0] - 1) * 2700) + ts[0],
+        st_f64x2(fb, c_tf + 2 * i + 1, R, (double)((per[0] - 1) * 2700) + ts[0],
                  (double)((per[1] - 1) * 2700) + ts[1]);
       }
       if (!ATOMIC) {
         if (c_sl >= 0) {
-          st_f64x2(args.fout, c_sl + 2 * i, ld, jb, c0[0], c0[1]);
-          st_f64x2(args.fout, c_sl + 2 * i + 1, ld, jb, c1[0], c1[1]);
+          st_f64x2(fb, c_sl + 2 * i, R, c0[0], c0[1]);
+          st_f64x2(fb, c_sl + 2 * i + 1, R, c1[0], c1[1]);
         }
         if (c_el >= 0) {
-          st_f64x2(args.fout, c_el + 2 * i, ld, jb, c2[0], c2[1]);
-          st_f64x2(args.fout, c_el + 2 * i + 1, ld, jb, c3[0], c3[1]);
+          st_f64x2(fb, c_el + 2 * i, R, c2[0], c2[1]);
+          st_f64x2(fb, c_el + 2 * i + 1, R, c3[0], c3[1]);
         }
         if (c_sp >= 0) {
           double dist[2], ang[2];
@@ -440,8 +454,8 @@ __global__ __launch_bounds__(256) void num_features_kernel(FeatArgs args) {
             dist[e] = sqrt(dx * dx + dy * dy);
             ang[e] = polar_angle(dy, dx);
           }
-          st_f64x2(args.fout, c_sp + 2 * i, ld, jb, dist[0], dist[1]);
-          st_f64x2(args.fout, c_sp + 2 * i + 1, ld, jb, ang[0], ang[1]);
+          st_f64x2(fb, c_sp + 2 * i, R, dist[0], dist[1]);
+          st_f64x2(fb, c_sp + 2 * i + 1, R, ang[0], ang[1]);
         }
         if (c_ep >= 0) {
           double dist[2], ang[2];
@@ -451,8 +465,8 @@ __global__ __launch_bounds__(256) void num_features_kernel(FeatArgs args) {
             dist[e] = sqrt(dx * dx + dy * dy);
             ang[e] = polar_angle(dy, dx);
           }
-          st_f64x2(args.fout, c_ep + 2 * i, ld, jb, dist[0], dist[1]);
-          st_f64x2(args.fout, c_ep + 2 * i + 1, ld, jb, ang[0], ang[1]);
+          st_f64x2(fb, c_ep + 2 * i, R, dist[0], dist[1]);
+          st_f64x2(fb, c_ep + 2 * i + 1, R, ang[0], ang[1]);
         }
         if (c_mv >= 0) {
           double mdx[2], mdy[2], mv[2];
@@ -462,9 +476,9 @@ __global__ __launch_bounds__(256) void num_features_kernel(FeatArgs args) {
             mdy[e] = c3[e] - c1[e];
             mv[e] = sqrt(mdx[e] * mdx[e] + mdy[e] * mdy[e]);
           }
-          st_f64x2(args.fout, c_mv + 3 * i, ld, jb, mdx[0], mdx[1]);
-          st_f64x2(args.fout, c_mv + 3 * i + 1, ld, jb, mdy[0], mdy[1]);
-          st_f64x2(args.fout, c_mv + 3 * i + 2, ld, jb, mv[0], mv[1]);
+          st_f64x2(fb, c_mv + 3 * i, R, mdx[0], mdx[1]);
+          st_f64x2(fb, c_mv + 3 * i + 1, R, mdy[0], mdy[1]);
+          st_f64x2(fb, c_mv + 3 * i + 2, R, mv[0], mv[1]);
         }
         if (i >= 1 && c_sd >= 0) {  // space_delta: a_i end - a0 start (features.py:491-499)
           double sdx[2], sdy[2], sm[2];
@@ -474,14 +488,14 @@ __global__ __launch_bounds__(256) void num_features_kernel(FeatArgs args) {
             sdy[e] = c3[e] - sy0[e];
             sm[e] = sqrt(sdx[e] * sdx[e] + sdy[e] * sdy[e]);
           }
-          st_f64x2(args.fout, c_sd + 3 * (i - 1), ld, jb, sdx[0], sdx[1]);
-          st_f64x2(args.fout, c_sd + 3 * (i - 1) + 1, ld, jb, sdy[0], sdy[1]);
-          st_f64x2(args.fout, c_sd + 3 * (i - 1) + 2, ld, jb, sm[0], sm[1]);
+          st_f64x2(fb, c_sd + 3 * (i - 1), R, sdx[0], sdx[1]);
+          st_f64x2(fb, c_sd + 3 * (i - 1) + 1, R, sdy[0], sdy[1]);
+          st_f64x2(fb, c_sd + 3 * (i - 1) + 2, R, sm[0], sm[1]);
         }
       } else {
         if (c_lo >= 0) {
-          st_f64x2(args.fout, c_lo + 2 * i, ld, jb, c0[0], c0[1]);
-          st_f64x2(args.fout, c_lo + 2 * i + 1, ld, jb, c1[0], c1[1]);
+          st_f64x2(fb, c_lo + 2 * i, R, c0[0], c0[1]);
+          st_f64x2(fb, c_lo + 2 * i + 1, R, c1[0], c1[1]);
         }
         if (c_po >= 0) {
           double dist[2], ang[2];
@@ -491,8 +505,8 @@ __global__ __launch_bounds__(256) void num_features_kernel(FeatArgs args) {
             dist[e] = sqrt(dx * dx + dy * dy);
             ang[e] = polar_angle(dy, dx);
           }
-          st_f64x2(args.fout, c_po + 2 * i, ld, jb, dist[0], dist[1]);
-          st_f64x2(args.fout, c_po + 2 * i + 1, ld, jb, ang[0], ang[1]);
+          st_f64x2(fb, c_po + 2 * i, R, dist[0], dist[1]);
+          st_f64x2(fb, c_po + 2 * i + 1, R, ang[0], ang[1]);
         }
         if (c_mp >= 0) {  // atomic/vaep/features.py:279-284
           double md[2], ma[2];
@@ -501,8 +515,8 @@ __global__ __launch_bounds__(256) void num_features_kernel(FeatArgs args) {
             md[e] = sqrt(c2[e] * c2[e] + c3[e] * c3[e]);
             ma[e] = (c3[e] == 0.0) ? 0.0 : atan2(c3[e], c2[e]);
           }
-          st_f64x2(args.fout, c_mp + 2 * i, ld, jb, md[0], md[1]);
-          st_f64x2(args.fout, c_mp + 2 * i + 1, ld, jb, ma[0], ma[1]);
+          st_f64x2(fb, c_mp + 2 * i, R, md[0], md[1]);
+          st_f64x2(fb, c_mp + 2 * i + 1, R, ma[0], ma[1]);
         }
         if (c_di >= 0) {  // atomic/vaep/features.py:302-310
           double ox[2], oy[2];
@@ -512,12 +526,12 @@ __global__ __launch_bounds__(256) void num_features_kernel(FeatArgs args) {
             ox[e] = td > 0.0 ? c2[e] / td : c2[e];
             oy[e] = td > 0.0 ? c3[e] / td : c3[e];
           }
-          st_f64x2(args.fout, c_di + 2 * i, ld, jb, ox[0], ox[1]);
-          st_f64x2(args.fout, c_di + 2 * i + 1, ld, jb, oy[0], oy[1]);
+          st_f64x2(fb, c_di + 2 * i, R, ox[0], ox[1]);
+          st_f64x2(fb, c_di + 2 * i + 1, R, oy[0], oy[1]);
         }
       }
       if (i >= 1 && c_td >= 0)  // time_delta: a0 time - a_i time (features.py:469-473)
-        st_f64x2(args.fout, c_td + (i - 1), ld, jb, t0[0] - ts[0], t0[1] - ts[1]);
+        st_f64x2(fb, c_td + (i - 1), R, t0[0] - ts[0], t0[1] - ts[1]);
     }
   }
 }
@@ -529,8 +543,8 @@ __global__ __launch_bounds__(256) void num_features_kernel(FeatArgs args) {
 constexpr int GS_THREADS = 256;
 
 template <bool ATOMIC>
-__global__ __launch_bounds__(GS_THREADS) void goalscore_kernel(sa_actions A, int64_t* __restrict__ out,
-                                                               int64_t ld) {
+__global__ __launch_bounds__(GS_THREADS) void goalscore_kernel(sa_actions A, int64_t* __restrict__ block,
+                                                               int64_t C, int64_t col, int64_t R) {
   __shared__ uint64_t wsum[GS_THREADS / WAVE];
   const int64_t g = blockIdx.x;
   const int64_t s = A.seg_off[g], e = A.seg_off[g + 1];
@@ -582,9 +596,10 @@ __global__ __launch_bounds__(GS_THREADS) void goalscore_kernel(sa_actions A, int
         const int64_t j = j0 + q;
         const int64_t cA = (int64_t)(excl & 0xFFFFFFFFull), cB = (int64_t)(excl >> 32);
         const int64_t tm = isA[q] ? cA : cB, op = isA[q] ? cB : cA;
-        out[j] = tm;
-        out[ld + j] = op;
-        out[2 * ld + j] = tm - op;
+        int64_t* o = block + tile_off(j, col, C, R);
+        o[0] = tm;
+        o[R] = op;
+        o[2 * R] = tm - op;
       }
       excl += inc[q];
     }
@@ -812,8 +827,16 @@ static int check_actions(const sa_actions* a, bool allow_explicit) {
   return SA_OK;
 }
 
+static int check_tile_rows(int64_t R, int64_t n) {
+  const int64_t n16 = ((n + 15) / 16) * 16;
+  if (R <= 0 || R % 16 != 0 || (R < n16 && R % SA_TILE_QUANTUM != 0))
+    return fail(SA_EINVAL, "tile_rows must be a multiple of 16 and either >= round_up(n, 16) "
+                           "or a multiple of %d", SA_TILE_QUANTUM);
+  return SA_OK;
+}
+
 extern "C" int sa_vaep_features(const sa_actions* a, const sa_feature_plan* plan, uint8_t* bool_out,
-                                double* f64_out, int64_t* i64_out, int64_t ld, void* stream) {
+                                double* f64_out, int64_t* i64_out, int64_t tile_rows, void* stream) {
   int rc = check_actions(a, true);
   if (rc) return rc;
   if (!plan) return fail(SA_EINVAL, "null plan");
@@ -821,8 +844,8 @@ extern "C" int sa_vaep_features(const sa_actions* a, const sa_feature_plan* plan
   if (K < 1 || K > SA_MAX_FRAMES) return fail(SA_EINVAL, "nb_prev_actions must be in [1, 8]");
   if (a->n_frames > 1 && a->n_frames != K)
     return fail(SA_EINVAL, "explicit mode needs n_frames == nb_prev_actions");
-  if (ld % 16 != 0 || ld < ((a->n + 15) / 16) * 16)
-    return fail(SA_EINVAL, "ld must be a multiple of 16 and >= round_up(n, 16)");
+  rc = check_tile_rows(tile_rows, a->n);
+  if (rc) return rc;
   if (!aligned16(bool_out) || !aligned16(f64_out) || !aligned16(i64_out))
     return fail(SA_EINVAL, "output blocks must be 16-byte aligned");
   bool wb = false, wn = false;
@@ -850,7 +873,12 @@ extern "C" int sa_vaep_features(const sa_actions* a, const sa_feature_plan* plan
   }
   if (a->n == 0) return SA_OK;
   hipStream_t st = (hipStream_t)stream;
-  FeatArgs args{*a, *plan, bool_out, f64_out, i64_out, ld};
+  for (int x = 0; x < SA_XFN_COUNT; ++x) {
+    if (plan->bool_col[x] >= plan->n_bool || plan->f64_col[x] >= plan->n_f64 ||
+        plan->i64_col[x] >= plan->n_i64)
+      return fail(SA_EINVAL, "plan column offset beyond the block's column count");
+  }
+  FeatArgs args{*a, *plan, bool_out, f64_out, i64_out, tile_rows};
   const dim3 grid((unsigned)((a->n + BLOCK_ACTS - 1) / BLOCK_ACTS)), block(BLOCK_WAVES * WAVE);
   const dim3 bgrid((unsigned)((a->n + BOOL_BLOCK_ACTS - 1) / BOOL_BLOCK_ACTS));
   const bool expl = a->n_frames > 1;
@@ -885,23 +913,26 @@ extern "C" int sa_vaep_features(const sa_actions* a, const sa_feature_plan* plan
     if (rc) return rc;
   }
   const int gc = plan->i64_col[SA_XFN_GOALSCORE];
-  if (gc >= 0) rc = sa_vaep_goalscore(a, i64_out + (int64_t)gc * ld, ld, stream);
+  if (gc >= 0) rc = sa_vaep_goalscore(a, i64_out, plan->n_i64, gc, tile_rows, stream);
   return rc;
 }
 
-extern "C" int sa_vaep_goalscore(const sa_actions* a, int64_t* out, int64_t ld, void* stream) {
+extern "C" int sa_vaep_goalscore(const sa_actions* a, int64_t* block, int32_t n_cols, int32_t col,
+                                 int64_t tile_rows, void* stream) {
   int rc = check_actions(a, true);
   if (rc) return rc;
-  if (!out) return fail(SA_EINVAL, "null goalscore output");
-  if (ld < a->n) return fail(SA_EINVAL, "ld < n");
+  if (!block) return fail(SA_EINVAL, "null goalscore output");
+  if (col < 0 || col + 3 > n_cols) return fail(SA_EINVAL, "goalscore columns outside the block");
+  rc = check_tile_rows(tile_rows, a->n);
+  if (rc) return rc;
   if (a->n == 0) return SA_OK;
   hipStream_t st = (hipStream_t)stream;
   if (a->atomic)
     hipLaunchKernelGGL((goalscore_kernel<true>), dim3((unsigned)a->n_segments), dim3(GS_THREADS), 0, st,
-                       *a, out, ld);
+                       *a, block, (int64_t)n_cols, (int64_t)col, tile_rows);
   else
     hipLaunchKernelGGL((goalscore_kernel<false>), dim3((unsigned)a->n_segments), dim3(GS_THREADS), 0,
-                       st, *a, out, ld);
+                       st, *a, block, (int64_t)n_cols, (int64_t)col, tile_rows);
   return check_launch("goalscore_kernel");
 }
 

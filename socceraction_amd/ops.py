@@ -25,29 +25,52 @@ def _ld(n: int) -> int:
 
 @dataclass
 class FeatureBlocks:
-    """Column-major feature blocks in HBM: ``[n_cols, ld]`` each (rows >= n are scratch)."""
+    """Feature blocks in HBM, one per dtype, in the tiled column-major layout of
+    ``include/socceraction_amd.h``: tensors ``[n_tiles, n_cols, R]`` (R = rows per tile;
+    one tile of R >= n rows is plain column-major)."""
 
     plan: FeaturePlan
     n: int
-    ld: int
+    R: int
     bool_block: torch.Tensor
     f64_block: torch.Tensor
     i64_block: torch.Tensor
 
+    @property
+    def ld(self) -> int:  # single-tile leading dimension (kept for callers of the plain layout)
+        return self.R
+
+    def _blk(self, kind: str) -> torch.Tensor:
+        return {'b': self.bool_block, 'f': self.f64_block, 'i': self.i64_block}[kind]
+
+    def block(self, kind: str) -> torch.Tensor:
+        """``[n_cols, n]`` view (one tile) or untiled copy (several tiles), on device."""
+        t = self._blk(kind)
+        if t.shape[0] == 1:
+            return t[0, :, :self.n]
+        return t.permute(1, 0, 2).reshape(t.shape[1], -1)[:, :self.n]
+
+    def column(self, kind: str, col: int) -> torch.Tensor:
+        return self._blk(kind)[:, col, :].reshape(-1)[:self.n]
+
+    def to_numpy(self):
+        return tuple(self.block(k).cpu().numpy() for k in 'bfi')
+
     def to_frame(self, index=None):
         """Copy to host and build the reference-shaped DataFrame."""
-        b = self.bool_block.cpu().numpy()
-        f = self.f64_block.cpu().numpy()
-        i = self.i64_block.cpu().numpy()
+        b, f, i = self.to_numpy()
         return assemble_frame(self.plan, b, f, i, self.n, index)
 
 
-def alloc_feature_blocks(plan: FeaturePlan, n: int, dev) -> FeatureBlocks:
-    ld = _ld(n)
-    return FeatureBlocks(plan, n, ld,
-                         torch.empty((plan.n_bool, ld), dtype=torch.uint8, device=dev),
-                         torch.empty((plan.n_f64, ld), dtype=torch.float64, device=dev),
-                         torch.empty((plan.n_i64, ld), dtype=torch.int64, device=dev))
+def alloc_feature_blocks(plan: FeaturePlan, n: int, dev, tile_rows: Optional[int] = None
+                         ) -> FeatureBlocks:
+    """Allocate the three blocks; ``tile_rows=None`` = one tile (plain column-major)."""
+    R = _ld(n) if tile_rows is None else int(tile_rows)
+    tiles = max(1, -(-n // R))
+    return FeatureBlocks(plan, n, R,
+                         torch.empty((tiles, plan.n_bool, R), dtype=torch.uint8, device=dev),
+                         torch.empty((tiles, plan.n_f64, R), dtype=torch.float64, device=dev),
+                         torch.empty((tiles, plan.n_i64, R), dtype=torch.int64, device=dev))
 
 
 def _ptr(t: Optional[torch.Tensor]):
@@ -58,14 +81,15 @@ def features_into(s: _native.SaActions, out: FeatureBlocks) -> None:
     lib = _native.lib()
     _native.check(lib.sa_vaep_features(ctypes.byref(s), ctypes.byref(out.plan.struct),
                                        _ptr(out.bool_block), _ptr(out.f64_block),
-                                       _ptr(out.i64_block), out.ld, stream_handle()))
+                                       _ptr(out.i64_block), out.R, stream_handle()))
 
 
 def features(batch: ActionBatch, xfns: Sequence[str], k: int, flip: bool = True,
-             out: Optional[FeatureBlocks] = None) -> FeatureBlocks:
+             out: Optional[FeatureBlocks] = None, tile_rows: Optional[int] = None
+             ) -> FeatureBlocks:
     """Game-state features of every segment of ``batch`` (windowed mode)."""
     plan = out.plan if out is not None else build_plan(xfns, k, batch.atomic)
-    out = out or alloc_feature_blocks(plan, batch.n, batch.device)
+    out = out or alloc_feature_blocks(plan, batch.n, batch.device, tile_rows)
     features_into(batch.struct(flip=flip), out)
     return out
 
@@ -242,5 +266,5 @@ def goalscore_into(batch: ActionBatch, out: FeatureBlocks) -> None:
     if gc < 0:
         raise ValueError('plan has no goalscore columns')
     s = batch.struct()
-    _native.check(_native.lib().sa_vaep_goalscore(ctypes.byref(s), out.i64_block[gc].data_ptr(),
-                                                  out.ld, stream_handle()))
+    _native.check(_native.lib().sa_vaep_goalscore(ctypes.byref(s), _ptr(out.i64_block),
+                                                  out.plan.n_i64, gc, out.R, stream_handle()))

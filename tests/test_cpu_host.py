@@ -40,7 +40,7 @@ def test_ctypes_struct_layout_matches_header():
     from socceraction_amd import _native
     assert ctypes.sizeof(_native.SaFrame) == 80
     assert ctypes.sizeof(_native.SaActions) == 40 + 8 * 80
-    assert ctypes.sizeof(_native.SaFeaturePlan) == 4 * (1 + 3 * _native.SA_XFN_COUNT)
+    assert ctypes.sizeof(_native.SaFeaturePlan) == 4 * (1 + 3 * _native.SA_XFN_COUNT + 3)
     with open(os.path.join(ROOT, 'include', 'socceraction_amd.h')) as f:
         enum = f.read().split('enum sa_xfn {')[1].split('};')[0]
     names = re.findall(r'SA_XFN_([A-Z_]+)', enum)

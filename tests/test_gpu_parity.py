@@ -25,9 +25,7 @@ def sa():
 def _blocks_match(fb, g, k, n):
     names = list(g[f'k{k}_names_all'])
     assert fb.plan.names == names
-    b = fb.bool_block.cpu().numpy()
-    f = fb.f64_block.cpu().numpy()
-    i = fb.i64_block.cpu().numpy()
+    b, f, i = fb.to_numpy()
     blocks = {'b': b, 'f': f, 'i': i}
     got = {'b': [], 'f': [], 'i': []}
     for name, kind, col in fb.plan.order:
@@ -92,13 +90,13 @@ def test_batched_segments_match_per_game(sa, atomic):
     homes = [g['home_team_id'][0] for g in gs]
     ab = B.ActionBatch.from_frame(df, atomic=atomic, home_team_id=homes, segments='game')
     assert ab.n_segments == len(gs)
-    fb = ops.features(ab, default, 3)
+    fb = ops.features(ab, default, 3, tile_rows=1024)  # tiled layout, several tiles
+    assert fb.bool_block.shape[0] == -(-ab.n // 1024)
     lb = ops.labels(ab)
     ps = torch.tensor(np.concatenate([g['ps'] for g in gs]), device=ab.device)
     pc = torch.tensor(np.concatenate([g['pc'] for g in gs]), device=ab.device)
     v = ops.formula(ab, ps, pc).cpu().numpy()
-    b, f, i = (fb.bool_block.cpu().numpy(), fb.f64_block.cpu().numpy(),
-               fb.i64_block.cpu().numpy())
+    b, f, i = fb.to_numpy()
     o = 0
     for g in gs:
         n = len(g['type_id'] if 'type_id' in g else g['in_type_id'])
@@ -118,6 +116,22 @@ def test_batched_segments_match_per_game(sa, atomic):
         for r, c in enumerate(('offensive_value', 'defensive_value', 'vaep_value')):
             assert_close(v[r, sl], g[f'{c}_64'], c)
         o += n
+
+
+def test_tiled_and_plain_layouts_agree(sa):
+    """The tiled layout (R = 1024, 2048) holds exactly the plain column-major values."""
+    B, ops, syn = sa['batch'], sa['ops'], sa['synthetic']
+    d = syn.spadl_games(7, seed=3)
+    ab = B.ActionBatch.from_columns(d)
+    plain = ops.features(ab, vo.SPADL_DEFAULT, 3)
+    assert plain.bool_block.shape[0] == 1
+    ref = plain.to_numpy()
+    for R in (1024, 2048):
+        tiled = ops.features(ab, vo.SPADL_DEFAULT, 3, tile_rows=R)
+        for a, b in zip(tiled.to_numpy(), ref):
+            np.testing.assert_array_equal(a, b)
+    with pytest.raises(ValueError):
+        ops.features(ab, vo.SPADL_DEFAULT, 3, tile_rows=1000)
 
 
 def test_explicit_frames_match_windowed(sa):
@@ -182,7 +196,7 @@ def test_full_size_sampled_games_vs_oracle(sa):
     B, ops, syn = sa['batch'], sa['ops'], sa['synthetic']
     d = syn.spadl_games(10000)
     ab = B.ActionBatch.from_columns(d)
-    fb = ops.features(ab, vo.SPADL_DEFAULT, 3)
+    fb = ops.features(ab, vo.SPADL_DEFAULT, 3, tile_rows=1024)
     lb = ops.labels(ab)
     p = syn.probabilities(ab.n)
     ps = torch.from_numpy(p['scores']).to(ab.device)
@@ -195,7 +209,8 @@ def test_full_size_sampled_games_vs_oracle(sa):
     tr = [col for name, kind, col in plan.order if name.startswith('type_') and '_result_' in name]
     assert len(tr) == 414
     for i in range(3):
-        s = fb.bool_block[tr[i * 138]:tr[i * 138] + 138, :n].sum(dim=0, dtype=torch.int32)
+        s = fb.bool_block[:, tr[i * 138]:tr[i * 138] + 138, :].sum(dim=1, dtype=torch.int32)
+        s = s.reshape(-1)[:n]
         assert bool((s == 1).all())
     rng = np.random.default_rng(0)
     off = d['game_off']
@@ -207,8 +222,7 @@ def test_full_size_sampled_games_vs_oracle(sa):
                                        'bodypart_id')}
         ref = vo.features(cols, 3, vo.SPADL_DEFAULT, home=[d['home_team_id'][g]])
         assert [c[0] for c in ref] == names
-        blocks = {'b': fb.bool_block[:, s:e].cpu().numpy(), 'f': fb.f64_block[:, s:e].cpu().numpy(),
-                  'i': fb.i64_block[:, s:e].cpu().numpy()}
+        blocks = {k: fb.block(k)[:, s:e].cpu().numpy() for k in 'bfi'}
         for (name, kind, col), (_, _, rv) in zip(plan.order, ref):
             got = blocks[kind][col]
             if kind == 'f':
