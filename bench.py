@@ -85,8 +85,10 @@ def main() -> None:
     ap.add_argument('--games', type=int, default=10000, help='games per GPU (cfg2: 10k)')
     ap.add_argument('--cpu-seconds', type=float, default=15.0)
     ap.add_argument('--no-cpu', action='store_true')
-    ap.add_argument('--tile-rows', type=int, default=1024,
-                    help='rows per output tile (0 = one tile: plain column-major blocks)')
+    ap.add_argument('--bool-tile', type=int, default=1024,
+                    help='rows per bool-block tile (0 = one tile: plain column-major)')
+    ap.add_argument('--num-tile', type=int, default=128,
+                    help='rows per f64/i64-block tile (0 = one tile: plain column-major)')
     args = ap.parse_args()
 
     dist, rank, world = _dist()
@@ -95,7 +97,8 @@ def main() -> None:
     ab = B.ActionBatch.from_columns(d, dev=dev)
     n = ab.n
     plan = catalog.build_plan(SPADL_DEFAULT, 3)
-    out = ops.alloc_feature_blocks(plan, n, dev, tile_rows=args.tile_rows or None)
+    out = ops.alloc_feature_blocks(plan, n, dev, bool_tile=args.bool_tile or None,
+                                   num_tile=args.num_tile or None)
     ld = (n + 15) // 16 * 16
 
     def sub(keep):  # the same block layout with only some column families launched
@@ -108,7 +111,8 @@ def main() -> None:
                 q.struct.f64_col[x] = -1
             if 'i' not in keep or x == XFN['goalscore']:
                 q.struct.i64_col[x] = -1
-        return ops.FeatureBlocks(q, n, out.R, out.bool_block, out.f64_block, out.i64_block)
+        return ops.FeatureBlocks(q, n, out.Rb, out.Rn, out.bool_block, out.f64_block,
+                                 out.i64_block)
 
     bool_out, num_out = sub('b'), sub('fi')
     p = synthetic.probabilities(n)
@@ -184,7 +188,8 @@ def main() -> None:
         'config': {'workload': 'cfg2: 10k-game synthetic SPADL per GPU, VAEP compute_features '
                                '(k=3, default xfns, 568 cols) + compute_labels + formula.value (f64)',
                    'games_per_gpu': args.games, 'actions_per_gpu': n,
-                   'feature_layout': f'tiled column-major, {out.R} rows per tile',
+                   'feature_layout': f'tiled column-major: bool {out.Rb}, f64/i64 {out.Rn} rows '
+                                     'per tile',
                    'parallelism': f'games sharded over {world} GPU(s)'},
         'kernels': per_kernel,
         'roofline': {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS,

@@ -14,14 +14,14 @@
  *  - return 0 on success, a negative SA_E* code on failure; sa_last_error()
  *    returns a thread-local message.  No C++ exception crosses this ABI.
  *  - the caller owns every buffer.  Feature output blocks (one per dtype: bool, f64,
- *    i64) are TILED column-major: rows are grouped in tiles of R = tile_rows rows and
+ *    i64; see sa_block) are TILED column-major: rows are grouped in tiles of R rows and
  *    element (row j, column c) of a block with C columns lives at
  *        (j / R) * (C * R) + c * R + (j % R)
  *    i.e. each tile is a [C][R] column-major slab ("record batch").  With
  *    R >= round_up(n, 16) there is one tile and the block is plain column-major with
- *    leading dimension R (pandas' 2-D block layout).  R must be a multiple of 16 and
- *    either a multiple of SA_TILE_QUANTUM or >= round_up(n, 16).  A block holds
- *    ceil(n / R) * C * R elements; rows n.. of the last tile are scratch.
+ *    leading dimension R (pandas' 2-D block layout).  Otherwise R must be a multiple of
+ *    SA_BOOL_TILE_QUANTUM (bool block) / SA_NUM_TILE_QUANTUM (f64, i64 blocks).  A block
+ *    holds ceil(n / R) * C * R elements; rows n.. of the last tile are scratch.
  *  - input columns are length-n arrays, 16-byte aligned.
  *  - ids are uint8 (SPADL type 0-22, result 0-5, bodypart 0-3, period 1-5; atomic
  *    type 0-32); team ids are int32 codes whose equality equals the equality of
@@ -38,7 +38,8 @@ extern "C" {
 
 #define SA_ABI_VERSION 1
 #define SA_MAX_FRAMES 8 /* max nb_prev_actions (window frames) */
-#define SA_TILE_QUANTUM 1024 /* tiled layouts: tile_rows must be a multiple of this */
+#define SA_BOOL_TILE_QUANTUM 1024 /* bool block: rows per tile must be a multiple of this */
+#define SA_NUM_TILE_QUANTUM 128   /* f64 / i64 blocks: rows per tile must be a multiple of this */
 
 enum sa_status {
   SA_OK = 0,
@@ -116,22 +117,28 @@ typedef struct sa_feature_plan {
   int32_t bool_col[SA_XFN_COUNT];
   int32_t f64_col[SA_XFN_COUNT];
   int32_t i64_col[SA_XFN_COUNT];
-  int32_t n_bool, n_f64, n_i64;       /* total columns C of each block (tile stride) */
 } sa_feature_plan;
+
+/* One output block: device pointer (16-byte aligned), its column count C and rows per
+ * tile R (layout above). */
+typedef struct sa_block {
+  void* data;
+  int32_t n_cols;
+  int32_t reserved;
+  int64_t tile_rows;
+} sa_block;
 
 /* ---- VAEP / Atomic-VAEP ------------------------------------------------------
  * Replaces VAEP.compute_features (vaep/base.py:97-116): gamestates + flip + the
- * transformers of `plan`, for every segment of `a` at once.  Blocks may be NULL
- * when the plan writes no column of that dtype. */
-int sa_vaep_features(const sa_actions* a, const sa_feature_plan* plan, uint8_t* bool_out,
-                     double* f64_out, int64_t* i64_out, int64_t tile_rows, void* stream);
+ * transformers of `plan`, for every segment of `a` at once.  A block (or its data) may
+ * be NULL when the plan writes no column of that dtype. */
+int sa_vaep_features(const sa_actions* a, const sa_feature_plan* plan, const sa_block* bool_out,
+                     const sa_block* f64_out, const sa_block* i64_out, void* stream);
 
 /* goalscore alone (vaep/features.py:505-539; atomic/vaep/features.py:313-344): writes the
- * goalscore_team / _opponent / _diff columns col, col+1, col+2 of the tiled i64 block
- * `block` (n_cols columns, tile_rows rows per tile).  Also launched by sa_vaep_features
- * when the plan requests SA_XFN_GOALSCORE. */
-int sa_vaep_goalscore(const sa_actions* a, int64_t* block, int32_t n_cols, int32_t col,
-                      int64_t tile_rows, void* stream);
+ * goalscore_team / _opponent / _diff columns col, col+1, col+2 of the i64 block.  Also
+ * launched by sa_vaep_features when the plan requests SA_XFN_GOALSCORE. */
+int sa_vaep_goalscore(const sa_actions* a, const sa_block* i64_out, int32_t col, void* stream);
 
 /* Replaces labels.scores / concedes / goal_from_shot (vaep/labels.py:9-116;
  * atomic/vaep/labels.py:9-107): look-ahead of nr_actions (>=1) clamped at each

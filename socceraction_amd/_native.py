@@ -15,7 +15,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('SOCCERACTION_AMD_LIB') or os.path.join(HERE, '_lib', 'libsocceraction_amd.so')
 
 SA_MAX_FRAMES = 8
-SA_TILE_QUANTUM = 1024
+SA_BOOL_TILE_QUANTUM = 1024
+SA_NUM_TILE_QUANTUM = 128
 SA_OK, SA_EINVAL, SA_EHIP, SA_EDATA, SA_ENOMEM = 0, -1, -2, -3, -4
 
 # enum sa_xfn (order matters: mirrors include/socceraction_amd.h)
@@ -47,16 +48,21 @@ class SaFeaturePlan(ctypes.Structure):
     _fields_ = [('nb_prev_actions', ctypes.c_int32),
                 ('bool_col', ctypes.c_int32 * SA_XFN_COUNT),
                 ('f64_col', ctypes.c_int32 * SA_XFN_COUNT),
-                ('i64_col', ctypes.c_int32 * SA_XFN_COUNT),
-                ('n_bool', ctypes.c_int32), ('n_f64', ctypes.c_int32), ('n_i64', ctypes.c_int32)]
+                ('i64_col', ctypes.c_int32 * SA_XFN_COUNT)]
+
+
+class SaBlock(ctypes.Structure):
+    _fields_ = [('data', _p), ('n_cols', ctypes.c_int32), ('reserved', ctypes.c_int32),
+                ('tile_rows', ctypes.c_int64)]
 
 
 # name -> (restype, argtypes)
 _SIGNATURES = {
     'sa_vaep_features': (ctypes.c_int, [ctypes.POINTER(SaActions), ctypes.POINTER(SaFeaturePlan),
-                                        _p, _p, _p, ctypes.c_int64, _p]),
-    'sa_vaep_goalscore': (ctypes.c_int, [ctypes.POINTER(SaActions), _p, ctypes.c_int32,
-                                         ctypes.c_int32, ctypes.c_int64, _p]),
+                                        ctypes.POINTER(SaBlock), ctypes.POINTER(SaBlock),
+                                        ctypes.POINTER(SaBlock), _p]),
+    'sa_vaep_goalscore': (ctypes.c_int, [ctypes.POINTER(SaActions), ctypes.POINTER(SaBlock),
+                                         ctypes.c_int32, _p]),
     'sa_vaep_labels': (ctypes.c_int, [ctypes.POINTER(SaActions), ctypes.c_int32, _p, _p, _p,
                                       ctypes.c_int64, _p]),
     'sa_vaep_formula_f64': (ctypes.c_int, [ctypes.POINTER(SaActions), _p, _p, _p, _p, _p, _p]),

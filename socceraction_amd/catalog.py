@@ -151,7 +151,6 @@ def build_plan(xfns: Sequence[str], k: int, atomic: bool = False) -> FeaturePlan
             order.append((name, kind, base[kind][x] + slot))
     s = SaFeaturePlan()
     s.nb_prev_actions = k
-    s.n_bool, s.n_f64, s.n_i64 = count['b'], count['f'], count['i']
     for kind, arr in (('b', s.bool_col), ('f', s.f64_col), ('i', s.i64_col)):
         for j in range(SA_XFN_COUNT):
             arr[j] = -1

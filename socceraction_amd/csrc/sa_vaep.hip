@@ -44,7 +44,8 @@ struct FeatArgs {
   uint8_t* bout;
   double* fout;
   int64_t* iout;
-  int64_t R;  // rows per tile (see include/socceraction_amd.h: tiled column-major blocks)
+  int64_t Cb, Cf, Ci;  // columns of each block
+  int64_t Rb, Rf, Ri;  // rows per tile of each block (include/socceraction_amd.h)
 };
 
 // Element offset of (row j, column c) in a tiled column-major block with C columns.  A
@@ -169,7 +170,7 @@ __global__ __launch_bounds__(256) void bool_features_kernel(FeatArgs args) {
   const sa_feature_plan& P = args.p;
   const int64_t n = A.n;
   const int K = P.nb_prev_actions;
-  const int64_t R = args.R;
+  const int64_t R = args.Rb;
   const int64_t wave_base = ((int64_t)blockIdx.x * BLOCK_WAVES + wv) * BOOL_WAVE_ACTS;
   const sa_frame& F0 = A.frames[0];
   const int tcol = P.bool_col[SA_XFN_TEAM];
@@ -179,7 +180,7 @@ __global__ __launch_bounds__(256) void bool_features_kernel(FeatArgs args) {
 #pragma unroll
   for (int g = 0; g < BOOL_G; ++g) {
     j0[g] = wave_base + g * 1024 + (int64_t)lane * LANE_ACTS;
-    bb[g] = args.bout + tile_off(j0[g], 0, P.n_bool, R);
+    bb[g] = args.bout + tile_off(j0[g], 0, args.Cb, R);
   }
 
   // d = min(j - seg_start, 15) per action; rows >= n keep d = 0 (windows stay in range)
@@ -349,34 +350,247 @@ __global__ __launch_bounds__(256) void bool_features_kernel(FeatArgs args) {
 }
 
 // ------------------------------------------------------------------------------ f64/i64 block
-template <bool ATOMIC, bool EXPLICIT>
-__global__ __launch_bounds__(256) void num_features_kernel(FeatArgs args) {
+// A lane owns 2 consecutive actions (jb, jb+1); one store instruction writes 1 KiB of one
+// column, and with 128-row tiles (SA_NUM_TILE_QUANTUM) a wave's pass over 128 rows writes
+// one contiguous [C x 128] slab.
+struct NumCols {  // first column of each transformer in the f64 / i64 blocks (-1 = absent)
+  int at, re, bi, ti, tf, sl, el, sp, ep, mv, td, sd, lo, po, mp, di;
+};
+
+struct Win {  // one game-state window of the lane's 2 actions (flipped coordinates)
+  double c0[2], c1[2], c2[2], c3[2], ts[2];
+  int32_t per[2], typ[2], res[2], bp[2];
+};
+
+// Every f64 / i64 column of window i (features.py:151-499, atomic/vaep/features.py:135-310).
+template <bool ATOMIC>
+__device__ __forceinline__ void emit_window(const NumCols& C, int i, const Win& w,
+                                            const double (&sx0)[2], const double (&sy0)[2],
+                                            const double (&t0)[2], double* __restrict__ fb,
+                                            int64_t* __restrict__ ib, int64_t Rf, int64_t Ri) {
+  if (C.at >= 0) st_i64x2(ib, C.at + i, Ri, w.typ[0], w.typ[1]);
+  if (C.re >= 0) st_i64x2(ib, C.re + i, Ri, w.res[0], w.res[1]);
+  if (C.bi >= 0) st_i64x2(ib, C.bi + i, Ri, w.bp[0], w.bp[1]);
+  if (C.ti >= 0) st_i64x2(ib, C.ti + i, Ri, w.per[0], w.per[1]);
+  if (C.tf >= 0) {
+    st_f64x2(fb, C.tf + 2 * i, Rf, w.ts[0], w.ts[1]);
+    // ((period_id - 1) * 45 * 60) + time_seconds   (features.py:313)
+    st_f64x2(fb, C.tf + 2 * i + 1, Rf, (double)((w.per[0] - 1) * 2700) + w.ts[0],
+             (double)((w.per[1] - 1) * 2700) + w.ts[1]);
+  }
+  if (!ATOMIC) {
+    if (C.sl >= 0) {
+      st_f64x2(fb, C.sl + 2 * i, Rf, w.c0[0], w.c0[1]);
+      st_f64x2(fb, C.sl + 2 * i + 1, Rf, w.c1[0], w.c1[1]);
+    }
+    if (C.el >= 0) {
+      st_f64x2(fb, C.el + 2 * i, Rf, w.c2[0], w.c2[1]);
+      st_f64x2(fb, C.el + 2 * i + 1, Rf, w.c3[0], w.c3[1]);
+    }
+    if (C.sp >= 0) {
+      double dist[2], ang[2];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const double dx = fabs(FIELD_L - w.c0[e]), dy = fabs(GOAL_Y - w.c1[e]);
+        dist[e] = sqrt(dx * dx + dy * dy);
+        ang[e] = polar_angle(dy, dx);
+      }
+      st_f64x2(fb, C.sp + 2 * i, Rf, dist[0], dist[1]);
+      st_f64x2(fb, C.sp + 2 * i + 1, Rf, ang[0], ang[1]);
+    }
+    if (C.ep >= 0) {
+      double dist[2], ang[2];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const double dx = fabs(FIELD_L - w.c2[e]), dy = fabs(GOAL_Y - w.c3[e]);
+        dist[e] = sqrt(dx * dx + dy * dy);
+        ang[e] = polar_angle(dy, dx);
+      }
+      st_f64x2(fb, C.ep + 2 * i, Rf, dist[0], dist[1]);
+      st_f64x2(fb, C.ep + 2 * i + 1, Rf, ang[0], ang[1]);
+    }
+    if (C.mv >= 0) {
+      double mdx[2], mdy[2], mv[2];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        mdx[e] = w.c2[e] - w.c0[e];
+        mdy[e] = w.c3[e] - w.c1[e];
+        mv[e] = sqrt(mdx[e] * mdx[e] + mdy[e] * mdy[e]);
+      }
+      st_f64x2(fb, C.mv + 3 * i, Rf, mdx[0], mdx[1]);
+      st_f64x2(fb, C.mv + 3 * i + 1, Rf, mdy[0], mdy[1]);
+      st_f64x2(fb, C.mv + 3 * i + 2, Rf, mv[0], mv[1]);
+    }
+    if (i >= 1 && C.sd >= 0) {  // space_delta: a_i end - a0 start (features.py:491-499)
+      double sdx[2], sdy[2], sm[2];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        sdx[e] = w.c2[e] - sx0[e];
+        sdy[e] = w.c3[e] - sy0[e];
+        sm[e] = sqrt(sdx[e] * sdx[e] + sdy[e] * sdy[e]);
+      }
+      st_f64x2(fb, C.sd + 3 * (i - 1), Rf, sdx[0], sdx[1]);
+      st_f64x2(fb, C.sd + 3 * (i - 1) + 1, Rf, sdy[0], sdy[1]);
+      st_f64x2(fb, C.sd + 3 * (i - 1) + 2, Rf, sm[0], sm[1]);
+    }
+  } else {
+    if (C.lo >= 0) {
+      st_f64x2(fb, C.lo + 2 * i, Rf, w.c0[0], w.c0[1]);
+      st_f64x2(fb, C.lo + 2 * i + 1, Rf, w.c1[0], w.c1[1]);
+    }
+    if (C.po >= 0) {
+      double dist[2], ang[2];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const double dx = fabs(FIELD_L - w.c0[e]), dy = fabs(GOAL_Y - w.c1[e]);
+        dist[e] = sqrt(dx * dx + dy * dy);
+        ang[e] = polar_angle(dy, dx);
+      }
+      st_f64x2(fb, C.po + 2 * i, Rf, dist[0], dist[1]);
+      st_f64x2(fb, C.po + 2 * i + 1, Rf, ang[0], ang[1]);
+    }
+    if (C.mp >= 0) {  // atomic/vaep/features.py:279-284
+      double md[2], ma[2];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        md[e] = sqrt(w.c2[e] * w.c2[e] + w.c3[e] * w.c3[e]);
+        ma[e] = (w.c3[e] == 0.0) ? 0.0 : atan2(w.c3[e], w.c2[e]);
+      }
+      st_f64x2(fb, C.mp + 2 * i, Rf, md[0], md[1]);
+      st_f64x2(fb, C.mp + 2 * i + 1, Rf, ma[0], ma[1]);
+    }
+    if (C.di >= 0) {  // atomic/vaep/features.py:302-310
+      double ox[2], oy[2];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const double td = sqrt(w.c2[e] * w.c2[e] + w.c3[e] * w.c3[e]);
+        ox[e] = td > 0.0 ? w.c2[e] / td : w.c2[e];
+        oy[e] = td > 0.0 ? w.c3[e] / td : w.c3[e];
+      }
+      st_f64x2(fb, C.di + 2 * i, Rf, ox[0], ox[1]);
+      st_f64x2(fb, C.di + 2 * i + 1, Rf, oy[0], oy[1]);
+    }
+  }
+  if (i >= 1 && C.td >= 0)  // time_delta: a0 time - a_i time (features.py:469-473)
+    st_f64x2(fb, C.td + (i - 1), Rf, t0[0] - w.ts[0], t0[1] - w.ts[1]);
+}
+
+// play_left_to_right of one window value pair, keyed on the CURRENT action (features.py:109-115)
+template <bool ATOMIC>
+__device__ __forceinline__ void flip(Win& w, int e) {
+  w.c0[e] = FIELD_L - w.c0[e];
+  w.c1[e] = FIELD_W - w.c1[e];
+  if (ATOMIC) {
+    w.c2[e] = -w.c2[e];
+    w.c3[e] = -w.c3[e];
+  } else {
+    w.c2[e] = FIELD_L - w.c2[e];
+    w.c3[e] = FIELD_W - w.c3[e];
+  }
+}
+
+__device__ __forceinline__ void load_row(const sa_frame& F, int64_t r, bool atomic, Win& w, int e) {
+  w.c0[e] = F.c0[r];
+  w.c1[e] = F.c1[r];
+  w.c2[e] = F.c2[r];
+  w.c3[e] = F.c3[r];
+  w.ts[e] = F.time_seconds[r];
+  w.per[e] = F.period_id[r];
+  w.typ[e] = F.type_id[r];
+  w.res[e] = atomic ? 0 : F.result_id[r];
+  w.bp[e] = F.bodypart_id[r];
+}
+
+struct Row {  // one action row, raw: 5 f64 + the 4 u8 ids packed in one word
+  double c0, c1, c2, c3, ts;
+  uint32_t ids;  // period | type << 8 | result << 16 | bodypart << 24
+};
+
+__device__ __forceinline__ void load_row1(const sa_frame& F, int64_t r, bool atomic, Row& o) {
+  o.c0 = F.c0[r];
+  o.c1 = F.c1[r];
+  o.c2 = F.c2[r];
+  o.c3 = F.c3[r];
+  o.ts = F.time_seconds[r];
+  o.ids = (uint32_t)F.period_id[r] | ((uint32_t)F.type_id[r] << 8) |
+          ((uint32_t)(atomic ? 0 : F.result_id[r]) << 16) | ((uint32_t)F.bodypart_id[r] << 24);
+}
+
+// rows r, r+1 (r even: 16-B aligned f64 pairs, 2-B aligned id pairs)
+__device__ __forceinline__ void load_pair(const sa_frame& F, int64_t r, bool atomic, Row& a, Row& b) {
+  const f64x2 x0 = *reinterpret_cast<const f64x2*>(F.c0 + r);
+  const f64x2 x1 = *reinterpret_cast<const f64x2*>(F.c1 + r);
+  const f64x2 x2 = *reinterpret_cast<const f64x2*>(F.c2 + r);
+  const f64x2 x3 = *reinterpret_cast<const f64x2*>(F.c3 + r);
+  const f64x2 x4 = *reinterpret_cast<const f64x2*>(F.time_seconds + r);
+  const uint32_t pe = *reinterpret_cast<const uint16_t*>(F.period_id + r);
+  const uint32_t ty = *reinterpret_cast<const uint16_t*>(F.type_id + r);
+  const uint32_t rs = atomic ? 0u : *reinterpret_cast<const uint16_t*>(F.result_id + r);
+  const uint32_t bo = *reinterpret_cast<const uint16_t*>(F.bodypart_id + r);
+  a = Row{x0[0], x1[0], x2[0], x3[0], x4[0],
+          (pe & 0xFF) | ((ty & 0xFF) << 8) | ((rs & 0xFF) << 16) | ((bo & 0xFF) << 24)};
+  b = Row{x0[1], x1[1], x2[1], x3[1], x4[1],
+          (pe >> 8) | ((ty >> 8) << 8) | ((rs >> 8) << 16) | ((bo >> 8) << 24)};
+}
+
+__device__ __forceinline__ void row_to_win(const Row& r, Win& w, int e) {
+  w.c0[e] = r.c0;
+  w.c1[e] = r.c1;
+  w.c2[e] = r.c2;
+  w.c3[e] = r.c3;
+  w.ts[e] = r.ts;
+  w.per[e] = r.ids & 0xFF;
+  w.typ[e] = (r.ids >> 8) & 0xFF;
+  w.res[e] = (r.ids >> 16) & 0xFF;
+  w.bp[e] = r.ids >> 24;
+}
+
+// KF = 3: windowed mode with nb_prev_actions <= 3.  The pair's rows jb-2 .. jb+1 are read
+// once (16-B loads) and the windows are formed in registers (see the loop below).
+// KF = 0: any mode / any k (explicit frames, k <= 8): per-window row loads.
+#ifndef SA_NUM_FAST
+#define SA_NUM_FAST 1
+#endif
+#ifndef SA_NUM_MINWAVES
+#define SA_NUM_MINWAVES 1
+#endif
+template <bool ATOMIC, bool EXPLICIT, int KF>
+__global__ __launch_bounds__(256, SA_NUM_MINWAVES) void num_features_kernel(FeatArgs args) {
   const int lane = threadIdx.x & (WAVE - 1);
   const int wv = threadIdx.x / WAVE;
   const sa_actions& A = args.a;
   const sa_feature_plan& P = args.p;
   const int64_t n = A.n;
   const int K = P.nb_prev_actions;
-  const int64_t R = args.R;
+  const int64_t Rf = args.Rf, Ri = args.Ri;
   const int64_t wave_base = ((int64_t)blockIdx.x * BLOCK_WAVES + wv) * WAVE_ACTS;
   const sa_frame& F0 = A.frames[0];
   if (wave_base + 2 * lane >= n) return;
   SegCursor cur = {0, 0, 0};
   if (!EXPLICIT) cur = seg_at(A, wave_base + 2 * lane);
-  const int c_at = P.i64_col[SA_XFN_ACTIONTYPE], c_re = P.i64_col[SA_XFN_RESULT],
-            c_bi = P.i64_col[SA_XFN_BODYPART], c_ti = P.i64_col[SA_XFN_TIME],
-            c_tf = P.f64_col[SA_XFN_TIME], c_sl = P.f64_col[SA_XFN_STARTLOCATION],
-            c_el = P.f64_col[SA_XFN_ENDLOCATION], c_sp = P.f64_col[SA_XFN_STARTPOLAR],
-            c_ep = P.f64_col[SA_XFN_ENDPOLAR], c_mv = P.f64_col[SA_XFN_MOVEMENT],
-            c_td = P.f64_col[SA_XFN_TIME_DELTA], c_sd = P.f64_col[SA_XFN_SPACE_DELTA],
-            c_lo = P.f64_col[SA_XFN_LOCATION], c_po = P.f64_col[SA_XFN_POLAR],
-            c_mp = P.f64_col[SA_XFN_MOVEMENT_POLAR], c_di = P.f64_col[SA_XFN_DIRECTION];
+  NumCols C;
+  C.at = P.i64_col[SA_XFN_ACTIONTYPE];
+  C.re = P.i64_col[SA_XFN_RESULT];
+  C.bi = P.i64_col[SA_XFN_BODYPART];
+  C.ti = P.i64_col[SA_XFN_TIME];
+  C.tf = P.f64_col[SA_XFN_TIME];
+  C.sl = P.f64_col[SA_XFN_STARTLOCATION];
+  C.el = P.f64_col[SA_XFN_ENDLOCATION];
+  C.sp = P.f64_col[SA_XFN_STARTPOLAR];
+  C.ep = P.f64_col[SA_XFN_ENDPOLAR];
+  C.mv = P.f64_col[SA_XFN_MOVEMENT];
+  C.td = P.f64_col[SA_XFN_TIME_DELTA];
+  C.sd = P.f64_col[SA_XFN_SPACE_DELTA];
+  C.lo = P.f64_col[SA_XFN_LOCATION];
+  C.po = P.f64_col[SA_XFN_POLAR];
+  C.mp = P.f64_col[SA_XFN_MOVEMENT_POLAR];
+  C.di = P.f64_col[SA_XFN_DIRECTION];
 
   for (int pr = 0; pr < NUM_PAIRS; ++pr) {
     const int64_t jb = wave_base + pr * 2 * WAVE + 2 * lane;
     if (jb >= n) break;
-    double* fb = args.fout + tile_off(jb, 0, P.n_f64, R);      // column 0 of rows jb, jb+1
-    int64_t* ib = args.iout + tile_off(jb, 0, P.n_i64, R);
+    double* fb = args.fout + tile_off(jb, 0, args.Cf, Rf);  // column 0 of rows jb, jb+1
+    int64_t* ib = args.iout + tile_off(jb, 0, args.Ci, Ri);
     int64_t jr[2];
     int dd[2];
     bool away[2];
@@ -394,144 +608,63 @@ __global__ __launch_bounds__(256) void num_features_kernel(FeatArgs args) {
       }
     }
     double sx0[2], sy0[2], t0[2];
-    for (int i = 0; i < K; ++i) {
-      const sa_frame& Fi = EXPLICIT ? A.frames[i] : F0;
-      double c0[2], c1[2], c2[2], c3[2], ts[2];
-      int32_t per[2], typ[2], res[2], bp[2];
+    if (KF == 3) {
+      // Rows of the pair's windows: cand = current window rows of actions 0/1 (raw),
+      // pool = the next older rows jb-1, jb-2.  Moving from window i-1 to i, action 1 takes
+      // action 0's previous row and action 0 takes the next pool row, unless the action's
+      // window already reached its segment start (d < i): then it keeps its row.  (If
+      // action 0 is clamped so is action 1, whose d is at most d0 + 1.)
+      Row cand[2], pool[2];
+      if (jb >= 2 && jb + 2 <= n) {
+        load_pair(F0, jb, ATOMIC, cand[0], cand[1]);
+        load_pair(F0, jb - 2, ATOMIC, pool[1], pool[0]);
+      } else {  // first rows of the batch or the tail: guarded scalar loads
+        load_row1(F0, jr[0], ATOMIC, cand[0]);
+        load_row1(F0, jr[1], ATOMIC, cand[1]);
+        load_row1(F0, jb - 1 < 0 ? 0 : jb - 1, ATOMIC, pool[0]);
+        load_row1(F0, jb - 2 < 0 ? 0 : jb - 2, ATOMIC, pool[1]);
+      }
+#pragma unroll 1
+      for (int i = 0; i < K; ++i) {
+        if (i > 0) {
+          const Row prev0 = cand[0];
+          if (dd[1] >= i) cand[1] = prev0;
+          if (dd[0] >= i) cand[0] = pool[0];
+          pool[0] = pool[1];
+        }
+        Win wf;
 #pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        const int64_t r = EXPLICIT ? jr[e] : jr[e] - (dd[e] < i ? dd[e] : i);
-        c0[e] = Fi.c0[r];
-        c1[e] = Fi.c1[r];
-        c2[e] = Fi.c2[r];
-        c3[e] = Fi.c3[r];
-        ts[e] = Fi.time_seconds[r];
-        per[e] = Fi.period_id[r];
-        typ[e] = Fi.type_id[r];
-        res[e] = ATOMIC ? 0 : Fi.result_id[r];
-        bp[e] = Fi.bodypart_id[r];
-        if (!EXPLICIT && away[e]) {  // play_left_to_right, keyed on the CURRENT action
-          c0[e] = FIELD_L - c0[e];
-          c1[e] = FIELD_W - c1[e];
-          if (ATOMIC) {
-            c2[e] = -c2[e];
-            c3[e] = -c3[e];
-          } else {
-            c2[e] = FIELD_L - c2[e];
-            c3[e] = FIELD_W - c3[e];
-          }
+        for (int e = 0; e < 2; ++e) {
+          row_to_win(cand[e], wf, e);
+          if (!EXPLICIT && away[e]) flip<ATOMIC>(wf, e);
         }
         if (i == 0) {
-          sx0[e] = c0[e];
-          sy0[e] = c1[e];
-          t0[e] = ts[e];
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            sx0[e] = wf.c0[e];
+            sy0[e] = wf.c1[e];
+            t0[e] = wf.ts[e];
+          }
         }
+        emit_window<ATOMIC>(C, i, wf, sx0, sy0, t0, fb, ib, Rf, Ri);
       }
-      if (c_at >= 0) st_i64x2(ib, c_at + i, R, typ[0], typ[1]);
-      if (c_re >= 0) st_i64x2(ib, c_re + i, R, res[0], res[1]);
-      if (c_bi >= 0) st_i64x2(ib, c_bi + i, R, bp[0], bp[1]);
-      if (c_ti >= 0) st_i64x2(ib, c_ti + i, R, per[0], per[1]);
-      if (c_tf >= 0) {
-        st_f64x2(fb, c_tf + 2 * i, R, ts[0], ts[1]);
-        // ((period_id - 1) * 45 * 60) + time_seconds   (features.py:313)
-        st_f64x2(fb, c_tf + 2 * i + 1, R, (double)((per[0] - 1) * 2700) + ts[0],
-                 (double)((per[1] - 1) * 2700) + ts[1]);
+    } else {
+      for (int i = 0; i < K; ++i) {
+        const sa_frame& Fi = EXPLICIT ? A.frames[i] : F0;
+        Win w;
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const int64_t r = EXPLICIT ? jr[e] : jr[e] - (dd[e] < i ? dd[e] : i);
+          load_row(Fi, r, ATOMIC, w, e);
+          if (!EXPLICIT && away[e]) flip<ATOMIC>(w, e);
+          if (i == 0) {
+            sx0[e] = w.c0[e];
+            sy0[e] = w.c1[e];
+            t0[e] = w.ts[e];
+          }
+        }
+        emit_window<ATOMIC>(C, i, w, sx0, sy0, t0, fb, ib, Rf, Ri);
       }
-      if (!ATOMIC) {
-        if (c_sl >= 0) {
-          st_f64x2(fb, c_sl + 2 * i, R, c0[0], c0[1]);
-          st_f64x2(fb, c_sl + 2 * i + 1, R, c1[0], c1[1]);
-        }
-        if (c_el >= 0) {
-          st_f64x2(fb, c_el + 2 * i, R, c2[0], c2[1]);
-          st_f64x2(fb, c_el + 2 * i + 1, R, c3[0], c3[1]);
-        }
-        if (c_sp >= 0) {
-          double dist[2], ang[2];
-#pragma unroll
-          for (int e = 0; e < 2; ++e) {
-            const double dx = fabs(FIELD_L - c0[e]), dy = fabs(GOAL_Y - c1[e]);
-            dist[e] = sqrt(dx * dx + dy * dy);
-            ang[e] = polar_angle(dy, dx);
-          }
-          st_f64x2(fb, c_sp + 2 * i, R, dist[0], dist[1]);
-          st_f64x2(fb, c_sp + 2 * i + 1, R, ang[0], ang[1]);
-        }
-        if (c_ep >= 0) {
-          double dist[2], ang[2];
-#pragma unroll
-          for (int e = 0; e < 2; ++e) {
-            const double dx = fabs(FIELD_L - c2[e]), dy = fabs(GOAL_Y - c3[e]);
-            dist[e] = sqrt(dx * dx + dy * dy);
-            ang[e] = polar_angle(dy, dx);
-          }
-          st_f64x2(fb, c_ep + 2 * i, R, dist[0], dist[1]);
-          st_f64x2(fb, c_ep + 2 * i + 1, R, ang[0], ang[1]);
-        }
-        if (c_mv >= 0) {
-          double mdx[2], mdy[2], mv[2];
-#pragma unroll
-          for (int e = 0; e < 2; ++e) {
-            mdx[e] = c2[e] - c0[e];
-            mdy[e] = c3[e] - c1[e];
-            mv[e] = sqrt(mdx[e] * mdx[e] + mdy[e] * mdy[e]);
-          }
-          st_f64x2(fb, c_mv + 3 * i, R, mdx[0], mdx[1]);
-          st_f64x2(fb, c_mv + 3 * i + 1, R, mdy[0], mdy[1]);
-          st_f64x2(fb, c_mv + 3 * i + 2, R, mv[0], mv[1]);
-        }
-        if (i >= 1 && c_sd >= 0) {  // space_delta: a_i end - a0 start (features.py:491-499)
-          double sdx[2], sdy[2], sm[2];
-#pragma unroll
-          for (int e = 0; e < 2; ++e) {
-            sdx[e] = c2[e] - sx0[e];
-            sdy[e] = c3[e] - sy0[e];
-            sm[e] = sqrt(sdx[e] * sdx[e] + sdy[e] * sdy[e]);
-          }
-          st_f64x2(fb, c_sd + 3 * (i - 1), R, sdx[0], sdx[1]);
-          st_f64x2(fb, c_sd + 3 * (i - 1) + 1, R, sdy[0], sdy[1]);
-          st_f64x2(fb, c_sd + 3 * (i - 1) + 2, R, sm[0], sm[1]);
-        }
-      } else {
-        if (c_lo >= 0) {
-          st_f64x2(fb, c_lo + 2 * i, R, c0[0], c0[1]);
-          st_f64x2(fb, c_lo + 2 * i + 1, R, c1[0], c1[1]);
-        }
-        if (c_po >= 0) {
-          double dist[2], ang[2];
-#pragma unroll
-          for (int e = 0; e < 2; ++e) {
-            const double dx = fabs(FIELD_L - c0[e]), dy = fabs(GOAL_Y - c1[e]);
-            dist[e] = sqrt(dx * dx + dy * dy);
-            ang[e] = polar_angle(dy, dx);
-          }
-          st_f64x2(fb, c_po + 2 * i, R, dist[0], dist[1]);
-          st_f64x2(fb, c_po + 2 * i + 1, R, ang[0], ang[1]);
-        }
-        if (c_mp >= 0) {  // atomic/vaep/features.py:279-284
-          double md[2], ma[2];
-#pragma unroll
-          for (int e = 0; e < 2; ++e) {
-            md[e] = sqrt(c2[e] * c2[e] + c3[e] * c3[e]);
-            ma[e] = (c3[e] == 0.0) ? 0.0 : atan2(c3[e], c2[e]);
-          }
-          st_f64x2(fb, c_mp + 2 * i, R, md[0], md[1]);
-          st_f64x2(fb, c_mp + 2 * i + 1, R, ma[0], ma[1]);
-        }
-        if (c_di >= 0) {  // atomic/vaep/features.py:302-310
-          double ox[2], oy[2];
-#pragma unroll
-          for (int e = 0; e < 2; ++e) {
-            const double td = sqrt(c2[e] * c2[e] + c3[e] * c3[e]);
-            ox[e] = td > 0.0 ? c2[e] / td : c2[e];
-            oy[e] = td > 0.0 ? c3[e] / td : c3[e];
-          }
-          st_f64x2(fb, c_di + 2 * i, R, ox[0], ox[1]);
-          st_f64x2(fb, c_di + 2 * i + 1, R, oy[0], oy[1]);
-        }
-      }
-      if (i >= 1 && c_td >= 0)  // time_delta: a0 time - a_i time (features.py:469-473)
-        st_f64x2(fb, c_td + (i - 1), R, t0[0] - ts[0], t0[1] - ts[1]);
     }
   }
 }
@@ -827,16 +960,22 @@ static int check_actions(const sa_actions* a, bool allow_explicit) {
   return SA_OK;
 }
 
-static int check_tile_rows(int64_t R, int64_t n) {
+static int check_block(const sa_block* b, int64_t n, int64_t quantum, const char* what) {
   const int64_t n16 = ((n + 15) / 16) * 16;
-  if (R <= 0 || R % 16 != 0 || (R < n16 && R % SA_TILE_QUANTUM != 0))
-    return fail(SA_EINVAL, "tile_rows must be a multiple of 16 and either >= round_up(n, 16) "
-                           "or a multiple of %d", SA_TILE_QUANTUM);
+  if (!b || !b->data) return fail(SA_EINVAL, "%s block is null", what);
+  if (!aligned16(b->data)) return fail(SA_EINVAL, "%s block must be 16-byte aligned", what);
+  if (b->n_cols < 0) return fail(SA_EINVAL, "%s block has a negative column count", what);
+  const int64_t R = b->tile_rows;
+  if (R <= 0 || R % 16 != 0 || (R < n16 && R % quantum != 0))
+    return fail(SA_EINVAL,
+                "%s block: tile_rows must be a multiple of 16 and either >= round_up(n, 16) or a "
+                "multiple of %lld", what, (long long)quantum);
   return SA_OK;
 }
 
-extern "C" int sa_vaep_features(const sa_actions* a, const sa_feature_plan* plan, uint8_t* bool_out,
-                                double* f64_out, int64_t* i64_out, int64_t tile_rows, void* stream) {
+extern "C" int sa_vaep_features(const sa_actions* a, const sa_feature_plan* plan,
+                                const sa_block* bool_out, const sa_block* f64_out,
+                                const sa_block* i64_out, void* stream) {
   int rc = check_actions(a, true);
   if (rc) return rc;
   if (!plan) return fail(SA_EINVAL, "null plan");
@@ -844,19 +983,20 @@ extern "C" int sa_vaep_features(const sa_actions* a, const sa_feature_plan* plan
   if (K < 1 || K > SA_MAX_FRAMES) return fail(SA_EINVAL, "nb_prev_actions must be in [1, 8]");
   if (a->n_frames > 1 && a->n_frames != K)
     return fail(SA_EINVAL, "explicit mode needs n_frames == nb_prev_actions");
-  rc = check_tile_rows(tile_rows, a->n);
-  if (rc) return rc;
-  if (!aligned16(bool_out) || !aligned16(f64_out) || !aligned16(i64_out))
-    return fail(SA_EINVAL, "output blocks must be 16-byte aligned");
-  bool wb = false, wn = false;
+  bool wb = false, wf = false, wi = false, wn = false;
   for (int x = 0; x < SA_XFN_COUNT; ++x) {
     wb |= plan->bool_col[x] >= 0;
+    wf |= plan->f64_col[x] >= 0;
+    wi |= plan->i64_col[x] >= 0;
     wn |= plan->f64_col[x] >= 0 || (plan->i64_col[x] >= 0 && x != SA_XFN_GOALSCORE);
   }
+  if (wb && (rc = check_block(bool_out, a->n, SA_BOOL_TILE_QUANTUM, "bool"))) return rc;
+  if (wf && (rc = check_block(f64_out, a->n, SA_NUM_TILE_QUANTUM, "f64"))) return rc;
+  if (wi && (rc = check_block(i64_out, a->n, SA_NUM_TILE_QUANTUM, "i64"))) return rc;
   for (int x = 0; x < SA_XFN_COUNT; ++x) {
-    if ((plan->bool_col[x] >= 0 && !bool_out) || (plan->f64_col[x] >= 0 && !f64_out) ||
-        (plan->i64_col[x] >= 0 && !i64_out))
-      return fail(SA_EINVAL, "plan writes a block whose pointer is null");
+    if ((wb && plan->bool_col[x] >= bool_out->n_cols) || (wf && plan->f64_col[x] >= f64_out->n_cols) ||
+        (wi && plan->i64_col[x] >= i64_out->n_cols))
+      return fail(SA_EINVAL, "plan column offset beyond the block's column count");
   }
   if (a->atomic) {
     const int spadl_only[] = {SA_XFN_RESULT, SA_XFN_RESULT_ONEHOT, SA_XFN_ACTIONTYPE_RESULT_ONEHOT,
@@ -873,12 +1013,17 @@ extern "C" int sa_vaep_features(const sa_actions* a, const sa_feature_plan* plan
   }
   if (a->n == 0) return SA_OK;
   hipStream_t st = (hipStream_t)stream;
-  for (int x = 0; x < SA_XFN_COUNT; ++x) {
-    if (plan->bool_col[x] >= plan->n_bool || plan->f64_col[x] >= plan->n_f64 ||
-        plan->i64_col[x] >= plan->n_i64)
-      return fail(SA_EINVAL, "plan column offset beyond the block's column count");
-  }
-  FeatArgs args{*a, *plan, bool_out, f64_out, i64_out, tile_rows};
+  FeatArgs args{*a,
+                *plan,
+                wb ? (uint8_t*)bool_out->data : nullptr,
+                wf ? (double*)f64_out->data : nullptr,
+                wi ? (int64_t*)i64_out->data : nullptr,
+                wb ? bool_out->n_cols : 0,
+                wf ? f64_out->n_cols : 0,
+                wi ? i64_out->n_cols : 0,
+                wb ? bool_out->tile_rows : 16,
+                wf ? f64_out->tile_rows : 16,
+                wi ? i64_out->tile_rows : 16};
   const dim3 grid((unsigned)((a->n + BLOCK_ACTS - 1) / BLOCK_ACTS)), block(BLOCK_WAVES * WAVE);
   const dim3 bgrid((unsigned)((a->n + BOOL_BLOCK_ACTS - 1) / BOOL_BLOCK_ACTS));
   const bool expl = a->n_frames > 1;
@@ -898,41 +1043,45 @@ extern "C" int sa_vaep_features(const sa_actions* a, const sa_feature_plan* plan
     if (rc) return rc;
   }
   if (wn) {
+    const bool fast = SA_NUM_FAST && !expl && K <= 3;  // register-resident windows (KF = 3)
     if (a->atomic) {
       if (expl)
-        hipLaunchKernelGGL((num_features_kernel<true, true>), grid, block, 0, st, args);
+        hipLaunchKernelGGL((num_features_kernel<true, true, 0>), grid, block, 0, st, args);
+      else if (fast)
+        hipLaunchKernelGGL((num_features_kernel<true, false, 3>), grid, block, 0, st, args);
       else
-        hipLaunchKernelGGL((num_features_kernel<true, false>), grid, block, 0, st, args);
+        hipLaunchKernelGGL((num_features_kernel<true, false, 0>), grid, block, 0, st, args);
     } else {
       if (expl)
-        hipLaunchKernelGGL((num_features_kernel<false, true>), grid, block, 0, st, args);
+        hipLaunchKernelGGL((num_features_kernel<false, true, 0>), grid, block, 0, st, args);
+      else if (fast)
+        hipLaunchKernelGGL((num_features_kernel<false, false, 3>), grid, block, 0, st, args);
       else
-        hipLaunchKernelGGL((num_features_kernel<false, false>), grid, block, 0, st, args);
+        hipLaunchKernelGGL((num_features_kernel<false, false, 0>), grid, block, 0, st, args);
     }
     rc = check_launch("num_features_kernel");
     if (rc) return rc;
   }
   const int gc = plan->i64_col[SA_XFN_GOALSCORE];
-  if (gc >= 0) rc = sa_vaep_goalscore(a, i64_out, plan->n_i64, gc, tile_rows, stream);
+  if (gc >= 0) rc = sa_vaep_goalscore(a, i64_out, gc, stream);
   return rc;
 }
 
-extern "C" int sa_vaep_goalscore(const sa_actions* a, int64_t* block, int32_t n_cols, int32_t col,
-                                 int64_t tile_rows, void* stream) {
+extern "C" int sa_vaep_goalscore(const sa_actions* a, const sa_block* i64_out, int32_t col,
+                                 void* stream) {
   int rc = check_actions(a, true);
   if (rc) return rc;
-  if (!block) return fail(SA_EINVAL, "null goalscore output");
-  if (col < 0 || col + 3 > n_cols) return fail(SA_EINVAL, "goalscore columns outside the block");
-  rc = check_tile_rows(tile_rows, a->n);
-  if (rc) return rc;
+  if ((rc = check_block(i64_out, a->n, SA_NUM_TILE_QUANTUM, "i64"))) return rc;
+  if (col < 0 || col + 3 > i64_out->n_cols) return fail(SA_EINVAL, "goalscore columns outside the block");
   if (a->n == 0) return SA_OK;
   hipStream_t st = (hipStream_t)stream;
+  int64_t* blk = (int64_t*)i64_out->data;
   if (a->atomic)
     hipLaunchKernelGGL((goalscore_kernel<true>), dim3((unsigned)a->n_segments), dim3(GS_THREADS), 0, st,
-                       *a, block, (int64_t)n_cols, (int64_t)col, tile_rows);
+                       *a, blk, (int64_t)i64_out->n_cols, (int64_t)col, i64_out->tile_rows);
   else
     hipLaunchKernelGGL((goalscore_kernel<false>), dim3((unsigned)a->n_segments), dim3(GS_THREADS), 0,
-                       st, *a, block, (int64_t)n_cols, (int64_t)col, tile_rows);
+                       st, *a, blk, (int64_t)i64_out->n_cols, (int64_t)col, i64_out->tile_rows);
   return check_launch("goalscore_kernel");
 }
 

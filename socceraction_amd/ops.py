@@ -26,19 +26,17 @@ def _ld(n: int) -> int:
 @dataclass
 class FeatureBlocks:
     """Feature blocks in HBM, one per dtype, in the tiled column-major layout of
-    ``include/socceraction_amd.h``: tensors ``[n_tiles, n_cols, R]`` (R = rows per tile;
-    one tile of R >= n rows is plain column-major)."""
+    ``include/socceraction_amd.h``: tensors ``[n_tiles, n_cols, R]`` (R = rows per tile; a
+    single tile of R >= n rows is plain column-major). ``Rb`` is the bool block's tile,
+    ``Rn`` the f64 / i64 blocks' tile."""
 
     plan: FeaturePlan
     n: int
-    R: int
+    Rb: int
+    Rn: int
     bool_block: torch.Tensor
     f64_block: torch.Tensor
     i64_block: torch.Tensor
-
-    @property
-    def ld(self) -> int:  # single-tile leading dimension (kept for callers of the plain layout)
-        return self.R
 
     def _blk(self, kind: str) -> torch.Tensor:
         return {'b': self.bool_block, 'f': self.f64_block, 'i': self.i64_block}[kind]
@@ -61,16 +59,29 @@ class FeatureBlocks:
         b, f, i = self.to_numpy()
         return assemble_frame(self.plan, b, f, i, self.n, index)
 
+    def sa_blocks(self):
+        """The three ``sa_block`` descriptors of the C ABI."""
+        out = []
+        for t, R in ((self.bool_block, self.Rb), (self.f64_block, self.Rn),
+                     (self.i64_block, self.Rn)):
+            b = _native.SaBlock()
+            b.data = _ptr(t)
+            b.n_cols = t.shape[1]
+            b.tile_rows = R
+            out.append(b)
+        return out
 
-def alloc_feature_blocks(plan: FeaturePlan, n: int, dev, tile_rows: Optional[int] = None
-                         ) -> FeatureBlocks:
-    """Allocate the three blocks; ``tile_rows=None`` = one tile (plain column-major)."""
-    R = _ld(n) if tile_rows is None else int(tile_rows)
-    tiles = max(1, -(-n // R))
-    return FeatureBlocks(plan, n, R,
-                         torch.empty((tiles, plan.n_bool, R), dtype=torch.uint8, device=dev),
-                         torch.empty((tiles, plan.n_f64, R), dtype=torch.float64, device=dev),
-                         torch.empty((tiles, plan.n_i64, R), dtype=torch.int64, device=dev))
+
+def alloc_feature_blocks(plan: FeaturePlan, n: int, dev, bool_tile: Optional[int] = None,
+                         num_tile: Optional[int] = None) -> FeatureBlocks:
+    """Allocate the three blocks; a ``None`` tile = one tile (plain column-major)."""
+    Rb = _ld(n) if bool_tile is None else int(bool_tile)
+    Rn = _ld(n) if num_tile is None else int(num_tile)
+    tb, tn = max(1, -(-n // Rb)), max(1, -(-n // Rn))
+    return FeatureBlocks(plan, n, Rb, Rn,
+                         torch.empty((tb, plan.n_bool, Rb), dtype=torch.uint8, device=dev),
+                         torch.empty((tn, plan.n_f64, Rn), dtype=torch.float64, device=dev),
+                         torch.empty((tn, plan.n_i64, Rn), dtype=torch.int64, device=dev))
 
 
 def _ptr(t: Optional[torch.Tensor]):
@@ -78,18 +89,18 @@ def _ptr(t: Optional[torch.Tensor]):
 
 
 def features_into(s: _native.SaActions, out: FeatureBlocks) -> None:
-    lib = _native.lib()
-    _native.check(lib.sa_vaep_features(ctypes.byref(s), ctypes.byref(out.plan.struct),
-                                       _ptr(out.bool_block), _ptr(out.f64_block),
-                                       _ptr(out.i64_block), out.R, stream_handle()))
+    bb, fb, ib = out.sa_blocks()
+    _native.check(_native.lib().sa_vaep_features(ctypes.byref(s), ctypes.byref(out.plan.struct),
+                                                 ctypes.byref(bb), ctypes.byref(fb),
+                                                 ctypes.byref(ib), stream_handle()))
 
 
 def features(batch: ActionBatch, xfns: Sequence[str], k: int, flip: bool = True,
-             out: Optional[FeatureBlocks] = None, tile_rows: Optional[int] = None
-             ) -> FeatureBlocks:
+             out: Optional[FeatureBlocks] = None, bool_tile: Optional[int] = None,
+             num_tile: Optional[int] = None) -> FeatureBlocks:
     """Game-state features of every segment of ``batch`` (windowed mode)."""
     plan = out.plan if out is not None else build_plan(xfns, k, batch.atomic)
-    out = out or alloc_feature_blocks(plan, batch.n, batch.device, tile_rows)
+    out = out or alloc_feature_blocks(plan, batch.n, batch.device, bool_tile, num_tile)
     features_into(batch.struct(flip=flip), out)
     return out
 
@@ -266,5 +277,6 @@ def goalscore_into(batch: ActionBatch, out: FeatureBlocks) -> None:
     if gc < 0:
         raise ValueError('plan has no goalscore columns')
     s = batch.struct()
-    _native.check(_native.lib().sa_vaep_goalscore(ctypes.byref(s), _ptr(out.i64_block),
-                                                  out.plan.n_i64, gc, out.R, stream_handle()))
+    ib = out.sa_blocks()[2]
+    _native.check(_native.lib().sa_vaep_goalscore(ctypes.byref(s), ctypes.byref(ib), gc,
+                                                  stream_handle()))

@@ -40,7 +40,8 @@ def test_ctypes_struct_layout_matches_header():
     from socceraction_amd import _native
     assert ctypes.sizeof(_native.SaFrame) == 80
     assert ctypes.sizeof(_native.SaActions) == 40 + 8 * 80
-    assert ctypes.sizeof(_native.SaFeaturePlan) == 4 * (1 + 3 * _native.SA_XFN_COUNT + 3)
+    assert ctypes.sizeof(_native.SaFeaturePlan) == 4 * (1 + 3 * _native.SA_XFN_COUNT)
+    assert ctypes.sizeof(_native.SaBlock) == 24
     with open(os.path.join(ROOT, 'include', 'socceraction_amd.h')) as f:
         enum = f.read().split('enum sa_xfn {')[1].split('};')[0]
     names = re.findall(r'SA_XFN_([A-Z_]+)', enum)
@@ -56,7 +57,7 @@ def test_invalid_arguments_are_rejected_without_a_gpu():
     s = _native.SaActions()
     s.n, s.n_segments, s.n_frames = 10, 1, 0
     plan = _native.SaFeaturePlan()
-    rc = lib.sa_vaep_features(ctypes.byref(s), ctypes.byref(plan), None, None, None, 16, None)
+    rc = lib.sa_vaep_features(ctypes.byref(s), ctypes.byref(plan), None, None, None, None)
     assert rc == _native.SA_EINVAL
     assert b'n_frames' in lib.sa_last_error()
     with pytest.raises(ValueError):

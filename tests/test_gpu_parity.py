@@ -90,7 +90,7 @@ def test_batched_segments_match_per_game(sa, atomic):
     homes = [g['home_team_id'][0] for g in gs]
     ab = B.ActionBatch.from_frame(df, atomic=atomic, home_team_id=homes, segments='game')
     assert ab.n_segments == len(gs)
-    fb = ops.features(ab, default, 3, tile_rows=1024)  # tiled layout, several tiles
+    fb = ops.features(ab, default, 3, bool_tile=1024, num_tile=128)  # tiled, several tiles
     assert fb.bool_block.shape[0] == -(-ab.n // 1024)
     lb = ops.labels(ab)
     ps = torch.tensor(np.concatenate([g['ps'] for g in gs]), device=ab.device)
@@ -126,12 +126,14 @@ def test_tiled_and_plain_layouts_agree(sa):
     plain = ops.features(ab, vo.SPADL_DEFAULT, 3)
     assert plain.bool_block.shape[0] == 1
     ref = plain.to_numpy()
-    for R in (1024, 2048):
-        tiled = ops.features(ab, vo.SPADL_DEFAULT, 3, tile_rows=R)
+    for Rb, Rn in ((1024, 128), (2048, 1024), (1024, None), (None, 256)):
+        tiled = ops.features(ab, vo.SPADL_DEFAULT, 3, bool_tile=Rb, num_tile=Rn)
         for a, b in zip(tiled.to_numpy(), ref):
             np.testing.assert_array_equal(a, b)
     with pytest.raises(ValueError):
-        ops.features(ab, vo.SPADL_DEFAULT, 3, tile_rows=1000)
+        ops.features(ab, vo.SPADL_DEFAULT, 3, bool_tile=1000)
+    with pytest.raises(ValueError):
+        ops.features(ab, vo.SPADL_DEFAULT, 3, num_tile=100)
 
 
 def test_explicit_frames_match_windowed(sa):
@@ -196,7 +198,7 @@ def test_full_size_sampled_games_vs_oracle(sa):
     B, ops, syn = sa['batch'], sa['ops'], sa['synthetic']
     d = syn.spadl_games(10000)
     ab = B.ActionBatch.from_columns(d)
-    fb = ops.features(ab, vo.SPADL_DEFAULT, 3, tile_rows=1024)
+    fb = ops.features(ab, vo.SPADL_DEFAULT, 3, bool_tile=1024, num_tile=128)
     lb = ops.labels(ab)
     p = syn.probabilities(ab.n)
     ps = torch.from_numpy(p['scores']).to(ab.device)
