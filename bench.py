@@ -45,14 +45,52 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 
 def _dist():
+    """One process per GPU (torch.distributed.run); backend nccl = RCCL over xGMI.
+    SA_DIST_BACKEND=gloo is for rehearsing several ranks on one GPU."""
     ws = int(os.environ.get('WORLD_SIZE', '1'))
     if ws > 1:
         import torch.distributed as dist
         lr = int(os.environ.get('LOCAL_RANK', '0'))
-        torch.cuda.set_device(lr)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', lr))
+        backend = os.environ.get('SA_DIST_BACKEND', 'nccl')
+        torch.cuda.set_device(lr % max(1, torch.cuda.device_count()))
+        if backend == 'nccl':
+            dist.init_process_group('nccl', device_id=torch.device('cuda', lr))
+        else:
+            dist.init_process_group(backend)
         return dist, dist.get_rank(), ws
     return None, 0, 1
+
+
+def _reduce(dist, value, op, dev):
+    """All-reduce one scalar (RCCL on device tensors; gloo on host tensors)."""
+    on_dev = dist.get_backend() == 'nccl'
+    t = torch.tensor([value], dtype=torch.float64, device=dev if on_dev else 'cpu')
+    dist.all_reduce(t, op=op)
+    return float(t.item())
+
+
+def xt_extra(d, ab, dist, dev, reps: int = 3) -> dict:
+    """BASELINE cfg4 alongside the main line: xT 16x12 fit (count pass + RCCL all-reduce of
+    the counts when several ranks + value iteration to eps=1e-5) and rate over the batch."""
+    from socceraction_amd import shard
+    def once():
+        acc = ops.xt_count(ab, 16, 12)
+        if dist is not None:
+            if dist.get_backend() == 'nccl':
+                shard.allreduce_xt_counts(acc.shot, acc.goal, acc.move, acc.trans, acc.err)
+        sol = ops.xt_solve(acc)  # synchronises
+        out, _ = ops.xt_rate(ab, sol.mats[3].reshape(12, 16), 16, 12)
+        return sol, out
+    once()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        sol, _ = once()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / reps
+    return {'workload': 'cfg4: xT 16x12 fit (count + all-reduce + value iteration) + rate',
+            'ms_per_fit_and_rate': round(dt * 1e3, 3), 'iterations': sol.n_iter,
+            'actions_per_s_per_gpu': round(ab.n / dt, 1)}
 
 
 def cpu_baseline(d, seconds: float) -> dict:
@@ -85,6 +123,7 @@ def main() -> None:
     ap.add_argument('--games', type=int, default=10000, help='games per GPU (cfg2: 10k)')
     ap.add_argument('--cpu-seconds', type=float, default=15.0)
     ap.add_argument('--no-cpu', action='store_true')
+    ap.add_argument('--no-xt', action='store_true', help='skip the cfg4 xT side measurement')
     ap.add_argument('--bool-tile', type=int, default=1024,
                     help='rows per bool-block tile (0 = one tile: plain column-major)')
     ap.add_argument('--num-tile', type=int, default=128,
@@ -155,12 +194,9 @@ def main() -> None:
             for i, name in enumerate(KERNELS)}
     total_actions = n
     if dist:
-        t = torch.tensor([wall], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        wall = float(t.item())
-        c = torch.tensor([n], dtype=torch.int64, device=dev)
-        dist.all_reduce(c)
-        total_actions = int(c.item())
+        wall = _reduce(dist, wall, dist.ReduceOp.MAX, dev)
+        total_actions = int(_reduce(dist, n, dist.ReduceOp.SUM, dev))
+    extra_xt = xt_extra(d, ab, dist, dev) if not args.no_xt else None
     if rank != 0:
         if dist:
             dist.destroy_process_group()
@@ -194,9 +230,12 @@ def main() -> None:
         'kernels': per_kernel,
         'roofline': {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS,
                      'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 4),
-                     'traffic': traffic, 'kernel': f'{dom}_kernel',
+                     'traffic': traffic, 'traffic_unit': 'HBM bytes per launch (rocprofv3 PMC)',
+                     'algorithmic_bytes': BYTES[dom] * n, 'kernel': f'{dom}_kernel',
                      'bytes_per_action': BYTES[dom]},
     }
+    if extra_xt is not None:
+        line['xt_cfg4'] = extra_xt
     if not args.no_cpu:
         line['cpu_baseline'] = cpu_baseline(d, args.cpu_seconds)
     print(json.dumps(line), flush=True)

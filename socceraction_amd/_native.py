@@ -99,6 +99,12 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         raise ImportError(
             f'{path} is missing: build the HIP library first '
             '(python -m socceraction_amd.build). socceraction_amd has no CPU fallback.')
+    # torch ships its own libamdhip64 (SONAME libamdhip64.so.7, same as /opt/rocm's) and
+    # device memory comes from torch's allocator, so the process must hold ONE HIP runtime:
+    # load torch first and our NEEDED libamdhip64.so.7 binds to that copy.  dlopen-ing this
+    # library first would pull in /opt/rocm's runtime as a second instance, and the kernels
+    # would then see no device once torch initialises its own.
+    import torch  # noqa: F401
     lib = ctypes.CDLL(path)
     for name, (res, args) in _SIGNATURES.items():
         fn = getattr(lib, name)

@@ -347,3 +347,15 @@ def test_move_filters_on_reference_fixture():
     assert mv.type_id.isin([0, 21, 1]).all() and len(mv) > 0
     sm = xt.get_successful_move_actions(df)
     assert (sm.result_id == 1).all()
+
+
+def test_single_hip_runtime_after_load():
+    """The library must bind to torch's HIP runtime, never load a second copy."""
+    import subprocess
+    import sys
+    code = ("import socceraction_amd._native as n; n.load_library(); "
+            "import os; print(len({l.split()[-1] for l in open('/proc/self/maps') "
+            "if 'libamdhip64' in l}))")
+    out = subprocess.run([sys.executable, '-c', code], capture_output=True, text=True,
+                         check=True, cwd=os.path.dirname(os.path.dirname(__file__)))
+    assert out.stdout.strip().splitlines()[-1] == '1'
