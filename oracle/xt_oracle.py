@@ -78,11 +78,12 @@ def fit(cols: Dict[str, np.ndarray], l: int = 16, w: int = 12, eps: float = 1e-5
     gs = scoring * pshot
     xT = np.zeros((w, l))
     heat = [xT.copy()]
+    Tt = np.ascontiguousarray(T.T)  # Tt[c] = T[:, c]: same products, contiguous rows
     while True:
         x = xT.reshape(-1)
         tot = np.zeros(C)
         for c in range(C):  # sequential accumulation over the flat column index
-            tot += T[:, c] * x[c]
+            tot += Tt[c] * x[c]
         newxT = gs + pmove * tot.reshape((w, l))
         diff = newxT - xT
         xT = newxT

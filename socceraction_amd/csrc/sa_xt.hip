@@ -34,14 +34,17 @@ __device__ __forceinline__ int flat_index(double x, double y, int l, int w) {
 __device__ __forceinline__ bool is_move(int t) { return t == T_PASS || t == T_DRIBBLE || t == T_CROSS; }
 
 // ---------------------------------------------------------------------------------------------
-// Count pass.  SMALL: per-workgroup LDS histograms (u32 for the three C-vectors, the C x C
+// Count pass.  XC_SMALL: per-workgroup LDS histograms (u32 for the three C-vectors, the C x C
 // transition counts packed two u16 per word), flushed with one global atomic per non-zero
-// bin; a workgroup handles <= 65535 actions so a u16 bin cannot overflow.  Otherwise global
-// atomics straight into the caller's buffers.
+// bin; a workgroup handles <= 65535 actions so a u16 bin cannot overflow.  XC_VEC (C up to
+// ~10k, e.g. 105 x 68): only the three C-vectors in LDS -- every move hits move[start], so
+// global atomics there serialise on a few thousand hot addresses -- and the sparse C x C
+// transition counts as global atomics.  XC_GLOBAL: global atomics for everything.
 constexpr int XT_THREADS = 256;
-constexpr int XT_SMALL_ACTS = 32768;  // actions per workgroup in the LDS-privatised form
+constexpr int XT_SMALL_ACTS = 32768;  // actions per workgroup in the LDS-privatised forms
+enum { XC_GLOBAL = 0, XC_VEC = 1, XC_SMALL = 2 };
 
-template <bool SMALL>
+template <int MODE>
 __global__ __launch_bounds__(XT_THREADS) void xt_count_kernel(sa_actions A, int l, int w,
                                                              unsigned long long* __restrict__ shot,
                                                              unsigned long long* __restrict__ goal,
@@ -56,9 +59,10 @@ __global__ __launch_bounds__(XT_THREADS) void xt_count_kernel(sa_actions A, int 
   uint32_t* hg = lds + C;      // [C]
   uint32_t* hm = lds + 2 * C;  // [C]
   uint32_t* ht = lds + 3 * C;  // [(C*C+1)/2] packed u16 pairs
+  constexpr bool SMALL = MODE == XC_SMALL, VEC = MODE != XC_GLOBAL;
   int64_t begin, end, stride;
-  if (SMALL) {
-    const int tw = (C * C + 1) / 2;
+  if (VEC) {
+    const int tw = SMALL ? (C * C + 1) / 2 : 0;
     for (int k = threadIdx.x; k < 3 * C + tw; k += blockDim.x) lds[k] = 0;
     __syncthreads();
     begin = (int64_t)blockIdx.x * XT_SMALL_ACTS + threadIdx.x;
@@ -70,55 +74,70 @@ __global__ __launch_bounds__(XT_THREADS) void xt_count_kernel(sa_actions A, int 
     stride = (int64_t)gridDim.x * blockDim.x;
   }
   int32_t bad = 0;
-  for (int64_t j = begin; j < end; j += stride) {
-    const int t = F.type_id[j];
-    const bool shot_t = t == T_SHOT, move_t = is_move(t);
-    if (!shot_t && !move_t) continue;
-    const double sx = F.c0[j], sy = F.c1[j];
-    const int r = F.result_id[j];
-    if (shot_t) {
-      if (isnan(sx) || isnan(sy)) continue;  // _count drops NaN rows (xthreat.py:60-61)
-      if (!isfinite(sx) || !isfinite(sy)) {
-        bad |= 1;
-        continue;
-      }
-      const int c = flat_index(sx, sy, l, w);
-      if (SMALL) {
-        atomicAdd(&hs[c], 1u);
-        if (r == R_SUCCESS) atomicAdd(&hg[c], 1u);
-      } else {
-        atomicAdd(&shot[c], 1ull);
-        if (r == R_SUCCESS) atomicAdd(&goal[c], 1ull);
-      }
-    } else {
-      const double ex = F.c2[j], ey = F.c3[j];
-      if (!isfinite(sx) || !isfinite(sy) || !isfinite(ex) || !isfinite(ey)) {
-        bad |= 2;  // move_transition_matrix casts every move coordinate to int64
-        continue;
-      }
-      const int cs = flat_index(sx, sy, l, w);
-      if (SMALL)
-        atomicAdd(&hm[cs], 1u);
-      else
-        atomicAdd(&move[cs], 1ull);
-      if (r == R_SUCCESS) {
-        const int ce = flat_index(ex, ey, l, w);
-        const int64_t k = (int64_t)cs * C + ce;
-        if (SMALL)
-          atomicAdd(&ht[k >> 1], (k & 1) ? 0x10000u : 1u);
+  // XC_U actions per thread per pass, every load issued before any is used (the loop is
+  // otherwise one HBM round trip per action); rows past `end` are clamped and skipped
+  constexpr int XC_U = 4;
+  for (int64_t j0 = begin; j0 < end; j0 += XC_U * stride) {
+    int tt[XC_U], rr[XC_U];
+    double sx[XC_U], sy[XC_U], ex[XC_U], ey[XC_U];
+#pragma unroll
+    for (int u = 0; u < XC_U; ++u) {
+      const int64_t j = j0 + u * stride < end ? j0 + u * stride : end - 1;
+      tt[u] = j0 + u * stride < end ? F.type_id[j] : -1;
+      rr[u] = F.result_id[j];
+      sx[u] = F.c0[j];
+      sy[u] = F.c1[j];
+      ex[u] = F.c2[j];
+      ey[u] = F.c3[j];
+    }
+#pragma unroll
+    for (int u = 0; u < XC_U; ++u) {
+      const int t = tt[u], r = rr[u];
+      if (t == T_SHOT) {
+        if (isnan(sx[u]) || isnan(sy[u])) continue;  // _count drops NaN rows (xthreat.py:60-61)
+        if (!isfinite(sx[u]) || !isfinite(sy[u])) {
+          bad |= 1;
+          continue;
+        }
+        const int c = flat_index(sx[u], sy[u], l, w);
+        if (VEC) {
+          atomicAdd(&hs[c], 1u);
+          if (r == R_SUCCESS) atomicAdd(&hg[c], 1u);
+        } else {
+          atomicAdd(&shot[c], 1ull);
+          if (r == R_SUCCESS) atomicAdd(&goal[c], 1ull);
+        }
+      } else if (is_move(t)) {
+        if (!isfinite(sx[u]) || !isfinite(sy[u]) || !isfinite(ex[u]) || !isfinite(ey[u])) {
+          bad |= 2;  // move_transition_matrix casts every move coordinate to int64
+          continue;
+        }
+        const int cs = flat_index(sx[u], sy[u], l, w);
+        if (VEC)
+          atomicAdd(&hm[cs], 1u);
         else
-          atomicAdd(&trans[k], 1);
+          atomicAdd(&move[cs], 1ull);
+        if (r == R_SUCCESS) {
+          const int ce = flat_index(ex[u], ey[u], l, w);
+          const int64_t k = (int64_t)cs * C + ce;
+          if (SMALL)
+            atomicAdd(&ht[k >> 1], (k & 1) ? 0x10000u : 1u);
+          else
+            atomicAdd(&trans[k], 1);
+        }
       }
     }
   }
   if (bad) atomicOr(err, bad);
-  if (SMALL) {
+  if (VEC) {
     __syncthreads();
     for (int c = threadIdx.x; c < C; c += blockDim.x) {
       if (hs[c]) atomicAdd(&shot[c], (unsigned long long)hs[c]);
       if (hg[c]) atomicAdd(&goal[c], (unsigned long long)hg[c]);
       if (hm[c]) atomicAdd(&move[c], (unsigned long long)hm[c]);
     }
+  }
+  if (SMALL) {
     const int tw = (C * C + 1) / 2;
     for (int k = threadIdx.x; k < tw; k += blockDim.x) {
       const uint32_t v = ht[k];
@@ -233,26 +252,153 @@ __global__ __launch_bounds__(1024) void xt_solve_small_kernel(const double* __re
   if (r == 0) *n_iter = cont ? -1 : it;
 }
 
-// Large grids: one launch per iteration, one wave per 64 rows.  flags[it] != 0 <=> some cell
-// of iteration it changed by more than eps; a launch whose predecessor converged is a no-op.
-__global__ __launch_bounds__(64) void xt_iter_kernel(const double* __restrict__ Tt,
-                                                     const double* __restrict__ gs,
-                                                     const double* __restrict__ pmove, int C, double eps,
-                                                     int it, double* __restrict__ heat,
-                                                     int32_t* __restrict__ flags) {
+// Large grids (C > XT_SOLVE_MAX_C, e.g. 105 x 68 = 7140 cells): one launch per iteration.
+// The dense transition matrix is never materialised for the iteration: a workgroup owns
+// XI_ROWS rows r and streams their int32 count rows trans[r*C + c] (4 B per element instead
+// of 8 B of f64 T: 204 MB instead of 408 MB per iteration at 7140 cells, which then also
+// stays resident in the 256 MB Infinity Cache across iterations).  T[r,c] * x[c] is formed
+// exactly as the reference rounds it -- one correctly rounded division cnt / move[r], one
+// multiply -- and cnt == 0 gives +0, which leaves a non-negative running sum unchanged.  So
+// each loader wave compacts the non-zero columns of its rows (ballot + mbcnt, in column
+// order), divides only those, and the chain lanes add each row's compacted products strictly
+// left to right: the reference's sequential rounding, over nnz instead of C terms.
+// 8 loader waves (2 rows each) keep XI_DEPTH chunks of XI_CH columns in flight (unconditional loads from
+// clamped addresses); a fifth wave runs the 16 chains, one chunk behind the loaders (two LDS
+// buffers, one barrier per chunk).  Measured at 7140 cells (profiles/r01_xt_iteration.md):
+// 62 us per iteration; 4 loader waves 71 us, chains inside each loader wave without barriers
+// 98 us, dense division of every element +10 us, an uncompacted chain +45 us.  flags[it] != 0 <=>
+// some cell of iteration it moved by more than eps; a launch whose predecessor converged is
+// a no-op.
+#ifndef SA_XI_DEPTH
+#define SA_XI_DEPTH 2
+#endif
+#ifndef SA_XI_LOADERS
+#define SA_XI_LOADERS 8
+#endif
+constexpr int XI_ROWS = 16;
+constexpr int XI_LOADERS = SA_XI_LOADERS;        // loader waves; one more wave runs the chains
+constexpr int XI_RQ = XI_ROWS / XI_LOADERS;      // rows per loader wave
+constexpr int XI_THREADS = (XI_LOADERS + 1) * 64;
+constexpr int XI_CH = 128;             // columns per chunk = 2 per loader lane per row
+constexpr int XI_DEPTH = SA_XI_DEPTH;  // chunks in flight per loader lane
+constexpr int XI_LST = XI_CH + 1;      // list row stride (doubles): chain reads hit 16 banks
+
+struct XiChunk {
+  int32_t cnt[XI_RQ][2];  // [row q][column i]
+  double xv[2];       // x[c] of column i
+};
+
+__global__ __launch_bounds__(XI_THREADS) void xt_iter_kernel(const int32_t* __restrict__ trans,
+                                                             const unsigned long long* __restrict__ move,
+                                                             const double* __restrict__ gs,
+                                                             const double* __restrict__ pmove, int C,
+                                                             double eps, int it, double* __restrict__ heat,
+                                                             int32_t* __restrict__ flags) {
   if (it > 0 && __hip_atomic_load(&flags[it - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
     return;
-  const int r = blockIdx.x * 64 + threadIdx.x;
-  const double* x = heat + (int64_t)it * C;
-  int flag = 0;
-  if (r < C) {
-    const double tot = row_payoff(Tt, x, C, r);
-    const double mv = pmove[r] * tot;
-    const double nx = gs[r] + mv;
-    heat[(int64_t)(it + 1) * C + r] = nx;
-    flag = (nx - x[r]) > eps;
+  __shared__ double list[2][XI_ROWS * XI_LST];       // compacted x, then products, per row
+  __shared__ int32_t cbuf[XI_LOADERS][XI_RQ][XI_CH];  // compacted counts (loader-wave private)
+  __shared__ int32_t lens[2][XI_ROWS];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int r0 = blockIdx.x * XI_ROWS;
+  const double* __restrict__ x = heat + (int64_t)it * C;
+  const int nch = (C + XI_CH - 1) / XI_CH;
+  const int nchp = (nch + XI_DEPTH - 1) / XI_DEPTH * XI_DEPTH;
+  if (wv < XI_LOADERS) {  // ---- loader waves: rows r0 + RQ*wv + q, columns k*XI_CH + 64*i + lane
+    const int32_t* rowp[XI_RQ];
+    double mvq[XI_RQ];
+    bool rowok[XI_RQ];
+#pragma unroll
+    for (int q = 0; q < XI_RQ; ++q) {
+      const int r = r0 + XI_RQ * wv + q;
+      rowok[q] = r < C;
+      const int rc = rowok[q] ? r : C - 1;
+      rowp[q] = trans + (int64_t)rc * C;
+      mvq[q] = (double)move[rc];
+    }
+    auto issue = [&](XiChunk& R, int k) {  // unconditional loads from clamped addresses
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int c = k * XI_CH + 64 * i + lane;
+        const int cc = c < C ? c : C - 1;
+        R.xv[i] = x[cc];
+#pragma unroll
+        for (int q = 0; q < XI_RQ; ++q) R.cnt[q][i] = rowp[q][cc];
+      }
+    };
+    auto stage = [&](const XiChunk& R, int k, int par) {
+      double* lst = list[par];
+#pragma unroll
+      for (int q = 0; q < XI_RQ; ++q) {
+        const int row = XI_RQ * wv + q;
+        int base = 0;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {  // compact the non-zero columns, in column order
+          const bool cok = k * XI_CH + 64 * i + lane < C;
+          const int32_t cnt = (cok && rowok[q]) ? R.cnt[q][i] : 0;
+          const uint64_t m = __ballot(cnt != 0);
+          const int pos = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+          if (cnt != 0) {
+            lst[row * XI_LST + pos] = R.xv[i];
+            cbuf[wv][q][pos] = cnt;
+          }
+          base += __popcll(m);
+        }
+        for (int e = lane; e < base; e += 64) {  // T[r, c] * x[c] on the compacted entries
+          const double tv = (double)cbuf[wv][q][e] / mvq[q];
+          lst[row * XI_LST + e] = tv * lst[row * XI_LST + e];
+        }
+        if (lane == 0) lens[par][row] = base;
+      }
+    };
+    // a multiple of XI_DEPTH chunks with no data-dependent branches around the loads; the empty
+    // asm keeps each prefetch where it is issued (the compiler otherwise sinks it next to its
+    // use and the wait counts drain every load); chunks past C are empty
+    XiChunk R[XI_DEPTH];
+#pragma unroll
+    for (int d = 0; d < XI_DEPTH; ++d) issue(R[d], d);
+    asm volatile("" ::: "memory");
+    for (int k0 = 0; k0 < nchp; k0 += XI_DEPTH) {
+#pragma unroll
+      for (int d = 0; d < XI_DEPTH; ++d) {
+        const int k = k0 + d;
+        stage(R[d], k, k & 1);
+        issue(R[d], k + XI_DEPTH);  // past the end: clamped, harmless re-reads of column C-1
+        asm volatile("" ::: "memory");
+        __syncthreads();
+      }
+    }
+  } else {  // ---- chain wave: lane r adds its row's compacted products strictly left to right
+    double acc = 0.0;
+    const int r = lane & (XI_ROWS - 1);
+    for (int k = 0; k < nchp; ++k) {
+      __syncthreads();
+      const int par = k & 1;
+      const int len = lens[par][r];
+      int mx = 0;
+#pragma unroll
+      for (int u = 0; u < XI_ROWS; ++u) mx = max(mx, lens[par][u]);
+      const double* lst = list[par] + r * XI_LST;
+      for (int j = 0; j < mx; j += 8) {
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = lst[(j + u) & (XI_CH - 1)];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const double p = (j + u < len) ? v[u] : 0.0;
+          acc = acc + p;
+        }
+      }
+    }
+    if (lane < XI_ROWS && r0 + r < C) {
+      const int rr = r0 + r;
+      const double mv = pmove[rr] * acc;
+      const double nx = gs[rr] + mv;
+      heat[(int64_t)(it + 1) * C + rr] = nx;
+      if ((nx - x[rr]) > eps) atomicOr(&flags[it], 1);  // np.any(diff > eps): NaN is False
+    }
   }
-  if (__any(flag) && (threadIdx.x == 0)) atomicOr(&flags[it], 1);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -332,15 +478,19 @@ extern "C" int sa_xt_count(const sa_actions* a, int32_t l, int32_t w, int64_t* s
   auto* us = reinterpret_cast<unsigned long long*>(shot);
   auto* ug = reinterpret_cast<unsigned long long*>(goal);
   auto* um = reinterpret_cast<unsigned long long*>(move);
+  const size_t vec_lds = (size_t)3 * C * 4;
+  const unsigned wg_blocks = (unsigned)((a->n + XT_SMALL_ACTS - 1) / XT_SMALL_ACTS);
   if (small_lds <= 80 * 1024) {
-    const unsigned blocks = (unsigned)((a->n + XT_SMALL_ACTS - 1) / XT_SMALL_ACTS);
-    hipLaunchKernelGGL((xt_count_kernel<true>), dim3(blocks), dim3(XT_THREADS), small_lds, st, *a, l, w,
-                       us, ug, um, trans, err_flags);
+    hipLaunchKernelGGL((xt_count_kernel<XC_SMALL>), dim3(wg_blocks), dim3(XT_THREADS), small_lds, st, *a,
+                       l, w, us, ug, um, trans, err_flags);
+  } else if (vec_lds <= 120 * 1024) {
+    hipLaunchKernelGGL((xt_count_kernel<XC_VEC>), dim3(wg_blocks), dim3(XT_THREADS), vec_lds, st, *a, l,
+                       w, us, ug, um, trans, err_flags);
   } else {
     int64_t blocks = (a->n + XT_THREADS - 1) / XT_THREADS;
     if (blocks > 4096) blocks = 4096;
-    hipLaunchKernelGGL((xt_count_kernel<false>), dim3((unsigned)blocks), dim3(XT_THREADS), 0, st, *a, l,
-                       w, us, ug, um, trans, err_flags);
+    hipLaunchKernelGGL((xt_count_kernel<XC_GLOBAL>), dim3((unsigned)blocks), dim3(XT_THREADS), 0, st, *a,
+                       l, w, us, ug, um, trans, err_flags);
   }
   return check_launch("xt_count_kernel");
 }
@@ -389,8 +539,8 @@ extern "C" int sa_xt_solve(const int64_t* shot, const int64_t* goal, const int64
     for (int it0 = 0; !rc && it0 < max_iter && iters < 0; it0 += batch) {
       const int it1 = it0 + batch < max_iter ? it0 + batch : max_iter;
       for (int it = it0; it < it1; ++it)
-        hipLaunchKernelGGL(xt_iter_kernel, dim3((C + 63) / 64), dim3(64), 0, st, trans_t, gs, pm, C, eps,
-                           it, heatmaps, dflags);
+        hipLaunchKernelGGL(xt_iter_kernel, dim3((C + XI_ROWS - 1) / XI_ROWS), dim3(XI_THREADS), 0, st,
+                           trans, um, gs, pm, C, eps, it, heatmaps, dflags);
       rc = check_launch("xt_iter_kernel");
       if (!rc) rc = check_hip(hipMemcpyAsync(hflags.data() + it0, dflags + it0,
                                              sizeof(int32_t) * (it1 - it0), hipMemcpyDeviceToHost, st),

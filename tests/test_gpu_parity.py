@@ -192,6 +192,27 @@ def test_xt_goldens(sa):
                 assert_close(r.cpu().numpy(), g[f'{tag}_rate_interp'], f'{name} {tag} interp rate')
 
 
+@pytest.mark.parametrize('l,w,games', [(40, 30, 300), (105, 68, 300)])
+def test_xt_large_grid_vs_oracle(sa, l, w, games):
+    """Grids above the single-workgroup solver (C > 1024) take the streaming count-row
+    iteration; iterates, iteration count and matrices must be bit-identical to the oracle."""
+    B, ops, syn = sa['batch'], sa['ops'], sa['synthetic']
+    d = syn.spadl_games(games, game_id0=77)
+    ab = B.ActionBatch.from_columns(d)
+    acc = ops.xt_count(ab, l, w)
+    ops.xt_check_errors(acc)
+    sol = ops.xt_solve(acc)
+    ref = xo.fit(d, l, w)
+    m = sol.mats.cpu().numpy()
+    np.testing.assert_array_equal(m[0].reshape(w, l), ref['scoring_prob'])
+    np.testing.assert_array_equal(m[1].reshape(w, l), ref['shot_prob'])
+    np.testing.assert_array_equal(m[2].reshape(w, l), ref['move_prob'])
+    np.testing.assert_array_equal(sol.trans_t.cpu().numpy().T, ref['transition'])
+    assert sol.n_iter + 1 == len(ref['heatmaps'])
+    np.testing.assert_array_equal(sol.heatmaps.cpu().numpy().reshape(-1, w, l), ref['heatmaps'])
+    np.testing.assert_array_equal(m[3].reshape(w, l), ref['xT'])
+
+
 def test_full_size_sampled_games_vs_oracle(sa):
     """cfg2-sized batch (10k games, ~16M actions): sampled games checked against the oracle,
     plus size-independent invariants over the whole batch (one-hot rows sum to 1)."""
