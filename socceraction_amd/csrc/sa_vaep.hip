@@ -25,13 +25,30 @@
 #ifndef SA_NT_STORES
 #define SA_NT_STORES 1
 #endif
+#ifndef SA_BOOL_MODE
+// bool block: 0 = one wave per 1024-row tile, 1 = one wave per (tile, window),
+// 2 = one wave per (tile, column group) in XCD-contiguous sweep order
+#define SA_BOOL_MODE 2
+#endif
+#ifndef SA_XCD_REMAP
+#define SA_XCD_REMAP 1  // block -> output range mapping that gives each XCD a contiguous part
+#endif
+#ifndef SA_GS_WAVE
+#define SA_GS_WAVE 1  // goalscore: one wave per segment instead of one workgroup
+#endif
+#ifndef SA_FORMULA_VEC
+#define SA_FORMULA_VEC 1  // formula: 16-B vector loads of each lane's rows
+#endif
 
 namespace sa {
 
 constexpr int WAVE = 64;
 constexpr int LANE_ACTS = 16;
 #ifndef SA_NUM_PAIRS
-#define SA_NUM_PAIRS 8
+#define SA_NUM_PAIRS 1
+#endif
+#ifndef SA_CG_COLS
+#define SA_CG_COLS 32  // bool_colgroup_kernel: target columns per wave
 #endif
 constexpr int BLOCK_WAVES = 4;
 constexpr int NUM_PAIRS = SA_NUM_PAIRS;         // 2-action pairs per lane in num_features_kernel
@@ -47,6 +64,25 @@ struct FeatArgs {
   int64_t Cb, Cf, Ci;  // columns of each block
   int64_t Rb, Rf, Ri;  // rows per tile of each block (include/socceraction_amd.h)
 };
+
+// Workgroups are dispatched round-robin over the 8 XCDs (XCD = blockIdx % 8).  Writing the
+// output front to back in blockIdx order leaves every XCD's concurrent stores scattered over
+// the whole active window; remapped, XCD x owns the contiguous logical blocks
+// [x*per, (x+1)*per) and sweeps them in order, which keeps each XCD's open DRAM rows
+// together (scripts/probe_store_colgroup.hip: 6.1 -> 6.9 TB/s for the bool image).  The grid
+// must be a multiple of 8 blocks; logical blocks past the real count exit.
+__device__ __forceinline__ int64_t xcd_logical_block() {
+#if SA_XCD_REMAP
+  const int64_t b = blockIdx.x, per = gridDim.x / 8;
+  return (b % 8) * per + b / 8;
+#else
+  return blockIdx.x;
+#endif
+}
+
+static inline unsigned xcd_grid(int64_t blocks) {
+  return (unsigned)((blocks + 7) / 8 * 8);
+}
 
 // Element offset of (row j, column c) in a tiled column-major block with C columns.  A
 // lane's 16 (or 2) rows never straddle a tile because R % 16 == 0.
@@ -349,6 +385,336 @@ __global__ __launch_bounds__(256) void bool_features_kernel(FeatArgs args) {
   }
 }
 
+// Window-split form: a workgroup owns one 1024-row tile and has one wave per game-state
+// window; wave i writes only window i's columns (~172 of the 515 at k = 3).  Same stores,
+// same tile image as bool_features_kernel, but 3x as many waves of 1/3 the length, so the
+// drain at the end of a launch (a 16M-action launch is only ~2.5 whole-tile waves per
+// resident slot) leaves far less of the chip idle.  The tile's team codes are staged in LDS
+// once for all its waves.
+constexpr int BOOL_TILE = 1024;
+
+template <bool ATOMIC, bool EXPLICIT>
+__global__ __launch_bounds__(64 * SA_MAX_FRAMES) void bool_window_kernel(FeatArgs args) {
+  __shared__ int32_t team_lds[BOOL_TILE + 8];
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int i = threadIdx.x / WAVE;  // the window this wave writes
+  const sa_actions& A = args.a;
+  const sa_feature_plan& P = args.p;
+  const int64_t n = A.n;
+  const int K = P.nb_prev_actions;
+  const int64_t R = args.Rb;
+  const int64_t tile0 = xcd_logical_block() * BOOL_TILE;
+  const int64_t j0 = tile0 + (int64_t)lane * LANE_ACTS;
+  const sa_frame& F0 = A.frames[0];
+  const int tcol = P.bool_col[SA_XFN_TEAM];
+  const bool need_team = tcol >= 0 && K > 1;
+  if (!EXPLICIT && need_team) {  // team codes of rows tile0-8 .. tile0+1023 -> LDS
+    for (int k = threadIdx.x; k < BOOL_TILE + 8; k += blockDim.x)
+      team_lds[k] = ld_or0(F0.team, tile0 - 8 + k, n);
+  }
+  __syncthreads();
+  if (j0 >= n) return;
+  uint8_t* bb = args.bout + tile_off(j0, 0, args.Cb, R);
+  // d = min(j - seg_start, 15) per action (only windows i >= 1 need it)
+  uint32_t dw[4] = {0, 0, 0, 0};
+  if (!EXPLICIT && i > 0) {
+    SegCursor c = seg_at(A, j0);
+#pragma unroll
+    for (int m = 0; m < LANE_ACTS; ++m) {
+      const int64_t j = j0 + m;
+      if (j < n) {
+        seg_advance(A, c, j);
+        const int64_t dd = j - c.s;
+        const int d = dd > 15 ? 15 : (int)dd;
+        dw[m >> 2] |= (uint32_t)d << (8 * (m & 3));
+      }
+    }
+  }
+  uint32_t tw[4], rw[4], bw[4];  // window i of the lane's 16 actions
+  if (EXPLICIT) {
+    const sa_frame& Fi = A.frames[i];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      tw[q] = ld_u8x4(Fi.type_id, j0 / 4 + q, n);
+      rw[q] = ATOMIC ? 0u : ld_u8x4(Fi.result_id, j0 / 4 + q, n);
+      bw[q] = ld_u8x4(Fi.bodypart_id, j0 / 4 + q, n);
+    }
+  } else {
+    uint32_t TR[6], RR[6], BR[6];  // rows j0-8 .. j0+15
+    const int64_t wbase = j0 / 4 - 2;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      TR[k] = ld_u8x4(F0.type_id, wbase + k, n);
+      RR[k] = ATOMIC ? 0u : ld_u8x4(F0.result_id, wbase + k, n);
+      BR[k] = ld_u8x4(F0.bodypart_id, wbase + k, n);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      tw[q] = TR[2 + q];
+      rw[q] = RR[2 + q];
+      bw[q] = BR[2 + q];
+    }
+    for (int s = 1; s <= i; ++s) {  // window s = window s-1 shifted one row, clamped bytes kept
+      shift_rows(TR);
+      if (!ATOMIC) shift_rows(RR);
+      shift_rows(BR);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t mk = ge_mask(dw[q], s);
+        tw[q] = (TR[2 + q] & mk) | (tw[q] & ~mk);
+        rw[q] = (RR[2 + q] & mk) | (rw[q] & ~mk);
+        bw[q] = (BR[2 + q] & mk) | (bw[q] & ~mk);
+      }
+    }
+  }
+  const int c_type = P.bool_col[SA_XFN_ACTIONTYPE_ONEHOT];
+  const int c_res = ATOMIC ? -1 : P.bool_col[SA_XFN_RESULT_ONEHOT];
+  const int c_tr = ATOMIC ? -1 : P.bool_col[SA_XFN_ACTIONTYPE_RESULT_ONEHOT];
+  const int c_bp = P.bool_col[SA_XFN_BODYPART_ONEHOT];
+  if (c_type >= 0) {
+    if (!ATOMIC) {
+      for (int t = 0; t < N_TYPES; ++t)
+        st_bool16(bb, c_type + i * N_TYPES + t, R, bytes_eq(tw[0], t), bytes_eq(tw[1], t),
+                  bytes_eq(tw[2], t), bytes_eq(tw[3], t));
+    } else {
+      // 33 atomic names, 32 unique: 'interception' (ids 10 and 24) is ONE column true for
+      // both ids (atomic/vaep/features.py:114-132 + atomic/spadl/config.py:25-36)
+      for (int u = 0; u < N_ATOMIC_NAMES; ++u) {
+        const uint32_t id = u <= 23 ? (uint32_t)u : (uint32_t)u + 1;
+        uint32_t m0 = bytes_eq(tw[0], id), m1 = bytes_eq(tw[1], id), m2 = bytes_eq(tw[2], id),
+                 m3 = bytes_eq(tw[3], id);
+        if (u == 10) {
+          m0 |= bytes_eq(tw[0], AT_INTERCEPTION2);
+          m1 |= bytes_eq(tw[1], AT_INTERCEPTION2);
+          m2 |= bytes_eq(tw[2], AT_INTERCEPTION2);
+          m3 |= bytes_eq(tw[3], AT_INTERCEPTION2);
+        }
+        st_bool16(bb, c_type + i * N_ATOMIC_NAMES + u, R, m0, m1, m2, m3);
+      }
+    }
+  }
+  if (c_res >= 0) {
+    for (int r = 0; r < N_RESULTS; ++r)
+      st_bool16(bb, c_res + i * N_RESULTS + r, R, bytes_eq(rw[0], r), bytes_eq(rw[1], r),
+                bytes_eq(rw[2], r), bytes_eq(rw[3], r));
+  }
+  if (c_tr >= 0) {
+    // code = type*6 + result per byte (type <= 22, result <= 5: no carry between bytes)
+    uint32_t cw[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) cw[q] = (tw[q] << 2) + (tw[q] << 1) + rw[q];
+    const int64_t cb = c_tr + (int64_t)i * N_TYPES * N_RESULTS;
+    for (int code = 0; code < N_TYPES * N_RESULTS; ++code)
+      st_bool16(bb, cb + code, R, bytes_eq(cw[0], code), bytes_eq(cw[1], code),
+                bytes_eq(cw[2], code), bytes_eq(cw[3], code));
+  }
+  if (c_bp >= 0) {
+    for (int b = 0; b < N_BODYPARTS; ++b)
+      st_bool16(bb, c_bp + i * N_BODYPARTS + b, R, bytes_eq(bw[0], b), bytes_eq(bw[1], b),
+                bytes_eq(bw[2], b), bytes_eq(bw[3], b));
+  }
+  if (need_team && i >= 1) {  // team_i = team[a_i] == team[a0] (features.py:448-452)
+    uint32_t m[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int mm = 0; mm < LANE_ACTS; ++mm) {
+      int32_t t0, ti;
+      if (EXPLICIT) {
+        t0 = ld_or0(A.frames[0].team, j0 + mm, n);
+        ti = ld_or0(A.frames[i].team, j0 + mm, n);
+      } else {
+        const int d = (int)byte_of(dw[mm >> 2], mm & 3);
+        const int s = d < i ? d : i;
+        const int32_t* tl = team_lds + 8 + lane * LANE_ACTS + mm;
+        t0 = tl[0];
+        ti = tl[-s];
+      }
+      m[mm >> 2] |= (uint32_t)(t0 == ti) << (8 * (mm & 3));
+    }
+    st_bool16(bb, tcol + (i - 1), R, m[0], m[1], m[2], m[3]);
+  }
+}
+
+// Column-group form (default): the bool image is swept front to back like a fill.  A wave
+// owns one column group -- `gcols` consecutive block columns -- of one 1024-row tile, so a
+// tile is written by `ngroups` short waves whose 1-KiB column runs follow each other in
+// memory, and logical blocks are laid out per XCD (xcd_logical_block) so each XCD streams
+// through its own contiguous eighth of the image.  Every wave rebuilds the tile's game-state
+// windows from the id columns (L2 hits: a tile's groups run back to back on one XCD) and
+// writes only the (family, window, value) columns inside its range.
+constexpr int CG_WAVES = 4;  // waves per workgroup
+#if SA_PROBE_CHEAP  // timing probe only (wrong results): one VALU op per word instead of a compare
+#define CG_EQ(w, v) ((w) ^ (uint32_t)(v))
+#else
+#define CG_EQ(w, v) bytes_eq((w), (v))
+#endif
+
+template <bool ATOMIC, bool EXPLICIT>
+__global__ __launch_bounds__(64 * CG_WAVES) void bool_colgroup_kernel(FeatArgs args, int ngroups,
+                                                                      int gcols) {
+  __shared__ int32_t team_lds[CG_WAVES][BOOL_TILE + 8];
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int wv = threadIdx.x / WAVE;
+  const sa_actions& A = args.a;
+  const sa_feature_plan& P = args.p;
+  const int64_t n = A.n;
+  const int K = P.nb_prev_actions;
+  const int64_t R = args.Rb;
+  const int64_t w = xcd_logical_block() * CG_WAVES + wv;
+  const int64_t tile0 = (w / ngroups) * BOOL_TILE;
+  const int c_lo = (int)(w % ngroups) * gcols;
+  const int c_hi = c_lo + gcols < (int)args.Cb ? c_lo + gcols : (int)args.Cb;
+  const int64_t j0 = tile0 + (int64_t)lane * LANE_ACTS;
+  const sa_frame& F0 = A.frames[0];
+  const int tcol = P.bool_col[SA_XFN_TEAM];
+  // team_1 .. team_{K-1} columns inside [c_lo, c_hi)?
+  const bool need_team = tcol >= 0 && K > 1 && tcol < c_hi && tcol + K - 1 > c_lo;
+  if (!EXPLICIT && need_team && tile0 < n) {  // team codes of rows tile0-8 .. tile0+1023
+    int32_t* tl = team_lds[wv];
+    for (int k = lane; k < BOOL_TILE + 8; k += WAVE) tl[k] = ld_or0(F0.team, tile0 - 8 + k, n);
+  }
+  __syncthreads();
+  if (tile0 >= n || c_lo >= c_hi) return;
+  uint8_t* bb = args.bout + tile_off(j0 < n ? j0 : tile0, 0, args.Cb, R);
+  if (j0 >= n) return;
+  // d = min(j - seg_start, 15) per action: segment of the tile start (same for all lanes),
+  // then each lane advances to its own rows
+  uint32_t dw[4] = {0, 0, 0, 0};
+  if (!EXPLICIT && K > 1) {
+    SegCursor c = seg_at(A, tile0);
+#pragma unroll
+    for (int m = 0; m < LANE_ACTS; ++m) {
+      const int64_t j = j0 + m;
+      if (j < n) {
+        seg_advance(A, c, j);
+        const int64_t dd = j - c.s;
+        const int d = dd > 15 ? 15 : (int)dd;
+        dw[m >> 2] |= (uint32_t)d << (8 * (m & 3));
+      }
+    }
+  }
+  uint32_t TR[6], RR[6], BR[6];  // rows j0-8 .. j0+15 (windowed mode)
+  uint32_t tw[4], rw[4], bw[4];  // window i of the lane's 16 actions
+  if (!EXPLICIT) {
+    const int64_t wbase = j0 / 4 - 2;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      TR[k] = ld_u8x4(F0.type_id, wbase + k, n);
+      RR[k] = ATOMIC ? 0u : ld_u8x4(F0.result_id, wbase + k, n);
+      BR[k] = ld_u8x4(F0.bodypart_id, wbase + k, n);
+    }
+  }
+  const int c_type = P.bool_col[SA_XFN_ACTIONTYPE_ONEHOT];
+  const int c_res = ATOMIC ? -1 : P.bool_col[SA_XFN_RESULT_ONEHOT];
+  const int c_tr = ATOMIC ? -1 : P.bool_col[SA_XFN_ACTIONTYPE_RESULT_ONEHOT];
+  const int c_bp = P.bool_col[SA_XFN_BODYPART_ONEHOT];
+  const int ntypes = ATOMIC ? N_ATOMIC_NAMES : N_TYPES;
+  // [v0, v1): values v of a family whose column base + v lies in [c_lo, c_hi)
+  auto range = [&](int base, int nv, int& v0, int& v1) {
+    v0 = c_lo - base > 0 ? c_lo - base : 0;
+    v1 = c_hi - base < nv ? c_hi - base : nv;
+  };
+  for (int i = 0; i < K; ++i) {
+    if (EXPLICIT) {
+      const sa_frame& Fi = A.frames[i];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        tw[q] = ld_u8x4(Fi.type_id, j0 / 4 + q, n);
+        rw[q] = ATOMIC ? 0u : ld_u8x4(Fi.result_id, j0 / 4 + q, n);
+        bw[q] = ld_u8x4(Fi.bodypart_id, j0 / 4 + q, n);
+      }
+    } else if (i == 0) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        tw[q] = TR[2 + q];
+        rw[q] = RR[2 + q];
+        bw[q] = BR[2 + q];
+      }
+    } else {  // window i = window i-1 shifted one row, clamped bytes kept
+      shift_rows(TR);
+      if (!ATOMIC) shift_rows(RR);
+      shift_rows(BR);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t mk = ge_mask(dw[q], i);
+        tw[q] = (TR[2 + q] & mk) | (tw[q] & ~mk);
+        rw[q] = (RR[2 + q] & mk) | (rw[q] & ~mk);
+        bw[q] = (BR[2 + q] & mk) | (bw[q] & ~mk);
+      }
+    }
+    int v0, v1;
+    if (c_type >= 0) {
+      const int base = c_type + i * ntypes;
+      range(base, ntypes, v0, v1);
+      for (int u = v0; u < v1; ++u) {
+        if (!ATOMIC) {
+          st_bool16(bb, base + u, R, CG_EQ(tw[0], u), CG_EQ(tw[1], u), CG_EQ(tw[2], u),
+                    CG_EQ(tw[3], u));
+        } else {
+          // 33 atomic names, 32 unique: 'interception' (ids 10 and 24) is ONE column true for
+          // both ids (atomic/vaep/features.py:114-132 + atomic/spadl/config.py:25-36)
+          const uint32_t id = u <= 23 ? (uint32_t)u : (uint32_t)u + 1;
+          uint32_t m0 = CG_EQ(tw[0], id), m1 = CG_EQ(tw[1], id), m2 = CG_EQ(tw[2], id),
+                   m3 = CG_EQ(tw[3], id);
+          if (u == 10) {
+            m0 |= CG_EQ(tw[0], AT_INTERCEPTION2);
+            m1 |= CG_EQ(tw[1], AT_INTERCEPTION2);
+            m2 |= CG_EQ(tw[2], AT_INTERCEPTION2);
+            m3 |= CG_EQ(tw[3], AT_INTERCEPTION2);
+          }
+          st_bool16(bb, base + u, R, m0, m1, m2, m3);
+        }
+      }
+    }
+    if (c_res >= 0) {
+      const int base = c_res + i * N_RESULTS;
+      range(base, N_RESULTS, v0, v1);
+      for (int r = v0; r < v1; ++r)
+        st_bool16(bb, base + r, R, CG_EQ(rw[0], r), CG_EQ(rw[1], r), CG_EQ(rw[2], r),
+                  CG_EQ(rw[3], r));
+    }
+    if (c_tr >= 0) {
+      const int base = c_tr + i * N_TYPES * N_RESULTS;
+      range(base, N_TYPES * N_RESULTS, v0, v1);
+      if (v0 < v1) {
+        // code = type*6 + result per byte (type <= 22, result <= 5: no carry between bytes)
+        uint32_t cw[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) cw[q] = (tw[q] << 2) + (tw[q] << 1) + rw[q];
+        for (int code = v0; code < v1; ++code)
+          st_bool16(bb, base + code, R, CG_EQ(cw[0], code), CG_EQ(cw[1], code),
+                    CG_EQ(cw[2], code), CG_EQ(cw[3], code));
+      }
+    }
+    if (c_bp >= 0) {
+      const int base = c_bp + i * N_BODYPARTS;
+      range(base, N_BODYPARTS, v0, v1);
+      for (int b = v0; b < v1; ++b)
+        st_bool16(bb, base + b, R, CG_EQ(bw[0], b), CG_EQ(bw[1], b), CG_EQ(bw[2], b),
+                  CG_EQ(bw[3], b));
+    }
+    const int tc = tcol + i - 1;
+    if (need_team && i >= 1 && tc >= c_lo && tc < c_hi) {  // team_i (features.py:448-452)
+      uint32_t m[4] = {0, 0, 0, 0};
+#pragma unroll
+      for (int mm = 0; mm < LANE_ACTS; ++mm) {
+        int32_t t0, ti;
+        if (EXPLICIT) {
+          t0 = ld_or0(A.frames[0].team, j0 + mm, n);
+          ti = ld_or0(A.frames[i].team, j0 + mm, n);
+        } else {
+          const int d = (int)byte_of(dw[mm >> 2], mm & 3);
+          const int s = d < i ? d : i;
+          const int32_t* tl = team_lds[wv] + 8 + lane * LANE_ACTS + mm;
+          t0 = tl[0];
+          ti = tl[-s];
+        }
+        m[mm >> 2] |= (uint32_t)(t0 == ti) << (8 * (mm & 3));
+      }
+      st_bool16(bb, tc, R, m[0], m[1], m[2], m[3]);
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------ f64/i64 block
 // A lane owns 2 consecutive actions (jb, jb+1); one store instruction writes 1 KiB of one
 // column, and with 128-row tiles (SA_NUM_TILE_QUANTUM) a wave's pass over 128 rows writes
@@ -563,7 +929,7 @@ __global__ __launch_bounds__(256, SA_NUM_MINWAVES) void num_features_kernel(Feat
   const int64_t n = A.n;
   const int K = P.nb_prev_actions;
   const int64_t Rf = args.Rf, Ri = args.Ri;
-  const int64_t wave_base = ((int64_t)blockIdx.x * BLOCK_WAVES + wv) * WAVE_ACTS;
+  const int64_t wave_base = (xcd_logical_block() * BLOCK_WAVES + wv) * WAVE_ACTS;
   const sa_frame& F0 = A.frames[0];
   if (wave_base + 2 * lane >= n) return;
   SegCursor cur = {0, 0, 0};
@@ -740,6 +1106,103 @@ __global__ __launch_bounds__(GS_THREADS) void goalscore_kernel(sa_actions A, int
   }
 }
 
+// Wave-per-segment form: each wave scans one segment in passes of 128 rows, a lane owning 2
+// consecutive rows (u16 id loads, 8-B team load, one 16-B i64x2 store per column, i.e. 1 KiB
+// per wave-instruction), the scan is a wave shuffle scan with the carry broadcast from lane
+// 63; no barriers.  The next pass's inputs are loaded before the current pass is scanned.
+// A pair that straddles the segment's first or last row stores only its own row.
+struct GsIn {
+  uint32_t ty, rs;
+  int32_t t0, t1;
+};
+
+template <bool ATOMIC>
+__device__ __forceinline__ GsIn gs_load(const sa_frame& F, int64_t jb, int64_t n) {
+  GsIn v;
+  if (jb >= 0 && jb + 2 <= n) {
+    v.ty = *reinterpret_cast<const uint16_t*>(F.type_id + jb);
+    v.rs = ATOMIC ? 0u : *reinterpret_cast<const uint16_t*>(F.result_id + jb);
+    const int2 t = *reinterpret_cast<const int2*>(F.team + jb);
+    v.t0 = t.x;
+    v.t1 = t.y;
+  } else {
+    v.ty = (uint32_t)ld_or0(F.type_id, jb, n) | ((uint32_t)ld_or0(F.type_id, jb + 1, n) << 8);
+    v.rs = ATOMIC ? 0u
+                  : (uint32_t)ld_or0(F.result_id, jb, n) | ((uint32_t)ld_or0(F.result_id, jb + 1, n) << 8);
+    v.t0 = ld_or0(F.team, jb, n);
+    v.t1 = ld_or0(F.team, jb + 1, n);
+  }
+  return v;
+}
+
+template <bool ATOMIC>
+__global__ __launch_bounds__(256) void goalscore_wave_kernel(sa_actions A, int64_t* __restrict__ block,
+                                                             int64_t C, int64_t col, int64_t R) {
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int64_t g = (int64_t)blockIdx.x * (blockDim.x / WAVE) + threadIdx.x / WAVE;
+  if (g >= A.n_segments) return;
+  const int64_t s = A.seg_off[g], e = A.seg_off[g + 1];
+  if (s >= e) return;
+  const int64_t n = A.n;
+  const sa_frame& F = A.frames[0];
+  const int32_t teamA = F.team[s];
+  const int64_t base0 = s & ~(int64_t)1;
+  uint64_t carry = 0;  // low 32 bits: goals of team A before this pass; high: team B
+  GsIn cur = gs_load<ATOMIC>(F, base0 + 2 * lane, n);
+  for (int64_t base = base0; base < e; base += 2 * WAVE) {
+    const int64_t jb = base + 2 * lane;
+    const GsIn nxt = gs_load<ATOMIC>(F, jb + 2 * WAVE, n);  // prefetch the next pass
+    uint32_t gb, ob;
+    goal_bytes(cur.ty, cur.rs, ATOMIC, gb, ob);
+    uint64_t inc[2];
+    bool isA[2], valid[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int64_t j = jb + q;
+      valid[q] = j >= s && j < e;
+      isA[q] = (q ? cur.t1 : cur.t0) == teamA;
+      const bool goal = valid[q] && byte_of(gb, q), og = valid[q] && byte_of(ob, q);
+      const bool gA = (goal && isA[q]) || (og && !isA[q]);
+      const bool gB = (goal && !isA[q]) || (og && isA[q]);
+      inc[q] = (uint64_t)gA | ((uint64_t)gB << 32);
+    }
+    const uint64_t x = inc[0] + inc[1];
+    uint64_t incl = x;
+#pragma unroll
+    for (int off = 1; off < WAVE; off <<= 1) {
+      const uint64_t y = __shfl_up(incl, off, WAVE);
+      if (lane >= off) incl += y;
+    }
+    const uint64_t e0 = carry + incl - x, e1 = e0 + inc[0];  // exclusive counts of rows jb, jb+1
+    carry += __shfl(incl, WAVE - 1, WAVE);
+    int64_t tm[2], op[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const uint64_t ex = q ? e1 : e0;
+      const int64_t cA = (int64_t)(ex & 0xFFFFFFFFull), cB = (int64_t)(ex >> 32);
+      tm[q] = isA[q] ? cA : cB;
+      op[q] = isA[q] ? cB : cA;
+    }
+    if (valid[0] && valid[1]) {
+      int64_t* o = block + tile_off(jb, col, C, R);
+      st_i64x2(o, 0, R, tm[0], tm[1]);
+      st_i64x2(o, 1, R, op[0], op[1]);
+      st_i64x2(o, 2, R, tm[0] - op[0], tm[1] - op[1]);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        if (valid[q]) {
+          int64_t* o = block + tile_off(jb + q, col, C, R);
+          o[0] = tm[q];
+          o[R] = op[q];
+          o[2 * R] = tm[q] - op[q];
+        }
+      }
+    }
+    cur = nxt;
+  }
+}
+
 // ------------------------------------------------------------------------------ labels
 // vaep/labels.py:9-116, atomic/vaep/labels.py:9-107.  A lane owns 16 consecutive actions
 // and holds rows j0 .. j0+31 as goal / owngoal bit masks plus team codes, so a look-ahead of
@@ -844,7 +1307,8 @@ __global__ __launch_bounds__(256) void labels_kernel(sa_actions A, int nr, uint8
 template <bool ATOMIC, typename T>
 __global__ __launch_bounds__(256) void formula_kernel(sa_actions A, const T* __restrict__ ps,
                                                       const T* __restrict__ pc, T* __restrict__ off,
-                                                      T* __restrict__ def, T* __restrict__ val) {
+                                                      T* __restrict__ def, T* __restrict__ val,
+                                                      bool vec_ok) {
   constexpr int V = 16 / sizeof(T);
   const int64_t n = A.n;
   const int lane = threadIdx.x & (WAVE - 1);
@@ -854,15 +1318,50 @@ __global__ __launch_bounds__(256) void formula_kernel(sa_actions A, const T* __r
   T s_[V], c_[V];
   double t_[V];
   int32_t tm_[V], ty_[V], rs_[V];
+  typedef T vec_t __attribute__((ext_vector_type(V)));
+  if (vec_ok && active && j0 + V <= n) {  // whole 16-B vectors (vec_ok: 16-B aligned probabilities)
+    const vec_t vs = *reinterpret_cast<const vec_t*>(ps + j0);
+    const vec_t vc = *reinterpret_cast<const vec_t*>(pc + j0);
 #pragma unroll
-  for (int q = 0; q < V; ++q) {  // own rows j0 .. j0+V-1 (clamped to n-1 in the tail)
-    const int64_t j = active ? (j0 + q < n ? j0 + q : n - 1) : 0;
-    s_[q] = ps[j];
-    c_[q] = pc[j];
-    t_[q] = F.time_seconds[j];
-    tm_[q] = F.team[j];
-    ty_[q] = F.type_id[j];
-    rs_[q] = ATOMIC ? 0 : F.result_id[j];
+    for (int q = 0; q < V; q += 2) {
+      const f64x2 tv = *reinterpret_cast<const f64x2*>(F.time_seconds + j0 + q);
+      t_[q] = tv[0];
+      t_[q + 1] = tv[1];
+    }
+    uint32_t tyw, rsw = 0;
+    if (V == 4) {
+      const int4 tv = *reinterpret_cast<const int4*>(F.team + j0);
+      tm_[0] = tv.x;
+      tm_[1 % V] = tv.y;
+      tm_[2 % V] = tv.z;
+      tm_[3 % V] = tv.w;
+      tyw = *reinterpret_cast<const uint32_t*>(F.type_id + j0);
+      if (!ATOMIC) rsw = *reinterpret_cast<const uint32_t*>(F.result_id + j0);
+    } else {
+      const int2 tv = *reinterpret_cast<const int2*>(F.team + j0);
+      tm_[0] = tv.x;
+      tm_[1 % V] = tv.y;
+      tyw = *reinterpret_cast<const uint16_t*>(F.type_id + j0);
+      if (!ATOMIC) rsw = *reinterpret_cast<const uint16_t*>(F.result_id + j0);
+    }
+#pragma unroll
+    for (int q = 0; q < V; ++q) {
+      s_[q] = vs[q];
+      c_[q] = vc[q];
+      ty_[q] = (int32_t)byte_of(tyw, q);
+      rs_[q] = (int32_t)byte_of(rsw, q);
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < V; ++q) {  // own rows j0 .. j0+V-1 (clamped to n-1 in the tail)
+      const int64_t j = active ? (j0 + q < n ? j0 + q : n - 1) : 0;
+      s_[q] = ps[j];
+      c_[q] = pc[j];
+      t_[q] = F.time_seconds[j];
+      tm_[q] = F.team[j];
+      ty_[q] = F.type_id[j];
+      rs_[q] = ATOMIC ? 0 : F.result_id[j];
+    }
   }
   // row j0-1 comes from the previous lane (lane 0 loads it itself)
   T sp = __shfl_up(s_[V - 1], 1, WAVE), cp = __shfl_up(c_[V - 1], 1, WAVE);
@@ -880,7 +1379,6 @@ __global__ __launch_bounds__(256) void formula_kernel(sa_actions A, const T* __r
     rsp = ATOMIC ? 0 : F.result_id[p];
   }
   SegCursor cur = seg_at(A, j0);
-  typedef T vec_t __attribute__((ext_vector_type(V)));
   vec_t vo, vd, vv;
 #pragma unroll
   for (int q = 0; q < V; ++q) {
@@ -956,6 +1454,9 @@ static int check_actions(const sa_actions* a, bool allow_explicit) {
     if (!aligned16(F.type_id) || !aligned16(F.result_id) || !aligned16(F.bodypart_id) ||
         !aligned16(F.team))
       return fail(SA_EINVAL, "frame %d: id and team columns must be 16-byte aligned", f);
+    if (!aligned16(F.c0) || !aligned16(F.c1) || !aligned16(F.c2) || !aligned16(F.c3) ||
+        !aligned16(F.time_seconds))
+      return fail(SA_EINVAL, "frame %d: coordinate and time columns must be 16-byte aligned", f);
   }
   return SA_OK;
 }
@@ -1024,10 +1525,43 @@ extern "C" int sa_vaep_features(const sa_actions* a, const sa_feature_plan* plan
                 wb ? bool_out->tile_rows : 16,
                 wf ? f64_out->tile_rows : 16,
                 wi ? i64_out->tile_rows : 16};
-  const dim3 grid((unsigned)((a->n + BLOCK_ACTS - 1) / BLOCK_ACTS)), block(BLOCK_WAVES * WAVE);
+  const dim3 grid(xcd_grid((a->n + BLOCK_ACTS - 1) / BLOCK_ACTS)), block(BLOCK_WAVES * WAVE);
   const dim3 bgrid((unsigned)((a->n + BOOL_BLOCK_ACTS - 1) / BOOL_BLOCK_ACTS));
   const bool expl = a->n_frames > 1;
-  if (wb) {
+  if (wb && SA_BOOL_MODE == 2) {  // one wave per (tile, group of ~32 columns)
+    const int ng = (int)((args.Cb + SA_CG_COLS - 1) / SA_CG_COLS);
+    const int gc = (int)((args.Cb + ng - 1) / ng);
+    const int64_t waves = (a->n + BOOL_TILE - 1) / BOOL_TILE * ng;
+    const dim3 cgrid(xcd_grid((waves + CG_WAVES - 1) / CG_WAVES)), cblock(WAVE * CG_WAVES);
+    if (a->atomic) {
+      if (expl)
+        hipLaunchKernelGGL((bool_colgroup_kernel<true, true>), cgrid, cblock, 0, st, args, ng, gc);
+      else
+        hipLaunchKernelGGL((bool_colgroup_kernel<true, false>), cgrid, cblock, 0, st, args, ng, gc);
+    } else {
+      if (expl)
+        hipLaunchKernelGGL((bool_colgroup_kernel<false, true>), cgrid, cblock, 0, st, args, ng, gc);
+      else
+        hipLaunchKernelGGL((bool_colgroup_kernel<false, false>), cgrid, cblock, 0, st, args, ng, gc);
+    }
+    rc = check_launch("bool_colgroup_kernel");
+    if (rc) return rc;
+  } else if (wb && SA_BOOL_MODE == 1) {  // one 64*K-thread workgroup per 1024-row tile
+    const dim3 tgrid(xcd_grid((a->n + BOOL_TILE - 1) / BOOL_TILE)), tblock(WAVE * K);
+    if (a->atomic) {
+      if (expl)
+        hipLaunchKernelGGL((bool_window_kernel<true, true>), tgrid, tblock, 0, st, args);
+      else
+        hipLaunchKernelGGL((bool_window_kernel<true, false>), tgrid, tblock, 0, st, args);
+    } else {
+      if (expl)
+        hipLaunchKernelGGL((bool_window_kernel<false, true>), tgrid, tblock, 0, st, args);
+      else
+        hipLaunchKernelGGL((bool_window_kernel<false, false>), tgrid, tblock, 0, st, args);
+    }
+    rc = check_launch("bool_window_kernel");
+    if (rc) return rc;
+  } else if (wb) {
     if (a->atomic) {
       if (expl)
         hipLaunchKernelGGL((bool_features_kernel<true, true>), bgrid, block, 0, st, args);
@@ -1076,6 +1610,16 @@ extern "C" int sa_vaep_goalscore(const sa_actions* a, const sa_block* i64_out, i
   if (a->n == 0) return SA_OK;
   hipStream_t st = (hipStream_t)stream;
   int64_t* blk = (int64_t*)i64_out->data;
+  if (SA_GS_WAVE) {  // one wave per segment, 4 segments per workgroup
+    const dim3 g4((unsigned)((a->n_segments + 3) / 4));
+    if (a->atomic)
+      hipLaunchKernelGGL((goalscore_wave_kernel<true>), g4, dim3(256), 0, st, *a, blk,
+                         (int64_t)i64_out->n_cols, (int64_t)col, i64_out->tile_rows);
+    else
+      hipLaunchKernelGGL((goalscore_wave_kernel<false>), g4, dim3(256), 0, st, *a, blk,
+                         (int64_t)i64_out->n_cols, (int64_t)col, i64_out->tile_rows);
+    return check_launch("goalscore_wave_kernel");
+  }
   if (a->atomic)
     hipLaunchKernelGGL((goalscore_kernel<true>), dim3((unsigned)a->n_segments), dim3(GS_THREADS), 0, st,
                        *a, blk, (int64_t)i64_out->n_cols, (int64_t)col, i64_out->tile_rows);
@@ -1118,12 +1662,13 @@ static int launch_formula(const sa_actions* a, const T* ps, const T* pc, T* off,
   constexpr int V = 16 / sizeof(T);
   const int64_t lanes = (a->n + V - 1) / V;
   const dim3 grid((unsigned)((lanes + 255) / 256)), block(256);
+  const bool vec_ok = SA_FORMULA_VEC && aligned16(ps) && aligned16(pc);
   if (a->atomic)
     hipLaunchKernelGGL((formula_kernel<true, T>), grid, block, 0, (hipStream_t)stream, *a, ps, pc, off,
-                       def, val);
+                       def, val, vec_ok);
   else
     hipLaunchKernelGGL((formula_kernel<false, T>), grid, block, 0, (hipStream_t)stream, *a, ps, pc,
-                       off, def, val);
+                       off, def, val, vec_ok);
   return check_launch("formula_kernel");
 }
 
