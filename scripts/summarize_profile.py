@@ -20,7 +20,7 @@ import pandas as pd
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def main(tag: str, n_actions: int, dominant: str = 'bool_features_kernel') -> None:
+def main(tag: str, n_actions: int, dominant: str = 'bool_colgroup_kernel') -> None:
     out = os.path.join(ROOT, 'profiles')
     src = os.path.join(ROOT, 'gpurun_out')
     shutil.copy(os.path.join(src, f'prof_{tag}_trace', 'run_kernel_stats.csv'),
@@ -48,4 +48,4 @@ def main(tag: str, n_actions: int, dominant: str = 'bool_features_kernel') -> No
 
 if __name__ == '__main__':
     main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 15992198,
-         sys.argv[3] if len(sys.argv) > 3 else 'bool_features_kernel')
+         sys.argv[3] if len(sys.argv) > 3 else 'bool_colgroup_kernel')
