@@ -97,6 +97,80 @@ def xt_extra(d, ab, dist, dev, reps: int = 3) -> dict:
             'actions_per_s_per_gpu': round(ab.n / dt, 1)}
 
 
+ATOMIC_DEFAULT = ['actiontype', 'actiontype_onehot', 'bodypart', 'bodypart_onehot', 'time',
+                  'team', 'time_delta', 'location', 'polar', 'movement_polar', 'direction',
+                  'goalscore']
+
+
+def _events_ms(fn, reps: int) -> float:
+    """Mean ms of ``fn`` over ``reps`` back-to-back calls (HIP events, current stream)."""
+    fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / reps
+
+
+def atomic_extra(dist, rank, world, dev, games: int, reps: int = 5) -> dict:
+    """BASELINE cfg3 alongside the main line: Atomic-VAEP features (k=3, default xfns, 154
+    columns) + labels, ``games`` synthetic atomic games (~5M atomic actions) per rank."""
+    d = synthetic.atomic_games(games, game_id0=rank * games)
+    ab = B.ActionBatch.from_columns(d, atomic=True, dev=dev)
+    out = ops.features(ab, ATOMIC_DEFAULT, 3, bool_tile=1024, num_tile=128)
+    lab = ops.labels(ab)
+
+    def step():
+        ops.features(ab, ATOMIC_DEFAULT, 3, out=out)
+        ops.labels(ab, 10, lab)
+    ms = _events_ms(step, reps)
+    n, total, wall = ab.n, ab.n, ms
+    if dist is not None:
+        wall = _reduce(dist, ms, dist.ReduceOp.MAX, dev)
+        total = int(_reduce(dist, n, dist.ReduceOp.SUM, dev))
+    p = out.plan
+    bpa = 47 + p.n_bool + 8 * (p.n_f64 + p.n_i64) + 2
+    return {'workload': 'cfg3: Atomic-VAEP features (k=3, default xfns, 154 cols) + labels',
+            'atomic_actions_per_gpu': n, 'ms_per_step': round(wall, 4),
+            'atomic_actions_per_s': round(total / wall * 1e3, 1), 'bytes_per_action': bpa,
+            'frac_of_8TBs_per_gpu': round(bpa * n / ms * 1e-6 / HBM_PEAK_GBS, 4)}
+
+
+def xt105_extra(ab, dist, dev) -> dict:
+    """BASELINE cfg5 alongside the main line: xT 105x68 fit (count pass over this rank's
+    games, RCCL all-reduce of the 7140-cell count vectors and 204 MB transition counts, value
+    iteration over the 7140^2 system) + rate(use_interpolation=True) on the 1050x680 surface."""
+    from socceraction_amd import shard
+    l, w = 105, 68
+
+    def once():
+        acc = ops.xt_zero_counts(l, w, dev)
+        ops.xt_count(ab, l, w, acc)
+        if dist is not None and dist.get_backend() == 'nccl':
+            shard.allreduce_xt_counts(acc.shot, acc.goal, acc.move, acc.trans, acc.err)
+        sol = ops.xt_solve(acc)  # synchronises
+        grid = ops.xt_interp_grid(sol.mats[3].reshape(w, l), l, w)
+        ops.xt_rate(ab, grid, 1050, 680)
+        return sol
+    once()  # warm-up (allocator, first launches)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    sol = once()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    n, total = ab.n, ab.n
+    if dist is not None:
+        dt = _reduce(dist, dt, dist.ReduceOp.MAX, dev)
+        total = int(_reduce(dist, n, dist.ReduceOp.SUM, dev))
+    return {'workload': 'cfg5: xT 105x68 fit (count + all-reduce + value iteration) + '
+                        'rate(use_interpolation=True)',
+            'actions_per_gpu': n, 'iterations': sol.n_iter, 'ms_fit_and_rate': round(dt * 1e3, 3),
+            'actions_per_s': round(total / dt, 1)}
+
+
 def cpu_baseline(d, seconds: float) -> dict:
     """The oracle port (numpy, 1 thread) on the GPU box's host, over whole games."""
     from oracle import vaep_oracle as vo
@@ -128,6 +202,10 @@ def main() -> None:
     ap.add_argument('--cpu-seconds', type=float, default=15.0)
     ap.add_argument('--no-cpu', action='store_true')
     ap.add_argument('--no-xt', action='store_true', help='skip the cfg4 xT side measurement')
+    ap.add_argument('--no-side', action='store_true',
+                    help='skip the cfg3 (atomic) and cfg5 (xT 105x68) side measurements')
+    ap.add_argument('--atomic-games', type=int, default=1250,
+                    help='atomic games per GPU for cfg3 (1250 ~ 5M atomic actions)')
     ap.add_argument('--bool-tile', type=int, default=1024,
                     help='rows per bool-block tile (0 = one tile: plain column-major)')
     ap.add_argument('--num-tile', type=int, default=128,
@@ -201,6 +279,10 @@ def main() -> None:
         wall = _reduce(dist, wall, dist.ReduceOp.MAX, dev)
         total_actions = int(_reduce(dist, n, dist.ReduceOp.SUM, dev))
     extra_xt = xt_extra(d, ab, dist, dev) if not args.no_xt else None
+    extra_side = {}
+    if not args.no_side:
+        extra_side['xt105_cfg5'] = xt105_extra(ab, dist, dev)
+        extra_side['atomic_cfg3'] = atomic_extra(dist, rank, world, dev, args.atomic_games)
     if rank != 0:
         if dist:
             dist.destroy_process_group()
@@ -240,6 +322,7 @@ def main() -> None:
     }
     if extra_xt is not None:
         line['xt_cfg4'] = extra_xt
+    line.update(extra_side)
     if not args.no_cpu:
         line['cpu_baseline'] = cpu_baseline(d, args.cpu_seconds)
     print(json.dumps(line), flush=True)
