@@ -202,6 +202,63 @@ int sa_xt_interp_grid(const double* xT, const double* cx, const double* cy, int3
 int sa_xt_rate(const sa_actions* a, const double* grid, int32_t L, int32_t W, double* out,
                int32_t* err_flags, void* stream);
 
+/* ---- SPADL -> Atomic-SPADL (atomic/spadl/base.py:15-235) ------------------------
+ * Replaces convert_to_atomic: the four insertion passes (_extra_from_passes :38-112,
+ * spadl/base.py _add_dribbles :54-93, _extra_from_shots :115-165, _extra_from_fouls
+ * :168-196), each followed in the reference by a stable sort on (game_id, period_id,
+ * action_id), then _convert_columns (:199-220) and _simplify (:223-235).  Every inserted row
+ * lands right after the row that produced it, so the whole conversion is one expansion of
+ * each input row r (in sorted order) into 1..5 output rows that depends only on r, its
+ * input-order successor (first pass) and its sorted-order successor (later passes).
+ *
+ * Input: SPADL actions as device columns of length n.  game / team / player / event are
+ * int32 equality codes of game_id / team_id / player_id / original_event_id (the caller
+ * factorises them and decodes the output codes; event -1 = missing).  `order` lists the rows
+ * in (game_id, period_id, action_id) order (a stable sort; the keys must be unique), or is
+ * NULL when the rows are already in that order. */
+typedef struct sa_spadl_frame {
+  int64_t n;
+  const double* time_seconds;
+  const double* start_x;
+  const double* start_y;
+  const double* end_x;
+  const double* end_y;
+  const int32_t* game;
+  const int32_t* team;
+  const int32_t* player;
+  const int32_t* event;
+  const uint8_t* period_id;   /* 1..5 */
+  const uint8_t* type_id;     /* SPADL 0..22 */
+  const uint8_t* result_id;   /* 0..5 */
+  const uint8_t* bodypart_id; /* 0..3 */
+  const int64_t* order;       /* [n] or NULL */
+} sa_spadl_frame;
+
+/* Atomic-SPADL output columns (device, length n_out); action_id is the row position. */
+typedef struct sa_atomic_frame {
+  double* time_seconds;
+  double* x;
+  double* y;
+  double* dx;
+  double* dy;
+  int32_t* game;
+  int32_t* team;
+  int32_t* player;
+  int32_t* event;             /* -1 = missing (the dribbles of _add_dribbles) */
+  uint8_t* period_id;
+  uint8_t* type_id;           /* Atomic-SPADL 0..32 */
+  uint8_t* bodypart_id;
+} sa_atomic_frame;
+
+/* Device scratch the two calls below share (bytes, 16-byte aligned). */
+int64_t sa_atomic_scratch_bytes(int64_t n);
+/* Pass 1: the output row count of every 1024-row block and their exclusive prefix;
+ * *n_out [host] receives the total.  Synchronises the stream. */
+int sa_atomic_count(const sa_spadl_frame* in, void* scratch, int64_t* n_out, void* stream);
+/* Pass 2: writes the n_out output rows (scratch from sa_atomic_count, same input). */
+int sa_atomic_emit(const sa_spadl_frame* in, const void* scratch, const sa_atomic_frame* out,
+                   void* stream);
+
 /* ---- misc -------------------------------------------------------------------- */
 int sa_abi_version(void);
 const char* sa_last_error(void);

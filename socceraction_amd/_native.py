@@ -56,6 +56,19 @@ class SaBlock(ctypes.Structure):
                 ('tile_rows', ctypes.c_int64)]
 
 
+class SaSpadlFrame(ctypes.Structure):
+    _fields_ = [('n', ctypes.c_int64), ('time_seconds', _p), ('start_x', _p), ('start_y', _p),
+                ('end_x', _p), ('end_y', _p), ('game', _p), ('team', _p), ('player', _p),
+                ('event', _p), ('period_id', _p), ('type_id', _p), ('result_id', _p),
+                ('bodypart_id', _p), ('order', _p)]
+
+
+class SaAtomicFrame(ctypes.Structure):
+    _fields_ = [('time_seconds', _p), ('x', _p), ('y', _p), ('dx', _p), ('dy', _p),
+                ('game', _p), ('team', _p), ('player', _p), ('event', _p), ('period_id', _p),
+                ('type_id', _p), ('bodypart_id', _p)]
+
+
 # name -> (restype, argtypes)
 _SIGNATURES = {
     'sa_vaep_features': (ctypes.c_int, [ctypes.POINTER(SaActions), ctypes.POINTER(SaFeaturePlan),
@@ -78,6 +91,11 @@ _SIGNATURES = {
                                          ctypes.c_int32, _p, ctypes.c_int32, _p, _p]),
     'sa_xt_rate': (ctypes.c_int, [ctypes.POINTER(SaActions), _p, ctypes.c_int32, ctypes.c_int32,
                                   _p, _p, _p]),
+    'sa_atomic_scratch_bytes': (ctypes.c_int64, [ctypes.c_int64]),
+    'sa_atomic_count': (ctypes.c_int, [ctypes.POINTER(SaSpadlFrame), _p,
+                                       ctypes.POINTER(ctypes.c_int64), _p]),
+    'sa_atomic_emit': (ctypes.c_int, [ctypes.POINTER(SaSpadlFrame), _p,
+                                      ctypes.POINTER(SaAtomicFrame), _p]),
     'sa_abi_version': (ctypes.c_int, []),
     'sa_last_error': (ctypes.c_char_p, []),
 }

@@ -1,0 +1,223 @@
+"""SPADL -> Atomic-SPADL conversion on MI355X (drop-in for ``socceraction.atomic.spadl.base``).
+
+``convert_to_atomic`` (reference atomic/spadl/base.py:15-35) runs as one device expansion:
+the SPADL frame is flattened once into HBM columns (ids as int32 equality codes), one
+kernel counts how many Atomic-SPADL rows each input row becomes, one scans those counts and
+one writes the rows (``sa_atomic_count`` / ``sa_atomic_emit``, socceraction_amd/csrc/
+sa_atomic.hip). The host only factorises the id columns, decodes the output codes and
+builds the DataFrame. The reference's four concat + sort passes collapse into this single
+expansion because every inserted row lands directly after the row that produced it (see
+the kernel's header comment); the numpy restatement of the four passes in
+``oracle/atomic_convert_oracle.py`` and the reference's own outputs
+(``tests/golden/convert_*.npz``) are the parity checks.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import Dict, Optional, Tuple
+
+import numpy as np
+import pandas as pd
+import torch
+
+from ... import _native
+from ...batch import device, stream_handle
+
+_REQUIRED = ('game_id', 'original_event_id', 'action_id', 'period_id', 'time_seconds',
+             'team_id', 'player_id', 'start_x', 'start_y', 'end_x', 'end_y', 'type_id',
+             'result_id', 'bodypart_id')
+_OUT = ('game_id', 'original_event_id', 'action_id', 'period_id', 'time_seconds', 'team_id',
+        'player_id', 'x', 'y', 'dx', 'dy', 'type_id', 'bodypart_id')
+_ALIGN = 256
+
+
+def _pack(arrays: Dict[str, np.ndarray], dev) -> Tuple[torch.Tensor, Dict[str, torch.Tensor]]:
+    """One device allocation holding every array at 256-byte aligned offsets (one H2D copy)."""
+    offs, total = {}, 0
+    for k, a in arrays.items():
+        offs[k] = total
+        total += (max(a.nbytes, 16) + _ALIGN - 1) // _ALIGN * _ALIGN
+    host = np.zeros(max(total, _ALIGN), dtype=np.uint8)
+    for k, a in arrays.items():
+        host[offs[k]:offs[k] + a.nbytes] = np.ascontiguousarray(a).view(np.uint8).reshape(-1)
+    buf = torch.from_numpy(host).to(dev)
+    views = {k: buf[offs[k]:offs[k] + max(a.nbytes, a.itemsize)].view(torch.from_numpy(a[:0]).dtype)
+             for k, a in arrays.items()}
+    return buf, views
+
+
+def _codes(values, sort: bool = False) -> Tuple[np.ndarray, pd.Index]:
+    codes, uniques = pd.factorize(pd.Series(values), sort=sort, use_na_sentinel=True)
+    return codes.astype(np.int32), pd.Index(uniques)
+
+
+def _ids(df: pd.DataFrame, col: str, lo: int, hi: int) -> np.ndarray:
+    v = df[col].to_numpy()
+    if v.dtype.kind == 'f':
+        if np.isnan(v).any() or (v != np.floor(v)).any():
+            raise ValueError(f'{col} must hold integers')
+    if len(v) and (v.min() < lo or v.max() > hi):
+        raise ValueError(f'{col} values must lie in [{lo}, {hi}] (SPADL schema isin check)')
+    return v.astype(np.uint8)
+
+
+def _sorted_order(g: np.ndarray, per: np.ndarray, aid: np.ndarray) -> Optional[np.ndarray]:
+    """None when the rows already are in (game_id, period_id, action_id) order, else the
+    stable sort permutation the reference's sort_values applies (base.py:110). Equal keys
+    would let the reference interleave inserted rows of different parents: rejected."""
+    n = len(g)
+    if n < 2:
+        return None
+    aid = np.asarray(aid)
+    if aid.dtype.kind not in 'iuf':
+        raise ValueError('action_id must be numeric')
+
+    def strictly_increasing(gg, pp, aa):
+        d_g, d_p, d_a = np.diff(gg.astype(np.int64)), np.diff(pp.astype(np.int64)), np.diff(aa)
+        return bool(((d_g > 0) | ((d_g == 0) & ((d_p > 0) | ((d_p == 0) & (d_a > 0))))).all())
+
+    if strictly_increasing(g, per, aid):
+        return None
+    order = np.lexsort((aid, per, g)).astype(np.int64)
+    if not strictly_increasing(g[order], per[order], aid[order]):
+        raise ValueError('duplicate (game_id, period_id, action_id) keys are not supported')
+    return order
+
+
+@dataclass
+class SpadlFrame:
+    """A SPADL frame in HBM (``sa_spadl_frame``) plus the host tables decoding its codes."""
+
+    n: int
+    buffer: torch.Tensor
+    cols: Dict[str, torch.Tensor]
+    uniques: Dict[str, pd.Index]
+    dtypes: Dict[str, np.dtype]
+
+    @classmethod
+    def from_frame(cls, actions: pd.DataFrame, dev=None) -> 'SpadlFrame':
+        for c in _REQUIRED:
+            if c not in actions.columns:
+                raise AttributeError(f"'DataFrame' object has no attribute '{c}'")
+        dev = dev or device()
+        n = len(actions)
+        g, gu = _codes(actions['game_id'].to_numpy(), sort=True)  # order-preserving codes
+        if (g < 0).any():
+            raise ValueError('game_id contains missing values')
+        t, tu = _codes(actions['team_id'].to_numpy())
+        p, pu = _codes(actions['player_id'].to_numpy())
+        e, eu = _codes(actions['original_event_id'].to_numpy())  # missing -> -1
+        per = _ids(actions, 'period_id', 1, 5)
+        arrays = {
+            'time_seconds': actions['time_seconds'].to_numpy(np.float64),
+            'start_x': actions['start_x'].to_numpy(np.float64),
+            'start_y': actions['start_y'].to_numpy(np.float64),
+            'end_x': actions['end_x'].to_numpy(np.float64),
+            'end_y': actions['end_y'].to_numpy(np.float64),
+            'game': g, 'team': t, 'player': p, 'event': e,
+            'period_id': per,
+            'type_id': _ids(actions, 'type_id', 0, 22),
+            'result_id': _ids(actions, 'result_id', 0, 5),
+            'bodypart_id': _ids(actions, 'bodypart_id', 0, 3),
+        }
+        order = _sorted_order(g, per, actions['action_id'].to_numpy())
+        if order is not None:
+            arrays['order'] = order
+        buf, views = _pack(arrays, dev)
+        dtypes = {c: actions[c].dtype for c in ('game_id', 'team_id', 'player_id')}
+        return cls(n, buf, views, {'game': gu, 'team': tu, 'player': pu, 'event': eu}, dtypes)
+
+    def struct(self) -> _native.SaSpadlFrame:
+        s = _native.SaSpadlFrame()
+        s.n = self.n
+        for name in ('time_seconds', 'start_x', 'start_y', 'end_x', 'end_y', 'game', 'team',
+                     'player', 'event', 'period_id', 'type_id', 'result_id', 'bodypart_id'):
+            setattr(s, name, self.cols[name].data_ptr())
+        s.order = self.cols['order'].data_ptr() if 'order' in self.cols else None
+        return s
+
+
+@dataclass
+class AtomicColumns:
+    """Atomic-SPADL rows in HBM (``sa_atomic_frame``), codes as in the source SpadlFrame."""
+
+    n: int
+    buffer: torch.Tensor
+    cols: Dict[str, torch.Tensor]
+
+    def struct(self) -> _native.SaAtomicFrame:
+        s = _native.SaAtomicFrame()
+        for name in ('time_seconds', 'x', 'y', 'dx', 'dy', 'game', 'team', 'player', 'event',
+                     'period_id', 'type_id', 'bodypart_id'):
+            setattr(s, name, self.cols[name].data_ptr())
+        return s
+
+
+def convert_device(frame: SpadlFrame) -> AtomicColumns:
+    """Run the conversion on device; the result stays in HBM."""
+    lib = _native.lib()
+    dev = frame.buffer.device
+    s = frame.struct()
+    scratch = torch.empty(max(int(lib.sa_atomic_scratch_bytes(frame.n)), 16), dtype=torch.uint8,
+                          device=dev)
+    n_out = ctypes.c_int64(0)
+    _native.check(lib.sa_atomic_count(ctypes.byref(s), scratch.data_ptr(), ctypes.byref(n_out),
+                                      stream_handle()))
+    m = int(n_out.value)
+    spec = {'time_seconds': np.float64, 'x': np.float64, 'y': np.float64, 'dx': np.float64,
+            'dy': np.float64, 'game': np.int32, 'team': np.int32, 'player': np.int32,
+            'event': np.int32, 'period_id': np.uint8, 'type_id': np.uint8, 'bodypart_id': np.uint8}
+    buf, cols = _pack({k: np.empty(max(m, 1), dt) for k, dt in spec.items()}, dev)
+    out = AtomicColumns(m, buf, cols)
+    if m:
+        o = out.struct()
+        _native.check(lib.sa_atomic_emit(ctypes.byref(s), scratch.data_ptr(), ctypes.byref(o),
+                                         stream_handle()))
+    return out
+
+
+def _decode(codes: np.ndarray, uniques: pd.Index, dtype, missing=None) -> np.ndarray:
+    """Ids back from their codes (code -1 -> ``missing``)."""
+    neg = codes < 0
+    if len(uniques) == 0:
+        return np.full(len(codes), missing, dtype=object)
+    vals = uniques.take(np.where(neg, 0, codes)).to_numpy()
+    if neg.any():
+        vals = vals.astype(object)
+        vals[neg] = missing
+    elif dtype is not None and vals.dtype != dtype:
+        vals = vals.astype(dtype)
+    return vals
+
+
+def convert_to_atomic(actions: pd.DataFrame) -> pd.DataFrame:
+    """Convert regular SPADL actions to Atomic-SPADL actions (reference base.py:15-35)."""
+    for c in _REQUIRED:
+        if c not in actions.columns:
+            raise AttributeError(f"'DataFrame' object has no attribute '{c}'")
+    if len(actions) == 0:
+        cols = {c: np.zeros(0, np.int64) for c in _OUT}
+        for c in ('game_id', 'team_id', 'player_id'):
+            cols[c] = actions[c].to_numpy()[:0]
+        for c in ('time_seconds', 'x', 'y', 'dx', 'dy'):
+            cols[c] = np.zeros(0, np.float64)
+        cols['original_event_id'] = np.zeros(0, dtype=object)
+        return pd.DataFrame(cols, columns=list(_OUT))
+    frame = SpadlFrame.from_frame(actions)
+    out = convert_device(frame)
+    host = {k: v[:out.n].cpu().numpy() for k, v in out.cols.items()}
+    u = frame.uniques
+    res = {
+        'game_id': _decode(host['game'], u['game'], frame.dtypes['game_id']),
+        'original_event_id': _decode(host['event'], u['event'], None, missing=np.nan).astype(object),
+        'action_id': np.arange(out.n, dtype=np.int64),
+        'period_id': host['period_id'].astype(np.int64),
+        'time_seconds': host['time_seconds'],
+        'team_id': _decode(host['team'], u['team'], frame.dtypes['team_id']),
+        'player_id': _decode(host['player'], u['player'], frame.dtypes['player_id']),
+        'x': host['x'], 'y': host['y'], 'dx': host['dx'], 'dy': host['dy'],
+        'type_id': host['type_id'].astype(np.int64),
+        'bodypart_id': host['bodypart_id'].astype(np.int64),
+    }
+    return pd.DataFrame(res, columns=list(_OUT))

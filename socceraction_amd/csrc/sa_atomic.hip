@@ -1,0 +1,320 @@
+// SPADL -> Atomic-SPADL conversion on gfx950 (reference: socceraction/atomic/spadl/base.py).
+//
+// The reference runs four insertion passes, each a concat + stable sort on (game_id,
+// period_id, action_id) + action_id reset.  Every inserted row carries its parent's
+// action_id + 0.1 (and, for a dribble, the successor's game / period, which equal the
+// parent's position in sorted order), so it always lands directly after its parent.  Hence
+// row r of the (sorted) input expands into the fixed sequence
+//
+//     r, x4(r)?, x3(r)?, dA(r)?, e1(r)?, dB(r)?
+//
+//   e1  _extra_from_passes  (base.py:38-112)   r and its INPUT-order successor q
+//   dA  _add_dribbles        (spadl/base.py:54-93) r -> r'   (only without e1: e1 starts
+//                            where r ends, so r -> e1 is never far enough for a dribble)
+//   dB  _add_dribbles        e1 -> r'
+//   x3  _extra_from_shots    (base.py:115-165)  goal / owngoal / shot followed by a corner or
+//                            goalkick (the row after r is dA, e1 or r'; only r' can be one)
+//   x4  _extra_from_fouls    (base.py:168-196)  yellow / red card
+//
+// where r' is r's successor in sorted order.  Inserted rows never qualify for a later pass
+// (results -1 / success, non-shot types), which is why the sequence stops at five.  One
+// kernel counts each block's output rows, one scans the block totals, one writes the rows
+// (block scan + the block's prefix).  Everything is exact: the only arithmetic is the
+// reference's own (midpoint times, squared distances, end - start) in f64 with
+// -ffp-contract=off.
+#include <hip/hip_runtime.h>
+
+#include "sa_common.h"
+#include "sa_internal.h"
+
+namespace sa {
+
+constexpr int AC_THREADS = 256;
+constexpr int AC_PER_THREAD = 4;
+constexpr int AC_BLOCK_ROWS = AC_THREADS * AC_PER_THREAD;  // 1024 sorted rows per block
+
+// atomic/spadl/config.py:25-36 ids; `actiontypes.index('interception')` is the FIRST
+// position, 10 (base.py:96-99)
+constexpr int A_DRIBBLE = 21, A_RECEIVAL = 23, A_INTERCEPTION = 10, A_OUT = 25, A_OFFSIDE = 26,
+              A_GOAL = 27, A_OWNGOAL = 28, A_YELLOW = 29, A_RED = 30, A_CORNER = 31,
+              A_FREEKICK = 32;
+constexpr int T_THROW_IN = 2, T_GOALKICK = 22;
+
+struct SRow {
+  double t, sx, sy, ex, ey;
+  int32_t game, team, player, event;
+  int per, type, res, bp;
+};
+
+__device__ __forceinline__ SRow load_srow(const sa_spadl_frame& F, int64_t r) {
+  SRow o;
+  o.t = F.time_seconds[r];
+  o.sx = F.start_x[r];
+  o.sy = F.start_y[r];
+  o.ex = F.end_x[r];
+  o.ey = F.end_y[r];
+  o.game = F.game[r];
+  o.team = F.team[r];
+  o.player = F.player[r];
+  o.event = F.event[r];
+  o.per = F.period_id[r];
+  o.type = F.type_id[r];
+  o.res = F.result_id[r];
+  o.bp = F.bodypart_id[r];
+  return o;
+}
+
+__device__ __forceinline__ bool is_passlike(int t) {  // base.py:42-53
+  return t == 0 || t == 1 || t == 2 || t == 3 || t == 4 || t == 5 || t == 6 || t == 18 || t == 22;
+}
+__device__ __forceinline__ bool is_interceptionlike(int t) {  // base.py:55-63
+  return t == 10 || t == 9 || t == 16 || t == 14 || t == 15 || t == 17;
+}
+__device__ __forceinline__ bool is_shot(int t) { return t == 11 || t == 12 || t == 13; }
+
+// _add_dribbles predicate for an action ending at (ex, ey) by `team` at time t in period
+// `per`, followed by row n (spadl/base.py:57-69)
+__device__ __forceinline__ bool dribble(double ex, double ey, int32_t team, double t, int per,
+                                        const SRow& n) {
+  const double dx = ex - n.sx, dy = ey - n.sy;
+  const double d2 = dx * dx + dy * dy;
+  const double dt = n.t - t;
+  return team == n.team && d2 >= 9.0 && d2 <= 3600.0 && dt < 10.0 && per == n.per;
+}
+
+enum { G_X4 = 1, G_X3 = 2, G_DA = 4, G_E1 = 8, G_DB = 16 };
+
+struct Group {
+  SRow r, rp;  // the row and its sorted successor
+  uint32_t mask;
+  int x4_type, x3_type, e1_type;
+  int32_t e1_team, e1_player;
+  double e1_t;
+};
+
+__device__ __forceinline__ Group group_at(const sa_spadl_frame& F, int64_t p) {
+  const int64_t n = F.n;
+  Group G;
+  const int64_t r = F.order ? F.order[p] : p;
+  G.r = load_srow(F, r);
+  const bool has_rp = p + 1 < n;
+  if (has_rp) G.rp = load_srow(F, F.order ? F.order[p + 1] : p + 1);
+  const SRow& R = G.r;
+  G.mask = 0;
+  // e1: pass-like action followed (in INPUT order) by a non-interception in the same game
+  // and period
+  const bool has_q = r + 1 < n;
+  if (has_q && is_passlike(R.type)) {
+    const SRow Q = (F.order == nullptr && has_rp) ? G.rp : load_srow(F, r + 1);
+    if (Q.game == R.game && Q.per == R.per && !is_interceptionlike(Q.type)) {
+      const bool st = Q.team == R.team;
+      const bool out = (Q.type == T_GOALKICK && !st) || Q.type == T_THROW_IN;
+      const bool offside = R.res == 2;
+      int t = st ? A_RECEIVAL : A_INTERCEPTION;
+      if (out) t = A_OUT;
+      if (offside) t = A_OFFSIDE;
+      G.mask |= G_E1;
+      G.e1_type = t;
+      G.e1_team = t == A_INTERCEPTION ? Q.team : R.team;
+      G.e1_player = (out || offside) ? R.player : Q.player;
+      G.e1_t = (R.t + Q.t) / 2;
+    }
+  }
+  if (has_rp) {
+    if (G.mask & G_E1) {
+      if (dribble(R.ex, R.ey, G.e1_team, G.e1_t, R.per, G.rp)) G.mask |= G_DB;
+    } else if (dribble(R.ex, R.ey, R.team, R.t, R.per, G.rp)) {
+      G.mask |= G_DA;
+    }
+  }
+  const bool shot = is_shot(R.type);
+  const bool goal = shot && R.res == 1;
+  const bool owngoal = R.res == 3;
+  const bool out3 = shot && has_rp && !(G.mask & (G_DA | G_E1)) &&
+                    (G.rp.type == 5 || G.rp.type == 6 || G.rp.type == T_GOALKICK) &&
+                    G.rp.game == R.game && G.rp.per == R.per;
+  if (goal || owngoal || out3) {
+    G.mask |= G_X3;
+    G.x3_type = owngoal ? A_OWNGOAL : (goal ? A_GOAL : A_OUT);
+  }
+  if (R.res == 4 || R.res == 5) {
+    G.mask |= G_X4;
+    G.x4_type = R.res == 5 ? A_RED : A_YELLOW;
+  }
+  return G;
+}
+
+__device__ __forceinline__ int group_size(uint32_t mask) { return 1 + __popc(mask); }
+
+__device__ __forceinline__ int simplify(int t) {  // base.py:223-235
+  if (t == 5 || t == 6) return A_CORNER;
+  if (t == 3 || t == 4 || t == 13) return A_FREEKICK;
+  return t;
+}
+
+__device__ __forceinline__ void put(const sa_atomic_frame& O, int64_t k, double t, double x, double y,
+                                    double dx, double dy, int32_t game, int32_t team, int32_t player,
+                                    int32_t event, int per, int type, int bp) {
+  O.time_seconds[k] = t;
+  O.x[k] = x;
+  O.y[k] = y;
+  O.dx[k] = dx;
+  O.dy[k] = dy;
+  O.game[k] = game;
+  O.team[k] = team;
+  O.player[k] = player;
+  O.event[k] = event;
+  O.period_id[k] = (uint8_t)per;
+  O.type_id[k] = (uint8_t)type;
+  O.bodypart_id[k] = (uint8_t)bp;
+}
+
+// exclusive block scan of one int per thread (256 threads = 4 waves)
+__device__ __forceinline__ int64_t block_excl_scan(int64_t v, int64_t* wsum, int64_t& total) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int64_t incl = v;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int64_t y = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += y;
+  }
+  if (lane == 63) wsum[wv] = incl;
+  __syncthreads();
+  int64_t pre = 0;
+  total = 0;
+#pragma unroll
+  for (int k = 0; k < AC_THREADS / 64; ++k) {
+    pre += k < wv ? wsum[k] : 0;
+    total += wsum[k];
+  }
+  return pre + incl - v;
+}
+
+__global__ __launch_bounds__(AC_THREADS) void atomic_count_kernel(sa_spadl_frame F, int64_t* __restrict__ bsum) {
+  __shared__ int64_t wsum[AC_THREADS / 64];
+  const int64_t p0 = (int64_t)blockIdx.x * AC_BLOCK_ROWS + (int64_t)threadIdx.x * AC_PER_THREAD;
+  int64_t c = 0;
+#pragma unroll
+  for (int k = 0; k < AC_PER_THREAD; ++k)
+    if (p0 + k < F.n) c += group_size(group_at(F, p0 + k).mask);
+  int64_t total;
+  block_excl_scan(c, wsum, total);
+  if (threadIdx.x == 0) bsum[blockIdx.x] = total;
+}
+
+// exclusive prefix of the block totals, in place; bsum[nb] = grand total (one workgroup)
+__global__ __launch_bounds__(1024) void atomic_scan_kernel(int64_t* __restrict__ bsum, int64_t nb) {
+  __shared__ int64_t part[1024];
+  const int64_t per = (nb + 1023) / 1024;
+  const int64_t b0 = (int64_t)threadIdx.x * per;
+  int64_t s = 0;
+  for (int64_t b = b0; b < b0 + per && b < nb; ++b) s += bsum[b];
+  part[threadIdx.x] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {  // 1024 partial sums: a sequential pass is negligible
+    int64_t acc = 0;
+    for (int k = 0; k < 1024; ++k) {
+      const int64_t v = part[k];
+      part[k] = acc;
+      acc += v;
+    }
+    bsum[nb] = acc;
+  }
+  __syncthreads();
+  int64_t acc = part[threadIdx.x];
+  for (int64_t b = b0; b < b0 + per && b < nb; ++b) {
+    const int64_t v = bsum[b];
+    bsum[b] = acc;
+    acc += v;
+  }
+}
+
+__global__ __launch_bounds__(AC_THREADS) void atomic_emit_kernel(sa_spadl_frame F, const int64_t* __restrict__ bpre,
+                                                                sa_atomic_frame O) {
+  __shared__ int64_t wsum[AC_THREADS / 64];
+  const int64_t p0 = (int64_t)blockIdx.x * AC_BLOCK_ROWS + (int64_t)threadIdx.x * AC_PER_THREAD;
+  int64_t c = 0;
+#pragma unroll
+  for (int k = 0; k < AC_PER_THREAD; ++k)
+    if (p0 + k < F.n) c += group_size(group_at(F, p0 + k).mask);
+  int64_t total;
+  int64_t o = bpre[blockIdx.x] + block_excl_scan(c, wsum, total);
+  for (int k = 0; k < AC_PER_THREAD; ++k) {
+    if (p0 + k >= F.n) break;
+    const Group G = group_at(F, p0 + k);
+    const SRow& R = G.r;
+    const SRow& N = G.rp;
+    // r itself (_convert_columns: x, y = start; dx, dy = end - start)
+    put(O, o++, R.t, R.sx, R.sy, R.ex - R.sx, R.ey - R.sy, R.game, R.team, R.player, R.event, R.per,
+        simplify(R.type), R.bp);
+    if (G.mask & G_X4)  // card: start = end = r's end, r's time / bodypart / team / player
+      put(O, o++, R.t, R.ex, R.ey, R.ex - R.ex, R.ey - R.ey, R.game, R.team, R.player, R.event, R.per,
+          G.x4_type, R.bp);
+    if (G.mask & G_X3)  // out / goal / owngoal: same shape
+      put(O, o++, R.t, R.ex, R.ey, R.ex - R.ex, R.ey - R.ey, R.game, R.team, R.player, R.event, R.per,
+          G.x3_type, R.bp);
+    if (G.mask & G_DA)  // dribble r -> r': the successor's game, period, team, player; no event
+      put(O, o++, (R.t + N.t) / 2, R.ex, R.ey, N.sx - R.ex, N.sy - R.ey, N.game, N.team, N.player, -1,
+          N.per, A_DRIBBLE, 0);
+    if (G.mask & G_E1)  // receival / interception / out / offside at r's end, foot
+      put(O, o++, G.e1_t, R.ex, R.ey, R.ex - R.ex, R.ey - R.ey, R.game, G.e1_team, G.e1_player, R.event,
+          R.per, G.e1_type, 0);
+    if (G.mask & G_DB)  // dribble e1 -> r'
+      put(O, o++, (G.e1_t + N.t) / 2, R.ex, R.ey, N.sx - R.ex, N.sy - R.ey, N.game, N.team, N.player,
+          -1, N.per, A_DRIBBLE, 0);
+  }
+}
+
+}  // namespace sa
+
+// ================================== C ABI =================================================
+using namespace sa;
+
+static int64_t n_blocks(int64_t n) { return (n + AC_BLOCK_ROWS - 1) / AC_BLOCK_ROWS; }
+
+extern "C" int64_t sa_atomic_scratch_bytes(int64_t n) {
+  return n < 0 ? 0 : (n_blocks(n) + 1) * (int64_t)sizeof(int64_t);
+}
+
+static int check_spadl_frame(const sa_spadl_frame* F) {
+  if (!F || F->n < 0) return fail(SA_EINVAL, "bad sa_spadl_frame");
+  if (F->n > 0 && (!F->time_seconds || !F->start_x || !F->start_y || !F->end_x || !F->end_y ||
+                   !F->game || !F->team || !F->player || !F->event || !F->period_id ||
+                   !F->type_id || !F->result_id || !F->bodypart_id))
+    return fail(SA_EINVAL, "sa_spadl_frame has a null column");
+  return SA_OK;
+}
+
+extern "C" int sa_atomic_count(const sa_spadl_frame* in, void* scratch, int64_t* n_out, void* stream) {
+  int rc = check_spadl_frame(in);
+  if (rc) return rc;
+  if (!n_out || (in->n > 0 && !scratch)) return fail(SA_EINVAL, "null scratch or n_out");
+  *n_out = 0;
+  if (in->n == 0) return SA_OK;
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t nb = n_blocks(in->n);
+  int64_t* bsum = (int64_t*)scratch;
+  hipLaunchKernelGGL(atomic_count_kernel, dim3((unsigned)nb), dim3(AC_THREADS), 0, st, *in, bsum);
+  if ((rc = check_launch("atomic_count_kernel"))) return rc;
+  hipLaunchKernelGGL(atomic_scan_kernel, dim3(1), dim3(1024), 0, st, bsum, nb);
+  if ((rc = check_launch("atomic_scan_kernel"))) return rc;
+  if ((rc = check_hip(hipMemcpyAsync(n_out, bsum + nb, sizeof(int64_t), hipMemcpyDeviceToHost, st),
+                      "copy n_out")))
+    return rc;
+  return check_hip(hipStreamSynchronize(st), "hipStreamSynchronize");
+}
+
+extern "C" int sa_atomic_emit(const sa_spadl_frame* in, const void* scratch, const sa_atomic_frame* out,
+                              void* stream) {
+  int rc = check_spadl_frame(in);
+  if (rc) return rc;
+  if (in->n == 0) return SA_OK;
+  if (!scratch || !out || !out->time_seconds || !out->x || !out->y || !out->dx || !out->dy ||
+      !out->game || !out->team || !out->player || !out->event || !out->period_id || !out->type_id ||
+      !out->bodypart_id)
+    return fail(SA_EINVAL, "null scratch or output column");
+  const int64_t nb = n_blocks(in->n);
+  hipLaunchKernelGGL(atomic_emit_kernel, dim3((unsigned)nb), dim3(AC_THREADS), 0, (hipStream_t)stream,
+                     *in, (const int64_t*)scratch, *out);
+  return check_launch("atomic_emit_kernel");
+}

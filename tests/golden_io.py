@@ -55,3 +55,52 @@ def assert_close(a, b, name=''):
     tol = 1e-6 * np.abs(b[ok]) + 1e-12
     bad = err > tol
     assert not bad.any(), f'{name}: {bad.sum()} mismatches, max err {err.max()}'
+
+
+CONVERT_IN = ['game_id', 'original_event_id', 'action_id', 'period_id', 'time_seconds', 'team_id',
+              'player_id', 'start_x', 'start_y', 'end_x', 'end_y', 'type_id', 'result_id',
+              'bodypart_id']
+CONVERT_OUT = ['game_id', 'original_event_id', 'action_id', 'period_id', 'time_seconds',
+               'team_id', 'player_id', 'x', 'y', 'dx', 'dy', 'type_id', 'bodypart_id']
+
+
+def _convert_cols(g, prefix, names):
+    out = {}
+    for c in names:
+        v = g[prefix + c]
+        if c == 'original_event_id':
+            v = np.array([None if m else s for s, m in zip(v, g[prefix + c + '_isna'])],
+                         dtype=object)
+        out[c] = v
+    return out
+
+
+def convert_input(g):
+    """Input SPADL frame of a convert_* golden (tests/golden/make_golden_convert.py)."""
+    return pd.DataFrame(_convert_cols(g, 'in_', CONVERT_IN))
+
+
+def convert_output(g):
+    """The reference's Atomic-SPADL output of a convert_* golden as columns."""
+    return _convert_cols(g, 'out_', CONVERT_OUT)
+
+
+def assert_convert_equal(got: dict, ref: dict, name=''):
+    """Bit-exact ids / codes / counts; floats within the assert_close bar; same NaN pattern
+    of original_event_id."""
+    assert set(got) >= set(CONVERT_OUT), name
+    n = len(ref['type_id'])
+    for c in CONVERT_OUT:
+        a, b = got[c], ref[c]
+        assert len(a) == n, (name, c, len(a), n)
+        if c == 'original_event_id':
+            ma = np.array([x is None or (isinstance(x, float) and np.isnan(x)) for x in a], bool)
+            mb = np.array([x is None for x in b], bool)
+            np.testing.assert_array_equal(ma, mb, err_msg=f'{name} {c} missing pattern')
+            np.testing.assert_array_equal(np.asarray(a, object)[~ma].astype(str),
+                                          np.asarray(b, object)[~mb].astype(str), err_msg=name)
+        elif np.asarray(b).dtype.kind == 'f':
+            assert_close(a, b, f'{name} {c}')
+        else:
+            np.testing.assert_array_equal(np.asarray(a).astype(np.int64),
+                                          np.asarray(b).astype(np.int64), err_msg=f'{name} {c}')

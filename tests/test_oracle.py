@@ -80,3 +80,18 @@ def test_xt_oracle(name):
         assert_close(xo.rate(cols, g[f'{tag}_xT']), g[f'{tag}_rate'], 'rate')
         if f'{tag}_rate_interp' in g:
             assert_close(xo.rate(cols, g[f'{tag}_xT'], True), g[f'{tag}_rate_interp'], 'interp')
+
+
+@pytest.mark.parametrize('name', cases('convert'))
+def test_convert_oracle(name):
+    """oracle/atomic_convert_oracle.py == the reference's convert_to_atomic (goldens)."""
+    from golden_io import assert_convert_equal, convert_input, convert_output
+    from oracle import atomic_convert_oracle as co
+    g = load('convert', name)
+    df = convert_input(g)
+    got = co.convert_to_atomic({c: df[c].to_numpy() for c in co.COLS})
+    ref = convert_output(g)
+    assert_convert_equal(got, ref, name)
+    # floats are produced by the same operations as the reference: bit-exact here
+    for c in ('time_seconds', 'x', 'y', 'dx', 'dy'):
+        np.testing.assert_array_equal(got[c], ref[c], err_msg=f'{name} {c}')
