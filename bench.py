@@ -171,6 +171,40 @@ def xt105_extra(ab, dist, dev) -> dict:
             'actions_per_s': round(total / dt, 1)}
 
 
+def convert_extra(d, dist, dev, reps: int = 3) -> dict:
+    """SURVEY §8(f) row 1 alongside the main line: SPADL -> Atomic-SPADL conversion of this
+    rank's cfg2 games on device (count + scan + emit), then Atomic-VAEP features + labels on
+    the converted rows without leaving HBM (the producer of cfg3's input)."""
+    from socceraction_amd.atomic.spadl import base as cb
+    frame = cb.SpadlFrame.from_columns(d, dev=dev)
+    out = cb.convert_device(frame)  # warm-up
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        out = cb.convert_device(frame)
+    torch.cuda.synchronize()
+    ms_conv = (time.perf_counter() - t0) / reps * 1e3
+    ab = out.to_batch(frame, d['home_team_id'])
+    fo = ops.features(ab, ATOMIC_DEFAULT, 3, bool_tile=1024, num_tile=128)
+    lab = ops.labels(ab)
+
+    def step():
+        ops.features(ab, ATOMIC_DEFAULT, 3, out=fo)
+        ops.labels(ab, 10, lab)
+    ms_feat = _events_ms(step, reps)
+    n_in, n_out = frame.n, out.n
+    # count pass reads the 60-B input row (and its successor, cache-resident); emit reads it
+    # again and writes 59 B per atomic row
+    conv_bytes = 2 * 60 * n_in + 59 * n_out
+    return {'workload': 'SPADL -> Atomic-SPADL conversion (count + scan + emit) of the cfg2 '
+                        'games, then Atomic-VAEP features + labels on device',
+            'spadl_actions_per_gpu': n_in, 'atomic_actions_per_gpu': n_out,
+            'ms_convert_incl_host_sync': round(ms_conv, 4),
+            'convert_GBs': round(conv_bytes / ms_conv * 1e-6, 1),
+            'ms_atomic_features_labels': round(ms_feat, 4),
+            'spadl_actions_per_s_end_to_atomic_features': round(n_in / (ms_conv + ms_feat) * 1e3, 1)}
+
+
 def cpu_baseline(d, seconds: float) -> dict:
     """The oracle port (numpy, 1 thread) on the GPU box's host, over whole games."""
     from oracle import vaep_oracle as vo
@@ -283,6 +317,7 @@ def main() -> None:
     if not args.no_side:
         extra_side['xt105_cfg5'] = xt105_extra(ab, dist, dev)
         extra_side['atomic_cfg3'] = atomic_extra(dist, rank, world, dev, args.atomic_games)
+        extra_side['convert_to_atomic'] = convert_extra(d, dist, dev)
     if rank != 0:
         if dist:
             dist.destroy_process_group()

@@ -259,6 +259,12 @@ int sa_atomic_count(const sa_spadl_frame* in, void* scratch, int64_t* n_out, voi
 int sa_atomic_emit(const sa_spadl_frame* in, const void* scratch, const sa_atomic_frame* out,
                    void* stream);
 
+/* Segment (game) offsets of a row-sorted key column whose values are exactly 0..n_segments-1,
+ * each present -- e.g. the game codes of sa_atomic_emit's output:
+ * seg_off[g] = first row of g, seg_off[n_segments] = n. */
+int sa_segment_offsets(const int32_t* key, int64_t n, int64_t n_segments, int64_t* seg_off,
+                       void* stream);
+
 /* ---- misc -------------------------------------------------------------------- */
 int sa_abi_version(void);
 const char* sa_last_error(void);

@@ -152,15 +152,33 @@ def e2e(args) -> dict:
             'seconds': round(dt, 3), 'actions_per_s': round(n / dt, 1)}
 
 
+def convert(args) -> dict:
+    """SPADL -> Atomic-SPADL conversion on device (count + scan + emit), cfg2 games."""
+    from socceraction_amd.atomic.spadl import base as cb
+    dev = B.device()
+    d = synthetic.spadl_games(args.games)
+    frame = cb.SpadlFrame.from_columns(d, dev=dev)
+    out = cb.convert_device(frame)
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(args.steps):
+        out = cb.convert_device(frame)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t) / args.steps * 1e3
+    return {'workload': 'SPADL -> Atomic-SPADL conversion (device)', 'spadl_actions': frame.n,
+            'atomic_actions': out.n, 'ms_per_conversion': round(ms, 4),
+            'GBs': round((2 * 60 * frame.n + 59 * out.n) / ms * 1e-6, 1)}
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
-    ap.add_argument('workload', choices=('atomic', 'xt105', 'e2e'))
+    ap.add_argument('workload', choices=('atomic', 'xt105', 'e2e', 'convert'))
     ap.add_argument('--games', type=int, default=None)
     ap.add_argument('--steps', type=int, default=10)
     args = ap.parse_args()
     if args.games is None:
-        args.games = {'atomic': 10000, 'xt105': 7812, 'e2e': 500}[args.workload]
-    line = {'atomic': atomic, 'xt105': xt105, 'e2e': e2e}[args.workload](args)
+        args.games = {'atomic': 10000, 'xt105': 7812, 'e2e': 500, 'convert': 10000}[args.workload]
+    line = {'atomic': atomic, 'xt105': xt105, 'e2e': e2e, 'convert': convert}[args.workload](args)
     line['device'] = torch.cuda.get_device_name(0)
     print(json.dumps(line), flush=True)
 

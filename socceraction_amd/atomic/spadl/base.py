@@ -22,7 +22,6 @@ import pandas as pd
 import torch
 
 from ... import _native
-from ...batch import device, stream_handle
 
 _REQUIRED = ('game_id', 'original_event_id', 'action_id', 'period_id', 'time_seconds',
              'team_id', 'player_id', 'start_x', 'start_y', 'end_x', 'end_y', 'type_id',
@@ -30,6 +29,15 @@ _REQUIRED = ('game_id', 'original_event_id', 'action_id', 'period_id', 'time_sec
 _OUT = ('game_id', 'original_event_id', 'action_id', 'period_id', 'time_seconds', 'team_id',
         'player_id', 'x', 'y', 'dx', 'dy', 'type_id', 'bodypart_id')
 _ALIGN = 256
+
+
+def device():
+    from ...batch import device as _device  # lazy: batch imports this package's config
+    return _device()
+
+
+def stream_handle() -> int:
+    return torch.cuda.current_stream().cuda_stream
 
 
 def _pack(arrays: Dict[str, np.ndarray], dev) -> Tuple[torch.Tensor, Dict[str, torch.Tensor]]:
@@ -45,6 +53,19 @@ def _pack(arrays: Dict[str, np.ndarray], dev) -> Tuple[torch.Tensor, Dict[str, t
     views = {k: buf[offs[k]:offs[k] + max(a.nbytes, a.itemsize)].view(torch.from_numpy(a[:0]).dtype)
              for k, a in arrays.items()}
     return buf, views
+
+
+def _alloc(spec: Dict[str, type], n: int, dev) -> Tuple[torch.Tensor, Dict[str, torch.Tensor]]:
+    """One uninitialised device allocation carved into length-n columns (256-B aligned)."""
+    offs, total = {}, 0
+    for k, dt in spec.items():
+        offs[k] = total
+        total += (max(n * np.dtype(dt).itemsize, 16) + _ALIGN - 1) // _ALIGN * _ALIGN
+    buf = torch.empty(total, dtype=torch.uint8, device=dev)
+    tdt = {np.float64: torch.float64, np.int32: torch.int32, np.uint8: torch.uint8}
+    cols = {k: buf[offs[k]:offs[k] + n * np.dtype(dt).itemsize].view(tdt[dt])
+            for k, dt in spec.items()}
+    return buf, cols
 
 
 def _codes(values, sort: bool = False) -> Tuple[np.ndarray, pd.Index]:
@@ -128,6 +149,33 @@ class SpadlFrame:
         dtypes = {c: actions[c].dtype for c in ('game_id', 'team_id', 'player_id')}
         return cls(n, buf, views, {'game': gu, 'team': tu, 'player': pu, 'event': eu}, dtypes)
 
+    @classmethod
+    def from_columns(cls, d: Dict[str, np.ndarray], dev=None) -> 'SpadlFrame':
+        """From the flat, game-sorted numpy columns of :mod:`socceraction_amd.synthetic`
+        (integer ids; no original_event_id: every event code is missing)."""
+        dev = dev or device()
+        n = len(d['type_id'])
+        g, gu = _codes(d['game_id'], sort=True)
+        t, tu = _codes(d['team_id'])
+        player = d['player_id'] if 'player_id' in d else \
+            (np.asarray(d['team_id']) * 100 + np.asarray(d['pos']) % 11)
+        p, pu = _codes(player)
+        arrays = {'time_seconds': np.asarray(d['time_seconds'], np.float64)}
+        for c in ('start_x', 'start_y', 'end_x', 'end_y'):
+            arrays[c] = np.asarray(d[c], np.float64)
+        arrays.update(game=g, team=t, player=p, event=np.full(n, -1, np.int32))
+        for c in ('period_id', 'type_id', 'result_id', 'bodypart_id'):
+            arrays[c] = np.asarray(d[c]).astype(np.uint8)
+        aid = d['pos'] if 'pos' in d else np.arange(n)
+        order = _sorted_order(g, arrays['period_id'], np.asarray(aid))
+        if order is not None:
+            arrays['order'] = order
+        buf, views = _pack(arrays, dev)
+        dtypes = {'game_id': np.dtype(np.int64), 'team_id': np.dtype(np.int64),
+                  'player_id': np.dtype(np.int64)}
+        return cls(n, buf, views, {'game': gu, 'team': tu, 'player': pu,
+                                   'event': pd.Index([])}, dtypes)
+
     def struct(self) -> _native.SaSpadlFrame:
         s = _native.SaSpadlFrame()
         s.n = self.n
@@ -145,6 +193,26 @@ class AtomicColumns:
     n: int
     buffer: torch.Tensor
     cols: Dict[str, torch.Tensor]
+
+    def to_batch(self, frame: 'SpadlFrame', home_team_ids=None):
+        """The rows as an atomic :class:`~socceraction_amd.batch.ActionBatch` (one segment per
+        game, no copy), ready for the Atomic-VAEP feature / label / formula kernels.
+        ``home_team_ids``: one home team id per game, in game_id order (None: no flip)."""
+        from ...batch import ActionBatch
+        dev = self.buffer.device
+        G = len(frame.uniques['game'])
+        seg_off = torch.empty(G + 1, dtype=torch.int64, device=dev)
+        _native.check(_native.lib().sa_segment_offsets(self.cols['game'].data_ptr(), self.n, G,
+                                                       seg_off.data_ptr(), stream_handle()))
+        home = None
+        if home_team_ids is not None:
+            hc = frame.uniques['team'].get_indexer(pd.Index(home_team_ids)).astype(np.int32)
+            home = torch.from_numpy(hc).to(dev)
+        c = self.cols
+        cols = {'c0': c['x'], 'c1': c['y'], 'c2': c['dx'], 'c3': c['dy'],
+                'time_seconds': c['time_seconds'], 'team': c['team'], 'type_id': c['type_id'],
+                'bodypart_id': c['bodypart_id'], 'period_id': c['period_id']}
+        return ActionBatch.from_device(cols, self.n, seg_off, home, atomic=True)
 
     def struct(self) -> _native.SaAtomicFrame:
         s = _native.SaAtomicFrame()
@@ -168,7 +236,7 @@ def convert_device(frame: SpadlFrame) -> AtomicColumns:
     spec = {'time_seconds': np.float64, 'x': np.float64, 'y': np.float64, 'dx': np.float64,
             'dy': np.float64, 'game': np.int32, 'team': np.int32, 'player': np.int32,
             'event': np.int32, 'period_id': np.uint8, 'type_id': np.uint8, 'bodypart_id': np.uint8}
-    buf, cols = _pack({k: np.empty(max(m, 1), dt) for k, dt in spec.items()}, dev)
+    buf, cols = _alloc(spec, max(m, 1), dev)
     out = AtomicColumns(m, buf, cols)
     if m:
         o = out.struct()

@@ -196,6 +196,23 @@ class ActionBatch:
         return cls(cols, np.asarray(d['game_off'], dtype=np.int64), home if flip else None,
                    atomic, dev)
 
+    @classmethod
+    def from_device(cls, cols: Dict[str, torch.Tensor], n: int, seg_off: torch.Tensor,
+                    home: Optional[torch.Tensor], atomic: bool) -> 'ActionBatch':
+        """Wrap columns already in HBM (16-byte aligned; kernel dtypes of the module table),
+        e.g. the output of the device SPADL -> Atomic-SPADL conversion. No copy."""
+        self = cls.__new__(cls)
+        self.atomic = bool(atomic)
+        self.n = int(n)
+        self.n_segments = int(seg_off.numel() - 1)
+        self.cols = dict(cols)
+        self.cols['seg_off'] = seg_off
+        if home is not None:
+            self.cols['home'] = home
+        self.buffer = None
+        self.device = seg_off.device
+        return self
+
     # ------------------------------------------------------------------ C structs
     def _frame(self, fr) -> None:
         c = self.cols

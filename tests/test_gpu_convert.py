@@ -136,3 +136,42 @@ def test_convert_device_full_size(conv):
         ref = co.convert_to_atomic(_cols(sub))
         # a dribble across the boundary into game g belongs to game g's rows
         assert abs(int(counts[g]) - len(ref['type_id'])) <= 1, g
+
+
+def test_device_pipeline_convert_to_atomic_features(conv):
+    """SPADL columns -> device conversion -> atomic ActionBatch (no host round trip) ->
+    Atomic-VAEP features + labels for 20 games, vs the oracle chain with per-game segments."""
+    from golden_io import assert_close
+    from oracle import atomic_convert_oracle as co
+    from oracle import vaep_oracle as vo
+    from socceraction_amd import ops, synthetic
+    from socceraction_amd.atomic.spadl import base as cb
+    from socceraction_amd.batch import segment_offsets
+    d = synthetic.spadl_games(20, seed=94)
+    frame = cb.SpadlFrame.from_columns(d)
+    out = cb.convert_device(frame)
+    ab = out.to_batch(frame, d['home_team_id'])
+    fb = ops.features(ab, vo.ATOMIC_DEFAULT, 3)
+    lb = ops.labels(ab)
+    df = synthetic.to_frame(d)
+    df['original_event_id'] = None
+    ref = co.convert_to_atomic(_cols(df))
+    assert ab.n == len(ref['type_id'])
+    so = segment_offsets(ref['game_id'])
+    np.testing.assert_array_equal(ab.cols['seg_off'].cpu().numpy(), so)
+    cols = {c: ref[c] for c in ('period_id', 'time_seconds', 'team_id', 'x', 'y', 'dx', 'dy',
+                                'type_id', 'bodypart_id')}
+    rf = vo.features(cols, 3, vo.ATOMIC_DEFAULT, atomic=True, seg_off=so,
+                     home=list(d['home_team_id']))
+    blocks = dict(zip('bfi', fb.to_numpy()))
+    assert fb.plan.names == [c[0] for c in rf]
+    for (name, kind, col), (_, _, rv) in zip(fb.plan.order, rf):
+        got = blocks[kind][col, :ab.n]
+        if kind == 'f':
+            assert_close(got, rv, name)
+        else:
+            np.testing.assert_array_equal(got.astype(np.int64), np.asarray(rv).astype(np.int64),
+                                          err_msg=name)
+    lab = vo.labels(cols, atomic=True, seg_off=so)
+    np.testing.assert_array_equal(lb.scores[:ab.n].cpu().numpy().astype(bool), lab['scores'])
+    np.testing.assert_array_equal(lb.concedes[:ab.n].cpu().numpy().astype(bool), lab['concedes'])
