@@ -13,6 +13,7 @@ slots, so this table and the kernel must change together.
 from __future__ import annotations
 
 from dataclasses import dataclass
+from functools import lru_cache
 from typing import Dict, List, Sequence, Tuple
 
 import numpy as np
@@ -130,6 +131,12 @@ class FeaturePlan:
 
 
 def build_plan(xfns: Sequence[str], k: int, atomic: bool = False) -> FeaturePlan:
+    """The block layout of ``xfns`` (cached: callers treat plans as read-only)."""
+    return _build_plan(tuple(xfns), int(k), bool(atomic))
+
+
+@lru_cache(maxsize=128)
+def _build_plan(xfns: Tuple[str, ...], k: int, atomic: bool) -> FeaturePlan:
     valid = ATOMIC_XFNS if atomic else SPADL_XFNS
     if not 1 <= k <= 8:
         raise ValueError('nb_prev_actions must be between 1 and 8 on this backend')
@@ -159,22 +166,52 @@ def build_plan(xfns: Sequence[str], k: int, atomic: bool = False) -> FeaturePlan
     return FeaturePlan(tuple(xfns), k, atomic, count['b'], count['f'], count['i'], order, s)
 
 
+def _frame_from_blocks(plan: FeaturePlan, blocks: dict, n: int) -> pd.DataFrame:
+    """Zero-copy DataFrame over the host blocks: one pandas block per dtype, placed at the
+    reference's column positions (no per-column Series, no consolidation copy)."""
+    from pandas.core.internals import BlockManager
+    from pandas.core.internals.api import make_block
+    sizes = {'b': plan.n_bool, 'f': plan.n_f64, 'i': plan.n_i64}
+    pos = {k: np.full(sizes[k], -1, np.intp) for k in sizes}
+    for p, (_, kind, col) in enumerate(plan.order):
+        pos[kind][col] = p
+    mblocks = []
+    for kind in 'bfi':
+        if sizes[kind] == 0:
+            continue
+        if (pos[kind] < 0).any():
+            raise ValueError('block column without a name')
+        v = blocks[kind][:sizes[kind], :n]
+        mblocks.append(make_block(v.view(np.bool_) if kind == 'b' else v, placement=pos[kind],
+                                  ndim=2))
+    mgr = BlockManager(mblocks, [pd.Index(plan.names), pd.RangeIndex(n)])
+    return pd.DataFrame._from_mgr(mgr, mgr.axes)
+
+
 def assemble_frame(plan: FeaturePlan, bool_block: np.ndarray, f64_block: np.ndarray,
                    i64_block: np.ndarray, n: int, index=None) -> pd.DataFrame:
     """Build the feature DataFrame from column-major host blocks ``[cols, >= n]``."""
-    data = {}
     blocks = {'b': bool_block, 'f': f64_block, 'i': i64_block}
-    for name, kind, col in plan.order:
-        v = blocks[kind][col, :n]
-        data[name] = v.view(np.bool_) if kind == 'b' else v
-    if len(set(plan.names)) != len(plan.names):  # a transformer listed twice: keep duplicates
-        series = []
-        for name, kind, col in plan.order:
-            v = blocks[kind][col, :n]
-            series.append(pd.Series(v.view(np.bool_) if kind == 'b' else v, name=name, copy=False))
-        df = pd.concat(series, axis=1)
-    else:
-        df = pd.DataFrame(data, copy=False)
+    df = None
+    if len(set(plan.names)) == len(plan.names):
+        try:
+            df = _frame_from_blocks(plan, blocks, n)
+        except (ImportError, AttributeError, TypeError, ValueError):  # pandas internals moved
+            df = None
+    if df is None:
+        if len(set(plan.names)) != len(plan.names):  # a transformer listed twice: keep duplicates
+            series = []
+            for name, kind, col in plan.order:
+                v = blocks[kind][col, :n]
+                series.append(pd.Series(v.view(np.bool_) if kind == 'b' else v, name=name,
+                                        copy=False))
+            df = pd.concat(series, axis=1)
+        else:
+            data = {}
+            for name, kind, col in plan.order:
+                v = blocks[kind][col, :n]
+                data[name] = v.view(np.bool_) if kind == 'b' else v
+            df = pd.DataFrame(data, copy=False)
     if index is not None:
         df.index = index
     return df

@@ -52,7 +52,18 @@ class FeatureBlocks:
         return self._blk(kind)[:, col, :].reshape(-1)[:self.n]
 
     def to_numpy(self):
-        return tuple(self.block(k).cpu().numpy() for k in 'bfi')
+        """Host copies ``[n_cols, >= n]`` of the three blocks: whole tiles are copied (one
+        contiguous D2H per block into pinned memory, all three in flight together) and the
+        padding rows are sliced off on the host."""
+        hosts = []
+        for k in 'bfi':
+            t = self._blk(k)
+            src = t[0] if t.shape[0] == 1 else t.permute(1, 0, 2).reshape(t.shape[1], -1)
+            h = torch.empty(src.shape, dtype=src.dtype, pin_memory=True)
+            h.copy_(src, non_blocking=True)
+            hosts.append(h)
+        torch.cuda.current_stream().synchronize()
+        return tuple(h.numpy()[:, :self.n] for h in hosts)
 
     def to_frame(self, index=None):
         """Copy to host and build the reference-shaped DataFrame."""
