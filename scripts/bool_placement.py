@@ -5,6 +5,8 @@ trial lands at a different address) and the kernel is timed with HIP events.
 
     python scripts/bool_placement.py bool --pads 0,1,5 [--trials 3]
     python scripts/bool_placement.py num --pads 0,1,5 [--ipads 0,2]
+
+SOCCERACTION_AMD_LIB selects an A/B build of the library (scripts/ab_sweep.py convention).
 """
 import argparse
 import copy
@@ -46,6 +48,7 @@ def main():
     ap.add_argument('--trials', type=int, default=3)
     ap.add_argument('--pads', default='0,1')
     ap.add_argument('--ipads', default='0')
+    ap.add_argument('--keep', type=int, default=3, help='allocations kept alive at a time')
     args = ap.parse_args()
     dev = B.device()
     d = synthetic.spadl_games(args.games)
@@ -87,7 +90,7 @@ def main():
                 print(json.dumps({'kind': args.kind, 'pad': pad, 'ipad': ipad, 'trial': t,
                                   'ms': round(ms, 4),
                                   'TBps': round(bytes_pa * n / ms * 1e-9, 3)}), flush=True)
-                if len(keep) > 3:
+                if len(keep) > args.keep:
                     keep.pop(0)
     print(json.dumps(res))
 

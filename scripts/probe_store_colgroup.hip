@@ -25,7 +25,7 @@ __global__ __launch_bounds__(256) void fill1(u32x4* p, int64_t n16) {
   if (i < n16) p[i] = u32x4{(uint32_t)i, 1u, 2u, 3u};
 }
 
-template <int G, bool XCD>
+template <int G, bool XCD, bool NT = false>
 __global__ __launch_bounds__(256) void colgroup(uint8_t* out, int64_t tiles) {
   constexpr int NG = (C + G - 1) / G;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -40,8 +40,13 @@ __global__ __launch_bounds__(256) void colgroup(uint8_t* out, int64_t tiles) {
   if (t >= tiles) return;
   uint8_t* base = out + t * (int64_t)C * 1024 + lane * 16;
   const int c1 = (g + 1) * G < C ? (g + 1) * G : C;
-  for (int c = g * G; c < c1; ++c)
-    *(u32x4*)(base + (int64_t)c * 1024) = u32x4{(uint32_t)t + c, 1u, 2u, (uint32_t)c};
+  for (int c = g * G; c < c1; ++c) {
+    const u32x4 v = {(uint32_t)t + c, 1u, 2u, (uint32_t)c};
+    if (NT)
+      __builtin_nontemporal_store(v, (u32x4*)(base + (int64_t)c * 1024));
+    else
+      *(u32x4*)(base + (int64_t)c * 1024) = v;
+  }
 }
 
 template <typename L>
@@ -66,18 +71,20 @@ static int timeit(const char* name, L launch, double bytes) {
   return 0;
 }
 
-template <int G, bool X>
+template <int G, bool X, bool NT = false>
 static int run(const char* name, uint8_t* out, int64_t tiles) {
   constexpr int NG = (C + G - 1) / G;
   const unsigned blocks = (unsigned)((tiles * NG + 3) / 4);
   const unsigned nb = X ? (blocks + 7) / 8 * 8 : blocks;
-  return timeit(name, [&] { colgroup<G, X><<<nb, 256>>>(out, tiles); }, (double)tiles * 1024 * C);
+  return timeit(name, [&] { colgroup<G, X, NT><<<nb, 256>>>(out, tiles); }, (double)tiles * 1024 * C);
 }
 
 int main(int argc, char** argv) {
   const double bytes = (double)N * C;
   const int64_t n16 = N * C / 16, tiles = N / 1024;
   const int trials = argc > 1 ? atoi(argv[1]) : 1;
+  // argv[2] = 1: keep every allocation alive (each trial lands further into HBM)
+  const bool keep_all = argc > 2 && atoi(argv[2]) != 0;
   uint8_t* keep[3] = {nullptr, nullptr, nullptr};
   int rc = 0;
   for (int t = 0; t < trials; ++t) {
@@ -90,9 +97,13 @@ int main(int argc, char** argv) {
     rc |= run<32, false>("col32", out, tiles);
     rc |= run<16, true>("col16_xcd", out, tiles);
     rc |= run<32, true>("col32_xcd", out, tiles);
+    rc |= run<26, true, true>("col26_xcd_nt", out, tiles);
+    rc |= run<26, true, false>("col26_xcd", out, tiles);
     rc |= run<515, true>("col515_xcd", out, tiles);
-    if (keep[t % 3]) CHECK(hipFree(keep[t % 3]));
-    keep[t % 3] = out;
+    if (!keep_all) {
+      if (keep[t % 3]) CHECK(hipFree(keep[t % 3]));
+      keep[t % 3] = out;
+    }
   }
   return rc;
 }

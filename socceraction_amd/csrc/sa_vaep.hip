@@ -598,9 +598,15 @@ __global__ __launch_bounds__(64 * CG_WAVES) void bool_colgroup_kernel(FeatArgs a
     const int64_t wbase = j0 / 4 - 2;
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
+#if SA_PROBE_NOLOAD  // timing probe only (wrong results): no id loads
+      TR[k] = (uint32_t)(wbase + k) * 0x01010101u;
+      RR[k] = TR[k] >> 3;
+      BR[k] = TR[k] >> 5;
+#else
       TR[k] = ld_u8x4(F0.type_id, wbase + k, n);
       RR[k] = ATOMIC ? 0u : ld_u8x4(F0.result_id, wbase + k, n);
       BR[k] = ld_u8x4(F0.bodypart_id, wbase + k, n);
+#endif
     }
   }
   const int c_type = P.bool_col[SA_XFN_ACTIONTYPE_ONEHOT];
