@@ -1249,6 +1249,17 @@ __global__ __launch_bounds__(256) void labels_kernel(sa_actions A, int nr, uint8
 #pragma unroll
     for (int r = 0; r < 32; ++r) tm[r] = ld_or0(F.team, j0 + r, n);
   }
+  const int32_t t0 = tm[0];
+  int32_t t1 = t0;
+  uint32_t e0 = 0;
+#pragma unroll
+  for (int r = 0; r < 32; ++r) {
+    e0 |= (uint32_t)(tm[r] == t0) << r;
+    if (t1 == t0 && tm[r] != t0) t1 = tm[r];
+  }
+  uint32_t e1 = 0;
+#pragma unroll
+  for (int r = 0; r < 32; ++r) e1 |= (uint32_t)(tm[r] == t1) << r;
   SegCursor cur = seg_at(A, j0);
   uint32_t s_out[4] = {0, 0, 0, 0}, c_out[4] = {0, 0, 0, 0}, g_out[4] = {0, 0, 0, 0};
 #pragma unroll
@@ -1263,9 +1274,18 @@ __global__ __launch_bounds__(256) void labels_kernel(sa_actions A, int nr, uint8
         const int64_t hi = j + nr - 1 < last ? j + nr - 1 : last;
         const int span = (int)(hi - j);  // 0 .. 16
         const uint32_t win = span > 0 ? (((1u << span) - 1u) << (m + 1)) : 0u;
-        uint32_t same = 0;
+        // equality masks of the window's first two team codes cover every row whose team is
+        // one of them (two teams per game); a third code takes the full compare
+        uint32_t same;
+        if (tm[m] == t0)
+          same = e0;
+        else if (tm[m] == t1)
+          same = e1;
+        else {
+          same = 0;
 #pragma unroll
-        for (int r = 0; r < 32; ++r) same |= (uint32_t)(tm[r] == tm[m]) << r;
+          for (int r = 0; r < 32; ++r) same |= (uint32_t)(tm[r] == tm[m]) << r;
+        }
         scores = goal_j || (((gm & same) | (om & ~same)) & win) != 0;
         concedes = og_j || (((gm & ~same) | (om & same)) & win) != 0;
       } else {
