@@ -139,26 +139,34 @@ def atomic_extra(dist, rank, world, dev, games: int, reps: int = 5) -> dict:
             'frac_of_8TBs_per_gpu': round(bpa * n / ms * 1e-6 / HBM_PEAK_GBS, 4)}
 
 
-def xt105_extra(ab, dist, dev) -> dict:
+def xt105_extra(ab, dist, dev, sharded: bool = False) -> dict:
     """BASELINE cfg5 alongside the main line: xT 105x68 fit (count pass over this rank's
     games, RCCL all-reduce of the 7140-cell count vectors and 204 MB transition counts, value
     iteration over the 7140^2 system) + rate(use_interpolation=True) on the 1050x680 surface."""
     from socceraction_amd import shard
     l, w = 105, 68
 
+    world = dist.get_world_size() if dist is not None else 1
+
     def once():
-        acc = ops.xt_zero_counts(l, w, dev)
-        ops.xt_count(ab, l, w, acc)
-        if dist is not None and dist.get_backend() == 'nccl':
-            shard.allreduce_xt_counts(acc.shot, acc.goal, acc.move, acc.trans, acc.err)
-        sol = ops.xt_solve(acc)  # synchronises
-        grid = ops.xt_interp_grid(sol.mats[3].reshape(w, l), l, w)
+        if sharded and dist is not None:  # reduce-scatter of count rows + row-sharded solve
+            acc = ops.xt_zero_counts(l, w, dev, row_blocks=world)
+            ops.xt_count(ab, l, w, acc)
+            mats, _, n_iter = shard.xt_solve_sharded(acc)
+        else:  # one all-reduce of the counts, replicated solve
+            acc = ops.xt_zero_counts(l, w, dev)
+            ops.xt_count(ab, l, w, acc)
+            if dist is not None and dist.get_backend() == 'nccl':
+                shard.allreduce_xt_counts(acc.shot, acc.goal, acc.move, acc.trans, acc.err)
+            sol = ops.xt_solve(acc)  # synchronises
+            mats, n_iter = sol.mats, sol.n_iter
+        grid = ops.xt_interp_grid(mats[3].reshape(w, l), l, w)
         ops.xt_rate(ab, grid, 1050, 680)
-        return sol
+        return n_iter
     once()  # warm-up (allocator, first launches)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    sol = once()
+    n_iter = once()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     n, total = ab.n, ab.n
@@ -167,8 +175,9 @@ def xt105_extra(ab, dist, dev) -> dict:
         total = int(_reduce(dist, n, dist.ReduceOp.SUM, dev))
     return {'workload': 'cfg5: xT 105x68 fit (count + all-reduce + value iteration) + '
                         'rate(use_interpolation=True)',
-            'actions_per_gpu': n, 'iterations': sol.n_iter, 'ms_fit_and_rate': round(dt * 1e3, 3),
-            'actions_per_s': round(total / dt, 1)}
+            'actions_per_gpu': n, 'iterations': n_iter, 'ms_fit_and_rate': round(dt * 1e3, 3),
+            'actions_per_s': round(total / dt, 1),
+            'solve': 'row-sharded' if (sharded and dist is not None) else 'replicated'}
 
 
 def convert_extra(d, dist, dev, reps: int = 3) -> dict:
@@ -238,6 +247,9 @@ def main() -> None:
     ap.add_argument('--no-xt', action='store_true', help='skip the cfg4 xT side measurement')
     ap.add_argument('--no-side', action='store_true',
                     help='skip the cfg3 (atomic) and cfg5 (xT 105x68) side measurements')
+    ap.add_argument('--xt-sharded', action='store_true',
+                    help='cfg5 with N > 1: reduce-scatter the count rows and row-shard the value '
+                         'iteration (default: one all-reduce, replicated solve)')
     ap.add_argument('--atomic-games', type=int, default=1250,
                     help='atomic games per GPU for cfg3 (1250 ~ 5M atomic actions)')
     ap.add_argument('--bool-tile', type=int, default=1024,
@@ -315,7 +327,7 @@ def main() -> None:
     extra_xt = xt_extra(d, ab, dist, dev) if not args.no_xt else None
     extra_side = {}
     if not args.no_side:
-        extra_side['xt105_cfg5'] = xt105_extra(ab, dist, dev)
+        extra_side['xt105_cfg5'] = xt105_extra(ab, dist, dev, args.xt_sharded)
         extra_side['atomic_cfg3'] = atomic_extra(dist, rank, world, dev, args.atomic_games)
         extra_side['convert_to_atomic'] = convert_extra(d, dist, dev)
     if rank != 0:

@@ -187,6 +187,22 @@ int sa_xt_normalize(const int64_t* shot, const int64_t* goal, const int64_t* mov
                     const int32_t* trans, int32_t l, int32_t w, double* mats, double* trans_t,
                     void* stream);
 
+/* Row-sharded value iteration (multi-GPU fit of large grids, e.g. 105 x 68: every rank holds
+ * the count rows of its own row range after a reduce-scatter and the full x after each
+ * all-gather).  sa_xt_probabilities: mats[3*C] = scoring | shot | move probability (as
+ * sa_xt_normalize) and gs = scoring * shot, pmove = move probability (xthreat.py:296-297).
+ * sa_xt_iterate_rows: one iteration of rows [r0, r0 + nrows): cnt_rows holds their count
+ * rows (row r0 + i at cnt_rows + i*C), x the full current vector (length C);
+ * x_next_rows[i] = gs + pmove * sum_c (cnt / move[r]) * x[c] in the reference's summation
+ * order (xthreat.py:306-317), *flag_out |= some row moved by more than eps; a non-NULL
+ * *flag_prev == 0 makes the call a no-op.  Asynchronous. */
+int sa_xt_probabilities(const int64_t* shot, const int64_t* goal, const int64_t* move, int32_t C,
+                        double* mats, double* gs, double* pmove, void* stream);
+int sa_xt_iterate_rows(const int32_t* cnt_rows, const int64_t* move, const double* gs,
+                       const double* pmove, int32_t C, int32_t r0, int32_t nrows, const double* x,
+                       double eps, double* x_next_rows, const int32_t* flag_prev, int32_t* flag_out,
+                       void* stream);
+
 /* interp2d(x=cx, y=cy, z=xT, kind='linear')(xs, ys) of ExpectedThreat.interpolator
  * (xthreat.py:347-378): grid[r*L + h] = bilinear(xT; xs[h], ys[r]) through the cell
  * centres cx[l], cy[w], clamped to the centre hull (FITPACK evaluation clamps).  All

@@ -87,6 +87,9 @@ _SIGNATURES = {
                                    ctypes.POINTER(ctypes.c_int32), _p]),
     'sa_xt_normalize': (ctypes.c_int, [_p, _p, _p, _p, ctypes.c_int32, ctypes.c_int32, _p, _p,
                                        _p]),
+    'sa_xt_probabilities': (ctypes.c_int, [_p, _p, _p, ctypes.c_int32, _p, _p, _p, _p]),
+    'sa_xt_iterate_rows': (ctypes.c_int, [_p, _p, _p, _p, ctypes.c_int32, ctypes.c_int32,
+                                          ctypes.c_int32, _p, ctypes.c_double, _p, _p, _p, _p]),
     'sa_xt_interp_grid': (ctypes.c_int, [_p, _p, _p, ctypes.c_int32, ctypes.c_int32, _p,
                                          ctypes.c_int32, _p, ctypes.c_int32, _p, _p]),
     'sa_xt_rate': (ctypes.c_int, [ctypes.POINTER(SaActions), _p, ctypes.c_int32, ctypes.c_int32,

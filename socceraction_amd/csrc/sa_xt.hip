@@ -288,20 +288,26 @@ struct XiChunk {
   double xv[2];       // x[c] of column i
 };
 
+// Rows [rb, rb + nrows) of the system: `trans` points at the count row of row rb (row rb + i
+// at trans + i*C), x is the full current vector, xo[i] receives the new value of row rb + i
+// and *flag_out |= (some row moved by more than eps).  A non-null flag_prev == 0 (the
+// previous iteration converged) makes the launch a no-op.
 __global__ __launch_bounds__(XI_THREADS) void xt_iter_kernel(const int32_t* __restrict__ trans,
                                                              const unsigned long long* __restrict__ move,
                                                              const double* __restrict__ gs,
                                                              const double* __restrict__ pmove, int C,
-                                                             double eps, int it, double* __restrict__ heat,
-                                                             int32_t* __restrict__ flags) {
-  if (it > 0 && __hip_atomic_load(&flags[it - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
+                                                             int rb, int nrows, double eps,
+                                                             const double* __restrict__ x,
+                                                             double* __restrict__ xo,
+                                                             const int32_t* flag_prev,
+                                                             int32_t* __restrict__ flag_out) {
+  if (flag_prev && __hip_atomic_load(flag_prev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
     return;
   __shared__ double list[2][XI_ROWS * XI_LST];       // compacted x, then products, per row
   __shared__ int32_t cbuf[XI_LOADERS][XI_RQ][XI_CH];  // compacted counts (loader-wave private)
   __shared__ int32_t lens[2][XI_ROWS];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int r0 = blockIdx.x * XI_ROWS;
-  const double* __restrict__ x = heat + (int64_t)it * C;
+  const int r0 = blockIdx.x * XI_ROWS;  // local row index of the block's first row
   const int nch = (C + XI_CH - 1) / XI_CH;
   const int nchp = (nch + XI_DEPTH - 1) / XI_DEPTH * XI_DEPTH;
   if (wv < XI_LOADERS) {  // ---- loader waves: rows r0 + RQ*wv + q, columns k*XI_CH + 64*i + lane
@@ -311,10 +317,10 @@ __global__ __launch_bounds__(XI_THREADS) void xt_iter_kernel(const int32_t* __re
 #pragma unroll
     for (int q = 0; q < XI_RQ; ++q) {
       const int r = r0 + XI_RQ * wv + q;
-      rowok[q] = r < C;
-      const int rc = rowok[q] ? r : C - 1;
+      rowok[q] = r < nrows;
+      const int rc = rowok[q] ? r : nrows - 1;
       rowp[q] = trans + (int64_t)rc * C;
-      mvq[q] = (double)move[rc];
+      mvq[q] = (double)move[rb + rc];
     }
     auto issue = [&](XiChunk& R, int k) {  // unconditional loads from clamped addresses
 #pragma unroll
@@ -391,12 +397,12 @@ __global__ __launch_bounds__(XI_THREADS) void xt_iter_kernel(const int32_t* __re
         }
       }
     }
-    if (lane < XI_ROWS && r0 + r < C) {
-      const int rr = r0 + r;
+    if (lane < XI_ROWS && r0 + r < nrows) {
+      const int rr = rb + r0 + r;  // global row
       const double mv = pmove[rr] * acc;
       const double nx = gs[rr] + mv;
-      heat[(int64_t)(it + 1) * C + rr] = nx;
-      if ((nx - x[rr]) > eps) atomicOr(&flags[it], 1);  // np.any(diff > eps): NaN is False
+      xo[r0 + r] = nx;
+      if ((nx - x[rr]) > eps) atomicOr(flag_out, 1);  // np.any(diff > eps): NaN is False
     }
   }
 }
@@ -540,7 +546,9 @@ extern "C" int sa_xt_solve(const int64_t* shot, const int64_t* goal, const int64
       const int it1 = it0 + batch < max_iter ? it0 + batch : max_iter;
       for (int it = it0; it < it1; ++it)
         hipLaunchKernelGGL(xt_iter_kernel, dim3((C + XI_ROWS - 1) / XI_ROWS), dim3(XI_THREADS), 0, st,
-                           trans, um, gs, pm, C, eps, it, heatmaps, dflags);
+                           trans, um, gs, pm, C, 0, C, eps, heatmaps + (int64_t)it * C,
+                           heatmaps + (int64_t)(it + 1) * C, it > 0 ? dflags + it - 1 : nullptr,
+                           dflags + it);
       rc = check_launch("xt_iter_kernel");
       if (!rc) rc = check_hip(hipMemcpyAsync(hflags.data() + it0, dflags + it0,
                                              sizeof(int32_t) * (it1 - it0), hipMemcpyDeviceToHost, st),
@@ -608,4 +616,28 @@ extern "C" int sa_xt_rate(const sa_actions* a, const double* grid, int32_t L, in
   hipLaunchKernelGGL(xt_rate_kernel, dim3((unsigned)((a->n + 255) / 256)), dim3(256), 0,
                      (hipStream_t)stream, *a, grid, L, W, out, err_flags);
   return check_launch("xt_rate_kernel");
+}
+
+extern "C" int sa_xt_probabilities(const int64_t* shot, const int64_t* goal, const int64_t* move, int32_t C,
+                                   double* mats, double* gs, double* pmove, void* stream) {
+  if (C < 1 || !shot || !goal || !move || !mats || !gs || !pmove) return fail(SA_EINVAL, "bad xt probability args");
+  hipLaunchKernelGGL(xt_prob_kernel, dim3((C + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                     reinterpret_cast<const unsigned long long*>(shot),
+                     reinterpret_cast<const unsigned long long*>(goal),
+                     reinterpret_cast<const unsigned long long*>(move), C, mats, gs, pmove);
+  return check_launch("xt_prob_kernel");
+}
+
+extern "C" int sa_xt_iterate_rows(const int32_t* cnt_rows, const int64_t* move, const double* gs,
+                                  const double* pmove, int32_t C, int32_t r0, int32_t nrows, const double* x,
+                                  double eps, double* x_next_rows, const int32_t* flag_prev, int32_t* flag_out,
+                                  void* stream) {
+  if (C < 1 || r0 < 0 || nrows < 0 || r0 + nrows > C) return fail(SA_EINVAL, "row range outside [0, C)");
+  if (!move || !gs || !pmove || !x || !flag_out || (nrows > 0 && (!cnt_rows || !x_next_rows)))
+    return fail(SA_EINVAL, "null xt iteration pointer");
+  if (nrows == 0) return SA_OK;
+  hipLaunchKernelGGL(xt_iter_kernel, dim3((nrows + XI_ROWS - 1) / XI_ROWS), dim3(XI_THREADS), 0,
+                     (hipStream_t)stream, cnt_rows, reinterpret_cast<const unsigned long long*>(move), gs,
+                     pmove, C, r0, nrows, eps, x, x_next_rows, flag_prev, flag_out);
+  return check_launch("xt_iter_kernel");
 }

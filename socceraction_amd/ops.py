@@ -179,12 +179,18 @@ class XTCounts:
         return self.l * self.w
 
 
-def xt_zero_counts(l: int, w: int, dev) -> XTCounts:
+def xt_zero_counts(l: int, w: int, dev, row_blocks: int = 1) -> XTCounts:
+    """Zeroed count buffers. ``row_blocks`` > 1 pads the C x C transition counts to a whole
+    number of equal row blocks (``XTCounts.trans_padded``) so they can be reduce-scattered by
+    rows across that many ranks; ``trans`` is the C*C view the count kernel fills."""
     C = l * w
     vec = torch.zeros((3, C), dtype=torch.int64, device=dev)
-    return XTCounts(l, w, vec[0], vec[1], vec[2],
-                    torch.zeros(C * C, dtype=torch.int32, device=dev),
-                    torch.zeros(1, dtype=torch.int32, device=dev))
+    rows = -(-C // row_blocks) * row_blocks
+    padded = torch.zeros(rows * C, dtype=torch.int32, device=dev)
+    acc = XTCounts(l, w, vec[0], vec[1], vec[2], padded[:C * C],
+                   torch.zeros(1, dtype=torch.int32, device=dev))
+    acc.trans_padded = padded
+    return acc
 
 
 def xt_count(batch: ActionBatch, l: int, w: int, acc: Optional[XTCounts] = None) -> XTCounts:

@@ -72,6 +72,11 @@ def _count(x: pd.Series, y: pd.Series, l: int = N, w: int = M) -> np.ndarray:
     return acc.shot.cpu().numpy().astype(np.float64).reshape((w, l))
 
 
+def _device():
+    from .batch import device
+    return device()
+
+
 def _safe_divide(a, b) -> np.ndarray:
     return np.divide(a, b, out=np.zeros_like(a), where=b != 0)
 
@@ -163,26 +168,45 @@ class ExpectedThreat:
         self.transition_matrix: Optional[np.ndarray] = None
         self._grid_cache = None
 
-    def fit(self, actions: pd.DataFrame, process_group=None, max_iter: int = 1000
-            ) -> 'ExpectedThreat':
+    def fit(self, actions: pd.DataFrame, process_group=None, max_iter: int = 1000,
+            shard_solve: bool = False) -> 'ExpectedThreat':
         """Fit the model (reference xthreat.py:322-345).
 
         With ``process_group`` each rank passes its own shard of games; counts are summed
-        with one RCCL all-reduce and every rank solves the same system.
+        with one RCCL all-reduce and every rank solves the same system. ``shard_solve=True``
+        instead reduce-scatters the transition counts by rows and splits the value iteration
+        over the ranks (one all-gather of x per iteration; bit-identical results) for large
+        grids; the C x C ``transition_matrix`` is then not materialised (left ``None``).
         """
-        acc = _fit_counts(actions, self.l, self.w, process_group)
-        sol = ops.xt_solve(acc, self.eps, max_iter)
         w, l = self.w, self.l
-        m = sol.mats.cpu().numpy()
+        if shard_solve and process_group is not None:
+            import torch.distributed as dist
+
+            from .shard import xt_solve_sharded
+            world = dist.get_world_size(process_group)
+            if len(actions):
+                acc = ops.xt_zero_counts(l, w, _device(), row_blocks=world)
+                ops.xt_count(ActionBatch.from_frame(actions), l, w, acc)
+            else:
+                acc = ops.xt_zero_counts(l, w, _device(), row_blocks=world)
+            mats, heat_t, n_iter = xt_solve_sharded(acc, self.eps, max_iter, process_group)
+            ops.xt_check_errors(acc)
+            trans = None
+        else:
+            acc = _fit_counts(actions, l, w, process_group)
+            sol = ops.xt_solve(acc, self.eps, max_iter)
+            mats, heat_t, n_iter = sol.mats, sol.heatmaps, sol.n_iter
+            trans = np.ascontiguousarray(sol.trans_t.cpu().numpy().T)
+        m = mats.cpu().numpy()
         self.scoring_prob_matrix = m[0].reshape((w, l))
         self.shot_prob_matrix = m[1].reshape((w, l))
         self.move_prob_matrix = m[2].reshape((w, l))
-        self.transition_matrix = np.ascontiguousarray(sol.trans_t.cpu().numpy().T)
+        self.transition_matrix = trans
         self.xT = m[3].reshape((w, l)).copy()
-        heat = sol.heatmaps.cpu().numpy().reshape((-1, w, l))
+        heat = heat_t.cpu().numpy().reshape((-1, w, l))
         self.heatmaps = [h.copy() for h in heat]
         self._grid_cache = None
-        print('# iterations: ', sol.n_iter)
+        print('# iterations: ', n_iter)
         return self
 
     def interpolator(self, kind: str = 'linear') -> Callable[[np.ndarray, np.ndarray], np.ndarray]:
