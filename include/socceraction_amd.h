@@ -281,6 +281,21 @@ int sa_atomic_emit(const sa_spadl_frame* in, const void* scratch, const sa_atomi
 int sa_segment_offsets(const int32_t* key, int64_t n, int64_t n_segments, int64_t* seg_off,
                        void* stream);
 
+/* ---- gradient-boosted trees on the feature blocks --------------------------------
+ * The learner call of VAEP.rate (`_estimate_probabilities`, vaep/base.py:284-294): P(class 1)
+ * of a binary gradient-boosted tree ensemble for every row of the feature blocks.
+ * nodes: n_nodes records of 24 bytes { double threshold_or_leaf_value; int32 feature (-1 =
+ * leaf); int32 left; int32 right | (default_left << 31); int32 pad } with absolute child
+ * indices; roots[n_trees] the root node of each tree, summed in that order onto base_margin.
+ * feature_slots[f] = (kind << 24) | column locates model feature f in the blocks (kind 0 =
+ * bool block, 1 = f64, 2 = i64).  le = 1: `x <= threshold` goes left (scikit-learn), 0:
+ * `x < threshold` (xgboost); NaN follows default_left.  f32 = 1: xgboost float32 arithmetic
+ * and float output p_out[n], else float64 (scikit-learn).  p = 1 / (1 + exp(-margin)). */
+int sa_tree_predict(const void* nodes, int32_t n_nodes, const int32_t* roots, int32_t n_trees,
+                    const int32_t* feature_slots, int32_t n_features, const sa_block* bool_blk,
+                    const sa_block* f64_blk, const sa_block* i64_blk, int64_t n, double base_margin,
+                    int32_t le, int32_t f32, void* p_out, void* stream);
+
 /* ---- misc -------------------------------------------------------------------- */
 int sa_abi_version(void);
 const char* sa_last_error(void);

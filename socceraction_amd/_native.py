@@ -100,6 +100,10 @@ _SIGNATURES = {
     'sa_atomic_emit': (ctypes.c_int, [ctypes.POINTER(SaSpadlFrame), _p,
                                       ctypes.POINTER(SaAtomicFrame), _p]),
     'sa_segment_offsets': (ctypes.c_int, [_p, ctypes.c_int64, ctypes.c_int64, _p, _p]),
+    'sa_tree_predict': (ctypes.c_int, [_p, ctypes.c_int32, _p, ctypes.c_int32, _p, ctypes.c_int32,
+                                       ctypes.POINTER(SaBlock), ctypes.POINTER(SaBlock),
+                                       ctypes.POINTER(SaBlock), ctypes.c_int64, ctypes.c_double,
+                                       ctypes.c_int32, ctypes.c_int32, _p, _p]),
     'sa_abi_version': (ctypes.c_int, []),
     'sa_last_error': (ctypes.c_char_p, []),
 }

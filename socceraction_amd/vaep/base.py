@@ -252,13 +252,51 @@ class VAEP:
         return Y_hat
 
     # ---------------------------------------------------------------- rating
+    def _device_models(self):
+        """The fitted learners as device tree ensembles (socceraction_amd.trees) when every
+        one is a supported binary tree model and every transformer is a known one; else None
+        (rate then runs the reference's host predict_proba)."""
+        from ..trees import TreeEnsemble
+        if not {'scores', 'concedes'} <= set(self.__models) or self._split_xfns()[1]:
+            return None
+        key = tuple((c, id(m)) for c, m in self.__models.items())
+        cached = getattr(self, '_trees_cache', None)
+        if cached is not None and cached[0] == key:
+            return cached[1]
+        trees = {c: TreeEnsemble.from_model(m) for c, m in self.__models.items()}
+        res = trees if all(t is not None for t in trees.values()) else None
+        self._trees_cache = (key, res)
+        return res
+
+    def _rate_device(self, ab: ActionBatch, trees) -> pd.DataFrame:
+        """features -> predict_proba -> formula without leaving HBM; only the three value
+        columns are copied back. The probability dtype is the learner's (float32 for
+        xgboost, float64 for scikit-learn), as in the reference's host path."""
+        import torch
+        known, _ = self._split_xfns()
+        fb = ops.features(ab, known, self.nb_prev_actions)
+        ps = trees['scores'].predict_blocks(fb)
+        pc = trees['concedes'].predict_blocks(fb)
+        if ps.dtype != pc.dtype:  # pandas would upcast the mixed pair
+            ps, pc = ps.to(torch.float64), pc.to(torch.float64)
+        v = ops.formula(ab, ps, pc).cpu().numpy()[:, :ab.n]
+        return pd.DataFrame({'offensive_value': v[0], 'defensive_value': v[1],
+                             'vaep_value': v[2]})
+
     def rate(self, game: pd.Series, game_actions: pd.DataFrame,
              game_states: Optional[pd.DataFrame] = None) -> pd.DataFrame:
-        """VAEP values of one game's actions (reference vaep/base.py:296-333)."""
+        """VAEP values of one game's actions (reference vaep/base.py:296-333). Supported
+        tree learners (xgboost JSON-dumpable boosters, scikit-learn HistGradientBoosting)
+        are evaluated on the device feature blocks when ``game_states`` is not given."""
         if not self.__models:
             raise NotFittedError()
         actions = self._spadlcfg.add_names(game_actions)
         if game_states is None:
+            trees = self._device_models()
+            if trees is not None:
+                ab = ActionBatch.from_frame(game_actions, atomic=self._atomic,
+                                            home_team_id=game.home_team_id)
+                return self._rate_device(ab, trees)
             game_states = self.compute_features(game, game_actions)
         y_hat = self._estimate_probabilities(game_states)
         return self._vaep.value(actions, y_hat.scores, y_hat.concedes)
@@ -270,6 +308,12 @@ class VAEP:
         if not self.__models:
             raise NotFittedError()
         if game_states is None:
+            trees = self._device_models()
+            if trees is not None:
+                home_of = games.set_index('game_id')['home_team_id']
+                ab = ActionBatch.from_frame(actions, atomic=self._atomic, home_team_id=home_of,
+                                            segments='game')
+                return self._rate_device(ab, trees)
             game_states = self.compute_features_batch(games, actions)
         y_hat = self._estimate_probabilities(game_states)
         n = len(actions)

@@ -1,0 +1,127 @@
+"""GPU tree inference on the feature blocks (the predict_proba step of VAEP.rate,
+reference vaep/base.py:284-333) and the device rate path.
+
+scikit-learn HistGradientBoostingClassifier: pinned against its own predict_proba (float64,
+rtol 1e-12). xgboost-format models (xgboost is not installed): against the numpy restatement in
+oracle/tree_oracle.py (float32; within 1e-6 relative: expf vs numpy exp can differ in the last
+bit). Features come from the golden games' device blocks, in the reference's column order.
+"""
+import numpy as np
+import pandas as pd
+import pytest
+
+from golden_io import assert_close, frame, load
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip('torch')
+
+
+@pytest.fixture(scope='module')
+def sa():
+    from socceraction_amd import _native, batch, ops, trees
+    _native.load_library()
+    return dict(batch=batch, ops=ops, trees=trees)
+
+
+def _game(sa, name='full0'):
+    from oracle import vaep_oracle as vo
+    g = load('spadl', name)
+    df = frame(g)
+    ab = sa['batch'].ActionBatch.from_frame(df, home_team_id=g['home_team_id'][0])
+    fb = sa['ops'].features(ab, vo.SPADL_DEFAULT, 3)
+    b, f, i = fb.to_numpy()
+    blocks = {'b': b, 'f': f, 'i': i}
+    X = np.stack([blocks[k][c, :fb.n].astype(np.float64) for _, k, c in fb.plan.order], axis=1)
+    return g, df, ab, fb, X
+
+
+def test_sklearn_hgb_on_device_equals_predict_proba(sa):
+    from sklearn.ensemble import HistGradientBoostingClassifier
+    g, df, ab, fb, X = _game(sa)
+    y = g['scores'].astype(int).copy()
+    y[::5] = 1
+    Xdf = pd.DataFrame(X, columns=fb.plan.names)
+    clf = HistGradientBoostingClassifier(max_iter=40, max_depth=4, random_state=0).fit(Xdf, y)
+    te = sa['trees'].TreeEnsemble.from_model(clf)
+    assert te is not None and te.feature_names == fb.plan.names
+    p = te.predict_blocks(fb).cpu().numpy()
+    assert p.dtype == np.float64
+    np.testing.assert_allclose(p, clf.predict_proba(Xdf)[:, 1], rtol=1e-12, atol=0)
+
+
+def test_xgboost_json_on_device_equals_oracle(sa):
+    from oracle import tree_oracle as to
+    g, df, ab, fb, X = _game(sa)
+    kinds = [k for _, k, _ in fb.plan.order]
+    model = sa['trees'].synthetic_xgboost_json(len(kinds), n_trees=100, depth=3, seed=3,
+                                               feature_kinds=kinds, base_score=0.3)
+    te = sa['trees'].TreeEnsemble.from_model(model)
+    p = te.predict_blocks(fb).cpu().numpy()
+    assert p.dtype == np.float32
+    ref = to.predict_xgboost_json(model, X)
+    np.testing.assert_allclose(p, ref, rtol=1e-6, atol=0)
+
+
+def test_missing_values_follow_default_direction(sa):
+    """NaN written into a device feature column takes default_left, like the oracle."""
+    from oracle import tree_oracle as to
+    g, df, ab, fb, X = _game(sa)
+    kinds = [k for _, k, _ in fb.plan.order]
+    fcols = [j for j, k in enumerate(kinds) if k == 'f']
+    model = sa['trees'].synthetic_xgboost_json(len(kinds), n_trees=50, depth=3, seed=4,
+                                               feature_kinds=kinds)
+    used = sorted({j for t in model['learner']['gradient_booster']['model']['trees']
+                   for j, lc in zip(t['split_indices'], t['left_children']) if lc >= 0} & set(fcols))
+    j = used[0]
+    col = fb.plan.order[j][2]
+    rows = np.arange(0, fb.n, 3)
+    blk = fb.f64_block  # [tiles, C, R]; one tile here
+    blk[0, col, torch.from_numpy(rows).to(blk.device)] = float('nan')
+    X = X.copy()
+    X[rows, j] = np.nan
+    te = sa['trees'].TreeEnsemble.from_model(model)
+    np.testing.assert_allclose(te.predict_blocks(fb).cpu().numpy(),
+                               to.predict_xgboost_json(model, X), rtol=1e-6, atol=0)
+
+
+def test_vaep_rate_on_device(sa):
+    """VAEP.rate / rate_batch with tree learners: features, predict_proba and formula on the
+    device == the reference's host path (host predict_proba on compute_features output ->
+    formula.value)."""
+    from oracle import vaep_oracle as vo
+    from socceraction_amd import synthetic
+    import socceraction_amd.vaep as vaep
+    from sklearn.ensemble import HistGradientBoostingClassifier
+    d = synthetic.spadl_games(6, seed=21)
+    actions = synthetic.to_frame(d)
+    games = synthetic.games_frame(d)
+    model = vaep.VAEP()
+    X = model.compute_features_batch(games, actions)
+    Y = model.compute_labels_batch(games, actions)
+    sk = {c: HistGradientBoostingClassifier(max_iter=20, max_depth=3, random_state=0)
+          .fit(X, Y[c]) for c in ('scores', 'concedes')}
+    model._VAEP__models = sk
+    got = model.rate_batch(games, actions)
+    assert list(got.columns) == ['offensive_value', 'defensive_value', 'vaep_value']
+    off = d['game_off']
+    for gi in range(len(off) - 1):
+        s, e = int(off[gi]), int(off[gi + 1])
+        cols = {c: d[c][s:e] for c in ('period_id', 'time_seconds', 'team_id', 'type_id',
+                                       'result_id')}
+        ps = sk['scores'].predict_proba(X.iloc[s:e])[:, 1]
+        pc = sk['concedes'].predict_proba(X.iloc[s:e])[:, 1]
+        fo = vo.formula(cols, ps, pc)
+        for c in ('offensive_value', 'defensive_value', 'vaep_value'):
+            assert_close(got[c].to_numpy()[s:e], fo[c], c)
+    # per-game rate through the drop-in (device path) == the batched values
+    g0 = games.iloc[0]
+    one = model.rate(g0, actions[actions.game_id == g0.game_id].reset_index(drop=True))
+    assert_close(one['vaep_value'].to_numpy(), got['vaep_value'].to_numpy()[:len(one)], 'rate')
+    # xgboost-format learners: float32 probabilities -> float32 values (the reference's dtype)
+    kinds = ['f'] * X.shape[1]
+    xg = {c: sa['trees'].synthetic_xgboost_json(X.shape[1], n_trees=20, seed=s, feature_kinds=kinds)
+          for s, c in enumerate(('scores', 'concedes'))}
+    model._VAEP__models = xg
+    got32 = model.rate_batch(games, actions)
+    assert got32['vaep_value'].dtype == np.float32

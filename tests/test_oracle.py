@@ -95,3 +95,38 @@ def test_convert_oracle(name):
     # floats are produced by the same operations as the reference: bit-exact here
     for c in ('time_seconds', 'x', 'y', 'dx', 'dy'):
         np.testing.assert_array_equal(got[c], ref[c], err_msg=f'{name} {c}')
+
+
+def test_tree_oracle_matches_sklearn_predict_proba():
+    """The tree walk of oracle/tree_oracle.py (float64, x <= threshold) equals scikit-learn's
+    own HistGradientBoostingClassifier.predict_proba on VAEP features of a golden game, incl.
+    missing values."""
+    from sklearn.ensemble import HistGradientBoostingClassifier
+
+    from oracle import tree_oracle as to
+    g = load('spadl', 'full0')
+    X = np.concatenate([g['k3_feat_b'].astype(np.float64), g['k3_feat_f'],
+                        g['k3_feat_i'].astype(np.float64)], axis=1)
+    y = g['scores'].astype(int)
+    y[::7] = 1  # enough positives to grow real trees
+    X = X.copy()
+    X[::13, 520] = np.nan
+    clf = HistGradientBoostingClassifier(max_iter=30, max_depth=3, random_state=0).fit(X, y)
+    np.testing.assert_allclose(to.predict_sklearn_nodes(clf, X), clf.predict_proba(X)[:, 1],
+                               rtol=1e-12, atol=0)
+
+
+def test_tree_oracle_xgboost_rules():
+    """Hand-checked xgboost rules: x < threshold goes left (equality goes right), NaN follows
+    default_left, leaves sum in tree order in float32 onto logit(base_score)."""
+    from oracle import tree_oracle as to
+    tree = {'left_children': [1, -1, -1], 'right_children': [2, -1, -1],
+            'split_indices': [0, 0, 0], 'split_conditions': [1.0, -0.5, 0.25],
+            'default_left': [1, 0, 0]}
+    model = {'learner': {'objective': {'name': 'binary:logistic'},
+                         'learner_model_param': {'base_score': '5E-1'},
+                         'gradient_booster': {'model': {'trees': [tree, tree]}}}}
+    X = np.array([[0.5], [1.0], [2.0], [np.nan]])
+    p = to.predict_xgboost_json(model, X)
+    m = np.array([-1.0, 0.5, 0.5, -1.0], np.float32)
+    np.testing.assert_array_equal(p, (1 / (1 + np.exp(-m))).astype(np.float32))
