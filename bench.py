@@ -214,6 +214,27 @@ def convert_extra(d, dist, dev, reps: int = 3) -> dict:
             'spadl_actions_per_s_end_to_atomic_features': round(n_in / (ms_conv + ms_feat) * 1e3, 1)}
 
 
+def rate_extra(ab, out, n, dev, reps: int = 5) -> dict:
+    """VAEP.rate fully on device alongside the main line: the features already computed by
+    the main step feed two xgboost-shaped learners (100 trees, depth 3: the reference's default
+    XGBClassifier, vaep/base.py:226-231; random splits, xgboost is not installed) evaluated on
+    the feature blocks, then formula.value on their float32 probabilities."""
+    from socceraction_amd import trees
+    kinds = [k for _, k, _ in out.plan.order]
+    models = [trees.TreeEnsemble.from_xgboost_json(
+        trees.synthetic_xgboost_json(len(kinds), n_trees=100, depth=3, seed=s, feature_kinds=kinds))
+        for s in (1, 2)]
+    ps = models[0].predict_blocks(out)
+    pc = models[1].predict_blocks(out)
+    val = torch.empty((3, (n + 15) // 16 * 16), dtype=torch.float32, device=dev)
+    ms_tree = _events_ms(lambda: models[0].predict_blocks(out, out=ps), reps)
+    ms_formula = _events_ms(lambda: ops.formula(ab, ps, pc, val), reps)
+    return {'workload': 'VAEP.rate on device: 2 x xgboost-shaped tree ensembles (100 trees, depth '
+                        '3) on the cfg2 feature blocks + formula (float32 probabilities)',
+            'ms_per_model': round(ms_tree, 4), 'ms_formula_f32': round(ms_formula, 4),
+            'actions_per_s_predict_both_models': round(n / (2 * ms_tree) * 1e3, 1)}
+
+
 def cpu_baseline(d, seconds: float) -> dict:
     """The oracle port (numpy, 1 thread) on the GPU box's host, over whole games."""
     from oracle import vaep_oracle as vo
@@ -330,6 +351,7 @@ def main() -> None:
         extra_side['xt105_cfg5'] = xt105_extra(ab, dist, dev, args.xt_sharded)
         extra_side['atomic_cfg3'] = atomic_extra(dist, rank, world, dev, args.atomic_games)
         extra_side['convert_to_atomic'] = convert_extra(d, dist, dev)
+        extra_side['rate_on_device'] = rate_extra(ab, out, n, dev)
     if rank != 0:
         if dist:
             dist.destroy_process_group()

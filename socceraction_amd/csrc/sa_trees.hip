@@ -11,13 +11,15 @@
 //     p = 1 / (1 + exp(-margin)) in float32.
 //   scikit-learn HistGradientBoostingClassifier: float64; `x <= threshold` goes left; NaN
 //     follows missing_go_to_left; p = expit(margin) in float64.
-// The model's nodes are staged in LDS when they fit (a default 100-tree depth-3 model is 36 KB)
-// so the per-node loads of divergent lanes are LDS reads; feature values are read from the
+// The model's nodes are staged in LDS when they fit (a default 100-tree depth-3 model is 36 KB),
+// sized to the model and shared by 16 waves per workgroup (occupancy), so the per-node loads of
+// divergent lanes are LDS reads; feature values are read from the
 // tiled blocks (row j of a column is contiguous across lanes: coalesced at the root, L2-resident
 // afterwards).
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <type_traits>
 
 #include "sa_common.h"
 #include "sa_internal.h"
@@ -32,81 +34,105 @@ struct TNode {  // 24 B
   int32_t pad;
 };
 
-constexpr int TR_THREADS = 256;
+constexpr int TR_THREADS = 1024;  // 16 waves share one LDS copy of the model
 constexpr int TR_LDS_NODES = 2048;  // 48 KB
+constexpr int TR_LDS_SLOTS = 2048;  // 8 KB
+constexpr int TG = 8;               // trees walked together per thread
 
-__device__ __forceinline__ double feature_value(const sa_block& Bb, const sa_block& Bf,
-                                                const sa_block& Bi, int32_t slot, int64_t j) {
-  const int kind = slot >> 24, col = slot & 0xFFFFFF;
-  if (kind == 0) {
-    const int64_t R = Bb.tile_rows, t = j / R;
-    return (double)((const uint8_t*)Bb.data)[t * Bb.n_cols * R + (int64_t)col * R + (j - t * R)];
-  }
-  if (kind == 1) {
-    const int64_t R = Bf.tile_rows, t = j / R;
-    return ((const double*)Bf.data)[t * Bf.n_cols * R + (int64_t)col * R + (j - t * R)];
-  }
-  const int64_t R = Bi.tile_rows, t = j / R;
-  return (double)((const int64_t*)Bi.data)[t * Bi.n_cols * R + (int64_t)col * R + (j - t * R)];
+// Row j's element of column `col` in each tiled block is base[kind] + col * R[kind]; the
+// per-row bases are computed once (one division per block) instead of per feature read.
+struct RowBases {
+  const uint8_t* b;
+  const double* f;
+  const int64_t* i;
+  int64_t Rb, Rf, Ri;
+};
+
+__device__ __forceinline__ RowBases row_bases(const sa_block& Bb, const sa_block& Bf, const sa_block& Bi,
+                                              int64_t j) {
+  RowBases r;
+  const int64_t tb = j / Bb.tile_rows, tf = j / Bf.tile_rows, ti = j / Bi.tile_rows;
+  r.Rb = Bb.tile_rows;
+  r.Rf = Bf.tile_rows;
+  r.Ri = Bi.tile_rows;
+  r.b = (const uint8_t*)Bb.data + (tb * Bb.n_cols * r.Rb + (j - tb * r.Rb));
+  r.f = (const double*)Bf.data + (tf * Bf.n_cols * r.Rf + (j - tf * r.Rf));
+  r.i = (const int64_t*)Bi.data + (ti * Bi.n_cols * r.Ri + (j - ti * r.Ri));
+  return r;
 }
 
-template <bool F32>
+__device__ __forceinline__ double feature_value(const RowBases& r, int32_t slot) {
+  const int kind = slot >> 24;
+  const int64_t col = slot & 0xFFFFFF;
+  if (kind == 0) return (double)r.b[col * r.Rb];
+  if (kind == 1) return r.f[col * r.Rf];
+  return (double)r.i[col * r.Ri];
+}
+
+template <bool F32, bool STAGED>
 __global__ __launch_bounds__(TR_THREADS) void tree_predict_kernel(const TNode* __restrict__ nodes, int n_nodes,
                                                                    const int32_t* __restrict__ roots, int n_trees,
-                                                                   const int32_t* __restrict__ slots,
+                                                                   const int32_t* __restrict__ slots, int n_slots,
                                                                    sa_block Bb, sa_block Bf, sa_block Bi,
                                                                    int64_t n, double base, int le,
                                                                    void* __restrict__ out) {
-  __shared__ TNode lds[TR_LDS_NODES];
-  const bool staged = n_nodes <= TR_LDS_NODES;
-  if (staged) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char tr_lds[];  // nodes, then slots
+  TNode* lds = reinterpret_cast<TNode*>(tr_lds);
+  int32_t* lslots = reinterpret_cast<int32_t*>(tr_lds + (size_t)n_nodes * sizeof(TNode));
+  // STAGED (host-checked: nodes and slots fit): every node / slot read is an LDS read; the
+  // pointers must not be a runtime select between LDS and global, which compiles to flat
+  // loads on the memory path
+  if (STAGED) {
     for (int k = threadIdx.x; k < n_nodes; k += blockDim.x) lds[k] = nodes[k];
+    for (int k = threadIdx.x; k < n_slots; k += blockDim.x) lslots[k] = slots[k];
     __syncthreads();
   }
-  const TNode* __restrict__ N = staged ? lds : nodes;
+  const TNode* __restrict__ N = STAGED ? lds : nodes;
+  const int32_t* __restrict__ S = STAGED ? lslots : slots;
   const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n) return;
-  if (F32) {
-    float m = (float)base;
-    for (int t = 0; t < n_trees; ++t) {
-      int k = roots[t];
-      for (;;) {
-        const TNode nd = N[k];
+  const RowBases rb = row_bases(Bb, Bf, Bi, j);
+  // TG trees walked together: their feature reads are independent, so a wave keeps TG loads
+  // in flight instead of one dependent load per level; leaf values are added in tree order.
+  using A = typename std::conditional<F32, float, double>::type;
+  A m = (A)base;
+  for (int t0 = 0; t0 < n_trees; t0 += TG) {
+    int k[TG];
+    A leafv[TG];
+    uint32_t live = 0;
+#pragma unroll
+    for (int u = 0; u < TG; ++u) {
+      k[u] = t0 + u < n_trees ? roots[t0 + u] : 0;
+      leafv[u] = A(0);
+      if (t0 + u < n_trees) live |= 1u << u;
+    }
+    while (live) {
+#pragma unroll
+      for (int u = 0; u < TG; ++u) {
+        if (!(live & (1u << u))) continue;
+        const TNode nd = N[k[u]];
         if (nd.feature < 0) {
-          m = m + (float)nd.thr_or_value;
-          break;
+          leafv[u] = (A)nd.thr_or_value;
+          live &= ~(1u << u);
+          continue;
         }
-        const float v = (float)feature_value(Bb, Bf, Bi, slots[nd.feature], j);
-        const bool dl = nd.right < 0;
+        const A v = (A)feature_value(rb, S[nd.feature]);
+        const A thr = (A)nd.thr_or_value;
         const int right = nd.right & 0x7FFFFFFF;
         if (isnan(v))
-          k = dl ? nd.left : right;
+          k[u] = nd.right < 0 ? nd.left : right;
         else
-          k = (le ? v <= (float)nd.thr_or_value : v < (float)nd.thr_or_value) ? nd.left : right;
+          k[u] = (le ? v <= thr : v < thr) ? nd.left : right;
       }
     }
-    ((float*)out)[j] = 1.0f / (1.0f + expf(-m));
-  } else {
-    double m = base;
-    for (int t = 0; t < n_trees; ++t) {
-      int k = roots[t];
-      for (;;) {
-        const TNode nd = N[k];
-        if (nd.feature < 0) {
-          m = m + nd.thr_or_value;
-          break;
-        }
-        const double v = feature_value(Bb, Bf, Bi, slots[nd.feature], j);
-        const bool dl = nd.right < 0;
-        const int right = nd.right & 0x7FFFFFFF;
-        if (isnan(v))
-          k = dl ? nd.left : right;
-        else
-          k = (le ? v <= nd.thr_or_value : v < nd.thr_or_value) ? nd.left : right;
-      }
-    }
-    ((double*)out)[j] = 1.0 / (1.0 + exp(-m));
+#pragma unroll
+    for (int u = 0; u < TG; ++u)
+      if (t0 + u < n_trees) m = m + leafv[u];
   }
+  if (F32)
+    ((float*)out)[j] = 1.0f / (1.0f + expf(-(float)m));
+  else
+    ((double*)out)[j] = 1.0 / (1.0 + exp(-(double)m));
 }
 
 }  // namespace sa
@@ -120,17 +146,25 @@ extern "C" int sa_tree_predict(const void* nodes, int32_t n_nodes, const int32_t
   if (n < 0 || n_nodes < 1 || n_trees < 0 || n_features < 0 || !nodes || !roots || !p_out ||
       (n_features > 0 && !feature_slots))
     return fail(SA_EINVAL, "bad tree model arguments");
-  sa_block z{nullptr, 0, 0, 16};
+  sa_block z{nullptr, 0, 0, 16};  // absent block: never read (no slot refers to it)
   const sa_block Bb = bool_blk ? *bool_blk : z, Bf = f64_blk ? *f64_blk : z, Bi = i64_blk ? *i64_blk : z;
   if (n == 0) return SA_OK;
   const dim3 grid((unsigned)((n + TR_THREADS - 1) / TR_THREADS)), block(TR_THREADS);
   hipStream_t st = (hipStream_t)stream;
   const TNode* nd = (const TNode*)nodes;
-  if (f32)
-    hipLaunchKernelGGL(tree_predict_kernel<true>, grid, block, 0, st, nd, n_nodes, roots, n_trees, feature_slots,
-                       Bb, Bf, Bi, n, base_margin, le, p_out);
+  const bool staged = n_nodes <= TR_LDS_NODES && n_features <= TR_LDS_SLOTS;
+  const size_t lds_bytes = (size_t)n_nodes * sizeof(TNode) + (size_t)n_features * sizeof(int32_t);
+#define SA_TREE_LAUNCH(F, S)                                                                       \
+  hipLaunchKernelGGL((tree_predict_kernel<F, S>), grid, block, S ? lds_bytes : 0, st, nd, n_nodes, roots, n_trees, \
+                     feature_slots, n_features, Bb, Bf, Bi, n, base_margin, le, p_out)
+  if (f32 && staged)
+    SA_TREE_LAUNCH(true, true);
+  else if (f32)
+    SA_TREE_LAUNCH(true, false);
+  else if (staged)
+    SA_TREE_LAUNCH(false, true);
   else
-    hipLaunchKernelGGL(tree_predict_kernel<false>, grid, block, 0, st, nd, n_nodes, roots, n_trees,
-                       feature_slots, Bb, Bf, Bi, n, base_margin, le, p_out);
+    SA_TREE_LAUNCH(false, false);
+#undef SA_TREE_LAUNCH
   return check_launch("tree_predict_kernel");
 }
