@@ -37,7 +37,10 @@ struct TNode {  // 24 B
 constexpr int TR_THREADS = 1024;  // 16 waves share one LDS copy of the model
 constexpr int TR_LDS_NODES = 2048;  // 48 KB
 constexpr int TR_LDS_SLOTS = 2048;  // 8 KB
-constexpr int TG = 8;               // trees walked together per thread
+#ifndef SA_TREE_TG
+#define SA_TREE_TG 8
+#endif
+constexpr int TG = SA_TREE_TG;      // trees walked together per thread
 
 // Row j's element of column `col` in each tiled block is base[kind] + col * R[kind]; the
 // per-row bases are computed once (one division per block) instead of per feature read.
