@@ -275,6 +275,46 @@ int sa_atomic_count(const sa_spadl_frame* in, void* scratch, int64_t* n_out, voi
 int sa_atomic_emit(const sa_spadl_frame* in, const void* scratch, const sa_atomic_frame* out,
                    void* stream);
 
+/* ---- _add_dribbles (spadl/base.py:54-93) ------------------------------------------
+ * SPADL rows out (device, length n_out): the input columns' codes plus `src`, the input row a
+ * row came from (>= 0), or ~q for a dribble inserted before input row q (the successor whose
+ * game / team / player / timestamp it carries). action_id is the row position. */
+typedef struct sa_spadl_out {
+  double* time_seconds;
+  double* start_x;
+  double* start_y;
+  double* end_x;
+  double* end_y;
+  int32_t* game;
+  int32_t* team;
+  int32_t* player;
+  int32_t* event;             /* -1 = missing (the dribbles) */
+  uint8_t* period_id;
+  uint8_t* type_id;
+  uint8_t* result_id;
+  uint8_t* bodypart_id;
+  int64_t* src;
+} sa_spadl_out;
+
+/* Pass 1 (replaces the shift / predicate half of spadl/base.py:54-69): marks row j (flags[j],
+ * optional) when a dribble is inserted between it and its input-order successor, and leaves
+ * the per-block output counts and their prefix in scratch (sa_atomic_scratch_bytes(n) bytes);
+ * *n_out [host] = n + dribbles. Thresholds: min_dribble_length**2, max_dribble_length**2,
+ * max_dribble_duration (spadl/base.py:49-51). in->order must be NULL. With action_id (device,
+ * f64 [n], the sort key the reference compares after its concat), *n_misplaced [host,
+ * optional] counts the rows that rule out the fast layout of sa_dribble_emit (keys not
+ * strictly increasing, or a dribble not sorting between its row and the next); -1 without
+ * action_id. Game codes must preserve the game_id order. Synchronises. */
+int sa_dribble_count(const sa_spadl_frame* in, double min_len2, double max_len2, double max_dt,
+                     const double* action_id, void* scratch, uint8_t* flags, int64_t* n_out,
+                     int64_t* n_misplaced, void* stream);
+/* Pass 2 (spadl/base.py:71-93): writes the n_out rows in the reference's sorted order.
+ * dest == NULL: input keys strictly increasing and every dribble sorting directly after its
+ * row (row j at j + dribbles before j, its dribble next); else dest[n_out] is the output
+ * position of each concatenated row (the n inputs, then the dribbles in input order). */
+int sa_dribble_emit(const sa_spadl_frame* in, double min_len2, double max_len2, double max_dt,
+                    const void* scratch, const int64_t* dest, const sa_spadl_out* out, void* stream);
+
 /* Segment (game) offsets of a row-sorted key column whose values are exactly 0..n_segments-1,
  * each present -- e.g. the game codes of sa_atomic_emit's output:
  * seg_off[g] = first row of g, seg_off[n_segments] = n. */

@@ -158,6 +158,19 @@ def _extra_from_fouls(f):
     return _merge(f, e)
 
 
+def add_dribbles(cols: Dict[str, np.ndarray]) -> Dict[str, np.ndarray]:
+    """spadl/base.py:54-93 on its own (the SPADL converters' last step): the SPADL columns of
+    COLS in, the same columns out with action_id reset to int64 positions."""
+    f = {c: np.asarray(cols[c]) for c in COLS}
+    f['action_id'] = f['action_id'].astype(np.float64)
+    f['original_event_id'] = f['original_event_id'].astype(object)
+    if len(f['type_id']) == 0:
+        return {c: (v.astype(np.int64) if c == 'action_id' else v) for c, v in f.items()}
+    f = _add_dribbles(f)
+    f['action_id'] = f['action_id'].astype(np.int64)
+    return f
+
+
 def convert_to_atomic(cols: Dict[str, np.ndarray]) -> Dict[str, np.ndarray]:
     """base.py:15-35: the four passes, _convert_columns (:199-220) and _simplify (:223-235)."""
     f = {c: np.asarray(cols[c]) for c in COLS}

@@ -6,6 +6,8 @@ profiles/.
     python scripts/bench_workloads.py atomic [--games 10000]   # cfg3: ~4.0e7 atomic actions
     python scripts/bench_workloads.py xt105 [--games 7812]      # cfg5 per-GPU slice: ~1.25e7
     python scripts/bench_workloads.py e2e [--games 500]         # pandas in -> pandas out
+    python scripts/bench_workloads.py convert [--games 10000]   # SPADL -> Atomic-SPADL
+    python scripts/bench_workloads.py dribbles [--games 10000]  # spadl.base._add_dribbles
 
 All device timings are HIP events on torch's current stream (the launch stream); wall
 times bracket torch.cuda.synchronize().
@@ -170,15 +172,51 @@ def convert(args) -> dict:
             'GBs': round((2 * 60 * frame.n + 59 * out.n) / ms * 1e-6, 1)}
 
 
+def dribbles(args) -> dict:
+    """_add_dribbles on device (count + scan + emit) over cfg2 games, plus the drop-in's
+    DataFrame-in / DataFrame-out time on a 500-game slice."""
+    from socceraction_amd.atomic.spadl import base as cb
+    from socceraction_amd.spadl import base as sb
+    dev = B.device()
+    d = synthetic.spadl_games(args.games)
+    df = synthetic.to_frame(d)
+    df['original_event_id'] = None
+    aid = np.arange(len(df), dtype=np.int64)
+    df['action_id'] = aid
+    frame = cb.SpadlFrame.from_frame(df, dev=dev, sort=False)
+    aid = torch.from_numpy(aid).to(dev)
+    out = sb.add_dribbles_device(frame, aid)
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(args.steps):
+        out = sb.add_dribbles_device(frame, aid)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t) / args.steps * 1e3
+    small = df.iloc[:int(d['game_off'][min(500, len(d['game_off']) - 1)])].copy()
+    small['action_id'] = small.groupby('game_id').cumcount().astype(np.int64)
+    sb._add_dribbles(small)
+    t = time.perf_counter()
+    res = sb._add_dribbles(small)
+    ms_df = (time.perf_counter() - t) * 1e3
+    return {'workload': '_add_dribbles (device count + scan + emit)', 'spadl_actions': frame.n,
+            'out_actions': out.n, 'ms_per_call': round(ms, 4),
+            'GBs': round((120 * frame.n + 68 * out.n) / ms * 1e-6, 1),
+            'dropin_dataframe_actions': len(small), 'dropin_out_actions': len(res),
+            'dropin_ms': round(ms_df, 2),
+            'dropin_actions_per_s': round(len(small) / ms_df * 1e3, 1)}
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
-    ap.add_argument('workload', choices=('atomic', 'xt105', 'e2e', 'convert'))
+    ap.add_argument('workload', choices=('atomic', 'xt105', 'e2e', 'convert', 'dribbles'))
     ap.add_argument('--games', type=int, default=None)
     ap.add_argument('--steps', type=int, default=10)
     args = ap.parse_args()
     if args.games is None:
-        args.games = {'atomic': 10000, 'xt105': 7812, 'e2e': 500, 'convert': 10000}[args.workload]
-    line = {'atomic': atomic, 'xt105': xt105, 'e2e': e2e, 'convert': convert}[args.workload](args)
+        args.games = {'atomic': 10000, 'xt105': 7812, 'e2e': 500, 'convert': 10000,
+                      'dribbles': 10000}[args.workload]
+    line = {'atomic': atomic, 'xt105': xt105, 'e2e': e2e, 'convert': convert,
+            'dribbles': dribbles}[args.workload](args)
     line['device'] = torch.cuda.get_device_name(0)
     print(json.dumps(line), flush=True)
 

@@ -69,6 +69,13 @@ class SaAtomicFrame(ctypes.Structure):
                 ('type_id', _p), ('bodypart_id', _p)]
 
 
+class SaSpadlOut(ctypes.Structure):
+    _fields_ = [('time_seconds', _p), ('start_x', _p), ('start_y', _p), ('end_x', _p),
+                ('end_y', _p), ('game', _p), ('team', _p), ('player', _p), ('event', _p),
+                ('period_id', _p), ('type_id', _p), ('result_id', _p), ('bodypart_id', _p),
+                ('src', _p)]
+
+
 # name -> (restype, argtypes)
 _SIGNATURES = {
     'sa_vaep_features': (ctypes.c_int, [ctypes.POINTER(SaActions), ctypes.POINTER(SaFeaturePlan),
@@ -99,6 +106,13 @@ _SIGNATURES = {
                                        ctypes.POINTER(ctypes.c_int64), _p]),
     'sa_atomic_emit': (ctypes.c_int, [ctypes.POINTER(SaSpadlFrame), _p,
                                       ctypes.POINTER(SaAtomicFrame), _p]),
+    'sa_dribble_count': (ctypes.c_int, [ctypes.POINTER(SaSpadlFrame), ctypes.c_double,
+                                        ctypes.c_double, ctypes.c_double, _p, _p, _p,
+                                        ctypes.POINTER(ctypes.c_int64),
+                                        ctypes.POINTER(ctypes.c_int64), _p]),
+    'sa_dribble_emit': (ctypes.c_int, [ctypes.POINTER(SaSpadlFrame), ctypes.c_double,
+                                       ctypes.c_double, ctypes.c_double, _p, _p,
+                                       ctypes.POINTER(SaSpadlOut), _p]),
     'sa_segment_offsets': (ctypes.c_int, [_p, ctypes.c_int64, ctypes.c_int64, _p, _p]),
     'sa_tree_predict': (ctypes.c_int, [_p, ctypes.c_int32, _p, ctypes.c_int32, _p, ctypes.c_int32,
                                        ctypes.POINTER(SaBlock), ctypes.POINTER(SaBlock),

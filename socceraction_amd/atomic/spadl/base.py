@@ -117,7 +117,8 @@ class SpadlFrame:
     dtypes: Dict[str, np.dtype]
 
     @classmethod
-    def from_frame(cls, actions: pd.DataFrame, dev=None) -> 'SpadlFrame':
+    def from_frame(cls, actions: pd.DataFrame, dev=None, sort: bool = True) -> 'SpadlFrame':
+        """``sort=False``: rows stay in input order (no ``order`` permutation)."""
         for c in _REQUIRED:
             if c not in actions.columns:
                 raise AttributeError(f"'DataFrame' object has no attribute '{c}'")
@@ -142,7 +143,7 @@ class SpadlFrame:
             'result_id': _ids(actions, 'result_id', 0, 5),
             'bodypart_id': _ids(actions, 'bodypart_id', 0, 3),
         }
-        order = _sorted_order(g, per, actions['action_id'].to_numpy())
+        order = _sorted_order(g, per, actions['action_id'].to_numpy()) if sort else None
         if order is not None:
             arrays['order'] = order
         buf, views = _pack(arrays, dev)

@@ -353,6 +353,113 @@ __global__ __launch_bounds__(AC_THREADS) void atomic_emit_kernel(sa_spadl_frame 
     for (int k = threadIdx.x; k < tot; k += AC_THREADS) uo[col][base + k] = lu[col * AC_MAX_OUT + k];
 }
 
+// ---- _add_dribbles as an operator of its own (spadl/base.py:54-93) -----------------------
+// Row j is compared with its INPUT-order successor (shift(-1, fill_value=0): the last row meets
+// an all-zero row whose period 0 never matches).  A dribble row j' carries the successor's
+// game / period / team / player, the midpoint time, start = j's end and end = the successor's
+// start, foot / dribble / success.  Output order: when the (game, period, action_id) keys of
+// the input increase strictly and every dribble's key (successor's game and period, action_id
+// + 0.1) falls below its successor's key (host-checked), the reference's sort puts j' directly
+// after j, so rows are written at j + (dribbles before j) (+1 for j'); otherwise the host's
+// stable lexsort of the concatenated keys gives every row's position in `dest` (first the n
+// input rows, then the dribbles in input order -- the reference's concat order).
+struct DribbleRule {
+  double min2, max2, max_dt;  // min_dribble_length**2, max_dribble_length**2, max_dribble_duration
+};
+
+__device__ __forceinline__ bool dribble_after(const sa_spadl_frame& F, int64_t j, const DribbleRule& D,
+                                              SRow& R, SRow& Q) {
+  R = load_srow(F, j);
+  if (j + 1 >= F.n) return false;
+  Q = load_srow(F, j + 1);
+  const double dx = R.ex - Q.sx, dy = R.ey - Q.sy;
+  const double d2 = dx * dx + dy * dy;
+  const double dt = Q.t - R.t;
+  return R.team == Q.team && d2 >= D.min2 && d2 <= D.max2 && dt < D.max_dt && R.per == Q.per;
+}
+
+// Also counts (into *misplaced) the rows that rule out the fast layout: input keys (game code,
+// period, action_id) not strictly above the previous row's, or a dribble whose key
+// (action_id + 0.1) does not fall strictly between its row's and its successor's.
+__global__ __launch_bounds__(AC_THREADS) void dribble_count_kernel(sa_spadl_frame F, DribbleRule D,
+                                                                  const double* __restrict__ aid,
+                                                                  int64_t* __restrict__ bsum,
+                                                                  unsigned long long* __restrict__ misplaced,
+                                                                  uint8_t* __restrict__ flags) {
+  __shared__ int64_t wsum[AC_THREADS / 64];
+  const int64_t p = (int64_t)blockIdx.x * AC_BLOCK_ROWS + threadIdx.x;
+  int64_t c = 0;
+  bool bad = false;
+  if (p < F.n) {
+    SRow R, Q;
+    const bool d = dribble_after(F, p, D, R, Q);
+    if (flags) flags[p] = d;
+    c = 1 + d;
+    if (aid) {
+      const double a = aid[p];
+      if (p > 0) {
+        const int32_t g0 = F.game[p - 1];
+        const int p0 = F.period_id[p - 1];
+        const double a0 = aid[p - 1];
+        bad = !(g0 < R.game || (g0 == R.game && (p0 < R.per || (p0 == R.per && a0 < a))));
+      }
+      if (d) {
+        const double da = a + 0.1;
+        bad |= !(da > a && da < aid[p + 1]);
+      }
+    }
+  }
+  const uint64_t m = __ballot(bad);
+  if ((threadIdx.x & 63) == 0 && m) atomicAdd(misplaced, (unsigned long long)__popcll(m));
+  int64_t total;
+  block_excl_scan(c, wsum, total);
+  if (threadIdx.x == 0) bsum[blockIdx.x] = total;
+}
+
+__device__ __forceinline__ void put_spadl_row(const sa_spadl_out& O, int64_t o, double t, double sx, double sy,
+                                              double ex, double ey, int32_t game, int32_t team,
+                                              int32_t player, int32_t event, int per, int type, int res,
+                                              int bp, int64_t src) {
+  O.time_seconds[o] = t;
+  O.start_x[o] = sx;
+  O.start_y[o] = sy;
+  O.end_x[o] = ex;
+  O.end_y[o] = ey;
+  O.game[o] = game;
+  O.team[o] = team;
+  O.player[o] = player;
+  O.event[o] = event;
+  O.period_id[o] = (uint8_t)per;
+  O.type_id[o] = (uint8_t)type;
+  O.result_id[o] = (uint8_t)res;
+  O.bodypart_id[o] = (uint8_t)bp;
+  O.src[o] = src;
+}
+
+__global__ __launch_bounds__(AC_THREADS) void dribble_emit_kernel(sa_spadl_frame F, DribbleRule D,
+                                                                 const int64_t* __restrict__ bpre,
+                                                                 const int64_t* __restrict__ dest,
+                                                                 sa_spadl_out O) {
+  __shared__ int64_t wsum[AC_THREADS / 64];
+  const int64_t p = (int64_t)blockIdx.x * AC_BLOCK_ROWS + threadIdx.x;
+  const bool live = p < F.n;
+  SRow R, Q;
+  bool d = false;
+  if (live) d = dribble_after(F, p, D, R, Q);
+  int64_t total;
+  const int64_t lo = block_excl_scan(live ? 1 + d : 0, wsum, total);
+  if (!live) return;
+  const int64_t g = bpre[blockIdx.x] + lo;  // row p's position in the fast layout
+  const int64_t o = dest ? dest[p] : g;
+  put_spadl_row(O, o, R.t, R.sx, R.sy, R.ex, R.ey, R.game, R.team, R.player, R.event, R.per, R.type, R.res,
+                R.bp, p);
+  if (d) {
+    const int64_t od = dest ? dest[F.n + (g - p)] : g + 1;  // g - p = dribbles before row p
+    put_spadl_row(O, od, (R.t + Q.t) / 2, R.ex, R.ey, Q.sx, Q.sy, Q.game, Q.team, Q.player, -1, Q.per,
+                  A_DRIBBLE, 1, 0, ~(p + 1));
+  }
+}
+
 // seg_off[key[k]] = k at every run start of the sorted keys 0..n_seg-1 (each present)
 __global__ __launch_bounds__(256) void segment_offsets_kernel(const int32_t* __restrict__ key, int64_t n,
                                                               int64_t n_seg, int64_t* __restrict__ seg_off) {
@@ -371,7 +478,7 @@ using namespace sa;
 static int64_t n_blocks(int64_t n) { return (n + AC_BLOCK_ROWS - 1) / AC_BLOCK_ROWS; }
 
 extern "C" int64_t sa_atomic_scratch_bytes(int64_t n) {
-  return n < 0 ? 0 : (n_blocks(n) + 1) * (int64_t)sizeof(int64_t);
+  return n < 0 ? 0 : (n_blocks(n) + 2) * (int64_t)sizeof(int64_t);
 }
 
 static int check_spadl_frame(const sa_spadl_frame* F) {
@@ -415,6 +522,57 @@ extern "C" int sa_atomic_emit(const sa_spadl_frame* in, const void* scratch, con
   hipLaunchKernelGGL(atomic_emit_kernel, dim3((unsigned)nb), dim3(AC_THREADS), 0, (hipStream_t)stream,
                      *in, (const int64_t*)scratch, *out);
   return check_launch("atomic_emit_kernel");
+}
+
+static int check_dribble_rule(double min2, double max2, double max_dt) {
+  if (!(min2 >= 0) || !(max2 >= 0) || max_dt != max_dt) return fail(SA_EINVAL, "bad dribble thresholds");
+  return SA_OK;
+}
+
+extern "C" int sa_dribble_count(const sa_spadl_frame* in, double min_len2, double max_len2, double max_dt,
+                                const double* action_id, void* scratch, uint8_t* flags, int64_t* n_out,
+                                int64_t* n_misplaced, void* stream) {
+  int rc = check_spadl_frame(in);
+  if (rc || (rc = check_dribble_rule(min_len2, max_len2, max_dt))) return rc;
+  if (in->order) return fail(SA_EINVAL, "_add_dribbles reads rows in input order: order must be NULL");
+  if (!n_out || (in->n > 0 && !scratch)) return fail(SA_EINVAL, "null scratch or n_out");
+  *n_out = 0;
+  if (n_misplaced) *n_misplaced = action_id ? 0 : -1;
+  if (in->n == 0) return SA_OK;
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t nb = n_blocks(in->n);
+  int64_t* bsum = (int64_t*)scratch;  // [nb] block counts -> prefix, [nb] total, [nb + 1] misplaced
+  if ((rc = check_hip(hipMemsetAsync(bsum + nb + 1, 0, sizeof(int64_t), st), "memset"))) return rc;
+  hipLaunchKernelGGL(dribble_count_kernel, dim3((unsigned)nb), dim3(AC_THREADS), 0, st, *in,
+                     DribbleRule{min_len2, max_len2, max_dt}, action_id, bsum,
+                     (unsigned long long*)(bsum + nb + 1), flags);
+  if ((rc = check_launch("dribble_count_kernel"))) return rc;
+  hipLaunchKernelGGL(atomic_scan_kernel, dim3(1), dim3(SC_THREADS), 0, st, bsum, nb);
+  if ((rc = check_launch("atomic_scan_kernel"))) return rc;
+  int64_t res[2] = {0, 0};
+  if ((rc = check_hip(hipMemcpyAsync(res, bsum + nb, sizeof(res), hipMemcpyDeviceToHost, st), "copy n_out")))
+    return rc;
+  if ((rc = check_hip(hipStreamSynchronize(st), "hipStreamSynchronize"))) return rc;
+  *n_out = res[0];
+  if (n_misplaced && action_id) *n_misplaced = res[1];
+  return SA_OK;
+}
+
+extern "C" int sa_dribble_emit(const sa_spadl_frame* in, double min_len2, double max_len2, double max_dt,
+                               const void* scratch, const int64_t* dest, const sa_spadl_out* out,
+                               void* stream) {
+  int rc = check_spadl_frame(in);
+  if (rc || (rc = check_dribble_rule(min_len2, max_len2, max_dt))) return rc;
+  if (in->order) return fail(SA_EINVAL, "_add_dribbles reads rows in input order: order must be NULL");
+  if (in->n == 0) return SA_OK;
+  if (!scratch || !out || !out->time_seconds || !out->start_x || !out->start_y || !out->end_x ||
+      !out->end_y || !out->game || !out->team || !out->player || !out->event || !out->period_id ||
+      !out->type_id || !out->result_id || !out->bodypart_id || !out->src)
+    return fail(SA_EINVAL, "null scratch or output column");
+  const int64_t nb = n_blocks(in->n);
+  hipLaunchKernelGGL(dribble_emit_kernel, dim3((unsigned)nb), dim3(AC_THREADS), 0, (hipStream_t)stream, *in,
+                     DribbleRule{min_len2, max_len2, max_dt}, (const int64_t*)scratch, dest, *out);
+  return check_launch("dribble_emit_kernel");
 }
 
 extern "C" int sa_segment_offsets(const int32_t* key, int64_t n, int64_t n_segments, int64_t* seg_off,

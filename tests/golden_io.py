@@ -104,3 +104,36 @@ def assert_convert_equal(got: dict, ref: dict, name=''):
         else:
             np.testing.assert_array_equal(np.asarray(a).astype(np.int64),
                                           np.asarray(b).astype(np.int64), err_msg=f'{name} {c}')
+
+
+def dribbles_frame(g, prefix='in_'):
+    """A dribbles_* golden's input (``in_``) or the reference's output (``out_``) as a DataFrame
+    with the stored dtypes (tests/golden/make_golden_dribbles.py)."""
+    cols = {}
+    for c in g[prefix + '__columns']:
+        c = str(c)
+        dt = str(g[prefix + c + '__dtype'])
+        v = g[prefix + c]
+        if dt == 'object':
+            v = np.array([np.nan if m else s for s, m in zip(v, g[prefix + c + '__isna'])],
+                         dtype=object)
+        cols[c] = pd.Series(v, dtype=dt)
+    return pd.DataFrame(cols)
+
+
+def assert_frame_same(got: pd.DataFrame, ref: pd.DataFrame, name=''):
+    """Same columns, order and dtypes; values bit-exact (floats too; NaN where the reference
+    has NaN); object columns equal as strings with the same missing pattern."""
+    assert list(got.columns) == list(ref.columns), (name, list(got.columns), list(ref.columns))
+    assert len(got) == len(ref), (name, len(got), len(ref))
+    assert got.index.equals(pd.RangeIndex(len(ref))), name
+    for c in ref.columns:
+        a, b = got[c], ref[c]
+        assert a.dtype == b.dtype, (name, c, a.dtype, b.dtype)
+        if b.dtype == object:
+            ma, mb = a.isna().to_numpy(), b.isna().to_numpy()
+            np.testing.assert_array_equal(ma, mb, err_msg=f'{name} {c} missing pattern')
+            np.testing.assert_array_equal(a[~ma].astype(str).to_numpy(),
+                                          b[~mb].astype(str).to_numpy(), err_msg=f'{name} {c}')
+        else:
+            np.testing.assert_array_equal(a.to_numpy(), b.to_numpy(), err_msg=f'{name} {c}')

@@ -1,5 +1,6 @@
 """The CPU oracle reproduces the reference's goldens (CPU only, no GPU)."""
 import numpy as np
+import pandas as pd
 import pytest
 
 from golden_io import assert_close, cases, inputs, ks, load
@@ -80,6 +81,23 @@ def test_xt_oracle(name):
         assert_close(xo.rate(cols, g[f'{tag}_xT']), g[f'{tag}_rate'], 'rate')
         if f'{tag}_rate_interp' in g:
             assert_close(xo.rate(cols, g[f'{tag}_xT'], True), g[f'{tag}_rate_interp'], 'interp')
+
+
+@pytest.mark.parametrize('name', cases('dribbles'))
+def test_add_dribbles_oracle(name):
+    """oracle add_dribbles == the reference's spadl.base._add_dribbles (goldens)."""
+    from golden_io import dribbles_frame
+    from oracle import atomic_convert_oracle as co
+    g = load('dribbles', name)
+    df = dribbles_frame(g, 'in_')
+    ref = dribbles_frame(g, 'out_')
+    got = co.add_dribbles({c: df[c].to_numpy() for c in co.COLS})
+    assert len(got['type_id']) == len(ref)
+    for c in co.COLS:
+        if c == 'original_event_id':
+            np.testing.assert_array_equal(pd.isna(got[c]), ref[c].isna().to_numpy())
+            continue
+        np.testing.assert_array_equal(np.asarray(got[c]), ref[c].to_numpy(), err_msg=c)
 
 
 @pytest.mark.parametrize('name', cases('convert'))
