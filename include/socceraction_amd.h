@@ -321,6 +321,13 @@ int sa_dribble_emit(const sa_spadl_frame* in, double min_len2, double max_len2, 
 int sa_segment_offsets(const int32_t* key, int64_t n, int64_t n_segments, int64_t* seg_off,
                        void* stream);
 
+/* ---- Arrow / Parquet export --------------------------------------------------------
+ * The per-game feature and label stores of the notebooks (2-compute-features-and-labels.ipynb:
+ * `X.to_hdf(features_h5, f"game_{game_id}")`): bool columns leave the device as Arrow bitmaps
+ * (LSB first, rows >= n zero). bits: [n_cols][col_stride] bytes, col_stride even and
+ * >= 2*ceil(n/16); the block's tile_rows a multiple of 16 and its data 16-byte aligned. */
+int sa_pack_bits(const sa_block* bool_blk, int64_t n, uint8_t* bits, int64_t col_stride, void* stream);
+
 /* ---- gradient-boosted trees on the feature blocks --------------------------------
  * The learner call of VAEP.rate (`_estimate_probabilities`, vaep/base.py:284-294): P(class 1)
  * of a binary gradient-boosted tree ensemble for every row of the feature blocks.

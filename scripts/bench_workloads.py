@@ -8,6 +8,7 @@ profiles/.
     python scripts/bench_workloads.py e2e [--games 500]         # pandas in -> pandas out
     python scripts/bench_workloads.py convert [--games 10000]   # SPADL -> Atomic-SPADL
     python scripts/bench_workloads.py dribbles [--games 10000]  # spadl.base._add_dribbles
+    python scripts/bench_workloads.py store [--games 1000]      # per-game Parquet stores
 
 All device timings are HIP events on torch's current stream (the launch stream); wall
 times bracket torch.cuda.synchronize().
@@ -206,17 +207,78 @@ def dribbles(args) -> dict:
             'dropin_actions_per_s': round(len(small) / ms_df * 1e3, 1)}
 
 
+def store(args) -> dict:
+    """Feature + label stores (the notebooks' per-game to_hdf, as Parquet): device features ->
+    device bitmaps -> Arrow -> part files written in parallel, against the same games written
+    from the DataFrame (pandas -> Arrow conversion packs the bools on the host)."""
+    import shutil
+    import tempfile
+    import socceraction_amd.vaep as vaep
+    from socceraction_amd import store as S
+    d = synthetic.spadl_games(args.games)
+    actions = synthetic.to_frame(d)
+    games = synthetic.games_frame(d)
+    model = vaep.VAEP()
+    root = tempfile.mkdtemp(prefix='sa_store_', dir=os.environ.get('TMPDIR', '/tmp'))
+    out = {'workload': 'feature + label stores (Parquet, lz4), cfg2-shaped games',
+           'actions': len(actions), 'games': len(games)}
+    try:
+        with S.FeatureStore(os.path.join(root, 'warm'), mode='w') as st:
+            S.store_features_batch(model, games.iloc[:2], actions[actions.game_id.isin(
+                games.game_id.iloc[:2])], st)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        with S.FeatureStore(os.path.join(root, 'features'), mode='w') as st:
+            S.store_features_batch(model, games, actions, st, parts=16)
+        with S.FeatureStore(os.path.join(root, 'labels'), mode='w') as st:
+            S.store_labels_batch(model, games, actions, st, parts=16)
+        dt = time.perf_counter() - t
+        size = sum(os.path.getsize(os.path.join(dp, f)) for dp, _, fs in os.walk(root)
+                   for f in fs)
+        out.update(store_s=round(dt, 3), store_actions_per_s=round(len(actions) / dt, 1),
+                   bytes_on_disk=size)
+        # the feature blocks -> Arrow step alone (device bitmaps + pinned D2H)
+        from socceraction_amd import ops
+        ab = B.ActionBatch.from_frame(actions, home_team_id=games.set_index('game_id')[
+            'home_team_id'], segments='game')
+        fb = ops.features(ab, model._split_xfns()[0], 3)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        tab = S.features_to_arrow(fb)
+        out['to_arrow_ms'] = round((time.perf_counter() - t) * 1e3, 2)
+        t = time.perf_counter()
+        X = fb.to_frame()
+        out['to_frame_ms'] = round((time.perf_counter() - t) * 1e3, 2)
+        t = time.perf_counter()
+        tab2 = __import__('pyarrow').Table.from_pandas(X, preserve_index=False)
+        out['frame_to_arrow_host_ms'] = round((time.perf_counter() - t) * 1e3, 2)
+        assert tab2.num_rows == tab.num_rows
+        # per-game DataFrame writes (the notebooks' loop shape) on a 50-game slice
+        sub = games.iloc[:50]
+        t = time.perf_counter()
+        with S.FeatureStore(os.path.join(root, 'loop'), mode='w') as st:
+            for g in sub.itertuples():
+                ga = actions[actions.game_id == g.game_id].reset_index(drop=True)
+                st.put(f'game_{g.game_id}', model.compute_features(g, ga))
+        dt = time.perf_counter() - t
+        n_sub = int(actions.game_id.isin(sub.game_id).sum())
+        out['per_game_loop_actions_per_s'] = round(n_sub / dt, 1)
+    finally:
+        shutil.rmtree(root, ignore_errors=True)
+    return out
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
-    ap.add_argument('workload', choices=('atomic', 'xt105', 'e2e', 'convert', 'dribbles'))
+    ap.add_argument('workload', choices=('atomic', 'xt105', 'e2e', 'convert', 'dribbles', 'store'))
     ap.add_argument('--games', type=int, default=None)
     ap.add_argument('--steps', type=int, default=10)
     args = ap.parse_args()
     if args.games is None:
         args.games = {'atomic': 10000, 'xt105': 7812, 'e2e': 500, 'convert': 10000,
-                      'dribbles': 10000}[args.workload]
+                      'dribbles': 10000, 'store': 1000}[args.workload]
     line = {'atomic': atomic, 'xt105': xt105, 'e2e': e2e, 'convert': convert,
-            'dribbles': dribbles}[args.workload](args)
+            'dribbles': dribbles, 'store': store}[args.workload](args)
     line['device'] = torch.cuda.get_device_name(0)
     print(json.dumps(line), flush=True)
 

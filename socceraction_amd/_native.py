@@ -113,6 +113,8 @@ _SIGNATURES = {
     'sa_dribble_emit': (ctypes.c_int, [ctypes.POINTER(SaSpadlFrame), ctypes.c_double,
                                        ctypes.c_double, ctypes.c_double, _p, _p,
                                        ctypes.POINTER(SaSpadlOut), _p]),
+    'sa_pack_bits': (ctypes.c_int, [ctypes.POINTER(SaBlock), ctypes.c_int64, _p, ctypes.c_int64,
+                                    _p]),
     'sa_segment_offsets': (ctypes.c_int, [_p, ctypes.c_int64, ctypes.c_int64, _p, _p]),
     'sa_tree_predict': (ctypes.c_int, [_p, ctypes.c_int32, _p, ctypes.c_int32, _p, ctypes.c_int32,
                                        ctypes.POINTER(SaBlock), ctypes.POINTER(SaBlock),

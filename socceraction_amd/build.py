@@ -15,7 +15,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, 'csrc')
 OUT = os.path.join(HERE, '_lib', 'libsocceraction_amd.so')
-SOURCES = ['sa_api.hip', 'sa_vaep.hip', 'sa_xt.hip', 'sa_atomic.hip', 'sa_trees.hip']
+SOURCES = ['sa_api.hip', 'sa_vaep.hip', 'sa_xt.hip', 'sa_atomic.hip', 'sa_trees.hip', 'sa_store.hip']
 HEADERS = ['sa_common.h', 'sa_internal.h', os.path.join('..', '..', 'include', 'socceraction_amd.h')]
 FLAGS = ['-O3', '--offload-arch=gfx950', '-ffp-contract=off', '-fPIC', '-shared', '-std=c++17',
          '-Wall']
