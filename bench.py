@@ -39,12 +39,14 @@ SPADL_DEFAULT = ['actiontype_onehot', 'result_onehot', 'actiontype_result_onehot
 # DESIGN.md "Kernels and rooflines")
 BYTES = {'bool_features': 7 + 515,             # type/result/bodypart u8 + team i32 -> 515 bools
          'num_features': 48 + 47 * 8 + 3 * 8,  # 5 f64 + 4 u8 + team -> 47 f64 + 3 i64
-         'goalscore': 6 + 24, 'labels': 6 + 2, 'formula': 30 + 24}
-KERNELS = ('bool_features', 'num_features', 'goalscore', 'labels', 'formula')
+         'goalscore': 6 + 24, 'labels': 6 + 2, 'formula': 30 + 24,
+         'xt_fit_rate': 34 + 42}               # count pass 34 B + rate 42 B (solve: 192 cells)
+KERNELS = ('bool_features', 'num_features', 'goalscore', 'labels', 'formula', 'xt_fit_rate')
 # the HIP kernel each step entry launches (socceraction_amd/csrc/sa_vaep.hip)
 KERNEL_NAMES = {'bool_features': 'bool_colgroup_kernel', 'num_features': 'num_features_kernel',
                 'goalscore': 'goalscore_wave_kernel', 'labels': 'labels_kernel',
-                'formula': 'formula_kernel'}
+                'formula': 'formula_kernel',
+                'xt_fit_rate': 'xt_count_kernel + xt_solve_small_kernel + xt_rate_kernel'}
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 
@@ -73,28 +75,27 @@ def _reduce(dist, value, op, dev):
     return float(t.item())
 
 
-def xt_extra(d, ab, dist, dev, reps: int = 3) -> dict:
-    """BASELINE cfg4 alongside the main line: xT 16x12 fit (count pass + RCCL all-reduce of
-    the counts when several ranks + value iteration to eps=1e-5) and rate over the batch."""
+def xt_step(ab, dist):
+    """BASELINE cfg4 inside the step: xT 16x12 fit on the step's actions (count pass, RCCL
+    all-reduce of the counts across ranks, value iteration to eps=1e-5; the solve synchronises)
+    and ExpectedThreat.rate of every action. Returns the closure and a holder of the last
+    solution (iterations)."""
     from socceraction_amd import shard
+    last = {}
+
     def once():
         acc = ops.xt_count(ab, 16, 12)
-        if dist is not None:
-            if dist.get_backend() == 'nccl':
-                shard.allreduce_xt_counts(acc.shot, acc.goal, acc.move, acc.trans, acc.err)
+        if dist is not None and dist.get_backend() == 'nccl':
+            shard.allreduce_xt_counts(acc.shot, acc.goal, acc.move, acc.trans, acc.err)
+        elif dist is not None:  # gloo rehearsal: the same sum through host memory
+            for t in (acc.shot, acc.goal, acc.move, acc.trans):
+                h = t.cpu()
+                dist.all_reduce(h)
+                t.copy_(h)
         sol = ops.xt_solve(acc)  # synchronises
-        out, _ = ops.xt_rate(ab, sol.mats[3].reshape(12, 16), 16, 12)
-        return sol, out
-    once()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(reps):
-        sol, _ = once()
-    torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / reps
-    return {'workload': 'cfg4: xT 16x12 fit (count + all-reduce + value iteration) + rate',
-            'ms_per_fit_and_rate': round(dt * 1e3, 3), 'iterations': sol.n_iter,
-            'actions_per_s_per_gpu': round(ab.n / dt, 1)}
+        ops.xt_rate(ab, sol.mats[3].reshape(12, 16), 16, 12)
+        last['sol'] = sol
+    return once, last
 
 
 ATOMIC_DEFAULT = ['actiontype', 'actiontype_onehot', 'bodypart', 'bodypart_onehot', 'time',
@@ -236,8 +237,10 @@ def rate_extra(ab, out, n, dev, reps: int = 5) -> dict:
 
 
 def cpu_baseline(d, seconds: float) -> dict:
-    """The oracle port (numpy, 1 thread) on the GPU box's host, over whole games."""
+    """The oracle port (numpy, 1 thread) on the GPU box's host, over whole games: VAEP features
+    + labels + formula per game, then the xT 16x12 fit + rate over the games done."""
     from oracle import vaep_oracle as vo
+    from oracle import xt_oracle as xo
     p = synthetic.probabilities(int(d['game_off'][-1]))
     off = d['game_off']
     names = ('period_id', 'time_seconds', 'team_id', 'start_x', 'start_y', 'end_x', 'end_y',
@@ -251,10 +254,15 @@ def cpu_baseline(d, seconds: float) -> dict:
         vo.formula(cols, p['scores'][s:e], p['concedes'][s:e])
         done += e - s
         games += 1
+    # xT 16x12 fit + rate over the same sample (the step's second half)
+    e = int(off[games])
+    cols = {c: d[c][:e] for c in names}
+    fit = xo.fit(cols, 16, 12)
+    xo.rate(cols, fit['xT'])
     dt = time.perf_counter() - t0
     return {'value': round(done / dt, 1), 'unit': 'actions/s', 'cores': 1, 'kind': 'port',
-            'sample': f'{games} synthetic games ({done} actions) of the same workload, '
-                      f'numpy oracle, 1 thread, {dt:.1f} s'}
+            'sample': f'{games} synthetic games ({done} actions) of the same workload (VAEP per '
+                      f'game + xT 16x12 fit + rate), numpy oracle, 1 thread, {dt:.1f} s'}
 
 
 def main() -> None:
@@ -265,7 +273,6 @@ def main() -> None:
     ap.add_argument('--games', type=int, default=10000, help='games per GPU (cfg2: 10k)')
     ap.add_argument('--cpu-seconds', type=float, default=15.0)
     ap.add_argument('--no-cpu', action='store_true')
-    ap.add_argument('--no-xt', action='store_true', help='skip the cfg4 xT side measurement')
     ap.add_argument('--no-side', action='store_true',
                     help='skip the cfg3 (atomic) and cfg5 (xT 105x68) side measurements')
     ap.add_argument('--xt-sharded', action='store_true',
@@ -310,11 +317,13 @@ def main() -> None:
     lab = ops.LabelBlocks(n, lab_buf[0], lab_buf[1], None)
     val = torch.empty((3, ld), dtype=torch.float64, device=dev)
     s_act = ab.struct()
+    xt_once, xt_last = xt_step(ab, dist)
     calls = (lambda: ops.features_into(s_act, bool_out),
              lambda: ops.features_into(s_act, num_out),
              lambda: ops.goalscore_into(ab, out),
              lambda: ops.labels(ab, 10, lab),
-             lambda: ops.formula(ab, ps, pc, val))
+             lambda: ops.formula(ab, ps, pc, val),
+             xt_once)
 
     def step(ev=None):
         for i, call in enumerate(calls):
@@ -345,7 +354,6 @@ def main() -> None:
     if dist:
         wall = _reduce(dist, wall, dist.ReduceOp.MAX, dev)
         total_actions = int(_reduce(dist, n, dist.ReduceOp.SUM, dev))
-    extra_xt = xt_extra(d, ab, dist, dev) if not args.no_xt else None
     extra_side = {}
     if not args.no_side:
         extra_side['xt105_cfg5'] = xt105_extra(ab, dist, dev, args.xt_sharded)
@@ -376,8 +384,10 @@ def main() -> None:
         'warmup': args.warmup, 'ms_per_step': round(ms_per_step, 4), 'higher_is_better': True,
         'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f64',
         'data': 'synthetic (seeded SPADL games, BASELINE cfg2 shape; inputs resident in HBM)',
-        'config': {'workload': 'cfg2: 10k-game synthetic SPADL per GPU, VAEP compute_features '
-                               '(k=3, default xfns, 568 cols) + compute_labels + formula.value (f64)',
+        'config': {'workload': 'cfg2 + cfg4: 10k-game synthetic SPADL per GPU, VAEP '
+                               'compute_features (k=3, default xfns, 568 cols) + compute_labels + '
+                               'formula.value (f64), and xT 16x12 fit (counts all-reduced over '
+                               'the ranks) + rate of the same actions',
                    'games_per_gpu': args.games, 'actions_per_gpu': n,
                    'feature_layout': f'tiled column-major: bool {out.Rb}, f64/i64 {out.Rn} rows '
                                      'per tile',
@@ -389,8 +399,10 @@ def main() -> None:
                      'algorithmic_bytes': BYTES[dom] * n, 'kernel': KERNEL_NAMES[dom],
                      'bytes_per_action': BYTES[dom]},
     }
-    if extra_xt is not None:
-        line['xt_cfg4'] = extra_xt
+    line['xt_cfg4'] = {'workload': 'cfg4 inside the step: xT 16x12 fit (count + all-reduce + '
+                                   'value iteration to eps=1e-5) + rate of the step\'s actions',
+                       'ms': round(kern['xt_fit_rate'], 4),
+                       'iterations': xt_last['sol'].n_iter}
     line.update(extra_side)
     if not args.no_cpu:
         line['cpu_baseline'] = cpu_baseline(d, args.cpu_seconds)

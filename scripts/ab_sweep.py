@@ -26,7 +26,7 @@ def main():
             if v != 'default':
                 env['SOCCERACTION_AMD_LIB'] = os.path.join(
                     ROOT, 'socceraction_amd', '_lib', f'libsocceraction_amd_{v}.so')
-            args = [sys.executable, 'bench.py', '--steps', '20', '--warmup', '3', '--no-cpu', '--no-xt']
+            args = [sys.executable, 'bench.py', '--steps', '20', '--warmup', '3', '--no-cpu']
             args += [a for a in extra.split(',') if a]
             out = subprocess.run(args, cwd=ROOT, env=env, capture_output=True, text=True,
                                  timeout=300)

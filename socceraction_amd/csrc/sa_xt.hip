@@ -16,6 +16,10 @@
 #include "sa_common.h"
 #include "sa_internal.h"
 
+#ifndef SA_XT_WIDE
+#define SA_XT_WIDE 1  // C <= 197: XC_WIDE count pass (0: the 32k-action XC_SMALL workgroups)
+#endif
+
 namespace sa {
 
 // numpy float64 -> int64 cast (x86 cvttsd2si: NaN / out of range -> INT64_MIN), then clip.
@@ -40,17 +44,22 @@ __device__ __forceinline__ bool is_move(int t) { return t == T_PASS || t == T_DR
 // ~10k, e.g. 105 x 68): only the three C-vectors in LDS -- every move hits move[start], so
 // global atomics there serialise on a few thousand hot addresses -- and the sparse C x C
 // transition counts as global atomics.  XC_GLOBAL: global atomics for everything.
+// XC_WIDE (C <= 197, e.g. 16 x 12): all 3C + C*C bins as u32 in one 1024-thread workgroup's LDS
+// (150 KB at C = 192, one workgroup per CU), each workgroup counting one contiguous chunk of
+// the actions -- 16 waves per CU keep the loads in flight, and the C*C flush happens once per
+// CU instead of once per 32k actions (16M actions: 472 -> see DESIGN.md).
 constexpr int XT_THREADS = 256;
-constexpr int XT_SMALL_ACTS = 32768;  // actions per workgroup in the LDS-privatised forms
-enum { XC_GLOBAL = 0, XC_VEC = 1, XC_SMALL = 2 };
+constexpr int XT_WIDE_THREADS = 1024;
+constexpr int XT_SMALL_ACTS = 32768;  // actions per workgroup in XC_SMALL / XC_VEC
+enum { XC_GLOBAL = 0, XC_VEC = 1, XC_SMALL = 2, XC_WIDE = 3 };
 
 template <int MODE>
-__global__ __launch_bounds__(XT_THREADS) void xt_count_kernel(sa_actions A, int l, int w,
-                                                             unsigned long long* __restrict__ shot,
-                                                             unsigned long long* __restrict__ goal,
-                                                             unsigned long long* __restrict__ move,
-                                                             int32_t* __restrict__ trans,
-                                                             int32_t* __restrict__ err) {
+__global__ __launch_bounds__(XT_WIDE_THREADS) void xt_count_kernel(sa_actions A, int l, int w,
+                                                                  unsigned long long* __restrict__ shot,
+                                                                  unsigned long long* __restrict__ goal,
+                                                                  unsigned long long* __restrict__ move,
+                                                                  int32_t* __restrict__ trans,
+                                                                  int32_t* __restrict__ err, int64_t chunk) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   const int C = l * w;
   const int64_t n = A.n;
@@ -58,15 +67,15 @@ __global__ __launch_bounds__(XT_THREADS) void xt_count_kernel(sa_actions A, int 
   uint32_t* hs = lds;          // [C]
   uint32_t* hg = lds + C;      // [C]
   uint32_t* hm = lds + 2 * C;  // [C]
-  uint32_t* ht = lds + 3 * C;  // [(C*C+1)/2] packed u16 pairs
-  constexpr bool SMALL = MODE == XC_SMALL, VEC = MODE != XC_GLOBAL;
+  uint32_t* ht = lds + 3 * C;  // SMALL: [(C*C+1)/2] packed u16 pairs; WIDE: [C*C] u32
+  constexpr bool SMALL = MODE == XC_SMALL, WIDE = MODE == XC_WIDE, VEC = MODE != XC_GLOBAL;
   int64_t begin, end, stride;
   if (VEC) {
-    const int tw = SMALL ? (C * C + 1) / 2 : 0;
+    const int tw = SMALL ? (C * C + 1) / 2 : (WIDE ? C * C : 0);
     for (int k = threadIdx.x; k < 3 * C + tw; k += blockDim.x) lds[k] = 0;
     __syncthreads();
-    begin = (int64_t)blockIdx.x * XT_SMALL_ACTS + threadIdx.x;
-    end = min(n, (int64_t)(blockIdx.x + 1) * XT_SMALL_ACTS);
+    begin = (int64_t)blockIdx.x * chunk + threadIdx.x;
+    end = min(n, (int64_t)(blockIdx.x + 1) * chunk);
     stride = blockDim.x;
   } else {
     begin = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -122,6 +131,8 @@ __global__ __launch_bounds__(XT_THREADS) void xt_count_kernel(sa_actions A, int 
           const int64_t k = (int64_t)cs * C + ce;
           if (SMALL)
             atomicAdd(&ht[k >> 1], (k & 1) ? 0x10000u : 1u);
+          else if (WIDE)
+            atomicAdd(&ht[k], 1u);
           else
             atomicAdd(&trans[k], 1);
         }
@@ -135,6 +146,12 @@ __global__ __launch_bounds__(XT_THREADS) void xt_count_kernel(sa_actions A, int 
       if (hs[c]) atomicAdd(&shot[c], (unsigned long long)hs[c]);
       if (hg[c]) atomicAdd(&goal[c], (unsigned long long)hg[c]);
       if (hm[c]) atomicAdd(&move[c], (unsigned long long)hm[c]);
+    }
+  }
+  if (WIDE) {
+    for (int k = threadIdx.x; k < C * C; k += blockDim.x) {
+      const uint32_t v = ht[k];
+      if (v) atomicAdd(&trans[k], (int32_t)v);
     }
   }
   if (SMALL) {
@@ -191,7 +208,9 @@ __global__ __launch_bounds__(256) void xt_transpose_kernel(const int32_t* __rest
   }
 }
 
-// One value-iteration step for C rows; row r = one lane, sequential sum over c.
+// One value-iteration step for C rows; row r = one lane, sequential sum over c.  (Issuing the
+// T loads 16 columns ahead of the adds measured no faster at C = 192: ~5.6 us per iteration
+// either way, the strictly ordered f64 add chain of 3 waves is the limiter.)
 __device__ __forceinline__ double row_payoff(const double* __restrict__ Tt, const double* __restrict__ x,
                                              int C, int r) {
   double acc = 0.0;
@@ -443,24 +462,46 @@ __global__ void xt_interp_kernel(const double* __restrict__ xT, const double* __
 }
 
 // rate (xthreat.py:408-465): successful moves get grid[end] - grid[start], others NaN.
-__global__ __launch_bounds__(256) void xt_rate_kernel(sa_actions A, const double* __restrict__ grid,
-                                                      int L, int W, double* __restrict__ out,
-                                                      int32_t* __restrict__ err) {
-  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= A.n) return;
-  const sa_frame& F = A.frames[0];
-  const int t = F.type_id[j];
+__device__ __forceinline__ double rate_one(int t, int r, double sx, double sy, double ex, double ey,
+                                           const double* __restrict__ grid, int L, int W, int32_t& bad) {
   double v = __builtin_nan("");
-  if (is_move(t) && F.result_id[j] == R_SUCCESS) {
-    const double sx = F.c0[j], sy = F.c1[j], ex = F.c2[j], ey = F.c3[j];
+  if (is_move(t) && r == R_SUCCESS) {
     if (!isfinite(sx) || !isfinite(sy) || !isfinite(ex) || !isfinite(ey)) {
-      if (err) atomicOr(err, 4);
+      bad = 4;
     } else {
       const int s = flat_index(sx, sy, L, W), e = flat_index(ex, ey, L, W);
       v = grid[e] - grid[s];
     }
   }
-  out[j] = v;
+  return v;
+}
+
+// A thread rates 2 consecutive actions: 16-B loads of each coordinate column, 2-B loads of the
+// ids and one 16-B store (vec: host-checked alignment), so a wave moves 1 KiB per instruction
+// instead of 512 B (f64) or 64 B (ids).
+__global__ __launch_bounds__(256) void xt_rate_kernel(sa_actions A, const double* __restrict__ grid,
+                                                      int L, int W, double* __restrict__ out,
+                                                      int32_t* __restrict__ err, int vec) {
+  const int64_t j0 = 2 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x);
+  if (j0 >= A.n) return;
+  const sa_frame& F = A.frames[0];
+  int32_t bad = 0;
+  if (vec && j0 + 1 < A.n) {
+    const f64x2 sx = *reinterpret_cast<const f64x2*>(F.c0 + j0);
+    const f64x2 sy = *reinterpret_cast<const f64x2*>(F.c1 + j0);
+    const f64x2 ex = *reinterpret_cast<const f64x2*>(F.c2 + j0);
+    const f64x2 ey = *reinterpret_cast<const f64x2*>(F.c3 + j0);
+    const uint32_t ty = *reinterpret_cast<const uint16_t*>(F.type_id + j0);
+    const uint32_t rs = *reinterpret_cast<const uint16_t*>(F.result_id + j0);
+    f64x2 v;
+    v[0] = rate_one(ty & 0xFF, rs & 0xFF, sx[0], sy[0], ex[0], ey[0], grid, L, W, bad);
+    v[1] = rate_one(ty >> 8, rs >> 8, sx[1], sy[1], ex[1], ey[1], grid, L, W, bad);
+    __builtin_nontemporal_store(v, reinterpret_cast<f64x2*>(out + j0));
+  } else {
+    for (int64_t j = j0; j < j0 + 2 && j < A.n; ++j)
+      out[j] = rate_one(F.type_id[j], F.result_id[j], F.c0[j], F.c1[j], F.c2[j], F.c3[j], grid, L, W, bad);
+  }
+  if (bad && err) atomicOr(err, bad);
 }
 
 }  // namespace sa
@@ -486,17 +527,32 @@ extern "C" int sa_xt_count(const sa_actions* a, int32_t l, int32_t w, int64_t* s
   auto* um = reinterpret_cast<unsigned long long*>(move);
   const size_t vec_lds = (size_t)3 * C * 4;
   const unsigned wg_blocks = (unsigned)((a->n + XT_SMALL_ACTS - 1) / XT_SMALL_ACTS);
-  if (small_lds <= 80 * 1024) {
+  const size_t wide_lds = (size_t)(3 * C + C * C) * 4;
+  if (SA_XT_WIDE && wide_lds <= 150 * 1024) {
+    // one workgroup per CU (or fewer when there are few actions: >= 4096 actions each)
+    static int cus = 0;
+    if (!cus) {
+      int dev = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+        cus = 256;
+    }
+    int64_t blocks = (a->n + 4095) / 4096;
+    if (blocks > cus) blocks = cus;
+    const int64_t chunk = (a->n + blocks - 1) / blocks;
+    hipLaunchKernelGGL((xt_count_kernel<XC_WIDE>), dim3((unsigned)blocks), dim3(XT_WIDE_THREADS), wide_lds, st,
+                       *a, l, w, us, ug, um, trans, err_flags, chunk);
+  } else if (small_lds <= 80 * 1024) {
     hipLaunchKernelGGL((xt_count_kernel<XC_SMALL>), dim3(wg_blocks), dim3(XT_THREADS), small_lds, st, *a,
-                       l, w, us, ug, um, trans, err_flags);
+                       l, w, us, ug, um, trans, err_flags, (int64_t)XT_SMALL_ACTS);
   } else if (vec_lds <= 120 * 1024) {
     hipLaunchKernelGGL((xt_count_kernel<XC_VEC>), dim3(wg_blocks), dim3(XT_THREADS), vec_lds, st, *a, l,
-                       w, us, ug, um, trans, err_flags);
+                       w, us, ug, um, trans, err_flags, (int64_t)XT_SMALL_ACTS);
   } else {
     int64_t blocks = (a->n + XT_THREADS - 1) / XT_THREADS;
     if (blocks > 4096) blocks = 4096;
     hipLaunchKernelGGL((xt_count_kernel<XC_GLOBAL>), dim3((unsigned)blocks), dim3(XT_THREADS), 0, st, *a,
-                       l, w, us, ug, um, trans, err_flags);
+                       l, w, us, ug, um, trans, err_flags, (int64_t)0);
   }
   return check_launch("xt_count_kernel");
 }
@@ -613,8 +669,12 @@ extern "C" int sa_xt_rate(const sa_actions* a, const double* grid, int32_t L, in
                           int32_t* err_flags, void* stream) {
   if (!a || a->n < 0 || !grid || !out || L < 1 || W < 1) return fail(SA_EINVAL, "bad xt_rate args");
   if (a->n == 0) return SA_OK;
-  hipLaunchKernelGGL(xt_rate_kernel, dim3((unsigned)((a->n + 255) / 256)), dim3(256), 0,
-                     (hipStream_t)stream, *a, grid, L, W, out, err_flags);
+  const sa_frame& F = a->frames[0];
+  const int vec = aligned16(F.c0) && aligned16(F.c1) && aligned16(F.c2) && aligned16(F.c3) && aligned16(out) &&
+                  ((uintptr_t)F.type_id & 1u) == 0 && ((uintptr_t)F.result_id & 1u) == 0;
+  const int64_t threads = (a->n + 1) / 2;
+  hipLaunchKernelGGL(xt_rate_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, *a, grid, L, W, out, err_flags, vec);
   return check_launch("xt_rate_kernel");
 }
 

@@ -192,10 +192,12 @@ def test_xt_goldens(sa):
                 assert_close(r.cpu().numpy(), g[f'{tag}_rate_interp'], f'{name} {tag} interp rate')
 
 
-@pytest.mark.parametrize('l,w,games', [(40, 30, 300), (105, 68, 300)])
+@pytest.mark.parametrize('l,w,games', [(16, 12, 2000), (40, 30, 300), (105, 68, 300)])
 def test_xt_large_grid_vs_oracle(sa, l, w, games):
-    """Grids above the single-workgroup solver (C > 1024) take the streaming count-row
-    iteration; iterates, iteration count and matrices must be bit-identical to the oracle."""
+    """16 x 12 over ~3.2M actions: the one-workgroup-per-CU count pass (XC_WIDE, every CU's
+    chunk flushed into the same bins). Grids above the single-workgroup solver (C > 1024) take
+    the streaming count-row iteration. Iterates, iteration count and matrices must be
+    bit-identical to the oracle."""
     B, ops, syn = sa['batch'], sa['ops'], sa['synthetic']
     d = syn.spadl_games(games, game_id0=77)
     ab = B.ActionBatch.from_columns(d)
