@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define SA_ABI_VERSION 1
+#define SA_ABI_VERSION 2
 #define SA_MAX_FRAMES 8 /* max nb_prev_actions (window frames) */
 #define SA_BOOL_TILE_QUANTUM 1024 /* bool block: rows per tile must be a multiple of this */
 #define SA_NUM_TILE_QUANTUM 128   /* f64 / i64 blocks: rows per tile must be a multiple of this */
@@ -337,11 +337,13 @@ int sa_pack_bits(const sa_block* bool_blk, int64_t n, uint8_t* bits, int64_t col
  * feature_slots[f] = (kind << 24) | column locates model feature f in the blocks (kind 0 =
  * bool block, 1 = f64, 2 = i64).  le = 1: `x <= threshold` goes left (scikit-learn), 0:
  * `x < threshold` (xgboost); NaN follows default_left.  f32 = 1: xgboost float32 arithmetic
- * and float output p_out[n], else float64 (scikit-learn).  p = 1 / (1 + exp(-margin)). */
-int sa_tree_predict(const void* nodes, int32_t n_nodes, const int32_t* roots, int32_t n_trees,
-                    const int32_t* feature_slots, int32_t n_features, const sa_block* bool_blk,
-                    const sa_block* f64_blk, const sa_block* i64_blk, int64_t n, double base_margin,
-                    int32_t le, int32_t f32, void* p_out, void* stream);
+ * and float output p_out[n], else float64 (scikit-learn).  p = 1 / (1 + exp(-margin)).
+ * tree_depth (optional, device, [n_trees]): split levels on each tree's longest root-to-leaf
+ * path; with it (and a model that fits LDS) trees are walked a fixed number of levels. */
+int sa_tree_predict(const void* nodes, int32_t n_nodes, const int32_t* roots, const int32_t* tree_depth,
+                    int32_t n_trees, const int32_t* feature_slots, int32_t n_features,
+                    const sa_block* bool_blk, const sa_block* f64_blk, const sa_block* i64_blk, int64_t n,
+                    double base_margin, int32_t le, int32_t f32, void* p_out, void* stream);
 
 /* ---- misc -------------------------------------------------------------------- */
 int sa_abi_version(void);

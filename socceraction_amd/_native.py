@@ -116,7 +116,7 @@ _SIGNATURES = {
     'sa_pack_bits': (ctypes.c_int, [ctypes.POINTER(SaBlock), ctypes.c_int64, _p, ctypes.c_int64,
                                     _p]),
     'sa_segment_offsets': (ctypes.c_int, [_p, ctypes.c_int64, ctypes.c_int64, _p, _p]),
-    'sa_tree_predict': (ctypes.c_int, [_p, ctypes.c_int32, _p, ctypes.c_int32, _p, ctypes.c_int32,
+    'sa_tree_predict': (ctypes.c_int, [_p, ctypes.c_int32, _p, _p, ctypes.c_int32, _p, ctypes.c_int32,
                                        ctypes.POINTER(SaBlock), ctypes.POINTER(SaBlock),
                                        ctypes.POINTER(SaBlock), ctypes.c_int64, ctypes.c_double,
                                        ctypes.c_int32, ctypes.c_int32, _p, _p]),
@@ -152,7 +152,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.sa_abi_version() != 1:
+    if lib.sa_abi_version() != 2:
         raise ImportError('libsocceraction_amd ABI version mismatch')
     if path == LIB_PATH:
         _lib = lib

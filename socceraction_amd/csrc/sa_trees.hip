@@ -40,6 +40,9 @@ constexpr int TR_LDS_SLOTS = 2048;  // 8 KB
 #ifndef SA_TREE_TG
 #define SA_TREE_TG 8
 #endif
+#ifndef SA_TREE_FIXED
+#define SA_TREE_FIXED 1  // tree_depth given: fixed-depth walk over self-looping leaves
+#endif
 constexpr int TG = SA_TREE_TG;      // trees walked together per thread
 
 // Row j's element of column `col` in each tiled block is base[kind] + col * R[kind]; the
@@ -138,14 +141,96 @@ __global__ __launch_bounds__(TR_THREADS) void tree_predict_kernel(const TNode* _
     ((double*)out)[j] = 1.0 / (1.0 + exp(-(double)m));
 }
 
+// Fixed-depth walk (tree_depth given, the model staged in LDS): leaves become self-loops (left =
+// right = the leaf, a valid feature slot), so every tree of a TG-group is walked exactly the
+// group's depth levels with no per-lane "still walking" state -- straight-line code instead of
+// the divergent while-loop above, whose exec-mask juggling cost as many scalar as vector
+// instructions.  Nodes are restaged with the feature slot in the node (one LDS read per level
+// instead of two dependent ones) and the threshold in the model's arithmetic type.
+template <typename A>
+struct LNode {
+  A thr;  // threshold (or the leaf value)
+  int32_t slot, left, right;  // right: bit 31 = default_left
+};
+
+template <bool F32, bool LE>
+__global__ __launch_bounds__(TR_THREADS) void tree_fixed_kernel(const TNode* __restrict__ nodes, int n_nodes,
+                                                                 const int32_t* __restrict__ roots,
+                                                                 const int32_t* __restrict__ depth, int n_trees,
+                                                                 const int32_t* __restrict__ slots, sa_block Bb,
+                                                                 sa_block Bf, sa_block Bi, int64_t n, double base,
+                                                                 void* __restrict__ out) {
+  using A = typename std::conditional<F32, float, double>::type;
+  extern __shared__ __attribute__((aligned(16))) unsigned char tr_lds[];
+  LNode<A>* L = reinterpret_cast<LNode<A>*>(tr_lds);
+  __shared__ int32_t dummy_slot;
+  if (threadIdx.x == 0) {  // the slot of the first split node: leaves read a feature that exists
+    int32_t ds = 0;
+    for (int k = 0; k < n_nodes; ++k)
+      if (nodes[k].feature >= 0) {
+        ds = slots[nodes[k].feature];
+        break;
+      }
+    dummy_slot = ds;
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < n_nodes; k += blockDim.x) {
+    const TNode nd = nodes[k];
+    LNode<A> o;
+    o.thr = (A)nd.thr_or_value;
+    if (nd.feature < 0) {
+      o.slot = dummy_slot;
+      o.left = k;
+      o.right = k;
+    } else {
+      o.slot = slots[nd.feature];
+      o.left = nd.left;
+      o.right = nd.right;
+    }
+    L[k] = o;
+  }
+  __syncthreads();
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const RowBases rb = row_bases(Bb, Bf, Bi, j);
+  A m = (A)base;
+  for (int t0 = 0; t0 < n_trees; t0 += TG) {
+    int k[TG];
+    int D = 0;
+#pragma unroll
+    for (int u = 0; u < TG; ++u) {
+      const int t = t0 + u < n_trees ? t0 + u : n_trees - 1;
+      k[u] = roots[t];
+      D = max(D, depth[t]);
+    }
+    for (int d = 0; d < D; ++d) {
+#pragma unroll
+      for (int u = 0; u < TG; ++u) {
+        const LNode<A> nd = L[k[u]];
+        const A v = (A)feature_value(rb, nd.slot);
+        const bool left = isnan(v) ? nd.right < 0 : (LE ? v <= nd.thr : v < nd.thr);
+        k[u] = left ? nd.left : (nd.right & 0x7FFFFFFF);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < TG; ++u)
+      if (t0 + u < n_trees) m = m + L[k[u]].thr;
+  }
+  if (F32)
+    ((float*)out)[j] = 1.0f / (1.0f + expf(-(float)m));
+  else
+    ((double*)out)[j] = 1.0 / (1.0 + exp(-(double)m));
+}
+
 }  // namespace sa
 
 using namespace sa;
 
-extern "C" int sa_tree_predict(const void* nodes, int32_t n_nodes, const int32_t* roots, int32_t n_trees,
-                               const int32_t* feature_slots, int32_t n_features, const sa_block* bool_blk,
-                               const sa_block* f64_blk, const sa_block* i64_blk, int64_t n, double base_margin,
-                               int32_t le, int32_t f32, void* p_out, void* stream) {
+extern "C" int sa_tree_predict(const void* nodes, int32_t n_nodes, const int32_t* roots, const int32_t* tree_depth,
+                               int32_t n_trees, const int32_t* feature_slots, int32_t n_features,
+                               const sa_block* bool_blk, const sa_block* f64_blk, const sa_block* i64_blk,
+                               int64_t n, double base_margin, int32_t le, int32_t f32, void* p_out,
+                               void* stream) {
   if (n < 0 || n_nodes < 1 || n_trees < 0 || n_features < 0 || !nodes || !roots || !p_out ||
       (n_features > 0 && !feature_slots))
     return fail(SA_EINVAL, "bad tree model arguments");
@@ -157,6 +242,22 @@ extern "C" int sa_tree_predict(const void* nodes, int32_t n_nodes, const int32_t
   const TNode* nd = (const TNode*)nodes;
   const bool staged = n_nodes <= TR_LDS_NODES && n_features <= TR_LDS_SLOTS;
   const size_t lds_bytes = (size_t)n_nodes * sizeof(TNode) + (size_t)n_features * sizeof(int32_t);
+  if (SA_TREE_FIXED && tree_depth && n_nodes <= TR_LDS_NODES && n_trees > 0) {
+    const size_t fb = (size_t)n_nodes * (f32 ? sizeof(LNode<float>) : sizeof(LNode<double>));
+#define SA_TREE_FIXED_LAUNCH(F, LEQ)                                                                    \
+  hipLaunchKernelGGL((tree_fixed_kernel<F, LEQ>), grid, block, fb, st, nd, n_nodes, roots, tree_depth, n_trees, \
+                     feature_slots, Bb, Bf, Bi, n, base_margin, p_out)
+    if (f32 && le)
+      SA_TREE_FIXED_LAUNCH(true, true);
+    else if (f32)
+      SA_TREE_FIXED_LAUNCH(true, false);
+    else if (le)
+      SA_TREE_FIXED_LAUNCH(false, true);
+    else
+      SA_TREE_FIXED_LAUNCH(false, false);
+#undef SA_TREE_FIXED_LAUNCH
+    return check_launch("tree_fixed_kernel");
+  }
 #define SA_TREE_LAUNCH(F, S)                                                                       \
   hipLaunchKernelGGL((tree_predict_kernel<F, S>), grid, block, S ? lds_bytes : 0, st, nd, n_nodes, roots, n_trees, \
                      feature_slots, n_features, Bb, Bf, Bi, n, base_margin, le, p_out)

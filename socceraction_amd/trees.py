@@ -143,11 +143,28 @@ class TreeEnsemble:
     def n_trees(self) -> int:
         return len(self.roots)
 
+    def depths(self) -> np.ndarray:
+        """Split levels on each tree's longest root-to-leaf path (int32 [n_trees])."""
+        nd = self.nodes
+        out = np.zeros(len(self.roots), np.int32)
+        for t, r in enumerate(self.roots):
+            stack, best = [(int(r), 0)], 0
+            while stack:
+                k, d = stack.pop()
+                if nd['feature'][k] < 0:
+                    best = max(best, d)
+                else:
+                    stack.append((int(nd['left'][k]), d + 1))
+                    stack.append((int(nd['right'][k]) & 0x7FFFFFFF, d + 1))
+            out[t] = best
+        return out
+
     def _device(self, dev) -> dict:
         if self._dev is None or self._dev['dev'] != dev:
             self._dev = {'dev': dev,
                          'nodes': torch.from_numpy(self.nodes.view(np.uint8).copy()).to(dev),
-                         'roots': torch.from_numpy(self.roots).to(dev)}
+                         'roots': torch.from_numpy(self.roots).to(dev),
+                         'depth': torch.from_numpy(self.depths()).to(dev)}
         return self._dev
 
     def feature_slots(self, plan, feature_names: Optional[Sequence[str]] = None) -> np.ndarray:
@@ -183,7 +200,8 @@ class TreeEnsemble:
             out = torch.empty(max(n, 1), dtype=dt, device=dev)
         bb, fb, ib = blocks.sa_blocks()
         _native.check(_native.lib().sa_tree_predict(
-            d['nodes'].data_ptr(), len(self.nodes), d['roots'].data_ptr(), self.n_trees,
+            d['nodes'].data_ptr(), len(self.nodes), d['roots'].data_ptr(),
+            d['depth'].data_ptr() if self.n_trees else None, self.n_trees,
             slots.data_ptr(), len(slots), ctypes.byref(bb), ctypes.byref(fb), ctypes.byref(ib),
             n, float(self.base_margin), int(self.le), int(self.f32), out.data_ptr(),
             stream_handle()))

@@ -30,7 +30,7 @@ def test_library_builds_and_exports_every_declared_symbol():
     for sym in declared:
         assert hasattr(lib, sym), sym
     assert set(declared) == set(_native.EXPORTED_SYMBOLS)
-    assert lib.sa_abi_version() == 1
+    assert lib.sa_abi_version() == 2
 
 
 def test_ctypes_struct_layout_matches_header():
