@@ -436,10 +436,16 @@ __device__ __forceinline__ void put_spadl_row(const sa_spadl_out& O, int64_t o, 
   O.src[o] = src;
 }
 
+// Fast layout (dest == NULL): a block's rows form one contiguous output range; they are built
+// in LDS (the 5 f64 + src columns, then the 4 int32 + 4 u8 columns in the same bytes) and
+// copied out by consecutive threads, like atomic_emit_kernel.  With dest the rows scatter.
+constexpr int DE_MAX_OUT = 2 * AC_BLOCK_ROWS;
+
 __global__ __launch_bounds__(AC_THREADS) void dribble_emit_kernel(sa_spadl_frame F, DribbleRule D,
                                                                  const int64_t* __restrict__ bpre,
                                                                  const int64_t* __restrict__ dest,
                                                                  sa_spadl_out O) {
+  __shared__ double lds[6 * DE_MAX_OUT];  // 24 KiB
   __shared__ int64_t wsum[AC_THREADS / 64];
   const int64_t p = (int64_t)blockIdx.x * AC_BLOCK_ROWS + threadIdx.x;
   const bool live = p < F.n;
@@ -448,16 +454,74 @@ __global__ __launch_bounds__(AC_THREADS) void dribble_emit_kernel(sa_spadl_frame
   if (live) d = dribble_after(F, p, D, R, Q);
   int64_t total;
   const int64_t lo = block_excl_scan(live ? 1 + d : 0, wsum, total);
-  if (!live) return;
   const int64_t g = bpre[blockIdx.x] + lo;  // row p's position in the fast layout
-  const int64_t o = dest ? dest[p] : g;
-  put_spadl_row(O, o, R.t, R.sx, R.sy, R.ex, R.ey, R.game, R.team, R.player, R.event, R.per, R.type, R.res,
-                R.bp, p);
-  if (d) {
-    const int64_t od = dest ? dest[F.n + (g - p)] : g + 1;  // g - p = dribbles before row p
-    put_spadl_row(O, od, (R.t + Q.t) / 2, R.ex, R.ey, Q.sx, Q.sy, Q.game, Q.team, Q.player, -1, Q.per,
-                  A_DRIBBLE, 1, 0, ~(p + 1));
+  if (dest) {
+    if (!live) return;
+    put_spadl_row(O, dest[p], R.t, R.sx, R.sy, R.ex, R.ey, R.game, R.team, R.player, R.event, R.per, R.type,
+                  R.res, R.bp, p);
+    if (d)  // g - p = dribbles before row p
+      put_spadl_row(O, dest[F.n + (g - p)], (R.t + Q.t) / 2, R.ex, R.ey, Q.sx, Q.sy, Q.game, Q.team, Q.player,
+                    -1, Q.per, A_DRIBBLE, 1, 0, ~(p + 1));
+    return;
   }
+  const int tot = (int)total;
+  const int o = (int)lo;
+  const int64_t base = bpre[blockIdx.x];
+  int64_t* lsrc = reinterpret_cast<int64_t*>(lds + 5 * DE_MAX_OUT);
+  if (live) {
+    lds[0 * DE_MAX_OUT + o] = R.t;
+    lds[1 * DE_MAX_OUT + o] = R.sx;
+    lds[2 * DE_MAX_OUT + o] = R.sy;
+    lds[3 * DE_MAX_OUT + o] = R.ex;
+    lds[4 * DE_MAX_OUT + o] = R.ey;
+    lsrc[o] = p;
+    if (d) {
+      lds[0 * DE_MAX_OUT + o + 1] = (R.t + Q.t) / 2;
+      lds[1 * DE_MAX_OUT + o + 1] = R.ex;
+      lds[2 * DE_MAX_OUT + o + 1] = R.ey;
+      lds[3 * DE_MAX_OUT + o + 1] = Q.sx;
+      lds[4 * DE_MAX_OUT + o + 1] = Q.sy;
+      lsrc[o + 1] = ~(p + 1);
+    }
+  }
+  __syncthreads();
+  double* const fo[5] = {O.time_seconds, O.start_x, O.start_y, O.end_x, O.end_y};
+#pragma unroll
+  for (int col = 0; col < 5; ++col)
+    for (int k = threadIdx.x; k < tot; k += AC_THREADS) fo[col][base + k] = lds[col * DE_MAX_OUT + k];
+  for (int k = threadIdx.x; k < tot; k += AC_THREADS) O.src[base + k] = lsrc[k];
+  __syncthreads();
+  int32_t* li = reinterpret_cast<int32_t*>(lds);
+  uint8_t* lu = reinterpret_cast<uint8_t*>(li + 4 * DE_MAX_OUT);
+  if (live) {
+    li[0 * DE_MAX_OUT + o] = R.game;
+    li[1 * DE_MAX_OUT + o] = R.team;
+    li[2 * DE_MAX_OUT + o] = R.player;
+    li[3 * DE_MAX_OUT + o] = R.event;
+    lu[0 * DE_MAX_OUT + o] = (uint8_t)R.per;
+    lu[1 * DE_MAX_OUT + o] = (uint8_t)R.type;
+    lu[2 * DE_MAX_OUT + o] = (uint8_t)R.res;
+    lu[3 * DE_MAX_OUT + o] = (uint8_t)R.bp;
+    if (d) {
+      li[0 * DE_MAX_OUT + o + 1] = Q.game;
+      li[1 * DE_MAX_OUT + o + 1] = Q.team;
+      li[2 * DE_MAX_OUT + o + 1] = Q.player;
+      li[3 * DE_MAX_OUT + o + 1] = -1;
+      lu[0 * DE_MAX_OUT + o + 1] = (uint8_t)Q.per;
+      lu[1 * DE_MAX_OUT + o + 1] = (uint8_t)A_DRIBBLE;
+      lu[2 * DE_MAX_OUT + o + 1] = 1;
+      lu[3 * DE_MAX_OUT + o + 1] = 0;
+    }
+  }
+  __syncthreads();
+  int32_t* const io[4] = {O.game, O.team, O.player, O.event};
+#pragma unroll
+  for (int col = 0; col < 4; ++col)
+    for (int k = threadIdx.x; k < tot; k += AC_THREADS) io[col][base + k] = li[col * DE_MAX_OUT + k];
+  uint8_t* const uo[4] = {O.period_id, O.type_id, O.result_id, O.bodypart_id};
+#pragma unroll
+  for (int col = 0; col < 4; ++col)
+    for (int k = threadIdx.x; k < tot; k += AC_THREADS) uo[col][base + k] = lu[col * DE_MAX_OUT + k];
 }
 
 // seg_off[key[k]] = k at every run start of the sorted keys 0..n_seg-1 (each present)

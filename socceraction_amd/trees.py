@@ -201,7 +201,8 @@ class TreeEnsemble:
         bb, fb, ib = blocks.sa_blocks()
         _native.check(_native.lib().sa_tree_predict(
             d['nodes'].data_ptr(), len(self.nodes), d['roots'].data_ptr(),
-            d['depth'].data_ptr() if self.n_trees else None, self.n_trees,
+            d['depth'].data_ptr() if (self.n_trees and d['depth'] is not None) else None,
+            self.n_trees,
             slots.data_ptr(), len(slots), ctypes.byref(bb), ctypes.byref(fb), ctypes.byref(ib),
             n, float(self.base_margin), int(self.le), int(self.f32), out.data_ptr(),
             stream_handle()))

@@ -63,6 +63,29 @@ def test_xgboost_json_on_device_equals_oracle(sa):
     np.testing.assert_allclose(p, ref, rtol=1e-6, atol=0)
 
 
+@pytest.mark.parametrize('kind', ['xgboost', 'sklearn'])
+def test_fixed_depth_walk_equals_leaf_checked_walk(sa, kind):
+    """The fixed-depth walk (per-tree depths given) and the leaf-checked walk (no depths) give
+    bit-identical probabilities, on unbalanced scikit-learn trees too."""
+    g, df, ab, fb, X = _game(sa)
+    kinds = [k for _, k, _ in fb.plan.order]
+    if kind == 'xgboost':
+        model = sa['trees'].synthetic_xgboost_json(len(kinds), n_trees=37, depth=4, seed=5,
+                                                   feature_kinds=kinds)
+    else:
+        from sklearn.ensemble import HistGradientBoostingClassifier
+        y = g['scores'].astype(int).copy()
+        y[::3] = 1
+        model = HistGradientBoostingClassifier(max_iter=30, max_leaf_nodes=9,
+                                               random_state=0).fit(X, y)
+    te = sa['trees'].TreeEnsemble.from_model(model)
+    assert te is not None and te.depths().max() >= 3
+    fixed = te.predict_blocks(fb).cpu().numpy()
+    te._dev['depth'] = None
+    walked = te.predict_blocks(fb).cpu().numpy()
+    np.testing.assert_array_equal(fixed, walked)
+
+
 def test_missing_values_follow_default_direction(sa):
     """NaN written into a device feature column takes default_left, like the oracle."""
     from oracle import tree_oracle as to
