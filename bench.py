@@ -77,13 +77,13 @@ def _reduce(dist, value, op, dev):
 
 def xt_step(ab, dist):
     """BASELINE cfg4 inside the step: xT 16x12 fit on the step's actions (count pass, RCCL
-    all-reduce of the counts across ranks, value iteration to eps=1e-5; the solve synchronises)
-    and ExpectedThreat.rate of every action. Returns the closure and a holder of the last
-    solution (iterations)."""
+    all-reduce of the counts across ranks, value iteration to eps=1e-5; the solve synchronises
+    its stream) and ExpectedThreat.rate of every action, as two phases so the caller can enqueue
+    the VAEP kernels in between. Returns (start, finish, holder of the last solution)."""
     from socceraction_amd import shard
-    last = {}
+    state = {}
 
-    def once():
+    def start():
         acc = ops.xt_count(ab, 16, 12)
         if dist is not None and dist.get_backend() == 'nccl':
             shard.allreduce_xt_counts(acc.shot, acc.goal, acc.move, acc.trans, acc.err)
@@ -92,10 +92,13 @@ def xt_step(ab, dist):
                 h = t.cpu()
                 dist.all_reduce(h)
                 t.copy_(h)
-        sol = ops.xt_solve(acc)  # synchronises
+        state['acc'] = acc
+
+    def finish():
+        sol = ops.xt_solve(state.pop('acc'))  # synchronises the current stream
         ops.xt_rate(ab, sol.mats[3].reshape(12, 16), 16, 12)
-        last['sol'] = sol
-    return once, last
+        state['sol'] = sol
+    return start, finish, state
 
 
 ATOMIC_DEFAULT = ['actiontype', 'actiontype_onehot', 'bodypart', 'bodypart_onehot', 'time',
@@ -280,6 +283,9 @@ def main() -> None:
                          'iteration (default: one all-reduce, replicated solve)')
     ap.add_argument('--atomic-games', type=int, default=1250,
                     help='atomic games per GPU for cfg3 (1250 ~ 5M atomic actions)')
+    ap.add_argument('--serial', action='store_true',
+                    help='run the xT fit + rate after the VAEP kernels on the same stream '
+                         '(default: on a side stream, overlapped)')
     ap.add_argument('--bool-tile', type=int, default=1024,
                     help='rows per bool-block tile (0 = one tile: plain column-major)')
     ap.add_argument('--num-tile', type=int, default=128,
@@ -317,26 +323,53 @@ def main() -> None:
     lab = ops.LabelBlocks(n, lab_buf[0], lab_buf[1], None)
     val = torch.empty((3, ld), dtype=torch.float64, device=dev)
     s_act = ab.struct()
-    xt_once, xt_last = xt_step(ab, dist)
+    xt_start, xt_finish, xt_last = xt_step(ab, dist)
     calls = (lambda: ops.features_into(s_act, bool_out),
              lambda: ops.features_into(s_act, num_out),
              lambda: ops.goalscore_into(ab, out),
              lambda: ops.labels(ab, 10, lab),
-             lambda: ops.formula(ab, ps, pc, val),
-             xt_once)
+             lambda: ops.formula(ab, ps, pc, val))
+    main_s = torch.cuda.current_stream()
+    side = torch.cuda.Stream() if not args.serial else main_s
 
     def step(ev=None):
+        # default: the xT fit runs on a side stream next to the VAEP kernels -- its count pass
+        # and RCCL all-reduce are enqueued first, then the five VAEP kernels, then the solve (a
+        # single workgroup that would otherwise leave the GPU idle, and a host sync of the side
+        # stream) and the rate. --serial: xT after the VAEP kernels on the one stream.
+        nv = len(calls)
+        overlap = side is not main_s
+        if overlap:
+            fork = torch.cuda.Event()
+            fork.record(main_s)
+            side.wait_event(fork)
+            with torch.cuda.stream(side):
+                if ev is not None:
+                    ev[nv + 1].record(side)
+                xt_start()
         for i, call in enumerate(calls):
             if ev is not None:
-                ev[i].record()
+                ev[i].record(main_s)
             call()
         if ev is not None:
-            ev[len(calls)].record()
+            ev[nv].record(main_s)
+        if not overlap:
+            if ev is not None:
+                ev[nv + 1].record(main_s)
+            xt_start()
+        with torch.cuda.stream(side):
+            xt_finish()
+            if ev is not None:
+                ev[nv + 2].record(side)
+        if overlap:
+            join = torch.cuda.Event()
+            join.record(side)
+            main_s.wait_event(join)
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(len(calls) + 1)]
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(len(calls) + 3)]
            for _ in range(args.steps)]
     if dist:
         dist.barrier()
@@ -348,8 +381,10 @@ def main() -> None:
     if dist:
         dist.barrier()
     wall = time.perf_counter() - t0
+    nv = len(calls)
     kern = {name: float(np.mean([e[i].elapsed_time(e[i + 1]) for e in evs]))
-            for i, name in enumerate(KERNELS)}
+            for i, name in enumerate(KERNELS[:nv])}
+    kern['xt_fit_rate'] = float(np.mean([e[nv + 1].elapsed_time(e[nv + 2]) for e in evs]))
     total_actions = n
     if dist:
         wall = _reduce(dist, wall, dist.ReduceOp.MAX, dev)
@@ -401,8 +436,12 @@ def main() -> None:
     }
     line['xt_cfg4'] = {'workload': 'cfg4 inside the step: xT 16x12 fit (count + all-reduce + '
                                    'value iteration to eps=1e-5) + rate of the step\'s actions',
-                       'ms': round(kern['xt_fit_rate'], 4),
-                       'iterations': xt_last['sol'].n_iter}
+                       # overlapped: the side stream's span from its first launch to the
+                       # rate's end (it shares the GPU with the VAEP kernels meanwhile)
+                       'ms' if args.serial else 'span_ms': round(kern['xt_fit_rate'], 4),
+                       'iterations': xt_last['sol'].n_iter,
+                       'stream': 'main (serial)' if args.serial else 'side stream, overlapped '
+                                                                     'with the VAEP kernels'}
     line.update(extra_side)
     if not args.no_cpu:
         line['cpu_baseline'] = cpu_baseline(d, args.cpu_seconds)
