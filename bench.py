@@ -286,6 +286,10 @@ def main() -> None:
     ap.add_argument('--serial', action='store_true',
                     help='run the xT fit + rate after the VAEP kernels on the same stream '
                          '(default: on a side stream, overlapped)')
+    ap.add_argument('--xt-fork', type=int, default=0,
+                    help='overlapped mode: VAEP kernels enqueued before the side stream forks '
+                         'for the xT count pass (0: first; 1 / 2 / serial measured 1.9 / 4 / 6 %% '
+                         'slower per step, profiles/r01g_xt_fork_ab.log)')
     ap.add_argument('--bool-tile', type=int, default=1024,
                     help='rows per bool-block tile (0 = one tile: plain column-major)')
     ap.add_argument('--num-tile', type=int, default=128,
@@ -333,21 +337,22 @@ def main() -> None:
     side = torch.cuda.Stream() if not args.serial else main_s
 
     def step(ev=None):
-        # default: the xT fit runs on a side stream next to the VAEP kernels -- its count pass
-        # and RCCL all-reduce are enqueued first, then the five VAEP kernels, then the solve (a
-        # single workgroup that would otherwise leave the GPU idle, and a host sync of the side
-        # stream) and the rate. --serial: xT after the VAEP kernels on the one stream.
+        # default: the xT fit runs on a side stream next to the VAEP kernels -- the first
+        # `xt_fork` VAEP kernels are enqueued, then the side stream forks for the count pass and
+        # RCCL all-reduce, then the remaining VAEP kernels, then the solve (a single workgroup
+        # that would otherwise leave the GPU idle, and a host sync of the side stream) and the
+        # rate. --serial: xT after the VAEP kernels on the one stream.
         nv = len(calls)
         overlap = side is not main_s
-        if overlap:
-            fork = torch.cuda.Event()
-            fork.record(main_s)
-            side.wait_event(fork)
-            with torch.cuda.stream(side):
-                if ev is not None:
-                    ev[nv + 1].record(side)
-                xt_start()
         for i, call in enumerate(calls):
+            if overlap and i == min(args.xt_fork, nv - 1):
+                fork = torch.cuda.Event()
+                fork.record(main_s)
+                side.wait_event(fork)
+                with torch.cuda.stream(side):
+                    if ev is not None:
+                        ev[nv + 1].record(side)
+                    xt_start()
             if ev is not None:
                 ev[i].record(main_s)
             call()
@@ -440,8 +445,9 @@ def main() -> None:
                        # rate's end (it shares the GPU with the VAEP kernels meanwhile)
                        'ms' if args.serial else 'span_ms': round(kern['xt_fit_rate'], 4),
                        'iterations': xt_last['sol'].n_iter,
-                       'stream': 'main (serial)' if args.serial else 'side stream, overlapped '
-                                                                     'with the VAEP kernels'}
+                       'stream': 'main (serial)' if args.serial else
+                       f'side stream, forked after {args.xt_fork} VAEP kernel(s), overlapped '
+                       'with the rest'}
     line.update(extra_side)
     if not args.no_cpu:
         line['cpu_baseline'] = cpu_baseline(d, args.cpu_seconds)
