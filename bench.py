@@ -449,7 +449,7 @@ def main() -> None:
                        f'side stream, forked after {args.xt_fork} VAEP kernel(s), overlapped '
                        'with the rest'}
     line.update(extra_side)
-    if not args.no_cpu:
+    if not args.no_cpu and world == 1:  # the CPU comparator runs on rank 0 at N = 1 only
         line['cpu_baseline'] = cpu_baseline(d, args.cpu_seconds)
     print(json.dumps(line), flush=True)
     if dist:
