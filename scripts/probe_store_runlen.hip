@@ -97,10 +97,38 @@ static int timeit(const char* name, int G, int xcd, L launch, double bytes) {
   return 0;
 }
 
+// allocation flavours: 0 hipMalloc, 1 hipExtMallocWithFlags(hipDeviceMallocContiguous),
+// 2 one VMM physical handle of the whole size mapped at a reserved range
+static int alloc(uint8_t** out, size_t bytes, int how) {
+  if (how == 0) return hipMalloc(out, bytes) != hipSuccess;
+  if (how == 1) return hipExtMallocWithFlags((void**)out, bytes, hipDeviceMallocContiguous) != hipSuccess;
+  hipMemAllocationProp prop = {};
+  prop.type = hipMemAllocationTypePinned;
+  prop.location.type = hipMemLocationTypeDevice;
+  prop.location.id = 0;
+  size_t gran = 0;
+  CHECK(hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityRecommended));
+  const size_t sz = (bytes + gran - 1) / gran * gran;
+  hipMemGenericAllocationHandle_t h;
+  CHECK(hipMemCreate(&h, sz, &prop, 0));
+  void* va = nullptr;
+  CHECK(hipMemAddressReserve(&va, sz, 0, nullptr, 0));
+  CHECK(hipMemMap(va, sz, 0, h, 0));
+  hipMemAccessDesc acc = {};
+  acc.location = prop.location;
+  acc.flags = hipMemAccessFlagsProtReadWrite;
+  CHECK(hipMemSetAccess(va, sz, &acc, 1));
+  printf("{\"vmm_granularity\": %zu}\n", gran);
+  *out = (uint8_t*)va;
+  return 0;
+}
+
 int main(int argc, char** argv) {
   const double bytes = (double)N * C;
   const int64_t tiles = N / 1024, chunks = tiles * C;
   const int trials = argc > 1 ? atoi(argv[1]) : 1;
+  const int how = argc > 2 ? atoi(argv[2]) : 0;
+  const bool quick = argc > 3 && atoi(argv[3]) != 0;
   int rc = 0;
   const int Gs[] = {1, 2, 4, 31};
   u32x4* codes = nullptr;
@@ -108,8 +136,16 @@ int main(int argc, char** argv) {
   CHECK(hipMemset(codes, 0, 4096 * 64 * sizeof(u32x4)));
   for (int t = 0; t < trials; ++t) {
     uint8_t* out = nullptr;  // kept alive: every trial lands somewhere else
-    CHECK(hipMalloc(&out, (size_t)bytes));
+    if (alloc(&out, (size_t)bytes, how)) { fprintf(stderr, "allocation %d failed\n", how); return 1; }
     printf("{\"trial\": %d, \"ptr_GB\": %.2f}\n", t, (double)(uintptr_t)out / (1 << 30));
+    if (quick) {
+      for (int G : {1, 31}) {
+        const int64_t ng = (C + G - 1) / G;
+        const unsigned nb = (unsigned)(((tiles * ng + 3) / 4 + 7) / 8 * 8);
+        rc |= timeit("runs4", G, 1, [&] { runs<4><<<nb, 256>>>(out, tiles, G, 1); }, bytes);
+      }
+      continue;
+    }
     for (int G : Gs) {
       const int64_t ng = (C + G - 1) / G;
       const unsigned blocks = (unsigned)((tiles * ng + 3) / 4);
