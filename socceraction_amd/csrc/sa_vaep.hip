@@ -18,7 +18,6 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
-#include <mutex>
 
 #include "sa_common.h"
 #include "sa_internal.h"
@@ -28,12 +27,8 @@
 #endif
 #ifndef SA_BOOL_MODE
 // bool block: 0 = one wave per 1024-row tile, 1 = one wave per (tile, window),
-// 2 = one wave per (tile, column group) in XCD-contiguous sweep order,
-// 3 = window-code pre-pass + G columns per wave, XCD-contiguous (A/B only: not faster)
+// 2 = one wave per (tile, column group) in XCD-contiguous sweep order
 #define SA_BOOL_MODE 2
-#endif
-#ifndef SA_BOOL_G_COLS
-#define SA_BOOL_G_COLS 4  // bool_col_kernel: 1-KiB column chunks per wave (1, 2, 4 or 8)
 #endif
 #ifndef SA_XCD_REMAP
 #define SA_XCD_REMAP 1  // block -> output range mapping that gives each XCD a contiguous part
@@ -724,395 +719,6 @@ __global__ __launch_bounds__(64 * CG_WAVES) void bool_colgroup_kernel(FeatArgs a
       st_bool16(bb, tc, R, m[0], m[1], m[2], m[3]);
     }
   }
-}
-
-// Column form (default, SA_BOOL_MODE 3): every wave writes exactly ONE 1-KiB column chunk
-// (1024 rows of one column) and exits.  The pure-store probe scripts/probe_store_runlen.hip
-// (profiles/r01g_store_runlen.md) shows why: waves that each write G consecutive chunks of
-// the bool image run 7.1 - 7.3 TB/s at G = 1 on every allocation tried but 5.7 - 7.1 TB/s at
-// G = 31 (the column-group kernel's shape), depending on where the block lands; one or two
-// 16-B L2 loads ahead of the single store keep G = 1 at 7.3 - 7.5 TB/s.  Rebuilding the
-// game-state windows per chunk would cost far more than the store, so a pre-pass
-// (bool_codes_kernel) writes every 1024-row chunk's window ids once, as bytes:
-//   codes[chunk][window i][slot][1024 rows],  slot = type, result, type*6+result, bodypart,
-//                                              same-team-as-a0 (i >= 1)
-// (5k B/action, L2/MALL-resident between the two launches) and bool_col_kernel turns one
-// 16-B code word per lane into the column's 16 one-hot bytes.
-constexpr int CODE_SLOTS = 5;
-enum { CS_TYPE = 0, CS_RESULT = 1, CS_TR = 2, CS_BP = 3, CS_TEAM = 4 };
-constexpr int CODE_WAVES = 4;
-
-// find_segment(seg_off, nseg, j) for a wave-uniform row j < n: a 64-ary search, one load
-// per lane per level (3 dependent loads for 10k segments instead of 14).  Needs all 64 lanes.
-__device__ __forceinline__ int64_t wave_find_segment(const int64_t* __restrict__ seg_off,
-                                                     int64_t nseg, int64_t j) {
-  const int lane = threadIdx.x & (WAVE - 1);
-  int64_t lo = 0, hi = nseg;  // seg_off[lo] <= j < seg_off[hi]
-  while (hi - lo > 1) {
-    const int64_t step = (hi - lo + WAVE - 1) / WAVE;
-    const int64_t idx = lo + (int64_t)lane * step;
-    const bool ok = idx < hi && seg_off[idx] <= j;  // a prefix of the lanes (lane 0 always)
-    const uint64_t m = __ballot(ok);
-    const int64_t nlo = lo + (int64_t)(63 - __clzll(m)) * step;
-    hi = nlo + step < hi ? nlo + step : hi;
-    lo = nlo;
-  }
-  return lo;
-}
-
-// One wave writes the window codes of one 1024-row chunk.  `tl` is the wave's own LDS
-// staging area for team codes (BOOL_TILE + 8 ints); only wave-level synchronisation is used,
-// so any single wave may call this (bool_fused_kernel's fallback does).
-template <bool ATOMIC, bool EXPLICIT>
-__device__ __forceinline__ void codes_for_chunk(const FeatArgs& args, int64_t chunk, int32_t* tl,
-                                                uint8_t* __restrict__ codes) {
-  const int lane = threadIdx.x & (WAVE - 1);
-  const sa_actions& A = args.a;
-  const sa_feature_plan& P = args.p;
-  const int64_t n = A.n;
-  const int K = P.nb_prev_actions;
-  const int64_t tile0 = chunk * BOOL_TILE;
-  const int64_t j0 = tile0 + (int64_t)lane * LANE_ACTS;
-  const sa_frame& F0 = A.frames[0];
-  const bool need_team = P.bool_col[SA_XFN_TEAM] >= 0 && K > 1;
-  const bool need_type = P.bool_col[SA_XFN_ACTIONTYPE_ONEHOT] >= 0;
-  const bool need_res = !ATOMIC && P.bool_col[SA_XFN_RESULT_ONEHOT] >= 0;
-  const bool need_tr = !ATOMIC && P.bool_col[SA_XFN_ACTIONTYPE_RESULT_ONEHOT] >= 0;
-  const bool need_bp = P.bool_col[SA_XFN_BODYPART_ONEHOT] >= 0;
-  if (!EXPLICIT && need_team && tile0 < n) {  // team codes of rows tile0-8 .. tile0+1023
-    for (int k = lane; k < BOOL_TILE + 8; k += WAVE) tl[k] = ld_or0(F0.team, tile0 - 8 + k, n);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  }
-  int64_t g0 = 0;  // segment of the chunk's first row (wave-uniform)
-  if (!EXPLICIT && K > 1 && tile0 < n) g0 = wave_find_segment(A.seg_off, A.n_segments, tile0);
-  if (j0 >= n) return;
-  uint8_t* cb = codes + chunk * (int64_t)(CODE_SLOTS * K) * BOOL_TILE + lane * LANE_ACTS;
-  auto put = [&](int i, int slot, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
-    *reinterpret_cast<u32x4*>(cb + (int64_t)(i * CODE_SLOTS + slot) * BOOL_TILE) = u32x4{a, b, c, d};
-  };
-  uint32_t dw[4] = {0, 0, 0, 0};  // d = min(j - seg_start, 15) per action
-  if (!EXPLICIT && K > 1) {
-    SegCursor c{g0, A.seg_off[g0], A.seg_off[g0 + 1]};
-#pragma unroll
-    for (int m = 0; m < LANE_ACTS; ++m) {
-      const int64_t j = j0 + m;
-      if (j < n) {
-        seg_advance(A, c, j);
-        const int64_t dd = j - c.s;
-        const int d = dd > 15 ? 15 : (int)dd;
-        dw[m >> 2] |= (uint32_t)d << (8 * (m & 3));
-      }
-    }
-  }
-  uint32_t TR[6], RR[6], BR[6];  // rows j0-8 .. j0+15 (windowed mode)
-  uint32_t tw[4], rw[4], bw[4];  // window i of the lane's 16 actions
-  if (!EXPLICIT) {
-    const int64_t wbase = j0 / 4 - 2;
-#pragma unroll
-    for (int k = 0; k < 6; ++k) {
-      TR[k] = ld_u8x4(F0.type_id, wbase + k, n);
-      RR[k] = ATOMIC ? 0u : ld_u8x4(F0.result_id, wbase + k, n);
-      BR[k] = ld_u8x4(F0.bodypart_id, wbase + k, n);
-    }
-  }
-  for (int i = 0; i < K; ++i) {
-    if (EXPLICIT) {
-      const sa_frame& Fi = A.frames[i];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        tw[q] = ld_u8x4(Fi.type_id, j0 / 4 + q, n);
-        rw[q] = ATOMIC ? 0u : ld_u8x4(Fi.result_id, j0 / 4 + q, n);
-        bw[q] = ld_u8x4(Fi.bodypart_id, j0 / 4 + q, n);
-      }
-    } else if (i == 0) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        tw[q] = TR[2 + q];
-        rw[q] = RR[2 + q];
-        bw[q] = BR[2 + q];
-      }
-    } else {  // window i = window i-1 shifted one row, clamped bytes kept
-      shift_rows(TR);
-      if (!ATOMIC) shift_rows(RR);
-      shift_rows(BR);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const uint32_t mk = ge_mask(dw[q], i);
-        tw[q] = (TR[2 + q] & mk) | (tw[q] & ~mk);
-        rw[q] = (RR[2 + q] & mk) | (rw[q] & ~mk);
-        bw[q] = (BR[2 + q] & mk) | (bw[q] & ~mk);
-      }
-    }
-    if (need_type) put(i, CS_TYPE, tw[0], tw[1], tw[2], tw[3]);
-    if (need_res) put(i, CS_RESULT, rw[0], rw[1], rw[2], rw[3]);
-    if (need_tr) {
-      // code = type*6 + result per byte (type <= 22, result <= 5: no carry between bytes)
-      uint32_t cw[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) cw[q] = (tw[q] << 2) + (tw[q] << 1) + rw[q];
-      put(i, CS_TR, cw[0], cw[1], cw[2], cw[3]);
-    }
-    if (need_bp) put(i, CS_BP, bw[0], bw[1], bw[2], bw[3]);
-    if (need_team && i >= 1) {  // team_i (features.py:448-452)
-      uint32_t m[4] = {0, 0, 0, 0};
-#pragma unroll
-      for (int mm = 0; mm < LANE_ACTS; ++mm) {
-        int32_t t0, ti;
-        if (EXPLICIT) {
-          t0 = ld_or0(A.frames[0].team, j0 + mm, n);
-          ti = ld_or0(A.frames[i].team, j0 + mm, n);
-        } else {
-          const int d = (int)byte_of(dw[mm >> 2], mm & 3);
-          const int s = d < i ? d : i;
-          const int32_t* tr = tl + 8 + lane * LANE_ACTS + mm;
-          t0 = tr[0];
-          ti = tr[-s];
-        }
-        m[mm >> 2] |= (uint32_t)(t0 == ti) << (8 * (mm & 3));
-      }
-      put(i, CS_TEAM, m[0], m[1], m[2], m[3]);
-    }
-  }
-}
-
-template <bool ATOMIC, bool EXPLICIT>
-__global__ __launch_bounds__(64 * CODE_WAVES) void bool_codes_kernel(FeatArgs args,
-                                                                    uint8_t* __restrict__ codes) {
-  __shared__ int32_t team_lds[CODE_WAVES][BOOL_TILE + 8];
-  const int wv = threadIdx.x / WAVE;
-  codes_for_chunk<ATOMIC, EXPLICIT>(args, (int64_t)blockIdx.x * CODE_WAVES + wv, team_lds[wv], codes);
-}
-
-// Per-column descriptors of the bool block (host-built from the plan, passed by value so a
-// wave reads its column's entry with one scalar load from the kernel arguments):
-// desc[c] = slot << 8 | value, where slot = window * CODE_SLOTS + code slot; 0xFFFF = a
-// column no bool family writes.  The per-wave budget is tight -- a 16M-action launch is 8M
-// waves, ~80 VALU instructions each at HBM speed -- so all addressing is scalar.
-constexpr int SA_MAX_BOOL_COLS = (N_TYPES + N_RESULTS + N_TYPES * N_RESULTS + N_BODYPARTS) *
-                                     SA_MAX_FRAMES + SA_MAX_FRAMES - 1;
-struct BoolCols {
-  int32_t slots;          // code slots per chunk (CODE_SLOTS * k)
-  int32_t chunks_per_tile;  // tile_rows / 1024, or 0 when the block is one tile
-  uint16_t desc[SA_MAX_BOOL_COLS + 1];  // even count: read as u32 pairs
-};
-
-__device__ __forceinline__ u32x4 eq16(u32x4 x, uint32_t v) {
-  return u32x4{bytes_eq(x.x, v), bytes_eq(x.y, v), bytes_eq(x.z, v), bytes_eq(x.w, v)};
-}
-
-template <bool ATOMIC, int G>
-__global__ __launch_bounds__(64 * CODE_WAVES) void bool_col_kernel(FeatArgs args,
-                                                                  const uint8_t* __restrict__ codes,
-                                                                  BoolCols bc) {
-  const int lane = threadIdx.x & (WAVE - 1);
-  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
-  const uint32_t w = (uint32_t)xcd_logical_block() * CODE_WAVES + wv;  // (chunk, column group)
-  const uint32_t Cb = (uint32_t)args.Cb;
-  const uint32_t ng = (Cb + G - 1) / G;
-  const uint32_t chunk = w / ng, c0 = (w - chunk * ng) * G;
-  const int64_t n = args.a.n;
-  const int64_t row0 = (int64_t)chunk * BOOL_TILE;
-  if (row0 >= n || row0 + lane * LANE_ACTS >= n) return;
-  const uint8_t* cb = codes + (int64_t)chunk * bc.slots * BOOL_TILE + lane * LANE_ACTS;
-  // all G code words are loaded before the first store (their latency overlaps)
-  uint32_t d[G];
-  u32x4 x[G];
-#pragma unroll
-  for (int q = 0; q < G; ++q) {
-    const uint32_t c = c0 + q;
-    const uint32_t dd = c < Cb ? reinterpret_cast<const uint32_t*>(bc.desc)[c >> 1] : 0xFFFFFFFFu;
-    d[q] = (c & 1u) ? dd >> 16 : dd & 0xFFFFu;
-    if (d[q] != 0xFFFFu) x[q] = *reinterpret_cast<const u32x4*>(cb + (int64_t)(d[q] >> 8) * BOOL_TILE);
-  }
-  // tile_off(row0, c) with scalar arithmetic: the chunk's tile and its row inside the tile
-  const int64_t R = args.Rb;
-  const uint32_t t = bc.chunks_per_tile ? chunk / (uint32_t)bc.chunks_per_tile : 0u;
-  uint8_t* ob = args.bout + (int64_t)t * Cb * R + (row0 - (int64_t)t * R) + lane * LANE_ACTS;
-#pragma unroll
-  for (int q = 0; q < G; ++q) {
-    if (d[q] == 0xFFFFu) continue;
-    const uint32_t slot = d[q] >> 8, v = d[q] & 0xFFu, kind = slot % CODE_SLOTS;
-    u32x4 m;
-    if (kind == CS_TEAM) {
-      m = x[q];  // already 0 / 1 per row
-    } else if (ATOMIC && kind == CS_TYPE) {
-      // 33 atomic names, 32 unique: 'interception' (ids 10 and 24) is ONE column true for
-      // both ids (atomic/vaep/features.py:114-132 + atomic/spadl/config.py:25-36)
-      m = eq16(x[q], v <= 23 ? v : v + 1);
-      if (v == 10) m |= eq16(x[q], AT_INTERCEPTION2);
-    } else {
-      m = eq16(x[q], v);
-    }
-    st16(ob + (int64_t)(c0 + q) * R, m);
-  }
-}
-
-// Lean one-chunk-per-wave form (SA_BOOL_MODE 5): a 2-D grid (column block, chunk) so that no
-// wave divides -- at 8M waves per launch the per-wave budget is ~90 scalar and ~90 vector
-// instructions per CU at HBM speed (the scalar unit is shared by the CU's four SIMDs), and
-// the division-based (chunk, column) decode of bool_col_kernel<G = 1> alone exceeded it.
-// Blocks run in plain (linear) order: the XCD remap needs a division and buys ~3 % on the
-// pure-store pattern (profiles/r01g_store_runlen.md).
-template <bool ATOMIC>
-__global__ __launch_bounds__(64 * CODE_WAVES) void bool_col1_kernel(FeatArgs args,
-                                                                   const uint8_t* __restrict__ codes,
-                                                                   BoolCols bc) {
-  const uint32_t c = blockIdx.x * CODE_WAVES + __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
-  const int lane = threadIdx.x & (WAVE - 1);
-  const uint32_t dd = reinterpret_cast<const uint32_t*>(bc.desc)[c >> 1];  // one s_load
-  const uint32_t d = (c & 1u) ? dd >> 16 : dd & 0xFFFFu;
-  const int64_t chunk = blockIdx.y;
-  const int64_t row = chunk * BOOL_TILE + lane * LANE_ACTS;
-  if (c >= (uint32_t)args.Cb || d == 0xFFFFu || row >= args.a.n) return;
-  const uint32_t slot = d >> 8, v = d & 0xFFu;
-  const u32x4 x = *reinterpret_cast<const u32x4*>(codes + (chunk * bc.slots + slot) * BOOL_TILE +
-                                                  lane * LANE_ACTS);
-  u32x4 m;
-  if (slot % CODE_SLOTS == CS_TEAM) {
-    m = x;  // already 0 / 1 per row
-  } else if (ATOMIC && slot % CODE_SLOTS == CS_TYPE) {
-    // 33 atomic names, 32 unique: 'interception' (ids 10 and 24) is ONE column true for both
-    // ids (atomic/vaep/features.py:114-132 + atomic/spadl/config.py:25-36)
-    m = eq16(x, v <= 23 ? v : v + 1);
-    if (v == 10) m |= eq16(x, AT_INTERCEPTION2);
-  } else {
-    m = eq16(x, v);
-  }
-  const int64_t R = args.Rb;  // tile of the chunk: chunk (R = 1024), 0 (one tile) or chunk / cpt
-  const int64_t t = bc.chunks_per_tile == 1 ? chunk
-                    : bc.chunks_per_tile == 0 ? 0
-                                              : chunk / bc.chunks_per_tile;
-  st16(args.bout + t * args.Cb * R + (int64_t)c * R + (row - t * R), m);
-}
-
-// Fused form (SA_BOOL_MODE 4): the two launches above in ONE kernel, so the window codes
-// are read from L2 right after they are written instead of from HBM.  Each XCD (workgroup
-// x -> XCD x % 8) owns a contiguous range of chunk groups (CODE_WAVES chunks per group) and
-// walks it in dispatch order: FUSE_AHEAD producer workgroups first, then per group g one
-// producer workgroup for group g + FUSE_AHEAD followed by the Cb consumer workgroups of group g
-// (4 waves each, one (chunk, column) per wave, as bool_col_kernel at G = 1).  A producer wave
-// writes its chunk's codes, waits for the stores (s_waitcnt vmcnt(0): acked by the L2), and
-// publishes flag[chunk] = 1 + its XCD id.  A consumer spins (bounded) on the flag; codes are
-// trusted only from a producer on its own XCD (same L2) and read with L1-bypassing loads.  If
-// the flag does not show up in time, or shows another XCD, the consumer wave writes the chunk's
-// codes itself (the same bytes) and uses its own copy -- so results never depend on the
-// dispatch order, only the speed does.
-constexpr int FUSE_AHEAD = 16;
-constexpr int FUSE_SPIN = 4096;
-
-struct FuseLayout {
-  int64_t nchunks;
-  int32_t ngroups, gpx;  // chunk groups, groups per XCD
-};
-
-__device__ __forceinline__ uint32_t xcc_id() {
-  uint32_t id;
-  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(id));
-  return id & 0xFu;
-}
-
-__device__ __forceinline__ u32x4 ld16_l2(const uint8_t* p) {  // bypasses the (incoherent) L1
-  u32x4 x;
-  asm volatile("global_load_dwordx4 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(x) : "v"(p) : "memory");
-  return x;
-}
-
-#if SA_FUSE_STATS  // A/B diagnostics: consumers that waited / fell back / saw another XCD, total polls
-__device__ unsigned long long fuse_stats[4];
-#endif
-
-template <bool ATOMIC, bool EXPLICIT>
-__global__ __launch_bounds__(64 * CODE_WAVES) __attribute__((amdgpu_waves_per_eu(8, 8))) void bool_fused_kernel(FeatArgs args,
-                                                                    uint8_t* __restrict__ codes,
-                                                                    uint32_t* __restrict__ flags,
-                                                                    BoolCols bc, FuseLayout L) {
-  __shared__ int32_t team_lds[CODE_WAVES][BOOL_TILE + 8];
-  const int lane = threadIdx.x & (WAVE - 1);
-  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
-  const uint32_t x = blockIdx.x % 8, k = blockIdx.x / 8;
-  const int32_t g0 = (int32_t)x * L.gpx;
-  const int32_t g1 = g0 + L.gpx < L.ngroups ? g0 + L.gpx : L.ngroups;
-  const uint32_t Cb = (uint32_t)args.Cb;
-  const int64_t n = args.a.n;
-  int32_t prod = -1, g = -1;
-  uint32_t r = 0;
-  if (k < (uint32_t)FUSE_AHEAD) {
-    prod = g0 + (int32_t)k;
-  } else {
-    const uint32_t kk = k - FUSE_AHEAD;
-    g = g0 + (int32_t)(kk / (Cb + 1));
-    r = kk % (Cb + 1);
-    if (r == 0) prod = g + FUSE_AHEAD;
-  }
-  if (prod >= 0) {  // producer: one chunk per wave
-    const int64_t chunk = (int64_t)prod * CODE_WAVES + wv;
-    if (prod >= g1 || chunk >= L.nchunks) return;
-    codes_for_chunk<ATOMIC, EXPLICIT>(args, chunk, team_lds[wv], codes);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the code stores are in the L2
-    if (lane == 0)
-      __hip_atomic_store(flags + chunk, 1u + xcc_id(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return;
-  }
-  if (g >= g1) return;
-  const uint32_t w = (r - 1) * CODE_WAVES + wv;  // wave of the group: chunk 4g + w / Cb, column w % Cb
-  const uint32_t cq = w / Cb, c = w - cq * Cb;
-  const int64_t chunk = (int64_t)g * CODE_WAVES + cq;
-  if (chunk >= L.nchunks) return;
-  const uint32_t dd = reinterpret_cast<const uint32_t*>(bc.desc)[c >> 1];
-  const uint32_t d = (c & 1u) ? dd >> 16 : dd & 0xFFFFu;
-  if (d == 0xFFFFu) return;
-  const uint32_t want = 1u + xcc_id();
-  uint32_t seen = 0;
-  // first look through the L1 (a flag only goes 0 -> producer id during a launch, and the L1
-  // starts the launch empty, so a non-zero cached value is final); poll the L2 only on a miss
-  seen = __builtin_amdgcn_readfirstlane(*(volatile const uint32_t*)(flags + chunk));
-  int it = 0;
-  for (; !seen && it < FUSE_SPIN; ++it) {
-    seen = __hip_atomic_load(flags + chunk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (seen) break;
-    __builtin_amdgcn_s_sleep(2);
-  }
-#if SA_FUSE_STATS
-  if (lane == 0 && it > 0) {
-    atomicAdd(&fuse_stats[0], 1ull);
-    atomicAdd(&fuse_stats[3], (unsigned long long)it);
-  }
-#endif
-  seen = __builtin_amdgcn_readfirstlane(seen);
-#if SA_FUSE_STATS
-  if (lane == 0) {
-    if (seen != want) atomicAdd(&fuse_stats[1], 1ull);
-    if (seen && seen != want) atomicAdd(&fuse_stats[2], 1ull);
-  }
-#endif
-  if (seen != want) {
-    // no producer on this XCD in time: write the chunk's codes from this wave (the same bytes
-    // any producer writes, so the race is benign) and read them back from this XCD's L2
-    codes_for_chunk<ATOMIC, EXPLICIT>(args, chunk, team_lds[wv], codes);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  const int64_t row0 = chunk * BOOL_TILE;
-  if (row0 + lane * LANE_ACTS >= n) return;
-  const uint32_t slot = d >> 8, v = d & 0xFFu, kind = slot % CODE_SLOTS;
-  // plain load: this CU's L1 cannot hold a stale copy -- a chunk's code lines are read only
-  // after its flag showed the producer done (or after this wave wrote them itself)
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-  const u32x4 xw = *reinterpret_cast<const u32x4*>(codes + (chunk * bc.slots + slot) * BOOL_TILE +
-                                                   lane * LANE_ACTS);
-  u32x4 m;
-  if (kind == CS_TEAM) {
-    m = xw;
-  } else if (ATOMIC && kind == CS_TYPE) {
-    m = eq16(xw, v <= 23 ? v : v + 1);
-    if (v == 10) m |= eq16(xw, AT_INTERCEPTION2);
-  } else {
-    m = eq16(xw, v);
-  }
-  const int64_t R = args.Rb;
-  const uint32_t t = bc.chunks_per_tile ? (uint32_t)chunk / (uint32_t)bc.chunks_per_tile : 0u;
-  st16(args.bout + (int64_t)t * Cb * R + (int64_t)c * R + (row0 - (int64_t)t * R) + lane * LANE_ACTS, m);
 }
 
 // ------------------------------------------------------------------------------ f64/i64 block
@@ -1856,27 +1462,6 @@ __global__ __launch_bounds__(256) void formula_kernel(sa_actions A, const T* __r
 // ================================== C ABI =================================================
 using namespace sa;
 
-// Scratch of the bool pre-pass comes from the device's default stream-ordered pool
-// (hipMallocAsync / hipFreeAsync on the launch stream: no host sync, safe across streams);
-// the pool keeps its memory between calls instead of unmapping it at every synchronisation.
-static int codes_pool_init() {
-  static std::mutex mu;
-  static bool done[64] = {};
-  int dev = 0;
-  int rc = check_hip(hipGetDevice(&dev), "hipGetDevice");
-  if (rc || dev < 0 || dev >= 64) return rc;
-  std::lock_guard<std::mutex> lk(mu);
-  if (done[dev]) return SA_OK;
-  hipMemPool_t pool;
-  if ((rc = check_hip(hipDeviceGetDefaultMemPool(&pool, dev), "hipDeviceGetDefaultMemPool"))) return rc;
-  uint64_t keep = UINT64_MAX;
-  if ((rc = check_hip(hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep),
-                      "hipMemPoolSetAttribute")))
-    return rc;
-  done[dev] = true;
-  return SA_OK;
-}
-
 static int check_actions(const sa_actions* a, bool allow_explicit) {
   if (!a) return fail(SA_EINVAL, "null sa_actions");
   if (a->n < 0) return fail(SA_EINVAL, "n < 0");
@@ -1969,123 +1554,7 @@ extern "C" int sa_vaep_features(const sa_actions* a, const sa_feature_plan* plan
   const dim3 grid(xcd_grid((a->n + BLOCK_ACTS - 1) / BLOCK_ACTS)), block(BLOCK_WAVES * WAVE);
   const dim3 bgrid((unsigned)((a->n + BOOL_BLOCK_ACTS - 1) / BOOL_BLOCK_ACTS));
   const bool expl = a->n_frames > 1;
-  if (wb && SA_BOOL_MODE >= 3) {  // window codes, then one wave per (1024-row chunk, column(s))
-    const int64_t chunks = (a->n + BOOL_TILE - 1) / BOOL_TILE;
-    const int64_t waves = chunks * args.Cb;
-    if (waves >= ((int64_t)1 << 32)) return fail(SA_EINVAL, "bool block too large (%lld column chunks)",
-                                                 (long long)waves);
-    if (args.Cb > SA_MAX_BOOL_COLS + 1) return fail(SA_EINVAL, "bool block has too many columns");
-    BoolCols bc;
-    bc.slots = CODE_SLOTS * K;
-    bc.chunks_per_tile = bool_out->tile_rows % BOOL_TILE == 0 ? (int)(bool_out->tile_rows / BOOL_TILE) : 0;
-    for (int c = 0; c <= SA_MAX_BOOL_COLS; ++c) bc.desc[c] = 0xFFFFu;
-    const int ntypes = a->atomic ? N_ATOMIC_NAMES : N_TYPES;
-    auto add = [&](int xfn, int width, int nwin, int win0, int slot) {
-      const int base = plan->bool_col[xfn];
-      if (base < 0) return;
-      for (int i = 0; i < nwin; ++i)
-        for (int v = 0; v < width; ++v)
-          if (base + i * width + v < args.Cb)
-            bc.desc[base + i * width + v] = (uint16_t)((((win0 + i) * CODE_SLOTS + slot) << 8) | v);
-    };
-    add(SA_XFN_ACTIONTYPE_ONEHOT, ntypes, K, 0, CS_TYPE);
-    if (!a->atomic) {
-      add(SA_XFN_RESULT_ONEHOT, N_RESULTS, K, 0, CS_RESULT);
-      add(SA_XFN_ACTIONTYPE_RESULT_ONEHOT, N_TYPES * N_RESULTS, K, 0, CS_TR);
-    }
-    add(SA_XFN_BODYPART_ONEHOT, N_BODYPARTS, K, 0, CS_BP);
-    add(SA_XFN_TEAM, 1, K - 1, 1, CS_TEAM);
-    uint8_t* codes = nullptr;
-    if ((rc = codes_pool_init())) return rc;
-    if ((rc = check_hip(hipMallocAsync((void**)&codes, (size_t)(chunks * bc.slots * BOOL_TILE), st),
-                        "hipMallocAsync(bool window codes)")))
-      return rc;
-    const dim3 kgrid((unsigned)((chunks + CODE_WAVES - 1) / CODE_WAVES)), kblock(WAVE * CODE_WAVES);
-    if (SA_BOOL_MODE == 5) {  // codes pass, then one wave per (chunk, column) on a 2-D grid
-      if (chunks > 65535 * 1024ll) return fail(SA_EINVAL, "too many rows for the 2-D bool grid");
-      if (a->atomic) {
-        if (expl)
-          hipLaunchKernelGGL((bool_codes_kernel<true, true>), kgrid, kblock, 0, st, args, codes);
-        else
-          hipLaunchKernelGGL((bool_codes_kernel<true, false>), kgrid, kblock, 0, st, args, codes);
-      } else {
-        if (expl)
-          hipLaunchKernelGGL((bool_codes_kernel<false, true>), kgrid, kblock, 0, st, args, codes);
-        else
-          hipLaunchKernelGGL((bool_codes_kernel<false, false>), kgrid, kblock, 0, st, args, codes);
-      }
-      rc = check_launch("bool_codes_kernel");
-      const dim3 g2((unsigned)((args.Cb + CODE_WAVES - 1) / CODE_WAVES), (unsigned)chunks);
-      if (!rc) {
-        if (a->atomic)
-          hipLaunchKernelGGL((bool_col1_kernel<true>), g2, kblock, 0, st, args, codes, bc);
-        else
-          hipLaunchKernelGGL((bool_col1_kernel<false>), g2, kblock, 0, st, args, codes, bc);
-        rc = check_launch("bool_col1_kernel");
-      }
-      const int frc = check_hip(hipFreeAsync(codes, st), "hipFreeAsync(bool window codes)");
-      if (rc || (rc = frc)) return rc;
-    } else if (SA_BOOL_MODE == 4) {  // producers and consumers in one launch
-      FuseLayout L;
-      L.nchunks = chunks;
-      L.ngroups = (int32_t)((chunks + CODE_WAVES - 1) / CODE_WAVES);
-      L.gpx = (L.ngroups + 7) / 8;
-      const int64_t per_xcd = FUSE_AHEAD + (int64_t)L.gpx * (args.Cb + 1);
-      uint32_t* flags = nullptr;
-      if ((rc = check_hip(hipMallocAsync((void**)&flags, (size_t)chunks * 4, st), "hipMallocAsync(flags)")) ||
-          (rc = check_hip(hipMemsetAsync(flags, 0, (size_t)chunks * 4, st), "hipMemsetAsync(flags)"))) {
-        (void)hipFreeAsync(codes, st);
-        return rc;
-      }
-      const dim3 fgrid((unsigned)(8 * per_xcd));
-      if (a->atomic) {
-        if (expl)
-          hipLaunchKernelGGL((bool_fused_kernel<true, true>), fgrid, kblock, 0, st, args, codes, flags, bc, L);
-        else
-          hipLaunchKernelGGL((bool_fused_kernel<true, false>), fgrid, kblock, 0, st, args, codes, flags, bc, L);
-      } else {
-        if (expl)
-          hipLaunchKernelGGL((bool_fused_kernel<false, true>), fgrid, kblock, 0, st, args, codes, flags, bc, L);
-        else
-          hipLaunchKernelGGL((bool_fused_kernel<false, false>), fgrid, kblock, 0, st, args, codes, flags, bc, L);
-      }
-      rc = check_launch("bool_fused_kernel");
-      const int frc = check_hip(hipFreeAsync(flags, st), "hipFreeAsync(flags)");
-      const int frc2 = check_hip(hipFreeAsync(codes, st), "hipFreeAsync(bool window codes)");
-      if (rc || (rc = frc) || (rc = frc2)) return rc;
-    } else {
-    const int G = SA_BOOL_G_COLS;
-    const int64_t gwaves = chunks * ((args.Cb + G - 1) / G);
-    const dim3 cgrid(xcd_grid((gwaves + CODE_WAVES - 1) / CODE_WAVES));
-    if (a->atomic) {
-      if (expl)
-        hipLaunchKernelGGL((bool_codes_kernel<true, true>), kgrid, kblock, 0, st, args, codes);
-      else
-        hipLaunchKernelGGL((bool_codes_kernel<true, false>), kgrid, kblock, 0, st, args, codes);
-    } else {
-      if (expl)
-        hipLaunchKernelGGL((bool_codes_kernel<false, true>), kgrid, kblock, 0, st, args, codes);
-      else
-        hipLaunchKernelGGL((bool_codes_kernel<false, false>), kgrid, kblock, 0, st, args, codes);
-    }
-    rc = check_launch("bool_codes_kernel");
-    if (!rc) {
-#define SA_COL_LAUNCH(GG)                                                                    \
-  if (a->atomic)                                                                             \
-    hipLaunchKernelGGL((bool_col_kernel<true, GG>), cgrid, kblock, 0, st, args, codes, bc);  \
-  else                                                                                       \
-    hipLaunchKernelGGL((bool_col_kernel<false, GG>), cgrid, kblock, 0, st, args, codes, bc);
-      if (G == 1) { SA_COL_LAUNCH(1) }
-      else if (G == 2) { SA_COL_LAUNCH(2) }
-      else if (G == 8) { SA_COL_LAUNCH(8) }
-      else { SA_COL_LAUNCH(4) }
-#undef SA_COL_LAUNCH
-      rc = check_launch("bool_col_kernel");
-    }
-    const int frc = check_hip(hipFreeAsync(codes, st), "hipFreeAsync(bool window codes)");
-    if (rc || (rc = frc)) return rc;
-    }
-  } else if (wb && SA_BOOL_MODE == 2) {  // one wave per (tile, group of ~32 columns)
+  if (wb && SA_BOOL_MODE == 2) {  // one wave per (tile, group of ~32 columns)
     const int ng = (int)((args.Cb + SA_CG_COLS - 1) / SA_CG_COLS);
     const int gc = (int)((args.Cb + ng - 1) / ng);
     const int64_t waves = (a->n + BOOL_TILE - 1) / BOOL_TILE * ng;
@@ -2239,15 +1708,3 @@ extern "C" int sa_vaep_formula_f32(const sa_actions* a, const float* p_scores, c
                                    float* off, float* def, float* val, void* stream) {
   return launch_formula<float>(a, p_scores, p_concedes, off, def, val, stream);
 }
-
-#if SA_FUSE_STATS
-extern "C" int sa_debug_fuse_stats(unsigned long long* out, int reset) {
-  int rc = check_hip(hipMemcpyFromSymbol(out, HIP_SYMBOL(sa::fuse_stats), sizeof(unsigned long long) * 4),
-                     "fuse_stats");
-  if (!rc && reset) {
-    const unsigned long long z[4] = {0, 0, 0, 0};
-    rc = check_hip(hipMemcpyToSymbol(HIP_SYMBOL(sa::fuse_stats), z, sizeof(z)), "fuse_stats reset");
-  }
-  return rc;
-}
-#endif
