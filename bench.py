@@ -292,6 +292,9 @@ def main() -> None:
                          'slower per step, profiles/r01g_xt_fork_ab.log)')
     ap.add_argument('--bool-tile', type=int, default=1024,
                     help='rows per bool-block tile (0 = one tile: plain column-major)')
+    ap.add_argument('--aux', type=int, default=0,
+                    help='run the last A VAEP kernels (goalscore, labels, formula) on a third '
+                         'stream next to the feature kernels (0: all on the main stream)')
     ap.add_argument('--num-tile', type=int, default=128,
                     help='rows per f64/i64-block tile (0 = one tile: plain column-major)')
     args = ap.parse_args()
@@ -335,47 +338,57 @@ def main() -> None:
              lambda: ops.formula(ab, ps, pc, val))
     main_s = torch.cuda.current_stream()
     side = torch.cuda.Stream() if not args.serial else main_s
+    aux = torch.cuda.Stream() if args.aux > 0 and not args.serial else None
+    nv = len(calls)
+    n_main = nv - (args.aux if aux is not None else 0)  # calls[n_main:] run on `aux`
 
     def step(ev=None):
         # default: the xT fit runs on a side stream next to the VAEP kernels -- the first
         # `xt_fork` VAEP kernels are enqueued, then the side stream forks for the count pass and
         # RCCL all-reduce, then the remaining VAEP kernels, then the solve (a single workgroup
         # that would otherwise leave the GPU idle, and a host sync of the side stream) and the
-        # rate. --serial: xT after the VAEP kernels on the one stream.
-        nv = len(calls)
+        # rate. --aux A: the last A VAEP kernels (goalscore / labels / formula: latency-bound
+        # scans and look-aheads) run on a third stream next to the feature kernels.
+        # --serial: everything on the one stream.  ev[i] = (start, end) of call i on its stream.
         overlap = side is not main_s
+        if aux is not None:
+            fork_a = torch.cuda.Event()
+            fork_a.record(main_s)
+            aux.wait_event(fork_a)
         for i, call in enumerate(calls):
-            if overlap and i == min(args.xt_fork, nv - 1):
+            st = main_s if i < n_main else aux
+            if overlap and i == min(args.xt_fork, n_main - 1):
                 fork = torch.cuda.Event()
                 fork.record(main_s)
                 side.wait_event(fork)
                 with torch.cuda.stream(side):
                     if ev is not None:
-                        ev[nv + 1].record(side)
+                        ev[nv][0].record(side)
                     xt_start()
-            if ev is not None:
-                ev[i].record(main_s)
-            call()
-        if ev is not None:
-            ev[nv].record(main_s)
+            with torch.cuda.stream(st):
+                if ev is not None:
+                    ev[i][0].record(st)
+                call()
+                if ev is not None:
+                    ev[i][1].record(st)
         if not overlap:
             if ev is not None:
-                ev[nv + 1].record(main_s)
+                ev[nv][0].record(main_s)
             xt_start()
         with torch.cuda.stream(side):
             xt_finish()
             if ev is not None:
-                ev[nv + 2].record(side)
-        if overlap:
+                ev[nv][1].record(side)
+        for other in ((side,) if overlap else ()) + ((aux,) if aux is not None else ()):
             join = torch.cuda.Event()
-            join.record(side)
+            join.record(other)
             main_s.wait_event(join)
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(len(calls) + 3)]
-           for _ in range(args.steps)]
+    evs = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            for _ in range(nv + 1)] for _ in range(args.steps)]
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -386,10 +399,9 @@ def main() -> None:
     if dist:
         dist.barrier()
     wall = time.perf_counter() - t0
-    nv = len(calls)
-    kern = {name: float(np.mean([e[i].elapsed_time(e[i + 1]) for e in evs]))
+    kern = {name: float(np.mean([e[i][0].elapsed_time(e[i][1]) for e in evs]))
             for i, name in enumerate(KERNELS[:nv])}
-    kern['xt_fit_rate'] = float(np.mean([e[nv + 1].elapsed_time(e[nv + 2]) for e in evs]))
+    kern['xt_fit_rate'] = float(np.mean([e[nv][0].elapsed_time(e[nv][1]) for e in evs]))
     total_actions = n
     if dist:
         wall = _reduce(dist, wall, dist.ReduceOp.MAX, dev)
@@ -448,6 +460,10 @@ def main() -> None:
                        'stream': 'main (serial)' if args.serial else
                        f'side stream, forked after {args.xt_fork} VAEP kernel(s), overlapped '
                        'with the rest'}
+    line['streams'] = ('one stream' if args.serial else
+                       f'VAEP feature kernels on the main stream, xT on a side stream'
+                       + (f', {", ".join(KERNELS[n_main:nv])} on a third stream'
+                          if aux is not None else ''))
     line.update(extra_side)
     if not args.no_cpu and world == 1:  # the CPU comparator runs on rank 0 at N = 1 only
         line['cpu_baseline'] = cpu_baseline(d, args.cpu_seconds)

@@ -18,6 +18,9 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
 
 #include "sa_common.h"
 #include "sa_internal.h"
@@ -719,6 +722,152 @@ __global__ __launch_bounds__(64 * CG_WAVES) void bool_colgroup_kernel(FeatArgs a
       st_bool16(bb, tc, R, m[0], m[1], m[2], m[3]);
     }
   }
+}
+
+// Staged form: short workgroups that each write NW * G consecutive 1-KiB column chunks of one
+// 1024-row tile and exit.  The pure-store probes (profiles/r01g_store_runlen.md) run that shape
+// at 7.2 - 7.4 TB/s on every allocation, where the column-group shape (one 31-KiB run per
+// wave) spreads 5.7 - 7.1 TB/s with the placement; what it costs is a per-workgroup prologue,
+// so that prologue is one cheap LDS pass:
+//  1. raw ids + team codes of rows tile0-8 .. tile0+1023 -> LDS (coalesced), segment starts
+//     inside that window -> LDS flags (rows >= n are flagged too, so their windows stay on
+//     the row itself, as in the other forms);
+//  2. each thread builds 4 consecutive rows' window codes -- per window i: type (atomic: the
+//     column index of its name), result, type*6+result, bodypart, team[a_i]==team[a0] -- as
+//     byte rows of 1024 in LDS (window i = window i-1's row - 1 unless that row starts a
+//     segment: vaep/features.py:83-88);
+//  3. wave w writes columns c0 + s*NW + w (s < G): one ds_read_b128 of the column's code row
+//     per lane, a SWAR compare with the column's value, one 16-B store.
+// Windowed mode only (EXPLICIT frames use the column-group kernel).
+struct StagedCfg {
+  int nw, g;  // waves per workgroup, columns per wave
+};
+
+__device__ __forceinline__ bool staged_col(int c, int base, int nv, int K, int& i, int& v) {
+  if (base < 0 || c < base || c >= base + K * nv) return false;
+  i = (c - base) / nv;
+  v = c - base - i * nv;
+  return true;
+}
+
+template <bool ATOMIC>
+__global__ __launch_bounds__(1024) void bool_staged_kernel(FeatArgs args, int ncg, int nw, int g,
+                                                           int64_t n_logical) {
+  extern __shared__ __align__(16) uint8_t lds[];
+  const int K = args.p.nb_prev_actions;
+  constexpr int H = 8, W = BOOL_TILE + H;  // halo rows + window rows
+  uint8_t* typ = lds;                       // [W]
+  uint8_t* res = typ + W;                   // [W]
+  uint8_t* bpt = res + W;                   // [W]
+  uint8_t* flg = bpt + W;                   // [W] row starts a segment (or is >= n)
+  int32_t* tea = (int32_t*)(lds + ((4 * W + 15) & ~15));  // [W]
+  uint8_t* code = (uint8_t*)(tea + W);      // [(5K-1) x 1024]
+  const int64_t L = xcd_logical_block();
+  if (L >= n_logical) return;
+  const sa_actions& A = args.a;
+  const sa_feature_plan& P = args.p;
+  const int64_t n = A.n;
+  const int64_t chunk = L / ncg;
+  const int cg = (int)(L - chunk * ncg);
+  const int64_t tile0 = chunk * BOOL_TILE, h0 = tile0 - H;
+  const sa_frame& F0 = A.frames[0];
+  const int nt = nw * WAVE, t = threadIdx.x;
+  for (int k = t; k < W; k += nt) {
+    const int64_t j = h0 + k;
+    typ[k] = ld_or0(F0.type_id, j, n);
+    res[k] = ATOMIC ? 0 : ld_or0(F0.result_id, j, n);
+    bpt[k] = ld_or0(F0.bodypart_id, j, n);
+    tea[k] = ld_or0(F0.team, j, n);
+    flg[k] = j >= n;
+  }
+  __syncthreads();
+  if (K > 1) {  // segment starts inside [h0, tile0 + 1024)
+    const int64_t g0 = find_segment(A.seg_off, A.n_segments, h0 > 0 ? h0 : 0);
+    for (int64_t s = g0 + t; s < A.n_segments; s += nt) {
+      const int64_t st = A.seg_off[s];
+      if (st >= tile0 + BOOL_TILE) break;
+      if (st >= h0) flg[st - h0] = 1;
+    }
+    __syncthreads();
+  }
+  if (t < BOOL_TILE / 4) {
+    for (int i = 0; i < K; ++i) {
+      uint32_t wt = 0, wr = 0, wc = 0, wb = 0, ws = 0;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const int k0 = H + 4 * t + m;
+        int src = k0;  // window i of row k0: step back while the current row is no segment start
+        for (int s = 0; s < i && !flg[src]; ++s) --src;
+        uint32_t ty = typ[src];
+        if (ATOMIC) ty = ty < AT_INTERCEPTION2 ? ty : (ty == AT_INTERCEPTION2 ? 10u : ty - 1u);
+        const uint32_t re = res[src];
+        wt |= ty << (8 * m);
+        wr |= re << (8 * m);
+        wc |= (ty * N_RESULTS + re) << (8 * m);
+        wb |= (uint32_t)bpt[src] << (8 * m);
+        ws |= (uint32_t)(tea[src] == tea[k0]) << (8 * m);
+      }
+      uint32_t* cw = (uint32_t*)code;
+      cw[(0 * K + i) * 256 + t] = wt;
+      cw[(1 * K + i) * 256 + t] = wr;
+      cw[(2 * K + i) * 256 + t] = wc;
+      cw[(3 * K + i) * 256 + t] = wb;
+      if (i > 0) cw[(4 * K + i - 1) * 256 + t] = ws;
+    }
+  }
+  __syncthreads();
+  const int lane = t & (WAVE - 1), wv = t / WAVE;
+  const int64_t j0 = tile0 + (int64_t)lane * LANE_ACTS;
+  if (j0 >= n) return;
+  uint8_t* bb = args.bout + tile_off(j0, 0, args.Cb, args.Rb);
+  const int ntypes = ATOMIC ? N_ATOMIC_NAMES : N_TYPES;
+  const int c_type = P.bool_col[SA_XFN_ACTIONTYPE_ONEHOT];
+  const int c_res = ATOMIC ? -1 : P.bool_col[SA_XFN_RESULT_ONEHOT];
+  const int c_tr = ATOMIC ? -1 : P.bool_col[SA_XFN_ACTIONTYPE_RESULT_ONEHOT];
+  const int c_bp = P.bool_col[SA_XFN_BODYPART_ONEHOT];
+  const int tcol = P.bool_col[SA_XFN_TEAM];
+  const int cbase = cg * nw * g + wv;
+  for (int s = 0; s < g; ++s) {
+    const int c = cbase + s * nw;
+    if (c >= args.Cb) break;
+    int i, v, row;
+    if (staged_col(c, c_type, ntypes, K, i, v))
+      row = i;
+    else if (staged_col(c, c_res, N_RESULTS, K, i, v))
+      row = K + i;
+    else if (staged_col(c, c_tr, N_TYPES * N_RESULTS, K, i, v))
+      row = 2 * K + i;
+    else if (staged_col(c, c_bp, N_BODYPARTS, K, i, v))
+      row = 3 * K + i;
+    else if (staged_col(c, tcol, 1, K - 1, i, v)) {
+      row = 4 * K + i;
+      v = 1;
+    } else
+      continue;  // not a column of this plan
+    const u32x4 x = *(const u32x4*)(code + row * BOOL_TILE + lane * LANE_ACTS);
+    st_bool16(bb, c, args.Rb, bytes_eq(x[0], v), bytes_eq(x[1], v), bytes_eq(x[2], v),
+              bytes_eq(x[3], v));
+  }
+}
+
+static size_t staged_lds_bytes(int K) {
+  constexpr int W = BOOL_TILE + 8;
+  return (size_t)((4 * W + 15) & ~15) + 4 * W + (size_t)(5 * K - 1) * BOOL_TILE;
+}
+
+// SA_BOOL_KERNEL = "colgroup" (default) or "staged[:NW[:G]]", read at each launch (A/B runs
+// switch it between calls in one process, on the same allocations)
+static StagedCfg bool_kernel_choice() {
+  StagedCfg c{0, 0};
+  const char* e = getenv("SA_BOOL_KERNEL");
+  if (e && strncmp(e, "staged", 6) == 0) {
+    c.nw = 4;
+    c.g = 4;
+    int nw = 0, g = 0;
+    if (sscanf(e + 6, ":%d:%d", &nw, &g) >= 1 && nw >= 1 && nw <= 16) c.nw = nw;
+    if (g >= 1 && g <= 64) c.g = g;
+  }
+  return c;
 }
 
 // ------------------------------------------------------------------------------ f64/i64 block
@@ -1554,7 +1703,22 @@ extern "C" int sa_vaep_features(const sa_actions* a, const sa_feature_plan* plan
   const dim3 grid(xcd_grid((a->n + BLOCK_ACTS - 1) / BLOCK_ACTS)), block(BLOCK_WAVES * WAVE);
   const dim3 bgrid((unsigned)((a->n + BOOL_BLOCK_ACTS - 1) / BOOL_BLOCK_ACTS));
   const bool expl = a->n_frames > 1;
-  if (wb && SA_BOOL_MODE == 2) {  // one wave per (tile, group of ~32 columns)
+  const StagedCfg scfg = bool_kernel_choice();
+  if (wb && scfg.nw > 0 && !expl) {  // short workgroups, window codes staged in LDS
+    const int per = scfg.nw * scfg.g;
+    const int ncg = (int)((args.Cb + per - 1) / per);
+    const int64_t nl = (a->n + BOOL_TILE - 1) / BOOL_TILE * ncg;
+    const dim3 sgrid(xcd_grid(nl)), sblock(WAVE * scfg.nw);
+    const size_t shm = staged_lds_bytes(K);
+    if (a->atomic)
+      hipLaunchKernelGGL((bool_staged_kernel<true>), sgrid, sblock, shm, st, args, ncg, scfg.nw,
+                         scfg.g, nl);
+    else
+      hipLaunchKernelGGL((bool_staged_kernel<false>), sgrid, sblock, shm, st, args, ncg, scfg.nw,
+                         scfg.g, nl);
+    rc = check_launch("bool_staged_kernel");
+    if (rc) return rc;
+  } else if (wb && SA_BOOL_MODE == 2) {  // one wave per (tile, group of ~32 columns)
     const int ng = (int)((args.Cb + SA_CG_COLS - 1) / SA_CG_COLS);
     const int gc = (int)((args.Cb + ng - 1) / ng);
     const int64_t waves = (a->n + BOOL_TILE - 1) / BOOL_TILE * ng;

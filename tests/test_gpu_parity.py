@@ -136,6 +136,42 @@ def test_tiled_and_plain_layouts_agree(sa):
         ops.features(ab, vo.SPADL_DEFAULT, 3, num_tile=100)
 
 
+@pytest.mark.parametrize('atomic', [False, True])
+def test_staged_bool_kernel_matches_colgroup(sa, atomic, monkeypatch):
+    """The opt-in staged bool kernel (SA_BOOL_KERNEL=staged:NW:G, short workgroups with the
+    window codes in LDS) writes the column-group kernel's block byte for byte: games of 1..40
+    actions (many segment starts per 1024-row chunk) and full games, k = 1..5, both layouts."""
+    B, ops, syn = sa['batch'], sa['ops'], sa['synthetic']
+    default = vo.ATOMIC_DEFAULT if atomic else vo.SPADL_DEFAULT
+    gen = syn.atomic_games if atomic else syn.spadl_games
+    d = gen(6, seed=11)
+    n0 = int(d['game_off'][-1])
+    rng = np.random.default_rng(5)
+    sizes = rng.integers(1, 41, 300)  # 300 small games appended (rows copied from the start)
+    m = int(sizes.sum())
+    rows = {c: v for c, v in d.items() if isinstance(v, np.ndarray) and v.shape == (n0,)}
+    d2 = {c: np.concatenate([v, v[:m]]) for c, v in rows.items()}
+    offs = n0 + np.concatenate([[0], np.cumsum(sizes)])
+    d2['game_off'] = np.concatenate([d['game_off'], offs[1:]])
+    d2['home_team_id'] = np.concatenate([d['home_team_id'], d2['team_id'][offs[:-1]]])
+    ab = B.ActionBatch.from_columns(d2, atomic=atomic)
+    assert ab.n_segments > 300
+    for k in (1, 2, 3, 5):
+        for Rb in (1024, None):
+            monkeypatch.delenv('SA_BOOL_KERNEL', raising=False)
+            ref = ops.features(ab, default, k, bool_tile=Rb).bool_block.cpu()
+            for v in ('staged:4:4', 'staged:16:1', 'staged:8:3'):
+                monkeypatch.setenv('SA_BOOL_KERNEL', v)
+                got = ops.features(ab, default, k, bool_tile=Rb).bool_block.cpu()
+                n = ab.n
+                if Rb is None:
+                    assert torch.equal(got[:, :, :n], ref[:, :, :n]), (k, v)
+                else:
+                    gf = got.permute(1, 0, 2).reshape(got.shape[1], -1)[:, :n]
+                    rf = ref.permute(1, 0, 2).reshape(ref.shape[1], -1)[:, :n]
+                    assert torch.equal(gf, rf), (k, v, Rb)
+
+
 def test_explicit_frames_match_windowed(sa):
     """Explicit-frame mode (module-level transformers) == windowed mode on the same states."""
     B, ops = sa['batch'], sa['ops']
