@@ -44,7 +44,7 @@ BYTES = {'bool_features': 7 + 515,             # type/result/bodypart u8 + team 
 KERNELS = ('bool_features', 'num_features', 'goalscore', 'labels', 'formula', 'xt_fit_rate')
 # the HIP kernel each step entry launches (socceraction_amd/csrc/sa_vaep.hip)
 KERNEL_NAMES = {'bool_features': 'bool_colgroup_kernel', 'num_features': 'num_features_kernel',
-                'goalscore': 'goalscore_wave_kernel', 'labels': 'labels_kernel',
+                'goalscore': 'goalscore_wave16_kernel', 'labels': 'labels_kernel',
                 'formula': 'formula_kernel',
                 'xt_fit_rate': 'xt_count_kernel + xt_solve_small_kernel + xt_rate_kernel'}
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)

@@ -855,6 +855,12 @@ static size_t staged_lds_bytes(int K) {
   return (size_t)((4 * W + 15) & ~15) + 4 * W + (size_t)(5 * K - 1) * BOOL_TILE;
 }
 
+// Run-time A/B switches of the launchers (read at each launch)
+static bool env_is(const char* var, const char* val) {
+  const char* e = getenv(var);
+  return e && strcmp(e, val) == 0;
+}
+
 // SA_BOOL_KERNEL = "colgroup" (default) or "staged[:NW[:G]]", read at each launch (A/B runs
 // switch it between calls in one process, on the same allocations)
 static StagedCfg bool_kernel_choice() {
@@ -1358,13 +1364,139 @@ __global__ __launch_bounds__(256) void goalscore_wave_kernel(sa_actions A, int64
   }
 }
 
+// 16-rows-per-lane form: passes of 1024 rows, so a ~1,600-row game is 2 passes instead of 13
+// and each pass issues all of its loads at once (16 type + 16 result bytes, 64 B of team codes
+// per lane; the next pass's loads go out before this pass is scanned).  A lane sums its 16
+// (goals A, goals B) increments as one packed u64, the wave scans the 64 lane totals, and the
+// lane then walks its rows with the exclusive count: 8 i64x2 stores per column per lane.
+struct Gs16In {
+  u32x4 ty, rs;
+  int32_t tm[16];
+};
+
+template <bool ATOMIC>
+__device__ __forceinline__ void gs16_load(const sa_frame& F, int64_t j0, int64_t n, Gs16In& v) {
+  if (j0 >= 0 && j0 + 16 <= n) {
+    v.ty = *reinterpret_cast<const u32x4*>(F.type_id + j0);
+    v.rs = ATOMIC ? u32x4{0, 0, 0, 0} : *reinterpret_cast<const u32x4*>(F.result_id + j0);
+    const int4* tp = reinterpret_cast<const int4*>(F.team + j0);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int4 t = tp[q];
+      v.tm[4 * q] = t.x;
+      v.tm[4 * q + 1] = t.y;
+      v.tm[4 * q + 2] = t.z;
+      v.tm[4 * q + 3] = t.w;
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      v.ty[q] = ld_u8x4(F.type_id, j0 / 4 + q, n);
+      v.rs[q] = ATOMIC ? 0u : ld_u8x4(F.result_id, j0 / 4 + q, n);
+    }
+#pragma unroll
+    for (int m = 0; m < 16; ++m) v.tm[m] = ld_or0(F.team, j0 + m, n);
+  }
+}
+
+constexpr int GS_LDS_PITCH = 18;  // i64 per lane: 16 rows + pad (144 B: 16-B aligned)
+
+__device__ __forceinline__ void wave_sync() {  // LDS hand-off between the lanes of one wave
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <bool ATOMIC>
+__global__ __launch_bounds__(256) void goalscore_wave16_kernel(sa_actions A,
+                                                               int64_t* __restrict__ block,
+                                                               int64_t C, int64_t col, int64_t R) {
+  __shared__ __align__(16) int64_t gs_lds[4][WAVE * GS_LDS_PITCH];
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int64_t g = (int64_t)blockIdx.x * (blockDim.x / WAVE) + threadIdx.x / WAVE;
+  if (g >= A.n_segments) return;
+  const int64_t s = A.seg_off[g], e = A.seg_off[g + 1];
+  if (s >= e) return;
+  const int64_t n = A.n;
+  const sa_frame& F = A.frames[0];
+  const int32_t teamA = F.team[s];
+  const int64_t base0 = s & ~(int64_t)127;  // 128-row aligned: whole 1-KiB column runs  // 16-row aligned: vector loads, whole 16-row runs
+  uint64_t carry = 0;  // low 32 bits: goals of team A before this pass; high: team B
+  Gs16In cur, nxt;
+  gs16_load<ATOMIC>(F, base0 + 16 * lane, n, cur);
+  for (int64_t base = base0; base < e; base += 16 * WAVE) {
+    const int64_t j0 = base + 16 * lane;
+    if (base + 16 * WAVE < e) gs16_load<ATOMIC>(F, j0 + 16 * WAVE, n, nxt);
+    uint32_t gm = 0, om = 0, am = 0;  // goal / owngoal / team-A row bits (valid rows only)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      uint32_t gb, ob;
+      goal_bytes(cur.ty[q], cur.rs[q], ATOMIC, gb, ob);
+      gm |= pack4(gb) << (4 * q);
+      om |= pack4(ob) << (4 * q);
+    }
+#pragma unroll
+    for (int m = 0; m < 16; ++m) am |= (uint32_t)(cur.tm[m] == teamA) << m;
+    const int lo = s > j0 ? (int)(s - j0) : 0;                // first valid row of the lane
+    const int hi = e < j0 + 16 ? (int)(e - j0) : 16;           // one past the last
+    const uint32_t vm = lo >= hi ? 0u : (0xFFFFu >> (16 - (hi - lo))) << lo;
+    const uint32_t gA = ((gm & am) | (om & ~am)) & vm, gB = ((gm & ~am) | (om & am)) & vm;
+    const uint64_t x = (uint64_t)__popc(gA) | ((uint64_t)__popc(gB) << 32);
+    uint64_t incl = x;
+#pragma unroll
+    for (int off = 1; off < WAVE; off <<= 1) {
+      const uint64_t y = __shfl_up(incl, off, WAVE);
+      if (lane >= off) incl += y;
+    }
+    const uint64_t ex = carry + incl - x;  // goals before row j0
+    carry += __shfl(incl, WAVE - 1, WAVE);
+    // the lane's 16 rows -> LDS one column at a time, then back out in pass-of-128 order
+    // (lane l: rows 2l, 2l+1 of each 128-row run), so every store instruction writes 1 KiB
+    // contiguous of one column (the lane's own 128-B run per instruction was 2.3x slower)
+    const int64_t cA0 = (int64_t)(ex & 0xFFFFFFFFull), cB0 = (int64_t)(ex >> 32);
+    int64_t* xl = gs_lds[threadIdx.x / WAVE];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      wave_sync();
+#pragma unroll
+      for (int m = 0; m < 16; m += 2) {
+        int64_t v[2];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const uint32_t below = (1u << (m + q)) - 1u;  // rows of this lane before m+q
+          const int64_t cA = cA0 + __popc(gA & below), cB = cB0 + __popc(gB & below);
+          const bool isA = (am >> (m + q)) & 1;
+          const int64_t tm = isA ? cA : cB, op = isA ? cB : cA;
+          v[q] = k == 0 ? tm : (k == 1 ? op : tm - op);
+        }
+        *reinterpret_cast<i64x2*>(xl + lane * GS_LDS_PITCH + m) = i64x2{(long long)v[0], (long long)v[1]};
+      }
+      wave_sync();
+#pragma unroll
+      for (int p = 0; p < 8; ++p) {
+        const int r = 128 * p + 2 * lane;  // row offset from `base`
+        const int64_t jr = base + r;
+        const i64x2 v = *reinterpret_cast<const i64x2*>(xl + (r / 16) * GS_LDS_PITCH + (r % 16));
+        int64_t* o = block + tile_off(jr, col + k, C, R);
+        if (jr >= s && jr + 1 < e) {
+          st16(o, v);
+        } else {
+          if (jr >= s && jr < e) o[0] = v[0];
+          if (jr + 1 >= s && jr + 1 < e) o[1] = v[1];
+        }
+      }
+    }
+    cur = nxt;
+  }
+}
+
 // ------------------------------------------------------------------------------ labels
 // vaep/labels.py:9-116, atomic/vaep/labels.py:9-107.  A lane owns 16 consecutive actions
 // and holds rows j0 .. j0+31 as goal / owngoal bit masks plus team codes, so a look-ahead of
 // nr_actions <= 17 needs no further loads.  The look-ahead clamps at the segment's last row,
 // which only repeats a row already in the window, so the window is rows j+1 .. min(j+nr-1,
 // last).
-template <bool ATOMIC>
+template <bool ATOMIC, bool WAVESEG>
 __global__ __launch_bounds__(256) void labels_kernel(sa_actions A, int nr, uint8_t* __restrict__ sc,
                                                      uint8_t* __restrict__ co,
                                                      uint8_t* __restrict__ gfs) {
@@ -1409,7 +1541,15 @@ __global__ __launch_bounds__(256) void labels_kernel(sa_actions A, int nr, uint8
   uint32_t e1 = 0;
 #pragma unroll
   for (int r = 0; r < 32; ++r) e1 |= (uint32_t)(tm[r] == t1) << r;
-  SegCursor cur = seg_at(A, j0);
+  SegCursor cur;
+  if (WAVESEG) {
+    // one search per wave (the first active lane's row, uniform: scalar loads), then each lane
+    // advances to its own rows -- a per-lane binary search was ~14 dependent divergent loads
+    const int64_t jw = (int64_t)__builtin_amdgcn_readfirstlane((int)(j0 / LANE_ACTS)) * LANE_ACTS;
+    cur = seg_at(A, jw);
+  } else {
+    cur = seg_at(A, j0);
+  }
   uint32_t s_out[4] = {0, 0, 0, 0}, c_out[4] = {0, 0, 0, 0}, g_out[4] = {0, 0, 0, 0};
 #pragma unroll
   for (int m = 0; m < LANE_ACTS; ++m) {
@@ -1800,8 +1940,17 @@ extern "C" int sa_vaep_goalscore(const sa_actions* a, const sa_block* i64_out, i
   if (a->n == 0) return SA_OK;
   hipStream_t st = (hipStream_t)stream;
   int64_t* blk = (int64_t*)i64_out->data;
-  if (SA_GS_WAVE) {  // one wave per segment, 4 segments per workgroup
-    const dim3 g4((unsigned)((a->n_segments + 3) / 4));
+  const dim3 g4((unsigned)((a->n_segments + 3) / 4));
+  if (!env_is("SA_GS_KERNEL", "wave2")) {  // one wave per segment, passes of 1024 rows
+    if (a->atomic)
+      hipLaunchKernelGGL((goalscore_wave16_kernel<true>), g4, dim3(256), 0, st, *a, blk,
+                         (int64_t)i64_out->n_cols, (int64_t)col, i64_out->tile_rows);
+    else
+      hipLaunchKernelGGL((goalscore_wave16_kernel<false>), g4, dim3(256), 0, st, *a, blk,
+                         (int64_t)i64_out->n_cols, (int64_t)col, i64_out->tile_rows);
+    return check_launch("goalscore_wave16_kernel");
+  }
+  if (SA_GS_WAVE) {  // A/B (SA_GS_KERNEL=wave2): passes of 128 rows, a lane owning 2
     if (a->atomic)
       hipLaunchKernelGGL((goalscore_wave_kernel<true>), g4, dim3(256), 0, st, *a, blk,
                          (int64_t)i64_out->n_cols, (int64_t)col, i64_out->tile_rows);
@@ -1831,12 +1980,23 @@ extern "C" int sa_vaep_labels(const sa_actions* a, int32_t nr_actions, uint8_t* 
   if (a->n == 0) return SA_OK;
   const int64_t lanes = (a->n + LANE_ACTS - 1) / LANE_ACTS;
   const dim3 grid((unsigned)((lanes + 255) / 256)), block(256);
-  if (a->atomic)
-    hipLaunchKernelGGL((labels_kernel<true>), grid, block, 0, (hipStream_t)stream, *a, nr_actions,
-                       scores, concedes, goal_from_shot);
-  else
-    hipLaunchKernelGGL((labels_kernel<false>), grid, block, 0, (hipStream_t)stream, *a, nr_actions,
-                       scores, concedes, goal_from_shot);
+  const bool lane_search = env_is("SA_LABELS_SEARCH", "lane");  // A/B: the per-lane search
+  hipStream_t st = (hipStream_t)stream;
+  if (a->atomic) {
+    if (lane_search)
+      hipLaunchKernelGGL((labels_kernel<true, false>), grid, block, 0, st, *a, nr_actions, scores,
+                         concedes, goal_from_shot);
+    else
+      hipLaunchKernelGGL((labels_kernel<true, true>), grid, block, 0, st, *a, nr_actions, scores,
+                         concedes, goal_from_shot);
+  } else {
+    if (lane_search)
+      hipLaunchKernelGGL((labels_kernel<false, false>), grid, block, 0, st, *a, nr_actions, scores,
+                         concedes, goal_from_shot);
+    else
+      hipLaunchKernelGGL((labels_kernel<false, true>), grid, block, 0, st, *a, nr_actions, scores,
+                         concedes, goal_from_shot);
+  }
   return check_launch("labels_kernel");
 }
 
