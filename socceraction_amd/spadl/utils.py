@@ -36,3 +36,8 @@ def play_left_to_right(actions: pd.DataFrame, home_team_id=None) -> pd.DataFrame
     for col in ('start_y', 'end_y'):
         ltr.loc[away, col] = spadlconfig.field_width - actions.loc[away, col].to_numpy()
     return ltr
+
+
+def play_left_to_right_sa(actions: pd.DataFrame, home_team_id: int) -> pd.DataFrame:
+    """Two-argument form of reference spadl/utils.py:31-57 (away-team rows flipped)."""
+    return play_left_to_right(actions, home_team_id)

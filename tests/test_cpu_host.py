@@ -359,3 +359,17 @@ def test_single_hip_runtime_after_load():
     out = subprocess.run([sys.executable, '-c', code], capture_output=True, text=True,
                          check=True, cwd=os.path.dirname(os.path.dirname(__file__)))
     assert out.stdout.strip().splitlines()[-1] == '1'
+
+
+def test_play_left_to_right_sa_two_argument_form():
+    """spadl/utils.py:31-57: rows of the away team are mirrored, home rows unchanged."""
+    import pandas as pd
+    from socceraction_amd.spadl.utils import play_left_to_right, play_left_to_right_sa
+    df = pd.DataFrame({'team_id': [1, 2, 2], 'start_x': [1., 2., 105.], 'end_x': [3., 4., 0.],
+                       'start_y': [5., 6., 68.], 'end_y': [7., 8., 0.]})
+    out = play_left_to_right_sa(df, 1)
+    assert out.start_x.tolist() == [1., 103., 0.] and out.end_x.tolist() == [3., 101., 105.]
+    assert out.start_y.tolist() == [5., 62., 0.] and out.end_y.tolist() == [7., 60., 68.]
+    assert df.start_x.tolist() == [1., 2., 105.]  # input untouched
+    pd.testing.assert_frame_equal(out, play_left_to_right(df.assign(home_team_id=1)).drop(
+        columns='home_team_id'))
