@@ -292,6 +292,11 @@ def main() -> None:
                          'slower per step, profiles/r01g_xt_fork_ab.log)')
     ap.add_argument('--bool-tile', type=int, default=1024,
                     help='rows per bool-block tile (0 = one tile: plain column-major)')
+    ap.add_argument('--order', default='num_features,bool_features,goalscore,labels,formula',
+                    help='launch order of the VAEP kernels in the step (default measured 1.3 %% '
+                         'faster than bool first, in-process A/B: profiles/r01h_order_ab.log)')
+    ap.add_argument('--ab-orders', default='',
+                    help='dev tool: ";"-separated launch orders timed round-robin in one process')
     ap.add_argument('--aux', type=int, default=0,
                     help='run the last A VAEP kernels (goalscore, labels, formula) on a third '
                          'stream next to the feature kernels (0: all on the main stream)')
@@ -331,18 +336,22 @@ def main() -> None:
     val = torch.empty((3, ld), dtype=torch.float64, device=dev)
     s_act = ab.struct()
     xt_start, xt_finish, xt_last = xt_step(ab, dist)
-    calls = (lambda: ops.features_into(s_act, bool_out),
-             lambda: ops.features_into(s_act, num_out),
-             lambda: ops.goalscore_into(ab, out),
-             lambda: ops.labels(ab, 10, lab),
-             lambda: ops.formula(ab, ps, pc, val))
+    by_name = {'bool_features': lambda: ops.features_into(s_act, bool_out),
+               'num_features': lambda: ops.features_into(s_act, num_out),
+               'goalscore': lambda: ops.goalscore_into(ab, out),
+               'labels': lambda: ops.labels(ab, 10, lab),
+               'formula': lambda: ops.formula(ab, ps, pc, val)}
+    order = args.order.split(',')
+    if sorted(order) != sorted(by_name):
+        raise SystemExit(f'--order must be a permutation of {",".join(by_name)}')
+    calls = tuple(by_name[k] for k in order)
     main_s = torch.cuda.current_stream()
     side = torch.cuda.Stream() if not args.serial else main_s
     aux = torch.cuda.Stream() if args.aux > 0 and not args.serial else None
     nv = len(calls)
     n_main = nv - (args.aux if aux is not None else 0)  # calls[n_main:] run on `aux`
 
-    def step(ev=None):
+    def step(ev=None, calls=calls):
         # default: the xT fit runs on a side stream next to the VAEP kernels -- the first
         # `xt_fork` VAEP kernels are enqueued, then the side stream forks for the count pass and
         # RCCL all-reduce, then the remaining VAEP kernels, then the solve (a single workgroup
@@ -384,6 +393,23 @@ def main() -> None:
             join.record(other)
             main_s.wait_event(join)
 
+    if args.ab_orders:  # in-process A/B of launch orders on the same allocations (dev tool)
+        orders = [o.split(',') for o in args.ab_orders.split(';')]
+        ab_ms = {','.join(o): [] for o in orders}
+        for _ in range(args.warmup):
+            step()
+        for rnd in range(4):
+            for o in orders:
+                cs = tuple(by_name[k] for k in o)
+                step(calls=cs)
+                torch.cuda.synchronize()
+                t = time.perf_counter()
+                for _ in range(args.steps):
+                    step(calls=cs)
+                torch.cuda.synchronize()
+                ab_ms[','.join(o)].append(round((time.perf_counter() - t) / args.steps * 1e3, 4))
+        print(json.dumps({'ab_orders_ms_per_step': ab_ms}), flush=True)
+        return
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -400,7 +426,7 @@ def main() -> None:
         dist.barrier()
     wall = time.perf_counter() - t0
     kern = {name: float(np.mean([e[i][0].elapsed_time(e[i][1]) for e in evs]))
-            for i, name in enumerate(KERNELS[:nv])}
+            for i, name in enumerate(order)}
     kern['xt_fit_rate'] = float(np.mean([e[nv][0].elapsed_time(e[nv][1]) for e in evs]))
     total_actions = n
     if dist:
@@ -460,9 +486,10 @@ def main() -> None:
                        'stream': 'main (serial)' if args.serial else
                        f'side stream, forked after {args.xt_fork} VAEP kernel(s), overlapped '
                        'with the rest'}
+    line['vaep_order'] = order
     line['streams'] = ('one stream' if args.serial else
                        f'VAEP feature kernels on the main stream, xT on a side stream'
-                       + (f', {", ".join(KERNELS[n_main:nv])} on a third stream'
+                       + (f', {", ".join(order[n_main:])} on a third stream'
                           if aux is not None else ''))
     line.update(extra_side)
     if not args.no_cpu and world == 1:  # the CPU comparator runs on rank 0 at N = 1 only
