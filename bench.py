@@ -351,7 +351,7 @@ def main() -> None:
     nv = len(calls)
     n_main = nv - (args.aux if aux is not None else 0)  # calls[n_main:] run on `aux`
 
-    def step(ev=None, calls=calls):
+    def step(ev=None, calls=calls, xt_fork=args.xt_fork):
         # default: the xT fit runs on a side stream next to the VAEP kernels -- the first
         # `xt_fork` VAEP kernels are enqueued, then the side stream forks for the count pass and
         # RCCL all-reduce, then the remaining VAEP kernels, then the solve (a single workgroup
@@ -366,7 +366,7 @@ def main() -> None:
             aux.wait_event(fork_a)
         for i, call in enumerate(calls):
             st = main_s if i < n_main else aux
-            if overlap and i == min(args.xt_fork, n_main - 1):
+            if overlap and i == min(xt_fork, n_main - 1):
                 fork = torch.cuda.Event()
                 fork.record(main_s)
                 side.wait_event(fork)
@@ -394,20 +394,23 @@ def main() -> None:
             main_s.wait_event(join)
 
     if args.ab_orders:  # in-process A/B of launch orders on the same allocations (dev tool)
-        orders = [o.split(',') for o in args.ab_orders.split(';')]
-        ab_ms = {','.join(o): [] for o in orders}
+        # entries "k1,k2,...[@F]": a launch order, optionally with the xT fork point F
+        specs = args.ab_orders.split(';')
+        ab_ms = {sp: [] for sp in specs}
         for _ in range(args.warmup):
             step()
         for rnd in range(4):
-            for o in orders:
-                cs = tuple(by_name[k] for k in o)
-                step(calls=cs)
+            for sp in specs:
+                o, _, f = sp.partition('@')
+                cs = tuple(by_name[k] for k in o.split(','))
+                fk = int(f) if f else args.xt_fork
+                step(calls=cs, xt_fork=fk)
                 torch.cuda.synchronize()
                 t = time.perf_counter()
                 for _ in range(args.steps):
-                    step(calls=cs)
+                    step(calls=cs, xt_fork=fk)
                 torch.cuda.synchronize()
-                ab_ms[','.join(o)].append(round((time.perf_counter() - t) / args.steps * 1e3, 4))
+                ab_ms[sp].append(round((time.perf_counter() - t) / args.steps * 1e3, 4))
         print(json.dumps({'ab_orders_ms_per_step': ab_ms}), flush=True)
         return
     for _ in range(args.warmup):
