@@ -40,13 +40,14 @@ SPADL_DEFAULT = ['actiontype_onehot', 'result_onehot', 'actiontype_result_onehot
 BYTES = {'bool_features': 7 + 515,             # type/result/bodypart u8 + team i32 -> 515 bools
          'num_features': 48 + 47 * 8 + 3 * 8,  # 5 f64 + 4 u8 + team -> 47 f64 + 3 i64
          'goalscore': 6 + 24, 'labels': 6 + 2, 'formula': 30 + 24,
-         'xt_fit_rate': 34 + 42}               # count pass 34 B + rate 42 B (solve: 192 cells)
+         # count pass 34 B + its 4-B rate codes, rate 4 + 8 B (solve: 192 cells)
+         'xt_fit_rate': 34 + 4 + 4 + 8}
 KERNELS = ('bool_features', 'num_features', 'goalscore', 'labels', 'formula', 'xt_fit_rate')
 # the HIP kernel each step entry launches (socceraction_amd/csrc/sa_vaep.hip)
 KERNEL_NAMES = {'bool_features': 'bool_colgroup_kernel', 'num_features': 'num_features_kernel',
                 'goalscore': 'goalscore_wave16_kernel', 'labels': 'labels_kernel',
                 'formula': 'formula_kernel',
-                'xt_fit_rate': 'xt_count_kernel + xt_solve_small_kernel + xt_rate_kernel'}
+                'xt_fit_rate': 'xt_count_kernel + xt_solve_small_kernel + xt_rate_codes_kernel'}
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 
@@ -75,16 +76,20 @@ def _reduce(dist, value, op, dev):
     return float(t.item())
 
 
-def xt_step(ab, dist):
+def xt_step(ab, dist, use_codes: bool = True):
     """BASELINE cfg4 inside the step: xT 16x12 fit on the step's actions (count pass, RCCL
     all-reduce of the counts across ranks, value iteration to eps=1e-5; the solve synchronises
     its stream) and ExpectedThreat.rate of every action, as two phases so the caller can enqueue
     the VAEP kernels in between. Returns (start, finish, holder of the last solution)."""
     from socceraction_amd import shard
     state = {}
+    # the count pass also writes each action's rate operand (4 B), so the rate reads that
+    # instead of the coordinates and ids again (42 -> 12 B per action)
+    codes = ops.xt_rate_codes_buffer(ab.n, ab.device) if use_codes else None
+    rate_out = torch.empty(max((ab.n + 15) // 16 * 16, 16), dtype=torch.float64, device=ab.device)
 
     def start():
-        acc = ops.xt_count(ab, 16, 12)
+        acc = ops.xt_count(ab, 16, 12, codes=codes)
         if dist is not None and dist.get_backend() == 'nccl':
             shard.allreduce_xt_counts(acc.shot, acc.goal, acc.move, acc.trans, acc.err)
         elif dist is not None:  # gloo rehearsal: the same sum through host memory
@@ -96,7 +101,10 @@ def xt_step(ab, dist):
 
     def finish():
         sol = ops.xt_solve(state.pop('acc'))  # synchronises the current stream
-        ops.xt_rate(ab, sol.mats[3].reshape(12, 16), 16, 12)
+        if codes is not None:
+            ops.xt_rate_codes(codes, ab.n, sol.mats[3], out=rate_out)
+        else:
+            ops.xt_rate(ab, sol.mats[3].reshape(12, 16), 16, 12)
         state['sol'] = sol
     return start, finish, state
 
@@ -295,6 +303,8 @@ def main() -> None:
     ap.add_argument('--order', default='num_features,bool_features,goalscore,labels,formula',
                     help='launch order of the VAEP kernels in the step (default measured 1.3 %% '
                          'faster than bool first, in-process A/B: profiles/r01h_order_ab.log)')
+    ap.add_argument('--xt-rate-coords', action='store_true',
+                    help='xT rate from the coordinates (default: from the count pass\'s codes)')
     ap.add_argument('--ab-orders', default='',
                     help='dev tool: ";"-separated launch orders timed round-robin in one process')
     ap.add_argument('--aux', type=int, default=0,
@@ -335,7 +345,7 @@ def main() -> None:
     lab = ops.LabelBlocks(n, lab_buf[0], lab_buf[1], None)
     val = torch.empty((3, ld), dtype=torch.float64, device=dev)
     s_act = ab.struct()
-    xt_start, xt_finish, xt_last = xt_step(ab, dist)
+    xt_start, xt_finish, xt_last = xt_step(ab, dist, use_codes=not args.xt_rate_coords)
     by_name = {'bool_features': lambda: ops.features_into(s_act, bool_out),
                'num_features': lambda: ops.features_into(s_act, num_out),
                'goalscore': lambda: ops.goalscore_into(ab, out),
@@ -351,7 +361,7 @@ def main() -> None:
     nv = len(calls)
     n_main = nv - (args.aux if aux is not None else 0)  # calls[n_main:] run on `aux`
 
-    def step(ev=None, calls=calls, xt_fork=args.xt_fork):
+    def step(ev=None, calls=calls, xt_fork=args.xt_fork, xt_start=xt_start, xt_finish=xt_finish):
         # default: the xT fit runs on a side stream next to the VAEP kernels -- the first
         # `xt_fork` VAEP kernels are enqueued, then the side stream forks for the count pass and
         # RCCL all-reduce, then the remaining VAEP kernels, then the solve (a single workgroup
@@ -394,21 +404,25 @@ def main() -> None:
             main_s.wait_event(join)
 
     if args.ab_orders:  # in-process A/B of launch orders on the same allocations (dev tool)
-        # entries "k1,k2,...[@F]": a launch order, optionally with the xT fork point F
+        # entries "k1,k2,...[@F][#coords]": a launch order, optionally with the xT fork point F
+        # and the coordinate-reading xT rate instead of the count pass's codes
         specs = args.ab_orders.split(';')
+        xt_coords = xt_step(ab, dist, use_codes=False)
         ab_ms = {sp: [] for sp in specs}
         for _ in range(args.warmup):
             step()
         for rnd in range(4):
             for sp in specs:
-                o, _, f = sp.partition('@')
+                sp0, _, xv = sp.partition('#')
+                o, _, f = sp0.partition('@')
                 cs = tuple(by_name[k] for k in o.split(','))
                 fk = int(f) if f else args.xt_fork
-                step(calls=cs, xt_fork=fk)
+                xs, xf = (xt_coords[0], xt_coords[1]) if xv == 'coords' else (xt_start, xt_finish)
+                step(calls=cs, xt_fork=fk, xt_start=xs, xt_finish=xf)
                 torch.cuda.synchronize()
                 t = time.perf_counter()
                 for _ in range(args.steps):
-                    step(calls=cs, xt_fork=fk)
+                    step(calls=cs, xt_fork=fk, xt_start=xs, xt_finish=xf)
                 torch.cuda.synchronize()
                 ab_ms[sp].append(round((time.perf_counter() - t) / args.steps * 1e3, 4))
         print(json.dumps({'ab_orders_ms_per_step': ab_ms}), flush=True)

@@ -168,6 +168,15 @@ int sa_vaep_formula_f32(const sa_actions* a, const float* p_scores, const float*
 int sa_xt_count(const sa_actions* a, int32_t l, int32_t w, int64_t* shot, int64_t* goal,
                 int64_t* move, int32_t* trans, int32_t* err_flags, void* stream);
 
+/* sa_xt_count that also writes, per action, the operand of a later rate() of the SAME actions
+ * on the same (l, w) grid without interpolation (fit + rate of one frame, xthreat.py:322-345
+ * then :408-465): codes[j] = start cell | end cell << 16 for a successful move, 0xFFFFFFFE for
+ * a successful move with a non-finite coordinate, 0xFFFFFFFF otherwise.  codes: [n] u32,
+ * 16-byte aligned; l * w <= 65535. */
+int sa_xt_count_codes(const sa_actions* a, int32_t l, int32_t w, int64_t* shot, int64_t* goal,
+                      int64_t* move, int32_t* trans, int32_t* err_flags, uint32_t* codes,
+                      void* stream);
+
 /* Normalise the counts into the reference's matrices and run the value iteration
  * x <- s*p_shot + p_move * (T x) until no cell changes by more than eps
  * (xthreat.py:278-345).  Writes (all float64, device):
@@ -217,6 +226,12 @@ int sa_xt_interp_grid(const double* xT, const double* cx, const double* cy, int3
  * *err_flags (device int32, may be NULL). */
 int sa_xt_rate(const sa_actions* a, const double* grid, int32_t L, int32_t W, double* out,
                int32_t* err_flags, void* stream);
+
+/* sa_xt_rate from the codes of sa_xt_count_codes (grid = the fitted (w, l) xT surface):
+ * same values and err_flags bit 4 as sa_xt_rate on those actions, reading 4 B per action
+ * instead of the coordinates and ids.  out: [n] f64, 16-byte aligned. */
+int sa_xt_rate_codes(const uint32_t* codes, int64_t n, const double* grid, double* out,
+                     int32_t* err_flags, void* stream);
 
 /* ---- SPADL -> Atomic-SPADL (atomic/spadl/base.py:15-235) ------------------------
  * Replaces convert_to_atomic: the four insertion passes (_extra_from_passes :38-112,

@@ -37,6 +37,20 @@ __device__ __forceinline__ int flat_index(double x, double y, int l, int w) {
 
 __device__ __forceinline__ bool is_move(int t) { return t == T_PASS || t == T_DRIBBLE || t == T_CROSS; }
 
+// Rate operand of one action for a later rate() on the same (l, w) grid, written by the count
+// pass so the rate pass reads 4 B instead of the 34 B of coordinates and ids again
+// (xthreat.py:440-465 without interpolation): start cell | end cell << 16 for a successful
+// move with finite coordinates, XT_CODE_BAD for a successful move with a non-finite one (the
+// reference's int64 cast raises), XT_CODE_NAN for every other action (rated NaN).
+constexpr uint32_t XT_CODE_NAN = 0xFFFFFFFFu, XT_CODE_BAD = 0xFFFFFFFEu;
+
+__device__ __forceinline__ uint32_t rate_code(int t, int r, double sx, double sy, double ex, double ey,
+                                              int l, int w) {
+  if (!is_move(t) || r != R_SUCCESS) return XT_CODE_NAN;
+  if (!isfinite(sx) || !isfinite(sy) || !isfinite(ex) || !isfinite(ey)) return XT_CODE_BAD;
+  return (uint32_t)flat_index(sx, sy, l, w) | ((uint32_t)flat_index(ex, ey, l, w) << 16);
+}
+
 // ---------------------------------------------------------------------------------------------
 // Count pass.  XC_SMALL: per-workgroup LDS histograms (u32 for the three C-vectors, the C x C
 // transition counts packed two u16 per word), flushed with one global atomic per non-zero
@@ -59,7 +73,8 @@ __global__ __launch_bounds__(XT_WIDE_THREADS) void xt_count_kernel(sa_actions A,
                                                                   unsigned long long* __restrict__ goal,
                                                                   unsigned long long* __restrict__ move,
                                                                   int32_t* __restrict__ trans,
-                                                                  int32_t* __restrict__ err, int64_t chunk) {
+                                                                  int32_t* __restrict__ err, int64_t chunk,
+                                                                  uint32_t* __restrict__ codes) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   const int C = l * w;
   const int64_t n = A.n;
@@ -102,6 +117,7 @@ __global__ __launch_bounds__(XT_WIDE_THREADS) void xt_count_kernel(sa_actions A,
 #pragma unroll
     for (int u = 0; u < XC_U; ++u) {
       const int t = tt[u], r = rr[u];
+      if (codes && t >= 0) codes[j0 + u * stride] = rate_code(t, r, sx[u], sy[u], ex[u], ey[u], l, w);
       if (t == T_SHOT) {
         if (isnan(sx[u]) || isnan(sy[u])) continue;  // _count drops NaN rows (xthreat.py:60-61)
         if (!isfinite(sx[u]) || !isfinite(sy[u])) {
@@ -504,6 +520,34 @@ __global__ __launch_bounds__(256) void xt_rate_kernel(sa_actions A, const double
   if (bad && err) atomicOr(err, bad);
 }
 
+// rate() from the count pass's codes: a thread rates 4 actions (one 16-B code load, two 16-B
+// stores) -- 12 B per action instead of 42.
+__global__ __launch_bounds__(256) void xt_rate_codes_kernel(const uint32_t* __restrict__ codes, int64_t n,
+                                                            const double* __restrict__ grid,
+                                                            double* __restrict__ out,
+                                                            int32_t* __restrict__ err) {
+  const int64_t j0 = 4 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x);
+  if (j0 >= n) return;
+  int32_t bad = 0;
+  auto one = [&](uint32_t c) -> double {
+    if (c == XT_CODE_NAN) return __builtin_nan("");
+    if (c == XT_CODE_BAD) {
+      bad = 4;
+      return __builtin_nan("");
+    }
+    return grid[c >> 16] - grid[c & 0xFFFFu];
+  };
+  if (j0 + 4 <= n) {
+    const u32x4 c = *reinterpret_cast<const u32x4*>(codes + j0);
+    const f64x2 a = {one(c[0]), one(c[1])}, b = {one(c[2]), one(c[3])};
+    __builtin_nontemporal_store(a, reinterpret_cast<f64x2*>(out + j0));
+    __builtin_nontemporal_store(b, reinterpret_cast<f64x2*>(out + j0 + 2));
+  } else {
+    for (int64_t j = j0; j < n; ++j) out[j] = one(codes[j]);
+  }
+  if (bad && err) atomicOr(err, bad);
+}
+
 }  // namespace sa
 
 // ================================== C ABI =================================================
@@ -511,6 +555,12 @@ using namespace sa;
 
 extern "C" int sa_xt_count(const sa_actions* a, int32_t l, int32_t w, int64_t* shot, int64_t* goal,
                            int64_t* move, int32_t* trans, int32_t* err_flags, void* stream) {
+  return sa_xt_count_codes(a, l, w, shot, goal, move, trans, err_flags, nullptr, stream);
+}
+
+extern "C" int sa_xt_count_codes(const sa_actions* a, int32_t l, int32_t w, int64_t* shot,
+                                 int64_t* goal, int64_t* move, int32_t* trans, int32_t* err_flags,
+                                 uint32_t* codes, void* stream) {
   if (!a || a->n < 0) return fail(SA_EINVAL, "bad sa_actions");
   if (l < 1 || w < 1) return fail(SA_EINVAL, "l and w must be >= 1");
   if ((int64_t)l * w > 46340) return fail(SA_EINVAL, "grid too large (C*C must fit int32 indexing)");
@@ -518,6 +568,8 @@ extern "C" int sa_xt_count(const sa_actions* a, int32_t l, int32_t w, int64_t* s
   const sa_frame& F = a->frames[0];
   if (a->n > 0 && (!F.type_id || !F.result_id || !F.c0 || !F.c1 || !F.c2 || !F.c3))
     return fail(SA_EINVAL, "null input column");
+  if (codes && !aligned16(codes)) return fail(SA_EINVAL, "codes must be 16-byte aligned");
+  if (codes && (int64_t)l * w > 65535) return fail(SA_EINVAL, "rate codes need l * w <= 65535");
   if (a->n == 0) return SA_OK;
   const int C = l * w;
   const size_t small_lds = (size_t)(3 * C + (C * C + 1) / 2) * 4;
@@ -541,18 +593,18 @@ extern "C" int sa_xt_count(const sa_actions* a, int32_t l, int32_t w, int64_t* s
     if (blocks > cus) blocks = cus;
     const int64_t chunk = (a->n + blocks - 1) / blocks;
     hipLaunchKernelGGL((xt_count_kernel<XC_WIDE>), dim3((unsigned)blocks), dim3(XT_WIDE_THREADS), wide_lds, st,
-                       *a, l, w, us, ug, um, trans, err_flags, chunk);
+                       *a, l, w, us, ug, um, trans, err_flags, chunk, codes);
   } else if (small_lds <= 80 * 1024) {
     hipLaunchKernelGGL((xt_count_kernel<XC_SMALL>), dim3(wg_blocks), dim3(XT_THREADS), small_lds, st, *a,
-                       l, w, us, ug, um, trans, err_flags, (int64_t)XT_SMALL_ACTS);
+                       l, w, us, ug, um, trans, err_flags, (int64_t)XT_SMALL_ACTS, codes);
   } else if (vec_lds <= 120 * 1024) {
     hipLaunchKernelGGL((xt_count_kernel<XC_VEC>), dim3(wg_blocks), dim3(XT_THREADS), vec_lds, st, *a, l,
-                       w, us, ug, um, trans, err_flags, (int64_t)XT_SMALL_ACTS);
+                       w, us, ug, um, trans, err_flags, (int64_t)XT_SMALL_ACTS, codes);
   } else {
     int64_t blocks = (a->n + XT_THREADS - 1) / XT_THREADS;
     if (blocks > 4096) blocks = 4096;
     hipLaunchKernelGGL((xt_count_kernel<XC_GLOBAL>), dim3((unsigned)blocks), dim3(XT_THREADS), 0, st, *a,
-                       l, w, us, ug, um, trans, err_flags, (int64_t)0);
+                       l, w, us, ug, um, trans, err_flags, (int64_t)0, codes);
   }
   return check_launch("xt_count_kernel");
 }
@@ -700,4 +752,15 @@ extern "C" int sa_xt_iterate_rows(const int32_t* cnt_rows, const int64_t* move, 
                      (hipStream_t)stream, cnt_rows, reinterpret_cast<const unsigned long long*>(move), gs,
                      pmove, C, r0, nrows, eps, x, x_next_rows, flag_prev, flag_out);
   return check_launch("xt_iter_kernel");
+}
+
+extern "C" int sa_xt_rate_codes(const uint32_t* codes, int64_t n, const double* grid, double* out,
+                                int32_t* err_flags, void* stream) {
+  if (n < 0 || (n > 0 && (!codes || !grid || !out))) return fail(SA_EINVAL, "bad xt_rate_codes args");
+  if (n == 0) return SA_OK;
+  if (!aligned16(codes) || !aligned16(out)) return fail(SA_EINVAL, "codes and out must be 16-byte aligned");
+  const int64_t threads = (n + 3) / 4;
+  hipLaunchKernelGGL(xt_rate_codes_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, codes, n, grid, out, err_flags);
+  return check_launch("xt_rate_codes_kernel");
 }

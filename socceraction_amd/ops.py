@@ -193,13 +193,42 @@ def xt_zero_counts(l: int, w: int, dev, row_blocks: int = 1) -> XTCounts:
     return acc
 
 
-def xt_count(batch: ActionBatch, l: int, w: int, acc: Optional[XTCounts] = None) -> XTCounts:
+def xt_count(batch: ActionBatch, l: int, w: int, acc: Optional[XTCounts] = None,
+             codes: Optional[torch.Tensor] = None) -> XTCounts:
+    """Count pass of ExpectedThreat.fit. With ``codes`` (u32 [>= n], e.g. from
+    :func:`xt_rate_codes_buffer`) the pass also writes each action's rate operand for a later
+    :func:`xt_rate_codes` of the same actions on the same grid."""
     acc = acc or xt_zero_counts(l, w, batch.device)
     s = batch.struct()
-    _native.check(_native.lib().sa_xt_count(ctypes.byref(s), l, w, _ptr(acc.shot), _ptr(acc.goal),
-                                            _ptr(acc.move), _ptr(acc.trans), _ptr(acc.err),
-                                            stream_handle()))
+    if codes is None:
+        _native.check(_native.lib().sa_xt_count(ctypes.byref(s), l, w, _ptr(acc.shot),
+                                                _ptr(acc.goal), _ptr(acc.move), _ptr(acc.trans),
+                                                _ptr(acc.err), stream_handle()))
+    else:
+        if codes.dtype != torch.int32 or codes.numel() < batch.n:
+            raise ValueError('codes must be an int32 tensor of at least n elements')
+        _native.check(_native.lib().sa_xt_count_codes(ctypes.byref(s), l, w, _ptr(acc.shot),
+                                                      _ptr(acc.goal), _ptr(acc.move),
+                                                      _ptr(acc.trans), _ptr(acc.err),
+                                                      _ptr(codes), stream_handle()))
     return acc
+
+
+def xt_rate_codes_buffer(n: int, dev) -> torch.Tensor:
+    """u32 rate operands (stored as int32) for n actions."""
+    return torch.empty(max(_ld(n), 16), dtype=torch.int32, device=dev)
+
+
+def xt_rate_codes(codes: torch.Tensor, n: int, grid: torch.Tensor,
+                  out: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """ExpectedThreat.rate (no interpolation) of the actions whose count pass wrote ``codes``,
+    ``grid`` = the fitted (w, l) surface: same values and error bit as :func:`xt_rate`."""
+    dev = codes.device
+    out = torch.empty(max(_ld(n), 16), dtype=torch.float64, device=dev) if out is None else out
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    _native.check(_native.lib().sa_xt_rate_codes(_ptr(codes), n, _ptr(grid.contiguous()),
+                                                 _ptr(out), _ptr(err), stream_handle()))
+    return out[:n], err
 
 
 def xt_check_errors(acc: XTCounts) -> None:

@@ -251,6 +251,38 @@ def test_xt_large_grid_vs_oracle(sa, l, w, games):
     np.testing.assert_array_equal(m[3].reshape(w, l), ref['xT'])
 
 
+@pytest.mark.parametrize('l,w,games', [(16, 12, 400), (105, 68, 60), (1, 1, 5), (30, 20, 1)])
+def test_xt_rate_codes_match_rate(sa, l, w, games):
+    """fit + rate of one frame through the count pass's rate codes == the coordinate path:
+    counts, error bits, values and NaN pattern bit for bit, incl. NaN / inf coordinates on
+    successful moves, failed moves and shots, and a tail shorter than 4 actions."""
+    B, ops, syn = sa['batch'], sa['ops'], sa['synthetic']
+    d = syn.spadl_games(games, game_id0=5)
+    n = len(d['type_id'])
+    d = {k: (v[:n - 3].copy() if isinstance(v, np.ndarray) and v.shape == (n,) else v)
+         for k, v in d.items()}
+    d['game_off'] = np.minimum(d['game_off'], n - 3)
+    rng = np.random.default_rng(9)
+    for col, val in (('start_x', np.nan), ('end_y', np.inf), ('start_y', -np.inf),
+                     ('end_x', np.nan)):
+        d[col][rng.choice(n - 3, 7, replace=False)] = val
+    ab = B.ActionBatch.from_columns(d)
+    ref_acc = ops.xt_count(ab, l, w)
+    codes = ops.xt_rate_codes_buffer(ab.n, ab.device)
+    acc = ops.xt_count(ab, l, w, codes=codes)
+    for a, b in ((acc.shot, ref_acc.shot), (acc.goal, ref_acc.goal), (acc.move, ref_acc.move),
+                 (acc.trans, ref_acc.trans), (acc.err, ref_acc.err)):
+        assert torch.equal(a, b)
+    grid = torch.rand((w, l), dtype=torch.float64, device=ab.device)
+    ref, ref_err = ops.xt_rate(ab, grid, l, w)
+    got, err = ops.xt_rate_codes(codes, ab.n, grid)
+    r, g = ref.cpu().numpy(), got.cpu().numpy()
+    np.testing.assert_array_equal(np.isnan(g), np.isnan(r))
+    np.testing.assert_array_equal(g[~np.isnan(r)], r[~np.isnan(r)])
+    assert int(err.item()) == int(ref_err.item()) == 4
+    assert (~np.isnan(r)).sum() > 0
+
+
 def test_full_size_sampled_games_vs_oracle(sa):
     """cfg2-sized batch (10k games, ~16M actions): sampled games checked against the oracle,
     plus size-independent invariants over the whole batch (one-hot rows sum to 1)."""
