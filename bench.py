@@ -76,7 +76,7 @@ def _reduce(dist, value, op, dev):
     return float(t.item())
 
 
-def xt_step(ab, dist, use_codes: bool = True):
+def xt_step(ab, dist, use_codes: bool = True, shared: bool = True):
     """BASELINE cfg4 inside the step: xT 16x12 fit on the step's actions (count pass, RCCL
     all-reduce of the counts across ranks, value iteration to eps=1e-5; the solve synchronises
     its stream) and ExpectedThreat.rate of every action, as two phases so the caller can enqueue
@@ -89,7 +89,7 @@ def xt_step(ab, dist, use_codes: bool = True):
     rate_out = torch.empty(max((ab.n + 15) // 16 * 16, 16), dtype=torch.float64, device=ab.device)
 
     def start():
-        acc = ops.xt_count(ab, 16, 12, codes=codes)
+        acc = ops.xt_count(ab, 16, 12, codes=codes, shared=shared)
         if dist is not None and dist.get_backend() == 'nccl':
             shard.allreduce_xt_counts(acc.shot, acc.goal, acc.move, acc.trans, acc.err)
         elif dist is not None:  # gloo rehearsal: the same sum through host memory
@@ -345,7 +345,8 @@ def main() -> None:
     lab = ops.LabelBlocks(n, lab_buf[0], lab_buf[1], None)
     val = torch.empty((3, ld), dtype=torch.float64, device=dev)
     s_act = ab.struct()
-    xt_start, xt_finish, xt_last = xt_step(ab, dist, use_codes=not args.xt_rate_coords)
+    xt_start, xt_finish, xt_last = xt_step(ab, dist, use_codes=not args.xt_rate_coords,
+                                           shared=not args.serial)
     by_name = {'bool_features': lambda: ops.features_into(s_act, bool_out),
                'num_features': lambda: ops.features_into(s_act, num_out),
                'goalscore': lambda: ops.goalscore_into(ab, out),
@@ -413,7 +414,11 @@ def main() -> None:
             step()
         for rnd in range(4):
             for sp in specs:
-                sp0, _, xv = sp.partition('#')
+                sp1, _, env = sp.partition('!')  # "!VAR=value": set for this entry
+                if env:
+                    k_, _, v_ = env.partition('=')
+                    os.environ[k_] = v_
+                sp0, _, xv = sp1.partition('#')
                 o, _, f = sp0.partition('@')
                 cs = tuple(by_name[k] for k in o.split(','))
                 fk = int(f) if f else args.xt_fork
@@ -425,6 +430,8 @@ def main() -> None:
                     step(calls=cs, xt_fork=fk, xt_start=xs, xt_finish=xf)
                 torch.cuda.synchronize()
                 ab_ms[sp].append(round((time.perf_counter() - t) / args.steps * 1e3, 4))
+                if env:
+                    os.environ.pop(k_, None)
         print(json.dumps({'ab_orders_ms_per_step': ab_ms}), flush=True)
         return
     for _ in range(args.warmup):

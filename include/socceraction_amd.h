@@ -172,10 +172,12 @@ int sa_xt_count(const sa_actions* a, int32_t l, int32_t w, int64_t* shot, int64_
  * on the same (l, w) grid without interpolation (fit + rate of one frame, xthreat.py:322-345
  * then :408-465): codes[j] = start cell | end cell << 16 for a successful move, 0xFFFFFFFE for
  * a successful move with a non-finite coordinate, 0xFFFFFFFF otherwise.  codes: [n] u32,
- * 16-byte aligned; l * w <= 65535. */
+ * 16-byte aligned, or NULL; l * w <= 65535.  flags: SA_XT_COUNT_SHARED when the pass runs
+ * concurrently with other kernels (smaller workgroups that co-reside with them). */
+#define SA_XT_COUNT_SHARED 1
 int sa_xt_count_codes(const sa_actions* a, int32_t l, int32_t w, int64_t* shot, int64_t* goal,
                       int64_t* move, int32_t* trans, int32_t* err_flags, uint32_t* codes,
-                      void* stream);
+                      int32_t flags, void* stream);
 
 /* Normalise the counts into the reference's matrices and run the value iteration
  * x <- s*p_shot + p_move * (T x) until no cell changes by more than eps

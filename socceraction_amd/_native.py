@@ -90,7 +90,8 @@ _SIGNATURES = {
     'sa_xt_count': (ctypes.c_int, [ctypes.POINTER(SaActions), ctypes.c_int32, ctypes.c_int32,
                                    _p, _p, _p, _p, _p, _p]),
     'sa_xt_count_codes': (ctypes.c_int, [ctypes.POINTER(SaActions), ctypes.c_int32,
-                                         ctypes.c_int32, _p, _p, _p, _p, _p, _p, _p]),
+                                         ctypes.c_int32, _p, _p, _p, _p, _p, _p,
+                                         ctypes.c_int32, _p]),
     'sa_xt_rate_codes': (ctypes.c_int, [_p, ctypes.c_int64, _p, _p, _p, _p]),
     'sa_xt_solve': (ctypes.c_int, [_p, _p, _p, _p, ctypes.c_int32, ctypes.c_int32,
                                    ctypes.c_double, ctypes.c_int32, _p, _p, _p,

@@ -194,23 +194,25 @@ def xt_zero_counts(l: int, w: int, dev, row_blocks: int = 1) -> XTCounts:
 
 
 def xt_count(batch: ActionBatch, l: int, w: int, acc: Optional[XTCounts] = None,
-             codes: Optional[torch.Tensor] = None) -> XTCounts:
+             codes: Optional[torch.Tensor] = None, shared: bool = False) -> XTCounts:
     """Count pass of ExpectedThreat.fit. With ``codes`` (u32 [>= n], e.g. from
     :func:`xt_rate_codes_buffer`) the pass also writes each action's rate operand for a later
-    :func:`xt_rate_codes` of the same actions on the same grid."""
+    :func:`xt_rate_codes` of the same actions on the same grid. ``shared``: the pass runs next
+    to other kernels (workgroups sized to co-reside with them)."""
     acc = acc or xt_zero_counts(l, w, batch.device)
     s = batch.struct()
-    if codes is None:
+    if codes is None and not shared:
         _native.check(_native.lib().sa_xt_count(ctypes.byref(s), l, w, _ptr(acc.shot),
                                                 _ptr(acc.goal), _ptr(acc.move), _ptr(acc.trans),
                                                 _ptr(acc.err), stream_handle()))
     else:
-        if codes.dtype != torch.int32 or codes.numel() < batch.n:
+        if codes is not None and (codes.dtype != torch.int32 or codes.numel() < batch.n):
             raise ValueError('codes must be an int32 tensor of at least n elements')
         _native.check(_native.lib().sa_xt_count_codes(ctypes.byref(s), l, w, _ptr(acc.shot),
                                                       _ptr(acc.goal), _ptr(acc.move),
                                                       _ptr(acc.trans), _ptr(acc.err),
-                                                      _ptr(codes), stream_handle()))
+                                                      _ptr(codes), int(shared),
+                                                      stream_handle()))
     return acc
 
 

@@ -270,9 +270,12 @@ def test_xt_rate_codes_match_rate(sa, l, w, games):
     ref_acc = ops.xt_count(ab, l, w)
     codes = ops.xt_rate_codes_buffer(ab.n, ab.device)
     acc = ops.xt_count(ab, l, w, codes=codes)
-    for a, b in ((acc.shot, ref_acc.shot), (acc.goal, ref_acc.goal), (acc.move, ref_acc.move),
-                 (acc.trans, ref_acc.trans), (acc.err, ref_acc.err)):
-        assert torch.equal(a, b)
+    shared = ops.xt_count(ab, l, w, shared=True)  # co-resident workgroup shape, same counts
+    for got_acc in (acc, shared):
+        for a, b in ((got_acc.shot, ref_acc.shot), (got_acc.goal, ref_acc.goal),
+                     (got_acc.move, ref_acc.move), (got_acc.trans, ref_acc.trans),
+                     (got_acc.err, ref_acc.err)):
+            assert torch.equal(a, b)
     grid = torch.rand((w, l), dtype=torch.float64, device=ab.device)
     ref, ref_err = ops.xt_rate(ab, grid, l, w)
     got, err = ops.xt_rate_codes(codes, ab.n, grid)
