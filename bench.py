@@ -359,10 +359,12 @@ def main() -> None:
     main_s = torch.cuda.current_stream()
     side = torch.cuda.Stream() if not args.serial else main_s
     aux = torch.cuda.Stream() if args.aux > 0 and not args.serial else None
+    aux_ab = torch.cuda.Stream() if args.ab_orders else None  # for "^A" A/B entries
     nv = len(calls)
     n_main = nv - (args.aux if aux is not None else 0)  # calls[n_main:] run on `aux`
 
-    def step(ev=None, calls=calls, xt_fork=args.xt_fork, xt_start=xt_start, xt_finish=xt_finish):
+    def step(ev=None, calls=calls, xt_fork=args.xt_fork, xt_start=xt_start, xt_finish=xt_finish,
+             aux=aux, n_main=n_main):
         # default: the xT fit runs on a side stream next to the VAEP kernels -- the first
         # `xt_fork` VAEP kernels are enqueued, then the side stream forks for the count pass and
         # RCCL all-reduce, then the remaining VAEP kernels, then the solve (a single workgroup
@@ -418,16 +420,20 @@ def main() -> None:
                 if env:
                     k_, _, v_ = env.partition('=')
                     os.environ[k_] = v_
-                sp0, _, xv = sp1.partition('#')
+                sp2, _, na = sp1.partition('^')  # "^A": last A kernels on a third stream
+                sp0, _, xv = sp2.partition('#')
                 o, _, f = sp0.partition('@')
                 cs = tuple(by_name[k] for k in o.split(','))
                 fk = int(f) if f else args.xt_fork
                 xs, xf = (xt_coords[0], xt_coords[1]) if xv == 'coords' else (xt_start, xt_finish)
-                step(calls=cs, xt_fork=fk, xt_start=xs, xt_finish=xf)
+                kw = dict(calls=cs, xt_fork=fk, xt_start=xs, xt_finish=xf)
+                if na:
+                    kw.update(aux=aux_ab, n_main=len(cs) - int(na))
+                step(**kw)
                 torch.cuda.synchronize()
                 t = time.perf_counter()
                 for _ in range(args.steps):
-                    step(calls=cs, xt_fork=fk, xt_start=xs, xt_finish=xf)
+                    step(**kw)
                 torch.cuda.synchronize()
                 ab_ms[sp].append(round((time.perf_counter() - t) / args.steps * 1e3, 4))
                 if env:
