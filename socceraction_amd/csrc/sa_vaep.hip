@@ -163,7 +163,11 @@ __device__ __forceinline__ void st_i64x2(int64_t* __restrict__ base, int64_t col
 
 // nan_to_num(arctan(dy / dx)) of vaep/features.py:376 (atan(+-inf) = +-pi/2, 0/0 -> 0)
 __device__ __forceinline__ double polar_angle(double dy, double dx) {
+#if SA_PROBE_NOATAN  // timing probe only (wrong results): no ocml atan
+  const double a = dy / dx;
+#else
   const double a = atan(dy / dx);
+#endif
   return isnan(a) ? 0.0 : a;
 }
 
