@@ -70,7 +70,22 @@ def main():
             lab_ref = got
         else:
             res['labels_equal'] = bool(torch.equal(lab_ref, got))
-    for k in ('SA_GS_KERNEL', 'SA_LABELS_SEARCH'):
+    from socceraction_amd import synthetic as syn_
+    pr = syn_.probabilities(n)
+    ps = torch.from_numpy(pr['scores']).to(dev)
+    pc = torch.from_numpy(pr['concedes']).to(dev)
+    val = torch.zeros((3, ld), dtype=torch.float64, device=dev)
+    f_ref = None
+    for v in ('lane', 'wave'):
+        os.environ['SA_FORMULA_SEARCH'] = v
+        val.zero_()
+        res[f'formula_{v}_ms'] = timed(lambda: ops.formula(ab, ps, pc, val), args.reps)
+        got = val.clone()
+        if f_ref is None:
+            f_ref = got
+        else:
+            res['formula_equal'] = bool(torch.equal(f_ref, got))
+    for k in ('SA_GS_KERNEL', 'SA_LABELS_SEARCH', 'SA_FORMULA_SEARCH'):
         os.environ.pop(k, None)
     print(json.dumps(res), flush=True)
 

@@ -1623,7 +1623,7 @@ __global__ __launch_bounds__(256) void labels_kernel(sa_actions A, int nr, uint8
 // dtype and mirrors the pandas expression tree operation by operation.  A lane owns V
 // consecutive actions (16-B stores); the previous row's values come from the same lane or,
 // for the lane's first action, from the neighbouring lane by a wave shuffle.
-template <bool ATOMIC, typename T>
+template <bool ATOMIC, typename T, bool WAVESEG>
 __global__ __launch_bounds__(256) void formula_kernel(sa_actions A, const T* __restrict__ ps,
                                                       const T* __restrict__ pc, T* __restrict__ off,
                                                       T* __restrict__ def, T* __restrict__ val,
@@ -1697,7 +1697,11 @@ __global__ __launch_bounds__(256) void formula_kernel(sa_actions A, const T* __r
     typ = F.type_id[p];
     rsp = ATOMIC ? 0 : F.result_id[p];
   }
-  SegCursor cur = seg_at(A, j0);
+  SegCursor cur;
+  if (WAVESEG)  // one search per wave (uniform, scalar loads), lanes advance from it
+    cur = seg_at(A, (int64_t)__builtin_amdgcn_readfirstlane((int)(j0 / V)) * V);
+  else
+    cur = seg_at(A, j0);
   vec_t vo, vd, vv;
 #pragma unroll
   for (int q = 0; q < V; ++q) {
@@ -2017,12 +2021,22 @@ static int launch_formula(const sa_actions* a, const T* ps, const T* pc, T* off,
   const int64_t lanes = (a->n + V - 1) / V;
   const dim3 grid((unsigned)((lanes + 255) / 256)), block(256);
   const bool vec_ok = SA_FORMULA_VEC && aligned16(ps) && aligned16(pc);
-  if (a->atomic)
-    hipLaunchKernelGGL((formula_kernel<true, T>), grid, block, 0, (hipStream_t)stream, *a, ps, pc, off,
-                       def, val, vec_ok);
-  else
-    hipLaunchKernelGGL((formula_kernel<false, T>), grid, block, 0, (hipStream_t)stream, *a, ps, pc,
-                       off, def, val, vec_ok);
+  hipStream_t st = (hipStream_t)stream;
+  if (env_is("SA_FORMULA_SEARCH", "lane")) {  // A/B: the per-lane segment search
+    if (a->atomic)
+      hipLaunchKernelGGL((formula_kernel<true, T, false>), grid, block, 0, st, *a, ps, pc, off, def,
+                         val, vec_ok);
+    else
+      hipLaunchKernelGGL((formula_kernel<false, T, false>), grid, block, 0, st, *a, ps, pc, off, def,
+                         val, vec_ok);
+  } else {
+    if (a->atomic)
+      hipLaunchKernelGGL((formula_kernel<true, T, true>), grid, block, 0, st, *a, ps, pc, off, def,
+                         val, vec_ok);
+    else
+      hipLaunchKernelGGL((formula_kernel<false, T, true>), grid, block, 0, st, *a, ps, pc, off, def,
+                         val, vec_ok);
+  }
   return check_launch("formula_kernel");
 }
 
