@@ -60,11 +60,16 @@ def main():
             os.environ['SA_BOOL_KERNEL'] = v
             bb.zero_()
 
+            lib = N.lib()
+            if v.startswith('lib:'):  # a variant build loaded next to the default library
+                lib = N.load_library(os.path.join(ROOT, 'socceraction_amd', '_lib',
+                                                  f'libsocceraction_amd_{v[4:]}.so'))
+
             def run():
                 if v == 'torch_fill':  # store ceiling of this allocation: torch's fill kernel
                     bb.fill_(1)
                     return
-                N.check(N.lib().sa_vaep_features(ctypes.byref(s), ctypes.byref(q.struct),
+                N.check(lib.sa_vaep_features(ctypes.byref(s), ctypes.byref(q.struct),
                                                  ctypes.byref(bd), None, None, stream))
             run()
             torch.cuda.synchronize()
