@@ -172,6 +172,55 @@ def test_staged_bool_kernel_matches_colgroup(sa, atomic, monkeypatch):
                     assert torch.equal(gf, rf), (k, v, Rb)
 
 
+@pytest.mark.parametrize('atomic', [False, True])
+def test_run_time_variants_match_default(sa, atomic, monkeypatch):
+    """The launchers' run-time A/B switches (sa_vaep.hip: SA_GS_KERNEL=wave2, SA_LABELS_SEARCH=
+    lane, SA_FORMULA_SEARCH=lane) give the default kernels' outputs bit for bit: full games plus
+    300 games of 1..40 actions (many segment starts per wave), labels at nr_actions 10 and 20
+    (the > 17 path reloads rows), f64 and f32 probabilities."""
+    B, ops, syn = sa['batch'], sa['ops'], sa['synthetic']
+    default = vo.ATOMIC_DEFAULT if atomic else vo.SPADL_DEFAULT
+    gen = syn.atomic_games if atomic else syn.spadl_games
+    d = gen(8, seed=21)
+    n0 = int(d['game_off'][-1])
+    sizes = np.random.default_rng(9).integers(1, 41, 300)
+    m = int(sizes.sum())
+    rows = {c: v for c, v in d.items() if isinstance(v, np.ndarray) and v.shape == (n0,)}
+    d2 = {c: np.concatenate([v, v[:m]]) for c, v in rows.items()}
+    offs = n0 + np.concatenate([[0], np.cumsum(sizes)])
+    d2['game_off'] = np.concatenate([d['game_off'], offs[1:]])
+    d2['home_team_id'] = np.concatenate([d['home_team_id'], d2['team_id'][offs[:-1]]])
+    ab = B.ActionBatch.from_columns(d2, atomic=atomic)
+    n = ab.n
+    rng = np.random.default_rng(4)
+    probs = [(torch.tensor(rng.random(n), dtype=dt, device=ab.device),
+              torch.tensor(rng.random(n), dtype=dt, device=ab.device))
+             for dt in (torch.float64, torch.float32)]
+
+    def run():
+        i64 = ops.features(ab, default, 3, bool_tile=1024, num_tile=128).to_numpy()[2]
+        lab = []
+        for nr in (10, 20):
+            lb = ops.labels(ab, nr_actions=nr)
+            lab += [t[:n].cpu().numpy() for t in (lb.scores, lb.concedes, lb.goal_from_shot)]
+        vals = [ops.formula(ab, ps, pc).cpu().numpy()[:, :n] for ps, pc in probs]
+        return i64, lab, vals
+
+    for var in ('SA_GS_KERNEL', 'SA_LABELS_SEARCH', 'SA_FORMULA_SEARCH'):
+        monkeypatch.delenv(var, raising=False)
+    ref = run()
+    for var, val in (('SA_GS_KERNEL', 'wave2'), ('SA_LABELS_SEARCH', 'lane'),
+                     ('SA_FORMULA_SEARCH', 'lane')):
+        monkeypatch.setenv(var, val)
+        got = run()
+        monkeypatch.delenv(var)
+        np.testing.assert_array_equal(got[0], ref[0], err_msg=var)
+        for a, b in zip(got[1], ref[1]):
+            np.testing.assert_array_equal(a, b, err_msg=var)
+        for a, b in zip(got[2], ref[2]):
+            np.testing.assert_array_equal(a, b, err_msg=var)
+
+
 def test_explicit_frames_match_windowed(sa):
     """Explicit-frame mode (module-level transformers) == windowed mode on the same states."""
     B, ops = sa['batch'], sa['ops']
