@@ -57,13 +57,15 @@ def main():
         bd.data, bd.n_cols, bd.tile_rows = bb.data_ptr(), plan.n_bool, 1024
         ref = None
         for v in variants:
-            os.environ['SA_BOOL_KERNEL'] = v
+            # "lib:NAME@KERNEL" = variant build NAME with SA_BOOL_KERNEL=KERNEL
+            lv, _, kv = v.partition('@')
+            os.environ['SA_BOOL_KERNEL'] = kv if lv.startswith('lib:') and kv else v
             bb.zero_()
 
             lib = N.lib()
-            if v.startswith('lib:'):  # a variant build loaded next to the default library
+            if lv.startswith('lib:'):  # a variant build loaded next to the default library
                 lib = N.load_library(os.path.join(ROOT, 'socceraction_amd', '_lib',
-                                                  f'libsocceraction_amd_{v[4:]}.so'))
+                                                  f'libsocceraction_amd_{lv[4:]}.so'))
 
             def run():
                 if v == 'torch_fill':  # store ceiling of this allocation: torch's fill kernel
