@@ -785,7 +785,10 @@ __global__ __launch_bounds__(1024) void bool_staged_kernel(FeatArgs args, int nc
     flg[k] = j >= n;
   }
   __syncthreads();
-  if (K > 1) {  // segment starts inside [h0, tile0 + 1024)
+#ifndef SA_PROBE_STAGED_NOSEG
+#define SA_PROBE_STAGED_NOSEG 0  // timing probe only (wrong results at segment starts)
+#endif
+  if (K > 1 && !SA_PROBE_STAGED_NOSEG) {  // segment starts inside [h0, tile0 + 1024)
     const int64_t g0 = find_segment(A.seg_off, A.n_segments, h0 > 0 ? h0 : 0);
     for (int64_t s = g0 + t; s < A.n_segments; s += nt) {
       const int64_t st = A.seg_off[s];
