@@ -362,11 +362,23 @@ int sa_tree_predict(const void* nodes, int32_t n_nodes, const int32_t* roots, co
                     const sa_block* bool_blk, const sa_block* f64_blk, const sa_block* i64_blk, int64_t n,
                     double base_margin, int32_t le, int32_t f32, void* p_out, void* stream);
 
-/* ---- misc -------------------------------------------------------------------- */
+/* ---- runtime ------------------------------------------------------------------ */
 int sa_abi_version(void);
 const char* sa_last_error(void);
-/* Device-side timing of the last launch of each kernel family is not kept here;
- * benchmarks time with HIP events on the caller's stream. */
+/* Hash of the sources, headers, compile flags and defines the library was built from
+ * (socceraction_amd/build.py); the Python loader refuses a library built from other sources. */
+const char* sa_build_id(void);
+/* Scratch: sa_xt_solve / sa_xt_normalize take their device scratch from a per-device arena
+ * owned by the library (mutex-guarded, reused in stream order); sa_shutdown() waits for the
+ * last use of every slot and frees the arena.  The library stays usable afterwards. */
+int sa_shutdown(void);
+/* Debug build (-DSA_DEBUG=1, libsocceraction_amd_debug.so): kernels check tile offsets,
+ * column indices, segment cursors, LDS and grid-cell indices and record the first failure
+ * instead of accessing out of bounds.  sa_debug_check() synchronises the device and returns
+ * SA_EDATA with the source location in sa_last_error() if any check failed since the last
+ * call (always SA_OK in the default build); sa_debug_enabled() tells the builds apart. */
+int sa_debug_check(void);
+int sa_debug_enabled(void);
 
 #ifdef __cplusplus
 }

@@ -12,7 +12,12 @@ import os
 from typing import Optional
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get('SOCCERACTION_AMD_LIB') or os.path.join(HERE, '_lib', 'libsocceraction_amd.so')
+# SOCCERACTION_AMD_DEBUG=1 selects the debug build (device bounds checks, every call checked);
+# SOCCERACTION_AMD_LIB an explicit library file (A/B variants)
+DEBUG = os.environ.get('SOCCERACTION_AMD_DEBUG', '') not in ('', '0')
+DEFAULT_LIB = os.path.join(HERE, '_lib', 'libsocceraction_amd.so')
+DEBUG_LIB = os.path.join(HERE, '_lib', 'libsocceraction_amd_debug.so')
+LIB_PATH = os.environ.get('SOCCERACTION_AMD_LIB') or (DEBUG_LIB if DEBUG else DEFAULT_LIB)
 
 SA_MAX_FRAMES = 8
 SA_BOOL_TILE_QUANTUM = 1024
@@ -126,6 +131,10 @@ _SIGNATURES = {
                                        ctypes.c_int32, ctypes.c_int32, _p, _p]),
     'sa_abi_version': (ctypes.c_int, []),
     'sa_last_error': (ctypes.c_char_p, []),
+    'sa_build_id': (ctypes.c_char_p, []),
+    'sa_debug_enabled': (ctypes.c_int, []),
+    'sa_debug_check': (ctypes.c_int, []),
+    'sa_shutdown': (ctypes.c_int, []),
 }
 EXPORTED_SYMBOLS = tuple(_SIGNATURES)
 
@@ -158,17 +167,41 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         fn.argtypes = args
     if lib.sa_abi_version() != 2:
         raise ImportError('libsocceraction_amd ABI version mismatch')
+    _check_build_id(lib, path)
     if path == LIB_PATH:
         _lib = lib
     return lib
+
+
+def _check_build_id(lib: ctypes.CDLL, path: str) -> None:
+    """The default and debug libraries must come from the sources next to them (the build id is
+    a hash of the sources, flags and defines; socceraction_amd/build.py)."""
+    from . import build as _build
+    expected = {DEFAULT_LIB: (), DEBUG_LIB: _build.DEBUG_DEFINES}
+    if os.path.abspath(path) not in expected or not os.path.isdir(_build.CSRC):
+        return  # an explicitly chosen variant build
+    want = _build.build_id(expected[os.path.abspath(path)])
+    got = (lib.sa_build_id() or b'').decode()
+    if got != want:
+        raise ImportError(f'{path} was built from other sources (build id {got}, sources {want}): '
+                          'rebuild with python -m socceraction_amd.build')
 
 
 def lib() -> ctypes.CDLL:
     return load_library()
 
 
+def shutdown() -> None:
+    """Free the library's cached device scratch (sa_shutdown)."""
+    if _lib is not None:
+        check(_lib.sa_shutdown())
+
+
 def check(rc: int) -> None:
-    """Map a C-ABI status to the reference's exception types."""
+    """Map a C-ABI status to the reference's exception types.  With the debug build every call
+    is followed by the device bounds-check collection (synchronises the device)."""
+    if rc == SA_OK and DEBUG:
+        rc = lib().sa_debug_check()
     if rc == SA_OK:
         return
     msg = (lib().sa_last_error() or b'').decode(errors='replace')

@@ -1,8 +1,16 @@
-// Error reporting and version entry points of the C ABI.
+// Runtime pieces of the C ABI: error reporting, version / build id, the per-device scratch
+// arena (SURVEY.md §8(b) conventions) and the debug-build check collector.
 #include <cstdarg>
 #include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <vector>
 
 #include "sa_internal.h"
+
+#ifndef SA_BUILD_ID
+#define SA_BUILD_ID "unversioned"
+#endif
 
 namespace sa {
 static thread_local char g_err[512] = "";
@@ -21,7 +29,122 @@ int check_hip(hipError_t e, const char* what) {
 }
 
 int check_launch(const char* what) { return check_hip(hipGetLastError(), what); }
+
+// ------------------------------------------------------------------------ scratch arena
+// Library-owned device scratch, cached per device.  A slot is handed to one call at a time;
+// when the call releases it, an event recorded on the call's stream marks when the device is
+// done with it, so the slot is reused immediately by the same stream (stream order) and by
+// another stream once that event has completed.  Guarded by one mutex; freed by sa_shutdown().
+namespace {
+struct Slot {
+  int dev;
+  void* ptr;
+  size_t bytes;
+  hipStream_t last;
+  hipEvent_t done;
+  bool busy;
+};
+std::mutex g_arena_mu;
+std::vector<Slot> g_slots;
+}  // namespace
+
+int scratch_acquire(size_t bytes, hipStream_t st, Scratch* out) {
+  int dev = 0;
+  int rc = check_hip(hipGetDevice(&dev), "hipGetDevice");
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(g_arena_mu);
+  for (size_t i = 0; i < g_slots.size(); ++i) {
+    Slot& s = g_slots[i];
+    if (s.dev != dev || s.busy || s.bytes < bytes) continue;
+    if (s.last != st && hipEventQuery(s.done) != hipSuccess) continue;  // still in use elsewhere
+    s.busy = true;
+    out->ptr = s.ptr;
+    out->slot = (int)i;
+    return SA_OK;
+  }
+  size_t cap = 64 * 1024;
+  while (cap < bytes) cap *= 2;
+  Slot s{dev, nullptr, cap, st, nullptr, true};
+  if (hipMalloc(&s.ptr, cap) != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(SA_ENOMEM, "scratch arena: hipMalloc of %zu bytes failed", cap);
+  }
+  if ((rc = check_hip(hipEventCreateWithFlags(&s.done, hipEventDisableTiming), "hipEventCreate"))) {
+    (void)hipFree(s.ptr);
+    return rc;
+  }
+  g_slots.push_back(s);
+  out->ptr = s.ptr;
+  out->slot = (int)g_slots.size() - 1;
+  return SA_OK;
+}
+
+void scratch_release(const Scratch& s, hipStream_t st) {
+  if (s.slot < 0) return;
+  std::lock_guard<std::mutex> lk(g_arena_mu);
+  Slot& sl = g_slots[(size_t)s.slot];
+  (void)hipEventRecord(sl.done, st);
+  sl.last = st;
+  sl.busy = false;
+}
+
+// ------------------------------------------------------------------------ debug collector
+namespace {
+std::mutex g_dbg_mu;
+std::vector<debug_poll_fn>& polls() {
+  static std::vector<debug_poll_fn> v;
+  return v;
+}
+}  // namespace
+
+bool register_debug_poll(debug_poll_fn fn) {
+  std::lock_guard<std::mutex> lk(g_dbg_mu);
+  polls().push_back(fn);
+  return true;
+}
 }  // namespace sa
+
+using namespace sa;
 
 extern "C" int sa_abi_version(void) { return SA_ABI_VERSION; }
 extern "C" const char* sa_last_error(void) { return sa::g_err; }
+
+// The build id is also kept as a plain marker string, so a build script can tell which sources
+// a library file came from without loading it.
+static const char kBuildMarker[] = "sa-build-id:" SA_BUILD_ID;
+extern "C" const char* sa_build_id(void) { return kBuildMarker + 12; }
+
+extern "C" int sa_debug_enabled(void) { return SA_DEBUG; }
+
+extern "C" int sa_debug_check(void) {
+#if SA_DEBUG
+  int rc = check_hip(hipDeviceSynchronize(), "hipDeviceSynchronize");
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(g_dbg_mu);
+  char msg[400];
+  for (debug_poll_fn fn : polls()) {
+    const int r = fn(msg, (int)sizeof(msg));
+    if (r < 0) return fail(SA_EHIP, "sa_debug_check: reading the device record failed");
+    if (r > 0) return fail(SA_EDATA, "%s", msg);
+  }
+#endif
+  return SA_OK;
+}
+
+extern "C" int sa_shutdown(void) {
+  std::lock_guard<std::mutex> lk(g_arena_mu);
+  int rc = SA_OK;
+  int cur = 0;
+  (void)hipGetDevice(&cur);
+  for (Slot& s : g_slots) {
+    (void)hipSetDevice(s.dev);
+    if (s.done) {
+      if (!rc) rc = check_hip(hipEventSynchronize(s.done), "sa_shutdown: hipEventSynchronize");
+      (void)hipEventDestroy(s.done);
+    }
+    if (s.ptr && !rc) rc = check_hip(hipFree(s.ptr), "sa_shutdown: hipFree");
+  }
+  (void)hipSetDevice(cur);
+  g_slots.clear();
+  return rc;
+}

@@ -8,6 +8,7 @@
 #include <stdint.h>
 
 #include "../../include/socceraction_amd.h"
+#include "sa_debug.h"
 
 namespace sa {
 

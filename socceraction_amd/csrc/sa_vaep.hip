@@ -1,10 +1,10 @@
 // VAEP / Atomic-VAEP hot-path kernels for gfx950 (MI355X).
 //
-//   bool_features_kernel  one-hot + team features (gamestates + flip fused in), bool block
-//   num_features_kernel   time / location / polar / movement / deltas / ids, f64 + i64 blocks
-//   goalscore_kernel      segmented exclusive scan (one workgroup per segment)
-//   labels_kernel         scores / concedes / goal_from_shot look-ahead
-//   formula_kernel        offensive / defensive / vaep value (f64 or f32)
+//   bool_colgroup_kernel     one-hot + team features (gamestates + flip fused in), bool block
+//   num_features_kernel      time / location / polar / movement / deltas / ids, f64 + i64 blocks
+//   goalscore_wave16_kernel  segmented exclusive scan (one wave per segment)
+//   labels_kernel            scores / concedes / goal_from_shot look-ahead
+//   formula_kernel           offensive / defensive / vaep value (f64 or f32)
 //
 // All of it is HBM-bound byte/int/f64 streaming; nothing here is GEMM-shaped.  The output
 // is ~94 % of the traffic, so the kernels are built around full-width stores:
@@ -12,9 +12,14 @@
 //    so one store instruction writes 1 KiB of one column;
 //  * f64 / i64 columns: a lane owns 2 consecutive actions (one 16-B store), so one store
 //    instruction writes 1 KiB of one column.
-// Long runs per column per wave matter (see bool_features_kernel).  Game-state windows
+// Long runs per column per wave matter (see bool_colgroup_kernel).  Game-state windows
 // never leave registers: window i of action j is row j - min(i, j - segment_start)
 // (vaep/features.py:83-88), built with funnel shifts from the lane's rows j0-8 .. j0+15.
+//
+// Compile-time knobs (the default build is the measured configuration; variants are built
+// with `python -m socceraction_amd.build -DNAME=V --variant=tag`): SA_NT_STORES (non-temporal
+// stores), SA_XCD_REMAP (XCD-contiguous block order), SA_CG_COLS (bool columns per wave),
+// SA_DEBUG (device bounds checks, sa_debug.h).
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -28,33 +33,19 @@
 #ifndef SA_NT_STORES
 #define SA_NT_STORES 1
 #endif
-#ifndef SA_BOOL_MODE
-// bool block: 0 = one wave per 1024-row tile, 1 = one wave per (tile, window),
-// 2 = one wave per (tile, column group) in XCD-contiguous sweep order
-#define SA_BOOL_MODE 2
-#endif
 #ifndef SA_XCD_REMAP
 #define SA_XCD_REMAP 1  // block -> output range mapping that gives each XCD a contiguous part
-#endif
-#ifndef SA_GS_WAVE
-#define SA_GS_WAVE 1  // goalscore: one wave per segment instead of one workgroup
-#endif
-#ifndef SA_FORMULA_VEC
-#define SA_FORMULA_VEC 1  // formula: 16-B vector loads of each lane's rows
 #endif
 
 namespace sa {
 
 constexpr int WAVE = 64;
 constexpr int LANE_ACTS = 16;
-#ifndef SA_NUM_PAIRS
-#define SA_NUM_PAIRS 1
-#endif
 #ifndef SA_CG_COLS
 #define SA_CG_COLS 32  // bool_colgroup_kernel: target columns per wave
 #endif
 constexpr int BLOCK_WAVES = 4;
-constexpr int NUM_PAIRS = SA_NUM_PAIRS;         // 2-action pairs per lane in num_features_kernel
+constexpr int NUM_PAIRS = 1;                    // 2-action pairs per lane in num_features_kernel
 constexpr int WAVE_ACTS = 128 * NUM_PAIRS;      // actions per wave in num_features_kernel
 constexpr int BLOCK_ACTS = WAVE_ACTS * BLOCK_WAVES;
 
@@ -90,6 +81,7 @@ static inline unsigned xcd_grid(int64_t blocks) {
 // Element offset of (row j, column c) in a tiled column-major block with C columns.  A
 // lane's 16 (or 2) rows never straddle a tile because R % 16 == 0.
 __device__ __forceinline__ int64_t tile_off(int64_t j, int64_t c, int64_t C, int64_t R) {
+  SA_DCHECK(j >= 0 && c >= 0 && c < C && R > 0 && R % 16 == 0, j);
   const int64_t t = j / R;
   return t * C * R + c * R + (j - t * R);
 }
@@ -104,12 +96,14 @@ __device__ __forceinline__ SegCursor seg_at(const sa_actions& A, int64_t j) {
   c.g = find_segment(A.seg_off, A.n_segments, j);
   c.s = A.seg_off[c.g];
   c.e = A.seg_off[c.g + 1];
+  SA_DCHECK(c.g >= 0 && c.g < A.n_segments && c.s <= j && j < c.e, j);
   return c;
 }
 
 __device__ __forceinline__ void seg_advance(const sa_actions& A, SegCursor& c, int64_t j) {
   while (j >= c.e) {
     ++c.g;
+    SA_DGUARD(c.g < A.n_segments, j, --c.g; break);
     c.s = c.e;
     c.e = A.seg_off[c.g + 1];
   }
@@ -143,31 +137,30 @@ __device__ __forceinline__ void st16(P* p, V v) {
 
 // Stores into tiled blocks: `base` already points at the lane's (tile, row) position of
 // column 0, so column c is c * R elements further.
-__device__ __forceinline__ void st_bool16(uint8_t* __restrict__ base, int64_t col, int64_t R,
+__device__ __forceinline__ void st_bool16(uint8_t* __restrict__ base, int64_t col, int64_t C, int64_t R,
                                           uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
   u32x4 v = {w0, w1, w2, w3};
+  SA_DGUARD(col >= 0 && col < C, col, return);
   st16(base + col * R, v);
 }
 
-__device__ __forceinline__ void st_f64x2(double* __restrict__ base, int64_t col, int64_t R,
+__device__ __forceinline__ void st_f64x2(double* __restrict__ base, int64_t col, int64_t C, int64_t R,
                                          double v0, double v1) {
   f64x2 v = {v0, v1};
+  SA_DGUARD(col >= 0 && col < C, col, return);
   st16(base + col * R, v);
 }
 
-__device__ __forceinline__ void st_i64x2(int64_t* __restrict__ base, int64_t col, int64_t R,
+__device__ __forceinline__ void st_i64x2(int64_t* __restrict__ base, int64_t col, int64_t C, int64_t R,
                                          int64_t v0, int64_t v1) {
   i64x2 v = {(long long)v0, (long long)v1};
+  SA_DGUARD(col >= 0 && col < C, col, return);
   st16(base + col * R, v);
 }
 
 // nan_to_num(arctan(dy / dx)) of vaep/features.py:376 (atan(+-inf) = +-pi/2, 0/0 -> 0)
 __device__ __forceinline__ double polar_angle(double dy, double dx) {
-#if SA_PROBE_NOATAN  // timing probe only (wrong results): no ocml atan
-  const double a = dy / dx;
-#else
   const double a = atan(dy / dx);
-#endif
   return isnan(a) ? 0.0 : a;
 }
 
@@ -193,353 +186,7 @@ __device__ __forceinline__ void goal_bytes(uint32_t tw, uint32_t rw, bool atomic
 
 // ------------------------------------------------------------------------------ bool block
 // actiontype_onehot, result_onehot, actiontype_result_onehot, bodypart_onehot, team.
-// A wave owns BOOL_G runs of 1024 consecutive actions; lane l owns actions 16l .. 16l+15 of
-// every run, so one store instruction writes 1 KiB of one column and the wave writes
-// BOOL_G KiB of each column back to back (long runs per column keep HBM rows open: the
-// column-major layout otherwise scatters a wave's output over 515 streams 16 MB apart).
-#ifndef SA_BOOL_G
-#define SA_BOOL_G 1
-#endif
-constexpr int BOOL_G = SA_BOOL_G;
-constexpr int BOOL_WAVE_ACTS = 1024 * BOOL_G;
-constexpr int BOOL_BLOCK_ACTS = BOOL_WAVE_ACTS * BLOCK_WAVES;
-
-template <bool ATOMIC, bool EXPLICIT>
-__global__ __launch_bounds__(256) void bool_features_kernel(FeatArgs args) {
-  __shared__ int32_t team_lds[BLOCK_WAVES][BOOL_WAVE_ACTS + 8];
-  const int lane = threadIdx.x & (WAVE - 1);
-  const int wv = threadIdx.x / WAVE;
-  const sa_actions& A = args.a;
-  const sa_feature_plan& P = args.p;
-  const int64_t n = A.n;
-  const int K = P.nb_prev_actions;
-  const int64_t R = args.Rb;
-  const int64_t wave_base = ((int64_t)blockIdx.x * BLOCK_WAVES + wv) * BOOL_WAVE_ACTS;
-  const sa_frame& F0 = A.frames[0];
-  const int tcol = P.bool_col[SA_XFN_TEAM];
-  const bool need_team = tcol >= 0 && K > 1;
-  int64_t j0[BOOL_G];
-  uint8_t* bb[BOOL_G];  // column 0 of the lane's 16 rows in the tiled bool block
-#pragma unroll
-  for (int g = 0; g < BOOL_G; ++g) {
-    j0[g] = wave_base + g * 1024 + (int64_t)lane * LANE_ACTS;
-    bb[g] = args.bout + tile_off(j0[g], 0, args.Cb, R);
-  }
-
-  // d = min(j - seg_start, 15) per action; rows >= n keep d = 0 (windows stay in range)
-  uint32_t dw[BOOL_G][4];
-#pragma unroll
-  for (int g = 0; g < BOOL_G; ++g) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) dw[g][q] = 0;
-    if (!EXPLICIT && j0[g] < n) {
-      SegCursor c = seg_at(A, j0[g]);
-#pragma unroll
-      for (int m = 0; m < LANE_ACTS; ++m) {
-        const int64_t j = j0[g] + m;
-        if (j < n) {
-          seg_advance(A, c, j);
-          const int64_t dd = j - c.s;
-          const int d = dd > 15 ? 15 : (int)dd;
-          dw[g][m >> 2] |= (uint32_t)d << (8 * (m & 3));
-        }
-      }
-    }
-  }
-  if (!EXPLICIT && need_team) {  // team codes of rows wave_base-8 .. wave_base+1024G-1 -> LDS
-    int32_t* tl = team_lds[wv];
-#pragma unroll
-    for (int g = 0; g < BOOL_G; ++g) {
-#pragma unroll
-      for (int m = 0; m < LANE_ACTS; ++m)
-        tl[8 + g * 1024 + lane * LANE_ACTS + m] = ld_or0(F0.team, j0[g] + m, n);
-    }
-    if (lane < 8) tl[lane] = ld_or0(F0.team, wave_base - 8 + lane, n);
-  }
-  __syncthreads();
-  if (j0[0] >= n) return;
-  uint32_t TR[BOOL_G][6], RR[BOOL_G][6], BR[BOOL_G][6];  // rows j0-8 .. j0+15, shifted per window
-  uint32_t tw[BOOL_G][4], rw[BOOL_G][4], bw[BOOL_G][4];  // window i of the lane's actions
-  if (!EXPLICIT) {
-#pragma unroll
-    for (int g = 0; g < BOOL_G; ++g) {
-      const int64_t wbase = j0[g] / 4 - 2;  // word index of row j0-8
-#pragma unroll
-      for (int k = 0; k < 6; ++k) {
-        TR[g][k] = ld_u8x4(F0.type_id, wbase + k, n);
-        RR[g][k] = ATOMIC ? 0u : ld_u8x4(F0.result_id, wbase + k, n);
-        BR[g][k] = ld_u8x4(F0.bodypart_id, wbase + k, n);
-      }
-    }
-  }
-  const int c_type = P.bool_col[SA_XFN_ACTIONTYPE_ONEHOT];
-  const int c_res = ATOMIC ? -1 : P.bool_col[SA_XFN_RESULT_ONEHOT];
-  const int c_tr = ATOMIC ? -1 : P.bool_col[SA_XFN_ACTIONTYPE_RESULT_ONEHOT];
-  const int c_bp = P.bool_col[SA_XFN_BODYPART_ONEHOT];
-  for (int i = 0; i < K; ++i) {
-#pragma unroll
-    for (int g = 0; g < BOOL_G; ++g) {
-      if (EXPLICIT) {
-        const sa_frame& Fi = A.frames[i];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          tw[g][q] = ld_u8x4(Fi.type_id, j0[g] / 4 + q, n);
-          rw[g][q] = ATOMIC ? 0u : ld_u8x4(Fi.result_id, j0[g] / 4 + q, n);
-          bw[g][q] = ld_u8x4(Fi.bodypart_id, j0[g] / 4 + q, n);
-        }
-      } else if (i == 0) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          tw[g][q] = TR[g][2 + q];
-          rw[g][q] = RR[g][2 + q];
-          bw[g][q] = BR[g][2 + q];
-        }
-      } else {
-        shift_rows(TR[g]);
-        if (!ATOMIC) shift_rows(RR[g]);
-        shift_rows(BR[g]);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const uint32_t mk = ge_mask(dw[g][q], i);  // actions whose window i is a new row
-          tw[g][q] = (TR[g][2 + q] & mk) | (tw[g][q] & ~mk);
-          rw[g][q] = (RR[g][2 + q] & mk) | (rw[g][q] & ~mk);
-          bw[g][q] = (BR[g][2 + q] & mk) | (bw[g][q] & ~mk);
-        }
-      }
-    }
-    if (c_type >= 0) {
-      if (!ATOMIC) {
-        for (int t = 0; t < N_TYPES; ++t) {
-#pragma unroll
-          for (int g = 0; g < BOOL_G; ++g)
-            st_bool16(bb[g], c_type + i * N_TYPES + t, R, bytes_eq(tw[g][0], t),
-                      bytes_eq(tw[g][1], t), bytes_eq(tw[g][2], t), bytes_eq(tw[g][3], t));
-        }
-      } else {
-        // 33 atomic names, 32 unique: 'interception' (ids 10 and 24) is ONE column true for
-        // both ids (atomic/vaep/features.py:114-132 + atomic/spadl/config.py:25-36)
-        for (int u = 0; u < N_ATOMIC_NAMES; ++u) {
-          const uint32_t id = u <= 23 ? (uint32_t)u : (uint32_t)u + 1;
-#pragma unroll
-          for (int g = 0; g < BOOL_G; ++g) {
-            uint32_t m0 = bytes_eq(tw[g][0], id), m1 = bytes_eq(tw[g][1], id),
-                     m2 = bytes_eq(tw[g][2], id), m3 = bytes_eq(tw[g][3], id);
-            if (u == 10) {
-              m0 |= bytes_eq(tw[g][0], AT_INTERCEPTION2);
-              m1 |= bytes_eq(tw[g][1], AT_INTERCEPTION2);
-              m2 |= bytes_eq(tw[g][2], AT_INTERCEPTION2);
-              m3 |= bytes_eq(tw[g][3], AT_INTERCEPTION2);
-            }
-            st_bool16(bb[g], c_type + i * N_ATOMIC_NAMES + u, R, m0, m1, m2, m3);
-          }
-        }
-      }
-    }
-    if (c_res >= 0) {
-      for (int r = 0; r < N_RESULTS; ++r) {
-#pragma unroll
-        for (int g = 0; g < BOOL_G; ++g)
-          st_bool16(bb[g], c_res + i * N_RESULTS + r, R, bytes_eq(rw[g][0], r),
-                    bytes_eq(rw[g][1], r), bytes_eq(rw[g][2], r), bytes_eq(rw[g][3], r));
-      }
-    }
-    if (c_tr >= 0) {
-      // code = type*6 + result per byte (type <= 22, result <= 5: no carry between bytes)
-      uint32_t cw[BOOL_G][4];
-#pragma unroll
-      for (int g = 0; g < BOOL_G; ++g) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) cw[g][q] = (tw[g][q] << 2) + (tw[g][q] << 1) + rw[g][q];
-      }
-      const int64_t cb = c_tr + (int64_t)i * N_TYPES * N_RESULTS;
-      for (int code = 0; code < N_TYPES * N_RESULTS; ++code) {
-#pragma unroll
-        for (int g = 0; g < BOOL_G; ++g)
-          st_bool16(bb[g], cb + code, R, bytes_eq(cw[g][0], code),
-                    bytes_eq(cw[g][1], code), bytes_eq(cw[g][2], code), bytes_eq(cw[g][3], code));
-      }
-    }
-    if (c_bp >= 0) {
-      for (int b = 0; b < N_BODYPARTS; ++b) {
-#pragma unroll
-        for (int g = 0; g < BOOL_G; ++g)
-          st_bool16(bb[g], c_bp + i * N_BODYPARTS + b, R, bytes_eq(bw[g][0], b),
-                    bytes_eq(bw[g][1], b), bytes_eq(bw[g][2], b), bytes_eq(bw[g][3], b));
-      }
-    }
-    if (need_team && i >= 1) {  // team_i = team[a_i] == team[a0] (features.py:448-452)
-#pragma unroll
-      for (int g = 0; g < BOOL_G; ++g) {
-        uint32_t m[4] = {0, 0, 0, 0};
-#pragma unroll
-        for (int mm = 0; mm < LANE_ACTS; ++mm) {
-          int32_t t0, ti;
-          if (EXPLICIT) {
-            t0 = ld_or0(A.frames[0].team, j0[g] + mm, n);
-            ti = ld_or0(A.frames[i].team, j0[g] + mm, n);
-          } else {
-            const int d = (int)byte_of(dw[g][mm >> 2], mm & 3);
-            const int s = d < i ? d : i;
-            const int32_t* tl = team_lds[wv] + 8 + g * 1024 + lane * LANE_ACTS + mm;
-            t0 = tl[0];
-            ti = tl[-s];
-          }
-          m[mm >> 2] |= (uint32_t)(t0 == ti) << (8 * (mm & 3));
-        }
-        st_bool16(bb[g], tcol + (i - 1), R, m[0], m[1], m[2], m[3]);
-      }
-    }
-  }
-}
-
-// Window-split form: a workgroup owns one 1024-row tile and has one wave per game-state
-// window; wave i writes only window i's columns (~172 of the 515 at k = 3).  Same stores,
-// same tile image as bool_features_kernel, but 3x as many waves of 1/3 the length, so the
-// drain at the end of a launch (a 16M-action launch is only ~2.5 whole-tile waves per
-// resident slot) leaves far less of the chip idle.  The tile's team codes are staged in LDS
-// once for all its waves.
-constexpr int BOOL_TILE = 1024;
-
-template <bool ATOMIC, bool EXPLICIT>
-__global__ __launch_bounds__(64 * SA_MAX_FRAMES) void bool_window_kernel(FeatArgs args) {
-  __shared__ int32_t team_lds[BOOL_TILE + 8];
-  const int lane = threadIdx.x & (WAVE - 1);
-  const int i = threadIdx.x / WAVE;  // the window this wave writes
-  const sa_actions& A = args.a;
-  const sa_feature_plan& P = args.p;
-  const int64_t n = A.n;
-  const int K = P.nb_prev_actions;
-  const int64_t R = args.Rb;
-  const int64_t tile0 = xcd_logical_block() * BOOL_TILE;
-  const int64_t j0 = tile0 + (int64_t)lane * LANE_ACTS;
-  const sa_frame& F0 = A.frames[0];
-  const int tcol = P.bool_col[SA_XFN_TEAM];
-  const bool need_team = tcol >= 0 && K > 1;
-  if (!EXPLICIT && need_team) {  // team codes of rows tile0-8 .. tile0+1023 -> LDS
-    for (int k = threadIdx.x; k < BOOL_TILE + 8; k += blockDim.x)
-      team_lds[k] = ld_or0(F0.team, tile0 - 8 + k, n);
-  }
-  __syncthreads();
-  if (j0 >= n) return;
-  uint8_t* bb = args.bout + tile_off(j0, 0, args.Cb, R);
-  // d = min(j - seg_start, 15) per action (only windows i >= 1 need it)
-  uint32_t dw[4] = {0, 0, 0, 0};
-  if (!EXPLICIT && i > 0) {
-    SegCursor c = seg_at(A, j0);
-#pragma unroll
-    for (int m = 0; m < LANE_ACTS; ++m) {
-      const int64_t j = j0 + m;
-      if (j < n) {
-        seg_advance(A, c, j);
-        const int64_t dd = j - c.s;
-        const int d = dd > 15 ? 15 : (int)dd;
-        dw[m >> 2] |= (uint32_t)d << (8 * (m & 3));
-      }
-    }
-  }
-  uint32_t tw[4], rw[4], bw[4];  // window i of the lane's 16 actions
-  if (EXPLICIT) {
-    const sa_frame& Fi = A.frames[i];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      tw[q] = ld_u8x4(Fi.type_id, j0 / 4 + q, n);
-      rw[q] = ATOMIC ? 0u : ld_u8x4(Fi.result_id, j0 / 4 + q, n);
-      bw[q] = ld_u8x4(Fi.bodypart_id, j0 / 4 + q, n);
-    }
-  } else {
-    uint32_t TR[6], RR[6], BR[6];  // rows j0-8 .. j0+15
-    const int64_t wbase = j0 / 4 - 2;
-#pragma unroll
-    for (int k = 0; k < 6; ++k) {
-      TR[k] = ld_u8x4(F0.type_id, wbase + k, n);
-      RR[k] = ATOMIC ? 0u : ld_u8x4(F0.result_id, wbase + k, n);
-      BR[k] = ld_u8x4(F0.bodypart_id, wbase + k, n);
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      tw[q] = TR[2 + q];
-      rw[q] = RR[2 + q];
-      bw[q] = BR[2 + q];
-    }
-    for (int s = 1; s <= i; ++s) {  // window s = window s-1 shifted one row, clamped bytes kept
-      shift_rows(TR);
-      if (!ATOMIC) shift_rows(RR);
-      shift_rows(BR);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const uint32_t mk = ge_mask(dw[q], s);
-        tw[q] = (TR[2 + q] & mk) | (tw[q] & ~mk);
-        rw[q] = (RR[2 + q] & mk) | (rw[q] & ~mk);
-        bw[q] = (BR[2 + q] & mk) | (bw[q] & ~mk);
-      }
-    }
-  }
-  const int c_type = P.bool_col[SA_XFN_ACTIONTYPE_ONEHOT];
-  const int c_res = ATOMIC ? -1 : P.bool_col[SA_XFN_RESULT_ONEHOT];
-  const int c_tr = ATOMIC ? -1 : P.bool_col[SA_XFN_ACTIONTYPE_RESULT_ONEHOT];
-  const int c_bp = P.bool_col[SA_XFN_BODYPART_ONEHOT];
-  if (c_type >= 0) {
-    if (!ATOMIC) {
-      for (int t = 0; t < N_TYPES; ++t)
-        st_bool16(bb, c_type + i * N_TYPES + t, R, bytes_eq(tw[0], t), bytes_eq(tw[1], t),
-                  bytes_eq(tw[2], t), bytes_eq(tw[3], t));
-    } else {
-      // 33 atomic names, 32 unique: 'interception' (ids 10 and 24) is ONE column true for
-      // both ids (atomic/vaep/features.py:114-132 + atomic/spadl/config.py:25-36)
-      for (int u = 0; u < N_ATOMIC_NAMES; ++u) {
-        const uint32_t id = u <= 23 ? (uint32_t)u : (uint32_t)u + 1;
-        uint32_t m0 = bytes_eq(tw[0], id), m1 = bytes_eq(tw[1], id), m2 = bytes_eq(tw[2], id),
-                 m3 = bytes_eq(tw[3], id);
-        if (u == 10) {
-          m0 |= bytes_eq(tw[0], AT_INTERCEPTION2);
-          m1 |= bytes_eq(tw[1], AT_INTERCEPTION2);
-          m2 |= bytes_eq(tw[2], AT_INTERCEPTION2);
-          m3 |= bytes_eq(tw[3], AT_INTERCEPTION2);
-        }
-        st_bool16(bb, c_type + i * N_ATOMIC_NAMES + u, R, m0, m1, m2, m3);
-      }
-    }
-  }
-  if (c_res >= 0) {
-    for (int r = 0; r < N_RESULTS; ++r)
-      st_bool16(bb, c_res + i * N_RESULTS + r, R, bytes_eq(rw[0], r), bytes_eq(rw[1], r),
-                bytes_eq(rw[2], r), bytes_eq(rw[3], r));
-  }
-  if (c_tr >= 0) {
-    // code = type*6 + result per byte (type <= 22, result <= 5: no carry between bytes)
-    uint32_t cw[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) cw[q] = (tw[q] << 2) + (tw[q] << 1) + rw[q];
-    const int64_t cb = c_tr + (int64_t)i * N_TYPES * N_RESULTS;
-    for (int code = 0; code < N_TYPES * N_RESULTS; ++code)
-      st_bool16(bb, cb + code, R, bytes_eq(cw[0], code), bytes_eq(cw[1], code),
-                bytes_eq(cw[2], code), bytes_eq(cw[3], code));
-  }
-  if (c_bp >= 0) {
-    for (int b = 0; b < N_BODYPARTS; ++b)
-      st_bool16(bb, c_bp + i * N_BODYPARTS + b, R, bytes_eq(bw[0], b), bytes_eq(bw[1], b),
-                bytes_eq(bw[2], b), bytes_eq(bw[3], b));
-  }
-  if (need_team && i >= 1) {  // team_i = team[a_i] == team[a0] (features.py:448-452)
-    uint32_t m[4] = {0, 0, 0, 0};
-#pragma unroll
-    for (int mm = 0; mm < LANE_ACTS; ++mm) {
-      int32_t t0, ti;
-      if (EXPLICIT) {
-        t0 = ld_or0(A.frames[0].team, j0 + mm, n);
-        ti = ld_or0(A.frames[i].team, j0 + mm, n);
-      } else {
-        const int d = (int)byte_of(dw[mm >> 2], mm & 3);
-        const int s = d < i ? d : i;
-        const int32_t* tl = team_lds + 8 + lane * LANE_ACTS + mm;
-        t0 = tl[0];
-        ti = tl[-s];
-      }
-      m[mm >> 2] |= (uint32_t)(t0 == ti) << (8 * (mm & 3));
-    }
-    st_bool16(bb, tcol + (i - 1), R, m[0], m[1], m[2], m[3]);
-  }
-}
+constexpr int BOOL_TILE = 1024;  // rows per tile of the bool block image
 
 // Column-group form (default): the bool image is swept front to back like a fill.  A wave
 // owns one column group -- `gcols` consecutive block columns -- of one 1024-row tile, so a
@@ -549,11 +196,7 @@ __global__ __launch_bounds__(64 * SA_MAX_FRAMES) void bool_window_kernel(FeatArg
 // windows from the id columns (L2 hits: a tile's groups run back to back on one XCD) and
 // writes only the (family, window, value) columns inside its range.
 constexpr int CG_WAVES = 4;  // waves per workgroup
-#if SA_PROBE_CHEAP  // timing probe only (wrong results): one VALU op per word instead of a compare
-#define CG_EQ(w, v) ((w) ^ (uint32_t)(v))
-#else
 #define CG_EQ(w, v) bytes_eq((w), (v))
-#endif
 
 template <bool ATOMIC, bool EXPLICIT>
 __global__ __launch_bounds__(64 * CG_WAVES) void bool_colgroup_kernel(FeatArgs args, int ngroups,
@@ -605,15 +248,9 @@ __global__ __launch_bounds__(64 * CG_WAVES) void bool_colgroup_kernel(FeatArgs a
     const int64_t wbase = j0 / 4 - 2;
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
-#if SA_PROBE_NOLOAD  // timing probe only (wrong results): no id loads
-      TR[k] = (uint32_t)(wbase + k) * 0x01010101u;
-      RR[k] = TR[k] >> 3;
-      BR[k] = TR[k] >> 5;
-#else
       TR[k] = ld_u8x4(F0.type_id, wbase + k, n);
       RR[k] = ATOMIC ? 0u : ld_u8x4(F0.result_id, wbase + k, n);
       BR[k] = ld_u8x4(F0.bodypart_id, wbase + k, n);
-#endif
     }
   }
   const int c_type = P.bool_col[SA_XFN_ACTIONTYPE_ONEHOT];
@@ -660,7 +297,7 @@ __global__ __launch_bounds__(64 * CG_WAVES) void bool_colgroup_kernel(FeatArgs a
       range(base, ntypes, v0, v1);
       for (int u = v0; u < v1; ++u) {
         if (!ATOMIC) {
-          st_bool16(bb, base + u, R, CG_EQ(tw[0], u), CG_EQ(tw[1], u), CG_EQ(tw[2], u),
+          st_bool16(bb, base + u, args.Cb, R, CG_EQ(tw[0], u), CG_EQ(tw[1], u), CG_EQ(tw[2], u),
                     CG_EQ(tw[3], u));
         } else {
           // 33 atomic names, 32 unique: 'interception' (ids 10 and 24) is ONE column true for
@@ -674,7 +311,7 @@ __global__ __launch_bounds__(64 * CG_WAVES) void bool_colgroup_kernel(FeatArgs a
             m2 |= CG_EQ(tw[2], AT_INTERCEPTION2);
             m3 |= CG_EQ(tw[3], AT_INTERCEPTION2);
           }
-          st_bool16(bb, base + u, R, m0, m1, m2, m3);
+          st_bool16(bb, base + u, args.Cb, R, m0, m1, m2, m3);
         }
       }
     }
@@ -682,7 +319,7 @@ __global__ __launch_bounds__(64 * CG_WAVES) void bool_colgroup_kernel(FeatArgs a
       const int base = c_res + i * N_RESULTS;
       range(base, N_RESULTS, v0, v1);
       for (int r = v0; r < v1; ++r)
-        st_bool16(bb, base + r, R, CG_EQ(rw[0], r), CG_EQ(rw[1], r), CG_EQ(rw[2], r),
+        st_bool16(bb, base + r, args.Cb, R, CG_EQ(rw[0], r), CG_EQ(rw[1], r), CG_EQ(rw[2], r),
                   CG_EQ(rw[3], r));
     }
     if (c_tr >= 0) {
@@ -694,7 +331,7 @@ __global__ __launch_bounds__(64 * CG_WAVES) void bool_colgroup_kernel(FeatArgs a
 #pragma unroll
         for (int q = 0; q < 4; ++q) cw[q] = (tw[q] << 2) + (tw[q] << 1) + rw[q];
         for (int code = v0; code < v1; ++code)
-          st_bool16(bb, base + code, R, CG_EQ(cw[0], code), CG_EQ(cw[1], code),
+          st_bool16(bb, base + code, args.Cb, R, CG_EQ(cw[0], code), CG_EQ(cw[1], code),
                     CG_EQ(cw[2], code), CG_EQ(cw[3], code));
       }
     }
@@ -702,7 +339,7 @@ __global__ __launch_bounds__(64 * CG_WAVES) void bool_colgroup_kernel(FeatArgs a
       const int base = c_bp + i * N_BODYPARTS;
       range(base, N_BODYPARTS, v0, v1);
       for (int b = v0; b < v1; ++b)
-        st_bool16(bb, base + b, R, CG_EQ(bw[0], b), CG_EQ(bw[1], b), CG_EQ(bw[2], b),
+        st_bool16(bb, base + b, args.Cb, R, CG_EQ(bw[0], b), CG_EQ(bw[1], b), CG_EQ(bw[2], b),
                   CG_EQ(bw[3], b));
     }
     const int tc = tcol + i - 1;
@@ -717,170 +354,16 @@ __global__ __launch_bounds__(64 * CG_WAVES) void bool_colgroup_kernel(FeatArgs a
         } else {
           const int d = (int)byte_of(dw[mm >> 2], mm & 3);
           const int s = d < i ? d : i;
+          SA_DCHECK(s >= 0 && s <= 8, s);
           const int32_t* tl = team_lds[wv] + 8 + lane * LANE_ACTS + mm;
           t0 = tl[0];
           ti = tl[-s];
         }
         m[mm >> 2] |= (uint32_t)(t0 == ti) << (8 * (mm & 3));
       }
-      st_bool16(bb, tc, R, m[0], m[1], m[2], m[3]);
+      st_bool16(bb, tc, args.Cb, R, m[0], m[1], m[2], m[3]);
     }
   }
-}
-
-// Staged form: short workgroups that each write NW * G consecutive 1-KiB column chunks of one
-// 1024-row tile and exit.  The pure-store probes (profiles/r01g_store_runlen.md) run that shape
-// at 7.2 - 7.4 TB/s on every allocation, where the column-group shape (one 31-KiB run per
-// wave) spreads 5.7 - 7.1 TB/s with the placement; what it costs is a per-workgroup prologue,
-// so that prologue is one cheap LDS pass:
-//  1. raw ids + team codes of rows tile0-8 .. tile0+1023 -> LDS (coalesced), segment starts
-//     inside that window -> LDS flags (rows >= n are flagged too, so their windows stay on
-//     the row itself, as in the other forms);
-//  2. each thread builds 4 consecutive rows' window codes -- per window i: type (atomic: the
-//     column index of its name), result, type*6+result, bodypart, team[a_i]==team[a0] -- as
-//     byte rows of 1024 in LDS (window i = window i-1's row - 1 unless that row starts a
-//     segment: vaep/features.py:83-88);
-//  3. wave w writes columns c0 + s*NW + w (s < G): one ds_read_b128 of the column's code row
-//     per lane, a SWAR compare with the column's value, one 16-B store.
-// Windowed mode only (EXPLICIT frames use the column-group kernel).
-struct StagedCfg {
-  int nw, g;  // waves per workgroup, columns per wave
-};
-
-__device__ __forceinline__ bool staged_col(int c, int base, int nv, int K, int& i, int& v) {
-  if (base < 0 || c < base || c >= base + K * nv) return false;
-  i = (c - base) / nv;
-  v = c - base - i * nv;
-  return true;
-}
-
-template <bool ATOMIC>
-__global__ __launch_bounds__(1024) void bool_staged_kernel(FeatArgs args, int ncg, int nw, int g,
-                                                           int64_t n_logical) {
-  extern __shared__ __align__(16) uint8_t lds[];
-  const int K = args.p.nb_prev_actions;
-  constexpr int H = 8, W = BOOL_TILE + H;  // halo rows + window rows
-  uint8_t* typ = lds;                       // [W]
-  uint8_t* res = typ + W;                   // [W]
-  uint8_t* bpt = res + W;                   // [W]
-  uint8_t* flg = bpt + W;                   // [W] row starts a segment (or is >= n)
-  int32_t* tea = (int32_t*)(lds + ((4 * W + 15) & ~15));  // [W]
-  uint8_t* code = (uint8_t*)(tea + W);      // [(5K-1) x 1024]
-  const int64_t L = xcd_logical_block();
-  if (L >= n_logical) return;
-  const sa_actions& A = args.a;
-  const sa_feature_plan& P = args.p;
-  const int64_t n = A.n;
-  const int64_t chunk = L / ncg;
-  const int cg = (int)(L - chunk * ncg);
-  const int64_t tile0 = chunk * BOOL_TILE, h0 = tile0 - H;
-  const sa_frame& F0 = A.frames[0];
-  const int nt = nw * WAVE, t = threadIdx.x;
-  for (int k = t; k < W; k += nt) {
-    const int64_t j = h0 + k;
-    typ[k] = ld_or0(F0.type_id, j, n);
-    res[k] = ATOMIC ? 0 : ld_or0(F0.result_id, j, n);
-    bpt[k] = ld_or0(F0.bodypart_id, j, n);
-    tea[k] = ld_or0(F0.team, j, n);
-    flg[k] = j >= n;
-  }
-  __syncthreads();
-#ifndef SA_PROBE_STAGED_NOSEG
-#define SA_PROBE_STAGED_NOSEG 0  // timing probe only (wrong results at segment starts)
-#endif
-  if (K > 1 && !SA_PROBE_STAGED_NOSEG) {  // segment starts inside [h0, tile0 + 1024)
-    const int64_t g0 = find_segment(A.seg_off, A.n_segments, h0 > 0 ? h0 : 0);
-    for (int64_t s = g0 + t; s < A.n_segments; s += nt) {
-      const int64_t st = A.seg_off[s];
-      if (st >= tile0 + BOOL_TILE) break;
-      if (st >= h0) flg[st - h0] = 1;
-    }
-    __syncthreads();
-  }
-  if (t < BOOL_TILE / 4) {
-    for (int i = 0; i < K; ++i) {
-      uint32_t wt = 0, wr = 0, wc = 0, wb = 0, ws = 0;
-#pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        const int k0 = H + 4 * t + m;
-        int src = k0;  // window i of row k0: step back while the current row is no segment start
-        for (int s = 0; s < i && !flg[src]; ++s) --src;
-        uint32_t ty = typ[src];
-        if (ATOMIC) ty = ty < AT_INTERCEPTION2 ? ty : (ty == AT_INTERCEPTION2 ? 10u : ty - 1u);
-        const uint32_t re = res[src];
-        wt |= ty << (8 * m);
-        wr |= re << (8 * m);
-        wc |= (ty * N_RESULTS + re) << (8 * m);
-        wb |= (uint32_t)bpt[src] << (8 * m);
-        ws |= (uint32_t)(tea[src] == tea[k0]) << (8 * m);
-      }
-      uint32_t* cw = (uint32_t*)code;
-      cw[(0 * K + i) * 256 + t] = wt;
-      cw[(1 * K + i) * 256 + t] = wr;
-      cw[(2 * K + i) * 256 + t] = wc;
-      cw[(3 * K + i) * 256 + t] = wb;
-      if (i > 0) cw[(4 * K + i - 1) * 256 + t] = ws;
-    }
-  }
-  __syncthreads();
-  const int lane = t & (WAVE - 1), wv = t / WAVE;
-  const int64_t j0 = tile0 + (int64_t)lane * LANE_ACTS;
-  if (j0 >= n) return;
-  uint8_t* bb = args.bout + tile_off(j0, 0, args.Cb, args.Rb);
-  const int ntypes = ATOMIC ? N_ATOMIC_NAMES : N_TYPES;
-  const int c_type = P.bool_col[SA_XFN_ACTIONTYPE_ONEHOT];
-  const int c_res = ATOMIC ? -1 : P.bool_col[SA_XFN_RESULT_ONEHOT];
-  const int c_tr = ATOMIC ? -1 : P.bool_col[SA_XFN_ACTIONTYPE_RESULT_ONEHOT];
-  const int c_bp = P.bool_col[SA_XFN_BODYPART_ONEHOT];
-  const int tcol = P.bool_col[SA_XFN_TEAM];
-  const int cbase = cg * nw * g + wv;
-  for (int s = 0; s < g; ++s) {
-    const int c = cbase + s * nw;
-    if (c >= args.Cb) break;
-    int i, v, row;
-    if (staged_col(c, c_type, ntypes, K, i, v))
-      row = i;
-    else if (staged_col(c, c_res, N_RESULTS, K, i, v))
-      row = K + i;
-    else if (staged_col(c, c_tr, N_TYPES * N_RESULTS, K, i, v))
-      row = 2 * K + i;
-    else if (staged_col(c, c_bp, N_BODYPARTS, K, i, v))
-      row = 3 * K + i;
-    else if (staged_col(c, tcol, 1, K - 1, i, v)) {
-      row = 4 * K + i;
-      v = 1;
-    } else
-      continue;  // not a column of this plan
-    const u32x4 x = *(const u32x4*)(code + row * BOOL_TILE + lane * LANE_ACTS);
-    st_bool16(bb, c, args.Rb, bytes_eq(x[0], v), bytes_eq(x[1], v), bytes_eq(x[2], v),
-              bytes_eq(x[3], v));
-  }
-}
-
-static size_t staged_lds_bytes(int K) {
-  constexpr int W = BOOL_TILE + 8;
-  return (size_t)((4 * W + 15) & ~15) + 4 * W + (size_t)(5 * K - 1) * BOOL_TILE;
-}
-
-// Run-time A/B switches of the launchers (read at each launch)
-static bool env_is(const char* var, const char* val) {
-  const char* e = getenv(var);
-  return e && strcmp(e, val) == 0;
-}
-
-// SA_BOOL_KERNEL = "colgroup" (default) or "staged[:NW[:G]]", read at each launch (A/B runs
-// switch it between calls in one process, on the same allocations)
-static StagedCfg bool_kernel_choice() {
-  StagedCfg c{0, 0};
-  const char* e = getenv("SA_BOOL_KERNEL");
-  if (e && strncmp(e, "staged", 6) == 0) {
-    c.nw = 4;
-    c.g = 4;
-    int nw = 0, g = 0;
-    if (sscanf(e + 6, ":%d:%d", &nw, &g) >= 1 && nw >= 1 && nw <= 16) c.nw = nw;
-    if (g >= 1 && g <= 64) c.g = g;
-  }
-  return c;
 }
 
 // ------------------------------------------------------------------------------ f64/i64 block
@@ -889,6 +372,7 @@ static StagedCfg bool_kernel_choice() {
 // one contiguous [C x 128] slab.
 struct NumCols {  // first column of each transformer in the f64 / i64 blocks (-1 = absent)
   int at, re, bi, ti, tf, sl, el, sp, ep, mv, td, sd, lo, po, mp, di;
+  int nf, ni;  // column counts of the f64 / i64 blocks (bounds checks of the debug build)
 };
 
 struct Win {  // one game-state window of the lane's 2 actions (flipped coordinates)
@@ -902,24 +386,24 @@ __device__ __forceinline__ void emit_window(const NumCols& C, int i, const Win& 
                                             const double (&sx0)[2], const double (&sy0)[2],
                                             const double (&t0)[2], double* __restrict__ fb,
                                             int64_t* __restrict__ ib, int64_t Rf, int64_t Ri) {
-  if (C.at >= 0) st_i64x2(ib, C.at + i, Ri, w.typ[0], w.typ[1]);
-  if (C.re >= 0) st_i64x2(ib, C.re + i, Ri, w.res[0], w.res[1]);
-  if (C.bi >= 0) st_i64x2(ib, C.bi + i, Ri, w.bp[0], w.bp[1]);
-  if (C.ti >= 0) st_i64x2(ib, C.ti + i, Ri, w.per[0], w.per[1]);
+  if (C.at >= 0) st_i64x2(ib, C.at + i, C.ni, Ri, w.typ[0], w.typ[1]);
+  if (C.re >= 0) st_i64x2(ib, C.re + i, C.ni, Ri, w.res[0], w.res[1]);
+  if (C.bi >= 0) st_i64x2(ib, C.bi + i, C.ni, Ri, w.bp[0], w.bp[1]);
+  if (C.ti >= 0) st_i64x2(ib, C.ti + i, C.ni, Ri, w.per[0], w.per[1]);
   if (C.tf >= 0) {
-    st_f64x2(fb, C.tf + 2 * i, Rf, w.ts[0], w.ts[1]);
+    st_f64x2(fb, C.tf + 2 * i, C.nf, Rf, w.ts[0], w.ts[1]);
     // ((period_id - 1) * 45 * 60) + time_seconds   (features.py:313)
-    st_f64x2(fb, C.tf + 2 * i + 1, Rf, (double)((w.per[0] - 1) * 2700) + w.ts[0],
+    st_f64x2(fb, C.tf + 2 * i + 1, C.nf, Rf, (double)((w.per[0] - 1) * 2700) + w.ts[0],
              (double)((w.per[1] - 1) * 2700) + w.ts[1]);
   }
   if (!ATOMIC) {
     if (C.sl >= 0) {
-      st_f64x2(fb, C.sl + 2 * i, Rf, w.c0[0], w.c0[1]);
-      st_f64x2(fb, C.sl + 2 * i + 1, Rf, w.c1[0], w.c1[1]);
+      st_f64x2(fb, C.sl + 2 * i, C.nf, Rf, w.c0[0], w.c0[1]);
+      st_f64x2(fb, C.sl + 2 * i + 1, C.nf, Rf, w.c1[0], w.c1[1]);
     }
     if (C.el >= 0) {
-      st_f64x2(fb, C.el + 2 * i, Rf, w.c2[0], w.c2[1]);
-      st_f64x2(fb, C.el + 2 * i + 1, Rf, w.c3[0], w.c3[1]);
+      st_f64x2(fb, C.el + 2 * i, C.nf, Rf, w.c2[0], w.c2[1]);
+      st_f64x2(fb, C.el + 2 * i + 1, C.nf, Rf, w.c3[0], w.c3[1]);
     }
     if (C.sp >= 0) {
       double dist[2], ang[2];
@@ -929,8 +413,8 @@ __device__ __forceinline__ void emit_window(const NumCols& C, int i, const Win& 
         dist[e] = sqrt(dx * dx + dy * dy);
         ang[e] = polar_angle(dy, dx);
       }
-      st_f64x2(fb, C.sp + 2 * i, Rf, dist[0], dist[1]);
-      st_f64x2(fb, C.sp + 2 * i + 1, Rf, ang[0], ang[1]);
+      st_f64x2(fb, C.sp + 2 * i, C.nf, Rf, dist[0], dist[1]);
+      st_f64x2(fb, C.sp + 2 * i + 1, C.nf, Rf, ang[0], ang[1]);
     }
     if (C.ep >= 0) {
       double dist[2], ang[2];
@@ -940,8 +424,8 @@ __device__ __forceinline__ void emit_window(const NumCols& C, int i, const Win& 
         dist[e] = sqrt(dx * dx + dy * dy);
         ang[e] = polar_angle(dy, dx);
       }
-      st_f64x2(fb, C.ep + 2 * i, Rf, dist[0], dist[1]);
-      st_f64x2(fb, C.ep + 2 * i + 1, Rf, ang[0], ang[1]);
+      st_f64x2(fb, C.ep + 2 * i, C.nf, Rf, dist[0], dist[1]);
+      st_f64x2(fb, C.ep + 2 * i + 1, C.nf, Rf, ang[0], ang[1]);
     }
     if (C.mv >= 0) {
       double mdx[2], mdy[2], mv[2];
@@ -951,9 +435,9 @@ __device__ __forceinline__ void emit_window(const NumCols& C, int i, const Win& 
         mdy[e] = w.c3[e] - w.c1[e];
         mv[e] = sqrt(mdx[e] * mdx[e] + mdy[e] * mdy[e]);
       }
-      st_f64x2(fb, C.mv + 3 * i, Rf, mdx[0], mdx[1]);
-      st_f64x2(fb, C.mv + 3 * i + 1, Rf, mdy[0], mdy[1]);
-      st_f64x2(fb, C.mv + 3 * i + 2, Rf, mv[0], mv[1]);
+      st_f64x2(fb, C.mv + 3 * i, C.nf, Rf, mdx[0], mdx[1]);
+      st_f64x2(fb, C.mv + 3 * i + 1, C.nf, Rf, mdy[0], mdy[1]);
+      st_f64x2(fb, C.mv + 3 * i + 2, C.nf, Rf, mv[0], mv[1]);
     }
     if (i >= 1 && C.sd >= 0) {  // space_delta: a_i end - a0 start (features.py:491-499)
       double sdx[2], sdy[2], sm[2];
@@ -963,14 +447,14 @@ __device__ __forceinline__ void emit_window(const NumCols& C, int i, const Win& 
         sdy[e] = w.c3[e] - sy0[e];
         sm[e] = sqrt(sdx[e] * sdx[e] + sdy[e] * sdy[e]);
       }
-      st_f64x2(fb, C.sd + 3 * (i - 1), Rf, sdx[0], sdx[1]);
-      st_f64x2(fb, C.sd + 3 * (i - 1) + 1, Rf, sdy[0], sdy[1]);
-      st_f64x2(fb, C.sd + 3 * (i - 1) + 2, Rf, sm[0], sm[1]);
+      st_f64x2(fb, C.sd + 3 * (i - 1), C.nf, Rf, sdx[0], sdx[1]);
+      st_f64x2(fb, C.sd + 3 * (i - 1) + 1, C.nf, Rf, sdy[0], sdy[1]);
+      st_f64x2(fb, C.sd + 3 * (i - 1) + 2, C.nf, Rf, sm[0], sm[1]);
     }
   } else {
     if (C.lo >= 0) {
-      st_f64x2(fb, C.lo + 2 * i, Rf, w.c0[0], w.c0[1]);
-      st_f64x2(fb, C.lo + 2 * i + 1, Rf, w.c1[0], w.c1[1]);
+      st_f64x2(fb, C.lo + 2 * i, C.nf, Rf, w.c0[0], w.c0[1]);
+      st_f64x2(fb, C.lo + 2 * i + 1, C.nf, Rf, w.c1[0], w.c1[1]);
     }
     if (C.po >= 0) {
       double dist[2], ang[2];
@@ -980,8 +464,8 @@ __device__ __forceinline__ void emit_window(const NumCols& C, int i, const Win& 
         dist[e] = sqrt(dx * dx + dy * dy);
         ang[e] = polar_angle(dy, dx);
       }
-      st_f64x2(fb, C.po + 2 * i, Rf, dist[0], dist[1]);
-      st_f64x2(fb, C.po + 2 * i + 1, Rf, ang[0], ang[1]);
+      st_f64x2(fb, C.po + 2 * i, C.nf, Rf, dist[0], dist[1]);
+      st_f64x2(fb, C.po + 2 * i + 1, C.nf, Rf, ang[0], ang[1]);
     }
     if (C.mp >= 0) {  // atomic/vaep/features.py:279-284
       double md[2], ma[2];
@@ -990,8 +474,8 @@ __device__ __forceinline__ void emit_window(const NumCols& C, int i, const Win& 
         md[e] = sqrt(w.c2[e] * w.c2[e] + w.c3[e] * w.c3[e]);
         ma[e] = (w.c3[e] == 0.0) ? 0.0 : atan2(w.c3[e], w.c2[e]);
       }
-      st_f64x2(fb, C.mp + 2 * i, Rf, md[0], md[1]);
-      st_f64x2(fb, C.mp + 2 * i + 1, Rf, ma[0], ma[1]);
+      st_f64x2(fb, C.mp + 2 * i, C.nf, Rf, md[0], md[1]);
+      st_f64x2(fb, C.mp + 2 * i + 1, C.nf, Rf, ma[0], ma[1]);
     }
     if (C.di >= 0) {  // atomic/vaep/features.py:302-310
       double ox[2], oy[2];
@@ -1001,12 +485,12 @@ __device__ __forceinline__ void emit_window(const NumCols& C, int i, const Win& 
         ox[e] = td > 0.0 ? w.c2[e] / td : w.c2[e];
         oy[e] = td > 0.0 ? w.c3[e] / td : w.c3[e];
       }
-      st_f64x2(fb, C.di + 2 * i, Rf, ox[0], ox[1]);
-      st_f64x2(fb, C.di + 2 * i + 1, Rf, oy[0], oy[1]);
+      st_f64x2(fb, C.di + 2 * i, C.nf, Rf, ox[0], ox[1]);
+      st_f64x2(fb, C.di + 2 * i + 1, C.nf, Rf, oy[0], oy[1]);
     }
   }
   if (i >= 1 && C.td >= 0)  // time_delta: a0 time - a_i time (features.py:469-473)
-    st_f64x2(fb, C.td + (i - 1), Rf, t0[0] - w.ts[0], t0[1] - w.ts[1]);
+    st_f64x2(fb, C.td + (i - 1), C.nf, Rf, t0[0] - w.ts[0], t0[1] - w.ts[1]);
 }
 
 // play_left_to_right of one window value pair, keyed on the CURRENT action (features.py:109-115)
@@ -1082,14 +566,8 @@ __device__ __forceinline__ void row_to_win(const Row& r, Win& w, int e) {
 // KF = 3: windowed mode with nb_prev_actions <= 3.  The pair's rows jb-2 .. jb+1 are read
 // once (16-B loads) and the windows are formed in registers (see the loop below).
 // KF = 0: any mode / any k (explicit frames, k <= 8): per-window row loads.
-#ifndef SA_NUM_FAST
-#define SA_NUM_FAST 1
-#endif
-#ifndef SA_NUM_MINWAVES
-#define SA_NUM_MINWAVES 1
-#endif
 template <bool ATOMIC, bool EXPLICIT, int KF>
-__global__ __launch_bounds__(256, SA_NUM_MINWAVES) void num_features_kernel(FeatArgs args) {
+__global__ __launch_bounds__(256) void num_features_kernel(FeatArgs args) {
   const int lane = threadIdx.x & (WAVE - 1);
   const int wv = threadIdx.x / WAVE;
   const sa_actions& A = args.a;
@@ -1119,6 +597,8 @@ __global__ __launch_bounds__(256, SA_NUM_MINWAVES) void num_features_kernel(Feat
   C.po = P.f64_col[SA_XFN_POLAR];
   C.mp = P.f64_col[SA_XFN_MOVEMENT_POLAR];
   C.di = P.f64_col[SA_XFN_DIRECTION];
+  C.nf = (int)args.Cf;
+  C.ni = (int)args.Ci;
 
   for (int pr = 0; pr < NUM_PAIRS; ++pr) {
     const int64_t jb = wave_base + pr * 2 * WAVE + 2 * lane;
@@ -1204,172 +684,8 @@ __global__ __launch_bounds__(256, SA_NUM_MINWAVES) void num_features_kernel(Feat
 }
 
 // ------------------------------------------------------------------------------ goalscore
-// features.py:505-539 / atomic/vaep/features.py:313-344: per segment, teamA = team of the
-// segment's first row, exclusive cumsum of goals for A and for B.  One workgroup per
-// segment; each iteration covers 1024 rows (4 per thread, word-aligned loads).
-constexpr int GS_THREADS = 256;
-
-template <bool ATOMIC>
-__global__ __launch_bounds__(GS_THREADS) void goalscore_kernel(sa_actions A, int64_t* __restrict__ block,
-                                                               int64_t C, int64_t col, int64_t R) {
-  __shared__ uint64_t wsum[GS_THREADS / WAVE];
-  const int64_t g = blockIdx.x;
-  const int64_t s = A.seg_off[g], e = A.seg_off[g + 1];
-  if (s >= e) return;
-  const int64_t n = A.n;
-  const sa_frame& F = A.frames[0];
-  const int32_t teamA = F.team[s];
-  const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
-  uint64_t carry = 0;  // low 32 bits: goals of team A so far; high 32 bits: team B
-  for (int64_t base = s & ~(int64_t)3; base < e; base += 4 * GS_THREADS) {
-    const int64_t j0 = base + 4 * threadIdx.x;
-    const uint32_t tw = ld_u8x4(F.type_id, j0 / 4, n);
-    const uint32_t rw = ATOMIC ? 0u : ld_u8x4(F.result_id, j0 / 4, n);
-    uint32_t gb, ob;
-    goal_bytes(tw, rw, ATOMIC, gb, ob);
-    uint64_t inc[4];
-    bool isA[4], valid[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int64_t j = j0 + q;
-      valid[q] = j >= s && j < e;
-      isA[q] = valid[q] && F.team[j] == teamA;
-      const bool goal = valid[q] && byte_of(gb, q), og = valid[q] && byte_of(ob, q);
-      const bool gA = (goal && isA[q]) || (og && !isA[q]);
-      const bool gB = (goal && !isA[q]) || (og && isA[q]);
-      inc[q] = (uint64_t)gA | ((uint64_t)gB << 32);
-    }
-    const uint64_t x = inc[0] + inc[1] + inc[2] + inc[3];
-    uint64_t incl = x;
-#pragma unroll
-    for (int off = 1; off < WAVE; off <<= 1) {
-      const uint64_t y = __shfl_up(incl, off, WAVE);
-      if (lane >= off) incl += y;
-    }
-    if (lane == WAVE - 1) wsum[wv] = incl;
-    __syncthreads();
-    uint64_t wpre = 0, total = 0;
-#pragma unroll
-    for (int k = 0; k < GS_THREADS / WAVE; ++k) {
-      const uint64_t v = wsum[k];
-      wpre += k < wv ? v : 0;
-      total += v;
-    }
-    __syncthreads();
-    uint64_t excl = carry + wpre + incl - x;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      if (valid[q]) {
-        const int64_t j = j0 + q;
-        const int64_t cA = (int64_t)(excl & 0xFFFFFFFFull), cB = (int64_t)(excl >> 32);
-        const int64_t tm = isA[q] ? cA : cB, op = isA[q] ? cB : cA;
-        int64_t* o = block + tile_off(j, col, C, R);
-        o[0] = tm;
-        o[R] = op;
-        o[2 * R] = tm - op;
-      }
-      excl += inc[q];
-    }
-    carry += total;
-  }
-}
-
-// Wave-per-segment form: each wave scans one segment in passes of 128 rows, a lane owning 2
-// consecutive rows (u16 id loads, 8-B team load, one 16-B i64x2 store per column, i.e. 1 KiB
-// per wave-instruction), the scan is a wave shuffle scan with the carry broadcast from lane
-// 63; no barriers.  The next pass's inputs are loaded before the current pass is scanned.
-// A pair that straddles the segment's first or last row stores only its own row.
-struct GsIn {
-  uint32_t ty, rs;
-  int32_t t0, t1;
-};
-
-template <bool ATOMIC>
-__device__ __forceinline__ GsIn gs_load(const sa_frame& F, int64_t jb, int64_t n) {
-  GsIn v;
-  if (jb >= 0 && jb + 2 <= n) {
-    v.ty = *reinterpret_cast<const uint16_t*>(F.type_id + jb);
-    v.rs = ATOMIC ? 0u : *reinterpret_cast<const uint16_t*>(F.result_id + jb);
-    const int2 t = *reinterpret_cast<const int2*>(F.team + jb);
-    v.t0 = t.x;
-    v.t1 = t.y;
-  } else {
-    v.ty = (uint32_t)ld_or0(F.type_id, jb, n) | ((uint32_t)ld_or0(F.type_id, jb + 1, n) << 8);
-    v.rs = ATOMIC ? 0u
-                  : (uint32_t)ld_or0(F.result_id, jb, n) | ((uint32_t)ld_or0(F.result_id, jb + 1, n) << 8);
-    v.t0 = ld_or0(F.team, jb, n);
-    v.t1 = ld_or0(F.team, jb + 1, n);
-  }
-  return v;
-}
-
-template <bool ATOMIC>
-__global__ __launch_bounds__(256) void goalscore_wave_kernel(sa_actions A, int64_t* __restrict__ block,
-                                                             int64_t C, int64_t col, int64_t R) {
-  const int lane = threadIdx.x & (WAVE - 1);
-  const int64_t g = (int64_t)blockIdx.x * (blockDim.x / WAVE) + threadIdx.x / WAVE;
-  if (g >= A.n_segments) return;
-  const int64_t s = A.seg_off[g], e = A.seg_off[g + 1];
-  if (s >= e) return;
-  const int64_t n = A.n;
-  const sa_frame& F = A.frames[0];
-  const int32_t teamA = F.team[s];
-  const int64_t base0 = s & ~(int64_t)1;
-  uint64_t carry = 0;  // low 32 bits: goals of team A before this pass; high: team B
-  GsIn cur = gs_load<ATOMIC>(F, base0 + 2 * lane, n);
-  for (int64_t base = base0; base < e; base += 2 * WAVE) {
-    const int64_t jb = base + 2 * lane;
-    const GsIn nxt = gs_load<ATOMIC>(F, jb + 2 * WAVE, n);  // prefetch the next pass
-    uint32_t gb, ob;
-    goal_bytes(cur.ty, cur.rs, ATOMIC, gb, ob);
-    uint64_t inc[2];
-    bool isA[2], valid[2];
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int64_t j = jb + q;
-      valid[q] = j >= s && j < e;
-      isA[q] = (q ? cur.t1 : cur.t0) == teamA;
-      const bool goal = valid[q] && byte_of(gb, q), og = valid[q] && byte_of(ob, q);
-      const bool gA = (goal && isA[q]) || (og && !isA[q]);
-      const bool gB = (goal && !isA[q]) || (og && isA[q]);
-      inc[q] = (uint64_t)gA | ((uint64_t)gB << 32);
-    }
-    const uint64_t x = inc[0] + inc[1];
-    uint64_t incl = x;
-#pragma unroll
-    for (int off = 1; off < WAVE; off <<= 1) {
-      const uint64_t y = __shfl_up(incl, off, WAVE);
-      if (lane >= off) incl += y;
-    }
-    const uint64_t e0 = carry + incl - x, e1 = e0 + inc[0];  // exclusive counts of rows jb, jb+1
-    carry += __shfl(incl, WAVE - 1, WAVE);
-    int64_t tm[2], op[2];
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const uint64_t ex = q ? e1 : e0;
-      const int64_t cA = (int64_t)(ex & 0xFFFFFFFFull), cB = (int64_t)(ex >> 32);
-      tm[q] = isA[q] ? cA : cB;
-      op[q] = isA[q] ? cB : cA;
-    }
-    if (valid[0] && valid[1]) {
-      int64_t* o = block + tile_off(jb, col, C, R);
-      st_i64x2(o, 0, R, tm[0], tm[1]);
-      st_i64x2(o, 1, R, op[0], op[1]);
-      st_i64x2(o, 2, R, tm[0] - op[0], tm[1] - op[1]);
-    } else {
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        if (valid[q]) {
-          int64_t* o = block + tile_off(jb + q, col, C, R);
-          o[0] = tm[q];
-          o[R] = op[q];
-          o[2 * R] = tm[q] - op[q];
-        }
-      }
-    }
-    cur = nxt;
-  }
-}
+// features.py:505-539 / atomic/vaep/features.py:229-260: per segment, teamA = team of the
+// segment's first row, exclusive cumsum of goals for A and for B.  One wave per segment.
 
 // 16-rows-per-lane form: passes of 1024 rows, so a ~1,600-row game is 2 passes instead of 13
 // and each pass issues all of its loads at once (16 type + 16 result bytes, 64 B of team codes
@@ -1503,7 +819,7 @@ __global__ __launch_bounds__(256) void goalscore_wave16_kernel(sa_actions A,
 // nr_actions <= 17 needs no further loads.  The look-ahead clamps at the segment's last row,
 // which only repeats a row already in the window, so the window is rows j+1 .. min(j+nr-1,
 // last).
-template <bool ATOMIC, bool WAVESEG>
+template <bool ATOMIC>
 __global__ __launch_bounds__(256) void labels_kernel(sa_actions A, int nr, uint8_t* __restrict__ sc,
                                                      uint8_t* __restrict__ co,
                                                      uint8_t* __restrict__ gfs) {
@@ -1549,13 +865,11 @@ __global__ __launch_bounds__(256) void labels_kernel(sa_actions A, int nr, uint8
 #pragma unroll
   for (int r = 0; r < 32; ++r) e1 |= (uint32_t)(tm[r] == t1) << r;
   SegCursor cur;
-  if (WAVESEG) {
+  {
     // one search per wave (the first active lane's row, uniform: scalar loads), then each lane
     // advances to its own rows -- a per-lane binary search was ~14 dependent divergent loads
     const int64_t jw = (int64_t)__builtin_amdgcn_readfirstlane((int)(j0 / LANE_ACTS)) * LANE_ACTS;
     cur = seg_at(A, jw);
-  } else {
-    cur = seg_at(A, j0);
   }
   uint32_t s_out[4] = {0, 0, 0, 0}, c_out[4] = {0, 0, 0, 0}, g_out[4] = {0, 0, 0, 0};
 #pragma unroll
@@ -1626,7 +940,7 @@ __global__ __launch_bounds__(256) void labels_kernel(sa_actions A, int nr, uint8
 // dtype and mirrors the pandas expression tree operation by operation.  A lane owns V
 // consecutive actions (16-B stores); the previous row's values come from the same lane or,
 // for the lane's first action, from the neighbouring lane by a wave shuffle.
-template <bool ATOMIC, typename T, bool WAVESEG>
+template <bool ATOMIC, typename T>
 __global__ __launch_bounds__(256) void formula_kernel(sa_actions A, const T* __restrict__ ps,
                                                       const T* __restrict__ pc, T* __restrict__ off,
                                                       T* __restrict__ def, T* __restrict__ val,
@@ -1701,10 +1015,8 @@ __global__ __launch_bounds__(256) void formula_kernel(sa_actions A, const T* __r
     rsp = ATOMIC ? 0 : F.result_id[p];
   }
   SegCursor cur;
-  if (WAVESEG)  // one search per wave (uniform, scalar loads), lanes advance from it
-    cur = seg_at(A, (int64_t)__builtin_amdgcn_readfirstlane((int)(j0 / V)) * V);
-  else
-    cur = seg_at(A, j0);
+  // one search per wave (uniform, scalar loads), lanes advance from it
+  cur = seg_at(A, (int64_t)__builtin_amdgcn_readfirstlane((int)(j0 / V)) * V);
   vec_t vo, vd, vv;
 #pragma unroll
   for (int q = 0; q < V; ++q) {
@@ -1852,24 +1164,8 @@ extern "C" int sa_vaep_features(const sa_actions* a, const sa_feature_plan* plan
                 wf ? f64_out->tile_rows : 16,
                 wi ? i64_out->tile_rows : 16};
   const dim3 grid(xcd_grid((a->n + BLOCK_ACTS - 1) / BLOCK_ACTS)), block(BLOCK_WAVES * WAVE);
-  const dim3 bgrid((unsigned)((a->n + BOOL_BLOCK_ACTS - 1) / BOOL_BLOCK_ACTS));
   const bool expl = a->n_frames > 1;
-  const StagedCfg scfg = bool_kernel_choice();
-  if (wb && scfg.nw > 0 && !expl) {  // short workgroups, window codes staged in LDS
-    const int per = scfg.nw * scfg.g;
-    const int ncg = (int)((args.Cb + per - 1) / per);
-    const int64_t nl = (a->n + BOOL_TILE - 1) / BOOL_TILE * ncg;
-    const dim3 sgrid(xcd_grid(nl)), sblock(WAVE * scfg.nw);
-    const size_t shm = staged_lds_bytes(K);
-    if (a->atomic)
-      hipLaunchKernelGGL((bool_staged_kernel<true>), sgrid, sblock, shm, st, args, ncg, scfg.nw,
-                         scfg.g, nl);
-    else
-      hipLaunchKernelGGL((bool_staged_kernel<false>), sgrid, sblock, shm, st, args, ncg, scfg.nw,
-                         scfg.g, nl);
-    rc = check_launch("bool_staged_kernel");
-    if (rc) return rc;
-  } else if (wb && SA_BOOL_MODE == 2) {  // one wave per (tile, group of ~32 columns)
+  if (wb) {  // one wave per (tile, group of ~32 columns), XCD-contiguous sweep order
     const int ng = (int)((args.Cb + SA_CG_COLS - 1) / SA_CG_COLS);
     const int gc = (int)((args.Cb + ng - 1) / ng);
     const int64_t waves = (a->n + BOOL_TILE - 1) / BOOL_TILE * ng;
@@ -1887,38 +1183,9 @@ extern "C" int sa_vaep_features(const sa_actions* a, const sa_feature_plan* plan
     }
     rc = check_launch("bool_colgroup_kernel");
     if (rc) return rc;
-  } else if (wb && SA_BOOL_MODE == 1) {  // one 64*K-thread workgroup per 1024-row tile
-    const dim3 tgrid(xcd_grid((a->n + BOOL_TILE - 1) / BOOL_TILE)), tblock(WAVE * K);
-    if (a->atomic) {
-      if (expl)
-        hipLaunchKernelGGL((bool_window_kernel<true, true>), tgrid, tblock, 0, st, args);
-      else
-        hipLaunchKernelGGL((bool_window_kernel<true, false>), tgrid, tblock, 0, st, args);
-    } else {
-      if (expl)
-        hipLaunchKernelGGL((bool_window_kernel<false, true>), tgrid, tblock, 0, st, args);
-      else
-        hipLaunchKernelGGL((bool_window_kernel<false, false>), tgrid, tblock, 0, st, args);
-    }
-    rc = check_launch("bool_window_kernel");
-    if (rc) return rc;
-  } else if (wb) {
-    if (a->atomic) {
-      if (expl)
-        hipLaunchKernelGGL((bool_features_kernel<true, true>), bgrid, block, 0, st, args);
-      else
-        hipLaunchKernelGGL((bool_features_kernel<true, false>), bgrid, block, 0, st, args);
-    } else {
-      if (expl)
-        hipLaunchKernelGGL((bool_features_kernel<false, true>), bgrid, block, 0, st, args);
-      else
-        hipLaunchKernelGGL((bool_features_kernel<false, false>), bgrid, block, 0, st, args);
-    }
-    rc = check_launch("bool_features_kernel");
-    if (rc) return rc;
   }
   if (wn) {
-    const bool fast = SA_NUM_FAST && !expl && K <= 3;  // register-resident windows (KF = 3)
+    const bool fast = !expl && K <= 3;  // register-resident windows (KF = 3)
     if (a->atomic) {
       if (expl)
         hipLaunchKernelGGL((num_features_kernel<true, true, 0>), grid, block, 0, st, args);
@@ -1951,32 +1218,14 @@ extern "C" int sa_vaep_goalscore(const sa_actions* a, const sa_block* i64_out, i
   if (a->n == 0) return SA_OK;
   hipStream_t st = (hipStream_t)stream;
   int64_t* blk = (int64_t*)i64_out->data;
-  const dim3 g4((unsigned)((a->n_segments + 3) / 4));
-  if (!env_is("SA_GS_KERNEL", "wave2")) {  // one wave per segment, passes of 1024 rows
-    if (a->atomic)
-      hipLaunchKernelGGL((goalscore_wave16_kernel<true>), g4, dim3(256), 0, st, *a, blk,
-                         (int64_t)i64_out->n_cols, (int64_t)col, i64_out->tile_rows);
-    else
-      hipLaunchKernelGGL((goalscore_wave16_kernel<false>), g4, dim3(256), 0, st, *a, blk,
-                         (int64_t)i64_out->n_cols, (int64_t)col, i64_out->tile_rows);
-    return check_launch("goalscore_wave16_kernel");
-  }
-  if (SA_GS_WAVE) {  // A/B (SA_GS_KERNEL=wave2): passes of 128 rows, a lane owning 2
-    if (a->atomic)
-      hipLaunchKernelGGL((goalscore_wave_kernel<true>), g4, dim3(256), 0, st, *a, blk,
-                         (int64_t)i64_out->n_cols, (int64_t)col, i64_out->tile_rows);
-    else
-      hipLaunchKernelGGL((goalscore_wave_kernel<false>), g4, dim3(256), 0, st, *a, blk,
-                         (int64_t)i64_out->n_cols, (int64_t)col, i64_out->tile_rows);
-    return check_launch("goalscore_wave_kernel");
-  }
+  const dim3 g4((unsigned)((a->n_segments + 3) / 4));  // one wave per segment
   if (a->atomic)
-    hipLaunchKernelGGL((goalscore_kernel<true>), dim3((unsigned)a->n_segments), dim3(GS_THREADS), 0, st,
-                       *a, blk, (int64_t)i64_out->n_cols, (int64_t)col, i64_out->tile_rows);
+    hipLaunchKernelGGL((goalscore_wave16_kernel<true>), g4, dim3(256), 0, st, *a, blk,
+                       (int64_t)i64_out->n_cols, (int64_t)col, i64_out->tile_rows);
   else
-    hipLaunchKernelGGL((goalscore_kernel<false>), dim3((unsigned)a->n_segments), dim3(GS_THREADS), 0,
-                       st, *a, blk, (int64_t)i64_out->n_cols, (int64_t)col, i64_out->tile_rows);
-  return check_launch("goalscore_kernel");
+    hipLaunchKernelGGL((goalscore_wave16_kernel<false>), g4, dim3(256), 0, st, *a, blk,
+                       (int64_t)i64_out->n_cols, (int64_t)col, i64_out->tile_rows);
+  return check_launch("goalscore_wave16_kernel");
 }
 
 extern "C" int sa_vaep_labels(const sa_actions* a, int32_t nr_actions, uint8_t* scores,
@@ -1991,23 +1240,13 @@ extern "C" int sa_vaep_labels(const sa_actions* a, int32_t nr_actions, uint8_t* 
   if (a->n == 0) return SA_OK;
   const int64_t lanes = (a->n + LANE_ACTS - 1) / LANE_ACTS;
   const dim3 grid((unsigned)((lanes + 255) / 256)), block(256);
-  const bool lane_search = env_is("SA_LABELS_SEARCH", "lane");  // A/B: the per-lane search
   hipStream_t st = (hipStream_t)stream;
-  if (a->atomic) {
-    if (lane_search)
-      hipLaunchKernelGGL((labels_kernel<true, false>), grid, block, 0, st, *a, nr_actions, scores,
-                         concedes, goal_from_shot);
-    else
-      hipLaunchKernelGGL((labels_kernel<true, true>), grid, block, 0, st, *a, nr_actions, scores,
-                         concedes, goal_from_shot);
-  } else {
-    if (lane_search)
-      hipLaunchKernelGGL((labels_kernel<false, false>), grid, block, 0, st, *a, nr_actions, scores,
-                         concedes, goal_from_shot);
-    else
-      hipLaunchKernelGGL((labels_kernel<false, true>), grid, block, 0, st, *a, nr_actions, scores,
-                         concedes, goal_from_shot);
-  }
+  if (a->atomic)
+    hipLaunchKernelGGL((labels_kernel<true>), grid, block, 0, st, *a, nr_actions, scores, concedes,
+                       goal_from_shot);
+  else
+    hipLaunchKernelGGL((labels_kernel<false>), grid, block, 0, st, *a, nr_actions, scores, concedes,
+                       goal_from_shot);
   return check_launch("labels_kernel");
 }
 
@@ -2023,23 +1262,12 @@ static int launch_formula(const sa_actions* a, const T* ps, const T* pc, T* off,
   constexpr int V = 16 / sizeof(T);
   const int64_t lanes = (a->n + V - 1) / V;
   const dim3 grid((unsigned)((lanes + 255) / 256)), block(256);
-  const bool vec_ok = SA_FORMULA_VEC && aligned16(ps) && aligned16(pc);
+  const bool vec_ok = aligned16(ps) && aligned16(pc);
   hipStream_t st = (hipStream_t)stream;
-  if (env_is("SA_FORMULA_SEARCH", "lane")) {  // A/B: the per-lane segment search
-    if (a->atomic)
-      hipLaunchKernelGGL((formula_kernel<true, T, false>), grid, block, 0, st, *a, ps, pc, off, def,
-                         val, vec_ok);
-    else
-      hipLaunchKernelGGL((formula_kernel<false, T, false>), grid, block, 0, st, *a, ps, pc, off, def,
-                         val, vec_ok);
-  } else {
-    if (a->atomic)
-      hipLaunchKernelGGL((formula_kernel<true, T, true>), grid, block, 0, st, *a, ps, pc, off, def,
-                         val, vec_ok);
-    else
-      hipLaunchKernelGGL((formula_kernel<false, T, true>), grid, block, 0, st, *a, ps, pc, off, def,
-                         val, vec_ok);
-  }
+  if (a->atomic)
+    hipLaunchKernelGGL((formula_kernel<true, T>), grid, block, 0, st, *a, ps, pc, off, def, val, vec_ok);
+  else
+    hipLaunchKernelGGL((formula_kernel<false, T>), grid, block, 0, st, *a, ps, pc, off, def, val, vec_ok);
   return check_launch("formula_kernel");
 }
 

@@ -125,6 +125,7 @@ __global__ __launch_bounds__(XT_WIDE_THREADS) void xt_count_kernel(sa_actions A,
           continue;
         }
         const int c = flat_index(sx[u], sy[u], l, w);
+        SA_DGUARD(c >= 0 && c < C, c, continue);
         if (VEC) {
           atomicAdd(&hs[c], 1u);
           if (r == R_SUCCESS) atomicAdd(&hg[c], 1u);
@@ -138,12 +139,14 @@ __global__ __launch_bounds__(XT_WIDE_THREADS) void xt_count_kernel(sa_actions A,
           continue;
         }
         const int cs = flat_index(sx[u], sy[u], l, w);
+        SA_DGUARD(cs >= 0 && cs < C, cs, continue);
         if (VEC)
           atomicAdd(&hm[cs], 1u);
         else
           atomicAdd(&move[cs], 1ull);
         if (r == R_SUCCESS) {
           const int ce = flat_index(ex[u], ey[u], l, w);
+          SA_DGUARD(ce >= 0 && ce < C, ce, continue);
           const int64_t k = (int64_t)cs * C + ce;
           if (SMALL)
             atomicAdd(&ht[k >> 1], (k & 1) ? 0x10000u : 1u);
@@ -250,7 +253,91 @@ __device__ __forceinline__ double row_payoff(const double* __restrict__ Tt, cons
 
 // Small grids: one persistent workgroup runs every iteration; x lives in LDS.
 constexpr int XT_SOLVE_MAX_C = 1024;
+constexpr size_t XT_LDS_BUDGET = 160 * 1024;  // gfx950 LDS per workgroup
 
+// LDS bytes of xt_solve_lds_kernel: the C x C int32 counts + x.
+static inline size_t xt_solve_lds_bytes(int C) {
+  return ((size_t)C * C * 4 + 15) / 16 * 16 + (size_t)C * 8;
+}
+
+// Grids whose C x C int32 counts fit LDS with x (C <= 199, e.g. 16 x 12): one persistent
+// workgroup keeps the counts -- transposed, so the lanes of a wave read consecutive words -- and
+// x in LDS for every iteration, so nothing is re-read from L2/HBM per iteration (the Tt form
+// streams the 295 KB f64 matrix from L2 every iteration and slows down badly when it shares
+// the chip with the streaming VAEP kernels).  T[r, c] * x[c] is formed exactly as the
+// reference rounds it: one correctly rounded division cnt / move[r], one multiply, added to
+// the row's sum strictly left to right (cnt == 0 contributes T = 0, i.e. +0).
+__global__ __launch_bounds__(256) void xt_solve_lds_kernel(const int32_t* __restrict__ trans,
+                                                           const unsigned long long* __restrict__ move,
+                                                           const double* __restrict__ gs,
+                                                           const double* __restrict__ pmove, int C,
+                                                           double eps, int max_iter,
+                                                           double* __restrict__ heat,
+                                                           double* __restrict__ xT_out,
+                                                           int32_t* __restrict__ n_iter) {
+  extern __shared__ __align__(16) uint8_t xt_lds[];
+  int32_t* cnt = reinterpret_cast<int32_t*>(xt_lds);  // cnt[c * C + r] = trans[r * C + c]
+  double* xs = reinterpret_cast<double*>(xt_lds + ((size_t)C * C * 4 + 15) / 16 * 16);
+  for (int k = threadIdx.x; k < C * C; k += blockDim.x) {
+    const int rr = k / C, c = k - rr * C;
+    SA_DCHECK(c * C + rr < C * C, k);
+    cnt[c * C + rr] = trans[k];
+  }
+  const int r = threadIdx.x;
+  const bool act = r < C;
+  double m = 1.0, g = 0.0, pm = 0.0;
+  if (act) {
+    xs[r] = 0.0;
+    heat[r] = 0.0;
+    m = (double)move[r];
+    g = gs[r];
+    pm = pmove[r];
+  }
+  __syncthreads();
+  int it = 0;
+  bool cont = true;
+  while (cont && it < max_iter) {
+    double nx = 0.0;
+    int flag = 0;
+    if (act) {
+      double acc = 0.0;
+      int c = 0;
+      for (; c + 8 <= C; c += 8) {
+        int32_t v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = cnt[(c + u) * C + r];
+        double p[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const double t = v[u] != 0 ? (double)v[u] / m : 0.0;
+          p[u] = t * xs[c + u];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc = acc + p[u];
+      }
+      for (; c < C; ++c) {
+        const int32_t v = cnt[c * C + r];
+        const double t = v != 0 ? (double)v / m : 0.0;
+        const double p = t * xs[c];
+        acc = acc + p;
+      }
+      const double mv = pm * acc;
+      nx = g + mv;
+      const double diff = nx - xs[r];
+      flag = diff > eps;  // np.any(diff > eps): NaN compares False
+      heat[(int64_t)(it + 1) * C + r] = nx;
+    }
+    cont = __syncthreads_or(flag);
+    if (act) xs[r] = nx;
+    __syncthreads();
+    ++it;
+  }
+  if (act) xT_out[r] = xs[r];
+  if (r == 0) *n_iter = cont ? -1 : it;
+}
+
+// Grids up to XT_SOLVE_MAX_C cells whose counts do not fit LDS: the same iteration over the
+// normalised, transposed f64 matrix Tt read from global memory (L2-resident).
 __global__ __launch_bounds__(1024) void xt_solve_small_kernel(const double* __restrict__ Tt,
                                                               const double* __restrict__ gs,
                                                               const double* __restrict__ pmove, int C,
@@ -486,6 +573,7 @@ __device__ __forceinline__ double rate_one(int t, int r, double sx, double sy, d
       bad = 4;
     } else {
       const int s = flat_index(sx, sy, L, W), e = flat_index(ex, ey, L, W);
+      SA_DGUARD(s >= 0 && s < L * W && e >= 0 && e < L * W, s, return v);
       v = grid[e] - grid[s];
     }
   }
@@ -625,32 +713,35 @@ extern "C" int sa_xt_solve(const int64_t* shot, const int64_t* goal, const int64
   auto* us = reinterpret_cast<const unsigned long long*>(shot);
   auto* ug = reinterpret_cast<const unsigned long long*>(goal);
   auto* um = reinterpret_cast<const unsigned long long*>(move);
-  double* gs = nullptr;
-  int32_t* dflags = nullptr;
-  int rc = check_hip(hipMallocAsync((void**)&gs, sizeof(double) * 2 * C, st), "hipMallocAsync");
+  // scratch: gs[C] | pmove[C] | n_iter | convergence flags[max_iter + 1]
+  Scratch sc;
+  int rc = scratch_acquire(sizeof(double) * 2 * C + sizeof(int32_t) * (max_iter + 2), st, &sc);
   if (rc) return rc;
+  double* gs = static_cast<double*>(sc.ptr);
   double* pm = gs + C;
+  int32_t* dn = reinterpret_cast<int32_t*>(pm + C);
+  int32_t* dflags = dn + 1;
   int32_t iters = -1;
   hipLaunchKernelGGL(xt_prob_kernel, dim3((C + 255) / 256), dim3(256), 0, st, us, ug, um, C, mats, gs, pm);
   const dim3 tgrid((C + 31) / 32, (C + 31) / 32);
   hipLaunchKernelGGL(xt_transpose_kernel, tgrid, dim3(256), 0, st, trans, um, C, trans_t);
   rc = check_launch("xt normalise");
   if (!rc && C <= XT_SOLVE_MAX_C) {
-    int32_t* dn = nullptr;
-    rc = check_hip(hipMallocAsync((void**)&dn, sizeof(int32_t), st), "hipMallocAsync");
-    if (!rc) {
-      const int threads = ((C + 63) / 64) * 64;
-      hipLaunchKernelGGL(xt_solve_small_kernel, dim3(1), dim3(threads), 0, st, trans_t, gs, pm, C, eps,
-                         max_iter, heatmaps, mats + 3 * C, dn);
+    const size_t lds = xt_solve_lds_bytes(C);
+    if (lds <= XT_LDS_BUDGET) {
+      hipLaunchKernelGGL(xt_solve_lds_kernel, dim3(1), dim3(((C + 63) / 64) * 64), lds, st, trans, um,
+                         gs, pm, C, eps, max_iter, heatmaps, mats + 3 * C, dn);
+      rc = check_launch("xt_solve_lds_kernel");
+    } else {
+      hipLaunchKernelGGL(xt_solve_small_kernel, dim3(1), dim3(((C + 63) / 64) * 64), 0, st, trans_t, gs,
+                         pm, C, eps, max_iter, heatmaps, mats + 3 * C, dn);
       rc = check_launch("xt_solve_small_kernel");
-      if (!rc) rc = check_hip(hipMemcpyAsync(&iters, dn, sizeof(int32_t), hipMemcpyDeviceToHost, st),
-                              "copy n_iter");
-      if (!rc) rc = check_hip(hipStreamSynchronize(st), "hipStreamSynchronize");
-      (void)hipFreeAsync(dn, st);
     }
+    if (!rc) rc = check_hip(hipMemcpyAsync(&iters, dn, sizeof(int32_t), hipMemcpyDeviceToHost, st),
+                            "copy n_iter");
+    if (!rc) rc = check_hip(hipStreamSynchronize(st), "hipStreamSynchronize");
   } else if (!rc) {
-    rc = check_hip(hipMallocAsync((void**)&dflags, sizeof(int32_t) * (max_iter + 1), st), "hipMallocAsync");
-    if (!rc) rc = check_hip(hipMemsetAsync(dflags, 0, sizeof(int32_t) * (max_iter + 1), st), "memset");
+    rc = check_hip(hipMemsetAsync(dflags, 0, sizeof(int32_t) * (max_iter + 1), st), "memset");
     if (!rc) rc = check_hip(hipMemsetAsync(heatmaps, 0, sizeof(double) * C, st), "memset");
     std::vector<int32_t> hflags(max_iter + 1, 0);
     const int batch = 8;
@@ -679,10 +770,8 @@ extern "C" int sa_xt_solve(const int64_t* shot, const int64_t* goal, const int64
                      "copy xT");
       if (!rc) rc = check_hip(hipStreamSynchronize(st), "hipStreamSynchronize");
     }
-    (void)hipFreeAsync(dflags, st);
   }
-  (void)hipFreeAsync(gs, st);
-  if (!rc) rc = check_hip(hipStreamSynchronize(st), "hipStreamSynchronize");
+  scratch_release(sc, st);
   *n_iter = iters;
   return rc;
 }
@@ -709,15 +798,16 @@ extern "C" int sa_xt_normalize(const int64_t* shot, const int64_t* goal, const i
   auto* us = reinterpret_cast<const unsigned long long*>(shot);
   auto* ug = reinterpret_cast<const unsigned long long*>(goal);
   auto* um = reinterpret_cast<const unsigned long long*>(move);
-  double* gs = nullptr;
-  int rc = check_hip(hipMallocAsync((void**)&gs, sizeof(double) * 2 * C, st), "hipMallocAsync");
+  Scratch sc;  // gs[C] | pmove[C] (not returned by this entry point)
+  int rc = scratch_acquire(sizeof(double) * 2 * C, st, &sc);
   if (rc) return rc;
+  double* gs = static_cast<double*>(sc.ptr);
   hipLaunchKernelGGL(xt_prob_kernel, dim3((C + 255) / 256), dim3(256), 0, st, us, ug, um, C, mats, gs,
                      gs + C);
   const dim3 tgrid((C + 31) / 32, (C + 31) / 32);
   hipLaunchKernelGGL(xt_transpose_kernel, tgrid, dim3(256), 0, st, trans, um, C, trans_t);
   rc = check_launch("xt normalise");
-  (void)hipFreeAsync(gs, st);
+  scratch_release(sc, st);
   return rc;
 }
 

@@ -75,6 +75,11 @@ class FeatureBlocks:
         out = []
         for t, R in ((self.bool_block, self.Rb), (self.f64_block, self.Rn),
                      (self.i64_block, self.Rn)):
+            # the kernels write ceil(n / R) whole [C, R] tiles: the tensor must hold them
+            if (t.dim() != 3 or t.shape[2] != R or t.shape[0] * R < self.n
+                    or not t.is_contiguous()):
+                raise ValueError(f'feature block of shape {tuple(t.shape)} cannot hold {self.n} '
+                                 f'rows in tiles of {R}')
             b = _native.SaBlock()
             b.data = _ptr(t)
             b.n_cols = t.shape[1]

@@ -31,6 +31,43 @@ def test_library_builds_and_exports_every_declared_symbol():
         assert hasattr(lib, sym), sym
     assert set(declared) == set(_native.EXPORTED_SYMBOLS)
     assert lib.sa_abi_version() == 2
+    assert lib.sa_debug_enabled() == 0
+    assert lib.sa_debug_check() == 0  # default build: no device checks, no device call
+
+
+def test_build_id_ties_the_library_to_its_sources(tmp_path):
+    """sa_build_id() is the hash of the sources + flags; build.py rebuilds on a hash change (not
+    file times) and the loader refuses a library whose id differs from the sources next to it."""
+    from socceraction_amd import _native, build
+    build.build(force=False, verbose=False)
+    lib = _native.load_library()
+    bid = build.build_id()
+    assert lib.sa_build_id().decode() == bid == build.file_build_id(build.OUT)
+    assert build.build_id(build.DEBUG_DEFINES) != bid
+    # a stale copy (other defines) is refused when loaded as the default library
+    stale = tmp_path / 'libstale.so'
+    build.build(force=True, verbose=False, defines=('SA_NT_STORES=0',), out=str(stale))
+    assert build.file_build_id(str(stale)) == build.build_id(('SA_NT_STORES=0',))
+    other = _native.load_library(str(stale))  # an explicit variant path is not checked
+    with pytest.raises(ImportError):
+        _native._check_build_id(other, _native.DEFAULT_LIB)
+
+
+def test_debug_library_builds_with_device_checks():
+    from socceraction_amd import _native, build
+    path = build.build_debug(verbose=False)
+    lib = _native.load_library(path)
+    _native._check_build_id(lib, _native.DEBUG_LIB)
+    assert lib.sa_debug_enabled() == 1
+    assert lib.sa_build_id().decode() == build.build_id(build.DEBUG_DEFINES)
+    for sym in _native.EXPORTED_SYMBOLS:
+        assert hasattr(lib, sym), sym
+
+
+def test_shutdown_without_scratch_is_a_no_op():
+    from socceraction_amd import _native
+    lib = _native.load_library()
+    assert lib.sa_shutdown() == 0
 
 
 def test_ctypes_struct_layout_matches_header():

@@ -136,89 +136,67 @@ def test_tiled_and_plain_layouts_agree(sa):
         ops.features(ab, vo.SPADL_DEFAULT, 3, num_tile=100)
 
 
-@pytest.mark.parametrize('atomic', [False, True])
-def test_staged_bool_kernel_matches_colgroup(sa, atomic, monkeypatch):
-    """The opt-in staged bool kernel (SA_BOOL_KERNEL=staged:NW:G, short workgroups with the
-    window codes in LDS) writes the column-group kernel's block byte for byte: games of 1..40
-    actions (many segment starts per 1024-row chunk) and full games, k = 1..5, both layouts."""
-    B, ops, syn = sa['batch'], sa['ops'], sa['synthetic']
-    default = vo.ATOMIC_DEFAULT if atomic else vo.SPADL_DEFAULT
+def _small_games(syn, atomic, seed, n_small=300):
+    """Full games plus ``n_small`` games of 1..40 actions (many segment starts per tile / wave)."""
     gen = syn.atomic_games if atomic else syn.spadl_games
-    d = gen(6, seed=11)
+    d = gen(6, seed=seed)
     n0 = int(d['game_off'][-1])
-    rng = np.random.default_rng(5)
-    sizes = rng.integers(1, 41, 300)  # 300 small games appended (rows copied from the start)
+    sizes = np.random.default_rng(seed + 1).integers(1, 41, n_small)
     m = int(sizes.sum())
     rows = {c: v for c, v in d.items() if isinstance(v, np.ndarray) and v.shape == (n0,)}
     d2 = {c: np.concatenate([v, v[:m]]) for c, v in rows.items()}
     offs = n0 + np.concatenate([[0], np.cumsum(sizes)])
     d2['game_off'] = np.concatenate([d['game_off'], offs[1:]])
     d2['home_team_id'] = np.concatenate([d['home_team_id'], d2['team_id'][offs[:-1]]])
-    ab = B.ActionBatch.from_columns(d2, atomic=atomic)
+    return d2
+
+
+@pytest.mark.parametrize('atomic', [False, True])
+def test_many_small_segments_vs_oracle(sa, atomic):
+    """Full games + 300 games of 1..40 actions in one batch: features at k = 1, 3, 5 (both
+    layouts), labels at nr_actions 10 and 20 (the > 17 path reloads rows) and the formula with
+    f64 and f32 probabilities == the oracle with the same segment offsets."""
+    B, ops, syn = sa['batch'], sa['ops'], sa['synthetic']
+    default = vo.ATOMIC_DEFAULT if atomic else vo.SPADL_DEFAULT
+    d = _small_games(syn, atomic, 11)
+    ab = B.ActionBatch.from_columns(d, atomic=atomic)
     assert ab.n_segments > 300
-    for k in (1, 2, 3, 5):
-        for Rb in (1024, None):
-            monkeypatch.delenv('SA_BOOL_KERNEL', raising=False)
-            ref = ops.features(ab, default, k, bool_tile=Rb).bool_block.cpu()
-            for v in ('staged:4:4', 'staged:16:1', 'staged:8:3'):
-                monkeypatch.setenv('SA_BOOL_KERNEL', v)
-                got = ops.features(ab, default, k, bool_tile=Rb).bool_block.cpu()
-                n = ab.n
-                if Rb is None:
-                    assert torch.equal(got[:, :, :n], ref[:, :, :n]), (k, v)
+    n, so = ab.n, d['game_off']
+    names = (('period_id', 'time_seconds', 'team_id', 'x', 'y', 'dx', 'dy', 'type_id',
+              'bodypart_id') if atomic else
+             ('period_id', 'time_seconds', 'team_id', 'start_x', 'start_y', 'end_x', 'end_y',
+              'type_id', 'result_id', 'bodypart_id'))
+    cols = {c: d[c] for c in names}
+    for k in (1, 3, 5):
+        ref = vo.features(cols, k, default, atomic=atomic, seg_off=so, home=d['home_team_id'])
+        for Rb, Rn in ((1024, 128), (None, None)):
+            fb = ops.features(ab, default, k, bool_tile=Rb, num_tile=Rn)
+            assert fb.plan.names == [c[0] for c in ref]
+            blocks = {kk: fb.block(kk)[:, :n].cpu().numpy() for kk in 'bfi'}
+            for (name, kind, col), (_, _, rv) in zip(fb.plan.order, ref):
+                got = blocks[kind][col]
+                if kind == 'f':
+                    assert_close(got, rv, f'{name} k={k}')
                 else:
-                    gf = got.permute(1, 0, 2).reshape(got.shape[1], -1)[:, :n]
-                    rf = ref.permute(1, 0, 2).reshape(ref.shape[1], -1)[:, :n]
-                    assert torch.equal(gf, rf), (k, v, Rb)
-
-
-@pytest.mark.parametrize('atomic', [False, True])
-def test_run_time_variants_match_default(sa, atomic, monkeypatch):
-    """The launchers' run-time A/B switches (sa_vaep.hip: SA_GS_KERNEL=wave2, SA_LABELS_SEARCH=
-    lane, SA_FORMULA_SEARCH=lane) give the default kernels' outputs bit for bit: full games plus
-    300 games of 1..40 actions (many segment starts per wave), labels at nr_actions 10 and 20
-    (the > 17 path reloads rows), f64 and f32 probabilities."""
-    B, ops, syn = sa['batch'], sa['ops'], sa['synthetic']
-    default = vo.ATOMIC_DEFAULT if atomic else vo.SPADL_DEFAULT
-    gen = syn.atomic_games if atomic else syn.spadl_games
-    d = gen(8, seed=21)
-    n0 = int(d['game_off'][-1])
-    sizes = np.random.default_rng(9).integers(1, 41, 300)
-    m = int(sizes.sum())
-    rows = {c: v for c, v in d.items() if isinstance(v, np.ndarray) and v.shape == (n0,)}
-    d2 = {c: np.concatenate([v, v[:m]]) for c, v in rows.items()}
-    offs = n0 + np.concatenate([[0], np.cumsum(sizes)])
-    d2['game_off'] = np.concatenate([d['game_off'], offs[1:]])
-    d2['home_team_id'] = np.concatenate([d['home_team_id'], d2['team_id'][offs[:-1]]])
-    ab = B.ActionBatch.from_columns(d2, atomic=atomic)
-    n = ab.n
+                    np.testing.assert_array_equal(got.astype(np.int64), rv.astype(np.int64),
+                                                  err_msg=f'{name} k={k} {Rb}')
+    for nr in (10, 20):
+        lb = ops.labels(ab, nr_actions=nr)
+        lab = vo.labels(cols, atomic=atomic, nr_actions=nr, seg_off=so)
+        for c in ('scores', 'concedes', 'goal_from_shot'):
+            np.testing.assert_array_equal(getattr(lb, c)[:n].cpu().numpy().astype(bool), lab[c],
+                                          err_msg=f'{c} nr={nr}')
     rng = np.random.default_rng(4)
-    probs = [(torch.tensor(rng.random(n), dtype=dt, device=ab.device),
-              torch.tensor(rng.random(n), dtype=dt, device=ab.device))
-             for dt in (torch.float64, torch.float32)]
-
-    def run():
-        i64 = ops.features(ab, default, 3, bool_tile=1024, num_tile=128).to_numpy()[2]
-        lab = []
-        for nr in (10, 20):
-            lb = ops.labels(ab, nr_actions=nr)
-            lab += [t[:n].cpu().numpy() for t in (lb.scores, lb.concedes, lb.goal_from_shot)]
-        vals = [ops.formula(ab, ps, pc).cpu().numpy()[:, :n] for ps, pc in probs]
-        return i64, lab, vals
-
-    for var in ('SA_GS_KERNEL', 'SA_LABELS_SEARCH', 'SA_FORMULA_SEARCH'):
-        monkeypatch.delenv(var, raising=False)
-    ref = run()
-    for var, val in (('SA_GS_KERNEL', 'wave2'), ('SA_LABELS_SEARCH', 'lane'),
-                     ('SA_FORMULA_SEARCH', 'lane')):
-        monkeypatch.setenv(var, val)
-        got = run()
-        monkeypatch.delenv(var)
-        np.testing.assert_array_equal(got[0], ref[0], err_msg=var)
-        for a, b in zip(got[1], ref[1]):
-            np.testing.assert_array_equal(a, b, err_msg=var)
-        for a, b in zip(got[2], ref[2]):
-            np.testing.assert_array_equal(a, b, err_msg=var)
+    for dt in (np.float64, np.float32):
+        ps, pc = rng.random(n).astype(dt), rng.random(n).astype(dt)
+        v = ops.formula(ab, torch.from_numpy(ps).to(ab.device),
+                        torch.from_numpy(pc).to(ab.device)).cpu().numpy()[:, :n]
+        fo = vo.formula(cols, ps, pc, atomic=atomic, seg_off=so)
+        for r, c in enumerate(('offensive_value', 'defensive_value', 'vaep_value')):
+            if dt == np.float32:
+                np.testing.assert_allclose(v[r], fo[c], rtol=1e-6, atol=1e-7, err_msg=c)
+            else:
+                assert_close(v[r], fo[c], c)
 
 
 def test_explicit_frames_match_windowed(sa):
