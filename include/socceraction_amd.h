@@ -135,7 +135,7 @@ typedef struct sa_block {
 int sa_vaep_features(const sa_actions* a, const sa_feature_plan* plan, const sa_block* bool_out,
                      const sa_block* f64_out, const sa_block* i64_out, void* stream);
 
-/* goalscore alone (vaep/features.py:505-539; atomic/vaep/features.py:313-344): writes the
+/* goalscore alone (vaep/features.py:505-539; atomic/vaep/features.py:229-260): writes the
  * goalscore_team / _opponent / _diff columns col, col+1, col+2 of the i64 block.  Also
  * launched by sa_vaep_features when the plan requests SA_XFN_GOALSCORE. */
 int sa_vaep_goalscore(const sa_actions* a, const sa_block* i64_out, int32_t col, void* stream);
@@ -164,7 +164,10 @@ int sa_vaep_formula_f32(const sa_actions* a, const float* p_scores, const float*
  * Accumulates into the caller's zeroed buffers (RCCL-reducible), C = l*w.
  * NaN start coordinates are dropped from shot/goal/move counts (`_count`); a
  * non-finite coordinate that the reference would cast to int64 sets a bit in
- * *err_flags (device int32): 1 = non-finite shot start, 2 = non-finite move coord. */
+ * *err_flags (device int32): 1 = infinite shot start (scoring_prob, action_prob, fit raise),
+ * 2 = infinite move start (action_prob, move_transition_matrix, fit raise), 8 = NaN move start
+ * or non-finite move end (only move_transition_matrix and fit, which cast every move
+ * coordinate, raise; such a move is left out of the transition counts). */
 int sa_xt_count(const sa_actions* a, int32_t l, int32_t w, int64_t* shot, int64_t* goal,
                 int64_t* move, int32_t* trans, int32_t* err_flags, void* stream);
 

@@ -74,7 +74,7 @@ def _polar(x, y):
 
 def _goal_flags(cols: Dict[str, np.ndarray], atomic: bool):
     t = cols['type_id']
-    if atomic:  # atomic/vaep/features.py:330-331, atomic/vaep/labels.py:27-28
+    if atomic:  # atomic/vaep/features.py:246-247, atomic/vaep/labels.py:27-28
         return t == 27, t == 28
     shot = (t == 11) | (t == 12) | (t == 13)  # str.contains('shot') (vaep/features.py:522)
     r = cols['result_id']
@@ -86,7 +86,7 @@ def features(cols: Dict[str, np.ndarray], k: int, xfns: Sequence[str], atomic: b
     """Feature columns ``(name, kind, values)`` in reference order (vaep/base.py:113-116).
 
     ``home`` = per-segment home team id (None: no flip). Windows and the flip follow
-    vaep/features.py:62-116 / atomic/vaep/features.py:170-195.
+    vaep/features.py:62-116 / atomic/vaep/features.py:86-111.
     """
     n = len(cols['type_id'])
     so = segments_of(n, seg_off)
@@ -162,13 +162,13 @@ def features(cols: Dict[str, np.ndarray], k: int, xfns: Sequence[str], atomic: b
             elif x == 'polar':
                 d, g = _polar(a['x'], a['y'])
                 out += [(f'dist_to_goal_a{i}', 'f', d), (f'angle_to_goal_a{i}', 'f', g)]
-            elif x == 'movement_polar':  # atomic/vaep/features.py:279-284
+            elif x == 'movement_polar':  # atomic/vaep/features.py:196-199
                 md = np.sqrt(a['dx'] ** 2 + a['dy'] ** 2)
                 with np.errstate(divide='ignore', invalid='ignore'):
                     ma = np.arctan2(a['dy'], a['dx'])
                 ma = np.where(a['dy'] == 0, 0.0, ma)
                 out += [(f'mov_d_a{i}', 'f', md), (f'mov_angle_a{i}', 'f', ma)]
-            elif x == 'direction':  # atomic/vaep/features.py:302-310
+            elif x == 'direction':  # atomic/vaep/features.py:219-224
                 td = np.sqrt(a['dx'] ** 2 + a['dy'] ** 2)
                 with np.errstate(divide='ignore', invalid='ignore'):
                     ox = np.where(td > 0, a['dx'] / td, a['dx'])

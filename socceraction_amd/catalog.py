@@ -1,7 +1,7 @@
 """Feature-column catalogue: names, dtypes and block layout of every known transformer.
 
 The names and their order reproduce what the reference transformers emit
-(vaep/features.py:119-539, atomic/vaep/features.py:114-344): a ``@simple``
+(vaep/features.py:119-539, atomic/vaep/features.py:114-260): a ``@simple``
 transformer emits its per-frame columns for a0, then a1, ... with an ``_a{i}``
 suffix (features.py:135-143); state features emit one group per previous action.
 

@@ -380,7 +380,7 @@ struct Win {  // one game-state window of the lane's 2 actions (flipped coordina
   int32_t per[2], typ[2], res[2], bp[2];
 };
 
-// Every f64 / i64 column of window i (features.py:151-499, atomic/vaep/features.py:135-310).
+// Every f64 / i64 column of window i (features.py:151-499, atomic/vaep/features.py:135-226).
 template <bool ATOMIC>
 __device__ __forceinline__ void emit_window(const NumCols& C, int i, const Win& w,
                                             const double (&sx0)[2], const double (&sy0)[2],
@@ -467,7 +467,7 @@ __device__ __forceinline__ void emit_window(const NumCols& C, int i, const Win& 
       st_f64x2(fb, C.po + 2 * i, C.nf, Rf, dist[0], dist[1]);
       st_f64x2(fb, C.po + 2 * i + 1, C.nf, Rf, ang[0], ang[1]);
     }
-    if (C.mp >= 0) {  // atomic/vaep/features.py:279-284
+    if (C.mp >= 0) {  // atomic/vaep/features.py:196-199
       double md[2], ma[2];
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
@@ -477,7 +477,7 @@ __device__ __forceinline__ void emit_window(const NumCols& C, int i, const Win& 
       st_f64x2(fb, C.mp + 2 * i, C.nf, Rf, md[0], md[1]);
       st_f64x2(fb, C.mp + 2 * i + 1, C.nf, Rf, ma[0], ma[1]);
     }
-    if (C.di >= 0) {  // atomic/vaep/features.py:302-310
+    if (C.di >= 0) {  // atomic/vaep/features.py:219-224
       double ox[2], oy[2];
 #pragma unroll
       for (int e = 0; e < 2; ++e) {

@@ -134,8 +134,14 @@ __global__ __launch_bounds__(XT_WIDE_THREADS) void xt_count_kernel(sa_actions A,
           if (r == R_SUCCESS) atomicAdd(&goal[c], 1ull);
         }
       } else if (is_move(t)) {
-        if (!isfinite(sx[u]) || !isfinite(sy[u]) || !isfinite(ex[u]) || !isfinite(ey[u])) {
-          bad |= 2;  // move_transition_matrix casts every move coordinate to int64
+        // action_prob's _count drops moves with a NaN start and casts the others (inf raises);
+        // move_transition_matrix casts every move coordinate (NaN or inf raises)
+        if (isnan(sx[u]) || isnan(sy[u])) {
+          bad |= 8;
+          continue;
+        }
+        if (!isfinite(sx[u]) || !isfinite(sy[u])) {
+          bad |= 2;
           continue;
         }
         const int cs = flat_index(sx[u], sy[u], l, w);
@@ -144,6 +150,10 @@ __global__ __launch_bounds__(XT_WIDE_THREADS) void xt_count_kernel(sa_actions A,
           atomicAdd(&hm[cs], 1u);
         else
           atomicAdd(&move[cs], 1ull);
+        if (!isfinite(ex[u]) || !isfinite(ey[u])) {
+          bad |= 8;  // only move_transition_matrix reads the end coordinates
+          continue;
+        }
         if (r == R_SUCCESS) {
           const int ce = flat_index(ex[u], ey[u], l, w);
           SA_DGUARD(ce >= 0 && ce < C, ce, continue);

@@ -238,8 +238,18 @@ def xt_rate_codes(codes: torch.Tensor, n: int, grid: torch.Tensor,
     return out[:n], err
 
 
-def xt_check_errors(acc: XTCounts) -> None:
-    e = int(acc.err.item())
+XT_ERR_SHOT, XT_ERR_MOVE_START, XT_ERR_MOVE_OTHER = 1, 2, 8
+XT_ERR_FIT = XT_ERR_SHOT | XT_ERR_MOVE_START | XT_ERR_MOVE_OTHER
+
+
+def xt_check_errors(acc: XTCounts, mask: int = XT_ERR_FIT) -> None:
+    """Raise where the reference's int64 cast raises. ``mask`` selects what the caller reads:
+    shots (scoring_prob), shots and move starts (action_prob), every move coordinate
+    (move_transition_matrix) or everything (fit)."""
+    e = int(acc.err.item()) & mask
+    if e & XT_ERR_MOVE_OTHER:
+        raise ValueError('Cannot convert non-finite values (NA or inf) to integer '
+                         '(move coordinates)')
     if e & 1:
         raise ValueError('Cannot convert non-finite values (NA or inf) to integer '
                          '(shot start coordinates)')
@@ -279,12 +289,19 @@ def _centres(extent: float, cells: int) -> np.ndarray:
 
 
 def xt_interp_grid(xT: torch.Tensor, l: int, w: int, xs: Optional[np.ndarray] = None,
-                   ys: Optional[np.ndarray] = None, L: int = 1050, W: int = 680) -> torch.Tensor:
+                   ys: Optional[np.ndarray] = None, L: int = 1050, W: int = 680,
+                   cx: Optional[np.ndarray] = None, cy: Optional[np.ndarray] = None) -> torch.Tensor:
     """Bilinear xT surface on the nodes xs x ys (default: the reference's 1050 x 680
-    ``linspace`` grid of ExpectedThreat.rate, xthreat.py:443-451) as a ``[W, L]`` tensor."""
-    cx, cy = _centres(105.0, l), _centres(68.0, w)
+    ``linspace`` grid of ExpectedThreat.rate, xthreat.py:443-451) as a ``[W, L]`` tensor.
+    ``cx`` / ``cy``: the surface's node positions (default: the cell centres of
+    xthreat.py:372-376), strictly increasing."""
+    cx = _centres(105.0, l) if cx is None else np.asarray(cx, np.float64).reshape(-1)
+    cy = _centres(68.0, w) if cy is None else np.asarray(cy, np.float64).reshape(-1)
     if len(cx) != l or len(cy) != w:
         raise ValueError('x and y must have the lengths of the xT surface')  # interp2d would
+    if (np.diff(cx) <= 0).any() or (np.diff(cy) <= 0).any() or \
+            not (np.isfinite(cx).all() and np.isfinite(cy).all()):
+        raise ValueError('x and y must be finite and strictly increasing')
     if xs is None:
         xs = np.linspace(0, 105.0, L)
     if ys is None:

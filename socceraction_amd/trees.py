@@ -49,8 +49,11 @@ class TreeEnsemble:
 
     # ------------------------------------------------------------------ constructors
     @classmethod
-    def from_xgboost_json(cls, model) -> 'TreeEnsemble':
-        """From an xgboost JSON model (dict, JSON text/bytes, or a path to a .json file)."""
+    def from_xgboost_json(cls, model, n_iterations: Optional[int] = None) -> 'TreeEnsemble':
+        """From an xgboost JSON model (dict, JSON text/bytes, or a path to a .json file).
+        ``n_iterations``: keep only the trees of the first n boosting rounds (what
+        ``predict_proba`` evaluates after early stopping: ``iteration_range = (0,
+        best_iteration + 1)``); None = every tree (``Booster.predict``'s default)."""
         if isinstance(model, (bytes, bytearray)):
             model = json.loads(model.decode())
         elif isinstance(model, str):
@@ -67,6 +70,10 @@ class TreeEnsemble:
         if gb.get('name') != 'gbtree':
             raise NotImplementedError(f"xgboost booster {gb.get('name')!r} (gbtree only)")
         trees = gb['model']['trees']
+        if n_iterations is not None:
+            gparam = gb['model'].get('gbtree_model_param', {})
+            per_iter = int(gparam.get('num_parallel_tree', 1) or 1)
+            trees = trees[:max(0, int(n_iterations)) * per_iter]
         parts, roots, off = [], [], 0
         for t in trees:
             left = np.asarray(t['left_children'], np.int64)
@@ -124,18 +131,20 @@ class TreeEnsemble:
 
     @classmethod
     def from_model(cls, model) -> Optional['TreeEnsemble']:
-        """Any supported fitted learner -> TreeEnsemble; None when it is not supported."""
+        """Any supported fitted learner -> TreeEnsemble; None when it is not supported (the
+        caller then runs the learner's own host ``predict_proba``)."""
         try:
             if type(model).__name__ == 'HistGradientBoostingClassifier':
                 return cls.from_sklearn(model)
             if hasattr(model, 'get_booster'):          # xgboost.XGBClassifier
-                return cls.from_xgboost_json(model.get_booster().save_raw('json'))
+                raw = json.loads(bytes(model.get_booster().save_raw('json')).decode())
+                return cls.from_xgboost_json(raw, xgb_classifier_iterations(model, raw))
             if hasattr(model, 'save_raw'):             # xgboost.Booster
                 return cls.from_xgboost_json(model.save_raw('json'))
             if isinstance(model, dict) and 'learner' in model:
                 return cls.from_xgboost_json(model)
-        except NotImplementedError:
-            return None
+        except (NotImplementedError, KeyError, ValueError, TypeError, IndexError):
+            return None  # a model layout this flattening does not know: host predict_proba
         return None
 
     # ------------------------------------------------------------------ evaluation
@@ -209,6 +218,23 @@ class TreeEnsemble:
         return out[:n]
 
 
+def xgb_classifier_iterations(model, raw: Optional[dict] = None) -> Optional[int]:
+    """Boosting rounds ``XGBClassifier.predict_proba`` evaluates: ``best_iteration + 1`` after
+    early stopping (xgboost 1.6 ``XGBModel._get_iteration_range``: the reference's default
+    ``VAEP.fit`` passes ``early_stopping_rounds=10`` with an eval set, vaep/base.py:199-235),
+    else every round (None).  Read from the estimator, or from the booster attributes the JSON
+    model carries (``learner.attributes.best_iteration``)."""
+    try:
+        bi = model.best_iteration
+    except Exception:  # xgboost raises AttributeError when early stopping did not run
+        bi = None
+    if bi is None and raw is not None:
+        bi = raw.get('learner', {}).get('attributes', {}).get('best_iteration')
+    if bi is None:
+        return None
+    return int(bi) + 1
+
+
 def synthetic_xgboost_json(n_features: int, n_trees: int = 100, depth: int = 3, seed: int = 0,
                            feature_kinds: Optional[Sequence[str]] = None,
                            base_score: float = 0.5) -> dict:
@@ -247,4 +273,4 @@ def synthetic_xgboost_json(n_features: int, n_trees: int = 100, depth: int = 3, 
         'feature_names': []}, 'version': [1, 6, 2]}
 
 
-__all__ = ['TreeEnsemble', 'NODE_DTYPE', 'synthetic_xgboost_json']
+__all__ = ['TreeEnsemble', 'NODE_DTYPE', 'synthetic_xgboost_json', 'xgb_classifier_iterations']

@@ -259,9 +259,12 @@ class VAEP:
         from ..trees import TreeEnsemble
         if not {'scores', 'concedes'} <= set(self.__models) or self._split_xfns()[1]:
             return None
-        key = tuple((c, id(m)) for c, m in self.__models.items())
+        # the cache holds the model objects themselves (compared by identity), so a replaced
+        # model can never be mistaken for the cached one through a reused id()
+        key = tuple(self.__models.items())
         cached = getattr(self, '_trees_cache', None)
-        if cached is not None and cached[0] == key:
+        if cached is not None and len(cached[0]) == len(key) and all(
+                c0 == c1 and m0 is m1 for (c0, m0), (c1, m1) in zip(cached[0], key)):
             return cached[1]
         trees = {c: TreeEnsemble.from_model(m) for c, m in self.__models.items()}
         res = trees if all(t is not None for t in trees.values()) else None

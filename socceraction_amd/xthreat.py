@@ -81,7 +81,8 @@ def _safe_divide(a, b) -> np.ndarray:
     return np.divide(a, b, out=np.zeros_like(a), where=b != 0)
 
 
-def _fit_counts(actions: pd.DataFrame, l: int, w: int, process_group=None) -> ops.XTCounts:
+def _fit_counts(actions: pd.DataFrame, l: int, w: int, process_group=None,
+                mask: int = ops.XT_ERR_FIT) -> ops.XTCounts:
     if len(actions):
         acc = ops.xt_count(ActionBatch.from_frame(actions), l, w)
     else:
@@ -90,13 +91,13 @@ def _fit_counts(actions: pd.DataFrame, l: int, w: int, process_group=None) -> op
     if process_group is not None:
         from .shard import allreduce_xt_counts
         allreduce_xt_counts(acc.shot, acc.goal, acc.move, acc.trans, acc.err, process_group)
-    ops.xt_check_errors(acc)
+    ops.xt_check_errors(acc, mask)
     return acc
 
 
 def scoring_prob(actions: pd.DataFrame, l: int = N, w: int = M) -> np.ndarray:
     """P(goal | shot) per cell (reference xthreat.py:74-98)."""
-    mats, _ = ops.xt_normalize(_fit_counts(actions, l, w))
+    mats, _ = ops.xt_normalize(_fit_counts(actions, l, w, mask=ops.XT_ERR_SHOT))
     return mats[0].cpu().numpy().reshape((w, l))
 
 
@@ -113,30 +114,38 @@ def get_successful_move_actions(actions: pd.DataFrame) -> pd.DataFrame:
 
 def action_prob(actions: pd.DataFrame, l: int = N, w: int = M) -> Tuple[np.ndarray, np.ndarray]:
     """P(shoot) and P(move) per cell (reference xthreat.py:144-174)."""
-    mats, _ = ops.xt_normalize(_fit_counts(actions, l, w))
+    mats, _ = ops.xt_normalize(_fit_counts(actions, l, w,
+                                           mask=ops.XT_ERR_SHOT | ops.XT_ERR_MOVE_START))
     m = mats.cpu().numpy()
     return m[1].reshape((w, l)), m[2].reshape((w, l))
 
 
 def move_transition_matrix(actions: pd.DataFrame, l: int = N, w: int = M) -> np.ndarray:
     """P(successful move s -> e | move from s) (reference xthreat.py:177-218)."""
-    _, tt = ops.xt_normalize(_fit_counts(actions, l, w))
+    _, tt = ops.xt_normalize(_fit_counts(
+        actions, l, w, mask=ops.XT_ERR_MOVE_START | ops.XT_ERR_MOVE_OTHER))
     return np.ascontiguousarray(tt.cpu().numpy().T)
 
 
 def _gpu_interp2d(x, y, z, kind='linear', bounds_error=False):
-    """GPU stand-in for ``scipy.interpolate.interp2d`` on the xT cell centres."""
+    """GPU stand-in for ``scipy.interpolate.interp2d(x, y, z, kind='linear')`` on a regular
+    grid: z[j, i] sits at (x[i], y[j]); queries are clamped to the node hull."""
     if kind != 'linear':
         raise NotImplementedError("only kind='linear' is implemented on this backend")
     z = np.asarray(z, dtype=np.float64)
     w, l = z.shape
+    x = np.asarray(x, np.float64).reshape(-1)
+    y = np.asarray(y, np.float64).reshape(-1)
     if len(x) != l or len(y) != w:
         raise ValueError('x and y must have the lengths of the xT surface')
+    if l < 2 or w < 2:
+        raise ValueError('linear interpolation needs at least 2 nodes per axis')
     zt = torch.from_numpy(np.ascontiguousarray(z))
 
     def f(xs, ys):
         from .batch import device
-        g = ops.xt_interp_grid(zt.to(device()), l, w, np.atleast_1d(xs), np.atleast_1d(ys))
+        g = ops.xt_interp_grid(zt.to(device()), l, w, np.atleast_1d(xs), np.atleast_1d(ys),
+                               cx=x, cy=y)
         return g.cpu().numpy()
 
     return f

@@ -410,3 +410,71 @@ def test_play_left_to_right_sa_two_argument_form():
     assert df.start_x.tolist() == [1., 2., 105.]  # input untouched
     pd.testing.assert_frame_equal(out, play_left_to_right(df.assign(home_team_id=1)).drop(
         columns='home_team_id'))
+
+
+class _FakeBooster:
+    def __init__(self, raw):
+        self.raw = raw
+
+    def save_raw(self, fmt):
+        assert fmt == 'json'
+        return bytearray(json.dumps(self.raw).encode())
+
+
+class _FakeXGBClassifier:
+    """The two members of xgboost.XGBClassifier that TreeEnsemble.from_model reads."""
+
+    def __init__(self, raw, best_iteration=None):
+        self._b = _FakeBooster(raw)
+        if best_iteration is not None:
+            self.best_iteration = best_iteration
+
+    def get_booster(self):
+        return self._b
+
+
+def test_xgb_classifier_keeps_only_the_early_stopping_rounds():
+    """After the reference's default fit (early_stopping_rounds=10 with an eval set,
+    vaep/base.py:199-235) XGBClassifier.predict_proba evaluates rounds 0..best_iteration only:
+    the device model must hold exactly those trees -- from the estimator's attribute or from the
+    booster attribute in the JSON dump -- and the full model otherwise."""
+    from oracle import tree_oracle as to
+    from socceraction_amd import trees
+    raw = trees.synthetic_xgboost_json(12, n_trees=30, depth=3, seed=4)
+    full = trees.TreeEnsemble.from_model(_FakeXGBClassifier(raw))
+    assert full.n_trees == 30
+    cut = trees.TreeEnsemble.from_model(_FakeXGBClassifier(raw, best_iteration=19))
+    assert cut.n_trees == 20
+    hand = dict(raw)
+    hand['learner'] = dict(raw['learner'])
+    gb = dict(raw['learner']['gradient_booster'])
+    gb['model'] = dict(gb['model'], trees=raw['learner']['gradient_booster']['model']['trees'][:20])
+    hand['learner']['gradient_booster'] = gb
+    ref = trees.TreeEnsemble.from_xgboost_json(hand)
+    np.testing.assert_array_equal(cut.nodes, ref.nodes)
+    np.testing.assert_array_equal(cut.roots, ref.roots)
+    # the booster attribute inside the JSON dump (xgboost stores attributes as strings)
+    attr = dict(raw)
+    attr['learner'] = dict(raw['learner'], attributes={'best_iteration': '7'})
+    assert trees.TreeEnsemble.from_model(_FakeXGBClassifier(attr)).n_trees == 8
+    # a raw Booster / dict predicts with every tree (Booster.predict's default range)
+    assert trees.TreeEnsemble.from_model(attr).n_trees == 30
+    # the dropped rounds change the probabilities (oracle restatement of the prediction rule)
+    X = np.random.default_rng(1).normal(0, 30, (50, 12))
+    assert not np.array_equal(to.predict_xgboost_json(hand, X), to.predict_xgboost_json(raw, X))
+
+
+def test_unsupported_model_layouts_fall_back_to_the_host():
+    """A model dump this flattening does not know (missing keys, odd values) gives None, so
+    VAEP.rate runs the learner's own predict_proba instead of failing."""
+    from socceraction_amd import trees
+    raw = trees.synthetic_xgboost_json(4, n_trees=2, depth=2, seed=1)
+    broken = dict(raw)
+    broken['learner'] = dict(raw['learner'])
+    broken['learner'].pop('learner_model_param')
+    assert trees.TreeEnsemble.from_model(broken) is None
+    odd = dict(raw)
+    odd['learner'] = dict(raw['learner'], learner_model_param={'base_score': '[5E-1]',
+                                                               'num_feature': '4'})
+    assert trees.TreeEnsemble.from_model(odd) is None
+    assert trees.TreeEnsemble.from_model(object()) is None

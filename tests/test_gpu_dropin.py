@@ -301,3 +301,64 @@ def test_xt_row_sharded_solve_two_ranks(grid):
     assert out['world'] == 2 and out['grid'] == grid
     assert out['ok'] and out['bit_identical_matrices'] and out['bit_identical_heatmaps']
     assert out['iterations'] == out['single_iterations']
+
+
+def test_xt_module_functions_on_nan_move_ends():
+    """The reference's scoring_prob never reads moves and action_prob reads only their (NaN
+    dropped) starts, so NaN / inf end coordinates on passes leave both computable; only
+    move_transition_matrix (and fit) cast every move coordinate and raise
+    (xthreat.py:40-67, 74-98, 144-174, 177-218)."""
+    from oracle import xt_oracle as xo
+    from socceraction_amd import synthetic
+    from socceraction_amd import xthreat as xt
+    d = synthetic.spadl_games(6, seed=17)
+    n = len(d['type_id'])
+    rng = np.random.default_rng(3)
+    moves = np.nonzero(np.isin(d['type_id'], (0, 1, 21)))[0]
+    d['end_x'][rng.choice(moves, 25, replace=False)] = np.nan
+    d['end_y'][rng.choice(moves, 5, replace=False)] = np.inf
+    nan_start = rng.choice(moves, 9, replace=False)
+    d['start_y'][nan_start] = np.nan  # dropped by _count, cast (raise) by the transition matrix
+    df = synthetic.to_frame(d)
+    cols = {c: d[c] for c in ('type_id', 'result_id', 'start_x', 'start_y', 'end_x', 'end_y')}
+    ref = xo.fit(cols, 16, 12)  # its count() drops NaN starts like _count
+    np.testing.assert_array_equal(xt.scoring_prob(df), ref['scoring_prob'])
+    ps, pm = xt.action_prob(df)
+    np.testing.assert_array_equal(ps, ref['shot_prob'])
+    np.testing.assert_array_equal(pm, ref['move_prob'])
+    with pytest.raises(ValueError):
+        xt.move_transition_matrix(df)
+    with pytest.raises(ValueError):
+        xt.ExpectedThreat().fit(df)
+    # an infinite move START raises in action_prob too, but not in scoring_prob
+    d['start_y'][nan_start] = d['start_x'][nan_start]
+    d['start_x'][moves[0]] = np.inf
+    df = synthetic.to_frame(d)
+    with pytest.raises(ValueError):
+        xt.action_prob(df)
+    assert xt.scoring_prob(df).shape == (12, 16)
+    assert n == len(df)
+
+
+def test_interp2d_uses_the_given_nodes():
+    """xthreat.interp2d(x, y, z) interpolates between the nodes it is given (not always the
+    cell centres): the oracle's bilinear rule on shifted, unevenly spaced nodes."""
+    from socceraction_amd import xthreat as xt
+    rng = np.random.default_rng(8)
+    z = rng.random((5, 7))
+    x = np.cumsum(rng.random(7) + 0.5)
+    y = np.cumsum(rng.random(5) + 0.5)
+    xs, ys = np.linspace(-1, x[-1] + 1, 41), np.linspace(-1, y[-1] + 1, 37)
+    got = xt.interp2d(x=x, y=y, z=z, kind='linear', bounds_error=False)(xs, ys)
+
+    def br(c, q):
+        q = np.clip(q, c[0], c[-1])
+        i = np.clip(np.searchsorted(c, q, side='right') - 1, 0, len(c) - 2)
+        return i, (q - c[i]) / (c[i + 1] - c[i])
+    i, tx = br(x, xs)
+    j, ty = br(y, ys)
+    ref = ((1 - tx) * z[j][:, i] + tx * z[j][:, i + 1]) * (1 - ty)[:, None] + \
+        ((1 - tx) * z[j + 1][:, i] + tx * z[j + 1][:, i + 1]) * ty[:, None]
+    assert_close(got, ref, 'interp2d nodes')
+    with pytest.raises(ValueError):
+        xt.interp2d(x=x[::-1], y=y, z=z)

@@ -255,6 +255,34 @@ def test_xt_goldens(sa):
                 assert_close(r.cpu().numpy(), g[f'{tag}_rate_interp'], f'{name} {tag} interp rate')
 
 
+def test_xt105_interpolated_rate_golden(sa):
+    """cfg5's ExpectedThreat(105, 68).rate(use_interpolation=True) == the reference's own output
+    (tests/golden/make_golden_xt105.py): the 1050 x 680 surface (strided sample) and the rating
+    of every action, through ops and through the drop-in ExpectedThreat."""
+    import os
+
+    from golden_io import GOLDEN
+    from socceraction_amd import xthreat
+    B, ops = sa['batch'], sa['ops']
+    with np.load(os.path.join(GOLDEN, 'xt105_interp.npz'), allow_pickle=False) as z:
+        g = {k: z[k] for k in z.files}
+    df = frame(g)
+    ab = B.ActionBatch.from_frame(df)
+    rows, cols = g['grid_rows'], g['grid_cols']
+    for tag in ('fit', 'random'):
+        xT = torch.tensor(g[f'{tag}_xT'], device=ab.device)
+        grid = ops.xt_interp_grid(xT, 105, 68)
+        assert tuple(grid.shape) == (680, 1050)
+        assert_close(grid.cpu().numpy()[np.ix_(rows, cols)], g[f'{tag}_grid_sample'], f'{tag} grid')
+        r, err = ops.xt_rate(ab, grid, 1050, 680)
+        assert int(err.item()) == 0
+        assert_close(r.cpu().numpy(), g[f'{tag}_rate_interp'], f'{tag} interp rate')
+        m = xthreat.ExpectedThreat(l=105, w=68)
+        m.xT = g[f'{tag}_xT'].copy()
+        assert_close(m.rate(df, use_interpolation=True), g[f'{tag}_rate_interp'], f'{tag} drop-in')
+        assert_close(m.rate(df), g[f'{tag}_rate'], f'{tag} drop-in cells')
+
+
 @pytest.mark.parametrize('l,w,games', [(16, 12, 2000), (40, 30, 300), (105, 68, 300)])
 def test_xt_large_grid_vs_oracle(sa, l, w, games):
     """16 x 12 over ~3.2M actions: the one-workgroup-per-CU count pass (XC_WIDE, every CU's

@@ -1,9 +1,11 @@
 """The CPU oracle reproduces the reference's goldens (CPU only, no GPU)."""
+import os
+
 import numpy as np
 import pandas as pd
 import pytest
 
-from golden_io import assert_close, cases, inputs, ks, load
+from golden_io import GOLDEN, assert_close, cases, inputs, ks, load
 from oracle import vaep_oracle as vo
 from oracle import xt_oracle as xo
 
@@ -81,6 +83,25 @@ def test_xt_oracle(name):
         assert_close(xo.rate(cols, g[f'{tag}_xT']), g[f'{tag}_rate'], 'rate')
         if f'{tag}_rate_interp' in g:
             assert_close(xo.rate(cols, g[f'{tag}_xT'], True), g[f'{tag}_rate_interp'], 'interp')
+
+
+def _xt105():
+    with np.load(os.path.join(GOLDEN, 'xt105_interp.npz'), allow_pickle=False) as z:
+        return {k: z[k] for k in z.files}
+
+
+def test_xt105_interpolated_rate_oracle():
+    """cfg5's rate(use_interpolation=True) at 105 x 68 (reference-generated golden,
+    tests/golden/make_golden_xt105.py): surface sample and per-action ratings."""
+    g = _xt105()
+    cols = inputs(g)
+    rows, cs = g['grid_rows'], g['grid_cols']
+    for tag in ('fit', 'random'):
+        xT = g[f'{tag}_xT']
+        assert xT.shape == (68, 105)
+        assert_close(xo.interp_grid(xT)[np.ix_(rows, cs)], g[f'{tag}_grid_sample'], f'{tag} grid')
+        assert_close(xo.rate(cols, xT), g[f'{tag}_rate'], f'{tag} rate')
+        assert_close(xo.rate(cols, xT, True), g[f'{tag}_rate_interp'], f'{tag} interp rate')
 
 
 @pytest.mark.parametrize('name', cases('dribbles'))
