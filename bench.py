@@ -49,6 +49,33 @@ KERNEL_NAMES = {'bool_features': 'bool_colgroup_kernel', 'num_features': 'num_fe
                 'formula': 'formula_kernel',
                 'xt_fit_rate': 'xt_count_kernel + xt_solve_small_kernel + xt_rate_codes_kernel'}
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+STEP_BYTES = 1029  # VAEP feat + labels + formula, inputs read once + outputs written once
+
+
+def launch_ranks(n: int, argv, run=None) -> int:
+    """``bench.py --gpus N`` started outside torch.distributed.run: start one rank per GPU as a
+    CHILD ``python -m torch.distributed.run`` (this process has not touched the GPU; it never
+    execs) with the same arguments, let the child's rank 0 print the JSON line, and return the
+    child's exit status."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', f'--nproc-per-node={n}',
+           '--master-addr', '127.0.0.1', '--master-port', str(port), os.path.abspath(__file__)]
+    cmd += list(argv)
+    env = dict(os.environ, MASTER_ADDR='127.0.0.1')
+    env.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')  # dmabuf IPC only on this driver
+    return (run or subprocess.run)(cmd, env=env).returncode
+
+
+def check_world(gpus: int) -> None:
+    """Under torch.distributed.run the launched world must be the --gpus the line reports."""
+    ws = int(os.environ.get('WORLD_SIZE', '1'))
+    if ws != gpus:
+        print(f'bench.py: --gpus {gpus} but WORLD_SIZE={ws}', file=sys.stderr)
+        raise SystemExit(2)
 
 
 def _dist():
@@ -247,6 +274,70 @@ def rate_extra(ab, out, n, dev, reps: int = 5) -> dict:
             'actions_per_s_predict_both_models': round(n / (2 * ms_tree) * 1e3, 1)}
 
 
+def e2e_extra(d, games: int, reps: int = 2) -> dict:
+    """End to end through the pandas drop-in, the way a notebook would call the batched API
+    (SURVEY §8(d) "report end-to-end separately"): actions DataFrame in -> H2D -> features +
+    labels + formula kernels -> D2H -> reference-shaped DataFrames out, for the first ``games``
+    games of the step's batch (a bounded sample: the 16M x 568 frame of the whole batch is
+    15 GB of host memory)."""
+    from socceraction_amd import vaep
+    from socceraction_amd.batch import ActionBatch
+    off = d['game_off']
+    m = int(off[games])
+    sub = {k: (v[:m] if isinstance(v, np.ndarray) and v.shape == d['type_id'].shape else v)
+           for k, v in d.items()}
+    sub['game_off'] = off[:games + 1]
+    sub['home_team_id'] = d['home_team_id'][:games]
+    actions = synthetic.to_frame(sub)
+    gframe = synthetic.games_frame(sub)
+    p = synthetic.probabilities(m)
+    model = vaep.VAEP()
+    home_of = gframe.set_index('game_id')['home_team_id']
+
+    def once():
+        t = [time.perf_counter()]
+        X = model.compute_features_batch(gframe, actions)
+        t.append(time.perf_counter())
+        Y = model.compute_labels_batch(gframe, actions)
+        t.append(time.perf_counter())
+        ab = ActionBatch.from_frame(actions, home_team_id=home_of, segments='game')
+        v = ops.formula(ab, torch.from_numpy(p['scores']).to(ab.device),
+                        torch.from_numpy(p['concedes']).to(ab.device)).cpu().numpy()[:, :m]
+        V = pd.DataFrame({'offensive_value': v[0], 'defensive_value': v[1], 'vaep_value': v[2]})
+        t.append(time.perf_counter())
+        assert X.shape == (m, 568) and Y.shape == (m, 2) and len(V) == m
+        return np.diff(t)
+    import pandas as pd
+    once()  # warm-up (pinned buffers, first launches)
+    best = min((once() for _ in range(reps)), key=lambda x: x.sum())
+    return {'workload': f'pandas in -> pandas out through the drop-in batched API: '
+                        f'compute_features_batch + compute_labels_batch + formula of {games} games '
+                        '(H2D, kernels, D2H, DataFrame assembly; bounded sample of the step batch)',
+            'actions': m, 'seconds': round(float(best.sum()), 4),
+            'actions_per_s': round(m / float(best.sum()), 1),
+            'split_seconds': {'features_frame': round(float(best[0]), 4),
+                              'labels_frame': round(float(best[1]), 4),
+                              'formula_frame': round(float(best[2]), 4)}}
+
+
+def reference_cpu_record() -> dict:
+    """The reference's own CPU path (pandas), timed by scripts/time_reference.py in the BUILD
+    container (the reference never travels): profiles/reference_cpu.json, or None."""
+    path = os.path.join(ROOT, 'profiles', 'reference_cpu.json')
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        rec = json.load(f)
+    return {'value': rec['one_process']['actions_per_s'], 'unit': 'actions/s', 'cores': 1,
+            'kind': 'reference',
+            'pool': {'value': rec['pool']['actions_per_s'], 'processes': rec['pool']['processes']},
+            'step_one_process_with_xt_16x12': rec.get('step_one_process_actions_per_s'),
+            'where': f"build container ({rec['host']['cpu']}, {rec['host']['os_cpu_count']} "
+                     'vCPU), not the GPU host: the reference never travels',
+            'sample': rec['workload'], 'source': 'profiles/reference_cpu.json '
+                                                 '(scripts/time_reference.py)'}
+
+
 def cpu_baseline(d, seconds: float) -> dict:
     """The oracle port (numpy, 1 thread) on the GPU box's host, over whole games: VAEP features
     + labels + formula per game, then the xT 16x12 fit + rate over the games done."""
@@ -283,6 +374,8 @@ def main() -> None:
     ap.add_argument('--warmup', type=int, default=3)
     ap.add_argument('--games', type=int, default=10000, help='games per GPU (cfg2: 10k)')
     ap.add_argument('--cpu-seconds', type=float, default=15.0)
+    ap.add_argument('--e2e-games', type=int, default=1000,
+                    help='games of the end-to-end (pandas in -> pandas out) side entry (0: skip)')
     ap.add_argument('--no-cpu', action='store_true')
     ap.add_argument('--no-side', action='store_true',
                     help='skip the cfg3 (atomic) and cfg5 (xT 105x68) side measurements')
@@ -313,6 +406,11 @@ def main() -> None:
     ap.add_argument('--num-tile', type=int, default=128,
                     help='rows per f64/i64-block tile (0 = one tile: plain column-major)')
     args = ap.parse_args()
+    if args.gpus < 1:
+        raise SystemExit('--gpus must be >= 1')
+    if 'WORLD_SIZE' not in os.environ and args.gpus > 1:
+        raise SystemExit(launch_ranks(args.gpus, sys.argv[1:]))
+    check_world(args.gpus)
 
     dist, rank, world = _dist()
     dev = B.device()
@@ -468,6 +566,8 @@ def main() -> None:
         extra_side['atomic_cfg3'] = atomic_extra(dist, rank, world, dev, args.atomic_games)
         extra_side['convert_to_atomic'] = convert_extra(d, dist, dev)
         extra_side['rate_on_device'] = rate_extra(ab, out, n, dev)
+        if args.e2e_games > 0 and rank == 0:
+            extra_side['end_to_end'] = e2e_extra(d, min(args.e2e_games, args.games))
     if rank != 0:
         if dist:
             dist.destroy_process_group()
@@ -505,7 +605,12 @@ def main() -> None:
                      'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 4),
                      'traffic': traffic, 'traffic_unit': 'HBM bytes per launch (rocprofv3 PMC)',
                      'algorithmic_bytes': BYTES[dom] * n, 'kernel': KERNEL_NAMES[dom],
-                     'bytes_per_action': BYTES[dom]},
+                     'bytes_per_action': BYTES[dom],
+                     # the whole step against the roofline: the VAEP path's 1,029 B/action
+                     #  of every action of every rank / step time / N x 8 TB/s
+                     'step_frac': round(STEP_BYTES * total_actions / (ms_per_step * 1e-3)
+                                        / (world * HBM_PEAK_GBS * 1e9), 4),
+                     'step_bytes_per_action': STEP_BYTES},
     }
     line['xt_cfg4'] = {'workload': 'cfg4 inside the step: xT 16x12 fit (count + all-reduce + '
                                    'value iteration to eps=1e-5) + rate of the step\'s actions',
@@ -524,6 +629,9 @@ def main() -> None:
     line.update(extra_side)
     if not args.no_cpu and world == 1:  # the CPU comparator runs on rank 0 at N = 1 only
         line['cpu_baseline'] = cpu_baseline(d, args.cpu_seconds)
+        ref = reference_cpu_record()
+        if ref is not None:
+            line['cpu_baseline']['reference'] = ref
     print(json.dumps(line), flush=True)
     if dist:
         dist.destroy_process_group()

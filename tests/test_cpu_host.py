@@ -478,3 +478,40 @@ def test_unsupported_model_layouts_fall_back_to_the_host():
                                                                'num_feature': '4'})
     assert trees.TreeEnsemble.from_model(odd) is None
     assert trees.TreeEnsemble.from_model(object()) is None
+
+
+def test_bench_launches_one_rank_per_gpu(monkeypatch):
+    """bench.py --gpus N outside torch.distributed.run starts the N ranks as a child torchrun
+    (never exec) and forwards its exit status; under torchrun a world that is not --gpus is
+    refused, so a --gpus 8 run cannot print an N = 1 line."""
+    import sys
+
+    import bench
+    calls = []
+
+    class _Done:
+        returncode = 3
+
+    def fake_run(cmd, env):
+        calls.append((cmd, env))
+        return _Done()
+    assert bench.launch_ranks(2, ['--gpus', '2', '--steps', '3'], run=fake_run) == 3
+    cmd, env = calls[0]
+    assert cmd[:4] == [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1']
+    assert '--nproc-per-node=2' in cmd and cmd[cmd.index('--master-addr') + 1] == '127.0.0.1'
+    assert cmd[-4:] == ['--gpus', '2', '--steps', '3'] and cmd[-5].endswith('bench.py')
+    assert env['MASTER_ADDR'] == '127.0.0.1' and 'HSA_ENABLE_IPC_MODE_LEGACY' in env
+    monkeypatch.delenv('WORLD_SIZE', raising=False)
+    monkeypatch.setattr(bench, 'launch_ranks', lambda n, argv: 5 if n == 2 else 0)
+    monkeypatch.setattr(sys, 'argv', ['bench.py', '--gpus', '2', '--steps', '1'])
+    with pytest.raises(SystemExit) as e:
+        bench.main()
+    assert e.value.code == 5
+    monkeypatch.setenv('WORLD_SIZE', '4')
+    monkeypatch.setattr(sys, 'argv', ['bench.py', '--gpus', '2'])
+    with pytest.raises(SystemExit) as e:
+        bench.main()
+    assert e.value.code == 2
+    monkeypatch.setenv('WORLD_SIZE', '1')
+    monkeypatch.setattr(sys, 'argv', ['bench.py', '--gpus', '1'])
+    bench.check_world(1)  # the driver's N = 1 line under a 1-rank torchrun

@@ -1,0 +1,28 @@
+"""bench.py's multi-rank entry on the GPU box: ``bench.py --gpus 2`` (no torchrun around it)
+launches two ranks itself and prints ONE line with n_gpus == 2.  The rehearsal shares the test
+GPU between the ranks over gloo (SA_DIST_BACKEND=gloo); the driver's N = 1..8 runs use RCCL
+with one rank per GPU."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_bench_gpus_2_launches_two_ranks():
+    env = dict(os.environ, SA_DIST_BACKEND='gloo')
+    env.pop('WORLD_SIZE', None)
+    p = subprocess.run([sys.executable, 'bench.py', '--gpus', '2', '--games', '20', '--steps', '2',
+                        '--warmup', '1', '--no-side', '--no-cpu'], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=240)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith('{')]
+    assert p.returncode == 0 and len(lines) == 1, p.stdout[-2000:] + p.stderr[-3000:]
+    out = json.loads(lines[0])
+    assert out['n_gpus'] == 2 and out['value'] > 0
+    assert out['config']['actions_per_gpu'] > 0
+    assert 0 < out['roofline']['step_frac'] < 1
