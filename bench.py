@@ -43,11 +43,23 @@ BYTES = {'bool_features': 7 + 515,             # type/result/bodypart u8 + team 
          # count pass 34 B + its 4-B rate codes, rate 4 + 8 B (solve: 192 cells)
          'xt_fit_rate': 34 + 4 + 4 + 8}
 KERNELS = ('bool_features', 'num_features', 'goalscore', 'labels', 'formula', 'xt_fit_rate')
+STEP_CALLS = ('bool_features', 'num_features', 'goalscore', 'labels', 'formula')
 # the HIP kernel each step entry launches (socceraction_amd/csrc/sa_vaep.hip)
 KERNEL_NAMES = {'bool_features': 'bool_colgroup_kernel', 'num_features': 'num_features_kernel',
                 'goalscore': 'goalscore_wave16_kernel', 'labels': 'labels_kernel',
                 'formula': 'formula_kernel',
-                'xt_fit_rate': 'xt_count_kernel + xt_solve_small_kernel + xt_rate_codes_kernel'}
+                'xt_fit_rate': 'xt_count_kernel + xt_solve_lds_kernel + xt_rate_cells_kernel'}
+
+
+def step_bytes(xt_source: str) -> dict:
+    """Algorithmic bytes per action of each step entry for an xT source (bench xt_step)."""
+    b = dict(BYTES)
+    if xt_source == 'cells':  # the f64 pass writes 4 B of cell code; count reads 4, rate 4 + 8
+        b['num_features'] += 4
+        b['xt_fit_rate'] = 4 + 4 + 8
+    elif xt_source == 'coords':  # count 34 B, rate 34 + 8
+        b['xt_fit_rate'] = 34 + 34 + 8
+    return b
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 STEP_BYTES = 1029  # VAEP feat + labels + formula, inputs read once + outputs written once
 
@@ -103,20 +115,25 @@ def _reduce(dist, value, op, dev):
     return float(t.item())
 
 
-def xt_step(ab, dist, use_codes: bool = True, shared: bool = True):
+def xt_step(ab, dist, source: str = 'cells', cells=None, shared: bool = True):
     """BASELINE cfg4 inside the step: xT 16x12 fit on the step's actions (count pass, RCCL
     all-reduce of the counts across ranks, value iteration to eps=1e-5; the solve synchronises
     its stream) and ExpectedThreat.rate of every action, as two phases so the caller can enqueue
-    the VAEP kernels in between. Returns (start, finish, holder of the last solution)."""
+    the VAEP kernels in between. Returns (start, finish, holder of the last solution).
+
+    source 'cells': count and rate read the 4-B cell codes the f64 feature pass wrote into
+    ``cells`` (sa_vaep_features_xt); 'codes': the count pass reads the coordinates and writes a
+    4-B rate operand per action for the rate; 'coords': both passes read the coordinates."""
     from socceraction_amd import shard
     state = {}
-    # the count pass also writes each action's rate operand (4 B), so the rate reads that
-    # instead of the coordinates and ids again (42 -> 12 B per action)
-    codes = ops.xt_rate_codes_buffer(ab.n, ab.device) if use_codes else None
+    codes = ops.xt_rate_codes_buffer(ab.n, ab.device) if source == 'codes' else None
     rate_out = torch.empty(max((ab.n + 15) // 16 * 16, 16), dtype=torch.float64, device=ab.device)
 
     def start():
-        acc = ops.xt_count(ab, 16, 12, codes=codes, shared=shared)
+        if source == 'cells':
+            acc = ops.xt_count_cells(cells, ab.n, 16, 12, shared=shared)
+        else:
+            acc = ops.xt_count(ab, 16, 12, codes=codes, shared=shared)
         if dist is not None and dist.get_backend() == 'nccl':
             shard.allreduce_xt_counts(acc.shot, acc.goal, acc.move, acc.trans, acc.err)
         elif dist is not None:  # gloo rehearsal: the same sum through host memory
@@ -128,7 +145,9 @@ def xt_step(ab, dist, use_codes: bool = True, shared: bool = True):
 
     def finish():
         sol = ops.xt_solve(state.pop('acc'))  # synchronises the current stream
-        if codes is not None:
+        if source == 'cells':
+            ops.xt_rate_cells(cells, ab.n, 16, 12, sol.mats[3], out=rate_out)
+        elif source == 'codes':
             ops.xt_rate_codes(codes, ab.n, sol.mats[3], out=rate_out)
         else:
             ops.xt_rate(ab, sol.mats[3].reshape(12, 16), 16, 12)
@@ -387,22 +406,22 @@ def main() -> None:
     ap.add_argument('--serial', action='store_true',
                     help='run the xT fit + rate after the VAEP kernels on the same stream '
                          '(default: on a side stream, overlapped)')
-    ap.add_argument('--xt-fork', type=int, default=0,
-                    help='overlapped mode: VAEP kernels enqueued before the side stream forks '
-                         'for the xT count pass (0: first; 1 / 2 / serial measured 1.9 / 4 / 6 %% '
-                         'slower per step, profiles/r01g_xt_fork_ab.log)')
+    ap.add_argument('--xt-fork', type=int, default=-1,
+                    help='overlapped mode: VAEP calls enqueued before the side stream forks for '
+                         'the xT count pass (-1: right after num_features with --xt-source cells, '
+                         'else 0)')
     ap.add_argument('--bool-tile', type=int, default=1024,
                     help='rows per bool-block tile (0 = one tile: plain column-major)')
     ap.add_argument('--order', default='num_features,bool_features,goalscore,labels,formula',
                     help='launch order of the VAEP kernels in the step (default measured 1.3 %% '
                          'faster than bool first, in-process A/B: profiles/r01h_order_ab.log)')
-    ap.add_argument('--xt-rate-coords', action='store_true',
-                    help='xT rate from the coordinates (default: from the count pass\'s codes)')
-    ap.add_argument('--ab-orders', default='',
-                    help='dev tool: ";"-separated launch orders timed round-robin in one process')
-    ap.add_argument('--aux', type=int, default=0,
-                    help='run the last A VAEP kernels (goalscore, labels, formula) on a third '
-                         'stream next to the feature kernels (0: all on the main stream)')
+    ap.add_argument('--xt-source', default='cells', choices=('cells', 'codes', 'coords'),
+                    help='what the xT count + rate passes read: the cell codes the f64 feature '
+                         'pass writes (4 B/action, default), or the coordinates (34 B/action; '
+                         '"codes": the count pass writes 4-B rate operands for the rate)')
+    ap.add_argument('--ab', default='',
+                    help='dev tool: ";"-separated step variants "name:key=value/..." (keys xt, '
+                         'order with "+", fork) timed round-robin in one process')
     ap.add_argument('--num-tile', type=int, default=128,
                     help='rows per f64/i64-block tile (0 = one tile: plain column-major)')
     args = ap.parse_args()
@@ -443,101 +462,95 @@ def main() -> None:
     lab = ops.LabelBlocks(n, lab_buf[0], lab_buf[1], None)
     val = torch.empty((3, ld), dtype=torch.float64, device=dev)
     s_act = ab.struct()
-    xt_start, xt_finish, xt_last = xt_step(ab, dist, use_codes=not args.xt_rate_coords,
-                                           shared=not args.serial)
-    by_name = {'bool_features': lambda: ops.features_into(s_act, bool_out),
-               'num_features': lambda: ops.features_into(s_act, num_out),
-               'goalscore': lambda: ops.goalscore_into(ab, out),
-               'labels': lambda: ops.labels(ab, 10, lab),
-               'formula': lambda: ops.formula(ab, ps, pc, val)}
-    order = args.order.split(',')
-    if sorted(order) != sorted(by_name):
-        raise SystemExit(f'--order must be a permutation of {",".join(by_name)}')
-    calls = tuple(by_name[k] for k in order)
+    cells = ops.xt_cells_buffer(n, dev)
     main_s = torch.cuda.current_stream()
     side = torch.cuda.Stream() if not args.serial else main_s
-    aux = torch.cuda.Stream() if args.aux > 0 and not args.serial else None
-    aux_ab = torch.cuda.Stream() if args.ab_orders else None  # for "^A" A/B entries
-    nv = len(calls)
-    n_main = nv - (args.aux if aux is not None else 0)  # calls[n_main:] run on `aux`
+    overlap = side is not main_s
 
-    def step(ev=None, calls=calls, xt_fork=args.xt_fork, xt_start=xt_start, xt_finish=xt_finish,
-             aux=aux, n_main=n_main):
-        # default: the xT fit runs on a side stream next to the VAEP kernels -- the first
-        # `xt_fork` VAEP kernels are enqueued, then the side stream forks for the count pass and
-        # RCCL all-reduce, then the remaining VAEP kernels, then the solve (a single workgroup
-        # that would otherwise leave the GPU idle, and a host sync of the side stream) and the
-        # rate. --aux A: the last A VAEP kernels (goalscore / labels / formula: latency-bound
-        # scans and look-aheads) run on a third stream next to the feature kernels.
-        # --serial: everything on the one stream.  ev[i] = (start, end) of call i on its stream.
-        overlap = side is not main_s
-        if aux is not None:
-            fork_a = torch.cuda.Event()
-            fork_a.record(main_s)
-            aux.wait_event(fork_a)
-        for i, call in enumerate(calls):
-            st = main_s if i < n_main else aux
-            if overlap and i == min(xt_fork, n_main - 1):
-                fork = torch.cuda.Event()
-                fork.record(main_s)
-                side.wait_event(fork)
-                with torch.cuda.stream(side):
-                    if ev is not None:
-                        ev[nv][0].record(side)
-                    xt_start()
-            with torch.cuda.stream(st):
+    def make_step(spec):
+        """One step of the given variant: the VAEP kernels in `order` on the main stream; the xT
+        fit + rate on a side stream forked before VAEP call `fork` (after num_features at the
+        latest when the feature pass writes the xT cell codes), joined at the end."""
+        xt, order, fork = spec['xt'], spec['order'], spec['fork']
+        if sorted(order) != sorted(STEP_CALLS):
+            raise SystemExit(f'order must be a permutation of {",".join(STEP_CALLS)}')
+        if xt == 'cells' and overlap and fork <= order.index('num_features'):
+            raise SystemExit('xt=cells: the side stream forks after num_features')
+        by_name = {'bool_features': lambda: ops.features_into(s_act, bool_out),
+                   'num_features': (lambda: ops.features_into(s_act, num_out,
+                                                              xt_cells=(16, 12, cells)))
+                   if xt == 'cells' else (lambda: ops.features_into(s_act, num_out)),
+                   'goalscore': lambda: ops.goalscore_into(ab, out),
+                   'labels': lambda: ops.labels(ab, 10, lab),
+                   'formula': lambda: ops.formula(ab, ps, pc, val)}
+        calls = tuple(by_name[k] for k in order)
+        xt_start, xt_finish, xt_last = xt_step(ab, dist, xt, cells, shared=overlap)
+        nv = len(calls)
+
+        def step(ev=None):
+            # ev[i] = (start, end) of VAEP call i on the main stream, ev[nv] = the xT side
+            # stream's span (count pass + all-reduce, then solve -- a host sync of the side
+            # stream -- and rate); --serial: everything on the one stream
+            for i, call in enumerate(calls):
+                if overlap and i == fork:
+                    fk = torch.cuda.Event()
+                    fk.record(main_s)
+                    side.wait_event(fk)
+                    with torch.cuda.stream(side):
+                        if ev is not None:
+                            ev[nv][0].record(side)
+                        xt_start()
                 if ev is not None:
-                    ev[i][0].record(st)
+                    ev[i][0].record(main_s)
                 call()
                 if ev is not None:
-                    ev[i][1].record(st)
-        if not overlap:
-            if ev is not None:
-                ev[nv][0].record(main_s)
-            xt_start()
-        with torch.cuda.stream(side):
-            xt_finish()
-            if ev is not None:
-                ev[nv][1].record(side)
-        for other in ((side,) if overlap else ()) + ((aux,) if aux is not None else ()):
-            join = torch.cuda.Event()
-            join.record(other)
-            main_s.wait_event(join)
+                    ev[i][1].record(main_s)
+            if not overlap:
+                if ev is not None:
+                    ev[nv][0].record(main_s)
+                xt_start()
+            with torch.cuda.stream(side):
+                xt_finish()
+                if ev is not None:
+                    ev[nv][1].record(side)
+            if overlap:
+                join = torch.cuda.Event()
+                join.record(side)
+                main_s.wait_event(join)
+        return step, xt_last
 
-    if args.ab_orders:  # in-process A/B of launch orders on the same allocations (dev tool)
-        # entries "k1,k2,...[@F][#coords]": a launch order, optionally with the xT fork point F
-        # and the coordinate-reading xT rate instead of the count pass's codes
-        specs = args.ab_orders.split(';')
-        xt_coords = xt_step(ab, dist, use_codes=False)
-        ab_ms = {sp: [] for sp in specs}
-        for _ in range(args.warmup):
-            step()
-        for rnd in range(4):
-            for sp in specs:
-                sp1, _, env = sp.partition('!')  # "!VAR=value": set for this entry
-                if env:
-                    k_, _, v_ = env.partition('=')
-                    os.environ[k_] = v_
-                sp2, _, na = sp1.partition('^')  # "^A": last A kernels on a third stream
-                sp0, _, xv = sp2.partition('#')
-                o, _, f = sp0.partition('@')
-                cs = tuple(by_name[k] for k in o.split(','))
-                fk = int(f) if f else args.xt_fork
-                xs, xf = (xt_coords[0], xt_coords[1]) if xv == 'coords' else (xt_start, xt_finish)
-                kw = dict(calls=cs, xt_fork=fk, xt_start=xs, xt_finish=xf)
-                if na:
-                    kw.update(aux=aux_ab, n_main=len(cs) - int(na))
-                step(**kw)
+    base = {'xt': args.xt_source, 'order': args.order.split(','), 'fork': args.xt_fork}
+    if base['fork'] < 0:  # default: before the first VAEP call, or right after num_features
+        base['fork'] = (base['order'].index('num_features') + 1) if args.xt_source == 'cells' else 0
+    if args.ab:  # in-process A/B of step variants on the same allocations (dev tool)
+        # ";"-separated "name:key=value/key=value" with keys xt, order (names joined by "+"), fork
+        variants = {}
+        for spec in args.ab.split(';'):
+            name, _, opts = spec.partition(':')
+            v = dict(base)
+            for kv in [o for o in opts.split('/') if o]:
+                k_, _, v_ = kv.partition('=')
+                v[k_] = v_.split('+') if k_ == 'order' else (int(v_) if k_ == 'fork' else v_)
+            variants[name] = make_step(v)[0]
+        ab_ms = {k: [] for k in variants}
+        for fn in variants.values():
+            for _ in range(args.warmup):
+                fn()
+        for _ in range(4):
+            for k, fn in variants.items():
+                fn()
                 torch.cuda.synchronize()
                 t = time.perf_counter()
                 for _ in range(args.steps):
-                    step(**kw)
+                    fn()
                 torch.cuda.synchronize()
-                ab_ms[sp].append(round((time.perf_counter() - t) / args.steps * 1e3, 4))
-                if env:
-                    os.environ.pop(k_, None)
-        print(json.dumps({'ab_orders_ms_per_step': ab_ms}), flush=True)
+                ab_ms[k].append(round((time.perf_counter() - t) / args.steps * 1e3, 4))
+        if rank == 0:
+            print(json.dumps({'ab_ms_per_step': ab_ms, 'n': n}), flush=True)
         return
+    step, xt_last = make_step(base)
+    order = base['order']
+    nv = len(order)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -574,11 +587,12 @@ def main() -> None:
         return
     ms_per_step = wall / args.steps * 1e3
     value = total_actions * args.steps / wall
-    dom = max(KERNELS, key=lambda k: BYTES[k])  # dominant kernel by algorithmic bytes
-    achieved = BYTES[dom] * n / (kern[dom] * 1e-3) / 1e9
-    per_kernel = {k: {'ms': round(kern[k], 4), 'bytes_per_action': BYTES[k],
-                      'achieved_GBs': round(BYTES[k] * n / (kern[k] * 1e-3) / 1e9, 1)}
-                  for k in KERNELS}
+    bts = step_bytes(base['xt'])
+    dom = max(KERNELS, key=lambda k: bts[k])  # dominant kernel by algorithmic bytes
+    achieved = bts[dom] * n / (kern[dom] * 1e-3) / 1e9
+    per_kernel = {k: {'ms': round(kern[k], 4), 'bytes_per_action': bts[k],
+                      'achieved_GBs': round(bts[k] * n / (kern[k] * 1e-3) / 1e9, 1)}
+                  for k in KERNELS if k in kern}
     traffic = None
     pmc = os.path.join(ROOT, 'profiles', 'pmc_dominant_kernel.json')
     if os.path.exists(pmc):
@@ -604,8 +618,8 @@ def main() -> None:
         'roofline': {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS,
                      'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 4),
                      'traffic': traffic, 'traffic_unit': 'HBM bytes per launch (rocprofv3 PMC)',
-                     'algorithmic_bytes': BYTES[dom] * n, 'kernel': KERNEL_NAMES[dom],
-                     'bytes_per_action': BYTES[dom],
+                     'algorithmic_bytes': bts[dom] * n, 'kernel': KERNEL_NAMES[dom],
+                     'bytes_per_action': bts[dom],
                      # the whole step against the roofline: the VAEP path's 1,029 B/action
                      #  of every action of every rank / step time / N x 8 TB/s
                      'step_frac': round(STEP_BYTES * total_actions / (ms_per_step * 1e-3)
@@ -618,14 +632,15 @@ def main() -> None:
                        # rate's end (it shares the GPU with the VAEP kernels meanwhile)
                        'ms' if args.serial else 'span_ms': round(kern['xt_fit_rate'], 4),
                        'iterations': xt_last['sol'].n_iter,
+                       'source': {'cells': 'cell codes written by the f64 feature pass',
+                                  'codes': 'coordinates (count) + rate operands',
+                                  'coords': 'coordinates'}[base['xt']],
                        'stream': 'main (serial)' if args.serial else
-                       f'side stream, forked after {args.xt_fork} VAEP kernel(s), overlapped '
+                       f"side stream, forked after {base['fork']} VAEP call(s), overlapped "
                        'with the rest'}
     line['vaep_order'] = order
     line['streams'] = ('one stream' if args.serial else
-                       f'VAEP feature kernels on the main stream, xT on a side stream'
-                       + (f', {", ".join(order[n_main:])} on a third stream'
-                          if aux is not None else ''))
+                       'VAEP kernels on the main stream, xT on a side stream')
     line.update(extra_side)
     if not args.no_cpu and world == 1:  # the CPU comparator runs on rank 0 at N = 1 only
         line['cpu_baseline'] = cpu_baseline(d, args.cpu_seconds)

@@ -135,6 +135,14 @@ typedef struct sa_block {
 int sa_vaep_features(const sa_actions* a, const sa_feature_plan* plan, const sa_block* bool_out,
                      const sa_block* f64_out, const sa_block* i64_out, void* stream);
 
+/* sa_vaep_features that also writes, in the same pass, the xT cell code (sa_xt_cells) of every
+ * action for a fit + rate of these actions on the (xt_l, xt_w) grid -- the VAEP + xT step of
+ * one batch (BASELINE cfg2 + cfg4) reads the coordinates from HBM once.  SPADL windowed mode;
+ * xt_cells: [n] u32, 16-byte aligned. */
+int sa_vaep_features_xt(const sa_actions* a, const sa_feature_plan* plan, const sa_block* bool_out,
+                        const sa_block* f64_out, const sa_block* i64_out, int32_t xt_l, int32_t xt_w,
+                        uint32_t* xt_cells, void* stream);
+
 /* goalscore alone (vaep/features.py:505-539; atomic/vaep/features.py:229-260): writes the
  * goalscore_team / _opponent / _diff columns col, col+1, col+2 of the i64 block.  Also
  * launched by sa_vaep_features when the plan requests SA_XFN_GOALSCORE. */
@@ -181,6 +189,24 @@ int sa_xt_count(const sa_actions* a, int32_t l, int32_t w, int64_t* shot, int64_
 int sa_xt_count_codes(const sa_actions* a, int32_t l, int32_t w, int64_t* shot, int64_t* goal,
                       int64_t* move, int32_t* trans, int32_t* err_flags, uint32_t* codes,
                       int32_t flags, void* stream);
+
+/* xT cell codes: the binning of a fit + rate of the SAME actions on an (l, w) grid with
+ * l * w <= SA_XT_CELLS_MAX_C, computed once per action where the coordinates are read anyway
+ * (sa_vaep_features_xt, or sa_xt_cells alone) and consumed by sa_xt_count_cells and
+ * sa_xt_rate_cells, which then read 4 B per action instead of the 34 B of coordinates and ids.
+ * Code (u32): bits 0-11 start cell, 12-23 end cell (xthreat.py:25-37 binning), 24-25 class
+ * (1 = shot, type 11; 2 = move: pass / dribble / cross), 26 result == success, 27 NaN in the
+ * start coordinates, 28 start not finite, 29 end not finite.  cells: [n] u32, 16-byte aligned.
+ * sa_xt_count_cells accumulates exactly what sa_xt_count does on those actions (same counts,
+ * same err_flags bits); sa_xt_rate_cells equals sa_xt_rate without interpolation (grid = the
+ * (w, l) xT surface). */
+#define SA_XT_CELLS_MAX_C 4096
+int sa_xt_cells(const sa_actions* a, int32_t l, int32_t w, uint32_t* cells, void* stream);
+int sa_xt_count_cells(const uint32_t* cells, int64_t n, int32_t l, int32_t w, int64_t* shot,
+                      int64_t* goal, int64_t* move, int32_t* trans, int32_t* err_flags,
+                      int32_t flags, void* stream);
+int sa_xt_rate_cells(const uint32_t* cells, int64_t n, int32_t l, int32_t w, const double* grid,
+                     double* out, int32_t* err_flags, void* stream);
 
 /* Normalise the counts into the reference's matrices and run the value iteration
  * x <- s*p_shot + p_move * (T x) until no cell changes by more than eps

@@ -20,6 +20,7 @@ DEBUG_LIB = os.path.join(HERE, '_lib', 'libsocceraction_amd_debug.so')
 LIB_PATH = os.environ.get('SOCCERACTION_AMD_LIB') or (DEBUG_LIB if DEBUG else DEFAULT_LIB)
 
 SA_MAX_FRAMES = 8
+SA_XT_CELLS_MAX_C = 4096
 SA_BOOL_TILE_QUANTUM = 1024
 SA_NUM_TILE_QUANTUM = 128
 SA_OK, SA_EINVAL, SA_EHIP, SA_EDATA, SA_ENOMEM = 0, -1, -2, -3, -4
@@ -98,6 +99,16 @@ _SIGNATURES = {
                                          ctypes.c_int32, _p, _p, _p, _p, _p, _p,
                                          ctypes.c_int32, _p]),
     'sa_xt_rate_codes': (ctypes.c_int, [_p, ctypes.c_int64, _p, _p, _p, _p]),
+    'sa_vaep_features_xt': (ctypes.c_int, [ctypes.POINTER(SaActions),
+                                           ctypes.POINTER(SaFeaturePlan), ctypes.POINTER(SaBlock),
+                                           ctypes.POINTER(SaBlock), ctypes.POINTER(SaBlock),
+                                           ctypes.c_int32, ctypes.c_int32, _p, _p]),
+    'sa_xt_cells': (ctypes.c_int, [ctypes.POINTER(SaActions), ctypes.c_int32, ctypes.c_int32, _p,
+                                   _p]),
+    'sa_xt_count_cells': (ctypes.c_int, [_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, _p,
+                                         _p, _p, _p, _p, ctypes.c_int32, _p]),
+    'sa_xt_rate_cells': (ctypes.c_int, [_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, _p,
+                                        _p, _p, _p]),
     'sa_xt_solve': (ctypes.c_int, [_p, _p, _p, _p, ctypes.c_int32, ctypes.c_int32,
                                    ctypes.c_double, ctypes.c_int32, _p, _p, _p,
                                    ctypes.POINTER(ctypes.c_int32), _p]),

@@ -7,6 +7,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cmath>
+
 #include "../../include/socceraction_amd.h"
 #include "sa_debug.h"
 
@@ -71,6 +73,45 @@ __device__ __forceinline__ uint32_t ld_u8x4(const uint8_t* __restrict__ p, int64
 #pragma unroll
   for (int q = 0; q < 4; ++q) w |= (uint32_t)ld_or0(p, b + q, n) << (8 * q);
   return w;
+}
+
+// -------------------------------------------------------------------------------------
+// xT binning (reference xthreat.py:25-37): numpy float64 -> int64 cast (x86 cvttsd2si: NaN /
+// out of range -> INT64_MIN), then clip; (x / 105) * l in f64, divide THEN multiply.
+__device__ __forceinline__ int cell_index(double v, int l) {
+  long long c = (v >= -9.2233720368547758e18 && v < 9.2233720368547758e18) ? (long long)v
+                                                                             : (long long)INT64_MIN;
+  return c < 0 ? 0 : (c > l - 1 ? l - 1 : (int)c);
+}
+
+__device__ __forceinline__ int flat_index(double x, double y, int l, int w) {
+  int xi = cell_index(x / FIELD_L * (double)l, l);
+  int yj = cell_index(y / FIELD_W * (double)w, w);
+  return (w - 1 - yj) * l + xi;
+}
+
+__device__ __forceinline__ bool is_move(int t) { return t == T_PASS || t == T_DRIBBLE || t == T_CROSS; }
+
+// xT cell code of one SPADL action for a fit + rate of the same actions on an (l, w) grid with
+// l * w <= SA_XT_CELLS_MAX_C (include/socceraction_amd.h): written once per action where the
+// coordinates are already in registers (the VAEP feature pass, or sa_xt_cells), read by the
+// count and rate passes instead of the 34 B of coordinates and ids.
+//   bits 0-11 start cell, 12-23 end cell (0 when not binned), 24-25 class (1 shot = type 11,
+//   2 move = pass / dribble / cross), 26 result == success, 27 start has a NaN, 28 start not
+//   finite, 29 end not finite.
+constexpr uint32_t XT_CELL_SHOT = 1u, XT_CELL_MOVE = 2u;
+
+__device__ __forceinline__ uint32_t xt_cell_code(int t, int r, double sx, double sy, double ex,
+                                                 double ey, int l, int w) {
+  const uint32_t cls = t == T_SHOT ? XT_CELL_SHOT : (is_move(t) ? XT_CELL_MOVE : 0u);
+  const bool snan = isnan(sx) || isnan(sy);
+  const bool sfin = isfinite(sx) && isfinite(sy);
+  const bool efin = isfinite(ex) && isfinite(ey);
+  uint32_t c = (cls << 24) | ((uint32_t)(r == R_SUCCESS) << 26) | ((uint32_t)snan << 27) |
+               ((uint32_t)!sfin << 28) | ((uint32_t)!efin << 29);
+  if (cls != 0 && sfin) c |= (uint32_t)flat_index(sx, sy, l, w);
+  if (cls == XT_CELL_MOVE && efin) c |= (uint32_t)flat_index(ex, ey, l, w) << 12;
+  return c;
 }
 
 }  // namespace sa

@@ -57,6 +57,8 @@ struct FeatArgs {
   int64_t* iout;
   int64_t Cb, Cf, Ci;  // columns of each block
   int64_t Rb, Rf, Ri;  // rows per tile of each block (include/socceraction_amd.h)
+  uint32_t* xt_cells;  // optional: xT cell code of every action (sa_vaep_features_xt)
+  int32_t xt_l, xt_w;
 };
 
 // Workgroups are dispatched round-robin over the 8 XCDs (XCD = blockIdx % 8).  Writing the
@@ -638,6 +640,18 @@ __global__ __launch_bounds__(256) void num_features_kernel(FeatArgs args) {
         load_row1(F0, jb - 1 < 0 ? 0 : jb - 1, ATOMIC, pool[0]);
         load_row1(F0, jb - 2 < 0 ? 0 : jb - 2, ATOMIC, pool[1]);
       }
+      if (!ATOMIC && args.xt_cells) {  // the raw (unflipped) rows jb, jb+1: xT cell codes
+        uint32_t cc[2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+          cc[e] = xt_cell_code((cand[e].ids >> 8) & 0xFF, (cand[e].ids >> 16) & 0xFF, cand[e].c0,
+                               cand[e].c1, cand[e].c2, cand[e].c3, args.xt_l, args.xt_w);
+        if (jb + 2 <= n) {
+          *reinterpret_cast<uint2*>(args.xt_cells + jb) = make_uint2(cc[0], cc[1]);
+        } else {
+          args.xt_cells[jb] = cc[0];
+        }
+      }
 #pragma unroll 1
       for (int i = 0; i < K; ++i) {
         if (i > 0) {
@@ -670,6 +684,9 @@ __global__ __launch_bounds__(256) void num_features_kernel(FeatArgs args) {
         for (int e = 0; e < 2; ++e) {
           const int64_t r = EXPLICIT ? jr[e] : jr[e] - (dd[e] < i ? dd[e] : i);
           load_row(Fi, r, ATOMIC, w, e);
+          if (!ATOMIC && !EXPLICIT && i == 0 && args.xt_cells && jb + e < n)  // raw row jb+e
+            args.xt_cells[jb + e] = xt_cell_code(w.typ[e], w.res[e], w.c0[e], w.c1[e], w.c2[e],
+                                                 w.c3[e], args.xt_l, args.xt_w);
           if (!EXPLICIT && away[e]) flip<ATOMIC>(w, e);
           if (i == 0) {
             sx0[e] = w.c0[e];
@@ -1112,9 +1129,31 @@ static int check_block(const sa_block* b, int64_t n, int64_t quantum, const char
   return SA_OK;
 }
 
+static int launch_features(const sa_actions* a, const sa_feature_plan* plan, const sa_block* bool_out,
+                           const sa_block* f64_out, const sa_block* i64_out, int32_t xt_l,
+                           int32_t xt_w, uint32_t* xt_cells, void* stream);
+
 extern "C" int sa_vaep_features(const sa_actions* a, const sa_feature_plan* plan,
                                 const sa_block* bool_out, const sa_block* f64_out,
                                 const sa_block* i64_out, void* stream) {
+  return launch_features(a, plan, bool_out, f64_out, i64_out, 0, 0, nullptr, stream);
+}
+
+extern "C" int sa_vaep_features_xt(const sa_actions* a, const sa_feature_plan* plan,
+                                   const sa_block* bool_out, const sa_block* f64_out,
+                                   const sa_block* i64_out, int32_t xt_l, int32_t xt_w,
+                                   uint32_t* xt_cells, void* stream) {
+  if (!a) return fail(SA_EINVAL, "null sa_actions");
+  if (a->atomic || a->n_frames != 1) return fail(SA_EINVAL, "xT cells need SPADL actions in windowed mode");
+  if (xt_l < 1 || xt_w < 1 || (int64_t)xt_l * xt_w > SA_XT_CELLS_MAX_C)
+    return fail(SA_EINVAL, "xT cell codes need 1 <= l * w <= %d", SA_XT_CELLS_MAX_C);
+  if (!xt_cells || !aligned16(xt_cells)) return fail(SA_EINVAL, "xt_cells must be 16-byte aligned");
+  return launch_features(a, plan, bool_out, f64_out, i64_out, xt_l, xt_w, xt_cells, stream);
+}
+
+static int launch_features(const sa_actions* a, const sa_feature_plan* plan, const sa_block* bool_out,
+                           const sa_block* f64_out, const sa_block* i64_out, int32_t xt_l,
+                           int32_t xt_w, uint32_t* xt_cells, void* stream) {
   int rc = check_actions(a, true);
   if (rc) return rc;
   if (!plan) return fail(SA_EINVAL, "null plan");
@@ -1162,7 +1201,10 @@ extern "C" int sa_vaep_features(const sa_actions* a, const sa_feature_plan* plan
                 wi ? i64_out->n_cols : 0,
                 wb ? bool_out->tile_rows : 16,
                 wf ? f64_out->tile_rows : 16,
-                wi ? i64_out->tile_rows : 16};
+                wi ? i64_out->tile_rows : 16,
+                xt_cells,
+                xt_l,
+                xt_w};
   const dim3 grid(xcd_grid((a->n + BLOCK_ACTS - 1) / BLOCK_ACTS)), block(BLOCK_WAVES * WAVE);
   const bool expl = a->n_frames > 1;
   if (wb) {  // one wave per (tile, group of ~32 columns), XCD-contiguous sweep order
@@ -1184,7 +1226,7 @@ extern "C" int sa_vaep_features(const sa_actions* a, const sa_feature_plan* plan
     rc = check_launch("bool_colgroup_kernel");
     if (rc) return rc;
   }
-  if (wn) {
+  if (wn || xt_cells) {
     const bool fast = !expl && K <= 3;  // register-resident windows (KF = 3)
     if (a->atomic) {
       if (expl)

@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstring>
 #include <vector>
 
 #include "sa_common.h"
@@ -21,21 +22,6 @@
 #endif
 
 namespace sa {
-
-// numpy float64 -> int64 cast (x86 cvttsd2si: NaN / out of range -> INT64_MIN), then clip.
-__device__ __forceinline__ int cell_index(double v, int l) {
-  long long c = (v >= -9.2233720368547758e18 && v < 9.2233720368547758e18) ? (long long)v
-                                                                             : (long long)INT64_MIN;
-  return c < 0 ? 0 : (c > l - 1 ? l - 1 : (int)c);
-}
-
-__device__ __forceinline__ int flat_index(double x, double y, int l, int w) {
-  int xi = cell_index(x / FIELD_L * (double)l, l);
-  int yj = cell_index(y / FIELD_W * (double)w, w);
-  return (w - 1 - yj) * l + xi;
-}
-
-__device__ __forceinline__ bool is_move(int t) { return t == T_PASS || t == T_DRIBBLE || t == T_CROSS; }
 
 // Rate operand of one action for a later rate() on the same (l, w) grid, written by the count
 // pass so the rate pass reads 4 B instead of the 34 B of coordinates and ids again
@@ -67,8 +53,86 @@ constexpr int XT_WIDE_THREADS = 1024;
 constexpr int XT_SMALL_ACTS = 32768;  // actions per workgroup in XC_SMALL / XC_VEC
 enum { XC_GLOBAL = 0, XC_VEC = 1, XC_SMALL = 2, XC_WIDE = 3 };
 
+// One action's part of the count pass: shot/goal/move histograms and the successful-move
+// transition count, with the reference's non-finite rules (xthreat.py:40-67: _count drops rows
+// with a NaN start, casts the rest; :177-218: move_transition_matrix casts every move
+// coordinate).  Error bits: 1 = infinite shot start, 2 = infinite move start, 8 = NaN move start
+// or non-finite move end (see sa_xt_count).
+struct XtAct {
+  uint32_t cls;            // 0, XT_CELL_SHOT, XT_CELL_MOVE
+  bool succ, snan, sfin, efin;
+  int cs, ce;              // start / end cell (valid when binned)
+};
+
 template <int MODE>
-__global__ __launch_bounds__(XT_WIDE_THREADS) void xt_count_kernel(sa_actions A, int l, int w,
+__device__ __forceinline__ void count_one(const XtAct& a, int C, uint32_t* hs, uint32_t* hg, uint32_t* hm,
+                                          uint32_t* ht, unsigned long long* shot,
+                                          unsigned long long* goal, unsigned long long* move,
+                                          int32_t* trans, int32_t& bad) {
+  constexpr bool SMALL = MODE == XC_SMALL, WIDE = MODE == XC_WIDE, VEC = MODE != XC_GLOBAL;
+  if (a.cls == XT_CELL_SHOT) {
+    if (a.snan) return;  // _count drops NaN rows (xthreat.py:60-61)
+    if (!a.sfin) {
+      bad |= 1;
+      return;
+    }
+    SA_DGUARD(a.cs >= 0 && a.cs < C, a.cs, return);
+    if (VEC) {
+      atomicAdd(&hs[a.cs], 1u);
+      if (a.succ) atomicAdd(&hg[a.cs], 1u);
+    } else {
+      atomicAdd(&shot[a.cs], 1ull);
+      if (a.succ) atomicAdd(&goal[a.cs], 1ull);
+    }
+  } else if (a.cls == XT_CELL_MOVE) {
+    if (a.snan) {  // dropped by action_prob's _count; move_transition_matrix's cast raises
+      bad |= 8;
+      return;
+    }
+    if (!a.sfin) {
+      bad |= 2;
+      return;
+    }
+    SA_DGUARD(a.cs >= 0 && a.cs < C, a.cs, return);
+    if (VEC)
+      atomicAdd(&hm[a.cs], 1u);
+    else
+      atomicAdd(&move[a.cs], 1ull);
+    if (!a.efin) {
+      bad |= 8;  // only move_transition_matrix reads the end coordinates
+      return;
+    }
+    if (a.succ) {
+      SA_DGUARD(a.ce >= 0 && a.ce < C, a.ce, return);
+      const int64_t k = (int64_t)a.cs * C + a.ce;
+      if (SMALL)
+        atomicAdd(&ht[k >> 1], (k & 1) ? 0x10000u : 1u);
+      else if (WIDE)
+        atomicAdd(&ht[k], 1u);
+      else
+        atomicAdd(&trans[k], 1);
+    }
+  }
+}
+
+__device__ __forceinline__ XtAct decode_cell(uint32_t c) {
+  XtAct a;
+  a.cls = (c >> 24) & 3u;
+  a.succ = (c >> 26) & 1u;
+  a.snan = (c >> 27) & 1u;
+  a.sfin = !((c >> 28) & 1u);
+  a.efin = !((c >> 29) & 1u);
+  a.cs = (int)(c & 0xFFFu);
+  a.ce = (int)((c >> 12) & 0xFFFu);
+  return a;
+}
+
+// CELLS = false: reads the actions' coordinates and ids (34 B per action) and may write each
+// action's rate operand (`codes`, sa_xt_count_codes).  CELLS = true: reads the 4-B cell codes a
+// producer wrote (sa_xt_count_cells).
+template <int MODE, bool CELLS>
+__global__ __launch_bounds__(XT_WIDE_THREADS) void xt_count_kernel(sa_actions A, const uint32_t* __restrict__ cells,
+                                                                  int64_t n, int l, int w,
                                                                   unsigned long long* __restrict__ shot,
                                                                   unsigned long long* __restrict__ goal,
                                                                   unsigned long long* __restrict__ move,
@@ -77,7 +141,6 @@ __global__ __launch_bounds__(XT_WIDE_THREADS) void xt_count_kernel(sa_actions A,
                                                                   uint32_t* __restrict__ codes) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   const int C = l * w;
-  const int64_t n = A.n;
   const sa_frame& F = A.frames[0];
   uint32_t* hs = lds;          // [C]
   uint32_t* hg = lds + C;      // [C]
@@ -100,73 +163,50 @@ __global__ __launch_bounds__(XT_WIDE_THREADS) void xt_count_kernel(sa_actions A,
   int32_t bad = 0;
   // XC_U actions per thread per pass, every load issued before any is used (the loop is
   // otherwise one HBM round trip per action); rows past `end` are clamped and skipped
-  constexpr int XC_U = 4;
+  constexpr int XC_U = CELLS ? 8 : 4;
   for (int64_t j0 = begin; j0 < end; j0 += XC_U * stride) {
-    int tt[XC_U], rr[XC_U];
-    double sx[XC_U], sy[XC_U], ex[XC_U], ey[XC_U];
+    XtAct act[XC_U];
+    if (CELLS) {
+      uint32_t cv[XC_U];
 #pragma unroll
-    for (int u = 0; u < XC_U; ++u) {
-      const int64_t j = j0 + u * stride < end ? j0 + u * stride : end - 1;
-      tt[u] = j0 + u * stride < end ? F.type_id[j] : -1;
-      rr[u] = F.result_id[j];
-      sx[u] = F.c0[j];
-      sy[u] = F.c1[j];
-      ex[u] = F.c2[j];
-      ey[u] = F.c3[j];
-    }
+      for (int u = 0; u < XC_U; ++u) {
+        const int64_t j = j0 + u * stride < end ? j0 + u * stride : end - 1;
+        cv[u] = cells[j];
+      }
 #pragma unroll
-    for (int u = 0; u < XC_U; ++u) {
-      const int t = tt[u], r = rr[u];
-      if (codes && t >= 0) codes[j0 + u * stride] = rate_code(t, r, sx[u], sy[u], ex[u], ey[u], l, w);
-      if (t == T_SHOT) {
-        if (isnan(sx[u]) || isnan(sy[u])) continue;  // _count drops NaN rows (xthreat.py:60-61)
-        if (!isfinite(sx[u]) || !isfinite(sy[u])) {
-          bad |= 1;
-          continue;
-        }
-        const int c = flat_index(sx[u], sy[u], l, w);
-        SA_DGUARD(c >= 0 && c < C, c, continue);
-        if (VEC) {
-          atomicAdd(&hs[c], 1u);
-          if (r == R_SUCCESS) atomicAdd(&hg[c], 1u);
-        } else {
-          atomicAdd(&shot[c], 1ull);
-          if (r == R_SUCCESS) atomicAdd(&goal[c], 1ull);
-        }
-      } else if (is_move(t)) {
-        // action_prob's _count drops moves with a NaN start and casts the others (inf raises);
-        // move_transition_matrix casts every move coordinate (NaN or inf raises)
-        if (isnan(sx[u]) || isnan(sy[u])) {
-          bad |= 8;
-          continue;
-        }
-        if (!isfinite(sx[u]) || !isfinite(sy[u])) {
-          bad |= 2;
-          continue;
-        }
-        const int cs = flat_index(sx[u], sy[u], l, w);
-        SA_DGUARD(cs >= 0 && cs < C, cs, continue);
-        if (VEC)
-          atomicAdd(&hm[cs], 1u);
-        else
-          atomicAdd(&move[cs], 1ull);
-        if (!isfinite(ex[u]) || !isfinite(ey[u])) {
-          bad |= 8;  // only move_transition_matrix reads the end coordinates
-          continue;
-        }
-        if (r == R_SUCCESS) {
-          const int ce = flat_index(ex[u], ey[u], l, w);
-          SA_DGUARD(ce >= 0 && ce < C, ce, continue);
-          const int64_t k = (int64_t)cs * C + ce;
-          if (SMALL)
-            atomicAdd(&ht[k >> 1], (k & 1) ? 0x10000u : 1u);
-          else if (WIDE)
-            atomicAdd(&ht[k], 1u);
-          else
-            atomicAdd(&trans[k], 1);
-        }
+      for (int u = 0; u < XC_U; ++u) {
+        act[u] = decode_cell(cv[u]);
+        if (j0 + u * stride >= end) act[u].cls = 0;
+      }
+    } else {
+      int tt[XC_U], rr[XC_U];
+      double sx[XC_U], sy[XC_U], ex[XC_U], ey[XC_U];
+#pragma unroll
+      for (int u = 0; u < XC_U; ++u) {
+        const int64_t j = j0 + u * stride < end ? j0 + u * stride : end - 1;
+        tt[u] = j0 + u * stride < end ? F.type_id[j] : -1;
+        rr[u] = F.result_id[j];
+        sx[u] = F.c0[j];
+        sy[u] = F.c1[j];
+        ex[u] = F.c2[j];
+        ey[u] = F.c3[j];
+      }
+#pragma unroll
+      for (int u = 0; u < XC_U; ++u) {
+        const int t = tt[u], r = rr[u];
+        if (codes && t >= 0) codes[j0 + u * stride] = rate_code(t, r, sx[u], sy[u], ex[u], ey[u], l, w);
+        XtAct& a = act[u];
+        a.cls = t == T_SHOT ? XT_CELL_SHOT : (is_move(t) ? XT_CELL_MOVE : 0u);
+        a.succ = r == R_SUCCESS;
+        a.snan = isnan(sx[u]) || isnan(sy[u]);
+        a.sfin = isfinite(sx[u]) && isfinite(sy[u]);
+        a.efin = isfinite(ex[u]) && isfinite(ey[u]);
+        a.cs = (a.cls && a.sfin) ? flat_index(sx[u], sy[u], l, w) : 0;
+        a.ce = (a.cls == XT_CELL_MOVE && a.succ && a.efin) ? flat_index(ex[u], ey[u], l, w) : 0;
       }
     }
+#pragma unroll
+    for (int u = 0; u < XC_U; ++u) count_one<MODE>(act[u], C, hs, hg, hm, ht, shot, goal, move, trans, bad);
   }
   if (bad) atomicOr(err, bad);
   if (VEC) {
@@ -191,6 +231,23 @@ __global__ __launch_bounds__(XT_WIDE_THREADS) void xt_count_kernel(sa_actions A,
       if (v >> 16) atomicAdd(&trans[2 * k + 1], (int32_t)(v >> 16));
     }
   }
+}
+
+// Cell codes alone (the binning of the count pass): one thread per 4 actions, 16-B stores.
+__global__ __launch_bounds__(256) void xt_cells_kernel(sa_actions A, int l, int w, uint32_t* __restrict__ cells) {
+  const int64_t j0 = 4 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x);
+  if (j0 >= A.n) return;
+  const sa_frame& F = A.frames[0];
+  u32x4 v = {0, 0, 0, 0};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int64_t j = j0 + q < A.n ? j0 + q : A.n - 1;
+    v[q] = xt_cell_code(F.type_id[j], F.result_id[j], F.c0[j], F.c1[j], F.c2[j], F.c3[j], l, w);
+  }
+  if (j0 + 4 <= A.n)
+    *reinterpret_cast<u32x4*>(cells + j0) = v;
+  else
+    for (int q = 0; j0 + q < A.n; ++q) cells[j0 + q] = v[q];
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -646,6 +703,36 @@ __global__ __launch_bounds__(256) void xt_rate_codes_kernel(const uint32_t* __re
   if (bad && err) atomicOr(err, bad);
 }
 
+// rate() from the cell codes (grid = the fitted (w, l) surface): a thread rates 4 actions
+// (one 16-B code load, two 16-B stores) -- 12 B per action.
+__global__ __launch_bounds__(256) void xt_rate_cells_kernel(const uint32_t* __restrict__ cells, int64_t n,
+                                                            int C, const double* __restrict__ grid,
+                                                            double* __restrict__ out,
+                                                            int32_t* __restrict__ err) {
+  const int64_t j0 = 4 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x);
+  if (j0 >= n) return;
+  int32_t bad = 0;
+  auto one = [&](uint32_t c) -> double {
+    const XtAct a = decode_cell(c);
+    if (a.cls != XT_CELL_MOVE || !a.succ) return __builtin_nan("");
+    if (!a.sfin || !a.efin) {
+      bad = 4;  // the reference's int64 cast of a non-finite coordinate raises
+      return __builtin_nan("");
+    }
+    SA_DGUARD(a.cs < C && a.ce < C, c, return __builtin_nan(""));
+    return grid[a.ce] - grid[a.cs];
+  };
+  if (j0 + 4 <= n) {
+    const u32x4 c = *reinterpret_cast<const u32x4*>(cells + j0);
+    const f64x2 x = {one(c[0]), one(c[1])}, y = {one(c[2]), one(c[3])};
+    __builtin_nontemporal_store(x, reinterpret_cast<f64x2*>(out + j0));
+    __builtin_nontemporal_store(y, reinterpret_cast<f64x2*>(out + j0 + 2));
+  } else {
+    for (int64_t j = j0; j < n; ++j) out[j] = one(cells[j]);
+  }
+  if (bad && err) atomicOr(err, bad);
+}
+
 }  // namespace sa
 
 // ================================== C ABI =================================================
@@ -654,6 +741,58 @@ using namespace sa;
 extern "C" int sa_xt_count(const sa_actions* a, int32_t l, int32_t w, int64_t* shot, int64_t* goal,
                            int64_t* move, int32_t* trans, int32_t* err_flags, void* stream) {
   return sa_xt_count_codes(a, l, w, shot, goal, move, trans, err_flags, nullptr, 0, stream);
+}
+
+// Count-pass launcher shared by the coordinate path (cells == nullptr) and the cell-code path.
+static int launch_count(const sa_actions& A, const uint32_t* cells, int64_t n, int32_t l, int32_t w,
+                        int64_t* shot, int64_t* goal, int64_t* move, int32_t* trans, int32_t* err_flags,
+                        uint32_t* codes, int32_t flags, hipStream_t st) {
+  const int C = l * w;
+  const size_t small_lds = (size_t)(3 * C + (C * C + 1) / 2) * 4;
+  auto* us = reinterpret_cast<unsigned long long*>(shot);
+  auto* ug = reinterpret_cast<unsigned long long*>(goal);
+  auto* um = reinterpret_cast<unsigned long long*>(move);
+  const size_t vec_lds = (size_t)3 * C * 4;
+  const unsigned wg_blocks = (unsigned)((n + XT_SMALL_ACTS - 1) / XT_SMALL_ACTS);
+  const size_t wide_lds = (size_t)(3 * C + C * C) * 4;
+  const bool cl = cells != nullptr;
+  // SA_XT_COUNT_SHARED: the pass runs next to other kernels (bench.py's side stream), so use the
+  // 80-KB-LDS workgroups that co-reside with them instead of one 150-KB workgroup per CU, which
+  // waits for whole CUs to drain (in-process A/B: 3.35 vs 3.40 ms per step)
+  const bool shared = (flags & SA_XT_COUNT_SHARED) != 0;
+#define SA_COUNT_LAUNCH(MODE, GRID, BLOCK, LDS, CHUNK)                                                   \
+  do {                                                                                                  \
+    if (cl)                                                                                             \
+      hipLaunchKernelGGL((xt_count_kernel<MODE, true>), GRID, BLOCK, LDS, st, A, cells, n, l, w, us, ug,  \
+                         um, trans, err_flags, (int64_t)(CHUNK), nullptr);                              \
+    else                                                                                                \
+      hipLaunchKernelGGL((xt_count_kernel<MODE, false>), GRID, BLOCK, LDS, st, A, nullptr, n, l, w, us,   \
+                         ug, um, trans, err_flags, (int64_t)(CHUNK), codes);                            \
+  } while (0)
+  if (SA_XT_WIDE && wide_lds <= 150 * 1024 && !shared) {
+    // one workgroup per CU (or fewer when there are few actions: >= 4096 actions each)
+    static int cus = 0;
+    if (!cus) {
+      int dev = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+        cus = 256;
+    }
+    int64_t blocks = (n + 4095) / 4096;
+    if (blocks > cus) blocks = cus;
+    const int64_t chunk = (n + blocks - 1) / blocks;
+    SA_COUNT_LAUNCH(XC_WIDE, dim3((unsigned)blocks), dim3(XT_WIDE_THREADS), wide_lds, chunk);
+  } else if (small_lds <= 80 * 1024) {
+    SA_COUNT_LAUNCH(XC_SMALL, dim3(wg_blocks), dim3(XT_THREADS), small_lds, XT_SMALL_ACTS);
+  } else if (vec_lds <= 120 * 1024) {
+    SA_COUNT_LAUNCH(XC_VEC, dim3(wg_blocks), dim3(XT_THREADS), vec_lds, XT_SMALL_ACTS);
+  } else {
+    int64_t blocks = (n + XT_THREADS - 1) / XT_THREADS;
+    if (blocks > 4096) blocks = 4096;
+    SA_COUNT_LAUNCH(XC_GLOBAL, dim3((unsigned)blocks), dim3(XT_THREADS), 0, 0);
+  }
+#undef SA_COUNT_LAUNCH
+  return check_launch("xt_count_kernel");
 }
 
 extern "C" int sa_xt_count_codes(const sa_actions* a, int32_t l, int32_t w, int64_t* shot,
@@ -669,46 +808,37 @@ extern "C" int sa_xt_count_codes(const sa_actions* a, int32_t l, int32_t w, int6
   if (codes && !aligned16(codes)) return fail(SA_EINVAL, "codes must be 16-byte aligned");
   if (codes && (int64_t)l * w > 65535) return fail(SA_EINVAL, "rate codes need l * w <= 65535");
   if (a->n == 0) return SA_OK;
-  const int C = l * w;
-  const size_t small_lds = (size_t)(3 * C + (C * C + 1) / 2) * 4;
-  hipStream_t st = (hipStream_t)stream;
-  auto* us = reinterpret_cast<unsigned long long*>(shot);
-  auto* ug = reinterpret_cast<unsigned long long*>(goal);
-  auto* um = reinterpret_cast<unsigned long long*>(move);
-  const size_t vec_lds = (size_t)3 * C * 4;
-  const unsigned wg_blocks = (unsigned)((a->n + XT_SMALL_ACTS - 1) / XT_SMALL_ACTS);
-  const size_t wide_lds = (size_t)(3 * C + C * C) * 4;
-  // SA_XT_COUNT_SHARED: the pass runs next to other kernels (bench.py's side stream), so use the
-  // 80-KB-LDS workgroups that co-reside with them instead of one 150-KB workgroup per CU, which
-  // waits for whole CUs to drain (in-process A/B: 3.35 vs 3.40 ms per step)
-  const bool shared = (flags & SA_XT_COUNT_SHARED) != 0;
-  if (SA_XT_WIDE && wide_lds <= 150 * 1024 && !shared) {
-    // one workgroup per CU (or fewer when there are few actions: >= 4096 actions each)
-    static int cus = 0;
-    if (!cus) {
-      int dev = 0;
-      if (hipGetDevice(&dev) != hipSuccess ||
-          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
-        cus = 256;
-    }
-    int64_t blocks = (a->n + 4095) / 4096;
-    if (blocks > cus) blocks = cus;
-    const int64_t chunk = (a->n + blocks - 1) / blocks;
-    hipLaunchKernelGGL((xt_count_kernel<XC_WIDE>), dim3((unsigned)blocks), dim3(XT_WIDE_THREADS), wide_lds, st,
-                       *a, l, w, us, ug, um, trans, err_flags, chunk, codes);
-  } else if (small_lds <= 80 * 1024) {
-    hipLaunchKernelGGL((xt_count_kernel<XC_SMALL>), dim3(wg_blocks), dim3(XT_THREADS), small_lds, st, *a,
-                       l, w, us, ug, um, trans, err_flags, (int64_t)XT_SMALL_ACTS, codes);
-  } else if (vec_lds <= 120 * 1024) {
-    hipLaunchKernelGGL((xt_count_kernel<XC_VEC>), dim3(wg_blocks), dim3(XT_THREADS), vec_lds, st, *a, l,
-                       w, us, ug, um, trans, err_flags, (int64_t)XT_SMALL_ACTS, codes);
-  } else {
-    int64_t blocks = (a->n + XT_THREADS - 1) / XT_THREADS;
-    if (blocks > 4096) blocks = 4096;
-    hipLaunchKernelGGL((xt_count_kernel<XC_GLOBAL>), dim3((unsigned)blocks), dim3(XT_THREADS), 0, st, *a,
-                       l, w, us, ug, um, trans, err_flags, (int64_t)0, codes);
-  }
-  return check_launch("xt_count_kernel");
+  return launch_count(*a, nullptr, a->n, l, w, shot, goal, move, trans, err_flags, codes, flags,
+                      (hipStream_t)stream);
+}
+
+extern "C" int sa_xt_cells(const sa_actions* a, int32_t l, int32_t w, uint32_t* cells, void* stream) {
+  if (!a || a->n < 0 || a->atomic) return fail(SA_EINVAL, "bad sa_actions (SPADL actions required)");
+  if (l < 1 || w < 1 || (int64_t)l * w > SA_XT_CELLS_MAX_C)
+    return fail(SA_EINVAL, "cell codes need 1 <= l * w <= %d", SA_XT_CELLS_MAX_C);
+  if (a->n == 0) return SA_OK;
+  const sa_frame& F = a->frames[0];
+  if (!F.type_id || !F.result_id || !F.c0 || !F.c1 || !F.c2 || !F.c3 || !cells)
+    return fail(SA_EINVAL, "null input column or output");
+  if (!aligned16(cells)) return fail(SA_EINVAL, "cells must be 16-byte aligned");
+  const int64_t threads = (a->n + 3) / 4;
+  hipLaunchKernelGGL(xt_cells_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, *a, l, w, cells);
+  return check_launch("xt_cells_kernel");
+}
+
+extern "C" int sa_xt_count_cells(const uint32_t* cells, int64_t n, int32_t l, int32_t w, int64_t* shot,
+                                 int64_t* goal, int64_t* move, int32_t* trans, int32_t* err_flags,
+                                 int32_t flags, void* stream) {
+  if (n < 0 || l < 1 || w < 1 || (int64_t)l * w > SA_XT_CELLS_MAX_C)
+    return fail(SA_EINVAL, "cell codes need n >= 0 and 1 <= l * w <= %d", SA_XT_CELLS_MAX_C);
+  if (!shot || !goal || !move || !trans || !err_flags || (n > 0 && !cells))
+    return fail(SA_EINVAL, "null pointer");
+  if (n == 0) return SA_OK;
+  sa_actions none;
+  memset(&none, 0, sizeof(none));
+  return launch_count(none, cells, n, l, w, shot, goal, move, trans, err_flags, nullptr, flags,
+                      (hipStream_t)stream);
 }
 
 extern "C" int sa_xt_solve(const int64_t* shot, const int64_t* goal, const int64_t* move,
@@ -867,4 +997,17 @@ extern "C" int sa_xt_rate_codes(const uint32_t* codes, int64_t n, const double* 
   hipLaunchKernelGGL(xt_rate_codes_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
                      (hipStream_t)stream, codes, n, grid, out, err_flags);
   return check_launch("xt_rate_codes_kernel");
+}
+
+extern "C" int sa_xt_rate_cells(const uint32_t* cells, int64_t n, int32_t l, int32_t w, const double* grid,
+                                double* out, int32_t* err_flags, void* stream) {
+  if (n < 0 || l < 1 || w < 1 || (int64_t)l * w > SA_XT_CELLS_MAX_C)
+    return fail(SA_EINVAL, "cell codes need n >= 0 and 1 <= l * w <= %d", SA_XT_CELLS_MAX_C);
+  if (n > 0 && (!cells || !grid || !out)) return fail(SA_EINVAL, "null pointer");
+  if (n == 0) return SA_OK;
+  if (!aligned16(cells) || !aligned16(out)) return fail(SA_EINVAL, "cells and out must be 16-byte aligned");
+  const int64_t threads = (n + 3) / 4;
+  hipLaunchKernelGGL(xt_rate_cells_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, cells, n, l * w, grid, out, err_flags);
+  return check_launch("xt_rate_cells_kernel");
 }

@@ -104,11 +104,22 @@ def _ptr(t: Optional[torch.Tensor]):
     return t.data_ptr() if (t is not None and t.numel()) else None
 
 
-def features_into(s: _native.SaActions, out: FeatureBlocks) -> None:
+def features_into(s: _native.SaActions, out: FeatureBlocks, xt_cells: Optional[tuple] = None) -> None:
+    """Launch the feature kernels into ``out``. ``xt_cells = (l, w, cells)``: the same pass also
+    writes every action's xT cell code for a fit + rate on the (l, w) grid
+    (``sa_vaep_features_xt``; ``cells`` from :func:`xt_cells_buffer`)."""
     bb, fb, ib = out.sa_blocks()
-    _native.check(_native.lib().sa_vaep_features(ctypes.byref(s), ctypes.byref(out.plan.struct),
-                                                 ctypes.byref(bb), ctypes.byref(fb),
-                                                 ctypes.byref(ib), stream_handle()))
+    if xt_cells is None:
+        _native.check(_native.lib().sa_vaep_features(
+            ctypes.byref(s), ctypes.byref(out.plan.struct), ctypes.byref(bb), ctypes.byref(fb),
+            ctypes.byref(ib), stream_handle()))
+    else:
+        l, w, cells = xt_cells
+        if cells.dtype != torch.int32 or cells.numel() < s.n:
+            raise ValueError('cells must be an int32 tensor of at least n elements')
+        _native.check(_native.lib().sa_vaep_features_xt(
+            ctypes.byref(s), ctypes.byref(out.plan.struct), ctypes.byref(bb), ctypes.byref(fb),
+            ctypes.byref(ib), int(l), int(w), _ptr(cells), stream_handle()))
 
 
 def features(batch: ActionBatch, xfns: Sequence[str], k: int, flip: bool = True,
@@ -240,6 +251,43 @@ def xt_rate_codes(codes: torch.Tensor, n: int, grid: torch.Tensor,
 
 XT_ERR_SHOT, XT_ERR_MOVE_START, XT_ERR_MOVE_OTHER = 1, 2, 8
 XT_ERR_FIT = XT_ERR_SHOT | XT_ERR_MOVE_START | XT_ERR_MOVE_OTHER
+
+
+def xt_cells_buffer(n: int, dev) -> torch.Tensor:
+    """u32 xT cell codes (stored as int32) for n actions."""
+    return torch.empty(max(_ld(n), 16), dtype=torch.int32, device=dev)
+
+
+def xt_cells(batch: ActionBatch, l: int, w: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """The xT cell code of every action (``sa_xt_cells``: the count pass's binning alone)."""
+    out = xt_cells_buffer(batch.n, batch.device) if out is None else out
+    s = batch.struct()
+    _native.check(_native.lib().sa_xt_cells(ctypes.byref(s), int(l), int(w), _ptr(out),
+                                            stream_handle()))
+    return out
+
+
+def xt_count_cells(cells: torch.Tensor, n: int, l: int, w: int, acc: Optional[XTCounts] = None,
+                   shared: bool = False) -> XTCounts:
+    """The count pass of ExpectedThreat.fit from cell codes (4 B per action read)."""
+    acc = acc or xt_zero_counts(l, w, cells.device)
+    _native.check(_native.lib().sa_xt_count_cells(_ptr(cells), int(n), int(l), int(w),
+                                                  _ptr(acc.shot), _ptr(acc.goal), _ptr(acc.move),
+                                                  _ptr(acc.trans), _ptr(acc.err), int(shared),
+                                                  stream_handle()))
+    return acc
+
+
+def xt_rate_cells(cells: torch.Tensor, n: int, l: int, w: int, grid: torch.Tensor,
+                  out: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """ExpectedThreat.rate (no interpolation, grid = the (w, l) surface) from cell codes."""
+    dev = cells.device
+    out = torch.empty(max(_ld(n), 16), dtype=torch.float64, device=dev) if out is None else out
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    _native.check(_native.lib().sa_xt_rate_cells(_ptr(cells), int(n), int(l), int(w),
+                                                 _ptr(grid.contiguous()), _ptr(out), _ptr(err),
+                                                 stream_handle()))
+    return out[:n], err
 
 
 def xt_check_errors(acc: XTCounts, mask: int = XT_ERR_FIT) -> None:

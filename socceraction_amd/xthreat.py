@@ -140,6 +140,9 @@ def _gpu_interp2d(x, y, z, kind='linear', bounds_error=False):
         raise ValueError('x and y must have the lengths of the xT surface')
     if l < 2 or w < 2:
         raise ValueError('linear interpolation needs at least 2 nodes per axis')
+    if (np.diff(x) <= 0).any() or (np.diff(y) <= 0).any() or \
+            not (np.isfinite(x).all() and np.isfinite(y).all()):
+        raise ValueError('x and y must be finite and strictly increasing')
     zt = torch.from_numpy(np.ascontiguousarray(z))
 
     def f(xs, ys):

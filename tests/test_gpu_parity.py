@@ -386,3 +386,45 @@ def test_full_size_sampled_games_vs_oracle(sa):
         fo = vo.formula(cols, p['scores'][s:e], p['concedes'][s:e])
         for r, c in enumerate(('offensive_value', 'defensive_value', 'vaep_value')):
             assert_close(val[r, s:e].cpu().numpy(), fo[c], c)
+
+
+@pytest.mark.parametrize('l,w,games', [(16, 12, 300), (30, 20, 60), (64, 64, 40), (1, 1, 5)])
+def test_xt_cell_codes_match_coordinate_path(sa, l, w, games):
+    """The xT cell codes -- written by the VAEP feature pass (sa_vaep_features_xt, both the k <= 3
+    register-window path and the generic path) or alone (sa_xt_cells) -- give the coordinate
+    path's counts, error bits, rate values and NaN pattern bit for bit, incl. NaN / inf
+    coordinates on successful moves, failed moves and shots, and an odd-length tail."""
+    B, ops, syn = sa['batch'], sa['ops'], sa['synthetic']
+    d = syn.spadl_games(games, game_id0=9)
+    n = len(d['type_id'])
+    d = {k: (v[:n - 3].copy() if isinstance(v, np.ndarray) and v.shape == (n,) else v)
+         for k, v in d.items()}
+    d['game_off'] = np.minimum(d['game_off'], n - 3)
+    rng = np.random.default_rng(2)
+    for col, val in (('start_x', np.nan), ('end_y', np.inf), ('start_y', -np.inf),
+                     ('end_x', np.nan)):
+        d[col][rng.choice(n - 3, 9, replace=False)] = val
+    ab = B.ActionBatch.from_columns(d)
+    cells = ops.xt_cells(ab, l, w)
+    for k in (3, 5):
+        fb = ops.alloc_feature_blocks(sa['catalog'].build_plan(vo.SPADL_DEFAULT, k), ab.n,
+                                      ab.device, 1024, 128)
+        c2 = ops.xt_cells_buffer(ab.n, ab.device)
+        ops.features_into(ab.struct(), fb, xt_cells=(l, w, c2))
+        assert torch.equal(c2[:ab.n], cells[:ab.n]), k
+    ref = ops.xt_count(ab, l, w)
+    for shared in (False, True):
+        acc = ops.xt_count_cells(cells, ab.n, l, w, shared=shared)
+        for a, b in ((acc.shot, ref.shot), (acc.goal, ref.goal), (acc.move, ref.move),
+                     (acc.trans, ref.trans), (acc.err, ref.err)):
+            assert torch.equal(a, b), shared
+    assert int(ref.err.item()) != 0
+    grid = torch.rand((w, l), dtype=torch.float64, device=ab.device)
+    r_ref, e_ref = ops.xt_rate(ab, grid, l, w)
+    r, e = ops.xt_rate_cells(cells, ab.n, l, w, grid)
+    rr, gg = r_ref.cpu().numpy(), r.cpu().numpy()
+    np.testing.assert_array_equal(np.isnan(gg), np.isnan(rr))
+    np.testing.assert_array_equal(gg[~np.isnan(rr)], rr[~np.isnan(rr)])
+    assert int(e.item()) == int(e_ref.item()) == 4
+    with pytest.raises(ValueError):
+        ops.xt_cells(ab, 105, 68)  # 7140 cells do not fit the 12-bit fields
