@@ -1,0 +1,56 @@
+"""Standalone timing of the xT 16 x 12 fit pieces on cfg4's actions (10k synthetic games):
+count pass (coordinates and cell codes), value iteration (sa_xt_solve) and rate, each on an
+otherwise idle GPU, HIP events on the current stream.  Prints one JSON line.
+
+    python scripts/xt_solve_time.py [--games 10000] [--reps 10]
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from socceraction_amd import batch as B  # noqa: E402
+from socceraction_amd import ops, synthetic  # noqa: E402
+
+
+def _ms(fn, reps):
+    fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return round(a.elapsed_time(b) / reps, 4)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--games', type=int, default=10000)
+    ap.add_argument('--reps', type=int, default=10)
+    args = ap.parse_args()
+    ab = B.ActionBatch.from_columns(synthetic.spadl_games(args.games))
+    cells = ops.xt_cells(ab, 16, 12)
+    acc = ops.xt_count(ab, 16, 12)
+    out = {'n': ab.n}
+    out['count_coords_ms'] = _ms(lambda: ops.xt_count(ab, 16, 12), args.reps)
+    out['count_cells_ms'] = _ms(lambda: ops.xt_count_cells(cells, ab.n, 16, 12), args.reps)
+    out['count_cells_shared_ms'] = _ms(lambda: ops.xt_count_cells(cells, ab.n, 16, 12, shared=True),
+                                       args.reps)
+    out['cells_ms'] = _ms(lambda: ops.xt_cells(ab, 16, 12, out=cells), args.reps)
+    sol = ops.xt_solve(acc)
+    out['iterations'] = sol.n_iter
+    out['solve_ms_incl_host_sync'] = _ms(lambda: ops.xt_solve(acc), args.reps)
+    grid = sol.mats[3]
+    out['rate_cells_ms'] = _ms(lambda: ops.xt_rate_cells(cells, ab.n, 16, 12, grid), args.reps)
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == '__main__':
+    main()

@@ -203,7 +203,6 @@ constexpr int CG_WAVES = 4;  // waves per workgroup
 template <bool ATOMIC, bool EXPLICIT>
 __global__ __launch_bounds__(64 * CG_WAVES) void bool_colgroup_kernel(FeatArgs args, int ngroups,
                                                                       int gcols) {
-  __shared__ int32_t team_lds[CG_WAVES][BOOL_TILE + 8];
   const int lane = threadIdx.x & (WAVE - 1);
   const int wv = threadIdx.x / WAVE;
   const sa_actions& A = args.a;
@@ -220,11 +219,6 @@ __global__ __launch_bounds__(64 * CG_WAVES) void bool_colgroup_kernel(FeatArgs a
   const int tcol = P.bool_col[SA_XFN_TEAM];
   // team_1 .. team_{K-1} columns inside [c_lo, c_hi)?
   const bool need_team = tcol >= 0 && K > 1 && tcol < c_hi && tcol + K - 1 > c_lo;
-  if (!EXPLICIT && need_team && tile0 < n) {  // team codes of rows tile0-8 .. tile0+1023
-    int32_t* tl = team_lds[wv];
-    for (int k = lane; k < BOOL_TILE + 8; k += WAVE) tl[k] = ld_or0(F0.team, tile0 - 8 + k, n);
-  }
-  __syncthreads();
   if (tile0 >= n || c_lo >= c_hi) return;
   uint8_t* bb = args.bout + tile_off(j0 < n ? j0 : tile0, 0, args.Cb, R);
   if (j0 >= n) return;
@@ -357,9 +351,10 @@ __global__ __launch_bounds__(64 * CG_WAVES) void bool_colgroup_kernel(FeatArgs a
           const int d = (int)byte_of(dw[mm >> 2], mm & 3);
           const int s = d < i ? d : i;
           SA_DCHECK(s >= 0 && s <= 8, s);
-          const int32_t* tl = team_lds[wv] + 8 + lane * LANE_ACTS + mm;
-          t0 = tl[0];
-          ti = tl[-s];
+          // team codes straight from L1/L2 (a few waves per tile need them): the kernel keeps
+          // no LDS, so xT workgroups with large LDS footprints co-reside with it
+          t0 = ld_or0(F0.team, j0 + mm, n);
+          ti = ld_or0(F0.team, j0 + mm - s, n);
         }
         m[mm >> 2] |= (uint32_t)(t0 == ti) << (8 * (mm & 3));
       }

@@ -321,85 +321,130 @@ __device__ __forceinline__ double row_payoff(const double* __restrict__ Tt, cons
 // Small grids: one persistent workgroup runs every iteration; x lives in LDS.
 constexpr int XT_SOLVE_MAX_C = 1024;
 constexpr size_t XT_LDS_BUDGET = 160 * 1024;  // gfx950 LDS per workgroup
+constexpr int XS_THREADS = 1024;               // 16 waves: every wave forms products
 
-// LDS bytes of xt_solve_lds_kernel: the C x C int32 counts + x.
-static inline size_t xt_solve_lds_bytes(int C) {
-  return ((size_t)C * C * 4 + 15) / 16 * 16 + (size_t)C * 8;
+// LDS layout of xt_solve_lds_kernel for C cells and chunks of CH columns: u16 counts
+// (transposed), x, the row move counts, two product buffers of CH x C.
+__host__ __device__ inline size_t xs_counts_bytes(int C) { return ((size_t)C * C * 2 + 15) / 16 * 16; }
+static inline size_t xt_solve_lds_bytes(int C, int CH) {
+  return xs_counts_bytes(C) + (size_t)C * 16 + (size_t)2 * CH * C * 8;
+}
+// Widest chunk that fits the budget (0: the system does not fit this kernel).
+static inline int xt_solve_lds_chunk(int C) {
+  const size_t fixed = xs_counts_bytes(C) + (size_t)C * 16;
+  if (fixed >= XT_LDS_BUDGET) return 0;
+  int ch = (int)((XT_LDS_BUDGET - fixed) / ((size_t)16 * C));
+  if (ch > C) ch = C;
+  if (ch > 32) ch = 32;
+  return ch >= 4 ? ch : 0;
 }
 
-// Grids whose C x C int32 counts fit LDS with x (C <= 199, e.g. 16 x 12): one persistent
-// workgroup keeps the counts -- transposed, so the lanes of a wave read consecutive words -- and
-// x in LDS for every iteration, so nothing is re-read from L2/HBM per iteration (the Tt form
-// streams the 295 KB f64 matrix from L2 every iteration and slows down badly when it shares
-// the chip with the streaming VAEP kernels).  T[r, c] * x[c] is formed exactly as the
-// reference rounds it: one correctly rounded division cnt / move[r], one multiply, added to
-// the row's sum strictly left to right (cnt == 0 contributes T = 0, i.e. +0).
-__global__ __launch_bounds__(256) void xt_solve_lds_kernel(const int32_t* __restrict__ trans,
-                                                           const unsigned long long* __restrict__ move,
-                                                           const double* __restrict__ gs,
-                                                           const double* __restrict__ pmove, int C,
-                                                           double eps, int max_iter,
-                                                           double* __restrict__ heat,
-                                                           double* __restrict__ xT_out,
-                                                           int32_t* __restrict__ n_iter) {
+// Value iteration of grids whose C x C counts fit LDS as u16 (C <= ~200, e.g. 16 x 12): one
+// persistent workgroup keeps the counts (transposed: consecutive rows are consecutive words),
+// x and the rows' move counts in LDS for every iteration, so nothing is re-read from L2/HBM per
+// iteration (the Tt form streams the 295 KB f64 matrix from L2 every iteration and slows down
+// badly when it shares the chip with the streaming VAEP kernels).  Per iteration the columns
+// go by in chunks of CH: all 16 waves form the chunk's products T[r, c] * x[c] -- one correctly
+// rounded division cnt / move[r] and one multiply per element, exactly as the reference rounds
+// them (cnt == 0: T = 0, product +0) -- into a double-buffered LDS slab while the C row lanes
+// add the previous chunk's products to their sums strictly left to right (xthreat.py:306-312).
+// A count >= 65536 does not fit u16: the producers then read the exact T values of trans_t
+// (the same f64 quotients, formed once by xt_transpose_kernel) instead.
+__global__ __launch_bounds__(XS_THREADS) void xt_solve_lds_kernel(const int32_t* __restrict__ trans,
+                                                                  const double* __restrict__ Tt,
+                                                                  const unsigned long long* __restrict__ move,
+                                                                  const double* __restrict__ gs,
+                                                                  const double* __restrict__ pmove, int C,
+                                                                  int CH, double eps, int max_iter,
+                                                                  double* __restrict__ heat,
+                                                                  double* __restrict__ xT_out,
+                                                                  int32_t* __restrict__ n_iter) {
   extern __shared__ __align__(16) uint8_t xt_lds[];
-  int32_t* cnt = reinterpret_cast<int32_t*>(xt_lds);  // cnt[c * C + r] = trans[r * C + c]
-  double* xs = reinterpret_cast<double*>(xt_lds + ((size_t)C * C * 4 + 15) / 16 * 16);
-  for (int k = threadIdx.x; k < C * C; k += blockDim.x) {
+  uint16_t* cnt = reinterpret_cast<uint16_t*>(xt_lds);  // cnt[c * C + r] = trans[r * C + c]
+  double* xs = reinterpret_cast<double*>(xt_lds + xs_counts_bytes(C));
+  double* mv = xs + C;
+  double* buf = mv + C;  // [2][CH * C]
+  __shared__ int wide;   // some count >= 65536: read T from Tt
+  const int tid = threadIdx.x;
+  if (tid == 0) wide = 0;
+  __syncthreads();
+  int big = 0;
+  for (int k = tid; k < C * C; k += blockDim.x) {
+    const int32_t v = trans[k];
+    big |= (uint32_t)v > 0xFFFFu;
     const int rr = k / C, c = k - rr * C;
-    SA_DCHECK(c * C + rr < C * C, k);
-    cnt[c * C + rr] = trans[k];
+    cnt[c * C + rr] = (uint16_t)v;
   }
-  const int r = threadIdx.x;
-  const bool act = r < C;
-  double m = 1.0, g = 0.0, pm = 0.0;
-  if (act) {
+  if (big) wide = 1;  // benign race: every writer stores 1
+  for (int r = tid; r < C; r += blockDim.x) {
     xs[r] = 0.0;
     heat[r] = 0.0;
-    m = (double)move[r];
+    mv[r] = (double)move[r];
+  }
+  __syncthreads();
+  const bool use_tt = wide != 0;
+  const int r = tid;
+  const bool chain = r < C;
+  double g = 0.0, pm = 0.0;
+  if (chain) {
     g = gs[r];
     pm = pmove[r];
   }
-  __syncthreads();
+  const int nch = (C + CH - 1) / CH;
+  // products of columns [c0, c0 + CH) into buffer b
+  auto produce = [&](int c0, double* b) {
+    const int cols = C - c0 < CH ? C - c0 : CH;
+    for (int q = tid; q < cols * C; q += blockDim.x) {
+      const int cc = q / C, rr = q - cc * C;
+      const int c = c0 + cc;
+      double t;
+      if (use_tt) {
+        t = Tt[(int64_t)c * C + rr];
+      } else {
+        const uint32_t v = cnt[c * C + rr];
+        t = v != 0 ? (double)v / mv[rr] : 0.0;
+      }
+      b[q] = t * xs[c];
+    }
+  };
   int it = 0;
   bool cont = true;
   while (cont && it < max_iter) {
+    double acc = 0.0;
+    produce(0, buf);
+    __syncthreads();
+    for (int k = 0; k < nch; ++k) {
+      if (k + 1 < nch) produce((k + 1) * CH, buf + ((k + 1) & 1) * CH * C);
+      if (chain) {
+        const double* b = buf + (k & 1) * CH * C + r;
+        const int cols = C - k * CH < CH ? C - k * CH : CH;
+        int cc = 0;
+        for (; cc + 4 <= cols; cc += 4) {
+          const double p0 = b[cc * C], p1 = b[(cc + 1) * C], p2 = b[(cc + 2) * C], p3 = b[(cc + 3) * C];
+          acc = acc + p0;
+          acc = acc + p1;
+          acc = acc + p2;
+          acc = acc + p3;
+        }
+        for (; cc < cols; ++cc) acc = acc + b[cc * C];
+      }
+      __syncthreads();
+    }
     double nx = 0.0;
     int flag = 0;
-    if (act) {
-      double acc = 0.0;
-      int c = 0;
-      for (; c + 8 <= C; c += 8) {
-        int32_t v[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = cnt[(c + u) * C + r];
-        double p[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const double t = v[u] != 0 ? (double)v[u] / m : 0.0;
-          p[u] = t * xs[c + u];
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) acc = acc + p[u];
-      }
-      for (; c < C; ++c) {
-        const int32_t v = cnt[c * C + r];
-        const double t = v != 0 ? (double)v / m : 0.0;
-        const double p = t * xs[c];
-        acc = acc + p;
-      }
-      const double mv = pm * acc;
-      nx = g + mv;
+    if (chain) {
+      const double mvv = pm * acc;
+      nx = g + mvv;
       const double diff = nx - xs[r];
       flag = diff > eps;  // np.any(diff > eps): NaN compares False
       heat[(int64_t)(it + 1) * C + r] = nx;
     }
     cont = __syncthreads_or(flag);
-    if (act) xs[r] = nx;
+    if (chain) xs[r] = nx;
     __syncthreads();
     ++it;
   }
-  if (act) xT_out[r] = xs[r];
+  if (chain) xT_out[r] = xs[r];
   if (r == 0) *n_iter = cont ? -1 : it;
 }
 
@@ -867,10 +912,10 @@ extern "C" int sa_xt_solve(const int64_t* shot, const int64_t* goal, const int64
   hipLaunchKernelGGL(xt_transpose_kernel, tgrid, dim3(256), 0, st, trans, um, C, trans_t);
   rc = check_launch("xt normalise");
   if (!rc && C <= XT_SOLVE_MAX_C) {
-    const size_t lds = xt_solve_lds_bytes(C);
-    if (lds <= XT_LDS_BUDGET) {
-      hipLaunchKernelGGL(xt_solve_lds_kernel, dim3(1), dim3(((C + 63) / 64) * 64), lds, st, trans, um,
-                         gs, pm, C, eps, max_iter, heatmaps, mats + 3 * C, dn);
+    const int CH = C <= XS_THREADS ? xt_solve_lds_chunk(C) : 0;
+    if (CH > 0) {
+      hipLaunchKernelGGL(xt_solve_lds_kernel, dim3(1), dim3(XS_THREADS), xt_solve_lds_bytes(C, CH), st,
+                         trans, trans_t, um, gs, pm, C, CH, eps, max_iter, heatmaps, mats + 3 * C, dn);
       rc = check_launch("xt_solve_lds_kernel");
     } else {
       hipLaunchKernelGGL(xt_solve_small_kernel, dim3(1), dim3(((C + 63) / 64) * 64), 0, st, trans_t, gs,
