@@ -164,6 +164,19 @@ int sa_vaep_formula_f64(const sa_actions* a, const double* p_scores, const doubl
 int sa_vaep_formula_f32(const sa_actions* a, const float* p_scores, const float* p_concedes,
                         float* off, float* def, float* val, void* stream);
 
+/* compute_labels + formula.value of the same actions in one launch (the tail of a VAEP
+ * step: the ids and team codes are read once): exactly sa_vaep_labels then
+ * sa_vaep_formula_f64 / _f32 with the same arguments.  Formula outputs need length
+ * >= round_up(n, 16) here. */
+int sa_vaep_labels_formula_f64(const sa_actions* a, int32_t nr_actions, uint8_t* scores,
+                               uint8_t* concedes, uint8_t* goal_from_shot, int64_t ld,
+                               const double* p_scores, const double* p_concedes, double* off,
+                               double* def, double* val, void* stream);
+int sa_vaep_labels_formula_f32(const sa_actions* a, int32_t nr_actions, uint8_t* scores,
+                               uint8_t* concedes, uint8_t* goal_from_shot, int64_t ld,
+                               const float* p_scores, const float* p_concedes, float* off,
+                               float* def, float* val, void* stream);
+
 /* ---- Expected Threat (xthreat.py) --------------------------------------------
  * Count pass over SPADL actions (frames[0] of `a`; segments ignored):
  * shot[c] += shots (type 11) by start cell, goal[c] += successful shots,

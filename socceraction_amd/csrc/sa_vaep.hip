@@ -831,13 +831,12 @@ __global__ __launch_bounds__(256) void goalscore_wave16_kernel(sa_actions A,
 // nr_actions <= 17 needs no further loads.  The look-ahead clamps at the segment's last row,
 // which only repeats a row already in the window, so the window is rows j+1 .. min(j+nr-1,
 // last).
+// Rows j0 .. j0+15 of one lane (j0 < n); `cur` = a segment cursor at or before row j0.
 template <bool ATOMIC>
-__global__ __launch_bounds__(256) void labels_kernel(sa_actions A, int nr, uint8_t* __restrict__ sc,
-                                                     uint8_t* __restrict__ co,
-                                                     uint8_t* __restrict__ gfs) {
+__device__ __forceinline__ void labels_rows(const sa_actions& A, int nr, uint8_t* __restrict__ sc,
+                                            uint8_t* __restrict__ co, uint8_t* __restrict__ gfs,
+                                            int64_t j0, SegCursor cur) {
   const int64_t n = A.n;
-  const int64_t j0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * LANE_ACTS;
-  if (j0 >= n) return;
   const sa_frame& F = A.frames[0];
   uint32_t gm = 0, om = 0, shm = 0;  // goal / owngoal / shot(type 11) row bits
 #pragma unroll
@@ -876,13 +875,6 @@ __global__ __launch_bounds__(256) void labels_kernel(sa_actions A, int nr, uint8
   uint32_t e1 = 0;
 #pragma unroll
   for (int r = 0; r < 32; ++r) e1 |= (uint32_t)(tm[r] == t1) << r;
-  SegCursor cur;
-  {
-    // one search per wave (the first active lane's row, uniform: scalar loads), then each lane
-    // advances to its own rows -- a per-lane binary search was ~14 dependent divergent loads
-    const int64_t jw = (int64_t)__builtin_amdgcn_readfirstlane((int)(j0 / LANE_ACTS)) * LANE_ACTS;
-    cur = seg_at(A, jw);
-  }
   uint32_t s_out[4] = {0, 0, 0, 0}, c_out[4] = {0, 0, 0, 0}, g_out[4] = {0, 0, 0, 0};
 #pragma unroll
   for (int m = 0; m < LANE_ACTS; ++m) {
@@ -947,20 +939,39 @@ __global__ __launch_bounds__(256) void labels_kernel(sa_actions A, int nr, uint8
   if (gfs) st16(gfs + j0, u32x4{g_out[0], g_out[1], g_out[2], g_out[3]});
 }
 
+// Wave-uniform segment cursor of row jw: one search per wave (scalar loads); lanes then advance
+// from it to their own rows -- a per-lane binary search was ~14 dependent divergent loads.
+__device__ __forceinline__ SegCursor wave_cursor(const sa_actions& A, int64_t jw) {
+  const int lo = __builtin_amdgcn_readfirstlane((int)(jw & 0xFFFFFFFF));
+  const int hi = __builtin_amdgcn_readfirstlane((int)(jw >> 32));
+  return seg_at(A, ((int64_t)hi << 32) | (uint32_t)lo);
+}
+
+template <bool ATOMIC>
+__global__ __launch_bounds__(256) void labels_kernel(sa_actions A, int nr, uint8_t* __restrict__ sc,
+                                                     uint8_t* __restrict__ co,
+                                                     uint8_t* __restrict__ gfs) {
+  const int64_t j0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * LANE_ACTS;
+  if (j0 >= A.n) return;
+  labels_rows<ATOMIC>(A, nr, sc, co, gfs, j0, wave_cursor(A, j0));  // first active lane's row
+}
+
 // ------------------------------------------------------------------------------ formula
 // vaep/formula.py:8-151, atomic/vaep/formula.py:8-141.  Arithmetic stays in the probability
 // dtype and mirrors the pandas expression tree operation by operation.  A lane owns V
 // consecutive actions (16-B stores); the previous row's values come from the same lane or,
 // for the lane's first action, from the neighbouring lane by a wave shuffle.
+// Rows j0 .. j0+V-1 of one lane (V = 16 / sizeof(T)); every lane of the wave calls it with
+// consecutive j0 (the previous row comes from the neighbouring lane); `cur` = a segment cursor
+// at or before row j0, advanced by the call.
 template <bool ATOMIC, typename T>
-__global__ __launch_bounds__(256) void formula_kernel(sa_actions A, const T* __restrict__ ps,
-                                                      const T* __restrict__ pc, T* __restrict__ off,
-                                                      T* __restrict__ def, T* __restrict__ val,
-                                                      bool vec_ok) {
+__device__ __forceinline__ void formula_rows(const sa_actions& A, const T* __restrict__ ps,
+                                             const T* __restrict__ pc, T* __restrict__ off,
+                                             T* __restrict__ def, T* __restrict__ val, bool vec_ok,
+                                             int64_t j0, SegCursor& cur) {
   constexpr int V = 16 / sizeof(T);
   const int64_t n = A.n;
   const int lane = threadIdx.x & (WAVE - 1);
-  const int64_t j0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * V;
   const bool active = j0 < n;
   const sa_frame& F = A.frames[0];
   T s_[V], c_[V];
@@ -1026,9 +1037,6 @@ __global__ __launch_bounds__(256) void formula_kernel(sa_actions A, const T* __r
     typ = F.type_id[p];
     rsp = ATOMIC ? 0 : F.result_id[p];
   }
-  SegCursor cur;
-  // one search per wave (uniform, scalar loads), lanes advance from it
-  cur = seg_at(A, (int64_t)__builtin_amdgcn_readfirstlane((int)(j0 / V)) * V);
   vec_t vo, vd, vv;
 #pragma unroll
   for (int q = 0; q < V; ++q) {
@@ -1079,6 +1087,47 @@ __global__ __launch_bounds__(256) void formula_kernel(sa_actions A, const T* __r
   st16(off + j0, vo);
   st16(def + j0, vd);
   st16(val + j0, vv);
+}
+
+template <bool ATOMIC, typename T>
+__global__ __launch_bounds__(256) void formula_kernel(sa_actions A, const T* __restrict__ ps,
+                                                      const T* __restrict__ pc, T* __restrict__ off,
+                                                      T* __restrict__ def, T* __restrict__ val,
+                                                      bool vec_ok) {
+  constexpr int V = 16 / sizeof(T);
+  const int64_t j0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * V;
+  const int64_t jw = ((int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~(WAVE - 1))) * V;
+  if (jw >= A.n) return;  // whole wave past the end (the shuffles need every lane of a live wave)
+  SegCursor cur = wave_cursor(A, jw);
+  formula_rows<ATOMIC, T>(A, ps, pc, off, def, val, vec_ok, j0, cur);
+}
+
+// Labels and formula of the same 1024 rows in one wave (the step's tail: one launch, the ids
+// and team codes read once): the labels part as labels_kernel (a lane owns 16 rows), then the
+// formula part in passes of 64 * V rows as formula_kernel (a lane owns V rows), both lanes'
+// segment cursors advancing from one wave-uniform search.
+template <bool ATOMIC, typename T>
+__global__ __launch_bounds__(256) void labels_formula_kernel(sa_actions A, int nr, uint8_t* __restrict__ sc,
+                                                             uint8_t* __restrict__ co,
+                                                             uint8_t* __restrict__ gfs,
+                                                             const T* __restrict__ ps,
+                                                             const T* __restrict__ pc, T* __restrict__ off,
+                                                             T* __restrict__ def, T* __restrict__ val,
+                                                             bool vec_ok) {
+  constexpr int V = 16 / sizeof(T);
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int64_t jw = ((int64_t)blockIdx.x * (blockDim.x / WAVE) + threadIdx.x / WAVE) * (WAVE * LANE_ACTS);
+  if (jw >= A.n) return;
+  const SegCursor wc = wave_cursor(A, jw);
+  const int64_t jl = jw + (int64_t)lane * LANE_ACTS;
+  if (jl < A.n) labels_rows<ATOMIC>(A, nr, sc, co, gfs, jl, wc);
+  SegCursor fc = wc;
+#pragma unroll 1
+  for (int p = 0; p < LANE_ACTS / V; ++p) {
+    const int64_t base = jw + (int64_t)p * WAVE * V;
+    if (base >= A.n) break;  // uniform
+    formula_rows<ATOMIC, T>(A, ps, pc, off, def, val, vec_ok, base + (int64_t)lane * V, fc);
+  }
 }
 
 }  // namespace sa
@@ -1317,4 +1366,48 @@ extern "C" int sa_vaep_formula_f64(const sa_actions* a, const double* p_scores,
 extern "C" int sa_vaep_formula_f32(const sa_actions* a, const float* p_scores, const float* p_concedes,
                                    float* off, float* def, float* val, void* stream) {
   return launch_formula<float>(a, p_scores, p_concedes, off, def, val, stream);
+}
+
+template <typename T>
+static int launch_labels_formula(const sa_actions* a, int32_t nr_actions, uint8_t* scores,
+                                 uint8_t* concedes, uint8_t* goal_from_shot, int64_t ld, const T* ps,
+                                 const T* pc, T* off, T* def, T* val, void* stream) {
+  int rc = check_actions(a, false);
+  if (rc) return rc;
+  if (nr_actions < 1) return fail(SA_EINVAL, "nr_actions must be >= 1");
+  if (ld % 16 != 0 || ld < ((a->n + 15) / 16) * 16)
+    return fail(SA_EINVAL, "ld must be a multiple of 16 and >= round_up(n, 16)");
+  if (!aligned16(scores) || !aligned16(concedes) || !aligned16(goal_from_shot))
+    return fail(SA_EINVAL, "label outputs must be 16-byte aligned");
+  if (!ps || !pc || !off || !def || !val) return fail(SA_EINVAL, "null probability/output pointer");
+  if (!aligned16(off) || !aligned16(def) || !aligned16(val))
+    return fail(SA_EINVAL, "formula outputs must be 16-byte aligned (length >= round_up(n, 16))");
+  if (a->n == 0) return SA_OK;
+  const int64_t waves = (a->n + WAVE * LANE_ACTS - 1) / (WAVE * LANE_ACTS);
+  const dim3 grid((unsigned)((waves + 3) / 4)), block(256);
+  const bool vec_ok = aligned16(ps) && aligned16(pc);
+  hipStream_t st = (hipStream_t)stream;
+  if (a->atomic)
+    hipLaunchKernelGGL((labels_formula_kernel<true, T>), grid, block, 0, st, *a, nr_actions, scores,
+                       concedes, goal_from_shot, ps, pc, off, def, val, vec_ok);
+  else
+    hipLaunchKernelGGL((labels_formula_kernel<false, T>), grid, block, 0, st, *a, nr_actions, scores,
+                       concedes, goal_from_shot, ps, pc, off, def, val, vec_ok);
+  return check_launch("labels_formula_kernel");
+}
+
+extern "C" int sa_vaep_labels_formula_f64(const sa_actions* a, int32_t nr_actions, uint8_t* scores,
+                                          uint8_t* concedes, uint8_t* goal_from_shot, int64_t ld,
+                                          const double* p_scores, const double* p_concedes, double* off,
+                                          double* def, double* val, void* stream) {
+  return launch_labels_formula<double>(a, nr_actions, scores, concedes, goal_from_shot, ld, p_scores,
+                                       p_concedes, off, def, val, stream);
+}
+
+extern "C" int sa_vaep_labels_formula_f32(const sa_actions* a, int32_t nr_actions, uint8_t* scores,
+                                          uint8_t* concedes, uint8_t* goal_from_shot, int64_t ld,
+                                          const float* p_scores, const float* p_concedes, float* off,
+                                          float* def, float* val, void* stream) {
+  return launch_labels_formula<float>(a, nr_actions, scores, concedes, goal_from_shot, ld, p_scores,
+                                      p_concedes, off, def, val, stream);
 }

@@ -17,6 +17,9 @@
 #include "sa_common.h"
 #include "sa_internal.h"
 
+#ifndef SA_XT_SOLVE_STREAM
+#define SA_XT_SOLVE_STREAM 1  // small grids: xt_solve_stream_kernel (0: xt_solve_small_kernel, A/B)
+#endif
 #ifndef SA_XT_WIDE
 #define SA_XT_WIDE 1  // C <= 197: XC_WIDE count pass (0: the 32k-action XC_SMALL workgroups)
 #endif
@@ -321,68 +324,35 @@ __device__ __forceinline__ double row_payoff(const double* __restrict__ Tt, cons
 // Small grids: one persistent workgroup runs every iteration; x lives in LDS.
 constexpr int XT_SOLVE_MAX_C = 1024;
 constexpr size_t XT_LDS_BUDGET = 160 * 1024;  // gfx950 LDS per workgroup
-constexpr int XS_THREADS = 1024;               // 16 waves: every wave forms products
+constexpr int XS_THREADS = 1024;  // 16 waves stream the matrix; C of the lanes run the row sums
+constexpr int XS_CH = 16;         // columns per chunk
 
-// LDS layout of xt_solve_lds_kernel for C cells and chunks of CH columns: u16 counts
-// (transposed), x, the row move counts, two product buffers of CH x C.
-__host__ __device__ inline size_t xs_counts_bytes(int C) { return ((size_t)C * C * 2 + 15) / 16 * 16; }
-static inline size_t xt_solve_lds_bytes(int C, int CH) {
-  return xs_counts_bytes(C) + (size_t)C * 16 + (size_t)2 * CH * C * 8;
-}
-// Widest chunk that fits the budget (0: the system does not fit this kernel).
-static inline int xt_solve_lds_chunk(int C) {
-  const size_t fixed = xs_counts_bytes(C) + (size_t)C * 16;
-  if (fixed >= XT_LDS_BUDGET) return 0;
-  int ch = (int)((XT_LDS_BUDGET - fixed) / ((size_t)16 * C));
-  if (ch > C) ch = C;
-  if (ch > 32) ch = 32;
-  return ch >= 4 ? ch : 0;
-}
+// LDS bytes of xt_solve_stream_kernel: x + two chunk buffers of XS_CH x C doubles.
+static inline size_t xt_solve_stream_bytes(int C) { return (size_t)C * 8 + (size_t)2 * XS_CH * C * 8; }
 
-// Value iteration of grids whose C x C counts fit LDS as u16 (C <= ~200, e.g. 16 x 12): one
-// persistent workgroup keeps the counts (transposed: consecutive rows are consecutive words),
-// x and the rows' move counts in LDS for every iteration, so nothing is re-read from L2/HBM per
-// iteration (the Tt form streams the 295 KB f64 matrix from L2 every iteration and slows down
-// badly when it shares the chip with the streaming VAEP kernels).  Per iteration the columns
-// go by in chunks of CH: all 16 waves form the chunk's products T[r, c] * x[c] -- one correctly
-// rounded division cnt / move[r] and one multiply per element, exactly as the reference rounds
-// them (cnt == 0: T = 0, product +0) -- into a double-buffered LDS slab while the C row lanes
-// add the previous chunk's products to their sums strictly left to right (xthreat.py:306-312).
-// A count >= 65536 does not fit u16: the producers then read the exact T values of trans_t
-// (the same f64 quotients, formed once by xt_transpose_kernel) instead.
-__global__ __launch_bounds__(XS_THREADS) void xt_solve_lds_kernel(const int32_t* __restrict__ trans,
-                                                                  const double* __restrict__ Tt,
-                                                                  const unsigned long long* __restrict__ move,
-                                                                  const double* __restrict__ gs,
-                                                                  const double* __restrict__ pmove, int C,
-                                                                  int CH, double eps, int max_iter,
-                                                                  double* __restrict__ heat,
-                                                                  double* __restrict__ xT_out,
-                                                                  int32_t* __restrict__ n_iter) {
+// Value iteration of small grids (C <= XT_SOLVE_MAX_C, e.g. 16 x 12) in one persistent
+// workgroup.  The exact transposed transition matrix Tt (trans_t, f64: one correctly rounded
+// division cnt / move[s] per element, formed once by xt_transpose_kernel) is streamed from
+// L2 / MALL every iteration in chunks of XS_CH columns: all 16 waves load a chunk with 16-B
+// loads (contiguous XS_CH * C doubles) into a double-buffered LDS slab while the row lanes
+// add the previous chunk's products T[r, c] * x[c] to their sums strictly left to right
+// (xthreat.py:306-312), so the matrix read is spread over every wave of the CU instead of being
+// issued by the C row lanes alone (xt_solve_small_kernel).
+__global__ __launch_bounds__(XS_THREADS) void xt_solve_stream_kernel(const double* __restrict__ Tt,
+                                                                     const double* __restrict__ gs,
+                                                                     const double* __restrict__ pmove, int C,
+                                                                     double eps, int max_iter,
+                                                                     double* __restrict__ heat,
+                                                                     double* __restrict__ xT_out,
+                                                                     int32_t* __restrict__ n_iter) {
   extern __shared__ __align__(16) uint8_t xt_lds[];
-  uint16_t* cnt = reinterpret_cast<uint16_t*>(xt_lds);  // cnt[c * C + r] = trans[r * C + c]
-  double* xs = reinterpret_cast<double*>(xt_lds + xs_counts_bytes(C));
-  double* mv = xs + C;
-  double* buf = mv + C;  // [2][CH * C]
-  __shared__ int wide;   // some count >= 65536: read T from Tt
+  double* xs = reinterpret_cast<double*>(xt_lds);
+  double* buf = xs + C;  // [2][XS_CH * C]
   const int tid = threadIdx.x;
-  if (tid == 0) wide = 0;
-  __syncthreads();
-  int big = 0;
-  for (int k = tid; k < C * C; k += blockDim.x) {
-    const int32_t v = trans[k];
-    big |= (uint32_t)v > 0xFFFFu;
-    const int rr = k / C, c = k - rr * C;
-    cnt[c * C + rr] = (uint16_t)v;
-  }
-  if (big) wide = 1;  // benign race: every writer stores 1
   for (int r = tid; r < C; r += blockDim.x) {
     xs[r] = 0.0;
     heat[r] = 0.0;
-    mv[r] = (double)move[r];
   }
-  __syncthreads();
-  const bool use_tt = wide != 0;
   const int r = tid;
   const bool chain = r < C;
   double g = 0.0, pm = 0.0;
@@ -390,43 +360,40 @@ __global__ __launch_bounds__(XS_THREADS) void xt_solve_lds_kernel(const int32_t*
     g = gs[r];
     pm = pmove[r];
   }
-  const int nch = (C + CH - 1) / CH;
-  // products of columns [c0, c0 + CH) into buffer b
-  auto produce = [&](int c0, double* b) {
-    const int cols = C - c0 < CH ? C - c0 : CH;
-    for (int q = tid; q < cols * C; q += blockDim.x) {
-      const int cc = q / C, rr = q - cc * C;
-      const int c = c0 + cc;
-      double t;
-      if (use_tt) {
-        t = Tt[(int64_t)c * C + rr];
+  const int nch = (C + XS_CH - 1) / XS_CH;
+  // chunk k = columns [k * XS_CH, ...): Tt rows k*XS_CH .. (contiguous), 16-B pieces
+  auto load = [&](int k, double* b) {
+    const int c0 = k * XS_CH;
+    const int cols = C - c0 < XS_CH ? C - c0 : XS_CH;
+    const int64_t len = (int64_t)cols * C;  // doubles
+    const double* src = Tt + (int64_t)c0 * C;
+    for (int64_t q = 2 * tid; q < len; q += 2 * blockDim.x) {
+      if (q + 1 < len) {
+        *reinterpret_cast<f64x2*>(b + q) = *reinterpret_cast<const f64x2*>(src + q);
       } else {
-        const uint32_t v = cnt[c * C + rr];
-        t = v != 0 ? (double)v / mv[rr] : 0.0;
+        b[q] = src[q];
       }
-      b[q] = t * xs[c];
     }
   };
+  __syncthreads();
   int it = 0;
   bool cont = true;
   while (cont && it < max_iter) {
     double acc = 0.0;
-    produce(0, buf);
+    load(0, buf);
     __syncthreads();
     for (int k = 0; k < nch; ++k) {
-      if (k + 1 < nch) produce((k + 1) * CH, buf + ((k + 1) & 1) * CH * C);
+      if (k + 1 < nch) load(k + 1, buf + ((k + 1) & 1) * XS_CH * C);
       if (chain) {
-        const double* b = buf + (k & 1) * CH * C + r;
-        const int cols = C - k * CH < CH ? C - k * CH : CH;
-        int cc = 0;
-        for (; cc + 4 <= cols; cc += 4) {
-          const double p0 = b[cc * C], p1 = b[(cc + 1) * C], p2 = b[(cc + 2) * C], p3 = b[(cc + 3) * C];
-          acc = acc + p0;
-          acc = acc + p1;
-          acc = acc + p2;
-          acc = acc + p3;
-        }
-        for (; cc < cols; ++cc) acc = acc + b[cc * C];
+        const double* b = buf + (k & 1) * XS_CH * C + r;
+        const int c0 = k * XS_CH;
+        const int cols = C - c0 < XS_CH ? C - c0 : XS_CH;
+        double p[XS_CH];
+#pragma unroll
+        for (int cc = 0; cc < XS_CH; ++cc) p[cc] = cc < cols ? b[cc * C] * xs[c0 + cc] : 0.0;
+#pragma unroll
+        for (int cc = 0; cc < XS_CH; ++cc)
+          if (cc < cols) acc = acc + p[cc];
       }
       __syncthreads();
     }
@@ -912,11 +879,10 @@ extern "C" int sa_xt_solve(const int64_t* shot, const int64_t* goal, const int64
   hipLaunchKernelGGL(xt_transpose_kernel, tgrid, dim3(256), 0, st, trans, um, C, trans_t);
   rc = check_launch("xt normalise");
   if (!rc && C <= XT_SOLVE_MAX_C) {
-    const int CH = C <= XS_THREADS ? xt_solve_lds_chunk(C) : 0;
-    if (CH > 0) {
-      hipLaunchKernelGGL(xt_solve_lds_kernel, dim3(1), dim3(XS_THREADS), xt_solve_lds_bytes(C, CH), st,
-                         trans, trans_t, um, gs, pm, C, CH, eps, max_iter, heatmaps, mats + 3 * C, dn);
-      rc = check_launch("xt_solve_lds_kernel");
+    if (SA_XT_SOLVE_STREAM && xt_solve_stream_bytes(C) <= XT_LDS_BUDGET) {
+      hipLaunchKernelGGL(xt_solve_stream_kernel, dim3(1), dim3(XS_THREADS), xt_solve_stream_bytes(C), st,
+                         trans_t, gs, pm, C, eps, max_iter, heatmaps, mats + 3 * C, dn);
+      rc = check_launch("xt_solve_stream_kernel");
     } else {
       hipLaunchKernelGGL(xt_solve_small_kernel, dim3(1), dim3(((C + 63) / 64) * 64), 0, st, trans_t, gs,
                          pm, C, eps, max_iter, heatmaps, mats + 3 * C, dn);

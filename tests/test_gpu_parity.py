@@ -189,8 +189,14 @@ def test_many_small_segments_vs_oracle(sa, atomic):
     rng = np.random.default_rng(4)
     for dt in (np.float64, np.float32):
         ps, pc = rng.random(n).astype(dt), rng.random(n).astype(dt)
-        v = ops.formula(ab, torch.from_numpy(ps).to(ab.device),
-                        torch.from_numpy(pc).to(ab.device)).cpu().numpy()[:, :n]
+        tps, tpc = torch.from_numpy(ps).to(ab.device), torch.from_numpy(pc).to(ab.device)
+        v = ops.formula(ab, tps, tpc).cpu().numpy()[:, :n]
+        for nr in (10, 20):  # the fused labels + formula launch == the two separate ones
+            lf, vf = ops.labels_formula(ab, tps, tpc, nr_actions=nr)
+            lb = ops.labels(ab, nr_actions=nr)
+            for c in ('scores', 'concedes', 'goal_from_shot'):
+                assert torch.equal(getattr(lf, c)[:n], getattr(lb, c)[:n]), (c, nr, dt)
+            np.testing.assert_array_equal(vf.cpu().numpy()[:, :n], v)
         fo = vo.formula(cols, ps, pc, atomic=atomic, seg_off=so)
         for r, c in enumerate(('offensive_value', 'defensive_value', 'vaep_value')):
             if dt == np.float32:
