@@ -1,7 +1,7 @@
-# round-2 GPU call D: streamed xT solve, fused labels + formula
+# round-2 GPU call D: streamed xT solve, fused labels + formula, staged tree walk
 bash scripts/gpu_steps.sh \
- "tests:500:python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_dropin.py tests/test_gpu_debug.py -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider" \
+ "tests:500:python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_dropin.py tests/test_gpu_trees.py tests/test_gpu_debug.py -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider" \
  "xt_time:120:python scripts/xt_solve_time.py" \
  "xt_time_small:120:SOCCERACTION_AMD_LIB=socceraction_amd/_lib/libsocceraction_amd_solve_small.so python scripts/xt_solve_time.py" \
  "ab:240:python bench.py --no-side --no-cpu --steps 20 --warmup 3 --ab 'sep:xt=cells;fused:xt=cells/order=num_features+bool_features+goalscore+labels_formula;fused_gs_last:xt=cells/order=num_features+bool_features+labels_formula+goalscore'" \
- "prof:150:rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o r02d -- python bench.py --steps 10 --warmup 3 --no-cpu --no-side --order num_features,bool_features,goalscore,labels_formula"
+ "prof:200:rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o r02d -- python bench.py --steps 10 --warmup 3 --no-cpu --e2e-games 0 --order num_features,bool_features,goalscore,labels_formula"

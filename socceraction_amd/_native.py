@@ -144,6 +144,14 @@ _SIGNATURES = {
                                        ctypes.POINTER(SaBlock), ctypes.POINTER(SaBlock),
                                        ctypes.POINTER(SaBlock), ctypes.c_int64, ctypes.c_double,
                                        ctypes.c_int32, ctypes.c_int32, _p, _p]),
+    'sa_tree_staged_lds_bytes': (ctypes.c_int64, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                                  ctypes.c_int32]),
+    'sa_tree_predict_staged': (ctypes.c_int, [_p, ctypes.c_int32, _p, _p, ctypes.c_int32, _p,
+                                              ctypes.c_int32, _p, ctypes.c_int32,
+                                              ctypes.POINTER(SaBlock), ctypes.POINTER(SaBlock),
+                                              ctypes.POINTER(SaBlock), ctypes.c_int64,
+                                              ctypes.c_double, ctypes.c_int32, ctypes.c_int32, _p,
+                                              _p]),
     'sa_abi_version': (ctypes.c_int, []),
     'sa_last_error': (ctypes.c_char_p, []),
     'sa_build_id': (ctypes.c_char_p, []),

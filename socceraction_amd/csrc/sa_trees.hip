@@ -263,6 +263,130 @@ __global__ __launch_bounds__(TR_THREADS) void tree_fixed_kernel(const TNode* __r
     ((double*)out)[j] = 1.0 / (1.0 + exp(-(double)m));
 }
 
+// Staged walk (the model's used feature columns of the workgroup's rows copied into LDS once,
+// then every tree walked from LDS): the gathers of tree_fixed_kernel are divergent HBM/L2
+// loads -- one per lane, level and tree, ~582 B/action for a 100-tree model, but issued as
+// scattered single-lane accesses the memory pipeline serves a few lanes at a time.  Here a
+// workgroup of 256 rows first reads the used columns of its rows with coalesced 16-B loads:
+// bool columns (515 of the 568 default features) are packed on the fly into one bit per row
+// (a column's 256 rows = 4 u64, one per wave; a level reads the wave's u64 and shifts by the
+// lane), numeric columns are converted to the model's arithmetic type into a column-major
+// slab (conflict-free lane reads).  Nodes are restaged (host-prepared, `SNode`) with the
+// feature as a compact reference: bit 30 = numeric, the rest = index into the bool or numeric
+// column list; leaves are self-loops, so every tree of a group is walked exactly the group's
+// depth (tree_fixed_kernel's fixed-depth walk).  Values, split rule and summation order equal
+// tree_fixed_kernel's bit for bit.
+constexpr int TS_ROWS = 256;  // rows (threads) per workgroup
+constexpr int32_t TS_NUM = 1 << 30;
+
+template <typename A>
+struct SNode {
+  A thr;                      // threshold, or the leaf value
+  int32_t ref, left, right;   // right: bit 31 = default_left
+};
+
+template <bool F32, bool LE>
+__global__ __launch_bounds__(TS_ROWS) void tree_staged_kernel(const SNode<typename std::conditional<F32, float, double>::type>* __restrict__ nodes,
+                                                              int n_nodes, const int32_t* __restrict__ roots,
+                                                              const int32_t* __restrict__ depth, int n_trees,
+                                                              const int32_t* __restrict__ bool_cols, int n_bool,
+                                                              const int32_t* __restrict__ num_slots, int n_num,
+                                                              sa_block Bb, sa_block Bf, sa_block Bi, int64_t n,
+                                                              double base, void* __restrict__ out) {
+  using A = typename std::conditional<F32, float, double>::type;
+  extern __shared__ __attribute__((aligned(16))) unsigned char ts_lds[];
+  SNode<A>* L = reinterpret_cast<SNode<A>*>(ts_lds);
+  const size_t node_bytes = ((size_t)n_nodes * sizeof(SNode<A>) + 15) / 16 * 16;
+  const int nb = n_bool > 0 ? n_bool : 1;
+  uint16_t* M16 = reinterpret_cast<uint16_t*>(ts_lds + node_bytes);        // [nb][16] u16
+  const uint64_t* M = reinterpret_cast<const uint64_t*>(M16);              // [nb][4] u64
+  A* S = reinterpret_cast<A*>(ts_lds + node_bytes + (size_t)nb * 32);      // [nn][TS_ROWS]
+  const int tid = threadIdx.x;
+  const int64_t R0 = (int64_t)blockIdx.x * TS_ROWS;
+  for (int k = tid; k < n_nodes; k += TS_ROWS) L[k] = nodes[k];
+  if (n_bool == 0 && tid < 16) M16[tid] = 0;
+  if (n_num == 0) S[tid] = A(0);
+  // bool columns: item = (column u, 16-row piece p): one 16-B load -> 16 bits
+  for (int it = tid; it < n_bool * 16; it += TS_ROWS) {
+    const int u = it >> 4, p = it & 15;
+    const int64_t r = R0 + 16 * p;
+    uint32_t bits = 0;
+    if (r < n) {
+      const int64_t col = bool_cols[u];
+      SA_DCHECK(col >= 0 && col < Bb.n_cols, col);
+      const int64_t t = r / Bb.tile_rows;
+      const uint8_t* src = (const uint8_t*)Bb.data + (t * Bb.n_cols + col) * Bb.tile_rows + (r - t * Bb.tile_rows);
+      const u32x4 w = *reinterpret_cast<const u32x4*>(src);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) bits |= (((w[q] & 0x01010101u) * 0x01020408u) >> 24) << (4 * q);
+    }
+    M16[u * 16 + p] = (uint16_t)bits;
+  }
+  // numeric columns: item = (column v, 2-row piece p): one 16-B load -> 2 values of type A
+  for (int it = tid; it < n_num * (TS_ROWS / 2); it += TS_ROWS) {
+    const int v = it / (TS_ROWS / 2), p = it - v * (TS_ROWS / 2);
+    const int64_t r = R0 + 2 * p;
+    A x0 = A(0), x1 = A(0);
+    if (r < n) {
+      const int32_t slot = num_slots[v];
+      const int64_t col = slot & 0xFFFFFF;
+      if ((slot >> 24) == 1) {
+        SA_DCHECK(col < Bf.n_cols, col);
+        const int64_t t = r / Bf.tile_rows;
+        const f64x2 y = *reinterpret_cast<const f64x2*>((const double*)Bf.data + (t * Bf.n_cols + col) * Bf.tile_rows +
+                                                        (r - t * Bf.tile_rows));
+        x0 = (A)y[0];
+        x1 = (A)y[1];
+      } else {
+        SA_DCHECK(col < Bi.n_cols, col);
+        const int64_t t = r / Bi.tile_rows;
+        const i64x2 y = *reinterpret_cast<const i64x2*>((const int64_t*)Bi.data + (t * Bi.n_cols + col) * Bi.tile_rows +
+                                                        (r - t * Bi.tile_rows));
+        x0 = (A)(double)y[0];
+        x1 = (A)(double)y[1];
+      }
+    }
+    S[v * TS_ROWS + 2 * p] = x0;
+    S[v * TS_ROWS + 2 * p + 1] = x1;
+  }
+  __syncthreads();
+  const int64_t j = R0 + tid;
+  if (j >= n) return;
+  const int wv = tid >> 6, lane = tid & 63;
+  A m = (A)base;
+  for (int t0 = 0; t0 < n_trees; t0 += TG) {
+    int k[TG];
+    int D = 0;
+#pragma unroll
+    for (int u = 0; u < TG; ++u) {
+      const int t = t0 + u < n_trees ? t0 + u : n_trees - 1;
+      k[u] = roots[t];
+      D = max(D, depth[t]);
+    }
+    for (int d = 0; d < D; ++d) {
+#pragma unroll
+      for (int u = 0; u < TG; ++u) {
+        const SNode<A> nd = L[k[u]];
+        const bool num = (nd.ref & TS_NUM) != 0;
+        const int idx = nd.ref & (TS_NUM - 1);
+        SA_DCHECK(num ? idx < (n_num > 0 ? n_num : 1) : idx < nb, nd.ref);
+        const uint64_t mk = M[(num ? 0 : idx) * 4 + wv];
+        const A vn = S[(num ? idx : 0) * TS_ROWS + tid];
+        const A v = num ? vn : (A)((mk >> lane) & 1ull);
+        const bool left = isnan(v) ? nd.right < 0 : (LE ? v <= nd.thr : v < nd.thr);
+        k[u] = left ? nd.left : (nd.right & 0x7FFFFFFF);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < TG; ++u)
+      if (t0 + u < n_trees) m = m + L[k[u]].thr;
+  }
+  if (F32)
+    ((float*)out)[j] = 1.0f / (1.0f + expf(-(float)m));
+  else
+    ((double*)out)[j] = 1.0 / (1.0 + exp(-(double)m));
+}
+
 }  // namespace sa
 
 using namespace sa;
@@ -312,4 +436,47 @@ extern "C" int sa_tree_predict(const void* nodes, int32_t n_nodes, const int32_t
     SA_TREE_LAUNCH(false, false);
 #undef SA_TREE_LAUNCH
   return check_launch("tree_predict_kernel");
+}
+
+extern "C" int64_t sa_tree_staged_lds_bytes(int32_t n_nodes, int32_t n_bool, int32_t n_num, int32_t f32) {
+  const size_t node = f32 ? sizeof(SNode<float>) : sizeof(SNode<double>);
+  const size_t nb = n_bool > 0 ? n_bool : 1, nn = n_num > 0 ? n_num : 1;
+  return (int64_t)(((size_t)n_nodes * node + 15) / 16 * 16 + nb * 32 + nn * TS_ROWS * (f32 ? 4 : 8));
+}
+
+extern "C" int sa_tree_predict_staged(const void* snodes, int32_t n_nodes, const int32_t* roots,
+                                      const int32_t* tree_depth, int32_t n_trees, const int32_t* bool_cols,
+                                      int32_t n_bool, const int32_t* num_slots, int32_t n_num,
+                                      const sa_block* bool_blk, const sa_block* f64_blk,
+                                      const sa_block* i64_blk, int64_t n, double base_margin, int32_t le,
+                                      int32_t f32, void* p_out, void* stream) {
+  if (n < 0 || n_nodes < 1 || n_trees < 1 || n_bool < 0 || n_num < 0 || !snodes || !roots ||
+      !tree_depth || !p_out || (n_bool > 0 && (!bool_cols || !bool_blk)) || (n_num > 0 && !num_slots))
+    return fail(SA_EINVAL, "bad staged tree model arguments");
+  const int64_t lds = sa_tree_staged_lds_bytes(n_nodes, n_bool, n_num, f32);
+  if (lds > 160 * 1024) return fail(SA_EINVAL, "staged tree model needs %lld B of LDS", (long long)lds);
+  sa_block z{nullptr, 0, 0, 16};
+  const sa_block Bb = bool_blk ? *bool_blk : z, Bf = f64_blk ? *f64_blk : z, Bi = i64_blk ? *i64_blk : z;
+  if (n_bool > 0 && (Bb.tile_rows % 16 != 0 || !aligned16(Bb.data)))
+    return fail(SA_EINVAL, "bool block: 16-row tiles, 16-byte aligned");
+  if ((Bf.data && (Bf.tile_rows % 2 != 0 || !aligned16(Bf.data))) ||
+      (Bi.data && (Bi.tile_rows % 2 != 0 || !aligned16(Bi.data))))
+    return fail(SA_EINVAL, "numeric blocks: even tiles, 16-byte aligned");
+  if (n == 0) return SA_OK;
+  const dim3 grid((unsigned)((n + TS_ROWS - 1) / TS_ROWS)), block(TS_ROWS);
+  hipStream_t st = (hipStream_t)stream;
+#define SA_TS_LAUNCH(F, LEQ, A)                                                                         \
+  hipLaunchKernelGGL((tree_staged_kernel<F, LEQ>), grid, block, (size_t)lds, st,                         \
+                     (const SNode<A>*)snodes, n_nodes, roots, tree_depth, n_trees, bool_cols, n_bool,       \
+                     num_slots, n_num, Bb, Bf, Bi, n, base_margin, p_out)
+  if (f32 && le)
+    SA_TS_LAUNCH(true, true, float);
+  else if (f32)
+    SA_TS_LAUNCH(true, false, float);
+  else if (le)
+    SA_TS_LAUNCH(false, true, double);
+  else
+    SA_TS_LAUNCH(false, false, double);
+#undef SA_TS_LAUNCH
+  return check_launch("tree_staged_kernel");
 }

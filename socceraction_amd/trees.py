@@ -195,19 +195,75 @@ class TreeEnsemble:
             slots[f] = (kinds[kind] << 24) | col
         return slots
 
+    def staged_layout(self, slots: np.ndarray):
+        """The staged walk's model (sa_tree_predict_staged): ``(snodes, bool_cols, num_slots)``
+        for the feature slots of one block layout. Split nodes refer to their feature as an index
+        into the used bool columns, or (1 << 30) | index into the used numeric slots; leaves
+        become self-loops (left = right = the leaf)."""
+        nd = self.nodes
+        n = len(nd)
+        split = nd['feature'] >= 0
+        fslot = np.full(n, -1, np.int64)
+        fslot[split] = slots[nd['feature'][split]]
+        kind = fslot >> 24
+        bool_cols = np.unique(fslot[split & (kind == 0)] & 0xFFFFFF).astype(np.int32)
+        num_slots = np.unique(fslot[split & (kind != 0)]).astype(np.int32)
+        ref = np.zeros(n, np.int64)
+        isb = split & (kind == 0)
+        isn = split & (kind != 0)
+        ref[isb] = np.searchsorted(bool_cols, fslot[isb] & 0xFFFFFF)
+        ref[isn] = (1 << 30) | np.searchsorted(num_slots, fslot[isn])
+        if not len(bool_cols):
+            ref[~split] = 1 << 30  # leaves: any valid reference
+        idx = np.arange(n)
+        dt = np.dtype([('thr', '<f4'), ('ref', '<i4'), ('left', '<i4'), ('right', '<i4')]) \
+            if self.f32 else \
+            np.dtype([('thr', '<f8'), ('ref', '<i4'), ('left', '<i4'), ('right', '<i4'), ('pad', '<i4')])
+        sn = np.zeros(n, dt)
+        sn['thr'] = nd['thr'].astype(np.float32) if self.f32 else nd['thr']
+        sn['ref'] = ref.astype(np.int32)
+        sn['left'] = np.where(split, nd['left'], idx)
+        sn['right'] = np.where(split, nd['right'], idx)
+        return sn, bool_cols, num_slots
+
     def predict_blocks(self, blocks, feature_names: Optional[Sequence[str]] = None,
-                       out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                       out: Optional[torch.Tensor] = None, staged: Optional[bool] = None) -> torch.Tensor:
         """P(class 1) of every row of the device feature blocks (``ops.FeatureBlocks``):
-        float32 for xgboost models (as their ``predict_proba``), float64 for scikit-learn."""
+        float32 for xgboost models (as their ``predict_proba``), float64 for scikit-learn.
+        ``staged`` (default: whenever the model's staged form fits LDS): the staged walk
+        (sa_tree_predict_staged); False: the gather walk (sa_tree_predict)."""
         from .batch import stream_handle
         dev = blocks.bool_block.device
         d = self._device(dev)
-        slots = torch.from_numpy(self.feature_slots(blocks.plan, feature_names)).to(dev)
+        slots_np = self.feature_slots(blocks.plan, feature_names)
         n = blocks.n
         dt = torch.float32 if self.f32 else torch.float64
         if out is None:
             out = torch.empty(max(n, 1), dtype=dt, device=dev)
         bb, fb, ib = blocks.sa_blocks()
+        if staged is not False and self.n_trees and d['depth'] is not None:
+            key = ('staged', slots_np.tobytes())
+            st = d.get(key)
+            if st is None:
+                sn, bc, ns = self.staged_layout(slots_np)
+                lds = _native.lib().sa_tree_staged_lds_bytes(len(sn), len(bc), len(ns), int(self.f32))
+                st = None if lds > 160 * 1024 else (
+                    torch.from_numpy(sn.view(np.uint8).copy()).to(dev),
+                    torch.from_numpy(bc).to(dev) if len(bc) else None, len(bc),
+                    torch.from_numpy(ns).to(dev) if len(ns) else None, len(ns), len(sn))
+                d[key] = st if st is not None else False
+            if st:
+                sn_t, bc_t, nbc, ns_t, nns, nnodes = st
+                _native.check(_native.lib().sa_tree_predict_staged(
+                    sn_t.data_ptr(), nnodes, d['roots'].data_ptr(), d['depth'].data_ptr(),
+                    self.n_trees, bc_t.data_ptr() if bc_t is not None else None, nbc,
+                    ns_t.data_ptr() if ns_t is not None else None, nns, ctypes.byref(bb),
+                    ctypes.byref(fb), ctypes.byref(ib), n, float(self.base_margin), int(self.le),
+                    int(self.f32), out.data_ptr(), stream_handle()))
+                return out[:n]
+            elif staged:
+                raise ValueError('the staged form of this model does not fit LDS')
+        slots = torch.from_numpy(slots_np).to(dev)
         _native.check(_native.lib().sa_tree_predict(
             d['nodes'].data_ptr(), len(self.nodes), d['roots'].data_ptr(),
             d['depth'].data_ptr() if (self.n_trees and d['depth'] is not None) else None,

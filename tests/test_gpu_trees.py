@@ -148,3 +148,43 @@ def test_vaep_rate_on_device(sa):
     model._VAEP__models = xg
     got32 = model.rate_batch(games, actions)
     assert got32['vaep_value'].dtype == np.float32
+
+
+@pytest.mark.parametrize('kind', ['xgboost', 'sklearn', 'xgboost_bool_only', 'xgboost_num_only'])
+def test_staged_walk_equals_gather_walk(sa, kind):
+    """The LDS-staged walk (used columns of 256 rows staged, bools packed to bits) gives the
+    gather walk's probabilities bit for bit: xgboost float32 / scikit-learn float64 models,
+    models reading only bool or only numeric features, several tiles and a ragged last
+    workgroup (300 games), NaN in a numeric feature."""
+    from socceraction_amd import synthetic
+    from oracle import vaep_oracle as vo
+    B, ops, trees = sa['batch'], sa['ops'], sa['trees']
+    d = synthetic.spadl_games(300, seed=8)
+    ab = B.ActionBatch.from_columns(d)
+    fb = ops.features(ab, vo.SPADL_DEFAULT, 3, bool_tile=1024, num_tile=128)
+    kinds = [k for _, k, _ in fb.plan.order]
+    if kind.startswith('xgboost'):
+        fk = list(kinds)
+        model = trees.synthetic_xgboost_json(len(kinds), n_trees=100, depth=3, seed=11,
+                                             feature_kinds=fk)
+        keep = {'xgboost_bool_only': 'b', 'xgboost_num_only': 'fi'}.get(kind)
+        if keep:  # re-point every split at a feature of the wanted kinds
+            cand = [j for j, k in enumerate(kinds) if k in keep]
+            rng = np.random.default_rng(2)
+            for t in model['learner']['gradient_booster']['model']['trees']:
+                t['split_indices'] = [int(rng.choice(cand)) for _ in t['split_indices']]
+        te = trees.TreeEnsemble.from_model(model)
+    else:
+        from sklearn.ensemble import HistGradientBoostingClassifier
+        n = 20000
+        b, f, i = fb.to_numpy()
+        blocks = {'b': b, 'f': f, 'i': i}
+        X = np.stack([blocks[k][c, :n].astype(np.float64) for _, k, c in fb.plan.order], axis=1)
+        y = (X[:, 0] + np.random.default_rng(0).random(n) > 0.7).astype(int)
+        te = trees.TreeEnsemble.from_model(
+            HistGradientBoostingClassifier(max_iter=40, max_depth=4, random_state=0).fit(X, y))
+    fcol = [c for _, k, c in fb.plan.order if k == 'f'][5]
+    fb.f64_block[:, fcol, ::7] = float('nan')
+    got = te.predict_blocks(fb, staged=True).cpu().numpy()
+    ref = te.predict_blocks(fb, staged=False).cpu().numpy()
+    np.testing.assert_array_equal(got, ref)
