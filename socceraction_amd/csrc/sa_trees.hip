@@ -303,51 +303,92 @@ __global__ __launch_bounds__(TS_ROWS) void tree_staged_kernel(const SNode<typena
   A* S = reinterpret_cast<A*>(ts_lds + node_bytes + (size_t)nb * 32);      // [nn][TS_ROWS]
   const int tid = threadIdx.x;
   const int64_t R0 = (int64_t)blockIdx.x * TS_ROWS;
-  for (int k = tid; k < n_nodes; k += TS_ROWS) L[k] = nodes[k];
+  // every load of a staging pass is issued before any is used (TS_B per thread in flight):
+  // a pass is one memory latency, not TS_B of them
+  constexpr int TS_B = 8;
+  for (int k0 = 0; k0 < n_nodes; k0 += TS_ROWS * TS_B) {
+    SNode<A> v[TS_B];
+#pragma unroll
+    for (int b = 0; b < TS_B; ++b) {
+      const int k = k0 + b * TS_ROWS + tid;
+      if (k < n_nodes) v[b] = nodes[k];
+    }
+#pragma unroll
+    for (int b = 0; b < TS_B; ++b) {
+      const int k = k0 + b * TS_ROWS + tid;
+      if (k < n_nodes) L[k] = v[b];
+    }
+  }
   if (n_bool == 0 && tid < 16) M16[tid] = 0;
   if (n_num == 0) S[tid] = A(0);
-  // bool columns: item = (column u, 16-row piece p): one 16-B load -> 16 bits
-  for (int it = tid; it < n_bool * 16; it += TS_ROWS) {
-    const int u = it >> 4, p = it & 15;
-    const int64_t r = R0 + 16 * p;
-    uint32_t bits = 0;
-    if (r < n) {
-      const int64_t col = bool_cols[u];
-      SA_DCHECK(col >= 0 && col < Bb.n_cols, col);
-      const int64_t t = r / Bb.tile_rows;
-      const uint8_t* src = (const uint8_t*)Bb.data + (t * Bb.n_cols + col) * Bb.tile_rows + (r - t * Bb.tile_rows);
-      const u32x4 w = *reinterpret_cast<const u32x4*>(src);
+  // bool columns: item it = (column u = it / 16, 16-row piece p = it % 16): one 16-B load of
+  // the piece -> 16 bits at M16[it]
+  const int nbi = n_bool * 16;
+  for (int i0 = 0; i0 < nbi; i0 += TS_ROWS * TS_B) {
+    u32x4 w[TS_B];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) bits |= (((w[q] & 0x01010101u) * 0x01020408u) >> 24) << (4 * q);
-    }
-    M16[u * 16 + p] = (uint16_t)bits;
-  }
-  // numeric columns: item = (column v, 2-row piece p): one 16-B load -> 2 values of type A
-  for (int it = tid; it < n_num * (TS_ROWS / 2); it += TS_ROWS) {
-    const int v = it / (TS_ROWS / 2), p = it - v * (TS_ROWS / 2);
-    const int64_t r = R0 + 2 * p;
-    A x0 = A(0), x1 = A(0);
-    if (r < n) {
-      const int32_t slot = num_slots[v];
-      const int64_t col = slot & 0xFFFFFF;
-      if ((slot >> 24) == 1) {
-        SA_DCHECK(col < Bf.n_cols, col);
-        const int64_t t = r / Bf.tile_rows;
-        const f64x2 y = *reinterpret_cast<const f64x2*>((const double*)Bf.data + (t * Bf.n_cols + col) * Bf.tile_rows +
-                                                        (r - t * Bf.tile_rows));
-        x0 = (A)y[0];
-        x1 = (A)y[1];
-      } else {
-        SA_DCHECK(col < Bi.n_cols, col);
-        const int64_t t = r / Bi.tile_rows;
-        const i64x2 y = *reinterpret_cast<const i64x2*>((const int64_t*)Bi.data + (t * Bi.n_cols + col) * Bi.tile_rows +
-                                                        (r - t * Bi.tile_rows));
-        x0 = (A)(double)y[0];
-        x1 = (A)(double)y[1];
+    for (int b = 0; b < TS_B; ++b) {
+      const int it = i0 + b * TS_ROWS + tid;
+      w[b] = u32x4{0, 0, 0, 0};
+      const int64_t r = R0 + 16 * (it & 15);
+      if (it < nbi && r < n) {
+        const int64_t col = bool_cols[it >> 4];
+        SA_DCHECK(col >= 0 && col < Bb.n_cols, col);
+        const int64_t t = r / Bb.tile_rows;
+        w[b] = *reinterpret_cast<const u32x4*>((const uint8_t*)Bb.data + (t * Bb.n_cols + col) * Bb.tile_rows +
+                                               (r - t * Bb.tile_rows));
       }
     }
-    S[v * TS_ROWS + 2 * p] = x0;
-    S[v * TS_ROWS + 2 * p + 1] = x1;
+#pragma unroll
+    for (int b = 0; b < TS_B; ++b) {
+      const int it = i0 + b * TS_ROWS + tid;
+      uint32_t bits = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) bits |= (((w[b][q] & 0x01010101u) * 0x01020408u) >> 24) << (4 * q);
+      if (it < nbi) M16[it] = (uint16_t)bits;
+    }
+  }
+  // numeric columns: item it = (column v = it / 128, 2-row piece p = it % 128): one 16-B load
+  // -> 2 values of type A at S[v * TS_ROWS + 2p]
+  constexpr int PP = TS_ROWS / 2;
+  const int nni = n_num * PP;
+  for (int i0 = 0; i0 < nni; i0 += TS_ROWS * TS_B) {
+    f64x2 y[TS_B];
+    bool isf[TS_B];
+#pragma unroll
+    for (int b = 0; b < TS_B; ++b) {
+      const int it = i0 + b * TS_ROWS + tid;
+      y[b] = f64x2{0.0, 0.0};
+      isf[b] = true;
+      const int v = it / PP;
+      const int64_t r = R0 + 2 * (it - v * PP);
+      if (it < nni && r < n) {
+        const int32_t slot = num_slots[v];
+        const int64_t col = slot & 0xFFFFFF;
+        isf[b] = (slot >> 24) == 1;
+        const sa_block& Bk = isf[b] ? Bf : Bi;
+        SA_DCHECK(col < Bk.n_cols, col);
+        const int64_t t = r / Bk.tile_rows;
+        y[b] = *reinterpret_cast<const f64x2*>((const char*)Bk.data +
+                                               ((t * Bk.n_cols + col) * Bk.tile_rows + (r - t * Bk.tile_rows)) * 8);
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < TS_B; ++b) {
+      const int it = i0 + b * TS_ROWS + tid;
+      if (it < nni) {
+        A x0, x1;
+        if (isf[b]) {
+          x0 = (A)y[b][0];
+          x1 = (A)y[b][1];
+        } else {  // the i64 block: the same 16 bytes as two int64
+          x0 = (A)(double)__double_as_longlong(y[b][0]);
+          x1 = (A)(double)__double_as_longlong(y[b][1]);
+        }
+        S[it * 2] = x0;  // v * TS_ROWS + 2p == 2 * it
+        S[it * 2 + 1] = x1;
+      }
+    }
   }
   __syncthreads();
   const int64_t j = R0 + tid;

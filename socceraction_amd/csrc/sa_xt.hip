@@ -17,8 +17,8 @@
 #include "sa_common.h"
 #include "sa_internal.h"
 
-#ifndef SA_XT_SOLVE_STREAM
-#define SA_XT_SOLVE_STREAM 1  // small grids: xt_solve_stream_kernel (0: xt_solve_small_kernel, A/B)
+#ifndef SA_XT_SOLVE_REG
+#define SA_XT_SOLVE_REG 1  // C <= 192: xt_solve_reg_kernel (0: xt_solve_small_kernel, A/B)
 #endif
 #ifndef SA_XT_WIDE
 #define SA_XT_WIDE 1  // C <= 197: XC_WIDE count pass (0: the 32k-action XC_SMALL workgroups)
@@ -323,79 +323,81 @@ __device__ __forceinline__ double row_payoff(const double* __restrict__ Tt, cons
 
 // Small grids: one persistent workgroup runs every iteration; x lives in LDS.
 constexpr int XT_SOLVE_MAX_C = 1024;
-constexpr size_t XT_LDS_BUDGET = 160 * 1024;  // gfx950 LDS per workgroup
-constexpr int XS_THREADS = 1024;  // 16 waves stream the matrix; C of the lanes run the row sums
-constexpr int XS_CH = 16;         // columns per chunk
+// Value iteration of grids up to 192 cells (16 x 12) in one persistent workgroup of 1024
+// threads that keeps the whole exact transposed transition matrix Tt (trans_t, f64: one
+// correctly rounded division cnt / move[s] per element, formed once by xt_transpose_kernel) in
+// REGISTERS for every iteration: element q = c * C + r of the C * C <= 36,864 lives in thread
+// q % 1024, slot q / 1024 (36 doubles = 72 VGPRs per thread; the CU's register file holds the
+// 295 KB matrix, which LDS could not).  Per iteration the elements go by in 6 chunks of 6 slots:
+// every thread multiplies its 6 elements by x[c] into a double-buffered LDS slab (48 KB), one
+// barrier, and the C row lanes add the chunk's products of their row to their sums strictly
+// left to right in column order (xthreat.py:306-312) while the next chunk is formed.  Nothing
+// is read from L2 / HBM after the first load, so the solve no longer slows down when it shares
+// the chip with the streaming VAEP kernels (xt_solve_small_kernel re-reads Tt from L2 every
+// iteration).
+constexpr int XR_THREADS = 512;
+constexpr int XR_K = 72;        // matrix elements per thread
+constexpr int XR_CK = 12;        // elements per thread per chunk
+constexpr int XR_NCH = XR_K / XR_CK;
+constexpr int XR_CHUNK = XR_THREADS * XR_CK;  // elements per chunk
+constexpr int XR_MAX_C = 192;   // C * C <= XR_THREADS * XR_K
 
-// LDS bytes of xt_solve_stream_kernel: x + two chunk buffers of XS_CH x C doubles.
-static inline size_t xt_solve_stream_bytes(int C) { return (size_t)C * 8 + (size_t)2 * XS_CH * C * 8; }
-
-// Value iteration of small grids (C <= XT_SOLVE_MAX_C, e.g. 16 x 12) in one persistent
-// workgroup.  The exact transposed transition matrix Tt (trans_t, f64: one correctly rounded
-// division cnt / move[s] per element, formed once by xt_transpose_kernel) is streamed from
-// L2 / MALL every iteration in chunks of XS_CH columns: all 16 waves load a chunk with 16-B
-// loads (contiguous XS_CH * C doubles) into a double-buffered LDS slab while the row lanes
-// add the previous chunk's products T[r, c] * x[c] to their sums strictly left to right
-// (xthreat.py:306-312), so the matrix read is spread over every wave of the CU instead of being
-// issued by the C row lanes alone (xt_solve_small_kernel).
-__global__ __launch_bounds__(XS_THREADS) void xt_solve_stream_kernel(const double* __restrict__ Tt,
-                                                                     const double* __restrict__ gs,
-                                                                     const double* __restrict__ pmove, int C,
-                                                                     double eps, int max_iter,
-                                                                     double* __restrict__ heat,
-                                                                     double* __restrict__ xT_out,
-                                                                     int32_t* __restrict__ n_iter) {
-  extern __shared__ __align__(16) uint8_t xt_lds[];
-  double* xs = reinterpret_cast<double*>(xt_lds);
-  double* buf = xs + C;  // [2][XS_CH * C]
+__global__ __launch_bounds__(XR_THREADS) void xt_solve_reg_kernel(const double* __restrict__ Tt,
+                                                                  const double* __restrict__ gs,
+                                                                  const double* __restrict__ pmove, int C,
+                                                                  double eps, int max_iter,
+                                                                  double* __restrict__ heat,
+                                                                  double* __restrict__ xT_out,
+                                                                  int32_t* __restrict__ n_iter) {
+  __shared__ double xs[XR_MAX_C];
+  __shared__ double buf[2][XR_CHUNK];
   const int tid = threadIdx.x;
-  for (int r = tid; r < C; r += blockDim.x) {
-    xs[r] = 0.0;
-    heat[r] = 0.0;
-  }
+  const int CC = C * C;
+  const int kmax = CC > tid ? (CC - tid + XR_THREADS - 1) / XR_THREADS : 0;  // slots in use
+  double tv[XR_K];
+#pragma unroll
+  for (int k = 0; k < XR_K; ++k) tv[k] = k < kmax ? Tt[tid + XR_THREADS * k] : 0.0;
+  // column of slot k: c_k = (tid + 1024 k) / C, stepped incrementally
+  const int ca = XR_THREADS / C, cb = XR_THREADS - ca * C;
+  const int c0 = tid / C, r0 = tid - c0 * C;
   const int r = tid;
   const bool chain = r < C;
   double g = 0.0, pm = 0.0;
   if (chain) {
+    xs[r] = 0.0;
+    heat[r] = 0.0;
     g = gs[r];
     pm = pmove[r];
   }
-  const int nch = (C + XS_CH - 1) / XS_CH;
-  // chunk k = columns [k * XS_CH, ...): Tt rows k*XS_CH .. (contiguous), 16-B pieces
-  auto load = [&](int k, double* b) {
-    const int c0 = k * XS_CH;
-    const int cols = C - c0 < XS_CH ? C - c0 : XS_CH;
-    const int64_t len = (int64_t)cols * C;  // doubles
-    const double* src = Tt + (int64_t)c0 * C;
-    for (int64_t q = 2 * tid; q < len; q += 2 * blockDim.x) {
-      if (q + 1 < len) {
-        *reinterpret_cast<f64x2*>(b + q) = *reinterpret_cast<const f64x2*>(src + q);
-      } else {
-        b[q] = src[q];
-      }
-    }
-  };
   __syncthreads();
   int it = 0;
   bool cont = true;
   while (cont && it < max_iter) {
     double acc = 0.0;
-    load(0, buf);
-    __syncthreads();
-    for (int k = 0; k < nch; ++k) {
-      if (k + 1 < nch) load(k + 1, buf + ((k + 1) & 1) * XS_CH * C);
-      if (chain) {
-        const double* b = buf + (k & 1) * XS_CH * C + r;
-        const int c0 = k * XS_CH;
-        const int cols = C - c0 < XS_CH ? C - c0 : XS_CH;
-        double p[XS_CH];
+    int c = c0, rr = r0;  // column / row of slot k
 #pragma unroll
-        for (int cc = 0; cc < XS_CH; ++cc) p[cc] = cc < cols ? b[cc * C] * xs[c0 + cc] : 0.0;
+    for (int j = 0; j < XR_NCH; ++j) {
+      double* b = buf[j & 1];
 #pragma unroll
-        for (int cc = 0; cc < XS_CH; ++cc)
-          if (cc < cols) acc = acc + p[cc];
+      for (int u = 0; u < XR_CK; ++u) {
+        if (j * XR_CK + u < kmax) b[tid + XR_THREADS * u] = tv[j * XR_CK + u] * xs[c];
+        c += ca;
+        rr += cb;
+        if (rr >= C) {
+          rr -= C;
+          ++c;
+        }
       }
       __syncthreads();
+      if (chain) {
+        // this chunk holds elements [j * XR_CHUNK, (j + 1) * XR_CHUNK): columns c with
+        // j * XR_CHUNK <= c * C + r < (j + 1) * XR_CHUNK, in order
+        const int lo = j * XR_CHUNK, hi = lo + XR_CHUNK;
+        int cs = lo - r <= 0 ? 0 : (lo - r + C - 1) / C;
+        int ce = (hi - r + C - 1) / C;
+        if (ce > C) ce = C;
+        for (int cc = cs; cc < ce; ++cc) acc = acc + b[cc * C + r - lo];
+      }
     }
     double nx = 0.0;
     int flag = 0;
@@ -879,10 +881,10 @@ extern "C" int sa_xt_solve(const int64_t* shot, const int64_t* goal, const int64
   hipLaunchKernelGGL(xt_transpose_kernel, tgrid, dim3(256), 0, st, trans, um, C, trans_t);
   rc = check_launch("xt normalise");
   if (!rc && C <= XT_SOLVE_MAX_C) {
-    if (SA_XT_SOLVE_STREAM && xt_solve_stream_bytes(C) <= XT_LDS_BUDGET) {
-      hipLaunchKernelGGL(xt_solve_stream_kernel, dim3(1), dim3(XS_THREADS), xt_solve_stream_bytes(C), st,
-                         trans_t, gs, pm, C, eps, max_iter, heatmaps, mats + 3 * C, dn);
-      rc = check_launch("xt_solve_stream_kernel");
+    if (SA_XT_SOLVE_REG && C <= XR_MAX_C) {
+      hipLaunchKernelGGL(xt_solve_reg_kernel, dim3(1), dim3(XR_THREADS), 0, st, trans_t, gs, pm, C, eps,
+                         max_iter, heatmaps, mats + 3 * C, dn);
+      rc = check_launch("xt_solve_reg_kernel");
     } else {
       hipLaunchKernelGGL(xt_solve_small_kernel, dim3(1), dim3(((C + 63) / 64) * 64), 0, st, trans_t, gs,
                          pm, C, eps, max_iter, heatmaps, mats + 3 * C, dn);

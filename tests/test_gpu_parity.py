@@ -434,3 +434,42 @@ def test_xt_cell_codes_match_coordinate_path(sa, l, w, games):
     assert int(e.item()) == int(e_ref.item()) == 4
     with pytest.raises(ValueError):
         ops.xt_cells(ab, 105, 68)  # 7140 cells do not fit the 12-bit fields
+
+
+def test_atomic_cfg3_slice_sampled_games_vs_oracle(sa):
+    """cfg3's per-GPU slice (1,250 synthetic atomic games, ~5M atomic actions -- 40M over 8
+    GPUs): Atomic-VAEP features (k=3, default xfns, 154 columns) + labels of the whole batch,
+    12 sampled games checked against the oracle column by column, plus the whole-batch
+    invariant that every window's atomic type one-hot has exactly one True per action (the
+    duplicate 'interception' column is true for ids 10 and 24)."""
+    B, ops, syn = sa['batch'], sa['ops'], sa['synthetic']
+    d = syn.atomic_games(1250)
+    ab = B.ActionBatch.from_columns(d, atomic=True)
+    assert ab.n > 4_000_000
+    fb = ops.features(ab, vo.ATOMIC_DEFAULT, 3, bool_tile=1024, num_tile=128)
+    lb = ops.labels(ab)
+    torch.cuda.synchronize()
+    plan = fb.plan
+    tcols = [col for name, kind, col in plan.order if kind == 'b' and name.startswith('type_')]
+    assert len(tcols) == 3 * 32
+    for i in range(3):
+        s = fb.bool_block[:, tcols[i * 32]:tcols[i * 32] + 32, :].sum(dim=1, dtype=torch.int32)
+        assert bool((s.reshape(-1)[:ab.n] == 1).all())
+    rng = np.random.default_rng(1)
+    off = d['game_off']
+    names = ('period_id', 'time_seconds', 'team_id', 'x', 'y', 'dx', 'dy', 'type_id', 'bodypart_id')
+    for g in rng.choice(len(off) - 1, 12, replace=False):
+        s, e = int(off[g]), int(off[g + 1])
+        cols = {c: d[c][s:e] for c in names}
+        ref = vo.features(cols, 3, vo.ATOMIC_DEFAULT, atomic=True, home=[d['home_team_id'][g]])
+        assert [c[0] for c in ref] == plan.names
+        blocks = {k: fb.block(k)[:, s:e].cpu().numpy() for k in 'bfi'}
+        for (name, kind, col), (_, _, rv) in zip(plan.order, ref):
+            got = blocks[kind][col]
+            if kind == 'f':
+                assert_close(got, rv, name)
+            else:
+                np.testing.assert_array_equal(got.astype(np.int64), rv.astype(np.int64), err_msg=name)
+        lab = vo.labels(cols, atomic=True)
+        for c in ('scores', 'concedes', 'goal_from_shot'):
+            np.testing.assert_array_equal(getattr(lb, c)[s:e].cpu().numpy().astype(bool), lab[c])
