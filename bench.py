@@ -416,9 +416,11 @@ def main() -> None:
                          'else 0)')
     ap.add_argument('--bool-tile', type=int, default=1024,
                     help='rows per bool-block tile (0 = one tile: plain column-major)')
-    ap.add_argument('--order', default='num_features,bool_features,goalscore,labels,formula',
-                    help='launch order of the VAEP kernels in the step (default measured 1.3 %% '
-                         'faster than bool first, in-process A/B: profiles/r01h_order_ab.log)')
+    ap.add_argument('--order', default='num_features,bool_features,goalscore,labels_formula',
+                    help='launch order of the VAEP kernels in the step; labels_formula = labels + '
+                         'formula in one launch (num first: 1.3 %% faster than bool first, '
+                         'profiles/r01h_order_ab.log; fused tail 3.236 vs 3.244 ms, '
+                         'profiles/r02_step_ab.md)')
     ap.add_argument('--xt-source', default='cells', choices=('cells', 'codes', 'coords'),
                     help='what the xT count + rate passes read: the cell codes the f64 feature '
                          'pass writes (4 B/action, default), or the coordinates (34 B/action; '

@@ -404,13 +404,13 @@ int sa_tree_predict(const void* nodes, int32_t n_nodes, const int32_t* roots, co
                     const sa_block* bool_blk, const sa_block* f64_blk, const sa_block* i64_blk, int64_t n,
                     double base_margin, int32_t le, int32_t f32, void* p_out, void* stream);
 
-/* sa_tree_predict with the model's used feature columns staged in LDS per workgroup of 256
- * rows (coalesced reads; bool columns packed to bits) and every tree walked from LDS, a fixed
- * number of levels per tree.  snodes: n_nodes records { T threshold_or_leaf_value; int32 ref;
- * int32 left; int32 right | (default_left << 31); } with T = float (f32 = 1, 16 B) or double
- * (24 B incl. padding); leaves are self-loops (left = right = the leaf).  ref = index into
- * bool_cols (bool block columns) or (1 << 30) | index into num_slots ((kind << 24) | column,
- * kind 1 = f64 block, 2 = i64 block).  tree_depth is required.  Same probabilities as
+/* sa_tree_predict with the model's used bool feature columns staged in LDS per workgroup of
+ * 512 rows (coalesced reads, packed to one bit per row; numeric features stay gathers) and every
+ * tree walked a fixed number of levels.  snodes: n_nodes records { T threshold_or_leaf_value;
+ * int32 ref; int32 left; int32 right | (default_left << 31); } with T = float (f32 = 1, 16 B)
+ * or double (24 B incl. padding); leaves are self-loops (left = right = the leaf).  ref = index
+ * into bool_cols (bool block columns) or (1 << 30) | index into num_slots ((kind << 24) |
+ * column, kind 1 = f64 block, 2 = i64 block).  tree_depth is required.  Same probabilities as
  * sa_tree_predict bit for bit.  sa_tree_staged_lds_bytes: the LDS a model needs (<= 160 KiB). */
 int64_t sa_tree_staged_lds_bytes(int32_t n_nodes, int32_t n_bool, int32_t n_num, int32_t f32);
 int sa_tree_predict_staged(const void* snodes, int32_t n_nodes, const int32_t* roots,

@@ -263,21 +263,25 @@ __global__ __launch_bounds__(TR_THREADS) void tree_fixed_kernel(const TNode* __r
     ((double*)out)[j] = 1.0 / (1.0 + exp(-(double)m));
 }
 
-// Staged walk (the model's used feature columns of the workgroup's rows copied into LDS once,
-// then every tree walked from LDS): the gathers of tree_fixed_kernel are divergent HBM/L2
-// loads -- one per lane, level and tree, ~582 B/action for a 100-tree model, but issued as
-// scattered single-lane accesses the memory pipeline serves a few lanes at a time.  Here a
-// workgroup of 256 rows first reads the used columns of its rows with coalesced 16-B loads:
-// bool columns (515 of the 568 default features) are packed on the fly into one bit per row
-// (a column's 256 rows = 4 u64, one per wave; a level reads the wave's u64 and shifts by the
-// lane), numeric columns are converted to the model's arithmetic type into a column-major
-// slab (conflict-free lane reads).  Nodes are restaged (host-prepared, `SNode`) with the
-// feature as a compact reference: bit 30 = numeric, the rest = index into the bool or numeric
-// column list; leaves are self-loops, so every tree of a group is walked exactly the group's
-// depth (tree_fixed_kernel's fixed-depth walk).  Values, split rule and summation order equal
-// tree_fixed_kernel's bit for bit.
-constexpr int TS_ROWS = 256;  // rows (threads) per workgroup
+// Staged walk: the model's used BOOL feature columns of the workgroup's rows are copied into LDS
+// once, packed to one bit per row, and every tree is walked from LDS.  The gathers of
+// tree_fixed_kernel are divergent loads -- one per lane, level and tree, ~582 B/action for a
+// 100-tree model, served a few lanes at a time by the memory pipeline.  Here a workgroup of
+// 512 rows first reads the used bool columns of its rows with coalesced 16-B loads (515 of the
+// 568 default features are bool; a column's 512 rows become 8 u64, one per wave, and a level
+// reads the wave's u64 and shifts by the lane); the few numeric features stay gathers from the
+// f64 / i64 blocks (row bases computed once per thread).  Nodes are restaged (host-prepared,
+// `SNode`) with the feature as a compact reference: bit 30 = numeric, the rest = index into
+// the bool column list or the numeric slot list; leaves are self-loops, so every tree of a
+// group is walked exactly the group's depth (tree_fixed_kernel's fixed-depth walk).  Values,
+// split rule and summation order equal tree_fixed_kernel's bit for bit.
+constexpr int TS_ROWS = 512;              // rows (threads) per workgroup
+constexpr int TS_WAVES = TS_ROWS / 64;
+constexpr int TS_PIECES = TS_ROWS / 16;   // 16-row pieces per column
 constexpr int32_t TS_NUM = 1 << 30;
+#ifndef SA_TS_PROBE
+#define SA_TS_PROBE 0  // timing probes only (wrong results): 1 = no walk, 2 = no staging
+#endif
 
 template <typename A>
 struct SNode {
@@ -297,96 +301,53 @@ __global__ __launch_bounds__(TS_ROWS) void tree_staged_kernel(const SNode<typena
   extern __shared__ __attribute__((aligned(16))) unsigned char ts_lds[];
   SNode<A>* L = reinterpret_cast<SNode<A>*>(ts_lds);
   const size_t node_bytes = ((size_t)n_nodes * sizeof(SNode<A>) + 15) / 16 * 16;
-  const int nb = n_bool > 0 ? n_bool : 1;
-  uint16_t* M16 = reinterpret_cast<uint16_t*>(ts_lds + node_bytes);        // [nb][16] u16
-  const uint64_t* M = reinterpret_cast<const uint64_t*>(M16);              // [nb][4] u64
-  A* S = reinterpret_cast<A*>(ts_lds + node_bytes + (size_t)nb * 32);      // [nn][TS_ROWS]
+  const int nb = n_bool > 0 ? n_bool : 1, nn = n_num > 0 ? n_num : 1;
+  uint16_t* M16 = reinterpret_cast<uint16_t*>(ts_lds + node_bytes);            // [nb][TS_PIECES]
+  const uint64_t* M = reinterpret_cast<const uint64_t*>(M16);                  // [nb][TS_WAVES]
+  int32_t* NS = reinterpret_cast<int32_t*>(ts_lds + node_bytes + (size_t)nb * TS_ROWS / 8);  // [nn]
+  int32_t* BC = NS + nn;                                                       // [nb]
   const int tid = threadIdx.x;
   const int64_t R0 = (int64_t)blockIdx.x * TS_ROWS;
-  // every load of a staging pass is issued before any is used (TS_B per thread in flight):
-  // a pass is one memory latency, not TS_B of them
+  for (int k = tid; k < n_num; k += TS_ROWS) NS[k] = num_slots[k];
+  for (int k = tid; k < n_bool; k += TS_ROWS) BC[k] = bool_cols[k];
+  if (n_num == 0 && tid == 0) NS[0] = 1 << 24;
+  if (n_bool == 0 && tid < TS_PIECES) M16[tid] = 0;
+  // every load of a staging pass is issued before any is used (TS_B per thread in flight)
   constexpr int TS_B = 8;
   for (int k0 = 0; k0 < n_nodes; k0 += TS_ROWS * TS_B) {
-    SNode<A> v[TS_B];
 #pragma unroll
     for (int b = 0; b < TS_B; ++b) {
       const int k = k0 + b * TS_ROWS + tid;
-      if (k < n_nodes) v[b] = nodes[k];
-    }
-#pragma unroll
-    for (int b = 0; b < TS_B; ++b) {
-      const int k = k0 + b * TS_ROWS + tid;
-      if (k < n_nodes) L[k] = v[b];
+      if (k < n_nodes) L[k] = nodes[k];
     }
   }
-  if (n_bool == 0 && tid < 16) M16[tid] = 0;
-  if (n_num == 0) S[tid] = A(0);
-  // bool columns: item it = (column u = it / 16, 16-row piece p = it % 16): one 16-B load of
-  // the piece -> 16 bits at M16[it]
-  const int nbi = n_bool * 16;
-  for (int i0 = 0; i0 < nbi; i0 += TS_ROWS * TS_B) {
-    u32x4 w[TS_B];
+  __syncthreads();  // BC
+  if (SA_TS_PROBE != 2) {
+    // bool columns: item it = (column u = it / TS_PIECES, 16-row piece p): one 16-B load of the
+    // piece -> 16 bits at M16[it]
+    const int nbi = n_bool * TS_PIECES;
+    for (int i0 = 0; i0 < nbi; i0 += TS_ROWS * TS_B) {
+      u32x4 w[TS_B];
 #pragma unroll
-    for (int b = 0; b < TS_B; ++b) {
-      const int it = i0 + b * TS_ROWS + tid;
-      w[b] = u32x4{0, 0, 0, 0};
-      const int64_t r = R0 + 16 * (it & 15);
-      if (it < nbi && r < n) {
-        const int64_t col = bool_cols[it >> 4];
-        SA_DCHECK(col >= 0 && col < Bb.n_cols, col);
-        const int64_t t = r / Bb.tile_rows;
-        w[b] = *reinterpret_cast<const u32x4*>((const uint8_t*)Bb.data + (t * Bb.n_cols + col) * Bb.tile_rows +
-                                               (r - t * Bb.tile_rows));
-      }
-    }
-#pragma unroll
-    for (int b = 0; b < TS_B; ++b) {
-      const int it = i0 + b * TS_ROWS + tid;
-      uint32_t bits = 0;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) bits |= (((w[b][q] & 0x01010101u) * 0x01020408u) >> 24) << (4 * q);
-      if (it < nbi) M16[it] = (uint16_t)bits;
-    }
-  }
-  // numeric columns: item it = (column v = it / 128, 2-row piece p = it % 128): one 16-B load
-  // -> 2 values of type A at S[v * TS_ROWS + 2p]
-  constexpr int PP = TS_ROWS / 2;
-  const int nni = n_num * PP;
-  for (int i0 = 0; i0 < nni; i0 += TS_ROWS * TS_B) {
-    f64x2 y[TS_B];
-    bool isf[TS_B];
-#pragma unroll
-    for (int b = 0; b < TS_B; ++b) {
-      const int it = i0 + b * TS_ROWS + tid;
-      y[b] = f64x2{0.0, 0.0};
-      isf[b] = true;
-      const int v = it / PP;
-      const int64_t r = R0 + 2 * (it - v * PP);
-      if (it < nni && r < n) {
-        const int32_t slot = num_slots[v];
-        const int64_t col = slot & 0xFFFFFF;
-        isf[b] = (slot >> 24) == 1;
-        const sa_block& Bk = isf[b] ? Bf : Bi;
-        SA_DCHECK(col < Bk.n_cols, col);
-        const int64_t t = r / Bk.tile_rows;
-        y[b] = *reinterpret_cast<const f64x2*>((const char*)Bk.data +
-                                               ((t * Bk.n_cols + col) * Bk.tile_rows + (r - t * Bk.tile_rows)) * 8);
-      }
-    }
-#pragma unroll
-    for (int b = 0; b < TS_B; ++b) {
-      const int it = i0 + b * TS_ROWS + tid;
-      if (it < nni) {
-        A x0, x1;
-        if (isf[b]) {
-          x0 = (A)y[b][0];
-          x1 = (A)y[b][1];
-        } else {  // the i64 block: the same 16 bytes as two int64
-          x0 = (A)(double)__double_as_longlong(y[b][0]);
-          x1 = (A)(double)__double_as_longlong(y[b][1]);
+      for (int b = 0; b < TS_B; ++b) {
+        const int it = i0 + b * TS_ROWS + tid;
+        w[b] = u32x4{0, 0, 0, 0};
+        const int64_t r = R0 + 16 * (it % TS_PIECES);
+        if (it < nbi && r < n) {
+          const int64_t col = BC[it / TS_PIECES];
+          SA_DCHECK(col >= 0 && col < Bb.n_cols, col);
+          const int64_t t = r / Bb.tile_rows;
+          w[b] = *reinterpret_cast<const u32x4*>((const uint8_t*)Bb.data + (t * Bb.n_cols + col) * Bb.tile_rows +
+                                                 (r - t * Bb.tile_rows));
         }
-        S[it * 2] = x0;  // v * TS_ROWS + 2p == 2 * it
-        S[it * 2 + 1] = x1;
+      }
+#pragma unroll
+      for (int b = 0; b < TS_B; ++b) {
+        const int it = i0 + b * TS_ROWS + tid;
+        uint32_t bits = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) bits |= (((w[b][q] & 0x01010101u) * 0x01020408u) >> 24) << (4 * q);
+        if (it < nbi) M16[it] = (uint16_t)bits;
       }
     }
   }
@@ -394,8 +355,9 @@ __global__ __launch_bounds__(TS_ROWS) void tree_staged_kernel(const SNode<typena
   const int64_t j = R0 + tid;
   if (j >= n) return;
   const int wv = tid >> 6, lane = tid & 63;
+  const RowBases rb = row_bases(Bb, Bf, Bi, j);
   A m = (A)base;
-  for (int t0 = 0; t0 < n_trees; t0 += TG) {
+  for (int t0 = 0; t0 < (SA_TS_PROBE == 1 ? 0 : n_trees); t0 += TG) {
     int k[TG];
     int D = 0;
 #pragma unroll
@@ -405,17 +367,25 @@ __global__ __launch_bounds__(TS_ROWS) void tree_staged_kernel(const SNode<typena
       D = max(D, depth[t]);
     }
     for (int d = 0; d < D; ++d) {
+      // the TG trees' node reads, then all their feature reads (the numeric gathers of the
+      // lanes that need one go out together: one memory latency per level, not TG), then the
+      // decisions
+      SNode<A> nd[TG];
+#pragma unroll
+      for (int u = 0; u < TG; ++u) nd[u] = L[k[u]];
+      A v[TG];
 #pragma unroll
       for (int u = 0; u < TG; ++u) {
-        const SNode<A> nd = L[k[u]];
-        const bool num = (nd.ref & TS_NUM) != 0;
-        const int idx = nd.ref & (TS_NUM - 1);
-        SA_DCHECK(num ? idx < (n_num > 0 ? n_num : 1) : idx < nb, nd.ref);
-        const uint64_t mk = M[(num ? 0 : idx) * 4 + wv];
-        const A vn = S[(num ? idx : 0) * TS_ROWS + tid];
-        const A v = num ? vn : (A)((mk >> lane) & 1ull);
-        const bool left = isnan(v) ? nd.right < 0 : (LE ? v <= nd.thr : v < nd.thr);
-        k[u] = left ? nd.left : (nd.right & 0x7FFFFFFF);
+        const int idx = nd[u].ref & (TS_NUM - 1);
+        SA_DCHECK((nd[u].ref & TS_NUM) ? idx < nn : idx < nb, nd[u].ref);
+        if (nd[u].ref & TS_NUM) v[u] = (A)feature_value(rb, NS[idx]);
+      }
+#pragma unroll
+      for (int u = 0; u < TG; ++u) {
+        const int idx = nd[u].ref & (TS_NUM - 1);
+        if (!(nd[u].ref & TS_NUM)) v[u] = (A)((M[idx * TS_WAVES + wv] >> lane) & 1ull);
+        const bool left = isnan(v[u]) ? nd[u].right < 0 : (LE ? v[u] <= nd[u].thr : v[u] < nd[u].thr);
+        k[u] = left ? nd[u].left : (nd[u].right & 0x7FFFFFFF);
       }
     }
 #pragma unroll
@@ -482,7 +452,7 @@ extern "C" int sa_tree_predict(const void* nodes, int32_t n_nodes, const int32_t
 extern "C" int64_t sa_tree_staged_lds_bytes(int32_t n_nodes, int32_t n_bool, int32_t n_num, int32_t f32) {
   const size_t node = f32 ? sizeof(SNode<float>) : sizeof(SNode<double>);
   const size_t nb = n_bool > 0 ? n_bool : 1, nn = n_num > 0 ? n_num : 1;
-  return (int64_t)(((size_t)n_nodes * node + 15) / 16 * 16 + nb * 32 + nn * TS_ROWS * (f32 ? 4 : 8));
+  return (int64_t)(((size_t)n_nodes * node + 15) / 16 * 16 + nb * TS_ROWS / 8 + (nn + nb) * 4);
 }
 
 extern "C" int sa_tree_predict_staged(const void* snodes, int32_t n_nodes, const int32_t* roots,
@@ -500,9 +470,6 @@ extern "C" int sa_tree_predict_staged(const void* snodes, int32_t n_nodes, const
   const sa_block Bb = bool_blk ? *bool_blk : z, Bf = f64_blk ? *f64_blk : z, Bi = i64_blk ? *i64_blk : z;
   if (n_bool > 0 && (Bb.tile_rows % 16 != 0 || !aligned16(Bb.data)))
     return fail(SA_EINVAL, "bool block: 16-row tiles, 16-byte aligned");
-  if ((Bf.data && (Bf.tile_rows % 2 != 0 || !aligned16(Bf.data))) ||
-      (Bi.data && (Bi.tile_rows % 2 != 0 || !aligned16(Bi.data))))
-    return fail(SA_EINVAL, "numeric blocks: even tiles, 16-byte aligned");
   if (n == 0) return SA_OK;
   const dim3 grid((unsigned)((n + TS_ROWS - 1) / TS_ROWS)), block(TS_ROWS);
   hipStream_t st = (hipStream_t)stream;

@@ -17,9 +17,6 @@
 #include "sa_common.h"
 #include "sa_internal.h"
 
-#ifndef SA_XT_SOLVE_REG
-#define SA_XT_SOLVE_REG 1  // C <= 192: xt_solve_reg_kernel (0: xt_solve_small_kernel, A/B)
-#endif
 #ifndef SA_XT_WIDE
 #define SA_XT_WIDE 1  // C <= 197: XC_WIDE count pass (0: the 32k-action XC_SMALL workgroups)
 #endif
@@ -297,9 +294,8 @@ __global__ __launch_bounds__(256) void xt_transpose_kernel(const int32_t* __rest
   }
 }
 
-// One value-iteration step for C rows; row r = one lane, sequential sum over c.  (Issuing the
-// T loads 16 columns ahead of the adds measured no faster at C = 192: ~5.6 us per iteration
-// either way, the strictly ordered f64 add chain of 3 waves is the limiter.)
+// One value-iteration step for C rows; row r = one lane, sequential sum over c in runs of 8
+// loads (~5.4 us per iteration at C = 192; see xt_solve_small_kernel for what was tried).
 __device__ __forceinline__ double row_payoff(const double* __restrict__ Tt, const double* __restrict__ x,
                                              int C, int r) {
   double acc = 0.0;
@@ -321,111 +317,23 @@ __device__ __forceinline__ double row_payoff(const double* __restrict__ Tt, cons
   return acc;
 }
 
-// Small grids: one persistent workgroup runs every iteration; x lives in LDS.
 constexpr int XT_SOLVE_MAX_C = 1024;
-// Value iteration of grids up to 192 cells (16 x 12) in one persistent workgroup of 1024
-// threads that keeps the whole exact transposed transition matrix Tt (trans_t, f64: one
-// correctly rounded division cnt / move[s] per element, formed once by xt_transpose_kernel) in
-// REGISTERS for every iteration: element q = c * C + r of the C * C <= 36,864 lives in thread
-// q % 1024, slot q / 1024 (36 doubles = 72 VGPRs per thread; the CU's register file holds the
-// 295 KB matrix, which LDS could not).  Per iteration the elements go by in 6 chunks of 6 slots:
-// every thread multiplies its 6 elements by x[c] into a double-buffered LDS slab (48 KB), one
-// barrier, and the C row lanes add the chunk's products of their row to their sums strictly
-// left to right in column order (xthreat.py:306-312) while the next chunk is formed.  Nothing
-// is read from L2 / HBM after the first load, so the solve no longer slows down when it shares
-// the chip with the streaming VAEP kernels (xt_solve_small_kernel re-reads Tt from L2 every
-// iteration).
-constexpr int XR_THREADS = 512;
-constexpr int XR_K = 72;        // matrix elements per thread
-constexpr int XR_CK = 12;        // elements per thread per chunk
-constexpr int XR_NCH = XR_K / XR_CK;
-constexpr int XR_CHUNK = XR_THREADS * XR_CK;  // elements per chunk
-constexpr int XR_MAX_C = 192;   // C * C <= XR_THREADS * XR_K
 
-__global__ __launch_bounds__(XR_THREADS) void xt_solve_reg_kernel(const double* __restrict__ Tt,
-                                                                  const double* __restrict__ gs,
-                                                                  const double* __restrict__ pmove, int C,
-                                                                  double eps, int max_iter,
-                                                                  double* __restrict__ heat,
-                                                                  double* __restrict__ xT_out,
-                                                                  int32_t* __restrict__ n_iter) {
-  __shared__ double xs[XR_MAX_C];
-  __shared__ double buf[2][XR_CHUNK];
-  const int tid = threadIdx.x;
-  const int CC = C * C;
-  const int kmax = CC > tid ? (CC - tid + XR_THREADS - 1) / XR_THREADS : 0;  // slots in use
-  double tv[XR_K];
-#pragma unroll
-  for (int k = 0; k < XR_K; ++k) tv[k] = k < kmax ? Tt[tid + XR_THREADS * k] : 0.0;
-  // column of slot k: c_k = (tid + 1024 k) / C, stepped incrementally
-  const int ca = XR_THREADS / C, cb = XR_THREADS - ca * C;
-  const int c0 = tid / C, r0 = tid - c0 * C;
-  const int r = tid;
-  const bool chain = r < C;
-  double g = 0.0, pm = 0.0;
-  if (chain) {
-    xs[r] = 0.0;
-    heat[r] = 0.0;
-    g = gs[r];
-    pm = pmove[r];
-  }
-  __syncthreads();
-  int it = 0;
-  bool cont = true;
-  while (cont && it < max_iter) {
-    double acc = 0.0;
-    int c = c0, rr = r0;  // column / row of slot k
-#pragma unroll
-    for (int j = 0; j < XR_NCH; ++j) {
-      double* b = buf[j & 1];
-#pragma unroll
-      for (int u = 0; u < XR_CK; ++u) {
-        if (j * XR_CK + u < kmax) b[tid + XR_THREADS * u] = tv[j * XR_CK + u] * xs[c];
-        c += ca;
-        rr += cb;
-        if (rr >= C) {
-          rr -= C;
-          ++c;
-        }
-      }
-      __syncthreads();
-      if (chain) {
-        // this chunk holds elements [j * XR_CHUNK, (j + 1) * XR_CHUNK): columns c with
-        // j * XR_CHUNK <= c * C + r < (j + 1) * XR_CHUNK, in order
-        const int lo = j * XR_CHUNK, hi = lo + XR_CHUNK;
-        int cs = lo - r <= 0 ? 0 : (lo - r + C - 1) / C;
-        int ce = (hi - r + C - 1) / C;
-        if (ce > C) ce = C;
-        for (int cc = cs; cc < ce; ++cc) acc = acc + b[cc * C + r - lo];
-      }
-    }
-    double nx = 0.0;
-    int flag = 0;
-    if (chain) {
-      const double mvv = pm * acc;
-      nx = g + mvv;
-      const double diff = nx - xs[r];
-      flag = diff > eps;  // np.any(diff > eps): NaN compares False
-      heat[(int64_t)(it + 1) * C + r] = nx;
-    }
-    cont = __syncthreads_or(flag);
-    if (chain) xs[r] = nx;
-    __syncthreads();
-    ++it;
-  }
-  if (chain) xT_out[r] = xs[r];
-  if (r == 0) *n_iter = cont ? -1 : it;
-}
-
-// Grids up to XT_SOLVE_MAX_C cells whose counts do not fit LDS: the same iteration over the
-// normalised, transposed f64 matrix Tt read from global memory (L2-resident).
+// Small grids (C <= XT_SOLVE_MAX_C, e.g. 16 x 12): one persistent workgroup runs every
+// iteration, row r = one lane, x in LDS; Tt is the exact transposed matrix of
+// xt_transpose_kernel (L2-resident).  Measured at C = 192 (scripts/xt_solve_time.py, isolated,
+// 26 iterations incl. normalisation and the host sync): runs of 8 loads 0.181 ms; 32 / 64
+// columns software-pipelined ahead 0.347 / 0.367 ms (more registers, fewer resident waves); all
+// 16 waves streaming Tt through LDS 0.453 ms; the counts in LDS with one division per element
+// 0.469 ms; the whole matrix in the registers of 512 threads 0.343 ms (and it waits for a whole
+// idle CU next to the VAEP kernels: 1.49 ms in the step).
 __global__ __launch_bounds__(1024) void xt_solve_small_kernel(const double* __restrict__ Tt,
-                                                              const double* __restrict__ gs,
-                                                              const double* __restrict__ pmove, int C,
-                                                              double eps, int max_iter,
-                                                              double* __restrict__ heat,
-                                                              double* __restrict__ xT_out,
-                                                              int32_t* __restrict__ n_iter) {
+                                                                 const double* __restrict__ gs,
+                                                                 const double* __restrict__ pmove, int C,
+                                                                 double eps, int max_iter,
+                                                                 double* __restrict__ heat,
+                                                                 double* __restrict__ xT_out,
+                                                                 int32_t* __restrict__ n_iter) {
   __shared__ double xs[XT_SOLVE_MAX_C];
   const int r = threadIdx.x;
   if (r < C) {
@@ -881,15 +789,9 @@ extern "C" int sa_xt_solve(const int64_t* shot, const int64_t* goal, const int64
   hipLaunchKernelGGL(xt_transpose_kernel, tgrid, dim3(256), 0, st, trans, um, C, trans_t);
   rc = check_launch("xt normalise");
   if (!rc && C <= XT_SOLVE_MAX_C) {
-    if (SA_XT_SOLVE_REG && C <= XR_MAX_C) {
-      hipLaunchKernelGGL(xt_solve_reg_kernel, dim3(1), dim3(XR_THREADS), 0, st, trans_t, gs, pm, C, eps,
-                         max_iter, heatmaps, mats + 3 * C, dn);
-      rc = check_launch("xt_solve_reg_kernel");
-    } else {
-      hipLaunchKernelGGL(xt_solve_small_kernel, dim3(1), dim3(((C + 63) / 64) * 64), 0, st, trans_t, gs,
-                         pm, C, eps, max_iter, heatmaps, mats + 3 * C, dn);
-      rc = check_launch("xt_solve_small_kernel");
-    }
+    hipLaunchKernelGGL(xt_solve_small_kernel, dim3(1), dim3(((C + 63) / 64) * 64), 0, st, trans_t, gs, pm, C, eps,
+                       max_iter, heatmaps, mats + 3 * C, dn);
+    rc = check_launch("xt_solve_small_kernel");
     if (!rc) rc = check_hip(hipMemcpyAsync(&iters, dn, sizeof(int32_t), hipMemcpyDeviceToHost, st),
                             "copy n_iter");
     if (!rc) rc = check_hip(hipStreamSynchronize(st), "hipStreamSynchronize");
