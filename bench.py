@@ -52,7 +52,7 @@ FUSED_CALLS = {'labels_formula': ('labels', 'formula')}
 KERNEL_NAMES = {'bool_features': 'bool_colgroup_kernel', 'num_features': 'num_features_kernel',
                 'goalscore': 'goalscore_wave16_kernel', 'labels': 'labels_kernel',
                 'formula': 'formula_kernel', 'labels_formula': 'labels_formula_kernel',
-                'xt_fit_rate': 'xt_count_kernel + xt_solve_reg_kernel + xt_rate_cells_kernel'}
+                'xt_fit_rate': 'xt_count_kernel + xt_solve_small_kernel + xt_rate_cells_kernel'}
 
 
 def step_bytes(xt_source: str) -> dict:

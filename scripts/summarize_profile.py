@@ -3,7 +3,8 @@
     python scripts/summarize_profile.py r01 [N_ACTIONS]
 
 Reads gpurun_out/prof_<tag>_{trace,fetch,write}/ (see scripts/profile_round.sh) and writes
-  profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary
+  profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary of the step alone
+  profiles/<tag>_side_kernel_stats.csv   the same with bench.py's side entries
   profiles/<tag>_pmc.csv            per-kernel mean FETCH_SIZE / WRITE_SIZE (KiB) + HBM bytes
   profiles/pmc_dominant_kernel.json HBM bytes per action of the dominant kernel (read by bench.py)
 HBM bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024: on gfx950 FETCH_SIZE reports half the
@@ -25,6 +26,9 @@ def main(tag: str, n_actions: int, dominant: str = 'bool_colgroup_kernel') -> No
     src = os.path.join(ROOT, 'gpurun_out')
     shutil.copy(os.path.join(src, f'prof_{tag}_trace', 'run_kernel_stats.csv'),
                 os.path.join(out, f'{tag}_kernel_stats.csv'))
+    side = os.path.join(src, f'prof_{tag}_side', 'run_kernel_stats.csv')
+    if os.path.exists(side):
+        shutil.copy(side, os.path.join(out, f'{tag}_side_kernel_stats.csv'))
     rows = {}
     for kind in ('fetch', 'write'):
         p = os.path.join(src, f'prof_{tag}_{kind}', 'run_counter_collection.csv')

@@ -147,45 +147,11 @@ __global__ __launch_bounds__(TR_THREADS) void tree_predict_kernel(const TNode* _
 // the divergent while-loop above, whose exec-mask juggling cost as many scalar as vector
 // instructions.  Nodes are restaged with the feature slot in the node (one LDS read per level
 // instead of two dependent ones) and the threshold in the model's arithmetic type.
-// SA_TREE_UNIFIED: the node holds its feature's byte offset from the action's row base, with
-// the block kind in bits 62-63, so every level is ONE 8-B load whatever the lanes' kinds (the
-// bool byte is extracted from its aligned word; block sizes are multiples of 16 B) instead of
-// up to three predicated loads and a 64-bit multiply per kind.
-#ifndef SA_TREE_UNIFIED
-#define SA_TREE_UNIFIED 0  // A/B (profiles/r01k_tree_gather_ab.log): 1 = +10 %, 2 = equal
-#endif
 template <typename A>
 struct LNode {
   A thr;  // threshold (or the leaf value)
   int32_t slot, left, right;  // right: bit 31 = default_left
-#if SA_TREE_UNIFIED
-  int64_t boff;  // kind << 62 | byte offset of the feature from the row base of its block
-#endif
 };
-
-__device__ __forceinline__ int64_t node_boff(int32_t slot, const sa_block& Bb, const sa_block& Bf,
-                                             const sa_block& Bi) {
-  const int64_t kind = slot >> 24, col = slot & 0xFFFFFF;
-  const int64_t off = kind == 0 ? col * Bb.tile_rows : (kind == 1 ? col * Bf.tile_rows : col * Bi.tile_rows) * 8;
-  return off | (kind << 62);
-}
-
-__device__ __forceinline__ double feature_value_unified(const RowBases& r, int64_t boff) {
-  const int kind = (int)((uint64_t)boff >> 62);
-#if SA_TREE_UNIFIED == 2  // precomputed offsets, one load per kind present in the wave
-  const int64_t off = boff & 0x3FFFFFFFFFFFFFFFll;
-  if (kind == 0) return (double)*((const uint8_t*)r.b + off);
-  if (kind == 1) return *(const double*)((const char*)r.f + off);
-  return (double)*(const int64_t*)((const char*)r.i + off);
-#endif
-  const char* base = kind == 0 ? (const char*)r.b : (kind == 1 ? (const char*)r.f : (const char*)r.i);
-  const uintptr_t a = (uintptr_t)(base + (boff & 0x3FFFFFFFFFFFFFFFll));
-  const uint64_t w = *reinterpret_cast<const uint64_t*>(a & ~(uintptr_t)7);
-  const double vb = (double)(uint32_t)((w >> ((a & 7) * 8)) & 0xFF);
-  const double vf = __longlong_as_double((long long)w);
-  const double vi = (double)(int64_t)w;
-  return kind == 0 ? vb : (kind == 1 ? vf : vi);
-}
 
 template <bool F32, bool LE>
 __global__ __launch_bounds__(TR_THREADS) void tree_fixed_kernel(const TNode* __restrict__ nodes, int n_nodes,
@@ -221,9 +187,6 @@ __global__ __launch_bounds__(TR_THREADS) void tree_fixed_kernel(const TNode* __r
       o.left = nd.left;
       o.right = nd.right;
     }
-#if SA_TREE_UNIFIED
-    o.boff = node_boff(o.slot, Bb, Bf, Bi);
-#endif
     L[k] = o;
   }
   __syncthreads();
@@ -244,11 +207,7 @@ __global__ __launch_bounds__(TR_THREADS) void tree_fixed_kernel(const TNode* __r
 #pragma unroll
       for (int u = 0; u < TG; ++u) {
         const LNode<A> nd = L[k[u]];
-#if SA_TREE_UNIFIED
-        const A v = (A)feature_value_unified(rb, nd.boff);
-#else
         const A v = (A)feature_value(rb, nd.slot);
-#endif
         const bool left = isnan(v) ? nd.right < 0 : (LE ? v <= nd.thr : v < nd.thr);
         k[u] = left ? nd.left : (nd.right & 0x7FFFFFFF);
       }
@@ -279,9 +238,6 @@ constexpr int TS_ROWS = 512;              // rows (threads) per workgroup
 constexpr int TS_WAVES = TS_ROWS / 64;
 constexpr int TS_PIECES = TS_ROWS / 16;   // 16-row pieces per column
 constexpr int32_t TS_NUM = 1 << 30;
-#ifndef SA_TS_PROBE
-#define SA_TS_PROBE 0  // timing probes only (wrong results): 1 = no walk, 2 = no staging
-#endif
 
 template <typename A>
 struct SNode {
@@ -322,7 +278,7 @@ __global__ __launch_bounds__(TS_ROWS) void tree_staged_kernel(const SNode<typena
     }
   }
   __syncthreads();  // BC
-  if (SA_TS_PROBE != 2) {
+  {
     // bool columns: item it = (column u = it / TS_PIECES, 16-row piece p): one 16-B load of the
     // piece -> 16 bits at M16[it]
     const int nbi = n_bool * TS_PIECES;
@@ -357,7 +313,7 @@ __global__ __launch_bounds__(TS_ROWS) void tree_staged_kernel(const SNode<typena
   const int wv = tid >> 6, lane = tid & 63;
   const RowBases rb = row_bases(Bb, Bf, Bi, j);
   A m = (A)base;
-  for (int t0 = 0; t0 < (SA_TS_PROBE == 1 ? 0 : n_trees); t0 += TG) {
+  for (int t0 = 0; t0 < n_trees; t0 += TG) {
     int k[TG];
     int D = 0;
 #pragma unroll
