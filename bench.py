@@ -52,7 +52,7 @@ FUSED_CALLS = {'labels_formula': ('labels', 'formula')}
 KERNEL_NAMES = {'bool_features': 'bool_colgroup_kernel', 'num_features': 'num_features_kernel',
                 'goalscore': 'goalscore_wave16_kernel', 'labels': 'labels_kernel',
                 'formula': 'formula_kernel', 'labels_formula': 'labels_formula_kernel',
-                'xt_fit_rate': 'xt_count_kernel + xt_solve_small_kernel + xt_rate_cells_kernel'}
+                'xt_fit_rate': 'xt_count_kernel + xt_solve_reg_kernel + xt_rate_cells_kernel'}
 
 
 def step_bytes(xt_source: str) -> dict:
@@ -427,7 +427,10 @@ def main() -> None:
                          '"codes": the count pass writes 4-B rate operands for the rate)')
     ap.add_argument('--ab', default='',
                     help='dev tool: ";"-separated step variants "name:key=value/..." (keys xt, '
-                         'order with "+", fork) timed round-robin in one process')
+                         'order with "+", fork, prio) timed round-robin in one process')
+    ap.add_argument('--side-priority', default='high', choices=('normal', 'high'),
+                    help='priority of the xT side stream (high: 3.227 - 3.232 vs 3.230 - 3.246 '
+                         'ms per step in-process, profiles/r02_step_ab.md)')
     ap.add_argument('--num-tile', type=int, default=128,
                     help='rows per f64/i64-block tile (0 = one tile: plain column-major)')
     args = ap.parse_args()
@@ -470,14 +473,18 @@ def main() -> None:
     s_act = ab.struct()
     cells = ops.xt_cells_buffer(n, dev)
     main_s = torch.cuda.current_stream()
-    side = torch.cuda.Stream() if not args.serial else main_s
-    overlap = side is not main_s
+    overlap = not args.serial
+    # the xT side stream; --side-priority high: a high-priority HIP stream, so its few
+    # workgroups are dispatched ahead of the VAEP kernels' as CUs free up
+    sides = {p: (torch.cuda.Stream(priority=-1 if p == 'high' else 0) if overlap else main_s)
+             for p in ('normal', 'high')}
 
     def make_step(spec):
         """One step of the given variant: the VAEP kernels in `order` on the main stream; the xT
         fit + rate on a side stream forked before VAEP call `fork` (after num_features at the
         latest when the feature pass writes the xT cell codes), joined at the end."""
         xt, order, fork = spec['xt'], spec['order'], spec['fork']
+        side = sides[spec['prio']]
         covered = sorted(c for k in order for c in FUSED_CALLS.get(k, (k,)))
         if covered != sorted(STEP_CALLS):
             raise SystemExit(f'order must cover {",".join(STEP_CALLS)} once each '
@@ -528,7 +535,8 @@ def main() -> None:
                 main_s.wait_event(join)
         return step, xt_last
 
-    base = {'xt': args.xt_source, 'order': args.order.split(','), 'fork': args.xt_fork}
+    base = {'xt': args.xt_source, 'order': args.order.split(','), 'fork': args.xt_fork,
+            'prio': args.side_priority}
     if base['fork'] < 0:  # default: before the first VAEP call, or right after num_features
         base['fork'] = (base['order'].index('num_features') + 1) if args.xt_source == 'cells' else 0
     if args.ab:  # in-process A/B of step variants on the same allocations (dev tool)
@@ -645,8 +653,8 @@ def main() -> None:
                                   'codes': 'coordinates (count) + rate operands',
                                   'coords': 'coordinates'}[base['xt']],
                        'stream': 'main (serial)' if args.serial else
-                       f"side stream, forked after {base['fork']} VAEP call(s), overlapped "
-                       'with the rest'}
+                       f"{base['prio']}-priority side stream, forked after {base['fork']} VAEP "
+                       'call(s), overlapped with the rest'}
     line['vaep_order'] = order
     line['streams'] = ('one stream' if args.serial else
                        'VAEP kernels on the main stream, xT on a side stream')

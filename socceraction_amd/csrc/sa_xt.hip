@@ -363,6 +363,81 @@ __global__ __launch_bounds__(1024) void xt_solve_small_kernel(const double* __re
   if (r == 0) *n_iter = cont ? -1 : it;
 }
 
+// Grids up to 16 x 12 (C <= XR_MAX_C = 192, the default grid): the transition matrix lives in
+// registers for all iterations.  Each row is split into H parts of 192 / H columns; lane (row r,
+// part h) holds T[r][h*192/H .. (h+1)*192/H) (loaded once from the exact transposed matrix;
+// columns >= C and rows >= C hold +0), so a wave covers 64 / H rows.  Per iteration the part-0
+// lanes run the first terms of the row's sequential sum, hand the partial sum to their part-1
+// lane (a wave shuffle), which continues, and so on: the reference's left-to-right order
+// (xthreat.py:306-312), each product rounded before its add (-ffp-contract=off).  Padded terms
+// are +0 * +0 = +0 and leave the (non-negative) running sum unchanged, so any C <= 192 runs the
+// same 192 steps.  x is double-buffered in LDS; one barrier (which also ORs the convergence
+// flags) per iteration.  Nothing is read from memory after the first iteration's loads.
+// SA_XR_PARTS = H: 2 (default, 96 doubles per lane, 224 VGPRs, no spills): 71 us for 26
+// iterations (rocprofv3), 0.110 ms incl. normalisation + host sync; H = 1 (192 doubles, 256
+// VGPRs + 150 AGPRs) 0.144 ms, H = 4 0.134 ms (profiles/r02_step_ab.md).
+constexpr int XR_MAX_C = 192;
+#ifndef SA_XR_PARTS
+#define SA_XR_PARTS 2
+#endif
+
+template <int H>
+__global__ __launch_bounds__(H * XR_MAX_C) void xt_solve_reg_kernel(const double* __restrict__ Tt,
+                                                                    const double* __restrict__ gs,
+                                                                    const double* __restrict__ pmove, int C,
+                                                                    double eps, int max_iter,
+                                                                    double* __restrict__ heat,
+                                                                    double* __restrict__ xT_out,
+                                                                    int32_t* __restrict__ n_iter) {
+  static_assert(H == 1 || H == 2 || H == 4, "parts per row");
+  constexpr int NP = XR_MAX_C / H, RW = 64 / H;  // columns per part, rows per wave
+  __shared__ __attribute__((aligned(16))) double xs[2][XR_MAX_C];
+  const int lane = threadIdx.x & 63;
+  const int h = lane / RW;
+  const int r = (int)(threadIdx.x >> 6) * RW + lane % RW;
+  const bool own = h == H - 1 && r < C;  // the lane that finishes row r
+  double t[NP];
+#pragma unroll
+  for (int k = 0; k < NP; ++k) {
+    const int c = h * NP + k;
+    t[k] = (r < C && c < C) ? Tt[(int64_t)c * C + r] : 0.0;
+  }
+  const double g = own ? gs[r] : 0.0, pm = own ? pmove[r] : 0.0;
+  for (int c = threadIdx.x; c < 2 * XR_MAX_C; c += blockDim.x) (&xs[0][0])[c] = 0.0;
+  if (own) heat[r] = 0.0;
+  __syncthreads();
+  int it = 0;
+  bool cont = true;
+  while (cont && it < max_iter) {
+    const double* __restrict__ x = xs[it & 1] + h * NP;
+    double acc = 0.0;
+#pragma unroll
+    for (int q = 0; q < H; ++q) {
+      if (h == q) {
+#pragma unroll
+        for (int k = 0; k < NP; ++k) {
+          const double p = t[k] * x[k];
+          acc = acc + p;
+        }
+      }
+      if (q + 1 < H) acc = __shfl(acc, q * RW + lane % RW);  // part q+1 continues part q's sum
+    }
+    int flag = 0;
+    if (own) {
+      const double mv = pm * acc;
+      const double nx = g + mv;
+      const double diff = nx - xs[it & 1][r];
+      flag = diff > eps;  // np.any(diff > eps): NaN compares False
+      heat[(int64_t)(it + 1) * C + r] = nx;
+      xs[(it + 1) & 1][r] = nx;
+    }
+    cont = __syncthreads_or(flag);
+    ++it;
+  }
+  if (own) xT_out[r] = xs[it & 1][r];
+  if (threadIdx.x == 0) *n_iter = cont ? -1 : it;
+}
+
 // Large grids (C > XT_SOLVE_MAX_C, e.g. 105 x 68 = 7140 cells): one launch per iteration.
 // The dense transition matrix is never materialised for the iteration: a workgroup owns
 // XI_ROWS rows r and streams their int32 count rows trans[r*C + c] (4 B per element instead
@@ -789,9 +864,15 @@ extern "C" int sa_xt_solve(const int64_t* shot, const int64_t* goal, const int64
   hipLaunchKernelGGL(xt_transpose_kernel, tgrid, dim3(256), 0, st, trans, um, C, trans_t);
   rc = check_launch("xt normalise");
   if (!rc && C <= XT_SOLVE_MAX_C) {
-    hipLaunchKernelGGL(xt_solve_small_kernel, dim3(1), dim3(((C + 63) / 64) * 64), 0, st, trans_t, gs, pm, C, eps,
-                       max_iter, heatmaps, mats + 3 * C, dn);
-    rc = check_launch("xt_solve_small_kernel");
+    if (C <= XR_MAX_C) {
+      hipLaunchKernelGGL(xt_solve_reg_kernel<SA_XR_PARTS>, dim3(1), dim3(SA_XR_PARTS * XR_MAX_C), 0, st, trans_t, gs, pm, C, eps,
+                         max_iter, heatmaps, mats + 3 * C, dn);
+      rc = check_launch("xt_solve_reg_kernel");
+    } else {
+      hipLaunchKernelGGL(xt_solve_small_kernel, dim3(1), dim3(((C + 63) / 64) * 64), 0, st, trans_t, gs, pm, C,
+                         eps, max_iter, heatmaps, mats + 3 * C, dn);
+      rc = check_launch("xt_solve_small_kernel");
+    }
     if (!rc) rc = check_hip(hipMemcpyAsync(&iters, dn, sizeof(int32_t), hipMemcpyDeviceToHost, st),
                             "copy n_iter");
     if (!rc) rc = check_hip(hipStreamSynchronize(st), "hipStreamSynchronize");
