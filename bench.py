@@ -290,10 +290,13 @@ def rate_extra(ab, out, n, dev, reps: int = 5) -> dict:
     pc = models[1].predict_blocks(out)
     val = torch.empty((3, (n + 15) // 16 * 16), dtype=torch.float32, device=dev)
     ms_tree = _events_ms(lambda: models[0].predict_blocks(out, out=ps), reps)
+    ms_gather = _events_ms(lambda: models[0].predict_blocks(out, out=ps, method='gather'), reps)
     ms_formula = _events_ms(lambda: ops.formula(ab, ps, pc, val), reps)
     return {'workload': 'VAEP.rate on device: 2 x xgboost-shaped tree ensembles (100 trees, depth '
                         '3) on the cfg2 feature blocks + formula (float32 probabilities)',
-            'ms_per_model': round(ms_tree, 4), 'ms_formula_f32': round(ms_formula, 4),
+            'method': 'staged condition walk (sa_tree_predict_staged)',
+            'ms_per_model': round(ms_tree, 4), 'ms_per_model_gather_walk': round(ms_gather, 4),
+            'ms_formula_f32': round(ms_formula, 4),
             'actions_per_s_predict_both_models': round(n / (2 * ms_tree) * 1e3, 1)}
 
 

@@ -404,21 +404,36 @@ int sa_tree_predict(const void* nodes, int32_t n_nodes, const int32_t* roots, co
                     const sa_block* bool_blk, const sa_block* f64_blk, const sa_block* i64_blk, int64_t n,
                     double base_margin, int32_t le, int32_t f32, void* p_out, void* stream);
 
-/* sa_tree_predict with the model's used bool feature columns staged in LDS per workgroup of
- * 512 rows (coalesced reads, packed to one bit per row; numeric features stay gathers) and every
- * tree walked a fixed number of levels.  snodes: n_nodes records { T threshold_or_leaf_value;
- * int32 ref; int32 left; int32 right | (default_left << 31); } with T = float (f32 = 1, 16 B)
- * or double (24 B incl. padding); leaves are self-loops (left = right = the leaf).  ref = index
- * into bool_cols (bool block columns) or (1 << 30) | index into num_slots ((kind << 24) |
- * column, kind 1 = f64 block, 2 = i64 block).  tree_depth is required.  Same probabilities as
- * sa_tree_predict bit for bit.  sa_tree_staged_lds_bytes: the LDS a model needs (<= 160 KiB). */
-int64_t sa_tree_staged_lds_bytes(int32_t n_nodes, int32_t n_bool, int32_t n_num, int32_t f32);
-int sa_tree_predict_staged(const void* snodes, int32_t n_nodes, const int32_t* roots,
-                           const int32_t* tree_depth, int32_t n_trees, const int32_t* bool_cols,
-                           int32_t n_bool, const int32_t* num_slots, int32_t n_num,
+/* sa_tree_predict with every split turned into a condition bit staged in LDS per workgroup of
+ * 512 rows, then a branch-free fixed-depth walk (the same probabilities as sa_tree_predict bit
+ * for bit).  Conditions: 0 = never set (constant splits); 1 .. n_bool = bool block column
+ * bool_cols[i - 1] is set; 1 + n_bool + c = numeric condition c: the value of the numeric
+ * column q with col_start[q] <= c < col_start[q + 1] (num_cols[q] = (kind << 24) | column, kind
+ * 1 = f64 block, 2 = i64 block; n_ncol distinct columns, col_start[0] = 0, col_start[n_ncol] =
+ * n_num) goes right of num_thr[c] (T; `x <= thr` goes left for le = 1, `x < thr` for le = 0;
+ * NaN goes left iff num_dl[c]); 1 + n_bool + n_num <= 65536.  model: nodes, n_nodes (< 65536)
+ * uint32 { condition | first child << 16 }: a split's children are adjacent and a row takes
+ * first child + its condition bit; leaves are self-loops (condition 0, first child = the leaf);
+ * leaf: T[n_nodes] leaf values; roots[n_trees]: each tree's root; tree_depth[n_trees]: split
+ * levels of each tree; p_out[n]: the probabilities.  T = float for f32 = 1 (xgboost), else
+ * double.  sa_tree_staged_lds_bytes: the LDS a model needs (<= 160 KiB; n_cond = 1 + n_bool +
+ * n_num). */
+typedef struct sa_tree_model {
+  const void* nodes;
+  const void* leaf;
+  const int32_t* roots;
+  const int32_t* tree_depth;
+  int32_t n_nodes;
+  int32_t n_trees;
+  double base_margin;
+  void* p_out;
+} sa_tree_model;
+int64_t sa_tree_staged_lds_bytes(int32_t n_nodes, int32_t n_cond, int32_t f32);
+int sa_tree_predict_staged(const sa_tree_model* model, const int32_t* bool_cols, int32_t n_bool,
+                           const int32_t* num_cols, const int32_t* col_start, int32_t n_ncol,
+                           const void* num_thr, const int32_t* num_dl, int32_t n_num,
                            const sa_block* bool_blk, const sa_block* f64_blk, const sa_block* i64_blk,
-                           int64_t n, double base_margin, int32_t le, int32_t f32, void* p_out,
-                           void* stream);
+                           int64_t n, int32_t le, int32_t f32, void* stream);
 
 /* ---- runtime ------------------------------------------------------------------ */
 int sa_abi_version(void);

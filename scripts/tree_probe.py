@@ -44,16 +44,18 @@ def main():
     te = trees.TreeEnsemble.from_xgboost_json(trees.synthetic_xgboost_json(
         len(kinds), n_trees=100, depth=3, seed=1, feature_kinds=kinds))
     out = {'n': ab.n}
-    sn, bc, ns = te.staged_layout(te.feature_slots(fb.plan))
-    out['model'] = {'nodes': len(sn), 'bool_cols': len(bc), 'num_slots': len(ns)}
+    lay = te.staged_layout(te.feature_slots(fb.plan))
+    out['model'] = {'nodes': len(lay['models'][0]['nodes']), 'bool_conditions': len(lay['bool_cols']),
+                    'numeric_conditions': len(lay['num_slots']),
+                    'numeric_columns': len(set(lay['num_slots'].tolist()))}
     for name in args.libs.split(','):
         if name != 'default':  # every later call goes to the variant library
             _native._lib = _native.load_library(os.path.join(
                 ROOT, 'socceraction_amd', '_lib', f'libsocceraction_amd_{name}.so'))
         te._dev = None
-        res = {'staged': _ms(lambda: te.predict_blocks(fb, staged=True))}
+        res = {'staged': _ms(lambda: te.predict_blocks(fb, method='staged'))}
         if name == 'default':
-            res['gather'] = _ms(lambda: te.predict_blocks(fb, staged=False))
+            res['gather'] = _ms(lambda: te.predict_blocks(fb, method='gather'))
         out[name] = res
         print(json.dumps(out), flush=True)
 

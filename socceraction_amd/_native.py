@@ -62,6 +62,13 @@ class SaBlock(ctypes.Structure):
                 ('tile_rows', ctypes.c_int64)]
 
 
+class SaTreeModel(ctypes.Structure):
+    _fields_ = [('nodes', ctypes.c_void_p), ('leaf', ctypes.c_void_p), ('roots', ctypes.c_void_p),
+                ('tree_depth', ctypes.c_void_p), ('n_nodes', ctypes.c_int32),
+                ('n_trees', ctypes.c_int32), ('base_margin', ctypes.c_double),
+                ('p_out', ctypes.c_void_p)]
+
+
 class SaSpadlFrame(ctypes.Structure):
     _fields_ = [('n', ctypes.c_int64), ('time_seconds', _p), ('start_x', _p), ('start_y', _p),
                 ('end_x', _p), ('end_y', _p), ('game', _p), ('team', _p), ('player', _p),
@@ -144,14 +151,12 @@ _SIGNATURES = {
                                        ctypes.POINTER(SaBlock), ctypes.POINTER(SaBlock),
                                        ctypes.POINTER(SaBlock), ctypes.c_int64, ctypes.c_double,
                                        ctypes.c_int32, ctypes.c_int32, _p, _p]),
-    'sa_tree_staged_lds_bytes': (ctypes.c_int64, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
-                                                  ctypes.c_int32]),
-    'sa_tree_predict_staged': (ctypes.c_int, [_p, ctypes.c_int32, _p, _p, ctypes.c_int32, _p,
-                                              ctypes.c_int32, _p, ctypes.c_int32,
+    'sa_tree_staged_lds_bytes': (ctypes.c_int64, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]),
+    'sa_tree_predict_staged': (ctypes.c_int, [ctypes.POINTER(SaTreeModel), _p, ctypes.c_int32, _p, _p,
+                                              ctypes.c_int32, _p, _p, ctypes.c_int32,
                                               ctypes.POINTER(SaBlock), ctypes.POINTER(SaBlock),
-                                              ctypes.POINTER(SaBlock), ctypes.c_int64,
-                                              ctypes.c_double, ctypes.c_int32, ctypes.c_int32, _p,
-                                              _p]),
+                                              ctypes.POINTER(SaBlock), ctypes.c_int64, ctypes.c_int32,
+                                              ctypes.c_int32, _p]),
     'sa_abi_version': (ctypes.c_int, []),
     'sa_last_error': (ctypes.c_char_p, []),
     'sa_build_id': (ctypes.c_char_p, []),

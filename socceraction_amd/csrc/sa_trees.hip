@@ -222,136 +222,190 @@ __global__ __launch_bounds__(TR_THREADS) void tree_fixed_kernel(const TNode* __r
     ((double*)out)[j] = 1.0 / (1.0 + exp(-(double)m));
 }
 
-// Staged walk: the model's used BOOL feature columns of the workgroup's rows are copied into LDS
-// once, packed to one bit per row, and every tree is walked from LDS.  The gathers of
-// tree_fixed_kernel are divergent loads -- one per lane, level and tree, ~582 B/action for a
-// 100-tree model, served a few lanes at a time by the memory pipeline.  Here a workgroup of
-// 512 rows first reads the used bool columns of its rows with coalesced 16-B loads (515 of the
-// 568 default features are bool; a column's 512 rows become 8 u64, one per wave, and a level
-// reads the wave's u64 and shifts by the lane); the few numeric features stay gathers from the
-// f64 / i64 blocks (row bases computed once per thread).  Nodes are restaged (host-prepared,
-// `SNode`) with the feature as a compact reference: bit 30 = numeric, the rest = index into
-// the bool column list or the numeric slot list; leaves are self-loops, so every tree of a
-// group is walked exactly the group's depth (tree_fixed_kernel's fixed-depth walk).  Values,
-// split rule and summation order equal tree_fixed_kernel's bit for bit.
-constexpr int TS_ROWS = 512;              // rows (threads) per workgroup
-constexpr int TS_WAVES = TS_ROWS / 64;
-constexpr int TS_PIECES = TS_ROWS / 16;   // 16-row pieces per column
-constexpr int32_t TS_NUM = 1 << 30;
+// Staged condition walk (default when the model fits LDS).  Every split of the model is turned
+// into a CONDITION whose outcome per row is one bit:
+//   * a bool split: its column's value (a bool column whose threshold sends 0 and 1 the same
+//     way is a constant split: condition 0, never set);
+//   * a numeric split: (column, threshold, default direction) -- `x < thr` (xgboost, float32)
+//     or `x <= thr` (scikit-learn, float64) goes left, NaN follows the default direction.
+// Nodes are renumbered host-side so that each split's two children are adjacent, ordered (child
+// on a clear bit, child on a set bit); a node is then 4 bytes {condition | first child << 16}
+// and one level of the walk is child = first + bit.  A workgroup of 512 rows first evaluates
+// every condition for its rows into LDS (64 B per condition: one bit per row; the used bool
+// columns with one 16-B load per 16 rows, the distinct numeric columns with one coalesced 8-B
+// load per row, TS_B columns in flight, each threshold a ballot), then walks the trees from
+// LDS: per level a 4-B node read and a 1-B bit read, no branches, no float compares, no
+// divergent global gathers.  Leaves are self-loops (condition 0, first child = the leaf), so
+// an 8-tree group is walked exactly its depth; leaf values are summed in tree order: the
+// gather walk's probabilities bit for bit.  Measured per 100-tree model on 16M actions
+// (scripts/tree_probe.py): previous staged walk (bools staged, numeric splits gathered per
+// level) 3.75 ms; a wave-uniform evaluation of every split by 64-bit lane masks 5.4 ms (its
+// scalar instructions issue at the vector rate).
+constexpr int TS_ROWS = 512;               // rows per tile
+constexpr int TS_PIECES = TS_ROWS / 16;    // 16-row pieces per condition
+constexpr int TS_CSTRIDE = TS_ROWS / 8 + 4;  // bytes per condition (+4: conditions start in different banks)
+constexpr int TS_B = 8;                    // loads in flight per staging thread
 
 template <typename A>
-struct SNode {
-  A thr;                      // threshold, or the leaf value
-  int32_t ref, left, right;   // right: bit 31 = default_left
+struct CondSet {  // the model's conditions
+  const int32_t* bool_cols;
+  const int32_t* num_cols;
+  const int32_t* col_start;
+  const A* num_thr;
+  const int32_t* num_dl;
+  int n_bool, n_ncol, n_num;
 };
 
-template <bool F32, bool LE>
-__global__ __launch_bounds__(TS_ROWS) void tree_staged_kernel(const SNode<typename std::conditional<F32, float, double>::type>* __restrict__ nodes,
-                                                              int n_nodes, const int32_t* __restrict__ roots,
-                                                              const int32_t* __restrict__ depth, int n_trees,
-                                                              const int32_t* __restrict__ bool_cols, int n_bool,
-                                                              const int32_t* __restrict__ num_slots, int n_num,
-                                                              sa_block Bb, sa_block Bf, sa_block Bi, int64_t n,
-                                                              double base, void* __restrict__ out) {
-  using A = typename std::conditional<F32, float, double>::type;
-  extern __shared__ __attribute__((aligned(16))) unsigned char ts_lds[];
-  SNode<A>* L = reinterpret_cast<SNode<A>*>(ts_lds);
-  const size_t node_bytes = ((size_t)n_nodes * sizeof(SNode<A>) + 15) / 16 * 16;
-  const int nb = n_bool > 0 ? n_bool : 1, nn = n_num > 0 ? n_num : 1;
-  uint16_t* M16 = reinterpret_cast<uint16_t*>(ts_lds + node_bytes);            // [nb][TS_PIECES]
-  const uint64_t* M = reinterpret_cast<const uint64_t*>(M16);                  // [nb][TS_WAVES]
-  int32_t* NS = reinterpret_cast<int32_t*>(ts_lds + node_bytes + (size_t)nb * TS_ROWS / 8);  // [nn]
-  int32_t* BC = NS + nn;                                                       // [nb]
-  const int tid = threadIdx.x;
-  const int64_t R0 = (int64_t)blockIdx.x * TS_ROWS;
-  for (int k = tid; k < n_num; k += TS_ROWS) NS[k] = num_slots[k];
-  for (int k = tid; k < n_bool; k += TS_ROWS) BC[k] = bool_cols[k];
-  if (n_num == 0 && tid == 0) NS[0] = 1 << 24;
-  if (n_bool == 0 && tid < TS_PIECES) M16[tid] = 0;
-  // every load of a staging pass is issued before any is used (TS_B per thread in flight)
-  constexpr int TS_B = 8;
-  for (int k0 = 0; k0 < n_nodes; k0 += TS_ROWS * TS_B) {
+template <typename A>
+struct CondModel {  // the model's walk
+  const uint32_t* nodes;
+  const A* leaf;
+  const int32_t* roots;
+  const int32_t* depth;
+  int n_nodes, n_trees;
+  double base;
+  void* out;
+};
+
+
+// Condition bits of the TS_ROWS rows from R0 into M8 (TS_ROWS threads, s = 0 .. TS_ROWS-1; row
+// R0 + s belongs to thread s, whole waves).
+template <typename A, bool LE>
+__device__ __forceinline__ void stage_conditions(const CondSet<A>& P, const sa_block& Bb, const sa_block& Bf,
+                                                 const sa_block& Bi, int64_t n, int64_t R0, int s,
+                                                 uint8_t* __restrict__ M8) {
+  const int wv = s >> 6, lane = s & 63;
+  if (s < TS_CSTRIDE / 4) reinterpret_cast<uint32_t*>(M8)[s] = 0;  // condition 0: never set
+  // bool conditions: item it = (column u, 16-row piece p) -> 16 bits
+  const int nbi = P.n_bool * TS_PIECES;
+  for (int i0 = 0; i0 < nbi; i0 += TS_ROWS * TS_B) {
+    u32x4 w[TS_B];
 #pragma unroll
     for (int b = 0; b < TS_B; ++b) {
-      const int k = k0 + b * TS_ROWS + tid;
-      if (k < n_nodes) L[k] = nodes[k];
+      const int it = i0 + b * TS_ROWS + s;
+      w[b] = u32x4{0, 0, 0, 0};
+      const int64_t r = R0 + 16 * (it % TS_PIECES);
+      if (it < nbi && r < n) {
+        const int64_t col = P.bool_cols[it / TS_PIECES];
+        SA_DCHECK(col >= 0 && col < Bb.n_cols, col);
+        const int64_t t = r / Bb.tile_rows;
+        w[b] = *reinterpret_cast<const u32x4*>((const uint8_t*)Bb.data + (t * Bb.n_cols + col) * Bb.tile_rows +
+                                               (r - t * Bb.tile_rows));
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < TS_B; ++b) {
+      const int it = i0 + b * TS_ROWS + s;
+      uint32_t bits = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) bits |= (((w[b][q] & 0x01010101u) * 0x01020408u) >> 24) << (4 * q);
+      if (it < nbi)
+        *reinterpret_cast<uint16_t*>(M8 + (1 + it / TS_PIECES) * TS_CSTRIDE + 2 * (it % TS_PIECES)) = (uint16_t)bits;
     }
   }
-  __syncthreads();  // BC
-  {
-    // bool columns: item it = (column u = it / TS_PIECES, 16-row piece p): one 16-B load of the
-    // piece -> 16 bits at M16[it]
-    const int nbi = n_bool * TS_PIECES;
-    for (int i0 = 0; i0 < nbi; i0 += TS_ROWS * TS_B) {
-      u32x4 w[TS_B];
+  // numeric conditions: the distinct numeric columns num_cols[q] are read TS_B at a time (one
+  // 8-B load per row and column, all in flight before use), then column q's thresholds
+  // (conditions col_start[q] .. col_start[q+1]) are balloted into the wave's 64-bit words
+  const int64_t j = R0 + s < n ? R0 + s : n - 1;
+  const RowBases rb = row_bases(Bb, Bf, Bi, j);
+  for (int q0 = 0; q0 < P.n_ncol; q0 += TS_B) {
+    uint64_t raw[TS_B];
 #pragma unroll
-      for (int b = 0; b < TS_B; ++b) {
-        const int it = i0 + b * TS_ROWS + tid;
-        w[b] = u32x4{0, 0, 0, 0};
-        const int64_t r = R0 + 16 * (it % TS_PIECES);
-        if (it < nbi && r < n) {
-          const int64_t col = BC[it / TS_PIECES];
-          SA_DCHECK(col >= 0 && col < Bb.n_cols, col);
-          const int64_t t = r / Bb.tile_rows;
-          w[b] = *reinterpret_cast<const u32x4*>((const uint8_t*)Bb.data + (t * Bb.n_cols + col) * Bb.tile_rows +
-                                                 (r - t * Bb.tile_rows));
+    for (int b = 0; b < TS_B; ++b) {
+      const int32_t slot = P.num_cols[q0 + b < P.n_ncol ? q0 + b : P.n_ncol - 1];
+      const bool f = (slot >> 24) == 1;
+      const uint64_t* base = f ? reinterpret_cast<const uint64_t*>(rb.f) : reinterpret_cast<const uint64_t*>(rb.i);
+      raw[b] = base[(int64_t)(slot & 0xFFFFFF) * (f ? rb.Rf : rb.Ri)];
+    }
+#pragma unroll
+    for (int b = 0; b < TS_B; ++b) {
+      const int q = q0 + b;
+      if (q >= P.n_ncol) break;
+      const A x = (P.num_cols[q] >> 24) == 1 ? (A)__longlong_as_double((long long)raw[b]) : (A)(double)(int64_t)raw[b];
+      for (int c = P.col_start[q]; c < P.col_start[q + 1]; ++c) {
+        const A thr = P.num_thr[c];
+        const bool right = isnan(x) ? !P.num_dl[c] : !(LE ? x <= thr : x < thr);
+        const uint64_t word = __ballot(right);
+        if (lane == 0) {
+          uint32_t* dst = reinterpret_cast<uint32_t*>(M8 + (1 + P.n_bool + c) * TS_CSTRIDE + 8 * wv);
+          dst[0] = (uint32_t)word;
+          dst[1] = (uint32_t)(word >> 32);
         }
       }
-#pragma unroll
-      for (int b = 0; b < TS_B; ++b) {
-        const int it = i0 + b * TS_ROWS + tid;
-        uint32_t bits = 0;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) bits |= (((w[b][q] & 0x01010101u) * 0x01020408u) >> 24) << (4 * q);
-        if (it < nbi) M16[it] = (uint16_t)bits;
-      }
     }
   }
-  __syncthreads();
-  const int64_t j = R0 + tid;
-  if (j >= n) return;
-  const int wv = tid >> 6, lane = tid & 63;
-  const RowBases rb = row_bases(Bb, Bf, Bi, j);
-  A m = (A)base;
-  for (int t0 = 0; t0 < n_trees; t0 += TG) {
+}
+
+// Row R0 + s (s = 0 .. TS_ROWS-1) through every tree from the staged conditions M8.
+template <typename A>
+__device__ __forceinline__ A walk_conditions(const CondModel<A>& P, const uint32_t* __restrict__ N,
+                                             const A* __restrict__ LV, const uint8_t* __restrict__ M8, int s) {
+  const uint8_t* Mrow = M8 + (s >> 3);  // this row's byte of every condition
+  const int rbit = s & 7;
+  A m = (A)P.base;
+  for (int t0 = 0; t0 < P.n_trees; t0 += TG) {
     int k[TG];
     int D = 0;
 #pragma unroll
     for (int u = 0; u < TG; ++u) {
-      const int t = t0 + u < n_trees ? t0 + u : n_trees - 1;
-      k[u] = roots[t];
-      D = max(D, depth[t]);
+      const int t = t0 + u < P.n_trees ? t0 + u : P.n_trees - 1;
+      k[u] = P.roots[t];
+      D = max(D, P.depth[t]);
     }
     for (int d = 0; d < D; ++d) {
-      // the TG trees' node reads, then all their feature reads (the numeric gathers of the
-      // lanes that need one go out together: one memory latency per level, not TG), then the
-      // decisions
-      SNode<A> nd[TG];
+      uint32_t nd[TG];
 #pragma unroll
-      for (int u = 0; u < TG; ++u) nd[u] = L[k[u]];
-      A v[TG];
+      for (int u = 0; u < TG; ++u) nd[u] = N[k[u]];
 #pragma unroll
       for (int u = 0; u < TG; ++u) {
-        const int idx = nd[u].ref & (TS_NUM - 1);
-        SA_DCHECK((nd[u].ref & TS_NUM) ? idx < nn : idx < nb, nd[u].ref);
-        if (nd[u].ref & TS_NUM) v[u] = (A)feature_value(rb, NS[idx]);
-      }
-#pragma unroll
-      for (int u = 0; u < TG; ++u) {
-        const int idx = nd[u].ref & (TS_NUM - 1);
-        if (!(nd[u].ref & TS_NUM)) v[u] = (A)((M[idx * TS_WAVES + wv] >> lane) & 1ull);
-        const bool left = isnan(v[u]) ? nd[u].right < 0 : (LE ? v[u] <= nd[u].thr : v[u] < nd[u].thr);
-        k[u] = left ? nd[u].left : (nd[u].right & 0x7FFFFFFF);
+        const uint32_t bit = (Mrow[(nd[u] & 0xFFFFu) * TS_CSTRIDE] >> rbit) & 1u;
+        k[u] = (int)(nd[u] >> 16) + (int)bit;
       }
     }
+    A lv[TG];
+#pragma unroll
+    for (int u = 0; u < TG; ++u) lv[u] = LV[k[u]];
 #pragma unroll
     for (int u = 0; u < TG; ++u)
-      if (t0 + u < n_trees) m = m + L[k[u]].thr;
+      if (t0 + u < P.n_trees) m = m + lv[u];
   }
+  return m;
+}
+
+// One workgroup per tile: its 512 threads stage the tile's conditions, then walk its rows.
+// Measured alternatives (scripts/tree_probe.py, 100-tree depth-3 model, 16M actions): persistent
+// workgroups of 16 waves in two roles -- 8 staging tile i+1 while 8 walk tile i -- 7.6 ms (one
+// such workgroup per CU leaves the staging too few loads in flight); both VAEP.rate learners in
+// one launch over the union of their conditions 6.8 ms vs 2 x 2.9 (the larger LDS footprint
+// halves the resident workgroups); 256- / 1024-row tiles 3.0 / 3.7 ms.
+template <bool F32, bool LE>
+__global__ __launch_bounds__(TS_ROWS) void tree_cond_kernel(CondSet<typename std::conditional<F32, float, double>::type> C,
+                                                            CondModel<typename std::conditional<F32, float, double>::type> P,
+                                                            sa_block Bb, sa_block Bf, sa_block Bi, int64_t n) {
+  using A = typename std::conditional<F32, float, double>::type;
+  extern __shared__ __attribute__((aligned(16))) unsigned char ts_lds[];
+  // LDS carved by integer offsets from ts_lds (a pointer cast through uintptr_t would make
+  // every access a flat one): conditions, nodes, leaf values
+  const int n_cond = 1 + C.n_bool + C.n_num;
+  const size_t moff = ((size_t)n_cond * TS_CSTRIDE + 15) / 16 * 16;
+  uint8_t* M8 = ts_lds;
+  uint32_t* N = reinterpret_cast<uint32_t*>(ts_lds + moff);
+  A* LV = reinterpret_cast<A*>(ts_lds + moff + (size_t)(P.n_nodes + (P.n_nodes & 1)) * 4);
+  const int tid = threadIdx.x;
+  for (int k = tid; k < P.n_nodes; k += TS_ROWS) {
+    N[k] = P.nodes[k];
+    LV[k] = P.leaf[k];
+  }
+  const int64_t R0 = (int64_t)blockIdx.x * TS_ROWS;
+  stage_conditions<A, LE>(C, Bb, Bf, Bi, n, R0, tid, M8);
+  __syncthreads();
+  const int64_t j = R0 + tid;
+  if (j >= n) return;
+  const A m = walk_conditions<A>(P, N, LV, M8, tid);
   if (F32)
-    ((float*)out)[j] = 1.0f / (1.0f + expf(-(float)m));
+    ((float*)P.out)[j] = 1.0f / (1.0f + expf(-(float)m));
   else
-    ((double*)out)[j] = 1.0 / (1.0 + exp(-(double)m));
+    ((double*)P.out)[j] = 1.0 / (1.0 + exp(-(double)m));
 }
 
 }  // namespace sa
@@ -405,22 +459,25 @@ extern "C" int sa_tree_predict(const void* nodes, int32_t n_nodes, const int32_t
   return check_launch("tree_predict_kernel");
 }
 
-extern "C" int64_t sa_tree_staged_lds_bytes(int32_t n_nodes, int32_t n_bool, int32_t n_num, int32_t f32) {
-  const size_t node = f32 ? sizeof(SNode<float>) : sizeof(SNode<double>);
-  const size_t nb = n_bool > 0 ? n_bool : 1, nn = n_num > 0 ? n_num : 1;
-  return (int64_t)(((size_t)n_nodes * node + 15) / 16 * 16 + nb * TS_ROWS / 8 + (nn + nb) * 4);
+extern "C" int64_t sa_tree_staged_lds_bytes(int32_t n_nodes, int32_t n_cond, int32_t f32) {
+  return ((int64_t)n_cond * TS_CSTRIDE + 15) / 16 * 16 + (int64_t)(n_nodes + (n_nodes & 1)) * 4 +
+         (int64_t)n_nodes * (f32 ? 4 : 8);
 }
 
-extern "C" int sa_tree_predict_staged(const void* snodes, int32_t n_nodes, const int32_t* roots,
-                                      const int32_t* tree_depth, int32_t n_trees, const int32_t* bool_cols,
-                                      int32_t n_bool, const int32_t* num_slots, int32_t n_num,
-                                      const sa_block* bool_blk, const sa_block* f64_blk,
-                                      const sa_block* i64_blk, int64_t n, double base_margin, int32_t le,
-                                      int32_t f32, void* p_out, void* stream) {
-  if (n < 0 || n_nodes < 1 || n_trees < 1 || n_bool < 0 || n_num < 0 || !snodes || !roots ||
-      !tree_depth || !p_out || (n_bool > 0 && (!bool_cols || !bool_blk)) || (n_num > 0 && !num_slots))
-    return fail(SA_EINVAL, "bad staged tree model arguments");
-  const int64_t lds = sa_tree_staged_lds_bytes(n_nodes, n_bool, n_num, f32);
+extern "C" int sa_tree_predict_staged(const sa_tree_model* model, const int32_t* bool_cols, int32_t n_bool,
+                                      const int32_t* num_cols, const int32_t* col_start, int32_t n_ncol,
+                                      const void* num_thr, const int32_t* num_dl, int32_t n_num,
+                                      const sa_block* bool_blk, const sa_block* f64_blk, const sa_block* i64_blk,
+                                      int64_t n, int32_t le, int32_t f32, void* stream) {
+  if (!model || n < 0 || 1 + n_bool + n_num > 65536 || n_bool < 0 || n_num < 0 ||
+      (n_bool > 0 && (!bool_cols || !bool_blk)) || n_ncol < 0 ||
+      (n_num > 0 && (n_ncol < 1 || !num_cols || !col_start || !num_thr || !num_dl)))
+    return fail(SA_EINVAL, "bad staged tree arguments");
+  const sa_tree_model& m = *model;
+  if (m.n_nodes < 1 || m.n_nodes > 65535 || m.n_trees < 1 || !m.nodes || !m.leaf || !m.roots || !m.tree_depth ||
+      !m.p_out)
+    return fail(SA_EINVAL, "bad staged tree model");
+  const int64_t lds = sa_tree_staged_lds_bytes(m.n_nodes, 1 + n_bool + n_num, f32);
   if (lds > 160 * 1024) return fail(SA_EINVAL, "staged tree model needs %lld B of LDS", (long long)lds);
   sa_block z{nullptr, 0, 0, 16};
   const sa_block Bb = bool_blk ? *bool_blk : z, Bf = f64_blk ? *f64_blk : z, Bi = i64_blk ? *i64_blk : z;
@@ -429,10 +486,14 @@ extern "C" int sa_tree_predict_staged(const void* snodes, int32_t n_nodes, const
   if (n == 0) return SA_OK;
   const dim3 grid((unsigned)((n + TS_ROWS - 1) / TS_ROWS)), block(TS_ROWS);
   hipStream_t st = (hipStream_t)stream;
-#define SA_TS_LAUNCH(F, LEQ, A)                                                                         \
-  hipLaunchKernelGGL((tree_staged_kernel<F, LEQ>), grid, block, (size_t)lds, st,                         \
-                     (const SNode<A>*)snodes, n_nodes, roots, tree_depth, n_trees, bool_cols, n_bool,       \
-                     num_slots, n_num, Bb, Bf, Bi, n, base_margin, p_out)
+#define SA_TS_LAUNCH(F, LEQ, A)                                                                          \
+  do {                                                                                                  \
+    CondSet<A> C{bool_cols, num_cols, col_start, (const A*)num_thr, num_dl, n_bool, n_num > 0 ? n_ncol : 0, \
+                 n_num};                                                                                \
+    CondModel<A> P{(const uint32_t*)m.nodes, (const A*)m.leaf, m.roots, m.tree_depth, m.n_nodes,        \
+                   m.n_trees,                m.base_margin,    m.p_out};                                \
+    hipLaunchKernelGGL((tree_cond_kernel<F, LEQ>), grid, block, (size_t)lds, st, C, P, Bb, Bf, Bi, n);    \
+  } while (0)
   if (f32 && le)
     SA_TS_LAUNCH(true, true, float);
   else if (f32)
@@ -442,5 +503,5 @@ extern "C" int sa_tree_predict_staged(const void* snodes, int32_t n_nodes, const
   else
     SA_TS_LAUNCH(false, false, double);
 #undef SA_TS_LAUNCH
-  return check_launch("tree_staged_kernel");
+  return check_launch("tree_cond_kernel");
 }

@@ -195,44 +195,82 @@ class TreeEnsemble:
             slots[f] = (kinds[kind] << 24) | col
         return slots
 
-    def staged_layout(self, slots: np.ndarray):
-        """The staged walk's model (sa_tree_predict_staged): ``(snodes, bool_cols, num_slots)``
-        for the feature slots of one block layout. Split nodes refer to their feature as an index
-        into the used bool columns, or (1 << 30) | index into the used numeric slots; leaves
-        become self-loops (left = right = the leaf)."""
+    def _split_outcomes(self, k: int):
+        """(goes left on 0, goes left on 1) of split k as the producing library compares."""
+        A = np.float32 if self.f32 else np.float64
+        thr = A(self.nodes['thr'][k])
+        if self.le:
+            return bool(A(0) <= thr), bool(A(1) <= thr)
+        return bool(A(0) < thr), bool(A(1) < thr)
+
+    def conditions(self, slots: np.ndarray, bool_cols: set, num_keys: set) -> None:
+        """Add the conditions of this model's splits (staged walk) to the two sets: bool block
+        columns, and numeric (slot, threshold bytes, default_left) triples."""
         nd = self.nodes
-        n = len(nd)
-        split = nd['feature'] >= 0
-        fslot = np.full(n, -1, np.int64)
-        fslot[split] = slots[nd['feature'][split]]
-        kind = fslot >> 24
-        bool_cols = np.unique(fslot[split & (kind == 0)] & 0xFFFFFF).astype(np.int32)
-        num_slots = np.unique(fslot[split & (kind != 0)]).astype(np.int32)
-        ref = np.zeros(n, np.int64)
-        isb = split & (kind == 0)
-        isn = split & (kind != 0)
-        ref[isb] = np.searchsorted(bool_cols, fslot[isb] & 0xFFFFFF)
-        ref[isn] = (1 << 30) | np.searchsorted(num_slots, fslot[isn])
-        if not len(bool_cols):
-            ref[~split] = 1 << 30  # leaves: any valid reference
-        idx = np.arange(n)
-        dt = np.dtype([('thr', '<f4'), ('ref', '<i4'), ('left', '<i4'), ('right', '<i4')]) \
-            if self.f32 else \
-            np.dtype([('thr', '<f8'), ('ref', '<i4'), ('left', '<i4'), ('right', '<i4'), ('pad', '<i4')])
-        sn = np.zeros(n, dt)
-        sn['thr'] = nd['thr'].astype(np.float32) if self.f32 else nd['thr']
-        sn['ref'] = ref.astype(np.int32)
-        sn['left'] = np.where(split, nd['left'], idx)
-        sn['right'] = np.where(split, nd['right'], idx)
-        return sn, bool_cols, num_slots
+        A = np.float32 if self.f32 else np.float64
+        for k in np.nonzero(nd['feature'] >= 0)[0]:
+            slot = int(slots[nd['feature'][k]])
+            if slot >> 24 == 0:
+                l0, l1 = self._split_outcomes(k)
+                if l0 != l1:
+                    bool_cols.add(slot & 0xFFFFFF)
+            else:
+                num_keys.add((slot, A(nd['thr'][k]).tobytes(), bool(int(nd['right'][k]) < 0)))
+
+    def staged_nodes(self, slots: np.ndarray, bidx: dict, nidx: dict) -> dict:
+        """This model's nodes for the staged condition walk, given the condition numbering
+        (``bidx``: bool column -> condition, ``nidx``: numeric triple -> condition). Nodes are
+        renumbered tree by tree so that a split's children are adjacent -- (child on a clear
+        bit, child on a set bit) -- and stored as ``condition | first child << 16``; leaves are
+        self-loops with condition 0 (never set); a bool split whose threshold sends 0 and 1 the
+        same way is a condition-0 split whose first child is the one every row takes."""
+        nd = self.nodes
+        A = np.float32 if self.f32 else np.float64
+        feat = nd['feature']
+        cn = np.zeros(len(nd), np.uint32)
+        leaf = np.zeros(len(nd), A)
+        roots = np.empty(self.n_trees, np.int32)
+        nxt = 0
+        for t, r in enumerate(self.roots):
+            roots[t] = nxt
+            queue = [(int(r), nxt)]
+            nxt += 1
+            while queue:
+                k, new = queue.pop(0)
+                f = int(feat[k])
+                if f < 0:
+                    cn[new] = np.uint32(new) << np.uint32(16)
+                    leaf[new] = A(nd['thr'][k])
+                    continue
+                left, right = int(nd['left'][k]), int(nd['right'][k]) & 0x7FFFFFFF
+                slot = int(slots[f])
+                if slot >> 24 == 0:
+                    l0, l1 = self._split_outcomes(k)
+                    cond = 0 if l0 == l1 else bidx[slot & 0xFFFFFF]
+                    pair = (left, right) if l0 else (right, left)
+                else:
+                    cond = nidx[(slot, A(nd['thr'][k]).tobytes(), bool(int(nd['right'][k]) < 0))]
+                    pair = (left, right)
+                cn[new] = np.uint32(cond) | (np.uint32(nxt) << np.uint32(16))
+                queue += [(pair[0], nxt), (pair[1], nxt + 1)]
+                nxt += 2
+        return {'nodes': cn[:nxt], 'leaf': leaf[:nxt], 'roots': roots}
+
+    def staged_layout(self, slots: np.ndarray) -> dict:
+        """The staged condition walk's model (sa_tree_predict_staged) of this model alone."""
+        return staged_layout([self], [slots])
 
     def predict_blocks(self, blocks, feature_names: Optional[Sequence[str]] = None,
-                       out: Optional[torch.Tensor] = None, staged: Optional[bool] = None) -> torch.Tensor:
+                       out: Optional[torch.Tensor] = None, staged: Optional[bool] = None,
+                       method: Optional[str] = None) -> torch.Tensor:
         """P(class 1) of every row of the device feature blocks (``ops.FeatureBlocks``):
         float32 for xgboost models (as their ``predict_proba``), float64 for scikit-learn.
-        ``staged`` (default: whenever the model's staged form fits LDS): the staged walk
-        (sa_tree_predict_staged); False: the gather walk (sa_tree_predict)."""
+        ``method``: 'staged' (the staged condition walk, sa_tree_predict_staged; the default
+        whenever the model fits LDS) or 'gather' (sa_tree_predict). ``staged`` True / False is
+        the older spelling of the two."""
         from .batch import stream_handle
+        if method is None and staged is not None:
+            method = 'staged' if staged else 'gather'
         dev = blocks.bool_block.device
         d = self._device(dev)
         slots_np = self.feature_slots(blocks.plan, feature_names)
@@ -241,27 +279,39 @@ class TreeEnsemble:
         if out is None:
             out = torch.empty(max(n, 1), dtype=dt, device=dev)
         bb, fb, ib = blocks.sa_blocks()
-        if staged is not False and self.n_trees and d['depth'] is not None:
+        if method != 'gather' and self.n_trees:
             key = ('staged', slots_np.tobytes())
             st = d.get(key)
             if st is None:
-                sn, bc, ns = self.staged_layout(slots_np)
-                lds = _native.lib().sa_tree_staged_lds_bytes(len(sn), len(bc), len(ns), int(self.f32))
-                st = None if lds > 160 * 1024 else (
-                    torch.from_numpy(sn.view(np.uint8).copy()).to(dev),
-                    torch.from_numpy(bc).to(dev) if len(bc) else None, len(bc),
-                    torch.from_numpy(ns).to(dev) if len(ns) else None, len(ns), len(sn))
-                d[key] = st if st is not None else False
+                lay = self.staged_layout(slots_np)
+                lay.update(lay.pop('models')[0])
+                n_cond = 1 + len(lay['bool_cols']) + len(lay['num_slots'])
+                lds = _native.lib().sa_tree_staged_lds_bytes(len(lay['nodes']), n_cond, int(self.f32))
+                fits = lds <= 160 * 1024 and n_cond <= 65536 and len(lay['nodes']) < 65536
+
+                def t(v):
+                    if not len(v):
+                        return None
+                    v = np.ascontiguousarray(v)
+                    return torch.from_numpy(v.view(np.int32) if v.dtype == np.uint32 else v).to(dev)
+                st = {k: t(v) for k, v in lay.items()} if fits else False
+                if st:
+                    st['n_num'] = len(lay['num_slots'])
+                d[key] = st
             if st:
-                sn_t, bc_t, nbc, ns_t, nns, nnodes = st
+                def ptr(k):
+                    return st[k].data_ptr() if st[k] is not None else None
+                rec = _native.SaTreeModel(ptr('nodes'), ptr('leaf'), ptr('roots'), d['depth'].data_ptr(),
+                                          st['nodes'].numel(), self.n_trees, float(self.base_margin),
+                                          out.data_ptr())
                 _native.check(_native.lib().sa_tree_predict_staged(
-                    sn_t.data_ptr(), nnodes, d['roots'].data_ptr(), d['depth'].data_ptr(),
-                    self.n_trees, bc_t.data_ptr() if bc_t is not None else None, nbc,
-                    ns_t.data_ptr() if ns_t is not None else None, nns, ctypes.byref(bb),
-                    ctypes.byref(fb), ctypes.byref(ib), n, float(self.base_margin), int(self.le),
-                    int(self.f32), out.data_ptr(), stream_handle()))
+                    ctypes.byref(rec), ptr('bool_cols'),
+                    0 if st['bool_cols'] is None else st['bool_cols'].numel(), ptr('num_cols'),
+                    ptr('col_start'), 0 if st['num_cols'] is None else st['num_cols'].numel(),
+                    ptr('num_thr'), ptr('num_dl'), st['n_num'], ctypes.byref(bb), ctypes.byref(fb),
+                    ctypes.byref(ib), n, int(self.le), int(self.f32), stream_handle()))
                 return out[:n]
-            elif staged:
+            elif method == 'staged':
                 raise ValueError('the staged form of this model does not fit LDS')
         slots = torch.from_numpy(slots_np).to(dev)
         _native.check(_native.lib().sa_tree_predict(
@@ -272,6 +322,28 @@ class TreeEnsemble:
             n, float(self.base_margin), int(self.le), int(self.f32), out.data_ptr(),
             stream_handle()))
         return out[:n]
+
+
+def staged_layout(models: Sequence[TreeEnsemble], slots: Sequence[np.ndarray]) -> dict:
+    """The staged condition walk's conditions for models evaluated on the same blocks -- 0 never
+    set, then the used bool columns, then the distinct numeric (slot, threshold, default
+    direction) triples in slot order -- and each model's renumbered nodes."""
+    A = np.float32 if models[0].f32 else np.float64
+    bset: set = set()
+    nset: set = set()
+    for te, sl in zip(models, slots):
+        te.conditions(sl, bset, nset)
+    bool_cols = np.array(sorted(bset), np.int32)
+    bidx = {c: 1 + i for i, c in enumerate(bool_cols.tolist())}
+    keys = sorted(nset)
+    nidx = {key: 1 + len(bool_cols) + i for i, key in enumerate(keys)}
+    num_slots = np.array([key[0] for key in keys], np.int32)
+    num_cols, first = np.unique(num_slots, return_index=True)
+    return {'bool_cols': bool_cols, 'num_slots': num_slots, 'num_cols': num_cols.astype(np.int32),
+            'col_start': np.append(first, len(num_slots)).astype(np.int32),
+            'num_thr': np.array([np.frombuffer(key[1], A)[0] for key in keys], A),
+            'num_dl': np.array([int(key[2]) for key in keys], np.int32),
+            'models': [te.staged_nodes(sl, bidx, nidx) for te, sl in zip(models, slots)]}
 
 
 def xgb_classifier_iterations(model, raw: Optional[dict] = None) -> Optional[int]:
@@ -329,4 +401,5 @@ def synthetic_xgboost_json(n_features: int, n_trees: int = 100, depth: int = 3, 
         'feature_names': []}, 'version': [1, 6, 2]}
 
 
-__all__ = ['TreeEnsemble', 'NODE_DTYPE', 'synthetic_xgboost_json', 'xgb_classifier_iterations']
+__all__ = ['TreeEnsemble', 'NODE_DTYPE', 'staged_layout', 'synthetic_xgboost_json',
+           'xgb_classifier_iterations']

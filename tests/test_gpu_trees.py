@@ -80,9 +80,9 @@ def test_fixed_depth_walk_equals_leaf_checked_walk(sa, kind):
                                                random_state=0).fit(X, y)
     te = sa['trees'].TreeEnsemble.from_model(model)
     assert te is not None and te.depths().max() >= 3
-    fixed = te.predict_blocks(fb).cpu().numpy()
+    fixed = te.predict_blocks(fb, method='gather').cpu().numpy()
     te._dev['depth'] = None
-    walked = te.predict_blocks(fb).cpu().numpy()
+    walked = te.predict_blocks(fb, method='gather').cpu().numpy()
     np.testing.assert_array_equal(fixed, walked)
 
 
@@ -150,23 +150,26 @@ def test_vaep_rate_on_device(sa):
     assert got32['vaep_value'].dtype == np.float32
 
 
-@pytest.mark.parametrize('kind', ['xgboost', 'sklearn', 'xgboost_bool_only', 'xgboost_num_only'])
+@pytest.mark.parametrize('kind', ['xgboost', 'sklearn', 'xgboost_bool_only', 'xgboost_num_only',
+                                  'depth1', 'depth5', 'plain_layout'])
 def test_staged_walk_equals_gather_walk(sa, kind):
-    """The LDS-staged walk (used columns of 256 rows staged, bools packed to bits) gives the
-    gather walk's probabilities bit for bit: xgboost float32 / scikit-learn float64 models,
-    models reading only bool or only numeric features, several tiles and a ragged last
-    workgroup (300 games), NaN in a numeric feature."""
+    """The staged condition walk (every split a condition bit in LDS) gives the gather walk's
+    probabilities bit for bit: float32 xgboost / float64 scikit-learn models (unbalanced trees),
+    bool-only and numeric-only models, depths 1 - 5, several tiles and a ragged last workgroup
+    (300 games), NaN in a numeric feature, tiled and plain column-major blocks."""
     from socceraction_amd import synthetic
     from oracle import vaep_oracle as vo
     B, ops, trees = sa['batch'], sa['ops'], sa['trees']
     d = synthetic.spadl_games(300, seed=8)
     ab = B.ActionBatch.from_columns(d)
-    fb = ops.features(ab, vo.SPADL_DEFAULT, 3, bool_tile=1024, num_tile=128)
+    tiles = (None, None) if kind == 'plain_layout' else (1024, 128)
+    fb = ops.features(ab, vo.SPADL_DEFAULT, 3, bool_tile=tiles[0], num_tile=tiles[1])
+    assert fb.n % 512 != 0
     kinds = [k for _, k, _ in fb.plan.order]
-    if kind.startswith('xgboost'):
-        fk = list(kinds)
-        model = trees.synthetic_xgboost_json(len(kinds), n_trees=100, depth=3, seed=11,
-                                             feature_kinds=fk)
+    depth = {'depth1': 1, 'depth5': 5}.get(kind, 3)
+    if kind != 'sklearn':
+        model = trees.synthetic_xgboost_json(len(kinds), n_trees=100, depth=depth, seed=11,
+                                             feature_kinds=kinds)
         keep = {'xgboost_bool_only': 'b', 'xgboost_num_only': 'fi'}.get(kind)
         if keep:  # re-point every split at a feature of the wanted kinds
             cand = [j for j, k in enumerate(kinds) if k in keep]
@@ -182,9 +185,11 @@ def test_staged_walk_equals_gather_walk(sa, kind):
         X = np.stack([blocks[k][c, :n].astype(np.float64) for _, k, c in fb.plan.order], axis=1)
         y = (X[:, 0] + np.random.default_rng(0).random(n) > 0.7).astype(int)
         te = trees.TreeEnsemble.from_model(
-            HistGradientBoostingClassifier(max_iter=40, max_depth=4, random_state=0).fit(X, y))
+            HistGradientBoostingClassifier(max_iter=40, max_leaf_nodes=11, random_state=0).fit(X, y))
+        assert te.depths().min() < te.depths().max()
     fcol = [c for _, k, c in fb.plan.order if k == 'f'][5]
     fb.f64_block[:, fcol, ::7] = float('nan')
-    got = te.predict_blocks(fb, staged=True).cpu().numpy()
-    ref = te.predict_blocks(fb, staged=False).cpu().numpy()
+    got = te.predict_blocks(fb, method='staged').cpu().numpy()
+    ref = te.predict_blocks(fb, method='gather').cpu().numpy()
     np.testing.assert_array_equal(got, ref)
+    np.testing.assert_array_equal(te.predict_blocks(fb).cpu().numpy(), ref)  # the default path
