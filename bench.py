@@ -481,6 +481,7 @@ def main() -> None:
     # workgroups are dispatched ahead of the VAEP kernels' as CUs free up
     sides = {p: (torch.cuda.Stream(priority=-1 if p == 'high' else 0) if overlap else main_s)
              for p in ('normal', 'high')}
+    par_s = torch.cuda.Stream()
 
     def make_step(spec):
         """One step of the given variant: the VAEP kernels in `order` on the main stream; the xT
@@ -505,11 +506,23 @@ def main() -> None:
         calls = tuple(by_name[k] for k in order)
         xt_start, xt_finish, xt_last = xt_step(ab, dist, xt, cells, shared=overlap)
         nv = len(calls)
+        # par=1 (A/B only): bool_features on its own stream, concurrent with the calls before it
+        par = int(spec.get('par', 0)) and 'bool_features' in order
+        ib = order.index('bool_features') if par else -1
 
         def step(ev=None):
             # ev[i] = (start, end) of VAEP call i on the main stream, ev[nv] = the xT side
             # stream's span (count pass + all-reduce, then solve -- a host sync of the side
             # stream -- and rate); --serial: everything on the one stream
+            pj = None
+            if par:
+                pf = torch.cuda.Event()
+                pf.record(main_s)
+                par_s.wait_event(pf)
+                with torch.cuda.stream(par_s):
+                    calls[ib]()
+                pj = torch.cuda.Event()
+                pj.record(par_s)
             for i, call in enumerate(calls):
                 if overlap and i == fork:
                     fk = torch.cuda.Event()
@@ -519,6 +532,9 @@ def main() -> None:
                         if ev is not None:
                             ev[nv][0].record(side)
                         xt_start()
+                if par and i == ib:
+                    main_s.wait_event(pj)
+                    continue
                 if ev is not None:
                     ev[i][0].record(main_s)
                 call()
@@ -550,7 +566,7 @@ def main() -> None:
             v = dict(base)
             for kv in [o for o in opts.split('/') if o]:
                 k_, _, v_ = kv.partition('=')
-                v[k_] = v_.split('+') if k_ == 'order' else (int(v_) if k_ == 'fork' else v_)
+                v[k_] = v_.split('+') if k_ == 'order' else (int(v_) if k_ in ('fork', 'par') else v_)
             variants[name] = make_step(v)[0]
         ab_ms = {k: [] for k in variants}
         for fn in variants.values():
