@@ -134,6 +134,8 @@ def xt_step(ab, dist, source: str = 'cells', cells=None, shared: bool = True):
     rate_out = torch.empty(max((ab.n + 15) // 16 * 16, 16), dtype=torch.float64, device=ab.device)
 
     def start():
+        if source == 'none':  # --ab diagnostic only: the VAEP kernels without the xT part
+            return
         if source == 'cells':
             acc = ops.xt_count_cells(cells, ab.n, 16, 12, shared=shared)
         else:
@@ -148,6 +150,8 @@ def xt_step(ab, dist, source: str = 'cells', cells=None, shared: bool = True):
         state['acc'] = acc
 
     def finish():
+        if source == 'none':
+            return
         sol = ops.xt_solve(state.pop('acc'))  # synchronises the current stream
         if source == 'cells':
             ops.xt_rate_cells(cells, ab.n, 16, 12, sol.mats[3], out=rate_out)
@@ -162,6 +166,12 @@ def xt_step(ab, dist, source: str = 'cells', cells=None, shared: bool = True):
 ATOMIC_DEFAULT = ['actiontype', 'actiontype_onehot', 'bodypart', 'bodypart_onehot', 'time',
                   'team', 'time_delta', 'location', 'polar', 'movement_polar', 'direction',
                   'goalscore']
+
+
+def _record(stream) -> 'torch.cuda.Event':
+    e = torch.cuda.Event()
+    e.record(stream)
+    return e
 
 
 def _events_ms(fn, reps: int) -> float:
@@ -431,9 +441,12 @@ def main() -> None:
     ap.add_argument('--ab', default='',
                     help='dev tool: ";"-separated step variants "name:key=value/..." (keys xt, '
                          'order with "+", fork, prio) timed round-robin in one process')
-    ap.add_argument('--side-priority', default='high', choices=('normal', 'high'),
-                    help='priority of the xT side stream (high: 3.227 - 3.232 vs 3.230 - 3.246 '
-                         'ms per step in-process, profiles/r02_step_ab.md)')
+    ap.add_argument('--side-priority', default='normal', choices=('normal', 'high'),
+                    help='priority of the xT side stream (profiles/r02_step_ab.md)')
+    ap.add_argument('--xt-count', default='main', choices=('main', 'side'),
+                    help='where the xT count pass runs: on the main stream right after '
+                         'num_features in its one-workgroup-per-CU shape (default: 3.19 - 3.24 vs '
+                         '3.24 - 3.31 ms per step, profiles/r02_step_ab.md), or on the side stream')
     ap.add_argument('--num-tile', type=int, default=128,
                     help='rows per f64/i64-block tile (0 = one tile: plain column-major)')
     args = ap.parse_args()
@@ -498,13 +511,16 @@ def main() -> None:
         by_name = {'bool_features': lambda: ops.features_into(s_act, bool_out),
                    'num_features': (lambda: ops.features_into(s_act, num_out,
                                                               xt_cells=(16, 12, cells)))
-                   if xt == 'cells' else (lambda: ops.features_into(s_act, num_out)),
+                   if xt in ('cells', 'none') else (lambda: ops.features_into(s_act, num_out)),
                    'goalscore': lambda: ops.goalscore_into(ab, out),
                    'labels': lambda: ops.labels(ab, 10, lab),
                    'formula': lambda: ops.formula(ab, ps, pc, val),
                    'labels_formula': lambda: ops.labels_formula(ab, ps, pc, 10, lab, val)}
         calls = tuple(by_name[k] for k in order)
-        xt_start, xt_finish, xt_last = xt_step(ab, dist, xt, cells, shared=overlap)
+        # cm=1: the count pass runs on the main stream right after num_features, in the fast
+        # one-workgroup-per-CU shape; the side stream takes the solve and the rate
+        cm = int(spec.get('cm', 0)) and overlap
+        xt_start, xt_finish, xt_last = xt_step(ab, dist, xt, cells, shared=overlap and not cm)
         nv = len(calls)
         # par=1 (A/B only): bool_features on its own stream, concurrent with the calls before it
         par = int(spec.get('par', 0)) and 'bool_features' in order
@@ -525,13 +541,18 @@ def main() -> None:
                 pj.record(par_s)
             for i, call in enumerate(calls):
                 if overlap and i == fork:
+                    if cm:
+                        if ev is not None:
+                            ev[nv][0].record(main_s)
+                        xt_start()
                     fk = torch.cuda.Event()
                     fk.record(main_s)
                     side.wait_event(fk)
                     with torch.cuda.stream(side):
-                        if ev is not None:
+                        if ev is not None and not cm:
                             ev[nv][0].record(side)
-                        xt_start()
+                        if not cm:
+                            xt_start()
                 if par and i == ib:
                     main_s.wait_event(pj)
                     continue
@@ -540,10 +561,12 @@ def main() -> None:
                 call()
                 if ev is not None:
                     ev[i][1].record(main_s)
-            if not overlap:
-                if ev is not None:
-                    ev[nv][0].record(main_s)
-                xt_start()
+            if not overlap or fork >= nv:  # serial, or forked after the last VAEP call
+                (side if overlap else main_s).wait_event(_record(main_s))
+                with torch.cuda.stream(side):
+                    if ev is not None:
+                        ev[nv][0].record(side)
+                    xt_start()
             with torch.cuda.stream(side):
                 xt_finish()
                 if ev is not None:
@@ -555,7 +578,7 @@ def main() -> None:
         return step, xt_last
 
     base = {'xt': args.xt_source, 'order': args.order.split(','), 'fork': args.xt_fork,
-            'prio': args.side_priority}
+            'prio': args.side_priority, 'cm': int(args.xt_count == 'main')}
     if base['fork'] < 0:  # default: before the first VAEP call, or right after num_features
         base['fork'] = (base['order'].index('num_features') + 1) if args.xt_source == 'cells' else 0
     if args.ab:  # in-process A/B of step variants on the same allocations (dev tool)
@@ -566,7 +589,7 @@ def main() -> None:
             v = dict(base)
             for kv in [o for o in opts.split('/') if o]:
                 k_, _, v_ = kv.partition('=')
-                v[k_] = v_.split('+') if k_ == 'order' else (int(v_) if k_ in ('fork', 'par') else v_)
+                v[k_] = v_.split('+') if k_ == 'order' else (int(v_) if k_ in ('fork', 'par', 'cm') else v_)
             variants[name] = make_step(v)[0]
         ab_ms = {k: [] for k in variants}
         for fn in variants.values():
@@ -672,8 +695,11 @@ def main() -> None:
                                   'codes': 'coordinates (count) + rate operands',
                                   'coords': 'coordinates'}[base['xt']],
                        'stream': 'main (serial)' if args.serial else
-                       f"{base['prio']}-priority side stream, forked after {base['fork']} VAEP "
-                       'call(s), overlapped with the rest'}
+                       (f"count pass on the main stream after {base['fork']} VAEP call(s), solve "
+                        f"and rate on a {base['prio']}-priority side stream overlapped with the rest"
+                        if base['cm'] else
+                        f"{base['prio']}-priority side stream, forked after {base['fork']} VAEP "
+                        'call(s), overlapped with the rest')}
     line['vaep_order'] = order
     line['streams'] = ('one stream' if args.serial else
                        'VAEP kernels on the main stream, xT on a side stream')
