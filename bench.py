@@ -133,13 +133,18 @@ def xt_step(ab, dist, source: str = 'cells', cells=None, shared: bool = True):
     codes = ops.xt_rate_codes_buffer(ab.n, ab.device) if source == 'codes' else None
     rate_out = torch.empty(max((ab.n + 15) // 16 * 16, 16), dtype=torch.float64, device=ab.device)
 
-    def start():
+    def count():
         if source == 'none':  # --ab diagnostic only: the VAEP kernels without the xT part
             return
         if source == 'cells':
-            acc = ops.xt_count_cells(cells, ab.n, 16, 12, shared=shared)
+            state['acc'] = ops.xt_count_cells(cells, ab.n, 16, 12, shared=shared)
         else:
-            acc = ops.xt_count(ab, 16, 12, codes=codes, shared=shared)
+            state['acc'] = ops.xt_count(ab, 16, 12, codes=codes, shared=shared)
+
+    def reduce():
+        if source == 'none':
+            return
+        acc = state['acc']
         if dist is not None and dist.get_backend() == 'nccl':
             shard.allreduce_xt_counts(acc.shot, acc.goal, acc.move, acc.trans, acc.err)
         elif dist is not None:  # gloo rehearsal: the same sum through host memory
@@ -147,7 +152,10 @@ def xt_step(ab, dist, source: str = 'cells', cells=None, shared: bool = True):
                 h = t.cpu()
                 dist.all_reduce(h)
                 t.copy_(h)
-        state['acc'] = acc
+
+    def start():
+        count()
+        reduce()
 
     def finish():
         if source == 'none':
@@ -160,6 +168,7 @@ def xt_step(ab, dist, source: str = 'cells', cells=None, shared: bool = True):
         else:
             ops.xt_rate(ab, sol.mats[3].reshape(12, 16), 16, 12)
         state['sol'] = sol
+    start.count, start.reduce = count, reduce
     return start, finish, state
 
 
@@ -296,18 +305,26 @@ def rate_extra(ab, out, n, dev, reps: int = 5) -> dict:
     models = [trees.TreeEnsemble.from_xgboost_json(
         trees.synthetic_xgboost_json(len(kinds), n_trees=100, depth=3, seed=s, feature_kinds=kinds))
         for s in (1, 2)]
-    ps = models[0].predict_blocks(out)
-    pc = models[1].predict_blocks(out)
+    # VAEP.rate's features: the bool features as bitmaps (what the staged walk reads)
+    fbits = ops.features(ab, SPADL_DEFAULT, 3, num_tile=out.Rn, bool_bits=True)
+    ps = models[0].predict_blocks(fbits)
+    pc = models[1].predict_blocks(fbits)
     val = torch.empty((3, (n + 15) // 16 * 16), dtype=torch.float32, device=dev)
-    ms_tree = _events_ms(lambda: models[0].predict_blocks(out, out=ps), reps)
+    ms_feat = _events_ms(lambda: ops.features(ab, SPADL_DEFAULT, 3, out=fbits), reps)
+    ms_tree = _events_ms(lambda: models[0].predict_blocks(fbits, out=ps), reps)
+    ms_block = _events_ms(lambda: models[0].predict_blocks(out, out=ps), reps)
     ms_gather = _events_ms(lambda: models[0].predict_blocks(out, out=ps, method='gather'), reps)
     ms_formula = _events_ms(lambda: ops.formula(ab, ps, pc, val), reps)
-    return {'workload': 'VAEP.rate on device: 2 x xgboost-shaped tree ensembles (100 trees, depth '
-                        '3) on the cfg2 feature blocks + formula (float32 probabilities)',
-            'method': 'staged condition walk (sa_tree_predict_staged)',
-            'ms_per_model': round(ms_tree, 4), 'ms_per_model_gather_walk': round(ms_gather, 4),
-            'ms_formula_f32': round(ms_formula, 4),
-            'actions_per_s_predict_both_models': round(n / (2 * ms_tree) * 1e3, 1)}
+    del fbits
+    return {'workload': 'VAEP.rate on device: features (bool features as bitmaps) + 2 x '
+                        'xgboost-shaped tree ensembles (100 trees, depth 3) + formula (float32 '
+                        'probabilities), cfg2 actions',
+            'method': 'staged condition walk (sa_tree_predict_staged) over the bitmaps',
+            'ms_features_bitmap_form': round(ms_feat, 4), 'ms_per_model': round(ms_tree, 4),
+            'ms_per_model_from_bool_block': round(ms_block, 4),
+            'ms_per_model_gather_walk': round(ms_gather, 4), 'ms_formula_f32': round(ms_formula, 4),
+            'ms_rate_total': round(ms_feat + 2 * ms_tree + ms_formula, 4),
+            'actions_per_s_rate': round(n / (ms_feat + 2 * ms_tree + ms_formula) * 1e3, 1)}
 
 
 def e2e_extra(d, games: int, reps: int = 2) -> dict:
@@ -518,7 +535,7 @@ def main() -> None:
                    'labels_formula': lambda: ops.labels_formula(ab, ps, pc, 10, lab, val)}
         calls = tuple(by_name[k] for k in order)
         # cm=1: the count pass runs on the main stream right after num_features, in the fast
-        # one-workgroup-per-CU shape; the side stream takes the solve and the rate
+        # one-workgroup-per-CU shape; the side stream takes the all-reduce, solve and rate
         cm = int(spec.get('cm', 0)) and overlap
         xt_start, xt_finish, xt_last = xt_step(ab, dist, xt, cells, shared=overlap and not cm)
         nv = len(calls)
@@ -541,17 +558,19 @@ def main() -> None:
                 pj.record(par_s)
             for i, call in enumerate(calls):
                 if overlap and i == fork:
-                    if cm:
+                    if cm:  # the count pass on the main stream; its all-reduce on the side
                         if ev is not None:
                             ev[nv][0].record(main_s)
-                        xt_start()
+                        xt_start.count()
                     fk = torch.cuda.Event()
                     fk.record(main_s)
                     side.wait_event(fk)
                     with torch.cuda.stream(side):
                         if ev is not None and not cm:
                             ev[nv][0].record(side)
-                        if not cm:
+                        if cm:
+                            xt_start.reduce()
+                        else:
                             xt_start()
                 if par and i == ib:
                     main_s.wait_event(pj)
@@ -695,8 +714,8 @@ def main() -> None:
                                   'codes': 'coordinates (count) + rate operands',
                                   'coords': 'coordinates'}[base['xt']],
                        'stream': 'main (serial)' if args.serial else
-                       (f"count pass on the main stream after {base['fork']} VAEP call(s), solve "
-                        f"and rate on a {base['prio']}-priority side stream overlapped with the rest"
+                       (f"count pass on the main stream after {base['fork']} VAEP call(s); all-reduce, "
+                        f"solve and rate on a {base['prio']}-priority side stream overlapped with the rest"
                         if base['cm'] else
                         f"{base['prio']}-priority side stream, forked after {base['fork']} VAEP "
                         'call(s), overlapped with the rest')}

@@ -143,6 +143,15 @@ int sa_vaep_features_xt(const sa_actions* a, const sa_feature_plan* plan, const 
                         const sa_block* f64_out, const sa_block* i64_out, int32_t xt_l, int32_t xt_w,
                         uint32_t* xt_cells, void* stream);
 
+/* sa_vaep_features with the bool features written as bitmaps instead of a bool block (the
+ * on-device VAEP.rate: the tree kernels read one bit per value, 64 instead of 515 B/action
+ * written; windowed mode): bitmap c (plan bool column c, c < n_bool_cols) at bool_bits + c * bits_stride, bit i
+ * of byte k = row 8k + i (the Arrow layout of sa_pack_bits), rows >= n clear; bits_stride even
+ * and >= 2 * ceil(n / 16) (a multiple of 8 for sa_tree_predict_staged). */
+int sa_vaep_features_bits(const sa_actions* a, const sa_feature_plan* plan, uint8_t* bool_bits,
+                          int64_t bits_stride, int32_t n_bool_cols, const sa_block* f64_out,
+                          const sa_block* i64_out, void* stream);
+
 /* goalscore alone (vaep/features.py:505-539; atomic/vaep/features.py:229-260): writes the
  * goalscore_team / _opponent / _diff columns col, col+1, col+2 of the i64 block.  Also
  * launched by sa_vaep_features when the plan requests SA_XFN_GOALSCORE. */
@@ -416,8 +425,9 @@ int sa_tree_predict(const void* nodes, int32_t n_nodes, const int32_t* roots, co
  * first child + its condition bit; leaves are self-loops (condition 0, first child = the leaf);
  * leaf: T[n_nodes] leaf values; roots[n_trees]: each tree's root; tree_depth[n_trees]: split
  * levels of each tree; p_out[n]: the probabilities.  T = float for f32 = 1 (xgboost), else
- * double.  sa_tree_staged_lds_bytes: the LDS a model needs (<= 160 KiB; n_cond = 1 + n_bool +
- * n_num). */
+ * double.  The bool columns come from bool_blk, or -- when bool_bits is not NULL -- from the
+ * bitmaps of sa_vaep_features_bits (bool_cols index its bitmaps; bits_stride a multiple of 8).
+ * sa_tree_staged_lds_bytes: the LDS a model needs (<= 160 KiB; n_cond = 1 + n_bool + n_num). */
 typedef struct sa_tree_model {
   const void* nodes;
   const void* leaf;
@@ -432,8 +442,9 @@ int64_t sa_tree_staged_lds_bytes(int32_t n_nodes, int32_t n_cond, int32_t f32);
 int sa_tree_predict_staged(const sa_tree_model* model, const int32_t* bool_cols, int32_t n_bool,
                            const int32_t* num_cols, const int32_t* col_start, int32_t n_ncol,
                            const void* num_thr, const int32_t* num_dl, int32_t n_num,
-                           const sa_block* bool_blk, const sa_block* f64_blk, const sa_block* i64_blk,
-                           int64_t n, int32_t le, int32_t f32, void* stream);
+                           const sa_block* bool_blk, const uint8_t* bool_bits, int64_t bits_stride,
+                           const sa_block* f64_blk, const sa_block* i64_blk, int64_t n, int32_t le,
+                           int32_t f32, void* stream);
 
 /* ---- runtime ------------------------------------------------------------------ */
 int sa_abi_version(void);

@@ -40,10 +40,13 @@ def main():
     args = ap.parse_args()
     ab = B.ActionBatch.from_columns(synthetic.spadl_games(args.games))
     fb = ops.features(ab, SPADL_DEFAULT, 3, bool_tile=1024, num_tile=128)
+    fbits = ops.features(ab, SPADL_DEFAULT, 3, num_tile=128, bool_bits=True)
+    out_feat = {'features_block_ms': _ms(lambda: ops.features(ab, SPADL_DEFAULT, 3, out=fb)),
+                'features_bitmaps_ms': _ms(lambda: ops.features(ab, SPADL_DEFAULT, 3, out=fbits))}
     kinds = [k for _, k, _ in fb.plan.order]
     te = trees.TreeEnsemble.from_xgboost_json(trees.synthetic_xgboost_json(
         len(kinds), n_trees=100, depth=3, seed=1, feature_kinds=kinds))
-    out = {'n': ab.n}
+    out = {'n': ab.n, **out_feat}
     lay = te.staged_layout(te.feature_slots(fb.plan))
     out['model'] = {'nodes': len(lay['models'][0]['nodes']), 'bool_conditions': len(lay['bool_cols']),
                     'numeric_conditions': len(lay['num_slots']),
@@ -53,7 +56,8 @@ def main():
             _native._lib = _native.load_library(os.path.join(
                 ROOT, 'socceraction_amd', '_lib', f'libsocceraction_amd_{name}.so'))
         te._dev = None
-        res = {'staged': _ms(lambda: te.predict_blocks(fb, method='staged'))}
+        res = {'staged': _ms(lambda: te.predict_blocks(fb, method='staged')),
+               'staged_from_bitmaps': _ms(lambda: te.predict_blocks(fbits, method='staged'))}
         if name == 'default':
             res['gather'] = _ms(lambda: te.predict_blocks(fb, method='gather'))
         out[name] = res

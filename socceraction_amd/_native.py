@@ -110,6 +110,9 @@ _SIGNATURES = {
                                          ctypes.c_int32, _p, _p, _p, _p, _p, _p,
                                          ctypes.c_int32, _p]),
     'sa_xt_rate_codes': (ctypes.c_int, [_p, ctypes.c_int64, _p, _p, _p, _p]),
+    'sa_vaep_features_bits': (ctypes.c_int, [ctypes.POINTER(SaActions), ctypes.POINTER(SaFeaturePlan),
+                                             _p, ctypes.c_int64, ctypes.c_int32, ctypes.POINTER(SaBlock),
+                                             ctypes.POINTER(SaBlock), _p]),
     'sa_vaep_features_xt': (ctypes.c_int, [ctypes.POINTER(SaActions),
                                            ctypes.POINTER(SaFeaturePlan), ctypes.POINTER(SaBlock),
                                            ctypes.POINTER(SaBlock), ctypes.POINTER(SaBlock),
@@ -154,9 +157,9 @@ _SIGNATURES = {
     'sa_tree_staged_lds_bytes': (ctypes.c_int64, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]),
     'sa_tree_predict_staged': (ctypes.c_int, [ctypes.POINTER(SaTreeModel), _p, ctypes.c_int32, _p, _p,
                                               ctypes.c_int32, _p, _p, ctypes.c_int32,
+                                              ctypes.POINTER(SaBlock), _p, ctypes.c_int64,
                                               ctypes.POINTER(SaBlock), ctypes.POINTER(SaBlock),
-                                              ctypes.POINTER(SaBlock), ctypes.c_int64, ctypes.c_int32,
-                                              ctypes.c_int32, _p]),
+                                              ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, _p]),
     'sa_abi_version': (ctypes.c_int, []),
     'sa_last_error': (ctypes.c_char_p, []),
     'sa_build_id': (ctypes.c_char_p, []),

@@ -271,13 +271,37 @@ struct CondModel {  // the model's walk
 // Condition bits of the TS_ROWS rows from R0 into M8 (TS_ROWS threads, s = 0 .. TS_ROWS-1; row
 // R0 + s belongs to thread s, whole waves).
 template <typename A, bool LE>
-__device__ __forceinline__ void stage_conditions(const CondSet<A>& P, const sa_block& Bb, const sa_block& Bf,
-                                                 const sa_block& Bi, int64_t n, int64_t R0, int s,
-                                                 uint8_t* __restrict__ M8) {
+__device__ __forceinline__ void stage_conditions(const CondSet<A>& P, const sa_block& Bb, const uint8_t* __restrict__ bits,
+                                                 int64_t bstride, const sa_block& Bf, const sa_block& Bi, int64_t n,
+                                                 int64_t R0, int s, uint8_t* __restrict__ M8) {
   const int wv = s >> 6, lane = s & 63;
   if (s < TS_CSTRIDE / 4) reinterpret_cast<uint32_t*>(M8)[s] = 0;  // condition 0: never set
-  // bool conditions: item it = (column u, 16-row piece p) -> 16 bits
-  const int nbi = P.n_bool * TS_PIECES;
+  if (bits) {
+    // bool conditions from bitmaps: item it = (column u, 64-row word q): one 8-B load
+    constexpr int WQ = TS_ROWS / 64;
+    const int nwi = P.n_bool * WQ;
+    for (int i0 = 0; i0 < nwi; i0 += TS_ROWS * TS_B) {
+      uint64_t w[TS_B];
+#pragma unroll
+      for (int b = 0; b < TS_B; ++b) {
+        const int it = i0 + b * TS_ROWS + s;
+        const int64_t r = R0 + 64 * (it % WQ);
+        w[b] = it < nwi && r < n ? *reinterpret_cast<const uint64_t*>(bits + (int64_t)P.bool_cols[it / WQ] * bstride + r / 8)
+                                  : 0ull;
+      }
+#pragma unroll
+      for (int b = 0; b < TS_B; ++b) {
+        const int it = i0 + b * TS_ROWS + s;
+        if (it < nwi) {
+          uint32_t* dst = reinterpret_cast<uint32_t*>(M8 + (1 + it / WQ) * TS_CSTRIDE + 8 * (it % WQ));
+          dst[0] = (uint32_t)w[b];
+          dst[1] = (uint32_t)(w[b] >> 32);
+        }
+      }
+    }
+  }
+  // bool conditions from the bool block: item it = (column u, 16-row piece p) -> 16 bits
+  const int nbi = bits ? 0 : P.n_bool * TS_PIECES;
   for (int i0 = 0; i0 < nbi; i0 += TS_ROWS * TS_B) {
     u32x4 w[TS_B];
 #pragma unroll
@@ -381,7 +405,8 @@ __device__ __forceinline__ A walk_conditions(const CondModel<A>& P, const uint32
 template <bool F32, bool LE>
 __global__ __launch_bounds__(TS_ROWS) void tree_cond_kernel(CondSet<typename std::conditional<F32, float, double>::type> C,
                                                             CondModel<typename std::conditional<F32, float, double>::type> P,
-                                                            sa_block Bb, sa_block Bf, sa_block Bi, int64_t n) {
+                                                            sa_block Bb, const uint8_t* __restrict__ bits, int64_t bstride,
+                                                            sa_block Bf, sa_block Bi, int64_t n) {
   using A = typename std::conditional<F32, float, double>::type;
   extern __shared__ __attribute__((aligned(16))) unsigned char ts_lds[];
   // LDS carved by integer offsets from ts_lds (a pointer cast through uintptr_t would make
@@ -397,7 +422,7 @@ __global__ __launch_bounds__(TS_ROWS) void tree_cond_kernel(CondSet<typename std
     LV[k] = P.leaf[k];
   }
   const int64_t R0 = (int64_t)blockIdx.x * TS_ROWS;
-  stage_conditions<A, LE>(C, Bb, Bf, Bi, n, R0, tid, M8);
+  stage_conditions<A, LE>(C, Bb, bits, bstride, Bf, Bi, n, R0, tid, M8);
   __syncthreads();
   const int64_t j = R0 + tid;
   if (j >= n) return;
@@ -467,10 +492,12 @@ extern "C" int64_t sa_tree_staged_lds_bytes(int32_t n_nodes, int32_t n_cond, int
 extern "C" int sa_tree_predict_staged(const sa_tree_model* model, const int32_t* bool_cols, int32_t n_bool,
                                       const int32_t* num_cols, const int32_t* col_start, int32_t n_ncol,
                                       const void* num_thr, const int32_t* num_dl, int32_t n_num,
-                                      const sa_block* bool_blk, const sa_block* f64_blk, const sa_block* i64_blk,
-                                      int64_t n, int32_t le, int32_t f32, void* stream) {
+                                      const sa_block* bool_blk, const uint8_t* bool_bits, int64_t bits_stride,
+                                      const sa_block* f64_blk, const sa_block* i64_blk, int64_t n, int32_t le,
+                                      int32_t f32, void* stream) {
   if (!model || n < 0 || 1 + n_bool + n_num > 65536 || n_bool < 0 || n_num < 0 ||
-      (n_bool > 0 && (!bool_cols || !bool_blk)) || n_ncol < 0 ||
+      (n_bool > 0 && (!bool_cols || (!bool_blk && !bool_bits))) || n_ncol < 0 ||
+      (bool_bits && (bits_stride % 8 || bits_stride < 8 * ((n + 63) / 64) || ((uintptr_t)bool_bits & 7u))) ||
       (n_num > 0 && (n_ncol < 1 || !num_cols || !col_start || !num_thr || !num_dl)))
     return fail(SA_EINVAL, "bad staged tree arguments");
   const sa_tree_model& m = *model;
@@ -481,7 +508,7 @@ extern "C" int sa_tree_predict_staged(const sa_tree_model* model, const int32_t*
   if (lds > 160 * 1024) return fail(SA_EINVAL, "staged tree model needs %lld B of LDS", (long long)lds);
   sa_block z{nullptr, 0, 0, 16};
   const sa_block Bb = bool_blk ? *bool_blk : z, Bf = f64_blk ? *f64_blk : z, Bi = i64_blk ? *i64_blk : z;
-  if (n_bool > 0 && (Bb.tile_rows % 16 != 0 || !aligned16(Bb.data)))
+  if (n_bool > 0 && !bool_bits && (Bb.tile_rows % 16 != 0 || !aligned16(Bb.data)))
     return fail(SA_EINVAL, "bool block: 16-row tiles, 16-byte aligned");
   if (n == 0) return SA_OK;
   const dim3 grid((unsigned)((n + TS_ROWS - 1) / TS_ROWS)), block(TS_ROWS);
@@ -492,7 +519,8 @@ extern "C" int sa_tree_predict_staged(const sa_tree_model* model, const int32_t*
                  n_num};                                                                                \
     CondModel<A> P{(const uint32_t*)m.nodes, (const A*)m.leaf, m.roots, m.tree_depth, m.n_nodes,        \
                    m.n_trees,                m.base_margin,    m.p_out};                                \
-    hipLaunchKernelGGL((tree_cond_kernel<F, LEQ>), grid, block, (size_t)lds, st, C, P, Bb, Bf, Bi, n);    \
+    hipLaunchKernelGGL((tree_cond_kernel<F, LEQ>), grid, block, (size_t)lds, st, C, P, Bb, bool_bits,     \
+                       bits_stride, Bf, Bi, n);                                                          \
   } while (0)
   if (f32 && le)
     SA_TS_LAUNCH(true, true, float);

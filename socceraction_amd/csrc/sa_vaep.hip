@@ -59,6 +59,8 @@ struct FeatArgs {
   int64_t Rb, Rf, Ri;  // rows per tile of each block (include/socceraction_amd.h)
   uint32_t* xt_cells;  // optional: xT cell code of every action (sa_vaep_features_xt)
   int32_t xt_l, xt_w;
+  uint16_t* bbits;     // optional: bool features as bitmaps instead of bout (sa_vaep_features_bits)
+  int64_t bstride;     // u16 per bitmap
 };
 
 // Workgroups are dispatched round-robin over the 8 XCDs (XCD = blockIdx % 8).  Writing the
@@ -137,6 +139,11 @@ __device__ __forceinline__ void st16(P* p, V v) {
 #endif
 }
 
+// 0x01-per-byte mask -> 4 bits
+__device__ __forceinline__ uint32_t pack4(uint32_t x) {
+  return (x & 1u) | ((x >> 7) & 2u) | ((x >> 14) & 4u) | ((x >> 21) & 8u);
+}
+
 // Stores into tiled blocks: `base` already points at the lane's (tile, row) position of
 // column 0, so column c is c * R elements further.
 __device__ __forceinline__ void st_bool16(uint8_t* __restrict__ base, int64_t col, int64_t C, int64_t R,
@@ -144,6 +151,21 @@ __device__ __forceinline__ void st_bool16(uint8_t* __restrict__ base, int64_t co
   u32x4 v = {w0, w1, w2, w3};
   SA_DGUARD(col >= 0 && col < C, col, return);
   st16(base + col * R, v);
+}
+
+// The 16 bool values (0x01 bytes) of a lane's rows j0 .. j0+15 of column `col`: 16 bytes into
+// the tiled bool block, or -- bitmap mode -- 16 bits into bitmap `col` (rows >= n cleared).
+template <bool BITS>
+__device__ __forceinline__ void st_bool_out(const FeatArgs& a, uint8_t* __restrict__ bb, int64_t col, int64_t j0,
+                                            uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
+  if (BITS) {
+    SA_DGUARD(col >= 0 && col < a.Cb, col, return);
+    uint32_t b = pack4(w0) | (pack4(w1) << 4) | (pack4(w2) << 8) | (pack4(w3) << 12);
+    if (a.a.n - j0 < 16) b &= (1u << (a.a.n - j0)) - 1u;
+    a.bbits[col * a.bstride + j0 / 16] = (uint16_t)b;
+  } else {
+    st_bool16(bb, col, a.Cb, a.Rb, w0, w1, w2, w3);
+  }
 }
 
 __device__ __forceinline__ void st_f64x2(double* __restrict__ base, int64_t col, int64_t C, int64_t R,
@@ -166,10 +188,6 @@ __device__ __forceinline__ double polar_angle(double dy, double dx) {
   return isnan(a) ? 0.0 : a;
 }
 
-// 0x01-per-byte mask -> 4 bits
-__device__ __forceinline__ uint32_t pack4(uint32_t x) {
-  return (x & 1u) | ((x >> 7) & 2u) | ((x >> 14) & 4u) | ((x >> 21) & 8u);
-}
 
 // goal / owngoal bytes of a word of type / result bytes (vaep/labels.py:28-33;
 // atomic/vaep/labels.py:27-28)
@@ -200,7 +218,7 @@ constexpr int BOOL_TILE = 1024;  // rows per tile of the bool block image
 constexpr int CG_WAVES = 4;  // waves per workgroup
 #define CG_EQ(w, v) bytes_eq((w), (v))
 
-template <bool ATOMIC, bool EXPLICIT>
+template <bool ATOMIC, bool EXPLICIT, bool BITS>
 __global__ __launch_bounds__(64 * CG_WAVES) void bool_colgroup_kernel(FeatArgs args, int ngroups,
                                                                       int gcols) {
   const int lane = threadIdx.x & (WAVE - 1);
@@ -220,7 +238,7 @@ __global__ __launch_bounds__(64 * CG_WAVES) void bool_colgroup_kernel(FeatArgs a
   // team_1 .. team_{K-1} columns inside [c_lo, c_hi)?
   const bool need_team = tcol >= 0 && K > 1 && tcol < c_hi && tcol + K - 1 > c_lo;
   if (tile0 >= n || c_lo >= c_hi) return;
-  uint8_t* bb = args.bout + tile_off(j0 < n ? j0 : tile0, 0, args.Cb, R);
+  uint8_t* bb = BITS ? nullptr : args.bout + tile_off(j0 < n ? j0 : tile0, 0, args.Cb, R);
   if (j0 >= n) return;
   // d = min(j - seg_start, 15) per action: segment of the tile start (same for all lanes),
   // then each lane advances to its own rows
@@ -293,7 +311,7 @@ __global__ __launch_bounds__(64 * CG_WAVES) void bool_colgroup_kernel(FeatArgs a
       range(base, ntypes, v0, v1);
       for (int u = v0; u < v1; ++u) {
         if (!ATOMIC) {
-          st_bool16(bb, base + u, args.Cb, R, CG_EQ(tw[0], u), CG_EQ(tw[1], u), CG_EQ(tw[2], u),
+          st_bool_out<BITS>(args, bb, base + u, j0, CG_EQ(tw[0], u), CG_EQ(tw[1], u), CG_EQ(tw[2], u),
                     CG_EQ(tw[3], u));
         } else {
           // 33 atomic names, 32 unique: 'interception' (ids 10 and 24) is ONE column true for
@@ -307,7 +325,7 @@ __global__ __launch_bounds__(64 * CG_WAVES) void bool_colgroup_kernel(FeatArgs a
             m2 |= CG_EQ(tw[2], AT_INTERCEPTION2);
             m3 |= CG_EQ(tw[3], AT_INTERCEPTION2);
           }
-          st_bool16(bb, base + u, args.Cb, R, m0, m1, m2, m3);
+          st_bool_out<BITS>(args, bb, base + u, j0, m0, m1, m2, m3);
         }
       }
     }
@@ -315,7 +333,7 @@ __global__ __launch_bounds__(64 * CG_WAVES) void bool_colgroup_kernel(FeatArgs a
       const int base = c_res + i * N_RESULTS;
       range(base, N_RESULTS, v0, v1);
       for (int r = v0; r < v1; ++r)
-        st_bool16(bb, base + r, args.Cb, R, CG_EQ(rw[0], r), CG_EQ(rw[1], r), CG_EQ(rw[2], r),
+        st_bool_out<BITS>(args, bb, base + r, j0, CG_EQ(rw[0], r), CG_EQ(rw[1], r), CG_EQ(rw[2], r),
                   CG_EQ(rw[3], r));
     }
     if (c_tr >= 0) {
@@ -327,7 +345,7 @@ __global__ __launch_bounds__(64 * CG_WAVES) void bool_colgroup_kernel(FeatArgs a
 #pragma unroll
         for (int q = 0; q < 4; ++q) cw[q] = (tw[q] << 2) + (tw[q] << 1) + rw[q];
         for (int code = v0; code < v1; ++code)
-          st_bool16(bb, base + code, args.Cb, R, CG_EQ(cw[0], code), CG_EQ(cw[1], code),
+          st_bool_out<BITS>(args, bb, base + code, j0, CG_EQ(cw[0], code), CG_EQ(cw[1], code),
                     CG_EQ(cw[2], code), CG_EQ(cw[3], code));
       }
     }
@@ -335,7 +353,7 @@ __global__ __launch_bounds__(64 * CG_WAVES) void bool_colgroup_kernel(FeatArgs a
       const int base = c_bp + i * N_BODYPARTS;
       range(base, N_BODYPARTS, v0, v1);
       for (int b = v0; b < v1; ++b)
-        st_bool16(bb, base + b, args.Cb, R, CG_EQ(bw[0], b), CG_EQ(bw[1], b), CG_EQ(bw[2], b),
+        st_bool_out<BITS>(args, bb, base + b, j0, CG_EQ(bw[0], b), CG_EQ(bw[1], b), CG_EQ(bw[2], b),
                   CG_EQ(bw[3], b));
     }
     const int tc = tcol + i - 1;
@@ -358,7 +376,7 @@ __global__ __launch_bounds__(64 * CG_WAVES) void bool_colgroup_kernel(FeatArgs a
         }
         m[mm >> 2] |= (uint32_t)(t0 == ti) << (8 * (mm & 3));
       }
-      st_bool16(bb, tc, args.Cb, R, m[0], m[1], m[2], m[3]);
+      st_bool_out<BITS>(args, bb, tc, j0, m[0], m[1], m[2], m[3]);
     }
   }
 }
@@ -1175,7 +1193,8 @@ static int check_block(const sa_block* b, int64_t n, int64_t quantum, const char
 
 static int launch_features(const sa_actions* a, const sa_feature_plan* plan, const sa_block* bool_out,
                            const sa_block* f64_out, const sa_block* i64_out, int32_t xt_l,
-                           int32_t xt_w, uint32_t* xt_cells, void* stream);
+                           int32_t xt_w, uint32_t* xt_cells, void* stream, uint8_t* bits = nullptr,
+                           int64_t bits_stride = 0, int32_t n_bits = 0);
 
 extern "C" int sa_vaep_features(const sa_actions* a, const sa_feature_plan* plan,
                                 const sa_block* bool_out, const sa_block* f64_out,
@@ -1195,9 +1214,22 @@ extern "C" int sa_vaep_features_xt(const sa_actions* a, const sa_feature_plan* p
   return launch_features(a, plan, bool_out, f64_out, i64_out, xt_l, xt_w, xt_cells, stream);
 }
 
+extern "C" int sa_vaep_features_bits(const sa_actions* a, const sa_feature_plan* plan, uint8_t* bool_bits,
+                                     int64_t bits_stride, int32_t n_bool_cols, const sa_block* f64_out,
+                                     const sa_block* i64_out, void* stream) {
+  if (!a) return fail(SA_EINVAL, "null sa_actions");
+  if (!bool_bits || n_bool_cols < 1 || bits_stride < 2 * ((a->n + 15) / 16) || bits_stride % 2 ||
+      ((uintptr_t)bool_bits & 1u))
+    return fail(SA_EINVAL, "bool bitmaps: even stride of at least ceil(n/16)*2 bytes, 2-byte aligned");
+  if (a->n_frames != 1) return fail(SA_EINVAL, "bool bitmaps: windowed mode only");
+  return launch_features(a, plan, nullptr, f64_out, i64_out, 0, 0, nullptr, stream, bool_bits, bits_stride,
+                         n_bool_cols);
+}
+
 static int launch_features(const sa_actions* a, const sa_feature_plan* plan, const sa_block* bool_out,
                            const sa_block* f64_out, const sa_block* i64_out, int32_t xt_l,
-                           int32_t xt_w, uint32_t* xt_cells, void* stream) {
+                           int32_t xt_w, uint32_t* xt_cells, void* stream, uint8_t* bits,
+                           int64_t bits_stride, int32_t n_bits) {
   int rc = check_actions(a, true);
   if (rc) return rc;
   if (!plan) return fail(SA_EINVAL, "null plan");
@@ -1212,11 +1244,11 @@ static int launch_features(const sa_actions* a, const sa_feature_plan* plan, con
     wi |= plan->i64_col[x] >= 0;
     wn |= plan->f64_col[x] >= 0 || (plan->i64_col[x] >= 0 && x != SA_XFN_GOALSCORE);
   }
-  if (wb && (rc = check_block(bool_out, a->n, SA_BOOL_TILE_QUANTUM, "bool"))) return rc;
+  if (wb && !bits && (rc = check_block(bool_out, a->n, SA_BOOL_TILE_QUANTUM, "bool"))) return rc;
   if (wf && (rc = check_block(f64_out, a->n, SA_NUM_TILE_QUANTUM, "f64"))) return rc;
   if (wi && (rc = check_block(i64_out, a->n, SA_NUM_TILE_QUANTUM, "i64"))) return rc;
   for (int x = 0; x < SA_XFN_COUNT; ++x) {
-    if ((wb && plan->bool_col[x] >= bool_out->n_cols) || (wf && plan->f64_col[x] >= f64_out->n_cols) ||
+    if ((wb && plan->bool_col[x] >= (bits ? n_bits : bool_out->n_cols)) || (wf && plan->f64_col[x] >= f64_out->n_cols) ||
         (wi && plan->i64_col[x] >= i64_out->n_cols))
       return fail(SA_EINVAL, "plan column offset beyond the block's column count");
   }
@@ -1237,18 +1269,20 @@ static int launch_features(const sa_actions* a, const sa_feature_plan* plan, con
   hipStream_t st = (hipStream_t)stream;
   FeatArgs args{*a,
                 *plan,
-                wb ? (uint8_t*)bool_out->data : nullptr,
+                wb && !bits ? (uint8_t*)bool_out->data : nullptr,
                 wf ? (double*)f64_out->data : nullptr,
                 wi ? (int64_t*)i64_out->data : nullptr,
-                wb ? bool_out->n_cols : 0,
+                wb ? (bits ? (int64_t)n_bits : bool_out->n_cols) : 0,
                 wf ? f64_out->n_cols : 0,
                 wi ? i64_out->n_cols : 0,
-                wb ? bool_out->tile_rows : 16,
+                wb && !bits ? bool_out->tile_rows : BOOL_TILE,
                 wf ? f64_out->tile_rows : 16,
                 wi ? i64_out->tile_rows : 16,
                 xt_cells,
                 xt_l,
-                xt_w};
+                xt_w,
+                wb ? (uint16_t*)bits : nullptr,
+                bits_stride / 2};
   const dim3 grid(xcd_grid((a->n + BLOCK_ACTS - 1) / BLOCK_ACTS)), block(BLOCK_WAVES * WAVE);
   const bool expl = a->n_frames > 1;
   if (wb) {  // one wave per (tile, group of ~32 columns), XCD-contiguous sweep order
@@ -1256,16 +1290,21 @@ static int launch_features(const sa_actions* a, const sa_feature_plan* plan, con
     const int gc = (int)((args.Cb + ng - 1) / ng);
     const int64_t waves = (a->n + BOOL_TILE - 1) / BOOL_TILE * ng;
     const dim3 cgrid(xcd_grid((waves + CG_WAVES - 1) / CG_WAVES)), cblock(WAVE * CG_WAVES);
-    if (a->atomic) {
-      if (expl)
-        hipLaunchKernelGGL((bool_colgroup_kernel<true, true>), cgrid, cblock, 0, st, args, ng, gc);
+    if (bits) {  // the on-device VAEP.rate: SPADL or atomic, windowed or explicit, as bitmaps
+      if (a->atomic)
+        hipLaunchKernelGGL((bool_colgroup_kernel<true, false, true>), cgrid, cblock, 0, st, args, ng, gc);
       else
-        hipLaunchKernelGGL((bool_colgroup_kernel<true, false>), cgrid, cblock, 0, st, args, ng, gc);
+        hipLaunchKernelGGL((bool_colgroup_kernel<false, false, true>), cgrid, cblock, 0, st, args, ng, gc);
+    } else if (a->atomic) {
+      if (expl)
+        hipLaunchKernelGGL((bool_colgroup_kernel<true, true, false>), cgrid, cblock, 0, st, args, ng, gc);
+      else
+        hipLaunchKernelGGL((bool_colgroup_kernel<true, false, false>), cgrid, cblock, 0, st, args, ng, gc);
     } else {
       if (expl)
-        hipLaunchKernelGGL((bool_colgroup_kernel<false, true>), cgrid, cblock, 0, st, args, ng, gc);
+        hipLaunchKernelGGL((bool_colgroup_kernel<false, true, false>), cgrid, cblock, 0, st, args, ng, gc);
       else
-        hipLaunchKernelGGL((bool_colgroup_kernel<false, false>), cgrid, cblock, 0, st, args, ng, gc);
+        hipLaunchKernelGGL((bool_colgroup_kernel<false, false, false>), cgrid, cblock, 0, st, args, ng, gc);
     }
     rc = check_launch("bool_colgroup_kernel");
     if (rc) return rc;

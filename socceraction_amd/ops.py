@@ -34,12 +34,30 @@ class FeatureBlocks:
     n: int
     Rb: int
     Rn: int
-    bool_block: torch.Tensor
+    bool_block: Optional[torch.Tensor]
     f64_block: torch.Tensor
     i64_block: torch.Tensor
+    # bitmap form (features(..., bool_bits=True), the on-device VAEP.rate): the bool features
+    # as Arrow bitmaps [n_bool, words] int64 (bit i of word w = row 64w + i) instead of a block
+    bool_bits: Optional[torch.Tensor] = None
+
+    @property
+    def device(self):
+        return self.f64_block.device
 
     def _blk(self, kind: str) -> torch.Tensor:
+        if kind == 'b' and self.bool_block is None:
+            self.bool_block = self._unpacked_bools()
+            self.Rb = self.bool_block.shape[2]
         return {'b': self.bool_block, 'f': self.f64_block, 'i': self.i64_block}[kind]
+
+    def _unpacked_bools(self) -> torch.Tensor:
+        """A one-tile bool block [1, n_bool, ld] of the bitmaps (for host export)."""
+        ld = _ld(self.n)
+        bits = self.bool_bits.view(torch.uint8)[:, :ld // 8]
+        shifts = torch.arange(8, device=bits.device, dtype=torch.uint8)
+        out = ((bits.unsqueeze(-1) >> shifts) & 1).reshape(bits.shape[0], -1)[:, :ld]
+        return out.unsqueeze(0).contiguous()
 
     def block(self, kind: str) -> torch.Tensor:
         """``[n_cols, n]`` view (one tile) or untiled copy (several tiles), on device."""
@@ -73,8 +91,12 @@ class FeatureBlocks:
     def sa_blocks(self):
         """The three ``sa_block`` descriptors of the C ABI."""
         out = []
-        for t, R in ((self.bool_block, self.Rb), (self.f64_block, self.Rn),
-                     (self.i64_block, self.Rn)):
+        if self.bool_block is None:  # bitmap form: the bool descriptor only carries the count
+            b = _native.SaBlock()
+            b.data, b.n_cols, b.tile_rows = None, self.plan.n_bool, 1024
+            out.append(b)
+        for t, R in (((self.bool_block, self.Rb),) if self.bool_block is not None else ()) + (
+                (self.f64_block, self.Rn), (self.i64_block, self.Rn)):
             # the kernels write ceil(n / R) whole [C, R] tiles: the tensor must hold them
             if (t.dim() != 3 or t.shape[2] != R or t.shape[0] * R < self.n
                     or not t.is_contiguous()):
@@ -124,10 +146,31 @@ def features_into(s: _native.SaActions, out: FeatureBlocks, xt_cells: Optional[t
 
 def features(batch: ActionBatch, xfns: Sequence[str], k: int, flip: bool = True,
              out: Optional[FeatureBlocks] = None, bool_tile: Optional[int] = None,
-             num_tile: Optional[int] = None) -> FeatureBlocks:
-    """Game-state features of every segment of ``batch`` (windowed mode)."""
+             num_tile: Optional[int] = None, bool_bits: bool = False) -> FeatureBlocks:
+    """Game-state features of every segment of ``batch`` (windowed mode). ``bool_bits``: the
+    bool features as bitmaps (``sa_vaep_features_bits``; 64 instead of 515 B/action written:
+    what the staged tree walk of the on-device ``VAEP.rate`` reads)."""
     plan = out.plan if out is not None else build_plan(xfns, k, batch.atomic)
+    if bool_bits and out is None:
+        words = max(1, (batch.n + 63) // 64)
+        Rn = _ld(batch.n) if num_tile is None else int(num_tile)
+        tn = max(1, -(-batch.n // Rn))
+        out = FeatureBlocks(plan, batch.n, 1024, Rn, None,
+                            torch.empty((tn, plan.n_f64, Rn), dtype=torch.float64, device=batch.device),
+                            torch.empty((tn, plan.n_i64, Rn), dtype=torch.int64, device=batch.device),
+                            torch.empty((max(plan.n_bool, 1), words), dtype=torch.int64,
+                                        device=batch.device))
     out = out or alloc_feature_blocks(plan, batch.n, batch.device, bool_tile, num_tile)
+    if out.bool_bits is not None and out.bool_block is None:
+        _, fb, ib = out.sa_blocks()
+        _native.check(_native.lib().sa_vaep_features_bits(
+            ctypes.byref(batch.struct(flip=flip)), ctypes.byref(out.plan.struct),
+            out.bool_bits.data_ptr(), out.bool_bits.shape[1] * 8, max(plan.n_bool, 1),
+            ctypes.byref(fb), ctypes.byref(ib), stream_handle()))
+        if batch.n % 64:  # the kernel clears rows >= n of the 16-row group holding row n - 1;
+            # the last word's later groups are cleared here
+            out.bool_bits[:, -1] &= (1 << (batch.n % 64)) - 1
+        return out
     features_into(batch.struct(flip=flip), out)
     return out
 

@@ -271,7 +271,8 @@ class TreeEnsemble:
         from .batch import stream_handle
         if method is None and staged is not None:
             method = 'staged' if staged else 'gather'
-        dev = blocks.bool_block.device
+        dev = blocks.device
+        bits = getattr(blocks, 'bool_bits', None) if blocks.bool_block is None else None
         d = self._device(dev)
         slots_np = self.feature_slots(blocks.plan, feature_names)
         n = blocks.n
@@ -308,11 +309,16 @@ class TreeEnsemble:
                     ctypes.byref(rec), ptr('bool_cols'),
                     0 if st['bool_cols'] is None else st['bool_cols'].numel(), ptr('num_cols'),
                     ptr('col_start'), 0 if st['num_cols'] is None else st['num_cols'].numel(),
-                    ptr('num_thr'), ptr('num_dl'), st['n_num'], ctypes.byref(bb), ctypes.byref(fb),
+                    ptr('num_thr'), ptr('num_dl'), st['n_num'], ctypes.byref(bb),
+                    bits.data_ptr() if bits is not None else None,
+                    bits.shape[1] * 8 if bits is not None else 0, ctypes.byref(fb),
                     ctypes.byref(ib), n, int(self.le), int(self.f32), stream_handle()))
                 return out[:n]
             elif method == 'staged':
                 raise ValueError('the staged form of this model does not fit LDS')
+        if bits is not None:  # the gather walk reads bool values from a bool block
+            blocks._blk('b')
+            bb, fb, ib = blocks.sa_blocks()
         slots = torch.from_numpy(slots_np).to(dev)
         _native.check(_native.lib().sa_tree_predict(
             d['nodes'].data_ptr(), len(self.nodes), d['roots'].data_ptr(),

@@ -277,7 +277,8 @@ class VAEP:
         xgboost, float64 for scikit-learn), as in the reference's host path."""
         import torch
         known, _ = self._split_xfns()
-        fb = ops.features(ab, known, self.nb_prev_actions)
+        # the learners read the bool features as bitmaps (64 instead of 515 B/action written)
+        fb = ops.features(ab, known, self.nb_prev_actions, bool_bits=True)
         ps = trees['scores'].predict_blocks(fb)
         pc = trees['concedes'].predict_blocks(fb)
         if ps.dtype != pc.dtype:  # pandas would upcast the mixed pair

@@ -193,3 +193,48 @@ def test_staged_walk_equals_gather_walk(sa, kind):
     ref = te.predict_blocks(fb, method='gather').cpu().numpy()
     np.testing.assert_array_equal(got, ref)
     np.testing.assert_array_equal(te.predict_blocks(fb).cpu().numpy(), ref)  # the default path
+
+
+@pytest.mark.parametrize('atomic', [False, True])
+def test_bool_bitmap_features_and_trees(sa, atomic):
+    """sa_vaep_features_bits: the bool features as bitmaps equal the bool block bit for bit
+    (rows >= n clear), the f64 / i64 blocks are unchanged, host export of the bitmap form equals
+    the block form, and the staged walk reading the bitmaps equals the walk reading the block
+    (float32 xgboost, float64 scikit-learn) -- the on-device VAEP.rate path."""
+    from socceraction_amd import synthetic, catalog
+    from oracle import vaep_oracle as vo
+    from sklearn.ensemble import HistGradientBoostingClassifier
+    B, ops, trees = sa['batch'], sa['ops'], sa['trees']
+    if atomic:
+        d = synthetic.atomic_games(150, seed=6)
+        xfns = ['actiontype', 'actiontype_onehot', 'bodypart', 'bodypart_onehot', 'time', 'team',
+                'time_delta', 'location', 'polar', 'movement_polar', 'direction', 'goalscore']
+    else:
+        d = synthetic.spadl_games(150, seed=6)
+        xfns = vo.SPADL_DEFAULT
+    ab = B.ActionBatch.from_columns(d, atomic=atomic)
+    ref = ops.features(ab, xfns, 3, bool_tile=1024, num_tile=128)
+    got = ops.features(ab, xfns, 3, num_tile=128, bool_bits=True)
+    assert got.bool_block is None and ref.n % 64 != 0
+    rb = ref.block('b').cpu().numpy()
+    bits = got.bool_bits.cpu().numpy().view(np.uint8)
+    unpacked = np.unpackbits(bits, axis=1, bitorder='little')
+    np.testing.assert_array_equal(unpacked[:, :ref.n], rb)
+    assert not unpacked[:, ref.n:].any()
+    for k in 'fi':
+        np.testing.assert_array_equal(got.block(k).cpu().numpy(), ref.block(k).cpu().numpy())
+    if atomic:
+        return
+    kinds = [k for _, k, _ in ref.plan.order]
+    xg = trees.TreeEnsemble.from_model(trees.synthetic_xgboost_json(
+        len(kinds), n_trees=80, depth=3, seed=31, feature_kinds=kinds))
+    n = 12000
+    b, f, i = ref.to_numpy()
+    X = np.stack([{'b': b, 'f': f, 'i': i}[k][c, :n].astype(np.float64) for _, k, c in ref.plan.order], axis=1)
+    sk = trees.TreeEnsemble.from_model(HistGradientBoostingClassifier(
+        max_iter=25, max_depth=4, random_state=0).fit(X, (X[:, 7] + np.random.default_rng(0).random(n) > 0.6)))
+    for te in (xg, sk):
+        a = te.predict_blocks(got, method='staged').cpu().numpy()
+        np.testing.assert_array_equal(a, te.predict_blocks(ref, method='gather').cpu().numpy())
+        np.testing.assert_array_equal(te.predict_blocks(got, method='gather').cpu().numpy(), a)
+    pd.testing.assert_frame_equal(got.to_frame(), ref.to_frame())
