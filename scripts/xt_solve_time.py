@@ -34,6 +34,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--games', type=int, default=10000)
     ap.add_argument('--reps', type=int, default=10)
+    ap.add_argument('--large', action='store_true', help='also time the 105 x 68 solve (cfg5)')
     args = ap.parse_args()
     ab = B.ActionBatch.from_columns(synthetic.spadl_games(args.games))
     cells = ops.xt_cells(ab, 16, 12)
@@ -49,6 +50,12 @@ def main():
     out['solve_ms_incl_host_sync'] = _ms(lambda: ops.xt_solve(acc), args.reps)
     grid = sol.mats[3]
     out['rate_cells_ms'] = _ms(lambda: ops.xt_rate_cells(cells, ab.n, 16, 12, grid), args.reps)
+    if args.large:
+        big = ops.xt_count(ab, 105, 68)
+        out['count_105x68_ms'] = _ms(lambda: ops.xt_count(ab, 105, 68), args.reps)
+        sol = ops.xt_solve(big)
+        out['iterations_105x68'] = sol.n_iter
+        out['solve_105x68_ms_incl_host_sync'] = _ms(lambda: ops.xt_solve(big), args.reps)
     print(json.dumps(out), flush=True)
 
 
