@@ -239,8 +239,8 @@ def xt105_extra(ab, dist, dev, sharded: bool = False) -> dict:
             ops.xt_count(ab, l, w, acc)
             if dist is not None and dist.get_backend() == 'nccl':
                 shard.allreduce_xt_counts(acc.shot, acc.goal, acc.move, acc.trans, acc.err)
-            sol = ops.xt_solve(acc)  # synchronises
-            mats, n_iter = sol.mats, sol.n_iter
+            sol = ops.xt_solve(acc, transition=False)  # synchronises; ExpectedThreat.fit's
+            mats, n_iter = sol.mats, sol.n_iter           # call above 1024 cells
         grid = ops.xt_interp_grid(mats[3].reshape(w, l), l, w)
         ops.xt_rate(ab, grid, 1050, 680)
         return n_iter

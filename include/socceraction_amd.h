@@ -230,11 +230,15 @@ int sa_xt_count_cells(const uint32_t* cells, int64_t n, int32_t l, int32_t w, in
 int sa_xt_rate_cells(const uint32_t* cells, int64_t n, int32_t l, int32_t w, const double* grid,
                      double* out, int32_t* err_flags, void* stream);
 
+/* Grids up to SA_XT_SOLVE_MAX_C cells solve in one workgroup from the transposed matrix. */
+#define SA_XT_SOLVE_MAX_C 1024
+
 /* Normalise the counts into the reference's matrices and run the value iteration
  * x <- s*p_shot + p_move * (T x) until no cell changes by more than eps
  * (xthreat.py:278-345).  Writes (all float64, device):
  *   mats[4*C] = scoring_prob | shot_prob | move_prob | xT  (row-major w x l each)
- *   trans_t[C*C] = transition matrix TRANSPOSED (trans_t[e*C+s] = T[s,e])
+ *   trans_t[C*C] = transition matrix TRANSPOSED (trans_t[e*C+s] = T[s,e]); may be NULL when
+ *                  C > SA_XT_SOLVE_MAX_C (the large-grid iteration reads the counts directly)
  *   heatmaps[(max_iter+1)*C] = x after 0..n_iter iterations
  * *n_iter [host] receives the iteration count (-1: max_iter reached first).
  * Synchronises the stream. */

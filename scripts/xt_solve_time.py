@@ -56,6 +56,8 @@ def main():
         sol = ops.xt_solve(big)
         out['iterations_105x68'] = sol.n_iter
         out['solve_105x68_ms_incl_host_sync'] = _ms(lambda: ops.xt_solve(big), args.reps)
+        out['solve_105x68_no_transition_ms'] = _ms(lambda: ops.xt_solve(big, transition=False),
+                                                   args.reps)
     print(json.dumps(out), flush=True)
 
 

@@ -20,6 +20,7 @@ DEBUG_LIB = os.path.join(HERE, '_lib', 'libsocceraction_amd_debug.so')
 LIB_PATH = os.environ.get('SOCCERACTION_AMD_LIB') or (DEBUG_LIB if DEBUG else DEFAULT_LIB)
 
 SA_MAX_FRAMES = 8
+SA_XT_SOLVE_MAX_C = 1024  # sa_xt_solve: larger grids may pass trans_t = NULL
 SA_XT_CELLS_MAX_C = 4096
 SA_BOOL_TILE_QUANTUM = 1024
 SA_NUM_TILE_QUANTUM = 128

@@ -317,7 +317,7 @@ __device__ __forceinline__ double row_payoff(const double* __restrict__ Tt, cons
   return acc;
 }
 
-constexpr int XT_SOLVE_MAX_C = 1024;
+constexpr int XT_SOLVE_MAX_C = SA_XT_SOLVE_MAX_C;
 
 // Small grids (C <= XT_SOLVE_MAX_C, e.g. 16 x 12): one persistent workgroup runs every
 // iteration, row r = one lane, x in LDS; Tt is the exact transposed matrix of
@@ -843,9 +843,9 @@ extern "C" int sa_xt_solve(const int64_t* shot, const int64_t* goal, const int64
                            double* mats, double* trans_t, double* heatmaps, int32_t* n_iter,
                            void* stream) {
   if (l < 1 || w < 1 || max_iter < 0) return fail(SA_EINVAL, "bad l, w or max_iter");
-  if (!shot || !goal || !move || !trans || !mats || !trans_t || !heatmaps || !n_iter)
-    return fail(SA_EINVAL, "null pointer");
   const int C = l * w;
+  if (!shot || !goal || !move || !trans || !mats || (!trans_t && C <= XT_SOLVE_MAX_C) || !heatmaps || !n_iter)
+    return fail(SA_EINVAL, "null pointer");
   hipStream_t st = (hipStream_t)stream;
   auto* us = reinterpret_cast<const unsigned long long*>(shot);
   auto* ug = reinterpret_cast<const unsigned long long*>(goal);
@@ -860,8 +860,10 @@ extern "C" int sa_xt_solve(const int64_t* shot, const int64_t* goal, const int64
   int32_t* dflags = dn + 1;
   int32_t iters = -1;
   hipLaunchKernelGGL(xt_prob_kernel, dim3((C + 255) / 256), dim3(256), 0, st, us, ug, um, C, mats, gs, pm);
-  const dim3 tgrid((C + 31) / 32, (C + 31) / 32);
-  hipLaunchKernelGGL(xt_transpose_kernel, tgrid, dim3(256), 0, st, trans, um, C, trans_t);
+  if (trans_t) {  // the dense transposed matrix: read by the small-grid solve, optional above
+    const dim3 tgrid((C + 31) / 32, (C + 31) / 32);
+    hipLaunchKernelGGL(xt_transpose_kernel, tgrid, dim3(256), 0, st, trans, um, C, trans_t);
+  }
   rc = check_launch("xt normalise");
   if (!rc && C <= XT_SOLVE_MAX_C) {
     if (C <= XR_MAX_C) {

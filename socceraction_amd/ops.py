@@ -378,16 +378,22 @@ def xt_check_errors(acc: XTCounts, mask: int = XT_ERR_FIT) -> None:
 @dataclass
 class XTSolution:
     mats: torch.Tensor      # f64 [4, C]: scoring, shot, move, xT
-    trans_t: torch.Tensor   # f64 [C, C] transposed transition matrix
+    trans_t: Optional[torch.Tensor]  # f64 [C, C] transposed transition matrix (or None)
     heatmaps: torch.Tensor  # f64 [n_iter + 1, C]
     n_iter: int
 
 
-def xt_solve(acc: XTCounts, eps: float = 1e-5, max_iter: int = 1000) -> XTSolution:
+def xt_solve(acc: XTCounts, eps: float = 1e-5, max_iter: int = 1000,
+             transition: bool = True) -> XTSolution:
+    """Normalisation + value iteration. ``transition=False`` (grids above
+    ``SA_XT_SOLVE_MAX_C`` cells only) skips forming the dense transposed transition matrix,
+    which the large-grid iteration never reads (408 MB at 105 x 68)."""
     C = acc.C
     dev = acc.shot.device
     mats = torch.empty((4, C), dtype=torch.float64, device=dev)
-    tt = torch.empty((C, C), dtype=torch.float64, device=dev)
+    if not transition and C <= _native.SA_XT_SOLVE_MAX_C:
+        transition = True  # the small-grid solve reads the transposed matrix
+    tt = torch.empty((C, C), dtype=torch.float64, device=dev) if transition else None
     heat = torch.empty((max_iter + 1, C), dtype=torch.float64, device=dev)
     n_iter = ctypes.c_int32(0)
     _native.check(_native.lib().sa_xt_solve(_ptr(acc.shot), _ptr(acc.goal), _ptr(acc.move),

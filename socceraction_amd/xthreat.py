@@ -180,6 +180,24 @@ class ExpectedThreat:
         self.transition_matrix: Optional[np.ndarray] = None
         self._grid_cache = None
 
+    # The C x C transition matrix (reference attribute, xthreat.py:276, 337). Grids above
+    # LAZY_TRANSITION_CELLS leave it on the device after fit -- the solve never forms it, and
+    # at 105 x 68 it is 408 MB -- and it is normalised and copied to the host on first access.
+    LAZY_TRANSITION_CELLS = 1024
+
+    @property
+    def transition_matrix(self) -> Optional[np.ndarray]:
+        if self._transition is None and getattr(self, '_transition_counts', None) is not None:
+            _, tt = ops.xt_normalize(self._transition_counts)
+            self._transition = np.ascontiguousarray(tt.cpu().numpy().T)
+            self._transition_counts = None
+        return self._transition
+
+    @transition_matrix.setter
+    def transition_matrix(self, value: Optional[np.ndarray]) -> None:
+        self._transition = value
+        self._transition_counts = None
+
     def fit(self, actions: pd.DataFrame, process_group=None, max_iter: int = 1000,
             shard_solve: bool = False) -> 'ExpectedThreat':
         """Fit the model (reference xthreat.py:322-345).
@@ -206,14 +224,17 @@ class ExpectedThreat:
             trans = None
         else:
             acc = _fit_counts(actions, l, w, process_group)
-            sol = ops.xt_solve(acc, self.eps, max_iter)
+            lazy = l * w > self.LAZY_TRANSITION_CELLS
+            sol = ops.xt_solve(acc, self.eps, max_iter, transition=not lazy)
             mats, heat_t, n_iter = sol.mats, sol.heatmaps, sol.n_iter
-            trans = np.ascontiguousarray(sol.trans_t.cpu().numpy().T)
+            trans = None if lazy else np.ascontiguousarray(sol.trans_t.cpu().numpy().T)
         m = mats.cpu().numpy()
         self.scoring_prob_matrix = m[0].reshape((w, l))
         self.shot_prob_matrix = m[1].reshape((w, l))
         self.move_prob_matrix = m[2].reshape((w, l))
         self.transition_matrix = trans
+        if trans is None and not (shard_solve and process_group is not None):
+            self._transition_counts = acc  # normalised on first access
         self.xT = m[3].reshape((w, l)).copy()
         heat = heat_t.cpu().numpy().reshape((-1, w, l))
         self.heatmaps = [h.copy() for h in heat]

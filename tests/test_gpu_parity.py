@@ -310,6 +310,19 @@ def test_xt_large_grid_vs_oracle(sa, l, w, games):
     assert sol.n_iter + 1 == len(ref['heatmaps'])
     np.testing.assert_array_equal(sol.heatmaps.cpu().numpy().reshape(-1, w, l), ref['heatmaps'])
     np.testing.assert_array_equal(m[3].reshape(w, l), ref['xT'])
+    if l * w > 1024:
+        # the large-grid solve without the dense transposed matrix: same results, and the
+        # drop-in's transition_matrix (formed on first access) equals the oracle's
+        lean = ops.xt_solve(acc, transition=False)
+        assert lean.trans_t is None and lean.n_iter == sol.n_iter
+        np.testing.assert_array_equal(lean.mats.cpu().numpy(), m)
+        np.testing.assert_array_equal(lean.heatmaps.cpu().numpy(), sol.heatmaps.cpu().numpy())
+        from socceraction_amd import xthreat
+        model = xthreat.ExpectedThreat(l=l, w=w).fit(syn.to_frame(d))
+        assert model._transition is None
+        np.testing.assert_array_equal(model.xT, ref['xT'])
+        np.testing.assert_array_equal(model.transition_matrix, ref['transition'])
+        assert model._transition_counts is None
 
 
 @pytest.mark.parametrize('l,w,games', [(16, 12, 400), (105, 68, 60), (1, 1, 5), (30, 20, 1)])
