@@ -41,20 +41,17 @@ BYTES = {'bool_features': 7 + 515,             # type/result/bodypart u8 + team 
          'num_features': 48 + 47 * 8 + 3 * 8,  # 5 f64 + 4 u8 + team -> 47 f64 + 3 i64
          'goalscore': 6 + 24, 'labels': 6 + 2, 'formula': 30 + 24,
          'labels_formula': 30 + 2 + 24,  # type/result/team/time/2 probs -> 2 labels + 3 values
-         'game_tail': 30 + 24 + 2 + 24,  # the same inputs -> goalscore + 2 labels + 3 values
          # count pass 34 B + its 4-B rate codes, rate 4 + 8 B (solve: 192 cells)
          'xt_fit_rate': 34 + 4 + 4 + 8}
 KERNELS = ('bool_features', 'num_features', 'goalscore', 'labels', 'formula', 'labels_formula',
-           'game_tail', 'xt_fit_rate')
+           'xt_fit_rate')
 STEP_CALLS = ('bool_features', 'num_features', 'goalscore', 'labels', 'formula')
 # launch entries that cover several of STEP_CALLS in one kernel
-FUSED_CALLS = {'labels_formula': ('labels', 'formula'),
-               'game_tail': ('goalscore', 'labels', 'formula')}
+FUSED_CALLS = {'labels_formula': ('labels', 'formula')}
 # the HIP kernel each step entry launches (socceraction_amd/csrc/sa_vaep.hip)
 KERNEL_NAMES = {'bool_features': 'bool_colgroup_kernel', 'num_features': 'num_features_kernel',
                 'goalscore': 'goalscore_wave16_kernel', 'labels': 'labels_kernel',
                 'formula': 'formula_kernel', 'labels_formula': 'labels_formula_kernel',
-                'game_tail': 'game_tail_kernel',
                 'xt_fit_rate': 'xt_count_kernel + xt_solve_reg_kernel + xt_rate_cells_kernel'}
 
 
@@ -535,8 +532,7 @@ def main() -> None:
                    'goalscore': lambda: ops.goalscore_into(ab, out),
                    'labels': lambda: ops.labels(ab, 10, lab),
                    'formula': lambda: ops.formula(ab, ps, pc, val),
-                   'labels_formula': lambda: ops.labels_formula(ab, ps, pc, 10, lab, val),
-                   'game_tail': lambda: ops.game_tail(ab, out, ps, pc, 10, lab, val)}
+                   'labels_formula': lambda: ops.labels_formula(ab, ps, pc, 10, lab, val)}
         calls = tuple(by_name[k] for k in order)
         # cm=1: the count pass runs on the main stream right after num_features, in the fast
         # one-workgroup-per-CU shape; the side stream takes the all-reduce, solve and rate

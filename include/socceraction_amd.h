@@ -186,21 +186,6 @@ int sa_vaep_labels_formula_f32(const sa_actions* a, int32_t nr_actions, uint8_t*
                                const float* p_scores, const float* p_concedes, float* off,
                                float* def, float* val, void* stream);
 
-/* The whole tail of a VAEP step in one launch, one wave per segment: goalscore into
- * i64_out's columns col..col+2 (as sa_vaep_goalscore), then compute_labels and formula.value
- * of the segment's rows while its ids and team codes are in cache (as
- * sa_vaep_labels_formula_f64 / _f32, same arguments and output lengths). */
-int sa_vaep_game_tail_f64(const sa_actions* a, const sa_block* i64_out, int32_t col,
-                          int32_t nr_actions, uint8_t* scores, uint8_t* concedes,
-                          uint8_t* goal_from_shot, int64_t ld, const double* p_scores,
-                          const double* p_concedes, double* off, double* def, double* val,
-                          void* stream);
-int sa_vaep_game_tail_f32(const sa_actions* a, const sa_block* i64_out, int32_t col,
-                          int32_t nr_actions, uint8_t* scores, uint8_t* concedes,
-                          uint8_t* goal_from_shot, int64_t ld, const float* p_scores,
-                          const float* p_concedes, float* off, float* def, float* val,
-                          void* stream);
-
 /* ---- Expected Threat (xthreat.py) --------------------------------------------
  * Count pass over SPADL actions (frames[0] of `a`; segments ignored):
  * shot[c] += shots (type 11) by start cell, goal[c] += successful shots,

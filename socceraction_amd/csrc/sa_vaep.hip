@@ -3,7 +3,6 @@
 //   bool_colgroup_kernel     one-hot + team features (gamestates + flip fused in), bool block
 //   num_features_kernel      time / location / polar / movement / deltas / ids, f64 + i64 blocks
 //   goalscore_wave16_kernel  segmented exclusive scan (one wave per segment)
-//   game_tail_kernel         goalscore + labels + formula of a segment in one wave (the step's tail)
 //   labels_kernel            scores / concedes / goal_from_shot look-ahead
 //   formula_kernel           offensive / defensive / vaep value (f64 or f32)
 //
@@ -761,6 +760,89 @@ __device__ __forceinline__ void wave_sync() {  // LDS hand-off between the lanes
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+template <bool ATOMIC>
+__global__ __launch_bounds__(256) void goalscore_wave16_kernel(sa_actions A,
+                                                               int64_t* __restrict__ block,
+                                                               int64_t C, int64_t col, int64_t R) {
+  __shared__ __align__(16) int64_t gs_lds[4][WAVE * GS_LDS_PITCH];
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int64_t g = (int64_t)blockIdx.x * (blockDim.x / WAVE) + threadIdx.x / WAVE;
+  if (g >= A.n_segments) return;
+  const int64_t s = A.seg_off[g], e = A.seg_off[g + 1];
+  if (s >= e) return;
+  const int64_t n = A.n;
+  const sa_frame& F = A.frames[0];
+  const int32_t teamA = F.team[s];
+  const int64_t base0 = s & ~(int64_t)127;  // 128-row aligned: whole 1-KiB column runs  // 16-row aligned: vector loads, whole 16-row runs
+  uint64_t carry = 0;  // low 32 bits: goals of team A before this pass; high: team B
+  Gs16In cur, nxt;
+  gs16_load<ATOMIC>(F, base0 + 16 * lane, n, cur);
+  for (int64_t base = base0; base < e; base += 16 * WAVE) {
+    const int64_t j0 = base + 16 * lane;
+    if (base + 16 * WAVE < e) gs16_load<ATOMIC>(F, j0 + 16 * WAVE, n, nxt);
+    uint32_t gm = 0, om = 0, am = 0;  // goal / owngoal / team-A row bits (valid rows only)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      uint32_t gb, ob;
+      goal_bytes(cur.ty[q], cur.rs[q], ATOMIC, gb, ob);
+      gm |= pack4(gb) << (4 * q);
+      om |= pack4(ob) << (4 * q);
+    }
+#pragma unroll
+    for (int m = 0; m < 16; ++m) am |= (uint32_t)(cur.tm[m] == teamA) << m;
+    const int lo = s > j0 ? (int)(s - j0) : 0;                // first valid row of the lane
+    const int hi = e < j0 + 16 ? (int)(e - j0) : 16;           // one past the last
+    const uint32_t vm = lo >= hi ? 0u : (0xFFFFu >> (16 - (hi - lo))) << lo;
+    const uint32_t gA = ((gm & am) | (om & ~am)) & vm, gB = ((gm & ~am) | (om & am)) & vm;
+    const uint64_t x = (uint64_t)__popc(gA) | ((uint64_t)__popc(gB) << 32);
+    uint64_t incl = x;
+#pragma unroll
+    for (int off = 1; off < WAVE; off <<= 1) {
+      const uint64_t y = __shfl_up(incl, off, WAVE);
+      if (lane >= off) incl += y;
+    }
+    const uint64_t ex = carry + incl - x;  // goals before row j0
+    carry += __shfl(incl, WAVE - 1, WAVE);
+    // the lane's 16 rows -> LDS one column at a time, then back out in pass-of-128 order
+    // (lane l: rows 2l, 2l+1 of each 128-row run), so every store instruction writes 1 KiB
+    // contiguous of one column (the lane's own 128-B run per instruction was 2.3x slower)
+    const int64_t cA0 = (int64_t)(ex & 0xFFFFFFFFull), cB0 = (int64_t)(ex >> 32);
+    int64_t* xl = gs_lds[threadIdx.x / WAVE];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      wave_sync();
+#pragma unroll
+      for (int m = 0; m < 16; m += 2) {
+        int64_t v[2];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const uint32_t below = (1u << (m + q)) - 1u;  // rows of this lane before m+q
+          const int64_t cA = cA0 + __popc(gA & below), cB = cB0 + __popc(gB & below);
+          const bool isA = (am >> (m + q)) & 1;
+          const int64_t tm = isA ? cA : cB, op = isA ? cB : cA;
+          v[q] = k == 0 ? tm : (k == 1 ? op : tm - op);
+        }
+        *reinterpret_cast<i64x2*>(xl + lane * GS_LDS_PITCH + m) = i64x2{(long long)v[0], (long long)v[1]};
+      }
+      wave_sync();
+#pragma unroll
+      for (int p = 0; p < 8; ++p) {
+        const int r = 128 * p + 2 * lane;  // row offset from `base`
+        const int64_t jr = base + r;
+        const i64x2 v = *reinterpret_cast<const i64x2*>(xl + (r / 16) * GS_LDS_PITCH + (r % 16));
+        int64_t* o = block + tile_off(jr, col + k, C, R);
+        if (jr >= s && jr + 1 < e) {
+          st16(o, v);
+        } else {
+          if (jr >= s && jr < e) o[0] = v[0];
+          if (jr + 1 >= s && jr + 1 < e) o[1] = v[1];
+        }
+      }
+    }
+    cur = nxt;
+  }
+}
+
 // ------------------------------------------------------------------------------ labels
 // vaep/labels.py:9-116, atomic/vaep/labels.py:9-107.  A lane owns 16 consecutive actions
 // and holds rows j0 .. j0+31 as goal / owngoal bit masks plus team codes, so a look-ahead of
@@ -904,7 +986,7 @@ template <bool ATOMIC, typename T>
 __device__ __forceinline__ void formula_rows(const sa_actions& A, const T* __restrict__ ps,
                                              const T* __restrict__ pc, T* __restrict__ off,
                                              T* __restrict__ def, T* __restrict__ val, bool vec_ok,
-                                             int64_t j0, SegCursor& cur, bool keep = true) {
+                                             int64_t j0, SegCursor& cur) {
   constexpr int V = 16 / sizeof(T);
   const int64_t n = A.n;
   const int lane = threadIdx.x & (WAVE - 1);
@@ -1020,11 +1102,9 @@ __device__ __forceinline__ void formula_rows(const sa_actions& A, const T* __res
     vd[q] = d;
     vv[q] = o + d;
   }
-  if (keep) {
-    st16(off + j0, vo);
-    st16(def + j0, vd);
-    st16(val + j0, vv);
-  }
+  st16(off + j0, vo);
+  st16(def + j0, vd);
+  st16(val + j0, vv);
 }
 
 template <bool ATOMIC, typename T>
@@ -1066,140 +1146,6 @@ __global__ __launch_bounds__(256) void labels_formula_kernel(sa_actions A, int n
     if (base >= A.n) break;  // uniform
     formula_rows<ATOMIC, T>(A, ps, pc, off, def, val, vec_ok, base + (int64_t)lane * V, fc);
   }
-}
-
-// ------------------------------------------------------------------------------ game tail
-// One wave per segment, in passes of 1024 rows (a lane owns 16 consecutive rows).  TAIL=false
-// is the goalscore scan alone; TAIL=true also runs labels_rows on the lane's 16 rows and the
-// formula on the pass's rows (formula_rows, a lane V rows per sub-pass) while they are in
-// L1/L2, so the step's tail -- goalscore, labels, formula -- reads the ids and team codes once
-// and is one launch (game_tail_kernel).  Labels and formula values of a row depend only on its
-// own segment, and the segment cursor starts at the segment holding the pass's first row, so
-// the lanes straddling a segment edge write the neighbouring segment's bytes with the values
-// that segment's own wave writes (identical bytes; lanes wholly outside [s, e) write nothing).
-template <typename T>
-struct TailArgs {
-  int nr;
-  uint8_t *sc, *co, *gfs;
-  const T *ps, *pc;
-  T *off, *def, *val;
-  bool vec_ok;
-};
-
-template <bool ATOMIC, bool TAIL, typename T>
-__device__ __forceinline__ void game_scan(const sa_actions& A, int64_t* __restrict__ block, int64_t C,
-                                          int64_t col, int64_t R, const TailArgs<T>& t,
-                                          int64_t* __restrict__ xl) {
-  constexpr int V = 16 / sizeof(T);
-  const int lane = threadIdx.x & (WAVE - 1);
-  const int64_t g = (int64_t)blockIdx.x * (blockDim.x / WAVE) + threadIdx.x / WAVE;
-  if (g >= A.n_segments) return;
-  const int64_t s = A.seg_off[g], e = A.seg_off[g + 1];
-  if (s >= e) return;
-  const int64_t n = A.n;
-  const sa_frame& F = A.frames[0];
-  const int32_t teamA = F.team[s];
-  const int64_t base0 = s & ~(int64_t)127;  // 128-row aligned: whole 1-KiB column runs
-  SegCursor fc{g, s, e};                     // the segment holding row base0 (tail part)
-  if (TAIL)
-    while (fc.s > base0 && fc.g > 0) {
-      --fc.g;
-      fc.e = fc.s;
-      fc.s = A.seg_off[fc.g];
-    }
-  uint64_t carry = 0;  // low 32 bits: goals of team A before this pass; high: team B
-  Gs16In cur, nxt;
-  gs16_load<ATOMIC>(F, base0 + 16 * lane, n, cur);
-  for (int64_t base = base0; base < e; base += 16 * WAVE) {
-    const int64_t j0 = base + 16 * lane;
-    if (base + 16 * WAVE < e) gs16_load<ATOMIC>(F, j0 + 16 * WAVE, n, nxt);
-    uint32_t gm = 0, om = 0, am = 0;  // goal / owngoal / team-A row bits (valid rows only)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      uint32_t gb, ob;
-      goal_bytes(cur.ty[q], cur.rs[q], ATOMIC, gb, ob);
-      gm |= pack4(gb) << (4 * q);
-      om |= pack4(ob) << (4 * q);
-    }
-#pragma unroll
-    for (int m = 0; m < 16; ++m) am |= (uint32_t)(cur.tm[m] == teamA) << m;
-    const int lo = s > j0 ? (int)(s - j0) : 0;                // first valid row of the lane
-    const int hi = e < j0 + 16 ? (int)(e - j0) : 16;           // one past the last
-    const uint32_t vm = lo >= hi ? 0u : (0xFFFFu >> (16 - (hi - lo))) << lo;
-    const uint32_t gA = ((gm & am) | (om & ~am)) & vm, gB = ((gm & ~am) | (om & am)) & vm;
-    const uint64_t x = (uint64_t)__popc(gA) | ((uint64_t)__popc(gB) << 32);
-    uint64_t incl = x;
-#pragma unroll
-    for (int off = 1; off < WAVE; off <<= 1) {
-      const uint64_t y = __shfl_up(incl, off, WAVE);
-      if (lane >= off) incl += y;
-    }
-    const uint64_t ex = carry + incl - x;  // goals before row j0
-    carry += __shfl(incl, WAVE - 1, WAVE);
-    // the lane's 16 rows -> LDS one column at a time, then back out in pass-of-128 order
-    // (lane l: rows 2l, 2l+1 of each 128-row run), so every store instruction writes 1 KiB
-    // contiguous of one column (the lane's own 128-B run per instruction was 2.3x slower)
-    const int64_t cA0 = (int64_t)(ex & 0xFFFFFFFFull), cB0 = (int64_t)(ex >> 32);
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      wave_sync();
-#pragma unroll
-      for (int m = 0; m < 16; m += 2) {
-        int64_t v[2];
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          const uint32_t below = (1u << (m + q)) - 1u;  // rows of this lane before m+q
-          const int64_t cA = cA0 + __popc(gA & below), cB = cB0 + __popc(gB & below);
-          const bool isA = (am >> (m + q)) & 1;
-          const int64_t tm = isA ? cA : cB, op = isA ? cB : cA;
-          v[q] = k == 0 ? tm : (k == 1 ? op : tm - op);
-        }
-        *reinterpret_cast<i64x2*>(xl + lane * GS_LDS_PITCH + m) = i64x2{(long long)v[0], (long long)v[1]};
-      }
-      wave_sync();
-#pragma unroll
-      for (int p = 0; p < 8; ++p) {
-        const int r = 128 * p + 2 * lane;  // row offset from `base`
-        const int64_t jr = base + r;
-        const i64x2 v = *reinterpret_cast<const i64x2*>(xl + (r / 16) * GS_LDS_PITCH + (r % 16));
-        int64_t* o = block + tile_off(jr, col + k, C, R);
-        if (jr >= s && jr + 1 < e) {
-          st16(o, v);
-        } else {
-          if (jr >= s && jr < e) o[0] = v[0];
-          if (jr + 1 >= s && jr + 1 < e) o[1] = v[1];
-        }
-      }
-    }
-    if (TAIL) {
-      if (j0 < e && j0 + 16 > s) labels_rows<ATOMIC>(A, t.nr, t.sc, t.co, t.gfs, j0, fc);
-#pragma unroll 1
-      for (int p = 0; p < LANE_ACTS / V; ++p) {
-        const int64_t sb = base + (int64_t)p * WAVE * V;
-        if (sb >= e) break;  // uniform
-        const int64_t jf = sb + (int64_t)lane * V;
-        formula_rows<ATOMIC, T>(A, t.ps, t.pc, t.off, t.def, t.val, t.vec_ok, jf, fc,
-                                jf < e && jf + V > s);
-      }
-    }
-    cur = nxt;
-  }
-}
-
-template <bool ATOMIC>
-__global__ __launch_bounds__(256) void goalscore_wave16_kernel(sa_actions A,
-                                                               int64_t* __restrict__ block,
-                                                               int64_t C, int64_t col, int64_t R) {
-  __shared__ __align__(16) int64_t gs_lds[4][WAVE * GS_LDS_PITCH];
-  game_scan<ATOMIC, false, double>(A, block, C, col, R, TailArgs<double>{}, gs_lds[threadIdx.x / WAVE]);
-}
-
-template <bool ATOMIC, typename T>
-__global__ __launch_bounds__(256) void game_tail_kernel(sa_actions A, int64_t* __restrict__ block,
-                                                        int64_t C, int64_t col, int64_t R,
-                                                        TailArgs<T> t) {
-  __shared__ __align__(16) int64_t gs_lds[4][WAVE * GS_LDS_PITCH];
-  game_scan<ATOMIC, true, T>(A, block, C, col, R, t, gs_lds[threadIdx.x / WAVE]);
 }
 
 }  // namespace sa
@@ -1503,53 +1449,4 @@ extern "C" int sa_vaep_labels_formula_f32(const sa_actions* a, int32_t nr_action
                                           float* def, float* val, void* stream) {
   return launch_labels_formula<float>(a, nr_actions, scores, concedes, goal_from_shot, ld, p_scores,
                                       p_concedes, off, def, val, stream);
-}
-
-template <typename T>
-static int launch_game_tail(const sa_actions* a, const sa_block* i64_out, int32_t col, int32_t nr_actions,
-                            uint8_t* scores, uint8_t* concedes, uint8_t* goal_from_shot, int64_t ld,
-                            const T* ps, const T* pc, T* off, T* def, T* val, void* stream) {
-  int rc = check_actions(a, false);
-  if (rc) return rc;
-  if ((rc = check_block(i64_out, a->n, SA_NUM_TILE_QUANTUM, "i64"))) return rc;
-  if (col < 0 || col + 3 > i64_out->n_cols) return fail(SA_EINVAL, "goalscore columns outside the block");
-  if (nr_actions < 1) return fail(SA_EINVAL, "nr_actions must be >= 1");
-  if (ld % 16 != 0 || ld < ((a->n + 15) / 16) * 16)
-    return fail(SA_EINVAL, "ld must be a multiple of 16 and >= round_up(n, 16)");
-  if (!aligned16(scores) || !aligned16(concedes) || !aligned16(goal_from_shot))
-    return fail(SA_EINVAL, "label outputs must be 16-byte aligned");
-  if (!ps || !pc || !off || !def || !val) return fail(SA_EINVAL, "null probability/output pointer");
-  if (!aligned16(off) || !aligned16(def) || !aligned16(val))
-    return fail(SA_EINVAL, "formula outputs must be 16-byte aligned (length >= round_up(n, 16))");
-  if (a->n == 0) return SA_OK;
-  const dim3 g4((unsigned)((a->n_segments + 3) / 4));  // one wave per segment
-  const TailArgs<T> t{nr_actions, scores, concedes, goal_from_shot, ps, pc, off, def, val,
-                      aligned16(ps) && aligned16(pc)};
-  hipStream_t st = (hipStream_t)stream;
-  int64_t* blk = (int64_t*)i64_out->data;
-  if (a->atomic)
-    hipLaunchKernelGGL((game_tail_kernel<true, T>), g4, dim3(256), 0, st, *a, blk,
-                       (int64_t)i64_out->n_cols, (int64_t)col, i64_out->tile_rows, t);
-  else
-    hipLaunchKernelGGL((game_tail_kernel<false, T>), g4, dim3(256), 0, st, *a, blk,
-                       (int64_t)i64_out->n_cols, (int64_t)col, i64_out->tile_rows, t);
-  return check_launch("game_tail_kernel");
-}
-
-extern "C" int sa_vaep_game_tail_f64(const sa_actions* a, const sa_block* i64_out, int32_t col,
-                                     int32_t nr_actions, uint8_t* scores, uint8_t* concedes,
-                                     uint8_t* goal_from_shot, int64_t ld, const double* p_scores,
-                                     const double* p_concedes, double* off, double* def, double* val,
-                                     void* stream) {
-  return launch_game_tail<double>(a, i64_out, col, nr_actions, scores, concedes, goal_from_shot, ld,
-                                  p_scores, p_concedes, off, def, val, stream);
-}
-
-extern "C" int sa_vaep_game_tail_f32(const sa_actions* a, const sa_block* i64_out, int32_t col,
-                                     int32_t nr_actions, uint8_t* scores, uint8_t* concedes,
-                                     uint8_t* goal_from_shot, int64_t ld, const float* p_scores,
-                                     const float* p_concedes, float* off, float* def, float* val,
-                                     void* stream) {
-  return launch_game_tail<float>(a, i64_out, col, nr_actions, scores, concedes, goal_from_shot, ld,
-                                 p_scores, p_concedes, off, def, val, stream);
 }

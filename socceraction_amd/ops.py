@@ -248,39 +248,6 @@ def labels_formula(batch: ActionBatch, p_scores: torch.Tensor, p_concedes: torch
     return labels_out, values_out
 
 
-def game_tail(batch: ActionBatch, out: FeatureBlocks, p_scores: torch.Tensor,
-              p_concedes: torch.Tensor, nr_actions: int = 10,
-              labels_out: Optional[LabelBlocks] = None,
-              values_out: Optional[torch.Tensor] = None) -> Tuple[LabelBlocks, torch.Tensor]:
-    """The step's tail in one launch: :func:`goalscore_into` ``out`` + :func:`labels_formula`."""
-    from ._native import XFN
-    gc = out.plan.struct.i64_col[XFN['goalscore']]
-    if gc < 0:
-        raise ValueError('plan has no goalscore columns')
-    dt = p_scores.dtype
-    if dt not in (torch.float32, torch.float64) or p_concedes.dtype != dt:
-        raise TypeError('probabilities must both be float32 or both float64')
-    if p_scores.numel() < batch.n or p_concedes.numel() < batch.n:
-        raise ValueError('one probability per action is required')
-    ld = _ld(batch.n)
-    if labels_out is None:
-        buf = torch.empty((3, ld), dtype=torch.uint8, device=batch.device)
-        labels_out = LabelBlocks(batch.n, buf[0], buf[1], buf[2])
-    if values_out is None:
-        values_out = torch.empty((3, ld), dtype=dt, device=batch.device)
-    ps, pc = p_scores.contiguous(), p_concedes.contiguous()
-    s = batch.struct()
-    ib = out.sa_blocks()[2]
-    fn = _native.lib().sa_vaep_game_tail_f64 if dt == torch.float64 else \
-        _native.lib().sa_vaep_game_tail_f32
-    o = values_out
-    _native.check(fn(ctypes.byref(s), ctypes.byref(ib), gc, int(nr_actions),
-                     _ptr(labels_out.scores), _ptr(labels_out.concedes),
-                     _ptr(labels_out.goal_from_shot), ld, _ptr(ps), _ptr(pc), _ptr(o[0]),
-                     _ptr(o[1]), _ptr(o[2]), stream_handle()))
-    return labels_out, values_out
-
-
 # ------------------------------------------------------------------------------- xT
 @dataclass
 class XTCounts:

@@ -151,11 +151,6 @@ def _small_games(syn, atomic, seed, n_small=300):
     return d2
 
 
-def _native_xfn(name):
-    from socceraction_amd._native import XFN
-    return XFN[name]
-
-
 @pytest.mark.parametrize('atomic', [False, True])
 def test_many_small_segments_vs_oracle(sa, atomic):
     """Full games + 300 games of 1..40 actions in one batch: features at k = 1, 3, 5 (both
@@ -202,18 +197,6 @@ def test_many_small_segments_vs_oracle(sa, atomic):
             for c in ('scores', 'concedes', 'goal_from_shot'):
                 assert torch.equal(getattr(lf, c)[:n], getattr(lb, c)[:n]), (c, nr, dt)
             np.testing.assert_array_equal(vf.cpu().numpy()[:, :n], v)
-            # goalscore + labels + formula in one wave per segment == the separate launches
-            fb = ops.features(ab, default, 3)
-            gs = fb.block('i')[:, :n].clone()
-            fb.i64_block.fill_(-7)
-            lt, vt = ops.game_tail(ab, fb, tps, tpc, nr_actions=nr)
-            gcol = fb.plan.struct.i64_col[_native_xfn('goalscore')]
-            got = fb.block('i')[:, :n]
-            assert torch.equal(got[gcol:gcol + 3], gs[gcol:gcol + 3]), dt
-            assert bool((torch.cat([got[:gcol], got[gcol + 3:]]) == -7).all())
-            for c in ('scores', 'concedes', 'goal_from_shot'):
-                assert torch.equal(getattr(lt, c)[:n], getattr(lb, c)[:n]), (c, nr, dt)
-            np.testing.assert_array_equal(vt.cpu().numpy()[:, :n], v)
         fo = vo.formula(cols, ps, pc, atomic=atomic, seg_off=so)
         for r, c in enumerate(('offensive_value', 'defensive_value', 'vaep_value')):
             if dt == np.float32:
