@@ -198,8 +198,11 @@ def _events_ms(fn, reps: int) -> float:
 
 def atomic_extra(dist, rank, world, dev, games: int, reps: int = 5) -> dict:
     """BASELINE cfg3 alongside the main line: Atomic-VAEP features (k=3, default xfns, 154
-    columns) + labels, ``games`` synthetic atomic games (~5M atomic actions) per rank."""
-    d = synthetic.atomic_games(games, game_id0=rank * games)
+    columns) + labels of cfg3's ``games`` synthetic atomic games (10,000 ≈ 4.0e7 atomic
+    actions), sharded by game over the ranks (this entry scales strongly)."""
+    mine = games // world + (1 if rank < games % world else 0)
+    first = rank * (games // world) + min(rank, games % world)
+    d = synthetic.atomic_games(mine, game_id0=first)
     ab = B.ActionBatch.from_columns(d, atomic=True, dev=dev)
     out = ops.features(ab, ATOMIC_DEFAULT, 3, bool_tile=1024, num_tile=128)
     lab = ops.labels(ab)
@@ -214,35 +217,55 @@ def atomic_extra(dist, rank, world, dev, games: int, reps: int = 5) -> dict:
         total = int(_reduce(dist, n, dist.ReduceOp.SUM, dev))
     p = out.plan
     bpa = 47 + p.n_bool + 8 * (p.n_f64 + p.n_i64) + 2
-    return {'workload': 'cfg3: Atomic-VAEP features (k=3, default xfns, 154 cols) + labels',
-            'atomic_actions_per_gpu': n, 'ms_per_step': round(wall, 4),
+    return {'workload': f'cfg3: Atomic-VAEP features (k=3, default xfns, 154 cols) + labels of '
+                        f'{games:,} synthetic atomic games over {world} rank(s)',
+            'atomic_actions_per_gpu': n, 'atomic_actions_total': total, 'scaling': 'strong',
+            'ms_per_step': round(wall, 4),
             'atomic_actions_per_s': round(total / wall * 1e3, 1), 'bytes_per_action': bpa,
             'frac_of_8TBs_per_gpu': round(bpa * n / ms * 1e-6 / HBM_PEAK_GBS, 4)}
 
 
-def xt105_extra(ab, dist, dev, sharded: bool = False) -> dict:
-    """BASELINE cfg5 alongside the main line: xT 105x68 fit (count pass over this rank's
-    games, RCCL all-reduce of the 7140-cell count vectors and 204 MB transition counts, value
-    iteration over the 7140^2 system) + rate(use_interpolation=True) on the 1050x680 surface."""
+def xt105_extra(ab, dist, dev, sharded: bool = False, cfg5_games: int = 62500,
+                rank: int = 0, world: int = 1, step_games: int = 10000) -> dict:
+    """BASELINE cfg5 alongside the main line: xT 105x68 fit of cfg5's 62,500 games (≈1.0e8
+    actions; split over the ranks, so this entry scales strongly) -- count pass over this
+    rank's games, RCCL all-reduce of the 7140-cell count vectors and 204 MB transition counts,
+    value iteration over the 7140^2 system -- + rate(use_interpolation=True) of every action on
+    the 1050x680 surface. The rank's games are the step's own batch (when it holds no more
+    than the rank's share) plus freshly generated synthetic games, each a device-resident batch
+    before the timed region; ``cfg5_games=0`` times the step's batch alone."""
     from socceraction_amd import shard
     l, w = 105, 68
-
-    world = dist.get_world_size() if dist is not None else 1
+    batches = [ab]
+    if cfg5_games > 0:
+        mine = cfg5_games // world + (1 if rank < cfg5_games % world else 0)
+        batches = [ab] if mine >= step_games else []
+        left = mine - (step_games if batches else 0)
+        gid = 10_000_000 + rank * (cfg5_games + 1)  # ids disjoint from the step's games
+        while left > 0:
+            c = min(left, step_games)
+            batches.append(B.ActionBatch.from_columns(synthetic.spadl_games(c, game_id0=gid),
+                                                      dev=dev))
+            gid += c
+            left -= c
 
     def once():
         if sharded and dist is not None:  # reduce-scatter of count rows + row-sharded solve
-            acc = ops.xt_zero_counts(l, w, dev, row_blocks=world)
-            ops.xt_count(ab, l, w, acc)
+            acc = ops.xt_zero_counts(l, w, dev, row_blocks=dist.get_world_size())
+            for b in batches:
+                ops.xt_count(b, l, w, acc)
             mats, _, n_iter = shard.xt_solve_sharded(acc)
         else:  # one all-reduce of the counts, replicated solve
             acc = ops.xt_zero_counts(l, w, dev)
-            ops.xt_count(ab, l, w, acc)
+            for b in batches:
+                ops.xt_count(b, l, w, acc)
             if dist is not None and dist.get_backend() == 'nccl':
                 shard.allreduce_xt_counts(acc.shot, acc.goal, acc.move, acc.trans, acc.err)
             sol = ops.xt_solve(acc, transition=False)  # synchronises; ExpectedThreat.fit's
             mats, n_iter = sol.mats, sol.n_iter           # call above 1024 cells
         grid = ops.xt_interp_grid(mats[3].reshape(w, l), l, w)
-        ops.xt_rate(ab, grid, 1050, 680)
+        for b in batches:
+            ops.xt_rate(b, grid, 1050, 680)
         return n_iter
     once()  # warm-up (allocator, first launches)
     torch.cuda.synchronize()
@@ -250,14 +273,18 @@ def xt105_extra(ab, dist, dev, sharded: bool = False) -> dict:
     n_iter = once()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    n, total = ab.n, ab.n
+    n = sum(b.n for b in batches)
+    total = n
     if dist is not None:
         dt = _reduce(dist, dt, dist.ReduceOp.MAX, dev)
         total = int(_reduce(dist, n, dist.ReduceOp.SUM, dev))
-    return {'workload': 'cfg5: xT 105x68 fit (count + all-reduce + value iteration) + '
-                        'rate(use_interpolation=True)',
-            'actions_per_gpu': n, 'iterations': n_iter, 'ms_fit_and_rate': round(dt * 1e3, 3),
-            'actions_per_s': round(total / dt, 1),
+    games = (f'{cfg5_games:,} synthetic games over {world} rank(s)' if cfg5_games > 0 else
+             'the step batch')
+    return {'workload': f'cfg5: xT 105x68 fit (count + all-reduce + value iteration) + '
+                        f'rate(use_interpolation=True) of {games}',
+            'actions_per_gpu': n, 'actions_total': total, 'iterations': n_iter,
+            'ms_fit_and_rate': round(dt * 1e3, 3), 'actions_per_s': round(total / dt, 1),
+            'scaling': 'strong' if cfg5_games > 0 else 'weak',
             'solve': 'row-sharded' if (sharded and dist is not None) else 'replicated'}
 
 
@@ -432,11 +459,15 @@ def main() -> None:
     ap.add_argument('--no-cpu', action='store_true')
     ap.add_argument('--no-side', action='store_true',
                     help='skip the cfg3 (atomic) and cfg5 (xT 105x68) side measurements')
+    ap.add_argument('--cfg5-games', type=int, default=62500,
+                    help='games of the cfg5 side entry (BASELINE cfg5: 62,500 = 1.0e8 actions, '
+                         'split over the ranks; 0 = the step batch)')
     ap.add_argument('--xt-sharded', action='store_true',
                     help='cfg5 with N > 1: reduce-scatter the count rows and row-shard the value '
                          'iteration (default: one all-reduce, replicated solve)')
-    ap.add_argument('--atomic-games', type=int, default=1250,
-                    help='atomic games per GPU for cfg3 (1250 ~ 5M atomic actions)')
+    ap.add_argument('--atomic-games', type=int, default=10000,
+                    help='atomic games of the cfg3 side entry, split over the ranks (BASELINE '
+                         'cfg3: 10,000 = 4.0e7 atomic actions)')
     ap.add_argument('--serial', action='store_true',
                     help='run the xT fit + rate after the VAEP kernels on the same stream '
                          '(default: on a side stream, overlapped)')
@@ -653,7 +684,8 @@ def main() -> None:
         total_actions = int(_reduce(dist, n, dist.ReduceOp.SUM, dev))
     extra_side = {}
     if not args.no_side:
-        extra_side['xt105_cfg5'] = xt105_extra(ab, dist, dev, args.xt_sharded)
+        extra_side['xt105_cfg5'] = xt105_extra(ab, dist, dev, args.xt_sharded, args.cfg5_games,
+                                               rank, world, args.games)
         extra_side['atomic_cfg3'] = atomic_extra(dist, rank, world, dev, args.atomic_games)
         extra_side['convert_to_atomic'] = convert_extra(d, dist, dev)
         extra_side['rate_on_device'] = rate_extra(ab, out, n, dev)
