@@ -86,7 +86,8 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         out['ms'].setdefault('torch_fill', []).append(round(e0.elapsed_time(e1) / args.reps, 4))
-        print(json.dumps({'alloc': a, **{v: out['ms'][v][-1] for v in out['ms']}}), flush=True)
+        print(json.dumps({'alloc': a, 'va': hex(bb.data_ptr()),
+                          **{v: out['ms'][v][-1] for v in out['ms']}}), flush=True)
     print(json.dumps(out), flush=True)
 
 
