@@ -38,18 +38,22 @@ SPADL_DEFAULT = ['actiontype_onehot', 'result_onehot', 'actiontype_result_onehot
 # algorithmic bytes per action of each kernel (its inputs read once + outputs written once;
 # DESIGN.md "Kernels and rooflines")
 BYTES = {'bool_features': 7 + 515,             # type/result/bodypart u8 + team i32 -> 515 bools
-         'num_features': 48 + 47 * 8 + 3 * 8,  # 5 f64 + 4 u8 + team -> 47 f64 + 3 i64
+         # 5 f64 + 4 u8 + team -> 47 f64 + 6 i64 (period ids, and goalscore fused in)
+         'num_features': 48 + 47 * 8 + 6 * 8,
+         'num_features_nogs': 48 + 47 * 8 + 3 * 8,  # A/B: goalscore as its own scan
          'goalscore': 6 + 24, 'labels': 6 + 2, 'formula': 30 + 24,
          'labels_formula': 30 + 2 + 24,  # type/result/team/time/2 probs -> 2 labels + 3 values
          # count pass 34 B + its 4-B rate codes, rate 4 + 8 B (solve: 192 cells)
          'xt_fit_rate': 34 + 4 + 4 + 8}
-KERNELS = ('bool_features', 'num_features', 'goalscore', 'labels', 'formula', 'labels_formula',
-           'xt_fit_rate')
+KERNELS = ('bool_features', 'num_features', 'num_features_nogs', 'goalscore', 'labels', 'formula',
+           'labels_formula', 'xt_fit_rate')
 STEP_CALLS = ('bool_features', 'num_features', 'goalscore', 'labels', 'formula')
 # launch entries that cover several of STEP_CALLS in one kernel
-FUSED_CALLS = {'labels_formula': ('labels', 'formula')}
+FUSED_CALLS = {'labels_formula': ('labels', 'formula'), 'num_features': ('num_features', 'goalscore'),
+               'num_features_nogs': ('num_features',)}
 # the HIP kernel each step entry launches (socceraction_amd/csrc/sa_vaep.hip)
 KERNEL_NAMES = {'bool_features': 'bool_colgroup_kernel', 'num_features': 'num_features_kernel',
+                'num_features_nogs': 'num_features_kernel',
                 'goalscore': 'goalscore_wave16_kernel', 'labels': 'labels_kernel',
                 'formula': 'formula_kernel', 'labels_formula': 'labels_formula_kernel',
                 'xt_fit_rate': 'xt_count_kernel + xt_solve_reg_kernel + xt_rate_cells_kernel'}
@@ -60,6 +64,7 @@ def step_bytes(xt_source: str) -> dict:
     b = dict(BYTES)
     if xt_source == 'cells':  # the f64 pass writes 4 B of cell code; count reads 4, rate 4 + 8
         b['num_features'] += 4
+        b['num_features_nogs'] += 4
         b['xt_fit_rate'] = 4 + 4 + 8
     elif xt_source == 'coords':  # count 34 B, rate 34 + 8
         b['xt_fit_rate'] = 34 + 34 + 8
@@ -175,6 +180,11 @@ def xt_step(ab, dist, source: str = 'cells', cells=None, shared: bool = True):
 ATOMIC_DEFAULT = ['actiontype', 'actiontype_onehot', 'bodypart', 'bodypart_onehot', 'time',
                   'team', 'time_delta', 'location', 'polar', 'movement_polar', 'direction',
                   'goalscore']
+
+
+def _num_index(order) -> int:
+    """Position of the numeric feature pass (num_features or num_features_nogs) in a step order."""
+    return next(i for i, k in enumerate(order) if k.startswith('num_features'))
 
 
 def _record(stream) -> 'torch.cuda.Event':
@@ -477,8 +487,10 @@ def main() -> None:
                          'else 0)')
     ap.add_argument('--bool-tile', type=int, default=1024,
                     help='rows per bool-block tile (0 = one tile: plain column-major)')
-    ap.add_argument('--order', default='num_features,bool_features,goalscore,labels_formula',
-                    help='launch order of the VAEP kernels in the step; labels_formula = labels + '
+    ap.add_argument('--order', default='num_features,bool_features,labels_formula',
+                    help='launch order of the VAEP kernels in the step; num_features includes '
+                         'goalscore (num_features_nogs + goalscore: the separate scan); '
+                         'labels_formula = labels + '
                          'formula in one launch (num first: 1.3 %% faster than bool first, '
                          'profiles/r01h_order_ab.log; fused tail 3.236 vs 3.244 ms, '
                          'profiles/r02_step_ab.md)')
@@ -514,7 +526,7 @@ def main() -> None:
                                    num_tile=args.num_tile or None)
     ld = (n + 15) // 16 * 16
 
-    def sub(keep):  # the same block layout with only some column families launched
+    def sub(keep):  # the same block layout with only some column families launched ('g': goalscore)
         q = copy.copy(plan)
         q.struct = copy.deepcopy(plan.struct)
         for x in range(len(q.struct.bool_col)):
@@ -522,12 +534,12 @@ def main() -> None:
                 q.struct.bool_col[x] = -1
             if 'f' not in keep:
                 q.struct.f64_col[x] = -1
-            if 'i' not in keep or x == XFN['goalscore']:
+            if 'i' not in keep or (x == XFN['goalscore'] and 'g' not in keep):
                 q.struct.i64_col[x] = -1
         return ops.FeatureBlocks(q, n, out.Rb, out.Rn, out.bool_block, out.f64_block,
                                  out.i64_block)
 
-    bool_out, num_out = sub('b'), sub('fi')
+    bool_out, num_out, num_nogs = sub('b'), sub('fig'), sub('fi')
     p = synthetic.probabilities(n)
     ps = torch.from_numpy(p['scores']).to(dev)
     pc = torch.from_numpy(p['concedes']).to(dev)
@@ -554,12 +566,15 @@ def main() -> None:
         if covered != sorted(STEP_CALLS):
             raise SystemExit(f'order must cover {",".join(STEP_CALLS)} once each '
                              f'(fused entries: {FUSED_CALLS})')
-        if xt == 'cells' and overlap and fork <= order.index('num_features'):
+        if xt == 'cells' and overlap and fork <= _num_index(order):
             raise SystemExit('xt=cells: the side stream forks after num_features')
         by_name = {'bool_features': lambda: ops.features_into(s_act, bool_out),
                    'num_features': (lambda: ops.features_into(s_act, num_out,
                                                               xt_cells=(16, 12, cells)))
                    if xt in ('cells', 'none') else (lambda: ops.features_into(s_act, num_out)),
+                   'num_features_nogs': (lambda: ops.features_into(s_act, num_nogs,
+                                                                   xt_cells=(16, 12, cells)))
+                   if xt in ('cells', 'none') else (lambda: ops.features_into(s_act, num_nogs)),
                    'goalscore': lambda: ops.goalscore_into(ab, out),
                    'labels': lambda: ops.labels(ab, 10, lab),
                    'formula': lambda: ops.formula(ab, ps, pc, val),
@@ -630,7 +645,7 @@ def main() -> None:
     base = {'xt': args.xt_source, 'order': args.order.split(','), 'fork': args.xt_fork,
             'prio': args.side_priority, 'cm': int(args.xt_count == 'main')}
     if base['fork'] < 0:  # default: before the first VAEP call, or right after num_features
-        base['fork'] = (base['order'].index('num_features') + 1) if args.xt_source == 'cells' else 0
+        base['fork'] = (_num_index(base['order']) + 1) if args.xt_source == 'cells' else 0
     if args.ab:  # in-process A/B of step variants on the same allocations (dev tool)
         # ";"-separated "name:key=value/key=value" with keys xt, order (names joined by "+"), fork
         variants = {}

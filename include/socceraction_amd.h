@@ -153,8 +153,9 @@ int sa_vaep_features_bits(const sa_actions* a, const sa_feature_plan* plan, uint
                           const sa_block* i64_out, void* stream);
 
 /* goalscore alone (vaep/features.py:505-539; atomic/vaep/features.py:229-260): writes the
- * goalscore_team / _opponent / _diff columns col, col+1, col+2 of the i64 block.  Also
- * launched by sa_vaep_features when the plan requests SA_XFN_GOALSCORE. */
+ * goalscore_team / _opponent / _diff columns col, col+1, col+2 of the i64 block (one wave per
+ * segment).  sa_vaep_features computes the columns inside its numeric pass in windowed mode
+ * and launches this scan for explicit frames. */
 int sa_vaep_goalscore(const sa_actions* a, const sa_block* i64_out, int32_t col, void* stream);
 
 /* Replaces labels.scores / concedes / goal_from_shot (vaep/labels.py:9-116;

@@ -113,6 +113,14 @@ __device__ __forceinline__ void seg_advance(const sa_actions& A, SegCursor& c, i
   }
 }
 
+// Wave-uniform segment cursor of row jw: one search per wave (scalar loads); lanes then advance
+// from it to their own rows -- a per-lane binary search was ~14 dependent divergent loads.
+__device__ __forceinline__ SegCursor wave_cursor(const sa_actions& A, int64_t jw) {
+  const int lo = __builtin_amdgcn_readfirstlane((int)(jw & 0xFFFFFFFF));
+  const int hi = __builtin_amdgcn_readfirstlane((int)(jw >> 32));
+  return seg_at(A, ((int64_t)hi << 32) | (uint32_t)lo);
+}
+
 // Game-state windows of a lane's 16 actions, kept as 16 bytes (4 words) per id column.
 // R[0..5] holds rows j0-8 .. j0+15 (byte 8 = row j0).  Window i+1 is the window-i rows
 // shifted by one row, except for actions whose row already reached the segment start
@@ -202,6 +210,44 @@ __device__ __forceinline__ void goal_bytes(uint32_t tw, uint32_t rw, bool atomic
     g = shot & bytes_eq(rw, R_SUCCESS);
     o = shot & bytes_eq(rw, R_OWNGOAL);
   }
+}
+
+struct Gs16In {
+  u32x4 ty, rs;
+  int32_t tm[16];
+};
+
+template <bool ATOMIC>
+__device__ __forceinline__ void gs16_load(const sa_frame& F, int64_t j0, int64_t n, Gs16In& v) {
+  if (j0 >= 0 && j0 + 16 <= n) {
+    v.ty = *reinterpret_cast<const u32x4*>(F.type_id + j0);
+    v.rs = ATOMIC ? u32x4{0, 0, 0, 0} : *reinterpret_cast<const u32x4*>(F.result_id + j0);
+    const int4* tp = reinterpret_cast<const int4*>(F.team + j0);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int4 t = tp[q];
+      v.tm[4 * q] = t.x;
+      v.tm[4 * q + 1] = t.y;
+      v.tm[4 * q + 2] = t.z;
+      v.tm[4 * q + 3] = t.w;
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      v.ty[q] = ld_u8x4(F.type_id, j0 / 4 + q, n);
+      v.rs[q] = ATOMIC ? 0u : ld_u8x4(F.result_id, j0 / 4 + q, n);
+    }
+#pragma unroll
+    for (int m = 0; m < 16; ++m) v.tm[m] = ld_or0(F.team, j0 + m, n);
+  }
+}
+
+constexpr int GS_LDS_PITCH = 18;  // i64 per lane: 16 rows + pad (144 B: 16-B aligned)
+
+__device__ __forceinline__ void wave_sync() {  // LDS hand-off between the lanes of one wave
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 // ------------------------------------------------------------------------------ bool block
@@ -578,6 +624,119 @@ __device__ __forceinline__ void row_to_win(const Row& r, Win& w, int e) {
   w.bp[e] = r.ids >> 24;
 }
 
+// ------------------------------------------------------------------------------ goalscore,
+// fused into the numeric pass (windowed mode).  features.py:505-539 /
+// atomic/vaep/features.py:229-260: per segment, A = team of the segment's first row; for each
+// action the goals of its own team and of the other team before it (exclusive cumsum of the
+// goal / owngoal credits) and their difference.  A wave's 128 rows need (1) the goals of the
+// segment of its first row between that segment's start and the wave's first row -- counted
+// by the whole wave, 16 rows per lane per pass, from L2 (the neighbouring tiles of the same
+// game run on the same XCD) -- and (2) the exclusive counts inside the wave: four 64-bit
+// ballots (credits of A and of B on even and on odd rows) and a popcount of the lanes between
+// the row's segment start and the row.  No inter-wave dependency, no extra launch.
+
+// (goals of A, goals of B) in rows [s, e) of one segment whose first-row team is `ta`, packed
+// as low / high 32 bits; every lane of the wave must call it and gets the total.
+template <bool ATOMIC>
+__device__ __forceinline__ uint64_t wave_goals(const sa_frame& F, int64_t n, int64_t s, int64_t e,
+                                               int32_t ta) {
+  const int lane = threadIdx.x & (WAVE - 1);
+  uint64_t acc = 0;
+  for (int64_t base = s & ~(int64_t)15; base < e; base += 16 * WAVE) {  // wave-uniform
+    const int64_t j0 = base + 16 * lane;
+    if (j0 < e) {
+      Gs16In v;
+      gs16_load<ATOMIC>(F, j0, n, v);
+      uint32_t gm = 0, om = 0, am = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        uint32_t gb, ob;
+        goal_bytes(v.ty[q], v.rs[q], ATOMIC, gb, ob);
+        gm |= pack4(gb) << (4 * q);
+        om |= pack4(ob) << (4 * q);
+      }
+#pragma unroll
+      for (int m = 0; m < 16; ++m) am |= (uint32_t)(v.tm[m] == ta) << m;
+      const int lo = s > j0 ? (int)(s - j0) : 0;
+      const int hi = e < j0 + 16 ? (int)(e - j0) : 16;
+      const uint32_t vm = lo >= hi ? 0u : (0xFFFFu >> (16 - (hi - lo))) << lo;
+      const uint32_t gA = ((gm & am) | (om & ~am)) & vm, gB = ((gm & ~am) | (om & am)) & vm;
+      acc += (uint64_t)__popc(gA) | ((uint64_t)__popc(gB) << 32);
+    }
+  }
+#pragma unroll
+  for (int off = WAVE / 2; off > 0; off >>= 1) acc += __shfl_xor(acc, off, WAVE);
+  return acc;
+}
+
+// lanes [a, b) of a 64-bit ballot (0 <= a, b <= 64)
+__device__ __forceinline__ uint64_t lane_range(int a, int b) {
+  const uint64_t below_b = b >= 64 ? ~0ull : ((1ull << b) - 1ull);
+  const uint64_t below_a = a >= 64 ? ~0ull : ((1ull << a) - 1ull);
+  return a >= b ? 0ull : (below_b & ~below_a);
+}
+
+// goalscore_team / _opponent / _diff of the lane's rows jb, jb+1 (wave rows wb .. wb+127, rows
+// >= n write don't-care padding like the other columns).  Every lane of the wave must call it;
+// `c` = a segment cursor at or before row jb (clamped to n - 1).
+template <bool ATOMIC>
+__device__ __forceinline__ void goalscore_pair(const sa_actions& A, int64_t wb, int64_t jb, SegCursor c,
+                                               int64_t* __restrict__ ib, int gcol, int ni, int64_t Ri) {
+  const int64_t n = A.n;
+  const sa_frame& F = A.frames[0];
+  const int lane = threadIdx.x & (WAVE - 1);
+  const SegCursor c0 = wave_cursor(A, wb);  // segment of the wave's first row (uniform)
+  uint64_t carry = 0;
+  if (c0.s < wb) carry = wave_goals<ATOMIC>(F, n, c0.s, wb, F.team[c0.s]);
+  bool gA[2], gB[2], isA[2];
+  int64_t s[2];
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    const int64_t j = jb + e < n ? jb + e : n - 1;
+    seg_advance(A, c, j);
+    s[e] = c.s;
+    const int t = F.type_id[j];
+    bool goal, og;
+    if (ATOMIC) {
+      goal = t == AT_GOAL;
+      og = t == AT_OWNGOAL;
+    } else {
+      const bool shot = t == T_SHOT || t == T_SHOT_PENALTY || t == T_SHOT_FREEKICK;
+      const int r = F.result_id[j];
+      goal = shot && r == R_SUCCESS;
+      og = shot && r == R_OWNGOAL;
+    }
+    isA[e] = F.team[j] == F.team[c.s];
+    const bool valid = jb + e < n;
+    gA[e] = valid && ((goal && isA[e]) || (og && !isA[e]));
+    gB[e] = valid && ((goal && !isA[e]) || (og && isA[e]));
+  }
+  const uint64_t EA = __ballot(gA[0]), OA = __ballot(gA[1]);
+  const uint64_t EB = __ballot(gB[0]), OB = __ballot(gB[1]);
+  int64_t v[3][2];
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    const int t = 2 * lane + e;                           // row offset in the wave
+    const int lo = s[e] > wb ? (int)(s[e] - wb) : 0;      // first row of the segment in the wave
+    const uint64_t me = lane_range((lo + 1) >> 1, (t + 1) >> 1);  // even rows in [lo, t)
+    const uint64_t mo = lane_range(lo >> 1, t >> 1);              // odd rows in [lo, t)
+    int64_t cA = __popcll(EA & me) + __popcll(OA & mo);
+    int64_t cB = __popcll(EB & me) + __popcll(OB & mo);
+    if (s[e] < wb) {
+      cA += (int64_t)(carry & 0xFFFFFFFFull);
+      cB += (int64_t)(carry >> 32);
+    }
+    const int64_t tm = isA[e] ? cA : cB, op = isA[e] ? cB : cA;
+    v[0][e] = tm;
+    v[1][e] = op;
+    v[2][e] = tm - op;
+  }
+  if (jb < n) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) st_i64x2(ib, gcol + k, ni, Ri, v[k][0], v[k][1]);
+  }
+}
+
 // KF = 3: windowed mode with nb_prev_actions <= 3.  The pair's rows jb-2 .. jb+1 are read
 // once (16-B loads) and the windows are formed in registers (see the loop below).
 // KF = 0: any mode / any k (explicit frames, k <= 8): per-window row loads.
@@ -592,9 +751,18 @@ __global__ __launch_bounds__(256) void num_features_kernel(FeatArgs args) {
   const int64_t Rf = args.Rf, Ri = args.Ri;
   const int64_t wave_base = (xcd_logical_block() * BLOCK_WAVES + wv) * WAVE_ACTS;
   const sa_frame& F0 = A.frames[0];
-  if (wave_base + 2 * lane >= n) return;
+  if (wave_base >= n) return;  // whole wave past the end (uniform: the goalscore ballots need every lane)
   SegCursor cur = {0, 0, 0};
-  if (!EXPLICIT) cur = seg_at(A, wave_base + 2 * lane);
+  const int gcol = EXPLICIT ? -1 : P.i64_col[SA_XFN_GOALSCORE];
+  if (!EXPLICIT) {
+    const int64_t jl = wave_base + 2 * lane < n ? wave_base + 2 * lane : n - 1;
+    cur = wave_cursor(A, wave_base);
+    seg_advance(A, cur, jl);
+    if (gcol >= 0)
+      goalscore_pair<ATOMIC>(A, wave_base, wave_base + 2 * lane, cur,
+                             args.iout + tile_off(jl & ~(int64_t)1, 0, args.Ci, Ri), gcol, (int)args.Ci, Ri);
+  }
+  if (wave_base + 2 * lane >= n) return;
   NumCols C;
   C.at = P.i64_col[SA_XFN_ACTIONTYPE];
   C.re = P.i64_col[SA_XFN_RESULT];
@@ -722,44 +890,6 @@ __global__ __launch_bounds__(256) void num_features_kernel(FeatArgs args) {
 // per lane; the next pass's loads go out before this pass is scanned).  A lane sums its 16
 // (goals A, goals B) increments as one packed u64, the wave scans the 64 lane totals, and the
 // lane then walks its rows with the exclusive count: 8 i64x2 stores per column per lane.
-struct Gs16In {
-  u32x4 ty, rs;
-  int32_t tm[16];
-};
-
-template <bool ATOMIC>
-__device__ __forceinline__ void gs16_load(const sa_frame& F, int64_t j0, int64_t n, Gs16In& v) {
-  if (j0 >= 0 && j0 + 16 <= n) {
-    v.ty = *reinterpret_cast<const u32x4*>(F.type_id + j0);
-    v.rs = ATOMIC ? u32x4{0, 0, 0, 0} : *reinterpret_cast<const u32x4*>(F.result_id + j0);
-    const int4* tp = reinterpret_cast<const int4*>(F.team + j0);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int4 t = tp[q];
-      v.tm[4 * q] = t.x;
-      v.tm[4 * q + 1] = t.y;
-      v.tm[4 * q + 2] = t.z;
-      v.tm[4 * q + 3] = t.w;
-    }
-  } else {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      v.ty[q] = ld_u8x4(F.type_id, j0 / 4 + q, n);
-      v.rs[q] = ATOMIC ? 0u : ld_u8x4(F.result_id, j0 / 4 + q, n);
-    }
-#pragma unroll
-    for (int m = 0; m < 16; ++m) v.tm[m] = ld_or0(F.team, j0 + m, n);
-  }
-}
-
-constexpr int GS_LDS_PITCH = 18;  // i64 per lane: 16 rows + pad (144 B: 16-B aligned)
-
-__device__ __forceinline__ void wave_sync() {  // LDS hand-off between the lanes of one wave
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
 template <bool ATOMIC>
 __global__ __launch_bounds__(256) void goalscore_wave16_kernel(sa_actions A,
                                                                int64_t* __restrict__ block,
@@ -955,14 +1085,6 @@ __device__ __forceinline__ void labels_rows(const sa_actions& A, int nr, uint8_t
   if (sc) st16(sc + j0, u32x4{s_out[0], s_out[1], s_out[2], s_out[3]});
   if (co) st16(co + j0, u32x4{c_out[0], c_out[1], c_out[2], c_out[3]});
   if (gfs) st16(gfs + j0, u32x4{g_out[0], g_out[1], g_out[2], g_out[3]});
-}
-
-// Wave-uniform segment cursor of row jw: one search per wave (scalar loads); lanes then advance
-// from it to their own rows -- a per-lane binary search was ~14 dependent divergent loads.
-__device__ __forceinline__ SegCursor wave_cursor(const sa_actions& A, int64_t jw) {
-  const int lo = __builtin_amdgcn_readfirstlane((int)(jw & 0xFFFFFFFF));
-  const int hi = __builtin_amdgcn_readfirstlane((int)(jw >> 32));
-  return seg_at(A, ((int64_t)hi << 32) | (uint32_t)lo);
 }
 
 template <bool ATOMIC>
@@ -1309,7 +1431,8 @@ static int launch_features(const sa_actions* a, const sa_feature_plan* plan, con
     rc = check_launch("bool_colgroup_kernel");
     if (rc) return rc;
   }
-  if (wn || xt_cells) {
+  const int gc = plan->i64_col[SA_XFN_GOALSCORE];
+  if (wn || xt_cells || (gc >= 0 && !expl)) {  // windowed mode: goalscore fused into this pass
     const bool fast = !expl && K <= 3;  // register-resident windows (KF = 3)
     if (a->atomic) {
       if (expl)
@@ -1329,8 +1452,7 @@ static int launch_features(const sa_actions* a, const sa_feature_plan* plan, con
     rc = check_launch("num_features_kernel");
     if (rc) return rc;
   }
-  const int gc = plan->i64_col[SA_XFN_GOALSCORE];
-  if (gc >= 0) rc = sa_vaep_goalscore(a, i64_out, gc, stream);
+  if (gc >= 0 && expl) rc = sa_vaep_goalscore(a, i64_out, gc, stream);  // explicit frames: own scan
   return rc;
 }
 

@@ -486,3 +486,37 @@ def test_atomic_cfg3_slice_sampled_games_vs_oracle(sa):
         lab = vo.labels(cols, atomic=True)
         for c in ('scores', 'concedes', 'goal_from_shot'):
             np.testing.assert_array_equal(getattr(lb, c)[s:e].cpu().numpy().astype(bool), lab[c])
+
+
+@pytest.mark.parametrize('atomic', [False, True])
+def test_fused_goalscore_matches_scan(sa, atomic):
+    """The goalscore columns the numeric feature pass computes in windowed mode (a wave's carry
+    counted from its segment's start + ballot counts inside the wave) == the standalone
+    one-wave-per-segment scan (``sa_vaep_goalscore``), bit for bit: on a goal-dense batch
+    (every 7th action a goal / owngoal credit) of full games + 300 games of 1..40 actions at
+    k = 1, 3, 5, and on 2,000 full-size games, where the carries span whole games."""
+    B, ops, syn = sa['batch'], sa['ops'], sa['synthetic']
+    default = vo.ATOMIC_DEFAULT if atomic else vo.SPADL_DEFAULT
+    dense = _small_games(syn, atomic, 17)
+    n = int(dense['game_off'][-1])
+    rng = np.random.default_rng(5)
+    hit = rng.random(n) < 1 / 7
+    if atomic:
+        dense['type_id'] = np.where(hit, rng.choice([27, 28], n), dense['type_id'])
+    else:
+        dense['type_id'] = np.where(hit, rng.choice([11, 12, 13], n), dense['type_id'])
+        dense['result_id'] = np.where(hit, rng.choice([0, 1, 3], n), dense['result_id'])
+    gen = syn.atomic_games if atomic else syn.spadl_games
+    for d, kk in ((dense, (1, 3, 5)), (gen(2000, seed=9), (3,))):
+        ab = B.ActionBatch.from_columns(d, atomic=atomic)
+        for k in kk:
+            fb = ops.features(ab, default, k, bool_tile=1024, num_tile=128)
+            fused = fb.i64_block.clone()
+            fb.i64_block.fill_(-7)
+            ops.goalscore_into(ab, fb)
+            gc = [col for name, kind, col in fb.plan.order if name.startswith('goalscore')]
+            assert len(gc) == 3
+            got = fused[:, gc, :].permute(1, 0, 2).reshape(3, -1)[:, :ab.n]
+            ref = fb.i64_block[:, gc, :].permute(1, 0, 2).reshape(3, -1)[:, :ab.n]
+            assert torch.equal(got, ref), (atomic, k)
+            assert int(ref[0].max()) > 0
