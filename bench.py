@@ -43,21 +43,16 @@ BYTES = {'bool_features': 7 + 515,             # type/result/bodypart u8 + team 
          'num_features_nogs': 48 + 47 * 8 + 3 * 8,  # A/B: goalscore as its own scan
          'goalscore': 6 + 24, 'labels': 6 + 2, 'formula': 30 + 24,
          'labels_formula': 30 + 2 + 24,  # type/result/team/time/2 probs -> 2 labels + 3 values
-         # the bool pass with labels + formula riding in it: type/result/bodypart/team, time,
-         # 2 probs -> 515 bools + 2 labels + 3 values
-         'bool_tail': 7 + 8 + 16 + 515 + 2 + 24,
          # count pass 34 B + its 4-B rate codes, rate 4 + 8 B (solve: 192 cells)
          'xt_fit_rate': 34 + 4 + 4 + 8}
-KERNELS = ('bool_features', 'bool_tail', 'num_features', 'num_features_nogs', 'goalscore', 'labels',
-           'formula', 'labels_formula', 'xt_fit_rate')
+KERNELS = ('bool_features', 'num_features', 'num_features_nogs', 'goalscore', 'labels', 'formula',
+           'labels_formula', 'xt_fit_rate')
 STEP_CALLS = ('bool_features', 'num_features', 'goalscore', 'labels', 'formula')
 # launch entries that cover several of STEP_CALLS in one kernel
 FUSED_CALLS = {'labels_formula': ('labels', 'formula'), 'num_features': ('num_features', 'goalscore'),
-               'bool_tail': ('bool_features', 'labels', 'formula'),
                'num_features_nogs': ('num_features',)}
 # the HIP kernel each step entry launches (socceraction_amd/csrc/sa_vaep.hip)
-KERNEL_NAMES = {'bool_features': 'bool_colgroup_kernel', 'bool_tail': 'bool_colgroup_kernel',
-                'num_features': 'num_features_kernel',
+KERNEL_NAMES = {'bool_features': 'bool_colgroup_kernel', 'num_features': 'num_features_kernel',
                 'num_features_nogs': 'num_features_kernel',
                 'goalscore': 'goalscore_wave16_kernel', 'labels': 'labels_kernel',
                 'formula': 'formula_kernel', 'labels_formula': 'labels_formula_kernel',
@@ -583,8 +578,7 @@ def main() -> None:
                    'goalscore': lambda: ops.goalscore_into(ab, out),
                    'labels': lambda: ops.labels(ab, 10, lab),
                    'formula': lambda: ops.formula(ab, ps, pc, val),
-                   'labels_formula': lambda: ops.labels_formula(ab, ps, pc, 10, lab, val),
-                   'bool_tail': lambda: ops.features_tail_into(s_act, bool_out, ps, pc, 10, lab, val)}
+                   'labels_formula': lambda: ops.labels_formula(ab, ps, pc, 10, lab, val)}
         calls = tuple(by_name[k] for k in order)
         # cm=1: the count pass runs on the main stream right after num_features, in the fast
         # one-workgroup-per-CU shape; the side stream takes the all-reduce, solve and rate

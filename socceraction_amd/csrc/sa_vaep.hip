@@ -61,13 +61,6 @@ struct FeatArgs {
   int32_t xt_l, xt_w;
   uint16_t* bbits;     // optional: bool features as bitmaps instead of bout (sa_vaep_features_bits)
   int64_t bstride;     // u16 per bitmap
-  // optional tail (sa_vaep_features_tail_f64): labels + f64 formula of every tile, computed by
-  // the tile's last column-group wave of the bool pass
-  int32_t nr;
-  uint8_t *sc, *co, *gfs;
-  const double *ps, *pc;
-  double *off, *def, *val;
-  bool vec_ok;
 };
 
 // Workgroups are dispatched round-robin over the 8 XCDs (XCD = blockIdx % 8).  Writing the
@@ -271,13 +264,7 @@ constexpr int BOOL_TILE = 1024;  // rows per tile of the bool block image
 constexpr int CG_WAVES = 4;  // waves per workgroup
 #define CG_EQ(w, v) bytes_eq((w), (v))
 
-template <bool ATOMIC, typename T>
-__device__ void labels_formula_rows(const sa_actions& A, int nr, uint8_t* __restrict__ sc, uint8_t* __restrict__ co,
-                                    uint8_t* __restrict__ gfs, const T* __restrict__ ps, const T* __restrict__ pc,
-                                    T* __restrict__ off, T* __restrict__ def, T* __restrict__ val, bool vec_ok,
-                                    int64_t jw);
-
-template <bool ATOMIC, bool EXPLICIT, bool BITS, bool TAIL = false>
+template <bool ATOMIC, bool EXPLICIT, bool BITS>
 __global__ __launch_bounds__(64 * CG_WAVES) void bool_colgroup_kernel(FeatArgs args, int ngroups,
                                                                       int gcols) {
   const int lane = threadIdx.x & (WAVE - 1);
@@ -297,10 +284,6 @@ __global__ __launch_bounds__(64 * CG_WAVES) void bool_colgroup_kernel(FeatArgs a
   // team_1 .. team_{K-1} columns inside [c_lo, c_hi)?
   const bool need_team = tcol >= 0 && K > 1 && tcol < c_hi && tcol + K - 1 > c_lo;
   if (tile0 >= n || c_lo >= c_hi) return;
-  // the tile's last column group (the narrowest) also takes the tile's labels + formula rows
-  if (TAIL && w % ngroups == ngroups - 1)
-    labels_formula_rows<ATOMIC, double>(A, args.nr, args.sc, args.co, args.gfs, args.ps, args.pc, args.off,
-                                        args.def, args.val, args.vec_ok, tile0);
   uint8_t* bb = BITS ? nullptr : args.bout + tile_off(j0 < n ? j0 : tile0, 0, args.Cb, R);
   if (j0 >= n) return;
   // d = min(j - seg_start, 15) per action: segment of the tile start (same for all lanes),
@@ -1262,16 +1245,19 @@ __global__ __launch_bounds__(256) void formula_kernel(sa_actions A, const T* __r
 // Labels and formula of the same 1024 rows in one wave (the step's tail: one launch, the ids
 // and team codes read once): the labels part as labels_kernel (a lane owns 16 rows), then the
 // formula part in passes of 64 * V rows as formula_kernel (a lane owns V rows), both lanes'
-// segment cursors advancing from one wave-uniform search.  Rows jw .. jw+1023 of one wave
-// (jw < n, every lane of the wave present); also the tail of sa_vaep_features_tail_f64's bool
-// pass (bool_colgroup_kernel<..., TAIL>).
+// segment cursors advancing from one wave-uniform search.
 template <bool ATOMIC, typename T>
-__device__ void labels_formula_rows(const sa_actions& A, int nr, uint8_t* __restrict__ sc, uint8_t* __restrict__ co,
-                                    uint8_t* __restrict__ gfs, const T* __restrict__ ps, const T* __restrict__ pc,
-                                    T* __restrict__ off, T* __restrict__ def, T* __restrict__ val, bool vec_ok,
-                                    int64_t jw) {
+__global__ __launch_bounds__(256) void labels_formula_kernel(sa_actions A, int nr, uint8_t* __restrict__ sc,
+                                                             uint8_t* __restrict__ co,
+                                                             uint8_t* __restrict__ gfs,
+                                                             const T* __restrict__ ps,
+                                                             const T* __restrict__ pc, T* __restrict__ off,
+                                                             T* __restrict__ def, T* __restrict__ val,
+                                                             bool vec_ok) {
   constexpr int V = 16 / sizeof(T);
   const int lane = threadIdx.x & (WAVE - 1);
+  const int64_t jw = ((int64_t)blockIdx.x * (blockDim.x / WAVE) + threadIdx.x / WAVE) * (WAVE * LANE_ACTS);
+  if (jw >= A.n) return;
   const SegCursor wc = wave_cursor(A, jw);
   const int64_t jl = jw + (int64_t)lane * LANE_ACTS;
   if (jl < A.n) labels_rows<ATOMIC>(A, nr, sc, co, gfs, jl, wc);
@@ -1282,19 +1268,6 @@ __device__ void labels_formula_rows(const sa_actions& A, int nr, uint8_t* __rest
     if (base >= A.n) break;  // uniform
     formula_rows<ATOMIC, T>(A, ps, pc, off, def, val, vec_ok, base + (int64_t)lane * V, fc);
   }
-}
-
-template <bool ATOMIC, typename T>
-__global__ __launch_bounds__(256) void labels_formula_kernel(sa_actions A, int nr, uint8_t* __restrict__ sc,
-                                                             uint8_t* __restrict__ co,
-                                                             uint8_t* __restrict__ gfs,
-                                                             const T* __restrict__ ps,
-                                                             const T* __restrict__ pc, T* __restrict__ off,
-                                                             T* __restrict__ def, T* __restrict__ val,
-                                                             bool vec_ok) {
-  const int64_t jw = ((int64_t)blockIdx.x * (blockDim.x / WAVE) + threadIdx.x / WAVE) * (WAVE * LANE_ACTS);
-  if (jw >= A.n) return;
-  labels_formula_rows<ATOMIC, T>(A, nr, sc, co, gfs, ps, pc, off, def, val, vec_ok, jw);
 }
 
 }  // namespace sa
@@ -1340,17 +1313,10 @@ static int check_block(const sa_block* b, int64_t n, int64_t quantum, const char
   return SA_OK;
 }
 
-struct TailArgs {  // labels + f64 formula riding in the bool pass (sa_vaep_features_tail_f64)
-  int32_t nr;
-  uint8_t *sc, *co, *gfs;
-  const double *ps, *pc;
-  double *off, *def, *val;
-};
-
 static int launch_features(const sa_actions* a, const sa_feature_plan* plan, const sa_block* bool_out,
                            const sa_block* f64_out, const sa_block* i64_out, int32_t xt_l,
                            int32_t xt_w, uint32_t* xt_cells, void* stream, uint8_t* bits = nullptr,
-                           int64_t bits_stride = 0, int32_t n_bits = 0, const TailArgs* tail = nullptr);
+                           int64_t bits_stride = 0, int32_t n_bits = 0);
 
 extern "C" int sa_vaep_features(const sa_actions* a, const sa_feature_plan* plan,
                                 const sa_block* bool_out, const sa_block* f64_out,
@@ -1382,38 +1348,10 @@ extern "C" int sa_vaep_features_bits(const sa_actions* a, const sa_feature_plan*
                          n_bool_cols);
 }
 
-extern "C" int sa_vaep_features_tail_f64(const sa_actions* a, const sa_feature_plan* plan,
-                                         const sa_block* bool_out, const sa_block* f64_out,
-                                         const sa_block* i64_out, int32_t nr_actions, uint8_t* scores,
-                                         uint8_t* concedes, uint8_t* goal_from_shot, int64_t ld,
-                                         const double* p_scores, const double* p_concedes, double* off,
-                                         double* def, double* val, void* stream) {
-  int rc = check_actions(a, false);
-  if (rc) return rc;
-  if (nr_actions < 1) return fail(SA_EINVAL, "nr_actions must be >= 1");
-  if (ld % 16 != 0 || ld < ((a->n + 15) / 16) * 16)
-    return fail(SA_EINVAL, "ld must be a multiple of 16 and >= round_up(n, 16)");
-  if (!aligned16(scores) || !aligned16(concedes) || !aligned16(goal_from_shot))
-    return fail(SA_EINVAL, "label outputs must be 16-byte aligned");
-  if (!p_scores || !p_concedes || !off || !def || !val) return fail(SA_EINVAL, "null probability/output pointer");
-  if (!aligned16(off) || !aligned16(def) || !aligned16(val))
-    return fail(SA_EINVAL, "formula outputs must be 16-byte aligned (length >= round_up(n, 16))");
-  if (!plan) return fail(SA_EINVAL, "null plan");
-  bool wb = false;
-  for (int x = 0; x < SA_XFN_COUNT; ++x) wb |= plan->bool_col[x] >= 0;
-  if (!wb) {  // no bool pass to ride in: features, then the fused labels + formula launch
-    if ((rc = launch_features(a, plan, bool_out, f64_out, i64_out, 0, 0, nullptr, stream))) return rc;
-    return sa_vaep_labels_formula_f64(a, nr_actions, scores, concedes, goal_from_shot, ld, p_scores,
-                                      p_concedes, off, def, val, stream);
-  }
-  const TailArgs t{nr_actions, scores, concedes, goal_from_shot, p_scores, p_concedes, off, def, val};
-  return launch_features(a, plan, bool_out, f64_out, i64_out, 0, 0, nullptr, stream, nullptr, 0, 0, &t);
-}
-
 static int launch_features(const sa_actions* a, const sa_feature_plan* plan, const sa_block* bool_out,
                            const sa_block* f64_out, const sa_block* i64_out, int32_t xt_l,
                            int32_t xt_w, uint32_t* xt_cells, void* stream, uint8_t* bits,
-                           int64_t bits_stride, int32_t n_bits, const TailArgs* tail) {
+                           int64_t bits_stride, int32_t n_bits) {
   int rc = check_actions(a, true);
   if (rc) return rc;
   if (!plan) return fail(SA_EINVAL, "null plan");
@@ -1466,17 +1404,7 @@ static int launch_features(const sa_actions* a, const sa_feature_plan* plan, con
                 xt_l,
                 xt_w,
                 wb ? (uint16_t*)bits : nullptr,
-                bits_stride / 2,
-                tail ? tail->nr : 0,
-                tail ? tail->sc : nullptr,
-                tail ? tail->co : nullptr,
-                tail ? tail->gfs : nullptr,
-                tail ? tail->ps : nullptr,
-                tail ? tail->pc : nullptr,
-                tail ? tail->off : nullptr,
-                tail ? tail->def : nullptr,
-                tail ? tail->val : nullptr,
-                tail ? (aligned16(tail->ps) && aligned16(tail->pc)) : false};
+                bits_stride / 2};
   const dim3 grid(xcd_grid((a->n + BLOCK_ACTS - 1) / BLOCK_ACTS)), block(BLOCK_WAVES * WAVE);
   const bool expl = a->n_frames > 1;
   if (wb) {  // one wave per (tile, group of ~32 columns), XCD-contiguous sweep order
@@ -1489,11 +1417,6 @@ static int launch_features(const sa_actions* a, const sa_feature_plan* plan, con
         hipLaunchKernelGGL((bool_colgroup_kernel<true, false, true>), cgrid, cblock, 0, st, args, ng, gc);
       else
         hipLaunchKernelGGL((bool_colgroup_kernel<false, false, true>), cgrid, cblock, 0, st, args, ng, gc);
-    } else if (tail) {  // windowed mode (checked by the caller)
-      if (a->atomic)
-        hipLaunchKernelGGL((bool_colgroup_kernel<true, false, false, true>), cgrid, cblock, 0, st, args, ng, gc);
-      else
-        hipLaunchKernelGGL((bool_colgroup_kernel<false, false, false, true>), cgrid, cblock, 0, st, args, ng, gc);
     } else if (a->atomic) {
       if (expl)
         hipLaunchKernelGGL((bool_colgroup_kernel<true, true, false>), cgrid, cblock, 0, st, args, ng, gc);

@@ -520,41 +520,3 @@ def test_fused_goalscore_matches_scan(sa, atomic):
             ref = fb.i64_block[:, gc, :].permute(1, 0, 2).reshape(3, -1)[:, :ab.n]
             assert torch.equal(got, ref), (atomic, k)
             assert int(ref[0].max()) > 0
-
-
-@pytest.mark.parametrize('atomic', [False, True])
-def test_features_tail_matches_separate_launches(sa, atomic):
-    """sa_vaep_features_tail_f64 (labels + f64 formula computed by a wave of the bool pass) ==
-    sa_vaep_features followed by sa_vaep_labels_formula_f64, byte for byte: the goldens (edge
-    sizes 1..300, forced tail goals), full games + 300 games of 1..40 actions at nr_actions 1,
-    10 and 20 (the > 17 path reloads rows), both layouts, and 2,000 full-size games."""
-    B, ops, syn = sa['batch'], sa['ops'], sa['synthetic']
-    default = vo.ATOMIC_DEFAULT if atomic else vo.SPADL_DEFAULT
-    prefix = 'atomic' if atomic else 'spadl'
-    gen = syn.atomic_games if atomic else syn.spadl_games
-    batches = [B.ActionBatch.from_frame(frame(load(prefix, c), atomic), atomic=atomic,
-                                        home_team_id=load(prefix, c)['home_team_id'][0])
-               for c in cases(prefix)]
-    batches += [B.ActionBatch.from_columns(_small_games(syn, atomic, 23), atomic=atomic),
-                B.ActionBatch.from_columns(gen(2000, seed=31), atomic=atomic)]
-    rng = np.random.default_rng(8)
-    for bi, ab in enumerate(batches):
-        n = ab.n
-        ps = torch.from_numpy(rng.random(n)).to(ab.device)
-        pc = torch.from_numpy(rng.random(n)).to(ab.device)
-        layouts = ((1024, 128), (None, None)) if bi == len(batches) - 2 else ((1024, 128),)
-        for Rb, Rn in layouts:
-            for nr in ((1, 10, 20) if bi >= len(batches) - 2 else (10,)):
-                ref = ops.features(ab, default, 3, bool_tile=Rb, num_tile=Rn)
-                lref, vref = ops.labels_formula(ab, ps, pc, nr_actions=nr)
-                out = ops.alloc_feature_blocks(ref.plan, n, ab.device, Rb, Rn)
-                lab, val = ops.labels_formula(ab, ps, pc, nr_actions=nr)  # buffers of the right shape
-                for t in (lab.scores, lab.concedes, lab.goal_from_shot):
-                    t.fill_(7)
-                val.fill_(float('nan'))
-                ops.features_tail_into(ab.struct(), out, ps, pc, nr, lab, val)
-                for a, b in zip(out.to_numpy(), ref.to_numpy()):
-                    np.testing.assert_array_equal(a, b)
-                for c in ('scores', 'concedes', 'goal_from_shot'):
-                    assert torch.equal(getattr(lab, c)[:n], getattr(lref, c)[:n]), (bi, nr, c)
-                assert torch.equal(val[:, :n], vref[:, :n]), (bi, nr)
