@@ -41,19 +41,23 @@ BYTES = {'bool_features': 7 + 515,             # type/result/bodypart u8 + team 
          # 5 f64 + 4 u8 + team -> 47 f64 + 6 i64 (period ids, and goalscore fused in)
          'num_features': 48 + 47 * 8 + 6 * 8,
          'num_features_nogs': 48 + 47 * 8 + 3 * 8,  # A/B: goalscore as its own scan
+         # the numeric pass with labels + f64 formula riding in it (sa_vaep_step_f64): + 2 probs
+         # in, + 2 labels + 3 values out
+         'num_step': 48 + 16 + 47 * 8 + 6 * 8 + 2 + 24,
          'goalscore': 6 + 24, 'labels': 6 + 2, 'formula': 30 + 24,
          'labels_formula': 30 + 2 + 24,  # type/result/team/time/2 probs -> 2 labels + 3 values
          # count pass 34 B + its 4-B rate codes, rate 4 + 8 B (solve: 192 cells)
          'xt_fit_rate': 34 + 4 + 4 + 8}
-KERNELS = ('bool_features', 'num_features', 'num_features_nogs', 'goalscore', 'labels', 'formula',
-           'labels_formula', 'xt_fit_rate')
+KERNELS = ('bool_features', 'num_features', 'num_step', 'num_features_nogs', 'goalscore', 'labels',
+           'formula', 'labels_formula', 'xt_fit_rate')
 STEP_CALLS = ('bool_features', 'num_features', 'goalscore', 'labels', 'formula')
 # launch entries that cover several of STEP_CALLS in one kernel
 FUSED_CALLS = {'labels_formula': ('labels', 'formula'), 'num_features': ('num_features', 'goalscore'),
-               'num_features_nogs': ('num_features',)}
+               'num_features_nogs': ('num_features',),
+               'num_step': ('num_features', 'goalscore', 'labels', 'formula')}
 # the HIP kernel each step entry launches (socceraction_amd/csrc/sa_vaep.hip)
 KERNEL_NAMES = {'bool_features': 'bool_colgroup_kernel', 'num_features': 'num_features_kernel',
-                'num_features_nogs': 'num_features_kernel',
+                'num_features_nogs': 'num_features_kernel', 'num_step': 'num_features_kernel',
                 'goalscore': 'goalscore_wave16_kernel', 'labels': 'labels_kernel',
                 'formula': 'formula_kernel', 'labels_formula': 'labels_formula_kernel',
                 'xt_fit_rate': 'xt_count_kernel + xt_solve_reg_kernel + xt_rate_cells_kernel'}
@@ -65,6 +69,7 @@ def step_bytes(xt_source: str) -> dict:
     if xt_source == 'cells':  # the f64 pass writes 4 B of cell code; count reads 4, rate 4 + 8
         b['num_features'] += 4
         b['num_features_nogs'] += 4
+        b['num_step'] += 4
         b['xt_fit_rate'] = 4 + 4 + 8
     elif xt_source == 'coords':  # count 34 B, rate 34 + 8
         b['xt_fit_rate'] = 34 + 34 + 8
@@ -184,7 +189,7 @@ ATOMIC_DEFAULT = ['actiontype', 'actiontype_onehot', 'bodypart', 'bodypart_oneho
 
 def _num_index(order) -> int:
     """Position of the numeric feature pass (num_features or num_features_nogs) in a step order."""
-    return next(i for i, k in enumerate(order) if k.startswith('num_features'))
+    return next(i for i, k in enumerate(order) if k.startswith('num_'))
 
 
 def _record(stream) -> 'torch.cuda.Event':
@@ -487,10 +492,12 @@ def main() -> None:
                          'else 0)')
     ap.add_argument('--bool-tile', type=int, default=1024,
                     help='rows per bool-block tile (0 = one tile: plain column-major)')
-    ap.add_argument('--order', default='num_features,bool_features,labels_formula',
-                    help='launch order of the VAEP kernels in the step; num_features includes '
-                         'goalscore (num_features_nogs + goalscore: the separate scan); '
-                         'labels_formula = labels + '
+    ap.add_argument('--order', default='num_step,bool_features',
+                    help='launch order of the VAEP kernels in the step; num_step = the numeric '
+                         'pass with goalscore, labels and the f64 formula in it (sa_vaep_step_f64; '
+                         '3.115 vs 3.195 ms, profiles/r02u_goalscore_fused_ab.md); num_features = '
+                         'the numeric pass with goalscore; num_features_nogs + goalscore: the '
+                         'separate scan; labels_formula = labels + '
                          'formula in one launch (num first: 1.3 %% faster than bool first, '
                          'profiles/r01h_order_ab.log; fused tail 3.236 vs 3.244 ms, '
                          'profiles/r02_step_ab.md)')
@@ -509,6 +516,8 @@ def main() -> None:
                          '3.24 - 3.31 ms per step, profiles/r02_step_ab.md), or on the side stream')
     ap.add_argument('--num-tile', type=int, default=128,
                     help='rows per f64/i64-block tile (0 = one tile: plain column-major)')
+    ap.add_argument('--alloc-order', default='bool-first', choices=('bool-first', 'num-first'),
+                    help='dev knob: which feature block is allocated first')
     args = ap.parse_args()
     if args.gpus < 1:
         raise SystemExit('--gpus must be >= 1')
@@ -522,8 +531,15 @@ def main() -> None:
     ab = B.ActionBatch.from_columns(d, dev=dev)
     n = ab.n
     plan = catalog.build_plan(SPADL_DEFAULT, 3)
-    out = ops.alloc_feature_blocks(plan, n, dev, bool_tile=args.bool_tile or None,
-                                   num_tile=args.num_tile or None)
+    if args.alloc_order == 'num-first':  # dev knob: placement A/B of the output blocks
+        Rb, Rn = args.bool_tile or (n + 15) // 16 * 16, args.num_tile or (n + 15) // 16 * 16
+        fblk = torch.empty((-(-n // Rn), plan.n_f64, Rn), dtype=torch.float64, device=dev)
+        iblk = torch.empty((-(-n // Rn), plan.n_i64, Rn), dtype=torch.int64, device=dev)
+        bblk = torch.empty((-(-n // Rb), plan.n_bool, Rb), dtype=torch.uint8, device=dev)
+        out = ops.FeatureBlocks(plan, n, Rb, Rn, bblk, fblk, iblk)
+    else:
+        out = ops.alloc_feature_blocks(plan, n, dev, bool_tile=args.bool_tile or None,
+                                       num_tile=args.num_tile or None)
     ld = (n + 15) // 16 * 16
 
     def sub(keep):  # the same block layout with only some column families launched ('g': goalscore)
@@ -578,7 +594,10 @@ def main() -> None:
                    'goalscore': lambda: ops.goalscore_into(ab, out),
                    'labels': lambda: ops.labels(ab, 10, lab),
                    'formula': lambda: ops.formula(ab, ps, pc, val),
-                   'labels_formula': lambda: ops.labels_formula(ab, ps, pc, 10, lab, val)}
+                   'labels_formula': lambda: ops.labels_formula(ab, ps, pc, 10, lab, val),
+                   'num_step': lambda: ops.step_into(s_act, num_out, ps, pc, 10, lab, val,
+                                                     xt_cells=(16, 12, cells) if xt in ('cells', 'none')
+                                                     else None)}
         calls = tuple(by_name[k] for k in order)
         # cm=1: the count pass runs on the main stream right after num_features, in the fast
         # one-workgroup-per-CU shape; the side stream takes the all-reduce, solve and rate

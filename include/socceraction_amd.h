@@ -187,6 +187,18 @@ int sa_vaep_labels_formula_f32(const sa_actions* a, int32_t nr_actions, uint8_t*
                                const float* p_scores, const float* p_concedes, float* off,
                                float* def, float* val, void* stream);
 
+/* The batch valuation step in one call -- the notebook loop compute_features +
+ * compute_labels + formula.value (vaep/base.py:97-137, vaep/formula.py:116-151) over every
+ * segment: exactly sa_vaep_features (sa_vaep_features_xt when xt_cells != NULL) followed by
+ * sa_vaep_labels_formula_f64 with the same arguments.  With nb_prev_actions <= 3 and
+ * nr_actions <= 11 the labels and the formula are computed inside the numeric feature pass
+ * (no launch of their own); otherwise the two launches run.  Windowed mode. */
+int sa_vaep_step_f64(const sa_actions* a, const sa_feature_plan* plan, const sa_block* bool_out,
+                     const sa_block* f64_out, const sa_block* i64_out, int32_t xt_l, int32_t xt_w,
+                     uint32_t* xt_cells, int32_t nr_actions, uint8_t* scores, uint8_t* concedes,
+                     uint8_t* goal_from_shot, int64_t ld, const double* p_scores,
+                     const double* p_concedes, double* off, double* def, double* val, void* stream);
+
 /* ---- Expected Threat (xthreat.py) --------------------------------------------
  * Count pass over SPADL actions (frames[0] of `a`; segments ignored):
  * shot[c] += shots (type 11) by start cell, goal[c] += successful shots,

@@ -61,6 +61,13 @@ struct FeatArgs {
   int32_t xt_l, xt_w;
   uint16_t* bbits;     // optional: bool features as bitmaps instead of bout (sa_vaep_features_bits)
   int64_t bstride;     // u16 per bitmap
+  // optional tail (sa_vaep_step_f64): labels + f64 formula of the same rows, computed by the
+  // numeric pass (num_features_kernel<..., TAIL>)
+  int32_t nr;
+  uint8_t *sc, *co, *gfs;
+  const double *ps, *pc;
+  double *off, *def, *val;
+  bool vec_ok;
 };
 
 // Workgroups are dispatched round-robin over the 8 XCDs (XCD = blockIdx % 8).  Writing the
@@ -737,10 +744,109 @@ __device__ __forceinline__ void goalscore_pair(const sa_actions& A, int64_t wb, 
   }
 }
 
+// ------------------------------------------------------------------------------ tail in the
+// numeric pass (sa_vaep_step_f64): labels + f64 formula of the lane's rows jb, jb+1.
+template <bool ATOMIC, typename T>
+__device__ __forceinline__ void formula_rows(const sa_actions& A, const T* __restrict__ ps,
+                                             const T* __restrict__ pc, T* __restrict__ off,
+                                             T* __restrict__ def, T* __restrict__ val, bool vec_ok,
+                                             int64_t j0, SegCursor& cur);
+
+// goal (bit 0) / owngoal (bit 1) / shot (bit 2, atomic goal_from_shot) of row j
+template <bool ATOMIC>
+__device__ __forceinline__ uint32_t label_bits(const sa_frame& F, int64_t j) {
+  const int t = F.type_id[j];
+  if (ATOMIC) return (uint32_t)(t == AT_GOAL) | ((uint32_t)(t == AT_OWNGOAL) << 1) | ((uint32_t)(t == T_SHOT) << 2);
+  const bool shot = t == T_SHOT || t == T_SHOT_PENALTY || t == T_SHOT_FREEKICK;
+  const int r = F.result_id[j];
+  return (uint32_t)(shot && r == R_SUCCESS) | ((uint32_t)(shot && r == R_OWNGOAL) << 1);
+}
+
+// labels.scores / concedes / goal_from_shot (vaep/labels.py:9-116, atomic/vaep/labels.py:9-107)
+// of the lane's rows jb, jb+1 in the numeric pass's layout (lane l = rows wb + 2l, +1): the
+// look-ahead rows jb+2 .. jb+11 come from lanes l+1 .. l+5 by shuffles, the last five lanes load
+// the rows after the wave themselves.  nr_actions <= SA_STEP_MAX_NR.  Every lane of the wave
+// must call it; `c` = a segment cursor at or before row jb (clamped to n - 1).
+constexpr int SA_STEP_MAX_NR = 11;
+template <bool ATOMIC>
+__device__ __forceinline__ void labels_pair(const sa_actions& A, int nr, uint8_t* __restrict__ sc,
+                                            uint8_t* __restrict__ co, uint8_t* __restrict__ gfs, int64_t jb,
+                                            SegCursor c) {
+  const int64_t n = A.n;
+  const sa_frame& F = A.frames[0];
+  const int lane = threadIdx.x & (WAVE - 1);
+  uint32_t bits[6];   // rows jb + 2k (low nibble), jb + 2k + 1 (high nibble)
+  int32_t tm[6][2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int64_t j = jb + q < n ? jb + q : n - 1;
+    tm[0][q] = F.team[j];
+    bits[0] = q ? bits[0] | (label_bits<ATOMIC>(F, j) << 4) : label_bits<ATOMIC>(F, j);
+  }
+#pragma unroll
+  for (int k = 1; k < 6; ++k) {
+    bits[k] = __shfl_down(bits[0], k, WAVE);
+    tm[k][0] = __shfl_down(tm[0][0], k, WAVE);
+    tm[k][1] = __shfl_down(tm[0][1], k, WAVE);
+    if (lane + k >= WAVE) {  // rows after the wave
+      uint32_t b = 0;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int64_t j = jb + 2 * k + q < n ? jb + 2 * k + q : n - 1;
+        tm[k][q] = F.team[j];
+        b |= label_bits<ATOMIC>(F, j) << (4 * q);
+      }
+      bits[k] = b;
+    }
+  }
+  uint32_t so = 0, cout = 0, go = 0;
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    const int64_t j = jb + e;
+    if (j < n) {
+      seg_advance(A, c, j);
+      const int64_t last = c.e - 1;
+      const int64_t hj = j + nr - 1 < last ? j + nr - 1 : last;
+      const int hi = (int)(hj - jb);  // largest look-ahead offset from jb
+      const int32_t tj = tm[0][e];
+      const uint32_t bj = bits[0] >> (4 * e);
+      bool s = bj & 1u, cc = (bj >> 1) & 1u;
+#pragma unroll
+      for (int d = e + 1; d <= SA_STEP_MAX_NR; ++d) {
+        if (d <= hi) {
+          const uint32_t b = bits[d >> 1] >> (4 * (d & 1));
+          const bool same = tm[d >> 1][d & 1] == tj;
+          s |= ((b & 1u) && same) || ((b & 2u) && !same);
+          cc |= ((b & 1u) && !same) || ((b & 2u) && same);
+        }
+      }
+      bool gf;
+      if (ATOMIC)  // shot followed by a goal; the segment's last row compares NaN -> False
+        gf = ((bj >> 2) & 1u) && j < last && ((bits[(e + 1) >> 1] >> (4 * ((e + 1) & 1))) & 1u);
+      else
+        gf = bj & 1u;
+      so |= (uint32_t)s << (8 * e);
+      cout |= (uint32_t)cc << (8 * e);
+      go |= (uint32_t)gf << (8 * e);
+    }
+  }
+  if (jb < n) {
+    if (jb + 1 < n) {
+      if (sc) *reinterpret_cast<uint16_t*>(sc + jb) = (uint16_t)so;
+      if (co) *reinterpret_cast<uint16_t*>(co + jb) = (uint16_t)cout;
+      if (gfs) *reinterpret_cast<uint16_t*>(gfs + jb) = (uint16_t)go;
+    } else {
+      if (sc) sc[jb] = (uint8_t)so;
+      if (co) co[jb] = (uint8_t)cout;
+      if (gfs) gfs[jb] = (uint8_t)go;
+    }
+  }
+}
+
 // KF = 3: windowed mode with nb_prev_actions <= 3.  The pair's rows jb-2 .. jb+1 are read
 // once (16-B loads) and the windows are formed in registers (see the loop below).
 // KF = 0: any mode / any k (explicit frames, k <= 8): per-window row loads.
-template <bool ATOMIC, bool EXPLICIT, int KF>
+template <bool ATOMIC, bool EXPLICIT, int KF, bool TAIL = false>
 __global__ __launch_bounds__(256) void num_features_kernel(FeatArgs args) {
   const int lane = threadIdx.x & (WAVE - 1);
   const int wv = threadIdx.x / WAVE;
@@ -761,6 +867,12 @@ __global__ __launch_bounds__(256) void num_features_kernel(FeatArgs args) {
     if (gcol >= 0)
       goalscore_pair<ATOMIC>(A, wave_base, wave_base + 2 * lane, cur,
                              args.iout + tile_off(jl & ~(int64_t)1, 0, args.Ci, Ri), gcol, (int)args.Ci, Ri);
+    if (TAIL) {  // labels + formula of the same rows (every lane of the wave present)
+      labels_pair<ATOMIC>(A, args.nr, args.sc, args.co, args.gfs, wave_base + 2 * lane, cur);
+      SegCursor fc = cur;
+      formula_rows<ATOMIC, double>(A, args.ps, args.pc, args.off, args.def, args.val, args.vec_ok,
+                                   wave_base + 2 * lane, fc);
+    }
   }
   if (wave_base + 2 * lane >= n) return;
   NumCols C;
@@ -1313,10 +1425,17 @@ static int check_block(const sa_block* b, int64_t n, int64_t quantum, const char
   return SA_OK;
 }
 
+struct TailArgs {  // labels + f64 formula riding in the numeric pass (sa_vaep_step_f64)
+  int32_t nr;
+  uint8_t *sc, *co, *gfs;
+  const double *ps, *pc;
+  double *off, *def, *val;
+};
+
 static int launch_features(const sa_actions* a, const sa_feature_plan* plan, const sa_block* bool_out,
                            const sa_block* f64_out, const sa_block* i64_out, int32_t xt_l,
                            int32_t xt_w, uint32_t* xt_cells, void* stream, uint8_t* bits = nullptr,
-                           int64_t bits_stride = 0, int32_t n_bits = 0);
+                           int64_t bits_stride = 0, int32_t n_bits = 0, const TailArgs* tail = nullptr);
 
 extern "C" int sa_vaep_features(const sa_actions* a, const sa_feature_plan* plan,
                                 const sa_block* bool_out, const sa_block* f64_out,
@@ -1348,10 +1467,42 @@ extern "C" int sa_vaep_features_bits(const sa_actions* a, const sa_feature_plan*
                          n_bool_cols);
 }
 
+extern "C" int sa_vaep_step_f64(const sa_actions* a, const sa_feature_plan* plan, const sa_block* bool_out,
+                                const sa_block* f64_out, const sa_block* i64_out, int32_t xt_l, int32_t xt_w,
+                                uint32_t* xt_cells, int32_t nr_actions, uint8_t* scores, uint8_t* concedes,
+                                uint8_t* goal_from_shot, int64_t ld, const double* p_scores,
+                                const double* p_concedes, double* off, double* def, double* val,
+                                void* stream) {
+  int rc = check_actions(a, false);
+  if (rc) return rc;
+  if (!plan) return fail(SA_EINVAL, "null plan");
+  if (nr_actions < 1) return fail(SA_EINVAL, "nr_actions must be >= 1");
+  if (ld % 16 != 0 || ld < ((a->n + 15) / 16) * 16)
+    return fail(SA_EINVAL, "ld must be a multiple of 16 and >= round_up(n, 16)");
+  if (!aligned16(scores) || !aligned16(concedes) || !aligned16(goal_from_shot))
+    return fail(SA_EINVAL, "label outputs must be 16-byte aligned");
+  if (!p_scores || !p_concedes || !off || !def || !val) return fail(SA_EINVAL, "null probability/output pointer");
+  if (!aligned16(off) || !aligned16(def) || !aligned16(val))
+    return fail(SA_EINVAL, "formula outputs must be 16-byte aligned (length >= round_up(n, 16))");
+  if (xt_cells) {
+    if (a->atomic) return fail(SA_EINVAL, "xT cells need SPADL actions");
+    if (xt_l < 1 || xt_w < 1 || (int64_t)xt_l * xt_w > SA_XT_CELLS_MAX_C)
+      return fail(SA_EINVAL, "xT cell codes need 1 <= l * w <= %d", SA_XT_CELLS_MAX_C);
+    if (!aligned16(xt_cells)) return fail(SA_EINVAL, "xt_cells must be 16-byte aligned");
+  }
+  if (plan->nb_prev_actions > 3 || nr_actions > SA_STEP_MAX_NR) {  // no fused form: the separate launches
+    if ((rc = launch_features(a, plan, bool_out, f64_out, i64_out, xt_l, xt_w, xt_cells, stream))) return rc;
+    return sa_vaep_labels_formula_f64(a, nr_actions, scores, concedes, goal_from_shot, ld, p_scores,
+                                      p_concedes, off, def, val, stream);
+  }
+  const TailArgs t{nr_actions, scores, concedes, goal_from_shot, p_scores, p_concedes, off, def, val};
+  return launch_features(a, plan, bool_out, f64_out, i64_out, xt_l, xt_w, xt_cells, stream, nullptr, 0, 0, &t);
+}
+
 static int launch_features(const sa_actions* a, const sa_feature_plan* plan, const sa_block* bool_out,
                            const sa_block* f64_out, const sa_block* i64_out, int32_t xt_l,
                            int32_t xt_w, uint32_t* xt_cells, void* stream, uint8_t* bits,
-                           int64_t bits_stride, int32_t n_bits) {
+                           int64_t bits_stride, int32_t n_bits, const TailArgs* tail) {
   int rc = check_actions(a, true);
   if (rc) return rc;
   if (!plan) return fail(SA_EINVAL, "null plan");
@@ -1404,7 +1555,17 @@ static int launch_features(const sa_actions* a, const sa_feature_plan* plan, con
                 xt_l,
                 xt_w,
                 wb ? (uint16_t*)bits : nullptr,
-                bits_stride / 2};
+                bits_stride / 2,
+                tail ? tail->nr : 0,
+                tail ? tail->sc : nullptr,
+                tail ? tail->co : nullptr,
+                tail ? tail->gfs : nullptr,
+                tail ? tail->ps : nullptr,
+                tail ? tail->pc : nullptr,
+                tail ? tail->off : nullptr,
+                tail ? tail->def : nullptr,
+                tail ? tail->val : nullptr,
+                tail ? (aligned16(tail->ps) && aligned16(tail->pc)) : false};
   const dim3 grid(xcd_grid((a->n + BLOCK_ACTS - 1) / BLOCK_ACTS)), block(BLOCK_WAVES * WAVE);
   const bool expl = a->n_frames > 1;
   if (wb) {  // one wave per (tile, group of ~32 columns), XCD-contiguous sweep order
@@ -1432,9 +1593,14 @@ static int launch_features(const sa_actions* a, const sa_feature_plan* plan, con
     if (rc) return rc;
   }
   const int gc = plan->i64_col[SA_XFN_GOALSCORE];
-  if (wn || xt_cells || (gc >= 0 && !expl)) {  // windowed mode: goalscore fused into this pass
+  if (wn || xt_cells || tail || (gc >= 0 && !expl)) {  // windowed mode: goalscore fused into this pass
     const bool fast = !expl && K <= 3;  // register-resident windows (KF = 3)
-    if (a->atomic) {
+    if (tail) {  // windowed, K <= 3 (checked by sa_vaep_step_f64)
+      if (a->atomic)
+        hipLaunchKernelGGL((num_features_kernel<true, false, 3, true>), grid, block, 0, st, args);
+      else
+        hipLaunchKernelGGL((num_features_kernel<false, false, 3, true>), grid, block, 0, st, args);
+    } else if (a->atomic) {
       if (expl)
         hipLaunchKernelGGL((num_features_kernel<true, true, 0>), grid, block, 0, st, args);
       else if (fast)

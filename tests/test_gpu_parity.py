@@ -520,3 +520,61 @@ def test_fused_goalscore_matches_scan(sa, atomic):
             ref = fb.i64_block[:, gc, :].permute(1, 0, 2).reshape(3, -1)[:, :ab.n]
             assert torch.equal(got, ref), (atomic, k)
             assert int(ref[0].max()) > 0
+
+
+@pytest.mark.parametrize('atomic', [False, True])
+def test_step_matches_separate_launches(sa, atomic):
+    """sa_vaep_step_f64 (labels + f64 formula computed by the numeric pass, lane = 2 rows, the
+    look-ahead by wave shuffles) == sa_vaep_features (+ the xT cell codes) followed by
+    sa_vaep_labels_formula_f64, byte for byte: the goldens (edge sizes 1..300, forced tail goals),
+    full games + 300 games of 1..40 actions at nr_actions 1, 2, 10, 11 and 20 (the last runs the
+    separate launches), k = 1..4, both layouts, and 2,000 full-size games."""
+    B, ops, syn = sa['batch'], sa['ops'], sa['synthetic']
+    default = vo.ATOMIC_DEFAULT if atomic else vo.SPADL_DEFAULT
+    prefix = 'atomic' if atomic else 'spadl'
+    gen = syn.atomic_games if atomic else syn.spadl_games
+    batches = [B.ActionBatch.from_frame(frame(load(prefix, c), atomic), atomic=atomic,
+                                        home_team_id=load(prefix, c)['home_team_id'][0])
+               for c in cases(prefix)]
+    dense = _small_games(syn, atomic, 23)
+    hit = np.random.default_rng(3).random(len(dense['type_id'])) < 1 / 9
+    if atomic:
+        dense['type_id'] = np.where(hit, np.random.default_rng(4).choice([11, 27, 28], hit.size),
+                                    dense['type_id'])
+    else:
+        dense['type_id'] = np.where(hit, 11, dense['type_id'])
+        dense['result_id'] = np.where(hit, np.random.default_rng(4).choice([0, 1, 3], hit.size),
+                                      dense['result_id'])
+    batches += [B.ActionBatch.from_columns(dense, atomic=atomic),
+                B.ActionBatch.from_columns(gen(2000, seed=31), atomic=atomic)]
+    rng = np.random.default_rng(8)
+    for bi, ab in enumerate(batches):
+        n = ab.n
+        ps = torch.from_numpy(rng.random(n)).to(ab.device)
+        pc = torch.from_numpy(rng.random(n)).to(ab.device)
+        small = bi == len(batches) - 2
+        layouts = ((1024, 128), (None, None)) if small else ((1024, 128),)
+        for Rb, Rn in layouts:
+            for nr in ((1, 2, 10, 11, 20) if bi >= len(batches) - 2 else (10,)):
+                for k in ((1, 2, 3, 4) if small and nr == 10 else (3,)):
+                    xt = None if atomic else 16
+                    cells_ref = ops.xt_cells_buffer(n, ab.device) if xt else None
+                    ref = ops.alloc_feature_blocks(ops.build_plan(default, k, atomic), n, ab.device,
+                                                   Rb, Rn)
+                    ops.features_into(ab.struct(), ref, xt_cells=(16, 12, cells_ref) if xt else None)
+                    lref, vref = ops.labels_formula(ab, ps, pc, nr_actions=nr)
+                    out = ops.alloc_feature_blocks(ref.plan, n, ab.device, Rb, Rn)
+                    lab, val = ops.labels_formula(ab, ps, pc, nr_actions=nr)  # right-shaped buffers
+                    for t in (lab.scores, lab.concedes, lab.goal_from_shot):
+                        t.fill_(7)
+                    val.fill_(float('nan'))
+                    cells = ops.xt_cells_buffer(n, ab.device) if xt else None
+                    ops.step_into(ab.struct(), out, ps, pc, nr, lab, val,
+                                  xt_cells=(16, 12, cells) if xt else None)
+                    for a, b in zip(out.to_numpy(), ref.to_numpy()):
+                        np.testing.assert_array_equal(a, b)
+                    for c in ('scores', 'concedes', 'goal_from_shot'):
+                        assert torch.equal(getattr(lab, c)[:n], getattr(lref, c)[:n]), (bi, nr, k, c)
+                    assert torch.equal(val[:, :n], vref[:, :n]), (bi, nr, k)
+                    if xt:
+                        assert torch.equal(cells[:n], cells_ref[:n])
