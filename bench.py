@@ -579,7 +579,7 @@ def main() -> None:
         xt, order, fork = spec['xt'], spec['order'], spec['fork']
         side = sides[spec['prio']]
         covered = sorted(c for k in order for c in FUSED_CALLS.get(k, (k,)))
-        if covered != sorted(STEP_CALLS):
+        if covered != sorted(STEP_CALLS) and not int(spec.get('diag', 0)):  # diag=1: A/B probes only
             raise SystemExit(f'order must cover {",".join(STEP_CALLS)} once each '
                              f'(fused entries: {FUSED_CALLS})')
         if xt == 'cells' and overlap and fork <= _num_index(order):
@@ -673,14 +673,15 @@ def main() -> None:
             v = dict(base)
             for kv in [o for o in opts.split('/') if o]:
                 k_, _, v_ = kv.partition('=')
-                v[k_] = v_.split('+') if k_ == 'order' else (int(v_) if k_ in ('fork', 'par', 'cm') else v_)
-            variants[name] = make_step(v)[0]
+                v[k_] = v_.split('+') if k_ == 'order' else (int(v_) if k_ in ('fork', 'par', 'cm', 'diag') else v_)
+            variants[name] = (make_step(v)[0], v['order'])
         ab_ms = {k: [] for k in variants}
-        for fn in variants.values():
+        ab_kern = {}
+        for fn, _ in variants.values():
             for _ in range(args.warmup):
                 fn()
         for _ in range(4):
-            for k, fn in variants.items():
+            for k, (fn, _) in variants.items():
                 fn()
                 torch.cuda.synchronize()
                 t = time.perf_counter()
@@ -688,8 +689,16 @@ def main() -> None:
                     fn()
                 torch.cuda.synchronize()
                 ab_ms[k].append(round((time.perf_counter() - t) / args.steps * 1e3, 4))
+        for k, (fn, vorder) in variants.items():  # per-call HIP event means, one more round
+            evs = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                    for _ in range(len(vorder) + 1)] for _ in range(args.steps)]
+            for e in evs:
+                fn(e)
+            torch.cuda.synchronize()
+            ab_kern[k] = {c: round(float(np.mean([e[i][0].elapsed_time(e[i][1]) for e in evs])), 4)
+                          for i, c in enumerate(list(vorder) + ['xt_side'])}
         if rank == 0:
-            print(json.dumps({'ab_ms_per_step': ab_ms, 'n': n}), flush=True)
+            print(json.dumps({'ab_ms_per_step': ab_ms, 'ab_kernel_ms': ab_kern, 'n': n}), flush=True)
         return
     step, xt_last = make_step(base)
     order = base['order']

@@ -35,6 +35,18 @@ def main():
     for _ in range(3):
         ops.features(ab, SPADL_DEFAULT, 3, out=bits)
     torch.cuda.synchronize()
+    if '--time' in sys.argv:  # HIP-event ms per launch of each form (bool families only)
+        res = {}
+        for name, fn in (('block', lambda: ops.features_into(ab.struct(), blk)),
+                         ('bitmaps', lambda: ops.features(ab, SPADL_DEFAULT, 3, out=bits))):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            for _ in range(10):
+                fn()
+            b.record()
+            torch.cuda.synchronize()
+            res[name] = round(a.elapsed_time(b) / 10, 4)
+        print(res)
     print('done', ab.n)
 
 

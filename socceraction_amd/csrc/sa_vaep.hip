@@ -159,6 +159,28 @@ __device__ __forceinline__ uint32_t pack4(uint32_t x) {
   return (x & 1u) | ((x >> 7) & 2u) | ((x >> 14) & 4u) | ((x >> 21) & 8u);
 }
 
+// 4 x 4 byte transpose: word q byte k of the result = word k byte q of the input.  The bitmap
+// mode of the bool pass keeps a lane's 16 rows in this STRIDED order (word q byte k = row
+// 4k + q), so that the four compare words of a column combine into one word whose byte k holds
+// rows 4k .. 4k+3 as a nibble in row order (bits_of_strided).
+__device__ __forceinline__ void transpose_bytes4(uint32_t (&w)[4]) {
+  const uint32_t t0 = __builtin_amdgcn_perm(w[1], w[0], 0x05010400u);  // a0 b0 a1 b1
+  const uint32_t t1 = __builtin_amdgcn_perm(w[1], w[0], 0x07030602u);  // a2 b2 a3 b3
+  const uint32_t t2 = __builtin_amdgcn_perm(w[3], w[2], 0x05010400u);  // c0 d0 c1 d1
+  const uint32_t t3 = __builtin_amdgcn_perm(w[3], w[2], 0x07030602u);  // c2 d2 c3 d3
+  w[0] = __builtin_amdgcn_perm(t2, t0, 0x05040100u);                   // a0 b0 c0 d0
+  w[1] = __builtin_amdgcn_perm(t2, t0, 0x07060302u);                   // a1 b1 c1 d1
+  w[2] = __builtin_amdgcn_perm(t3, t1, 0x05040100u);                   // a2 b2 c2 d2
+  w[3] = __builtin_amdgcn_perm(t3, t1, 0x07060302u);                   // a3 b3 c3 d3
+}
+
+// 16 row bits (bit r = row r) of four 0x01-per-byte compare words in the strided order
+__device__ __forceinline__ uint32_t bits_of_strided(uint32_t e0, uint32_t e1, uint32_t e2, uint32_t e3) {
+  const uint32_t x = e0 | (e1 << 1) | (e2 << 2) | (e3 << 3);  // byte k: rows 4k .. 4k+3
+  const uint32_t y = x | (x >> 4);                             // bytes 0, 2: rows 0-7, 8-15
+  return (y & 0xFFu) | ((y >> 8) & 0xFF00u);
+}
+
 // Stores into tiled blocks: `base` already points at the lane's (tile, row) position of
 // column 0, so column c is c * R elements further.
 __device__ __forceinline__ void st_bool16(uint8_t* __restrict__ base, int64_t col, int64_t C, int64_t R,
@@ -169,13 +191,14 @@ __device__ __forceinline__ void st_bool16(uint8_t* __restrict__ base, int64_t co
 }
 
 // The 16 bool values (0x01 bytes) of a lane's rows j0 .. j0+15 of column `col`: 16 bytes into
-// the tiled bool block, or -- bitmap mode -- 16 bits into bitmap `col` (rows >= n cleared).
+// the tiled bool block (row order), or -- bitmap mode, words in the strided order -- 16 bits
+// into bitmap `col` (rows >= n cleared).
 template <bool BITS>
 __device__ __forceinline__ void st_bool_out(const FeatArgs& a, uint8_t* __restrict__ bb, int64_t col, int64_t j0,
                                             uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
   if (BITS) {
     SA_DGUARD(col >= 0 && col < a.Cb, col, return);
-    uint32_t b = pack4(w0) | (pack4(w1) << 4) | (pack4(w2) << 8) | (pack4(w3) << 12);
+    uint32_t b = bits_of_strided(w0, w1, w2, w3);
     if (a.a.n - j0 < 16) b &= (1u << (a.a.n - j0)) - 1u;
     a.bbits[col * a.bstride + j0 / 16] = (uint16_t)b;
   } else {
@@ -358,25 +381,38 @@ __global__ __launch_bounds__(64 * CG_WAVES) void bool_colgroup_kernel(FeatArgs a
         bw[q] = (BR[2 + q] & mk) | (bw[q] & ~mk);
       }
     }
+    // the compare operands: row order (byte block), strided order (bitmaps)
+    uint32_t xt[4], xr[4], xb[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      xt[q] = tw[q];
+      xr[q] = rw[q];
+      xb[q] = bw[q];
+    }
+    if (BITS) {
+      transpose_bytes4(xt);
+      if (!ATOMIC) transpose_bytes4(xr);
+      transpose_bytes4(xb);
+    }
     int v0, v1;
     if (c_type >= 0) {
       const int base = c_type + i * ntypes;
       range(base, ntypes, v0, v1);
       for (int u = v0; u < v1; ++u) {
         if (!ATOMIC) {
-          st_bool_out<BITS>(args, bb, base + u, j0, CG_EQ(tw[0], u), CG_EQ(tw[1], u), CG_EQ(tw[2], u),
-                    CG_EQ(tw[3], u));
+          st_bool_out<BITS>(args, bb, base + u, j0, CG_EQ(xt[0], u), CG_EQ(xt[1], u), CG_EQ(xt[2], u),
+                    CG_EQ(xt[3], u));
         } else {
           // 33 atomic names, 32 unique: 'interception' (ids 10 and 24) is ONE column true for
           // both ids (atomic/vaep/features.py:114-132 + atomic/spadl/config.py:25-36)
           const uint32_t id = u <= 23 ? (uint32_t)u : (uint32_t)u + 1;
-          uint32_t m0 = CG_EQ(tw[0], id), m1 = CG_EQ(tw[1], id), m2 = CG_EQ(tw[2], id),
-                   m3 = CG_EQ(tw[3], id);
+          uint32_t m0 = CG_EQ(xt[0], id), m1 = CG_EQ(xt[1], id), m2 = CG_EQ(xt[2], id),
+                   m3 = CG_EQ(xt[3], id);
           if (u == 10) {
-            m0 |= CG_EQ(tw[0], AT_INTERCEPTION2);
-            m1 |= CG_EQ(tw[1], AT_INTERCEPTION2);
-            m2 |= CG_EQ(tw[2], AT_INTERCEPTION2);
-            m3 |= CG_EQ(tw[3], AT_INTERCEPTION2);
+            m0 |= CG_EQ(xt[0], AT_INTERCEPTION2);
+            m1 |= CG_EQ(xt[1], AT_INTERCEPTION2);
+            m2 |= CG_EQ(xt[2], AT_INTERCEPTION2);
+            m3 |= CG_EQ(xt[3], AT_INTERCEPTION2);
           }
           st_bool_out<BITS>(args, bb, base + u, j0, m0, m1, m2, m3);
         }
@@ -386,8 +422,8 @@ __global__ __launch_bounds__(64 * CG_WAVES) void bool_colgroup_kernel(FeatArgs a
       const int base = c_res + i * N_RESULTS;
       range(base, N_RESULTS, v0, v1);
       for (int r = v0; r < v1; ++r)
-        st_bool_out<BITS>(args, bb, base + r, j0, CG_EQ(rw[0], r), CG_EQ(rw[1], r), CG_EQ(rw[2], r),
-                  CG_EQ(rw[3], r));
+        st_bool_out<BITS>(args, bb, base + r, j0, CG_EQ(xr[0], r), CG_EQ(xr[1], r), CG_EQ(xr[2], r),
+                  CG_EQ(xr[3], r));
     }
     if (c_tr >= 0) {
       const int base = c_tr + i * N_TYPES * N_RESULTS;
@@ -396,7 +432,7 @@ __global__ __launch_bounds__(64 * CG_WAVES) void bool_colgroup_kernel(FeatArgs a
         // code = type*6 + result per byte (type <= 22, result <= 5: no carry between bytes)
         uint32_t cw[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) cw[q] = (tw[q] << 2) + (tw[q] << 1) + rw[q];
+        for (int q = 0; q < 4; ++q) cw[q] = (xt[q] << 2) + (xt[q] << 1) + xr[q];
         for (int code = v0; code < v1; ++code)
           st_bool_out<BITS>(args, bb, base + code, j0, CG_EQ(cw[0], code), CG_EQ(cw[1], code),
                     CG_EQ(cw[2], code), CG_EQ(cw[3], code));
@@ -406,8 +442,8 @@ __global__ __launch_bounds__(64 * CG_WAVES) void bool_colgroup_kernel(FeatArgs a
       const int base = c_bp + i * N_BODYPARTS;
       range(base, N_BODYPARTS, v0, v1);
       for (int b = v0; b < v1; ++b)
-        st_bool_out<BITS>(args, bb, base + b, j0, CG_EQ(bw[0], b), CG_EQ(bw[1], b), CG_EQ(bw[2], b),
-                  CG_EQ(bw[3], b));
+        st_bool_out<BITS>(args, bb, base + b, j0, CG_EQ(xb[0], b), CG_EQ(xb[1], b), CG_EQ(xb[2], b),
+                  CG_EQ(xb[3], b));
     }
     const int tc = tcol + i - 1;
     if (need_team && i >= 1 && tc >= c_lo && tc < c_hi) {  // team_i (features.py:448-452)
@@ -427,7 +463,10 @@ __global__ __launch_bounds__(64 * CG_WAVES) void bool_colgroup_kernel(FeatArgs a
           t0 = ld_or0(F0.team, j0 + mm, n);
           ti = ld_or0(F0.team, j0 + mm - s, n);
         }
-        m[mm >> 2] |= (uint32_t)(t0 == ti) << (8 * (mm & 3));
+        if (BITS)  // strided order: word mm & 3, byte mm >> 2
+          m[mm & 3] |= (uint32_t)(t0 == ti) << (8 * (mm >> 2));
+        else
+          m[mm >> 2] |= (uint32_t)(t0 == ti) << (8 * (mm & 3));
       }
       st_bool_out<BITS>(args, bb, tc, j0, m[0], m[1], m[2], m[3]);
     }
