@@ -140,6 +140,9 @@ def xt_step(ab, dist, source: str = 'cells', cells=None, shared: bool = True):
     4-B rate operand per action for the rate; 'coords': both passes read the coordinates."""
     from socceraction_amd import shard
     state = {}
+    # the step's count buffers, allocated once and zeroed by ONE fill on the side stream while
+    # the numeric pass runs (zero()), not by per-step allocations on the main stream
+    acc0 = ops.xt_zero_counts(16, 12, ab.device)
     codes = ops.xt_rate_codes_buffer(ab.n, ab.device) if source == 'codes' else None
     rate_out = torch.empty(max((ab.n + 15) // 16 * 16, 16), dtype=torch.float64, device=ab.device)
 
@@ -147,9 +150,12 @@ def xt_step(ab, dist, source: str = 'cells', cells=None, shared: bool = True):
         if source == 'none':  # --ab diagnostic only: the VAEP kernels without the xT part
             return
         if source == 'cells':
-            state['acc'] = ops.xt_count_cells(cells, ab.n, 16, 12, shared=shared)
+            state['acc'] = ops.xt_count_cells(cells, ab.n, 16, 12, acc=acc0, shared=shared)
         else:
-            state['acc'] = ops.xt_count(ab, 16, 12, codes=codes, shared=shared)
+            state['acc'] = ops.xt_count(ab, 16, 12, acc=acc0, codes=codes, shared=shared)
+
+    def zero():
+        acc0.zero_()
 
     def reduce():
         if source == 'none':
@@ -178,7 +184,7 @@ def xt_step(ab, dist, source: str = 'cells', cells=None, shared: bool = True):
         else:
             ops.xt_rate(ab, sol.mats[3].reshape(12, 16), 16, 12)
         state['sol'] = sol
-    start.count, start.reduce = count, reduce
+    start.count, start.reduce, start.zero = count, reduce, zero
     return start, finish, state
 
 
@@ -613,6 +619,13 @@ def main() -> None:
             # stream's span (count pass + all-reduce, then solve -- a host sync of the side
             # stream -- and rate); --serial: everything on the one stream
             pj = None
+            # zero the xT counts on the side stream (idle until the fork) while the first VAEP
+            # call runs; the count pass waits for it
+            zs = side if overlap else main_s
+            zs.wait_event(_record(main_s))  # after the previous step's use of the counts
+            with torch.cuda.stream(zs):
+                xt_start.zero()
+            zev = _record(zs)
             if par:
                 pf = torch.cuda.Event()
                 pf.record(main_s)
@@ -626,6 +639,7 @@ def main() -> None:
                     if cm:  # the count pass on the main stream; its all-reduce on the side
                         if ev is not None:
                             ev[nv][0].record(main_s)
+                        main_s.wait_event(zev)
                         xt_start.count()
                     fk = torch.cuda.Event()
                     fk.record(main_s)

@@ -287,18 +287,28 @@ class XTCounts:
     def C(self) -> int:
         return self.l * self.w
 
+    def zero_(self) -> 'XTCounts':
+        """Zero every count in one fill of the backing buffer (on the current stream)."""
+        self.buf.zero_()
+        return self
+
 
 def xt_zero_counts(l: int, w: int, dev, row_blocks: int = 1) -> XTCounts:
-    """Zeroed count buffers. ``row_blocks`` > 1 pads the C x C transition counts to a whole
-    number of equal row blocks (``XTCounts.trans_padded``) so they can be reduce-scattered by
-    rows across that many ranks; ``trans`` is the C*C view the count kernel fills."""
+    """Zeroed count buffers, carved from ONE allocation (one fill kernel). ``row_blocks`` > 1
+    pads the C x C transition counts to a whole number of equal row blocks
+    (``XTCounts.trans_padded``) so they can be reduce-scattered by rows across that many ranks;
+    ``trans`` is the C*C view the count kernel fills."""
     C = l * w
-    vec = torch.zeros((3, C), dtype=torch.int64, device=dev)
     rows = -(-C // row_blocks) * row_blocks
-    padded = torch.zeros(rows * C, dtype=torch.int32, device=dev)
-    acc = XTCounts(l, w, vec[0], vec[1], vec[2], padded[:C * C],
-                   torch.zeros(1, dtype=torch.int32, device=dev))
+    a = lambda b: -(-b // 256) * 256  # noqa: E731  (256-B aligned parts)
+    o_tr = a(3 * C * 8)
+    o_err = o_tr + a(rows * C * 4)
+    buf = torch.zeros(o_err + 256, dtype=torch.uint8, device=dev)
+    vec = buf[:3 * C * 8].view(torch.int64).view(3, C)
+    padded = buf[o_tr:o_tr + rows * C * 4].view(torch.int32)
+    acc = XTCounts(l, w, vec[0], vec[1], vec[2], padded[:C * C], buf[o_err:o_err + 4].view(torch.int32))
     acc.trans_padded = padded
+    acc.buf = buf
     return acc
 
 
