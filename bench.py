@@ -353,22 +353,30 @@ def rate_extra(ab, out, n, dev, reps: int = 5) -> dict:
     models = [trees.TreeEnsemble.from_xgboost_json(
         trees.synthetic_xgboost_json(len(kinds), n_trees=100, depth=3, seed=s, feature_kinds=kinds))
         for s in (1, 2)]
-    # VAEP.rate's features: the bool features as bitmaps (what the staged walk reads)
-    fbits = ops.features(ab, SPADL_DEFAULT, 3, num_tile=out.Rn, bool_bits=True)
+    # VAEP.rate's features for xgboost learners: the bool features as bitmaps and the numeric
+    # features in float32 (what the staged walk reads); the float64 numeric form beside it
+    fbits = ops.features(ab, SPADL_DEFAULT, 3, num_tile=out.Rn, bool_bits=True, num32=True)
     ps = models[0].predict_blocks(fbits)
     pc = models[1].predict_blocks(fbits)
     val = torch.empty((3, (n + 15) // 16 * 16), dtype=torch.float32, device=dev)
     ms_feat = _events_ms(lambda: ops.features(ab, SPADL_DEFAULT, 3, out=fbits), reps)
     ms_tree = _events_ms(lambda: models[0].predict_blocks(fbits, out=ps), reps)
+    f64bits = ops.features(ab, SPADL_DEFAULT, 3, num_tile=out.Rn, bool_bits=True)
+    ms_feat64 = _events_ms(lambda: ops.features(ab, SPADL_DEFAULT, 3, out=f64bits), reps)
+    ms_tree64 = _events_ms(lambda: models[0].predict_blocks(f64bits, out=ps), reps)
+    del f64bits
     ms_block = _events_ms(lambda: models[0].predict_blocks(out, out=ps), reps)
     ms_gather = _events_ms(lambda: models[0].predict_blocks(out, out=ps, method='gather'), reps)
     ms_formula = _events_ms(lambda: ops.formula(ab, ps, pc, val), reps)
     del fbits
-    return {'workload': 'VAEP.rate on device: features (bool features as bitmaps) + 2 x '
-                        'xgboost-shaped tree ensembles (100 trees, depth 3) + formula (float32 '
-                        'probabilities), cfg2 actions',
-            'method': 'staged condition walk (sa_tree_predict_staged) over the bitmaps',
+    return {'workload': 'VAEP.rate on device: features (bool features as bitmaps, numeric '
+                        'features in float32) + 2 x xgboost-shaped tree ensembles (100 trees, '
+                        'depth 3) + formula (float32 probabilities), cfg2 actions',
+            'method': 'staged condition walk (sa_tree_predict_staged) over the bitmaps and the '
+                      'float32 numeric blocks',
             'ms_features_bitmap_form': round(ms_feat, 4), 'ms_per_model': round(ms_tree, 4),
+            'ms_features_bitmap_f64_form': round(ms_feat64, 4),
+            'ms_per_model_f64_numeric': round(ms_tree64, 4),
             'ms_per_model_from_bool_block': round(ms_block, 4),
             'ms_per_model_gather_walk': round(ms_gather, 4), 'ms_formula_f32': round(ms_formula, 4),
             'ms_rate_total': round(ms_feat + 2 * ms_tree + ms_formula, 4),

@@ -152,6 +152,14 @@ int sa_vaep_features_bits(const sa_actions* a, const sa_feature_plan* plan, uint
                           int64_t bits_stride, int32_t n_bool_cols, const sa_block* f64_out,
                           const sa_block* i64_out, void* stream);
 
+/* sa_vaep_features_bits with the numeric blocks in float32 (same tiled layout, 4-B elements:
+ * f32_out holds the plan's f64 columns rounded to nearest, i32f_out its i64 columns converted):
+ * the features of the on-device VAEP.rate for xgboost learners, which compare float32 values
+ * (the DMatrix conversion), so half the numeric bytes are written and staged.  k <= 3. */
+int sa_vaep_features_bits_f32(const sa_actions* a, const sa_feature_plan* plan, uint8_t* bool_bits,
+                              int64_t bits_stride, int32_t n_bool_cols, const sa_block* f32_out,
+                              const sa_block* i32f_out, void* stream);
+
 /* goalscore alone (vaep/features.py:505-539; atomic/vaep/features.py:229-260): writes the
  * goalscore_team / _opponent / _diff columns col, col+1, col+2 of the i64 block (one wave per
  * segment).  sa_vaep_features computes the columns inside its numeric pass in windowed mode
@@ -444,6 +452,8 @@ int sa_tree_predict(const void* nodes, int32_t n_nodes, const int32_t* roots, co
  * levels of each tree; p_out[n]: the probabilities.  T = float for f32 = 1 (xgboost), else
  * double.  The bool columns come from bool_blk, or -- when bool_bits is not NULL -- from the
  * bitmaps of sa_vaep_features_bits (bool_cols index its bitmaps; bits_stride a multiple of 8).
+ * f32 bit 1 (f32 = 3): the f64 / i64 blocks hold float32 values (sa_vaep_features_bits_f32);
+ * xgboost arithmetic only (bit 0 set), and the same probabilities bit for bit.
  * sa_tree_staged_lds_bytes: the LDS a model needs (<= 160 KiB; n_cond = 1 + n_bool + n_num). */
 typedef struct sa_tree_model {
   const void* nodes;

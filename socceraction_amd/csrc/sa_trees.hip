@@ -270,7 +270,7 @@ struct CondModel {  // the model's walk
 
 // Condition bits of the TS_ROWS rows from R0 into M8 (TS_ROWS threads, s = 0 .. TS_ROWS-1; row
 // R0 + s belongs to thread s, whole waves).
-template <typename A, bool LE>
+template <typename A, bool LE, bool N32>
 __device__ __forceinline__ void stage_conditions(const CondSet<A>& P, const sa_block& Bb, const uint8_t* __restrict__ bits,
                                                  int64_t bstride, const sa_block& Bf, const sa_block& Bi, int64_t n,
                                                  int64_t R0, int s, uint8_t* __restrict__ M8) {
@@ -331,6 +331,37 @@ __device__ __forceinline__ void stage_conditions(const CondSet<A>& P, const sa_b
   // 8-B load per row and column, all in flight before use), then column q's thresholds
   // (conditions col_start[q] .. col_start[q+1]) are balloted into the wave's 64-bit words
   const int64_t j = R0 + s < n ? R0 + s : n - 1;
+  if (N32) {  // float32 numeric blocks (sa_vaep_features_bits_f32): one 4-B load per row and column
+    const int64_t tf = j / Bf.tile_rows, ti = j / Bi.tile_rows;
+    const float* pf = (const float*)Bf.data + (tf * Bf.n_cols * Bf.tile_rows + (j - tf * Bf.tile_rows));
+    const float* pi = (const float*)Bi.data + (ti * Bi.n_cols * Bi.tile_rows + (j - ti * Bi.tile_rows));
+    for (int q0 = 0; q0 < P.n_ncol; q0 += TS_B) {
+      float raw[TS_B];
+#pragma unroll
+      for (int b = 0; b < TS_B; ++b) {
+        const int32_t slot = P.num_cols[q0 + b < P.n_ncol ? q0 + b : P.n_ncol - 1];
+        const bool f = (slot >> 24) == 1;
+        raw[b] = f ? pf[(int64_t)(slot & 0xFFFFFF) * Bf.tile_rows] : pi[(int64_t)(slot & 0xFFFFFF) * Bi.tile_rows];
+      }
+#pragma unroll
+      for (int b = 0; b < TS_B; ++b) {
+        const int q = q0 + b;
+        if (q >= P.n_ncol) break;
+        const A x = (A)raw[b];
+        for (int c = P.col_start[q]; c < P.col_start[q + 1]; ++c) {
+          const A thr = P.num_thr[c];
+          const bool right = isnan(x) ? !P.num_dl[c] : !(LE ? x <= thr : x < thr);
+          const uint64_t word = __ballot(right);
+          if (lane == 0) {
+            uint32_t* dst = reinterpret_cast<uint32_t*>(M8 + (1 + P.n_bool + c) * TS_CSTRIDE + 8 * wv);
+            dst[0] = (uint32_t)word;
+            dst[1] = (uint32_t)(word >> 32);
+          }
+        }
+      }
+    }
+    return;
+  }
   const RowBases rb = row_bases(Bb, Bf, Bi, j);
   for (int q0 = 0; q0 < P.n_ncol; q0 += TS_B) {
     uint64_t raw[TS_B];
@@ -402,7 +433,7 @@ __device__ __forceinline__ A walk_conditions(const CondModel<A>& P, const uint32
 // such workgroup per CU leaves the staging too few loads in flight); both VAEP.rate learners in
 // one launch over the union of their conditions 6.8 ms vs 2 x 2.9 (the larger LDS footprint
 // halves the resident workgroups); 256- / 1024-row tiles 3.0 / 3.7 ms.
-template <bool F32, bool LE>
+template <bool F32, bool LE, bool N32 = false>
 __global__ __launch_bounds__(TS_ROWS) void tree_cond_kernel(CondSet<typename std::conditional<F32, float, double>::type> C,
                                                             CondModel<typename std::conditional<F32, float, double>::type> P,
                                                             sa_block Bb, const uint8_t* __restrict__ bits, int64_t bstride,
@@ -422,7 +453,7 @@ __global__ __launch_bounds__(TS_ROWS) void tree_cond_kernel(CondSet<typename std
     LV[k] = P.leaf[k];
   }
   const int64_t R0 = (int64_t)blockIdx.x * TS_ROWS;
-  stage_conditions<A, LE>(C, Bb, bits, bstride, Bf, Bi, n, R0, tid, M8);
+  stage_conditions<A, LE, N32>(C, Bb, bits, bstride, Bf, Bi, n, R0, tid, M8);
   __syncthreads();
   const int64_t j = R0 + tid;
   if (j >= n) return;
@@ -513,23 +544,29 @@ extern "C" int sa_tree_predict_staged(const sa_tree_model* model, const int32_t*
   if (n == 0) return SA_OK;
   const dim3 grid((unsigned)((n + TS_ROWS - 1) / TS_ROWS)), block(TS_ROWS);
   hipStream_t st = (hipStream_t)stream;
-#define SA_TS_LAUNCH(F, LEQ, A)                                                                          \
+#define SA_TS_LAUNCH(F, LEQ, A, N32)                                                                     \
   do {                                                                                                  \
     CondSet<A> C{bool_cols, num_cols, col_start, (const A*)num_thr, num_dl, n_bool, n_num > 0 ? n_ncol : 0, \
                  n_num};                                                                                \
     CondModel<A> P{(const uint32_t*)m.nodes, (const A*)m.leaf, m.roots, m.tree_depth, m.n_nodes,        \
                    m.n_trees,                m.base_margin,    m.p_out};                                \
-    hipLaunchKernelGGL((tree_cond_kernel<F, LEQ>), grid, block, (size_t)lds, st, C, P, Bb, bool_bits,     \
+    hipLaunchKernelGGL((tree_cond_kernel<F, LEQ, N32>), grid, block, (size_t)lds, st, C, P, Bb, bool_bits, \
                        bits_stride, Bf, Bi, n);                                                          \
   } while (0)
-  if (f32 && le)
-    SA_TS_LAUNCH(true, true, float);
+  const bool n32 = (f32 & 2) != 0;  // float32 numeric blocks
+  if (n32 && !(f32 & 1)) return fail(SA_EINVAL, "float32 numeric blocks need float32 (xgboost) arithmetic");
+  if (n32 && le)
+    SA_TS_LAUNCH(true, true, float, true);
+  else if (n32)
+    SA_TS_LAUNCH(true, false, float, true);
+  else if (f32 && le)
+    SA_TS_LAUNCH(true, true, float, false);
   else if (f32)
-    SA_TS_LAUNCH(true, false, float);
+    SA_TS_LAUNCH(true, false, float, false);
   else if (le)
-    SA_TS_LAUNCH(false, true, double);
+    SA_TS_LAUNCH(false, true, double, false);
   else
-    SA_TS_LAUNCH(false, false, double);
+    SA_TS_LAUNCH(false, false, double, false);
 #undef SA_TS_LAUNCH
   return check_launch("tree_cond_kernel");
 }

@@ -26,6 +26,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 
 #include "sa_common.h"
 #include "sa_internal.h"
@@ -69,6 +70,7 @@ struct FeatArgs {
   double *off, *def, *val;
   bool vec_ok;
 };
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 // Workgroups are dispatched round-robin over the 8 XCDs (XCD = blockIdx % 8).  Writing the
 // output front to back in blockIdx order leaves every XCD's concurrent stores scattered over
@@ -216,6 +218,23 @@ __device__ __forceinline__ void st_f64x2(double* __restrict__ base, int64_t col,
 __device__ __forceinline__ void st_i64x2(int64_t* __restrict__ base, int64_t col, int64_t C, int64_t R,
                                          int64_t v0, int64_t v1) {
   i64x2 v = {(long long)v0, (long long)v1};
+  SA_DGUARD(col >= 0 && col < C, col, return);
+  st16(base + col * R, v);
+}
+
+// float32 form of the numeric blocks (sa_vaep_features_bits_f32: what xgboost learners compare,
+// values rounded to nearest like xgboost's own float32 conversion): 8-B stores, 512 B per wave
+// instruction
+__device__ __forceinline__ void st_f64x2(float* __restrict__ base, int64_t col, int64_t C, int64_t R,
+                                         double v0, double v1) {
+  f32x2 v = {(float)v0, (float)v1};
+  SA_DGUARD(col >= 0 && col < C, col, return);
+  st16(base + col * R, v);
+}
+
+__device__ __forceinline__ void st_i64x2(float* __restrict__ base, int64_t col, int64_t C, int64_t R,
+                                         int64_t v0, int64_t v1) {
+  f32x2 v = {(float)v0, (float)v1};
   SA_DGUARD(col >= 0 && col < C, col, return);
   st16(base + col * R, v);
 }
@@ -488,11 +507,11 @@ struct Win {  // one game-state window of the lane's 2 actions (flipped coordina
 };
 
 // Every f64 / i64 column of window i (features.py:151-499, atomic/vaep/features.py:135-226).
-template <bool ATOMIC>
+template <bool ATOMIC, typename FT, typename IT>
 __device__ __forceinline__ void emit_window(const NumCols& C, int i, const Win& w,
                                             const double (&sx0)[2], const double (&sy0)[2],
-                                            const double (&t0)[2], double* __restrict__ fb,
-                                            int64_t* __restrict__ ib, int64_t Rf, int64_t Ri) {
+                                            const double (&t0)[2], FT* __restrict__ fb,
+                                            IT* __restrict__ ib, int64_t Rf, int64_t Ri) {
   if (C.at >= 0) st_i64x2(ib, C.at + i, C.ni, Ri, w.typ[0], w.typ[1]);
   if (C.re >= 0) st_i64x2(ib, C.re + i, C.ni, Ri, w.res[0], w.res[1]);
   if (C.bi >= 0) st_i64x2(ib, C.bi + i, C.ni, Ri, w.bp[0], w.bp[1]);
@@ -725,9 +744,9 @@ __device__ __forceinline__ uint64_t lane_range(int a, int b) {
 // goalscore_team / _opponent / _diff of the lane's rows jb, jb+1 (wave rows wb .. wb+127, rows
 // >= n write don't-care padding like the other columns).  Every lane of the wave must call it;
 // `c` = a segment cursor at or before row jb (clamped to n - 1).
-template <bool ATOMIC>
+template <bool ATOMIC, typename IT>
 __device__ __forceinline__ void goalscore_pair(const sa_actions& A, int64_t wb, int64_t jb, SegCursor c,
-                                               int64_t* __restrict__ ib, int gcol, int ni, int64_t Ri) {
+                                               IT* __restrict__ ib, int gcol, int ni, int64_t Ri) {
   const int64_t n = A.n;
   const sa_frame& F = A.frames[0];
   const int lane = threadIdx.x & (WAVE - 1);
@@ -885,8 +904,11 @@ __device__ __forceinline__ void labels_pair(const sa_actions& A, int nr, uint8_t
 // KF = 3: windowed mode with nb_prev_actions <= 3.  The pair's rows jb-2 .. jb+1 are read
 // once (16-B loads) and the windows are formed in registers (see the loop below).
 // KF = 0: any mode / any k (explicit frames, k <= 8): per-window row loads.
-template <bool ATOMIC, bool EXPLICIT, int KF, bool TAIL = false>
+template <bool ATOMIC, bool EXPLICIT, int KF, bool TAIL = false, bool N32 = false>
 __global__ __launch_bounds__(256) void num_features_kernel(FeatArgs args) {
+  // N32: the f64 and i64 blocks hold float32 values (sa_vaep_features_bits_f32)
+  using FT = typename std::conditional<N32, float, double>::type;
+  using IT = typename std::conditional<N32, float, int64_t>::type;
   const int lane = threadIdx.x & (WAVE - 1);
   const int wv = threadIdx.x / WAVE;
   const sa_actions& A = args.a;
@@ -904,8 +926,9 @@ __global__ __launch_bounds__(256) void num_features_kernel(FeatArgs args) {
     cur = wave_cursor(A, wave_base);
     seg_advance(A, cur, jl);
     if (gcol >= 0)
-      goalscore_pair<ATOMIC>(A, wave_base, wave_base + 2 * lane, cur,
-                             args.iout + tile_off(jl & ~(int64_t)1, 0, args.Ci, Ri), gcol, (int)args.Ci, Ri);
+      goalscore_pair<ATOMIC, IT>(A, wave_base, wave_base + 2 * lane, cur,
+                                 reinterpret_cast<IT*>(args.iout) + tile_off(jl & ~(int64_t)1, 0, args.Ci, Ri),
+                                 gcol, (int)args.Ci, Ri);
     if (TAIL) {  // labels + formula of the same rows (every lane of the wave present)
       labels_pair<ATOMIC>(A, args.nr, args.sc, args.co, args.gfs, wave_base + 2 * lane, cur);
       SegCursor fc = cur;
@@ -937,8 +960,8 @@ __global__ __launch_bounds__(256) void num_features_kernel(FeatArgs args) {
   for (int pr = 0; pr < NUM_PAIRS; ++pr) {
     const int64_t jb = wave_base + pr * 2 * WAVE + 2 * lane;
     if (jb >= n) break;
-    double* fb = args.fout + tile_off(jb, 0, args.Cf, Rf);  // column 0 of rows jb, jb+1
-    int64_t* ib = args.iout + tile_off(jb, 0, args.Ci, Ri);
+    FT* fb = reinterpret_cast<FT*>(args.fout) + tile_off(jb, 0, args.Cf, Rf);  // column 0 of rows jb, jb+1
+    IT* ib = reinterpret_cast<IT*>(args.iout) + tile_off(jb, 0, args.Ci, Ri);
     int64_t jr[2];
     int dd[2];
     bool away[2];
@@ -1006,7 +1029,7 @@ __global__ __launch_bounds__(256) void num_features_kernel(FeatArgs args) {
             t0[e] = wf.ts[e];
           }
         }
-        emit_window<ATOMIC>(C, i, wf, sx0, sy0, t0, fb, ib, Rf, Ri);
+        emit_window<ATOMIC, FT, IT>(C, i, wf, sx0, sy0, t0, fb, ib, Rf, Ri);
       }
     } else {
       for (int i = 0; i < K; ++i) {
@@ -1026,7 +1049,7 @@ __global__ __launch_bounds__(256) void num_features_kernel(FeatArgs args) {
             t0[e] = w.ts[e];
           }
         }
-        emit_window<ATOMIC>(C, i, w, sx0, sy0, t0, fb, ib, Rf, Ri);
+        emit_window<ATOMIC, FT, IT>(C, i, w, sx0, sy0, t0, fb, ib, Rf, Ri);
       }
     }
   }
@@ -1474,7 +1497,8 @@ struct TailArgs {  // labels + f64 formula riding in the numeric pass (sa_vaep_s
 static int launch_features(const sa_actions* a, const sa_feature_plan* plan, const sa_block* bool_out,
                            const sa_block* f64_out, const sa_block* i64_out, int32_t xt_l,
                            int32_t xt_w, uint32_t* xt_cells, void* stream, uint8_t* bits = nullptr,
-                           int64_t bits_stride = 0, int32_t n_bits = 0, const TailArgs* tail = nullptr);
+                           int64_t bits_stride = 0, int32_t n_bits = 0, const TailArgs* tail = nullptr,
+                           bool num32 = false);
 
 extern "C" int sa_vaep_features(const sa_actions* a, const sa_feature_plan* plan,
                                 const sa_block* bool_out, const sa_block* f64_out,
@@ -1504,6 +1528,20 @@ extern "C" int sa_vaep_features_bits(const sa_actions* a, const sa_feature_plan*
   if (a->n_frames != 1) return fail(SA_EINVAL, "bool bitmaps: windowed mode only");
   return launch_features(a, plan, nullptr, f64_out, i64_out, 0, 0, nullptr, stream, bool_bits, bits_stride,
                          n_bool_cols);
+}
+
+extern "C" int sa_vaep_features_bits_f32(const sa_actions* a, const sa_feature_plan* plan, uint8_t* bool_bits,
+                                         int64_t bits_stride, int32_t n_bool_cols, const sa_block* f32_out,
+                                         const sa_block* i32f_out, void* stream) {
+  if (!a) return fail(SA_EINVAL, "null sa_actions");
+  if (!bool_bits || n_bool_cols < 1 || bits_stride < 2 * ((a->n + 15) / 16) || bits_stride % 2 ||
+      ((uintptr_t)bool_bits & 1u))
+    return fail(SA_EINVAL, "bool bitmaps: even stride of at least ceil(n/16)*2 bytes, 2-byte aligned");
+  if (a->n_frames != 1) return fail(SA_EINVAL, "bool bitmaps: windowed mode only");
+  if (!plan || plan->nb_prev_actions > 3)
+    return fail(SA_EINVAL, "float32 numeric blocks: nb_prev_actions <= 3 (use sa_vaep_features_bits)");
+  return launch_features(a, plan, nullptr, f32_out, i32f_out, 0, 0, nullptr, stream, bool_bits, bits_stride,
+                         n_bool_cols, nullptr, true);
 }
 
 extern "C" int sa_vaep_step_f64(const sa_actions* a, const sa_feature_plan* plan, const sa_block* bool_out,
@@ -1541,7 +1579,7 @@ extern "C" int sa_vaep_step_f64(const sa_actions* a, const sa_feature_plan* plan
 static int launch_features(const sa_actions* a, const sa_feature_plan* plan, const sa_block* bool_out,
                            const sa_block* f64_out, const sa_block* i64_out, int32_t xt_l,
                            int32_t xt_w, uint32_t* xt_cells, void* stream, uint8_t* bits,
-                           int64_t bits_stride, int32_t n_bits, const TailArgs* tail) {
+                           int64_t bits_stride, int32_t n_bits, const TailArgs* tail, bool num32) {
   int rc = check_actions(a, true);
   if (rc) return rc;
   if (!plan) return fail(SA_EINVAL, "null plan");
@@ -1634,7 +1672,12 @@ static int launch_features(const sa_actions* a, const sa_feature_plan* plan, con
   const int gc = plan->i64_col[SA_XFN_GOALSCORE];
   if (wn || xt_cells || tail || (gc >= 0 && !expl)) {  // windowed mode: goalscore fused into this pass
     const bool fast = !expl && K <= 3;  // register-resident windows (KF = 3)
-    if (tail) {  // windowed, K <= 3 (checked by sa_vaep_step_f64)
+    if (num32) {  // windowed, K <= 3 (checked by sa_vaep_features_bits_f32)
+      if (a->atomic)
+        hipLaunchKernelGGL((num_features_kernel<true, false, 3, false, true>), grid, block, 0, st, args);
+      else
+        hipLaunchKernelGGL((num_features_kernel<false, false, 3, false, true>), grid, block, 0, st, args);
+    } else if (tail) {  // windowed, K <= 3 (checked by sa_vaep_step_f64)
       if (a->atomic)
         hipLaunchKernelGGL((num_features_kernel<true, false, 3, true>), grid, block, 0, st, args);
       else

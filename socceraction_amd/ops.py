@@ -42,6 +42,12 @@ class FeatureBlocks:
     bool_bits: Optional[torch.Tensor] = None
 
     @property
+    def num32(self) -> bool:
+        """True when the f64 / i64 blocks hold float32 values (features(..., num32=True): the
+        on-device VAEP.rate of xgboost learners, which compare float32 values)."""
+        return self.f64_block.dtype == torch.float32
+
+    @property
     def device(self):
         return self.f64_block.device
 
@@ -146,24 +152,31 @@ def features_into(s: _native.SaActions, out: FeatureBlocks, xt_cells: Optional[t
 
 def features(batch: ActionBatch, xfns: Sequence[str], k: int, flip: bool = True,
              out: Optional[FeatureBlocks] = None, bool_tile: Optional[int] = None,
-             num_tile: Optional[int] = None, bool_bits: bool = False) -> FeatureBlocks:
+             num_tile: Optional[int] = None, bool_bits: bool = False,
+             num32: bool = False) -> FeatureBlocks:
     """Game-state features of every segment of ``batch`` (windowed mode). ``bool_bits``: the
     bool features as bitmaps (``sa_vaep_features_bits``; 64 instead of 515 B/action written:
-    what the staged tree walk of the on-device ``VAEP.rate`` reads)."""
+    what the staged tree walk of the on-device ``VAEP.rate`` reads). ``num32`` (with
+    ``bool_bits``, k <= 3): the numeric blocks in float32 (``sa_vaep_features_bits_f32``: what
+    xgboost learners compare; half the numeric bytes written and staged)."""
     plan = out.plan if out is not None else build_plan(xfns, k, batch.atomic)
+    if num32 and not bool_bits and out is None:
+        raise ValueError('float32 numeric blocks come with the bitmap form (bool_bits=True)')
     if bool_bits and out is None:
         words = max(1, (batch.n + 63) // 64)
         Rn = _ld(batch.n) if num_tile is None else int(num_tile)
         tn = max(1, -(-batch.n // Rn))
+        fdt, idt = (torch.float32, torch.float32) if num32 else (torch.float64, torch.int64)
         out = FeatureBlocks(plan, batch.n, 1024, Rn, None,
-                            torch.empty((tn, plan.n_f64, Rn), dtype=torch.float64, device=batch.device),
-                            torch.empty((tn, plan.n_i64, Rn), dtype=torch.int64, device=batch.device),
+                            torch.empty((tn, plan.n_f64, Rn), dtype=fdt, device=batch.device),
+                            torch.empty((tn, plan.n_i64, Rn), dtype=idt, device=batch.device),
                             torch.empty((max(plan.n_bool, 1), words), dtype=torch.int64,
                                         device=batch.device))
     out = out or alloc_feature_blocks(plan, batch.n, batch.device, bool_tile, num_tile)
     if out.bool_bits is not None and out.bool_block is None:
         _, fb, ib = out.sa_blocks()
-        _native.check(_native.lib().sa_vaep_features_bits(
+        fn = _native.lib().sa_vaep_features_bits_f32 if out.num32 else _native.lib().sa_vaep_features_bits
+        _native.check(fn(
             ctypes.byref(batch.struct(flip=flip)), ctypes.byref(out.plan.struct),
             out.bool_bits.data_ptr(), out.bool_bits.shape[1] * 8, max(plan.n_bool, 1),
             ctypes.byref(fb), ctypes.byref(ib), stream_handle()))

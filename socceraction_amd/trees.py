@@ -280,6 +280,9 @@ class TreeEnsemble:
         if out is None:
             out = torch.empty(max(n, 1), dtype=dt, device=dev)
         bb, fb, ib = blocks.sa_blocks()
+        n32 = getattr(blocks, 'num32', False)
+        if n32 and (not self.f32 or method == 'gather'):
+            raise ValueError('float32 feature blocks feed the staged walk of xgboost learners only')
         if method != 'gather' and self.n_trees:
             key = ('staged', slots_np.tobytes())
             st = d.get(key)
@@ -312,9 +315,10 @@ class TreeEnsemble:
                     ptr('num_thr'), ptr('num_dl'), st['n_num'], ctypes.byref(bb),
                     bits.data_ptr() if bits is not None else None,
                     bits.shape[1] * 8 if bits is not None else 0, ctypes.byref(fb),
-                    ctypes.byref(ib), n, int(self.le), int(self.f32), stream_handle()))
+                    ctypes.byref(ib), n, int(self.le), int(self.f32) | (2 if n32 else 0),
+                    stream_handle()))
                 return out[:n]
-            elif method == 'staged':
+            elif method == 'staged' or n32:
                 raise ValueError('the staged form of this model does not fit LDS')
         if bits is not None:  # the gather walk reads bool values from a bool block
             blocks._blk('b')

@@ -277,10 +277,21 @@ class VAEP:
         xgboost, float64 for scikit-learn), as in the reference's host path."""
         import torch
         known, _ = self._split_xfns()
-        # the learners read the bool features as bitmaps (64 instead of 515 B/action written)
-        fb = ops.features(ab, known, self.nb_prev_actions, bool_bits=True)
-        ps = trees['scores'].predict_blocks(fb)
-        pc = trees['concedes'].predict_blocks(fb)
+        # the learners read the bool features as bitmaps (64 instead of 515 B/action written);
+        # xgboost learners compare float32 values, so their numeric features are written and
+        # staged in float32 (half the bytes, the same probabilities bit for bit)
+        n32 = self.nb_prev_actions <= 3 and all(t.f32 for t in trees.values())
+        fb = ops.features(ab, known, self.nb_prev_actions, bool_bits=True, num32=n32)
+        try:
+            ps = trees['scores'].predict_blocks(fb)
+            pc = trees['concedes'].predict_blocks(fb)
+        except ValueError:
+            if not n32:
+                raise
+            # a learner whose staged form does not fit LDS: the gather walk reads float64 blocks
+            fb = ops.features(ab, known, self.nb_prev_actions, bool_bits=True)
+            ps = trees['scores'].predict_blocks(fb)
+            pc = trees['concedes'].predict_blocks(fb)
         if ps.dtype != pc.dtype:  # pandas would upcast the mixed pair
             ps, pc = ps.to(torch.float64), pc.to(torch.float64)
         v = ops.formula(ab, ps, pc).cpu().numpy()[:, :ab.n]

@@ -238,3 +238,39 @@ def test_bool_bitmap_features_and_trees(sa, atomic):
         np.testing.assert_array_equal(a, te.predict_blocks(ref, method='gather').cpu().numpy())
         np.testing.assert_array_equal(te.predict_blocks(got, method='gather').cpu().numpy(), a)
     pd.testing.assert_frame_equal(got.to_frame(), ref.to_frame())
+
+
+@pytest.mark.parametrize('atomic', [False, True])
+def test_float32_numeric_blocks_and_trees(sa, atomic):
+    """sa_vaep_features_bits_f32: the numeric blocks in float32 equal the float64 / int64 blocks
+    rounded to nearest (torch's cast), the bitmaps are unchanged, and the staged walk of an
+    xgboost learner over them gives the probabilities of the float64 form bit for bit (xgboost
+    compares float32 values); scikit-learn learners and the gather walk refuse them."""
+    from socceraction_amd import synthetic
+    from oracle import vaep_oracle as vo
+    B, ops, trees = sa['batch'], sa['ops'], sa['trees']
+    if atomic:
+        d = synthetic.atomic_games(150, seed=7)
+        xfns = ['actiontype', 'actiontype_onehot', 'bodypart', 'bodypart_onehot', 'time', 'team',
+                'time_delta', 'location', 'polar', 'movement_polar', 'direction', 'goalscore']
+    else:
+        d = synthetic.spadl_games(150, seed=7)
+        xfns = vo.SPADL_DEFAULT
+    ab = B.ActionBatch.from_columns(d, atomic=atomic)
+    ref = ops.features(ab, xfns, 3, num_tile=128, bool_bits=True)
+    got = ops.features(ab, xfns, 3, num_tile=128, bool_bits=True, num32=True)
+    assert got.num32 and not ref.num32
+    assert torch.equal(got.bool_bits, ref.bool_bits)
+    for k in 'fi':
+        assert torch.equal(got.block(k), ref.block(k).to(torch.float32)), k
+    kinds = [k for _, k, _ in ref.plan.order]
+    for seed in (31, 32):
+        xg = trees.TreeEnsemble.from_model(trees.synthetic_xgboost_json(
+            len(kinds), n_trees=80, depth=3, seed=seed, feature_kinds=kinds))
+        assert torch.equal(xg.predict_blocks(got), xg.predict_blocks(ref))
+        with pytest.raises(ValueError):
+            xg.predict_blocks(got, method='gather')
+    with pytest.raises(ValueError):
+        ops.features(ab, xfns, 3, num32=True)
+    with pytest.raises(ValueError):
+        ops.features(ab, xfns, 4, bool_bits=True, num32=True)
