@@ -473,21 +473,6 @@ int sa_tree_predict_staged(const sa_tree_model* model, const int32_t* bool_cols,
                            const sa_block* f64_blk, const sa_block* i64_blk, int64_t n, int32_t le,
                            int32_t f32, void* stream);
 
-/* Oblivious form of sa_tree_predict_staged for models whose trees are at most 3 split levels
- * deep (the reference's default XGBClassifier(max_depth=3), vaep/base.py:226-231): each tree
- * padded to a full depth-3 tree -- tree_conds[t][0..6] the conditions of its 7 split slots in
- * heap order (slot h's children are 2h+1 on a clear bit, 2h+2 on a set bit; a leaf above depth 3
- * becomes condition-0 slots whose leaves repeat it), tree_conds[t][7] = 0; tree_leaf[t][0..7]
- * (T) its 8 leaf values in heap order.  The conditions are those of sa_tree_predict_staged
- * (same arguments); the probabilities are the same bit for bit.  tree_conds 16-byte aligned. */
-int sa_tree_predict_oblivious(const uint16_t* tree_conds, const void* tree_leaf, int32_t n_trees,
-                              double base_margin, void* p_out, const int32_t* bool_cols, int32_t n_bool,
-                              const int32_t* num_cols, const int32_t* col_start, int32_t n_ncol,
-                              const void* num_thr, const int32_t* num_dl, int32_t n_num,
-                              const sa_block* bool_blk, const uint8_t* bool_bits, int64_t bits_stride,
-                              const sa_block* f64_blk, const sa_block* i64_blk, int64_t n, int32_t le,
-                              int32_t f32, void* stream);
-
 /* ---- runtime ------------------------------------------------------------------ */
 int sa_abi_version(void);
 const char* sa_last_error(void);

@@ -41,7 +41,6 @@ def main():
     ab = B.ActionBatch.from_columns(synthetic.spadl_games(args.games))
     fb = ops.features(ab, SPADL_DEFAULT, 3, bool_tile=1024, num_tile=128)
     fbits = ops.features(ab, SPADL_DEFAULT, 3, num_tile=128, bool_bits=True)
-    fbits32 = ops.features(ab, SPADL_DEFAULT, 3, num_tile=128, bool_bits=True, num32=True)
     out_feat = {'features_block_ms': _ms(lambda: ops.features(ab, SPADL_DEFAULT, 3, out=fb)),
                 'features_bitmaps_ms': _ms(lambda: ops.features(ab, SPADL_DEFAULT, 3, out=fbits))}
     kinds = [k for _, k, _ in fb.plan.order]
@@ -57,11 +56,8 @@ def main():
             _native._lib = _native.load_library(os.path.join(
                 ROOT, 'socceraction_amd', '_lib', f'libsocceraction_amd_{name}.so'))
         te._dev = None
-        res = {'oblivious_from_bitmaps_f32': _ms(lambda: te.predict_blocks(fbits32, method='oblivious')),
-               'oblivious_from_bitmaps': _ms(lambda: te.predict_blocks(fbits, method='oblivious')),
-               'staged': _ms(lambda: te.predict_blocks(fb, method='staged')),
-               'staged_from_bitmaps': _ms(lambda: te.predict_blocks(fbits, method='staged')),
-               'staged_from_bitmaps_f32': _ms(lambda: te.predict_blocks(fbits32, method='staged'))}
+        res = {'staged': _ms(lambda: te.predict_blocks(fb, method='staged')),
+               'staged_from_bitmaps': _ms(lambda: te.predict_blocks(fbits, method='staged'))}
         if name == 'default':
             res['gather'] = _ms(lambda: te.predict_blocks(fb, method='gather'))
         out[name] = res

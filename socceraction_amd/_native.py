@@ -164,12 +164,6 @@ _SIGNATURES = {
                                        ctypes.POINTER(SaBlock), ctypes.c_int64, ctypes.c_double,
                                        ctypes.c_int32, ctypes.c_int32, _p, _p]),
     'sa_tree_staged_lds_bytes': (ctypes.c_int64, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]),
-    'sa_tree_predict_oblivious': (ctypes.c_int, [_p, _p, ctypes.c_int32, ctypes.c_double, _p, _p,
-                                                 ctypes.c_int32, _p, _p, ctypes.c_int32, _p, _p,
-                                                 ctypes.c_int32, ctypes.POINTER(SaBlock), _p,
-                                                 ctypes.c_int64, ctypes.POINTER(SaBlock),
-                                                 ctypes.POINTER(SaBlock), ctypes.c_int64,
-                                                 ctypes.c_int32, ctypes.c_int32, _p]),
     'sa_tree_predict_staged': (ctypes.c_int, [ctypes.POINTER(SaTreeModel), _p, ctypes.c_int32, _p, _p,
                                               ctypes.c_int32, _p, _p, ctypes.c_int32,
                                               ctypes.POINTER(SaBlock), _p, ctypes.c_int64,

@@ -245,13 +245,6 @@ constexpr int TS_ROWS = 512;               // rows per tile
 constexpr int TS_PIECES = TS_ROWS / 16;    // 16-row pieces per condition
 constexpr int TS_CSTRIDE = TS_ROWS / 8 + 4;  // bytes per condition (+4: conditions start in different banks)
 constexpr int TS_B = 8;                    // loads in flight per staging thread
-#ifndef SA_TREE_NB32
-#define SA_TREE_NB32 8  // float32 numeric columns in flight per staging thread (A/B knob)
-#endif
-constexpr int TS_B32 = SA_TREE_NB32;
-#ifndef SA_PROBE_TS
-#define SA_PROBE_TS 0  // probe builds only (wrong results): 1 = staging only, 2 = walk only
-#endif
 
 template <typename A>
 struct CondSet {  // the model's conditions
@@ -277,12 +270,12 @@ struct CondModel {  // the model's walk
 
 // Condition bits of the TS_ROWS rows from R0 into M8 (TS_ROWS threads, s = 0 .. TS_ROWS-1; row
 // R0 + s belongs to thread s, whole waves).
-template <typename A, bool LE, bool N32, int CS = TS_CSTRIDE>
+template <typename A, bool LE, bool N32>
 __device__ __forceinline__ void stage_conditions(const CondSet<A>& P, const sa_block& Bb, const uint8_t* __restrict__ bits,
                                                  int64_t bstride, const sa_block& Bf, const sa_block& Bi, int64_t n,
                                                  int64_t R0, int s, uint8_t* __restrict__ M8) {
   const int wv = s >> 6, lane = s & 63;
-  if (s < CS / 4) reinterpret_cast<uint32_t*>(M8)[s] = 0;  // condition 0: never set
+  if (s < TS_CSTRIDE / 4) reinterpret_cast<uint32_t*>(M8)[s] = 0;  // condition 0: never set
   if (bits) {
     // bool conditions from bitmaps: item it = (column u, 64-row word q): one 8-B load
     constexpr int WQ = TS_ROWS / 64;
@@ -300,7 +293,7 @@ __device__ __forceinline__ void stage_conditions(const CondSet<A>& P, const sa_b
       for (int b = 0; b < TS_B; ++b) {
         const int it = i0 + b * TS_ROWS + s;
         if (it < nwi) {
-          uint32_t* dst = reinterpret_cast<uint32_t*>(M8 + (1 + it / WQ) * CS + 8 * (it % WQ));
+          uint32_t* dst = reinterpret_cast<uint32_t*>(M8 + (1 + it / WQ) * TS_CSTRIDE + 8 * (it % WQ));
           dst[0] = (uint32_t)w[b];
           dst[1] = (uint32_t)(w[b] >> 32);
         }
@@ -331,7 +324,7 @@ __device__ __forceinline__ void stage_conditions(const CondSet<A>& P, const sa_b
 #pragma unroll
       for (int q = 0; q < 4; ++q) bits |= (((w[b][q] & 0x01010101u) * 0x01020408u) >> 24) << (4 * q);
       if (it < nbi)
-        *reinterpret_cast<uint16_t*>(M8 + (1 + it / TS_PIECES) * CS + 2 * (it % TS_PIECES)) = (uint16_t)bits;
+        *reinterpret_cast<uint16_t*>(M8 + (1 + it / TS_PIECES) * TS_CSTRIDE + 2 * (it % TS_PIECES)) = (uint16_t)bits;
     }
   }
   // numeric conditions: the distinct numeric columns num_cols[q] are read TS_B at a time (one
@@ -342,16 +335,16 @@ __device__ __forceinline__ void stage_conditions(const CondSet<A>& P, const sa_b
     const int64_t tf = j / Bf.tile_rows, ti = j / Bi.tile_rows;
     const float* pf = (const float*)Bf.data + (tf * Bf.n_cols * Bf.tile_rows + (j - tf * Bf.tile_rows));
     const float* pi = (const float*)Bi.data + (ti * Bi.n_cols * Bi.tile_rows + (j - ti * Bi.tile_rows));
-    for (int q0 = 0; q0 < P.n_ncol; q0 += TS_B32) {
-      float raw[TS_B32];
+    for (int q0 = 0; q0 < P.n_ncol; q0 += TS_B) {
+      float raw[TS_B];
 #pragma unroll
-      for (int b = 0; b < TS_B32; ++b) {
+      for (int b = 0; b < TS_B; ++b) {
         const int32_t slot = P.num_cols[q0 + b < P.n_ncol ? q0 + b : P.n_ncol - 1];
         const bool f = (slot >> 24) == 1;
         raw[b] = f ? pf[(int64_t)(slot & 0xFFFFFF) * Bf.tile_rows] : pi[(int64_t)(slot & 0xFFFFFF) * Bi.tile_rows];
       }
 #pragma unroll
-      for (int b = 0; b < TS_B32; ++b) {
+      for (int b = 0; b < TS_B; ++b) {
         const int q = q0 + b;
         if (q >= P.n_ncol) break;
         const A x = (A)raw[b];
@@ -360,7 +353,7 @@ __device__ __forceinline__ void stage_conditions(const CondSet<A>& P, const sa_b
           const bool right = isnan(x) ? !P.num_dl[c] : !(LE ? x <= thr : x < thr);
           const uint64_t word = __ballot(right);
           if (lane == 0) {
-            uint32_t* dst = reinterpret_cast<uint32_t*>(M8 + (1 + P.n_bool + c) * CS + 8 * wv);
+            uint32_t* dst = reinterpret_cast<uint32_t*>(M8 + (1 + P.n_bool + c) * TS_CSTRIDE + 8 * wv);
             dst[0] = (uint32_t)word;
             dst[1] = (uint32_t)(word >> 32);
           }
@@ -389,7 +382,7 @@ __device__ __forceinline__ void stage_conditions(const CondSet<A>& P, const sa_b
         const bool right = isnan(x) ? !P.num_dl[c] : !(LE ? x <= thr : x < thr);
         const uint64_t word = __ballot(right);
         if (lane == 0) {
-          uint32_t* dst = reinterpret_cast<uint32_t*>(M8 + (1 + P.n_bool + c) * CS + 8 * wv);
+          uint32_t* dst = reinterpret_cast<uint32_t*>(M8 + (1 + P.n_bool + c) * TS_CSTRIDE + 8 * wv);
           dst[0] = (uint32_t)word;
           dst[1] = (uint32_t)(word >> 32);
         }
@@ -460,119 +453,20 @@ __global__ __launch_bounds__(TS_ROWS) void tree_cond_kernel(CondSet<typename std
     LV[k] = P.leaf[k];
   }
   const int64_t R0 = (int64_t)blockIdx.x * TS_ROWS;
-  if (SA_PROBE_TS != 2) stage_conditions<A, LE, N32>(C, Bb, bits, bstride, Bf, Bi, n, R0, tid, M8);
+  stage_conditions<A, LE, N32>(C, Bb, bits, bstride, Bf, Bi, n, R0, tid, M8);
   __syncthreads();
   const int64_t j = R0 + tid;
   if (j >= n) return;
-  const A m = SA_PROBE_TS == 1 ? (A)M8[tid] : walk_conditions<A>(P, N, LV, M8, tid);
+  const A m = walk_conditions<A>(P, N, LV, M8, tid);
   if (F32)
     ((float*)P.out)[j] = 1.0f / (1.0f + expf(-(float)m));
   else
     ((double*)P.out)[j] = 1.0 / (1.0 + exp(-(double)m));
 }
 
-// Oblivious form (every tree at most 3 split levels deep, the reference's default
-// XGBClassifier(max_depth=3), vaep/base.py:226-231): each tree padded to a full depth-3 tree
-// host-side -- 7 condition slots in heap order (a leaf above depth 3 becomes condition-0 slots
-// whose leaves repeat it) and 8 leaf values -- so a WAVE reads the same 7 conditions for all of
-// its rows: 7 broadcast LDS reads of the wave's 64-bit word per condition (one address per
-// wave: no bank conflicts) and a leaf index of 3 selects, instead of 3 levels of per-row node
-// and bit gathers.  Conditions are staged as in tree_cond_kernel with 64-B condition slots
-// (64 B per 512 rows: the wave's word at 8 * wave); the tree table is read with scalar loads.
-// Leaf values are summed in tree order: the staged walk's probabilities bit for bit.
-template <bool F32, bool LE, bool N32>
-__global__ __launch_bounds__(TS_ROWS) void tree_obl_kernel(CondSet<typename std::conditional<F32, float, double>::type> C,
-                                                           const uint4* __restrict__ tconds,
-                                                           const typename std::conditional<F32, float, double>::type* __restrict__ tleaf,
-                                                           int n_trees, double base, void* __restrict__ out, sa_block Bb,
-                                                           const uint8_t* __restrict__ bits, int64_t bstride, sa_block Bf,
-                                                           sa_block Bi, int64_t n) {
-  using A = typename std::conditional<F32, float, double>::type;
-  extern __shared__ __attribute__((aligned(16))) unsigned char ts_lds[];
-  uint8_t* M8 = ts_lds;
-  const int tid = threadIdx.x;
-  const int64_t R0 = (int64_t)blockIdx.x * TS_ROWS;
-  if (SA_PROBE_TS != 2) stage_conditions<A, LE, N32, 64>(C, Bb, bits, bstride, Bf, Bi, n, R0, tid, M8);
-  __syncthreads();
-  const int lane = tid & 63;
-  const uint64_t* Mw = reinterpret_cast<const uint64_t*>(M8) + (tid >> 6);  // condition c: Mw[8 * c]
-  A m = (A)base;
-  if (SA_PROBE_TS != 1) {
-#pragma unroll 4
-    for (int t = 0; t < n_trees; ++t) {
-      const uint4 q = tconds[t];  // 8 u16 condition slots (7 used), uniform
-      const uint32_t b0 = (uint32_t)(Mw[8 * (q.x & 0xFFFFu)] >> lane) & 1u;
-      const uint32_t l1 = (uint32_t)(Mw[8 * (q.x >> 16)] >> lane) & 1u;
-      const uint32_t r1 = (uint32_t)(Mw[8 * (q.y & 0xFFFFu)] >> lane) & 1u;
-      const uint32_t c0 = (uint32_t)(Mw[8 * (q.y >> 16)] >> lane) & 1u;
-      const uint32_t c1 = (uint32_t)(Mw[8 * (q.z & 0xFFFFu)] >> lane) & 1u;
-      const uint32_t c2 = (uint32_t)(Mw[8 * (q.z >> 16)] >> lane) & 1u;
-      const uint32_t c3 = (uint32_t)(Mw[8 * (q.w & 0xFFFFu)] >> lane) & 1u;
-      const uint32_t b1 = b0 ? r1 : l1;
-      const uint32_t b2 = b0 ? (b1 ? c3 : c2) : (b1 ? c1 : c0);
-      m = m + tleaf[8 * t + 4 * b0 + 2 * b1 + b2];
-    }
-  } else {
-    m = (A)M8[tid];
-  }
-  const int64_t j = R0 + tid;
-  if (j >= n) return;
-  if (F32)
-    ((float*)out)[j] = 1.0f / (1.0f + expf(-(float)m));
-  else
-    ((double*)out)[j] = 1.0 / (1.0 + exp(-(double)m));
-}
-
 }  // namespace sa
 
 using namespace sa;
-
-extern "C" int sa_tree_predict_oblivious(const uint16_t* tree_conds, const void* tree_leaf, int32_t n_trees,
-                                         double base_margin, void* p_out, const int32_t* bool_cols, int32_t n_bool,
-                                         const int32_t* num_cols, const int32_t* col_start, int32_t n_ncol,
-                                         const void* num_thr, const int32_t* num_dl, int32_t n_num,
-                                         const sa_block* bool_blk, const uint8_t* bool_bits, int64_t bits_stride,
-                                         const sa_block* f64_blk, const sa_block* i64_blk, int64_t n, int32_t le,
-                                         int32_t f32, void* stream) {
-  if (!tree_conds || !tree_leaf || !p_out || n < 0 || n_trees < 1 || 1 + n_bool + n_num > 65536 || n_bool < 0 ||
-      n_num < 0 || (n_bool > 0 && (!bool_cols || (!bool_blk && !bool_bits))) || n_ncol < 0 ||
-      ((uintptr_t)tree_conds & 15u) ||
-      (bool_bits && (bits_stride % 8 || bits_stride < 8 * ((n + 63) / 64) || ((uintptr_t)bool_bits & 7u))) ||
-      (n_num > 0 && (n_ncol < 1 || !num_cols || !col_start || !num_thr || !num_dl)))
-    return fail(SA_EINVAL, "bad oblivious tree arguments");
-  const int64_t lds = (int64_t)(1 + n_bool + n_num) * 64;
-  if (lds > 160 * 1024) return fail(SA_EINVAL, "oblivious tree model needs %lld B of LDS", (long long)lds);
-  sa_block z{nullptr, 0, 0, 16};
-  const sa_block Bb = bool_blk ? *bool_blk : z, Bf = f64_blk ? *f64_blk : z, Bi = i64_blk ? *i64_blk : z;
-  if (n_bool > 0 && !bool_bits && (Bb.tile_rows % 16 != 0 || !aligned16(Bb.data)))
-    return fail(SA_EINVAL, "bool block: 16-row tiles, 16-byte aligned");
-  const bool n32 = (f32 & 2) != 0;
-  if (n32 && !(f32 & 1)) return fail(SA_EINVAL, "float32 numeric blocks need float32 (xgboost) arithmetic");
-  if (n == 0) return SA_OK;
-  const dim3 grid((unsigned)((n + TS_ROWS - 1) / TS_ROWS)), block(TS_ROWS);
-  hipStream_t st = (hipStream_t)stream;
-#define SA_OBL_LAUNCH(F, LEQ, A, N32)                                                                      \
-  do {                                                                                                    \
-    CondSet<A> C{bool_cols, num_cols, col_start, (const A*)num_thr, num_dl, n_bool, n_num > 0 ? n_ncol : 0,   \
-                 n_num};                                                                                  \
-    hipLaunchKernelGGL((tree_obl_kernel<F, LEQ, N32>), grid, block, (size_t)lds, st, C, (const uint4*)tree_conds, \
-                       (const A*)tree_leaf, n_trees, base_margin, p_out, Bb, bool_bits, bits_stride, Bf, Bi, n); \
-  } while (0)
-  if (n32 && le)
-    SA_OBL_LAUNCH(true, true, float, true);
-  else if (n32)
-    SA_OBL_LAUNCH(true, false, float, true);
-  else if (f32 && le)
-    SA_OBL_LAUNCH(true, true, float, false);
-  else if (f32)
-    SA_OBL_LAUNCH(true, false, float, false);
-  else if (le)
-    SA_OBL_LAUNCH(false, true, double, false);
-  else
-    SA_OBL_LAUNCH(false, false, double, false);
-#undef SA_OBL_LAUNCH
-  return check_launch("tree_obl_kernel");
-}
 
 extern "C" int sa_tree_predict(const void* nodes, int32_t n_nodes, const int32_t* roots, const int32_t* tree_depth,
                                int32_t n_trees, const int32_t* feature_slots, int32_t n_features,

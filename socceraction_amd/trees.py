@@ -265,10 +265,9 @@ class TreeEnsemble:
                        method: Optional[str] = None) -> torch.Tensor:
         """P(class 1) of every row of the device feature blocks (``ops.FeatureBlocks``):
         float32 for xgboost models (as their ``predict_proba``), float64 for scikit-learn.
-        ``method``: 'oblivious' (sa_tree_predict_oblivious: trees at most 3 split levels deep,
-        the default when they are), 'staged' (the staged condition walk,
-        sa_tree_predict_staged; the default otherwise whenever the model fits LDS) or 'gather'
-        (sa_tree_predict). ``staged`` True / False is the older spelling of staged / gather."""
+        ``method``: 'staged' (the staged condition walk, sa_tree_predict_staged; the default
+        whenever the model fits LDS) or 'gather' (sa_tree_predict). ``staged`` True / False is
+        the older spelling of the two."""
         from .batch import stream_handle
         if method is None and staged is not None:
             method = 'staged' if staged else 'gather'
@@ -302,25 +301,7 @@ class TreeEnsemble:
                 st = {k: t(v) for k, v in lay.items()} if fits else False
                 if st:
                     st['n_num'] = len(lay['num_slots'])
-                    obl = oblivious_form(lay)
-                    st['obl'] = None if obl is None else (
-                        torch.from_numpy(obl[0].view(np.int16)).to(dev), torch.from_numpy(obl[1]).to(dev))
                 d[key] = st
-            if st and st['obl'] is not None and method in (None, 'oblivious'):
-                def ptr(k):
-                    return st[k].data_ptr() if st[k] is not None else None
-                oc, ol = st['obl']
-                _native.check(_native.lib().sa_tree_predict_oblivious(
-                    oc.data_ptr(), ol.data_ptr(), self.n_trees, float(self.base_margin), out.data_ptr(),
-                    ptr('bool_cols'), 0 if st['bool_cols'] is None else st['bool_cols'].numel(),
-                    ptr('num_cols'), ptr('col_start'), 0 if st['num_cols'] is None else st['num_cols'].numel(),
-                    ptr('num_thr'), ptr('num_dl'), st['n_num'], ctypes.byref(bb),
-                    bits.data_ptr() if bits is not None else None,
-                    bits.shape[1] * 8 if bits is not None else 0, ctypes.byref(fb), ctypes.byref(ib), n,
-                    int(self.le), int(self.f32) | (2 if n32 else 0), stream_handle()))
-                return out[:n]
-            if method == 'oblivious':
-                raise ValueError('the oblivious form needs trees at most 3 split levels deep')
             if st:
                 def ptr(k):
                     return st[k].data_ptr() if st[k] is not None else None
@@ -351,34 +332,6 @@ class TreeEnsemble:
             n, float(self.base_margin), int(self.le), int(self.f32), out.data_ptr(),
             stream_handle()))
         return out[:n]
-
-
-def oblivious_form(st: dict, depth: int = 3):
-    """The staged nodes of a model (``staged_nodes``) as full depth-3 trees for
-    sa_tree_predict_oblivious: per tree the conditions of its 7 split slots in heap order (slot
-    h's children 2h+1 on a clear bit, 2h+2 on a set bit; a leaf above depth 3 repeats itself as
-    condition-0 slots) and its 8 leaf values; None when a tree is deeper."""
-    cn, leaf, roots = st['nodes'], st['leaf'], st['roots']
-    n_int = 2 ** depth - 1
-    conds = np.zeros((len(roots), 8), np.uint16)
-    leaves = np.zeros((len(roots), 2 ** depth), leaf.dtype)
-    for t, r in enumerate(roots):
-        stack = [(int(r), 0)]  # (node, heap slot)
-        while stack:
-            k, h = stack.pop()
-            c, first = int(cn[k] & 0xFFFF), int(cn[k] >> 16)
-            is_leaf = c == 0 and first == k
-            if h >= n_int:
-                if not is_leaf:
-                    return None
-                leaves[t, h - n_int] = leaf[k]
-                continue
-            conds[t, h] = c
-            if is_leaf:
-                stack += [(k, 2 * h + 1), (k, 2 * h + 2)]
-            else:
-                stack += [(first, 2 * h + 1), (first + 1, 2 * h + 2)]
-    return conds, leaves
 
 
 def staged_layout(models: Sequence[TreeEnsemble], slots: Sequence[np.ndarray]) -> dict:

@@ -579,58 +579,3 @@ def test_staged_layout_restates_the_walk(depth):
     got = _eval_staged_layout(lay, te.roots, te.depths(), slot_feature, X, True, False, te.base_margin)
     with np.errstate(over='ignore'):
         np.testing.assert_array_equal(got, to.predict_xgboost_json(model, X))
-
-
-@pytest.mark.parametrize('depth', [1, 2, 3, 5])
-def test_oblivious_form_restates_the_walk(depth):
-    """trees.oblivious_form (the padded depth-3 trees of sa_tree_predict_oblivious): every row
-    reaches the same leaf as the staged walk -- numpy restatement of the kernel's 7 condition
-    reads and 3 selects per tree -- for complete, unbalanced (a leaf at depth 1) and constant-split
-    trees; deeper models have no oblivious form."""
-    from oracle import tree_oracle as to
-    from socceraction_amd import trees
-    rng = np.random.default_rng(10 + depth)
-    nf = 30
-    kinds = ['b' if f % 3 else 'f' for f in range(nf)]
-    model = trees.synthetic_xgboost_json(nf, n_trees=25, depth=depth, seed=depth, feature_kinds=kinds)
-    tl = model['learner']['gradient_booster']['model']['trees']
-    for t in tl[::4]:
-        if depth > 1:
-            t['left_children'][1] = -1
-            t['right_children'][1] = -1
-    for q, t in enumerate(tl[1::5]):
-        for k, f in enumerate(t['split_indices']):
-            if kinds[f] == 'b' and t['left_children'][k] >= 0:
-                t['split_conditions'][k] = (1.5, -0.5)[(k + q) % 2]
-    X = np.where(np.array(kinds) == 'b', rng.random((500, nf)) < 0.3,
-                 rng.normal(0, 30, (500, nf))).astype(np.float64)
-    X[rng.random(X.shape) < 0.05 * (np.array(kinds) == 'f')] = np.nan
-    te = trees.TreeEnsemble.from_xgboost_json(model)
-    slots = np.array([f if k == 'b' else (1 << 24 | f) for f, k in enumerate(kinds)], np.int32)
-    slot_feature = {int(s_) if (int(s_) >> 24) else int(s_) & 0xFFFFFF: f for f, s_ in enumerate(slots)}
-    lay = te.staged_layout(slots)
-    lay.update(lay['models'][0])
-    obl = trees.oblivious_form(lay)
-    if depth > 3:
-        assert obl is None
-        return
-    conds, leaves = obl
-    assert conds.shape == (25, 8) and leaves.shape == (25, 8) and not conds[:, 7].any()
-    nb = len(lay['bool_cols'])
-    bits = np.zeros((1 + nb + len(lay['num_slots']), X.shape[0]), np.int64)
-    for i, col in enumerate(lay['bool_cols']):
-        bits[1 + i] = X[:, slot_feature[int(col)]] != 0
-    for c, (sl, thr, dl) in enumerate(zip(lay['num_slots'], lay['num_thr'], lay['num_dl'])):
-        x = X[:, slot_feature[int(sl)]].astype(np.float32)
-        bits[1 + nb + c] = ~np.where(np.isnan(x), dl == 1, x < thr)
-    m = np.full(X.shape[0], np.float32(te.base_margin), np.float32)
-    for t in range(25):
-        b = [bits[int(c)] for c in conds[t, :7]]
-        b1 = np.where(b[0] == 1, b[2], b[1])
-        b2 = np.where(b[0] == 1, np.where(b1 == 1, b[6], b[5]), np.where(b1 == 1, b[4], b[3]))
-        m = (m + leaves[t, 4 * b[0] + 2 * b1 + b2]).astype(np.float32)
-    got = (np.float32(1) / (np.float32(1) + np.exp(-m))).astype(np.float32)
-    ref = _eval_staged_layout(lay, te.roots, te.depths(), slot_feature, X, True, False, te.base_margin)
-    np.testing.assert_array_equal(got, ref)
-    with np.errstate(over='ignore'):
-        np.testing.assert_array_equal(got, to.predict_xgboost_json(model, X))

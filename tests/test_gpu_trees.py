@@ -274,54 +274,3 @@ def test_float32_numeric_blocks_and_trees(sa, atomic):
         ops.features(ab, xfns, 3, num32=True)
     with pytest.raises(ValueError):
         ops.features(ab, xfns, 4, bool_bits=True, num32=True)
-
-
-def test_oblivious_walk_matches_staged(sa):
-    """sa_tree_predict_oblivious (depth <= 3 trees padded to full depth-3 trees, 7 wave-uniform
-    condition reads per tree) == the staged walk bit for bit: xgboost-shaped models (complete,
-    with a leaf at depth 1, with constant bool splits) over the bool block, the bitmaps and the
-    float32 numeric blocks, and scikit-learn HistGradientBoosting (float64, `<=`) of depth 3;
-    deeper models fall back to the staged walk and refuse method='oblivious'."""
-    from socceraction_amd import synthetic
-    from oracle import vaep_oracle as vo
-    from sklearn.ensemble import HistGradientBoostingClassifier
-    B, ops, trees = sa['batch'], sa['ops'], sa['trees']
-    ab = B.ActionBatch.from_columns(synthetic.spadl_games(150, seed=9))
-    blk = ops.features(ab, vo.SPADL_DEFAULT, 3, bool_tile=1024, num_tile=128)
-    bits = ops.features(ab, vo.SPADL_DEFAULT, 3, num_tile=128, bool_bits=True)
-    b32 = ops.features(ab, vo.SPADL_DEFAULT, 3, num_tile=128, bool_bits=True, num32=True)
-    kinds = [k for _, k, _ in blk.plan.order]
-    for depth in (1, 2, 3, 4):
-        model = trees.synthetic_xgboost_json(len(kinds), n_trees=60, depth=depth, seed=depth,
-                                             feature_kinds=kinds)
-        tl = model['learner']['gradient_booster']['model']['trees']
-        if depth > 1:
-            for t in tl[::3]:
-                t['left_children'][1] = -1
-                t['right_children'][1] = -1
-        for t in tl[1::4]:
-            for k, f in enumerate(t['split_indices']):
-                if kinds[f] == 'b' and t['left_children'][k] >= 0:
-                    t['split_conditions'][k] = 1.5
-        te = trees.TreeEnsemble.from_xgboost_json(model)
-        for fb in (blk, bits, b32):
-            ref = te.predict_blocks(fb, method='staged')
-            if depth <= 3:
-                assert torch.equal(te.predict_blocks(fb, method='oblivious'), ref), (depth, fb.num32)
-            else:
-                with pytest.raises(ValueError):
-                    te.predict_blocks(fb, method='oblivious')
-            assert torch.equal(te.predict_blocks(fb), ref)
-    n = 10000
-    b, f, i = blk.to_numpy()
-    X = np.stack([{'b': b, 'f': f, 'i': i}[k][c, :n].astype(np.float64) for _, k, c in blk.plan.order], axis=1)
-    y = X[:, 7] + np.random.default_rng(0).random(n) > 0.6
-    for md in (3, 5):
-        sk = trees.TreeEnsemble.from_model(HistGradientBoostingClassifier(
-            max_iter=20, max_depth=md, random_state=0).fit(X, y))
-        for fb in (blk, bits):
-            assert torch.equal(sk.predict_blocks(fb),
-                               sk.predict_blocks(fb, method='staged'))
-        if md == 3:
-            assert torch.equal(sk.predict_blocks(blk, method='oblivious'),
-                               sk.predict_blocks(blk, method='gather'))
