@@ -1,0 +1,80 @@
+"""A/B of the feature kernels across library builds on the SAME blocks: the default library and
+variant builds (``python -m socceraction_amd.build -DNAME=V --variant=tag``) time
+``sa_vaep_features`` (numeric families only, and the whole plan) on one batch with HIP events,
+round-robin; outputs must be byte-identical.
+
+    python scripts/feature_lib_ab.py --atomic --games 10000 --variants w4
+"""
+import argparse
+import copy
+import ctypes
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from socceraction_amd import _native as N  # noqa: E402
+from socceraction_amd import batch as B, catalog, ops, synthetic  # noqa: E402
+
+SPADL_DEFAULT = ['actiontype_onehot', 'result_onehot', 'actiontype_result_onehot',
+                 'bodypart_onehot', 'time', 'startlocation', 'endlocation', 'startpolar',
+                 'endpolar', 'movement', 'team', 'time_delta', 'space_delta', 'goalscore']
+ATOMIC_DEFAULT = ['actiontype', 'actiontype_onehot', 'bodypart', 'bodypart_onehot', 'time',
+                  'team', 'time_delta', 'location', 'polar', 'movement_polar', 'direction',
+                  'goalscore']
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--games', type=int, default=10000)
+    ap.add_argument('--atomic', action='store_true')
+    ap.add_argument('--reps', type=int, default=10)
+    ap.add_argument('--variants', default='')
+    args = ap.parse_args()
+    libs = {'default': N.lib()}
+    for v in [x for x in args.variants.split(',') if x]:
+        libs[v] = N.load_library(os.path.join(ROOT, 'socceraction_amd', '_lib',
+                                              f'libsocceraction_amd_{v}.so'))
+    gen = synthetic.atomic_games if args.atomic else synthetic.spadl_games
+    ab = B.ActionBatch.from_columns(gen(args.games), atomic=args.atomic)
+    plan = catalog.build_plan(ATOMIC_DEFAULT if args.atomic else SPADL_DEFAULT, 3, args.atomic)
+    num = copy.copy(plan)
+    num.struct = copy.deepcopy(plan.struct)
+    for x in range(len(num.struct.bool_col)):
+        num.struct.bool_col[x] = -1
+    out = ops.alloc_feature_blocks(plan, ab.n, ab.device, 1024, 128)
+    s = ab.struct()
+    stream = torch.cuda.current_stream().cuda_stream
+    bb, fb, ib = out.sa_blocks()
+    res = {'n': ab.n, 'atomic': args.atomic, 'ms': {}, 'equal': {}}
+    ref = None
+    for rnd in range(3):
+        for name, lib in libs.items():
+            for tag, p in (('num', num), ('all', plan)):
+                def run():
+                    N.check(lib.sa_vaep_features(ctypes.byref(s), ctypes.byref(p.struct), ctypes.byref(bb),
+                                                 ctypes.byref(fb), ctypes.byref(ib), stream))
+                run()
+                torch.cuda.synchronize()
+                if tag == 'all':
+                    got = [t.clone() for t in (out.bool_block, out.f64_block, out.i64_block)]
+                    if ref is None:
+                        ref = got
+                    res['equal'][name] = all(torch.equal(a, b) for a, b in zip(got, ref))
+                    del got
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record()
+                for _ in range(args.reps):
+                    run()
+                b.record()
+                torch.cuda.synchronize()
+                res['ms'].setdefault(f'{name}:{tag}', []).append(round(a.elapsed_time(b) / args.reps, 4))
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == '__main__':
+    main()
