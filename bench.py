@@ -530,7 +530,7 @@ def main() -> None:
                          '3.24 - 3.31 ms per step, profiles/r02_step_ab.md), or on the side stream')
     ap.add_argument('--num-tile', type=int, default=128,
                     help='rows per f64/i64-block tile (0 = one tile: plain column-major)')
-    ap.add_argument('--alloc-order', default='bool-first', choices=('bool-first', 'num-first'),
+    ap.add_argument('--alloc-order', default='bool-first', choices=('bool-first', 'num-first', 'single', 'single-bool-first'),
                     help='dev knob: which feature block is allocated first')
     args = ap.parse_args()
     if args.gpus < 1:
@@ -545,11 +545,20 @@ def main() -> None:
     ab = B.ActionBatch.from_columns(d, dev=dev)
     n = ab.n
     plan = catalog.build_plan(SPADL_DEFAULT, 3)
-    if args.alloc_order == 'num-first':  # dev knob: placement A/B of the output blocks
+    if args.alloc_order in ('num-first', 'single', 'single-bool-first'):  # dev knob: block placement A/B
         Rb, Rn = args.bool_tile or (n + 15) // 16 * 16, args.num_tile or (n + 15) // 16 * 16
-        fblk = torch.empty((-(-n // Rn), plan.n_f64, Rn), dtype=torch.float64, device=dev)
-        iblk = torch.empty((-(-n // Rn), plan.n_i64, Rn), dtype=torch.int64, device=dev)
-        bblk = torch.empty((-(-n // Rb), plan.n_bool, Rb), dtype=torch.uint8, device=dev)
+        shapes = [((-(-n // Rn), plan.n_f64, Rn), torch.float64), ((-(-n // Rn), plan.n_i64, Rn), torch.int64),
+                  ((-(-n // Rb), plan.n_bool, Rb), torch.uint8)]
+        if args.alloc_order.startswith('single'):  # one allocation, the three blocks carved from it
+            if args.alloc_order == 'single-bool-first':
+                shapes = shapes[2:] + shapes[:2]
+            sizes = [int(np.prod(sh)) * torch.tensor([], dtype=dt).element_size() for sh, dt in shapes]
+            offs = np.cumsum([0] + [-(-z // 4096) * 4096 for z in sizes])
+            arena = torch.empty(int(offs[-1]), dtype=torch.uint8, device=dev)
+            blks = [arena[int(o):int(o) + z].view(dt).view(sh) for o, z, (sh, dt) in zip(offs, sizes, shapes)]
+            fblk, iblk, bblk = blks[1:] + blks[:1] if args.alloc_order == 'single-bool-first' else blks
+        else:
+            fblk, iblk, bblk = [torch.empty(sh, dtype=dt, device=dev) for sh, dt in shapes]
         out = ops.FeatureBlocks(plan, n, Rb, Rn, bblk, fblk, iblk)
     else:
         out = ops.alloc_feature_blocks(plan, n, dev, bool_tile=args.bool_tile or None,
