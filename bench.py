@@ -228,9 +228,10 @@ def atomic_extra(dist, rank, world, dev, games: int, reps: int = 5) -> dict:
     out = ops.features(ab, ATOMIC_DEFAULT, 3, bool_tile=1024, num_tile=128)
     lab = ops.labels(ab)
 
-    def step():
-        ops.features(ab, ATOMIC_DEFAULT, 3, out=out)
-        ops.labels(ab, 10, lab)
+    s = ab.struct()
+
+    def step():  # features + labels in two launches: the labels ride in the numeric pass
+        ops.step_into(s, out, None, None, 10, lab, None)
     ms = _events_ms(step, reps)
     n, total, wall = ab.n, ab.n, ms
     if dist is not None:

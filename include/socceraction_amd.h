@@ -200,7 +200,8 @@ int sa_vaep_labels_formula_f32(const sa_actions* a, int32_t nr_actions, uint8_t*
  * segment: exactly sa_vaep_features (sa_vaep_features_xt when xt_cells != NULL) followed by
  * sa_vaep_labels_formula_f64 with the same arguments.  With nb_prev_actions <= 3 and
  * nr_actions <= 11 the labels and the formula are computed inside the numeric feature pass
- * (no launch of their own); otherwise the two launches run.  Windowed mode. */
+ * (no launch of their own); otherwise the two launches run.  Windowed mode.  With p_scores,
+ * p_concedes, off, def and val all NULL: features + labels only (compute_labels, no formula). */
 int sa_vaep_step_f64(const sa_actions* a, const sa_feature_plan* plan, const sa_block* bool_out,
                      const sa_block* f64_out, const sa_block* i64_out, int32_t xt_l, int32_t xt_w,
                      uint32_t* xt_cells, int32_t nr_actions, uint8_t* scores, uint8_t* concedes,

@@ -931,9 +931,11 @@ __global__ __launch_bounds__(256) void num_features_kernel(FeatArgs args) {
                                  gcol, (int)args.Ci, Ri);
     if (TAIL) {  // labels + formula of the same rows (every lane of the wave present)
       labels_pair<ATOMIC>(A, args.nr, args.sc, args.co, args.gfs, wave_base + 2 * lane, cur);
-      SegCursor fc = cur;
-      formula_rows<ATOMIC, double>(A, args.ps, args.pc, args.off, args.def, args.val, args.vec_ok,
-                                   wave_base + 2 * lane, fc);
+      if (args.ps) {  // uniform: labels only when no probabilities are given
+        SegCursor fc = cur;
+        formula_rows<ATOMIC, double>(A, args.ps, args.pc, args.off, args.def, args.val, args.vec_ok,
+                                     wave_base + 2 * lane, fc);
+      }
     }
   }
   if (wave_base + 2 * lane >= n) return;
@@ -1558,7 +1560,9 @@ extern "C" int sa_vaep_step_f64(const sa_actions* a, const sa_feature_plan* plan
     return fail(SA_EINVAL, "ld must be a multiple of 16 and >= round_up(n, 16)");
   if (!aligned16(scores) || !aligned16(concedes) || !aligned16(goal_from_shot))
     return fail(SA_EINVAL, "label outputs must be 16-byte aligned");
-  if (!p_scores || !p_concedes || !off || !def || !val) return fail(SA_EINVAL, "null probability/output pointer");
+  const bool formula = p_scores || p_concedes || off || def || val;  // all NULL: labels only
+  if (formula && (!p_scores || !p_concedes || !off || !def || !val))
+    return fail(SA_EINVAL, "null probability/output pointer");
   if (!aligned16(off) || !aligned16(def) || !aligned16(val))
     return fail(SA_EINVAL, "formula outputs must be 16-byte aligned (length >= round_up(n, 16))");
   if (xt_cells) {
@@ -1569,6 +1573,7 @@ extern "C" int sa_vaep_step_f64(const sa_actions* a, const sa_feature_plan* plan
   }
   if (plan->nb_prev_actions > 3 || nr_actions > SA_STEP_MAX_NR) {  // no fused form: the separate launches
     if ((rc = launch_features(a, plan, bool_out, f64_out, i64_out, xt_l, xt_w, xt_cells, stream))) return rc;
+    if (!formula) return sa_vaep_labels(a, nr_actions, scores, concedes, goal_from_shot, ld, stream);
     return sa_vaep_labels_formula_f64(a, nr_actions, scores, concedes, goal_from_shot, ld, p_scores,
                                       p_concedes, off, def, val, stream);
   }

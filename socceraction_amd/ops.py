@@ -261,23 +261,28 @@ def labels_formula(batch: ActionBatch, p_scores: torch.Tensor, p_concedes: torch
     return labels_out, values_out
 
 
-def step_into(s: _native.SaActions, out: FeatureBlocks, p_scores: torch.Tensor,
-              p_concedes: torch.Tensor, nr_actions: int, labels_out: LabelBlocks,
-              values_out: torch.Tensor, xt_cells: Optional[tuple] = None) -> None:
+def step_into(s: _native.SaActions, out: FeatureBlocks, p_scores: Optional[torch.Tensor],
+              p_concedes: Optional[torch.Tensor], nr_actions: int, labels_out: LabelBlocks,
+              values_out: Optional[torch.Tensor], xt_cells: Optional[tuple] = None) -> None:
     """The batch valuation step in one call (``sa_vaep_step_f64``): the features of ``out``'s
     plan (and, with ``xt_cells = (l, w, cells)``, every action's xT cell code), the labels and
     the f64 formula of the same actions -- exactly :func:`features_into` followed by
-    :func:`labels_formula`, with the labels and formula computed inside the numeric pass."""
-    if p_scores.dtype != torch.float64 or p_concedes.dtype != torch.float64:
-        raise TypeError('the fused step takes float64 probabilities (float32: labels_formula)')
-    if p_scores.numel() < s.n or p_concedes.numel() < s.n:
-        raise ValueError('one probability per action is required')
+    :func:`labels_formula`, with the labels and formula computed inside the numeric pass.
+    ``p_scores = p_concedes = values_out = None``: features + labels only."""
+    if p_scores is not None:
+        if p_scores.dtype != torch.float64 or p_concedes.dtype != torch.float64:
+            raise TypeError('the fused step takes float64 probabilities (float32: labels_formula)')
+        if p_scores.numel() < s.n or p_concedes.numel() < s.n:
+            raise ValueError('one probability per action is required')
+        ps, pc = p_scores.contiguous(), p_concedes.contiguous()
+        o = (values_out[0], values_out[1], values_out[2])
+    else:  # features + labels only
+        ps = pc = None
+        o = (None, None, None)
     l, w, cells = xt_cells if xt_cells is not None else (0, 0, None)
     if cells is not None and (cells.dtype != torch.int32 or cells.numel() < s.n):
         raise ValueError('cells must be an int32 tensor of at least n elements')
-    ps, pc = p_scores.contiguous(), p_concedes.contiguous()
     bb, fb, ib = out.sa_blocks()
-    o = values_out
     _native.check(_native.lib().sa_vaep_step_f64(
         ctypes.byref(s), ctypes.byref(out.plan.struct), ctypes.byref(bb), ctypes.byref(fb),
         ctypes.byref(ib), int(l), int(w), _ptr(cells), int(nr_actions), _ptr(labels_out.scores),

@@ -528,7 +528,8 @@ def test_step_matches_separate_launches(sa, atomic):
     look-ahead by wave shuffles) == sa_vaep_features (+ the xT cell codes) followed by
     sa_vaep_labels_formula_f64, byte for byte: the goldens (edge sizes 1..300, forced tail goals),
     full games + 300 games of 1..40 actions at nr_actions 1, 2, 10, 11 and 20 (the last runs the
-    separate launches), k = 1..4, both layouts, and 2,000 full-size games."""
+    separate launches), k = 1..4, both layouts, and 2,000 full-size games; and the labels-only
+    form (no probabilities) == features + labels."""
     B, ops, syn = sa['batch'], sa['ops'], sa['synthetic']
     default = vo.ATOMIC_DEFAULT if atomic else vo.SPADL_DEFAULT
     prefix = 'atomic' if atomic else 'spadl'
@@ -578,3 +579,13 @@ def test_step_matches_separate_launches(sa, atomic):
                     assert torch.equal(val[:, :n], vref[:, :n]), (bi, nr, k)
                     if xt:
                         assert torch.equal(cells[:n], cells_ref[:n])
+                    if k == 3:  # features + labels only (no probabilities): the cfg3 step
+                        out2 = ops.alloc_feature_blocks(ref.plan, n, ab.device, Rb, Rn)
+                        lab2, _ = ops.labels_formula(ab, ps, pc, nr_actions=nr)
+                        for t in (lab2.scores, lab2.concedes, lab2.goal_from_shot):
+                            t.fill_(7)
+                        ops.step_into(ab.struct(), out2, None, None, nr, lab2, None)
+                        for a, b in zip(out2.to_numpy(), ref.to_numpy()):
+                            np.testing.assert_array_equal(a, b)
+                        for c in ('scores', 'concedes', 'goal_from_shot'):
+                            assert torch.equal(getattr(lab2, c)[:n], getattr(lref, c)[:n]), (bi, nr, c)
