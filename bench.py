@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import argparse
 import copy
+import ctypes
 import json
 import os
 import sys
@@ -129,7 +130,7 @@ def _reduce(dist, value, op, dev):
     return float(t.item())
 
 
-def xt_step(ab, dist, source: str = 'cells', cells=None, shared: bool = True):
+def xt_step(ab, dist, source: str = 'cells', cells=None, shared: bool = True, sync_solve: bool = False):
     """BASELINE cfg4 inside the step: xT 16x12 fit on the step's actions (count pass, RCCL
     all-reduce of the counts across ranks, value iteration to eps=1e-5; the solve synchronises
     its stream) and ExpectedThreat.rate of every action, as two phases so the caller can enqueue
@@ -140,6 +141,7 @@ def xt_step(ab, dist, source: str = 'cells', cells=None, shared: bool = True):
     4-B rate operand per action for the rate; 'coords': both passes read the coordinates."""
     from socceraction_amd import shard
     state = {}
+    cur_cells = cells if callable(cells) else (lambda: cells)  # the step's cell-code buffer
     # the step's count buffers, allocated once and zeroed by ONE fill on the side stream while
     # the numeric pass runs (zero()), not by per-step allocations on the main stream
     acc0 = ops.xt_zero_counts(16, 12, ab.device)
@@ -150,7 +152,7 @@ def xt_step(ab, dist, source: str = 'cells', cells=None, shared: bool = True):
         if source == 'none':  # --ab diagnostic only: the VAEP kernels without the xT part
             return
         if source == 'cells':
-            state['acc'] = ops.xt_count_cells(cells, ab.n, 16, 12, acc=acc0, shared=shared)
+            state['acc'] = ops.xt_count_cells(cur_cells(), ab.n, 16, 12, acc=acc0, shared=shared)
         else:
             state['acc'] = ops.xt_count(ab, 16, 12, acc=acc0, codes=codes, shared=shared)
 
@@ -176,9 +178,11 @@ def xt_step(ab, dist, source: str = 'cells', cells=None, shared: bool = True):
     def finish():
         if source == 'none':
             return
-        sol = ops.xt_solve(state.pop('acc'))  # synchronises the current stream
+        # the solve without a host round trip (its iteration count stays on the device until
+        # the report), so the rate is enqueued right behind it; sync_solve: the round-trip form
+        sol = (ops.xt_solve(state.pop('acc')) if sync_solve else ops.xt_solve_async(state.pop('acc')))
         if source == 'cells':
-            ops.xt_rate_cells(cells, ab.n, 16, 12, sol.mats[3], out=rate_out)
+            ops.xt_rate_cells(cur_cells(), ab.n, 16, 12, sol.mats[3], out=rate_out)
         elif source == 'codes':
             ops.xt_rate_codes(codes, ab.n, sol.mats[3], out=rate_out)
         else:
@@ -191,6 +195,14 @@ def xt_step(ab, dist, source: str = 'cells', cells=None, shared: bool = True):
 ATOMIC_DEFAULT = ['actiontype', 'actiontype_onehot', 'bodypart', 'bodypart_onehot', 'time',
                   'team', 'time_delta', 'location', 'polar', 'movement_polar', 'direction',
                   'goalscore']
+
+
+def _iterations(sol) -> int:
+    """The value iteration's count (a device tensor for the asynchronous solve)."""
+    n = sol.n_iter if isinstance(sol.n_iter, int) else int(sol.n_iter.item())
+    if n < 0:
+        raise RuntimeError('xT value iteration did not converge')
+    return n
 
 
 def _num_index(order) -> int:
@@ -531,8 +543,13 @@ def main() -> None:
                          '3.24 - 3.31 ms per step, profiles/r02_step_ab.md), or on the side stream')
     ap.add_argument('--num-tile', type=int, default=128,
                     help='rows per f64/i64-block tile (0 = one tile: plain column-major)')
-    ap.add_argument('--alloc-order', default='bool-first', choices=('bool-first', 'num-first', 'single', 'single-bool-first'),
-                    help='dev knob: which feature block is allocated first')
+    ap.add_argument('--reserve-cu', type=int, default=0,
+                    help='dev knob: run the step on a stream masked off the last N CUs')
+    ap.add_argument('--alloc-order', default='contig',
+                    choices=('contig', 'bool-first', 'num-first', 'single', 'single-bool-first'),
+                    help='output blocks: contig = the bool block in physically contiguous VRAM '
+                         '(default; profiles/r02u_goalscore_fused_ab.md r02aq - r02au), else '
+                         'placement A/B knobs (bool-first = three caching-allocator blocks)')
     args = ap.parse_args()
     if args.gpus < 1:
         raise SystemExit('--gpus must be >= 1')
@@ -546,7 +563,10 @@ def main() -> None:
     ab = B.ActionBatch.from_columns(d, dev=dev)
     n = ab.n
     plan = catalog.build_plan(SPADL_DEFAULT, 3)
-    if args.alloc_order in ('num-first', 'single', 'single-bool-first'):  # dev knob: block placement A/B
+    if args.alloc_order == 'contig':  # the bool block in physically contiguous VRAM (default)
+        out = ops.alloc_feature_blocks(plan, n, dev, bool_tile=args.bool_tile or None,
+                                       num_tile=args.num_tile or None, contiguous=True)
+    elif args.alloc_order in ('num-first', 'single', 'single-bool-first'):  # dev knob: block placement A/B
         Rb, Rn = args.bool_tile or (n + 15) // 16 * 16, args.num_tile or (n + 15) // 16 * 16
         shapes = [((-(-n // Rn), plan.n_f64, Rn), torch.float64), ((-(-n // Rn), plan.n_i64, Rn), torch.int64),
                   ((-(-n // Rb), plan.n_bool, Rb), torch.uint8)]
@@ -587,7 +607,18 @@ def main() -> None:
     lab = ops.LabelBlocks(n, lab_buf[0], lab_buf[1], None)
     val = torch.empty((3, ld), dtype=torch.float64, device=dev)
     s_act = ab.struct()
-    cells = ops.xt_cells_buffer(n, dev)
+    # two cell-code buffers used by alternate steps: with the xT side stream of step k still
+    # rating from its codes while step k+1's numeric pass writes the other buffer (pipelined)
+    ring = {'bufs': [ops.xt_cells_buffer(n, dev), ops.xt_cells_buffer(n, dev)], 'k': 0, 'done': [None, None]}
+
+    def cells():
+        return ring['bufs'][ring['k']]
+    if args.reserve_cu > 0:  # dev knob: the VAEP passes on a CU-masked stream (xT side stream free)
+        from socceraction_amd import _native as NN
+        hs = ctypes.c_void_p()
+        NN.check(NN.lib().sa_stream_create_cu_masked(args.reserve_cu, ctypes.byref(hs)))
+        main_s = torch.cuda.ExternalStream(hs.value)
+        torch.cuda.set_stream(main_s)
     main_s = torch.cuda.current_stream()
     overlap = not args.serial
     # the xT side stream; --side-priority high: a high-priority HIP stream, so its few
@@ -610,33 +641,39 @@ def main() -> None:
             raise SystemExit('xt=cells: the side stream forks after num_features')
         by_name = {'bool_features': lambda: ops.features_into(s_act, bool_out),
                    'num_features': (lambda: ops.features_into(s_act, num_out,
-                                                              xt_cells=(16, 12, cells)))
+                                                              xt_cells=(16, 12, cells())))
                    if xt in ('cells', 'none') else (lambda: ops.features_into(s_act, num_out)),
                    'num_features_nogs': (lambda: ops.features_into(s_act, num_nogs,
-                                                                   xt_cells=(16, 12, cells)))
+                                                                   xt_cells=(16, 12, cells())))
                    if xt in ('cells', 'none') else (lambda: ops.features_into(s_act, num_nogs)),
                    'goalscore': lambda: ops.goalscore_into(ab, out),
                    'labels': lambda: ops.labels(ab, 10, lab),
                    'formula': lambda: ops.formula(ab, ps, pc, val),
                    'labels_formula': lambda: ops.labels_formula(ab, ps, pc, 10, lab, val),
                    'num_step': lambda: ops.step_into(s_act, num_out, ps, pc, 10, lab, val,
-                                                     xt_cells=(16, 12, cells) if xt in ('cells', 'none')
+                                                     xt_cells=(16, 12, cells()) if xt in ('cells', 'none')
                                                      else None)}
         calls = tuple(by_name[k] for k in order)
         # cm=1: the count pass runs on the main stream right after num_features, in the fast
         # one-workgroup-per-CU shape; the side stream takes the all-reduce, solve and rate
         cm = int(spec.get('cm', 0)) and overlap
-        xt_start, xt_finish, xt_last = xt_step(ab, dist, xt, cells, shared=overlap and not cm)
+        xt_start, xt_finish, xt_last = xt_step(ab, dist, xt, cells, shared=overlap and not cm,
+                                               sync_solve=bool(int(spec.get('xsync', 0))))
         nv = len(calls)
         # par=1 (A/B only): bool_features on its own stream, concurrent with the calls before it
         par = int(spec.get('par', 0)) and 'bool_features' in order
         ib = order.index('bool_features') if par else -1
+
+        pipe = int(spec.get('pipe', 1)) and overlap
 
         def step(ev=None):
             # ev[i] = (start, end) of VAEP call i on the main stream, ev[nv] = the xT side
             # stream's span (count pass + all-reduce, then solve -- a host sync of the side
             # stream -- and rate); --serial: everything on the one stream
             pj = None
+            if pipe and ring['done'][ring['k']] is not None:
+                # this step's cell-code buffer was last read by the xT rate two steps ago
+                main_s.wait_event(ring['done'][ring['k']])
             # zero the xT counts on the side stream (idle until the fork) while the first VAEP
             # call runs; the count pass waits for it
             zs = side if overlap else main_s
@@ -687,7 +724,10 @@ def main() -> None:
                 xt_finish()
                 if ev is not None:
                     ev[nv][1].record(side)
-            if overlap:
+            if pipe:  # pipelined: the xT work of this step overlaps the next step's passes
+                ring['done'][ring['k']] = _record(side)
+                ring['k'] ^= 1
+            elif overlap:
                 join = torch.cuda.Event()
                 join.record(side)
                 main_s.wait_event(join)
@@ -705,7 +745,7 @@ def main() -> None:
             v = dict(base)
             for kv in [o for o in opts.split('/') if o]:
                 k_, _, v_ = kv.partition('=')
-                v[k_] = v_.split('+') if k_ == 'order' else (int(v_) if k_ in ('fork', 'par', 'cm', 'diag') else v_)
+                v[k_] = v_.split('+') if k_ == 'order' else (int(v_) if k_ in ('fork', 'par', 'cm', 'diag', 'xsync', 'pipe') else v_)
             variants[name] = (make_step(v)[0], v['order'])
         ab_ms = {k: [] for k in variants}
         ab_kern = {}
@@ -797,7 +837,8 @@ def main() -> None:
                                'the ranks) + rate of the same actions',
                    'games_per_gpu': args.games, 'actions_per_gpu': n,
                    'feature_layout': f'tiled column-major: bool {out.Rb}, f64/i64 {out.Rn} rows '
-                                     'per tile',
+                                     'per tile' + ('; bool block in physically contiguous VRAM'
+                                                   if getattr(out, '_arena', None) is not None else ''),
                    'parallelism': f'games sharded over {world} GPU(s)'},
         'kernels': per_kernel,
         'roofline': {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS,
@@ -816,7 +857,7 @@ def main() -> None:
                        # overlapped: the side stream's span from its first launch to the
                        # rate's end (it shares the GPU with the VAEP kernels meanwhile)
                        'ms' if args.serial else 'span_ms': round(kern['xt_fit_rate'], 4),
-                       'iterations': xt_last['sol'].n_iter,
+                       'iterations': _iterations(xt_last['sol']),
                        'source': {'cells': 'cell codes written by the f64 feature pass',
                                   'codes': 'coordinates (count) + rate operands',
                                   'coords': 'coordinates'}[base['xt']],
@@ -828,7 +869,9 @@ def main() -> None:
                         'call(s), overlapped with the rest')}
     line['vaep_order'] = order
     line['streams'] = ('one stream' if args.serial else
-                       'VAEP kernels on the main stream, xT on a side stream')
+                       'VAEP kernels on the main stream, xT solve + rate on a side stream without a '
+                       'host round trip, pipelined: step k\'s xT work may finish during step k+1 (two '
+                       'cell-code buffers); the timed region ends after every stream is synchronised')
     line.update(extra_side)
     if not args.no_cpu and world == 1:  # the CPU comparator runs on rank 0 at N = 1 only
         line['cpu_baseline'] = cpu_baseline(d, args.cpu_seconds)

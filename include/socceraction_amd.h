@@ -267,6 +267,14 @@ int sa_xt_rate_cells(const uint32_t* cells, int64_t n, int32_t l, int32_t w, con
 int sa_xt_solve(const int64_t* shot, const int64_t* goal, const int64_t* move,
                 const int32_t* trans, int32_t l, int32_t w, double eps, int32_t max_iter,
                 double* mats, double* trans_t, double* heatmaps, int32_t* n_iter, void* stream);
+/* sa_xt_solve for grids of <= SA_XT_SOLVE_MAX_C cells without the host round trip: the
+ * iteration count (-1: max_iter reached first) is written to device memory *n_iter_dev and
+ * nothing is synchronised, so a consumer of the surface (sa_xt_rate_cells) can be enqueued
+ * right behind it (the bench step's side stream). */
+int sa_xt_solve_async(const int64_t* shot, const int64_t* goal, const int64_t* move,
+                      const int32_t* trans, int32_t l, int32_t w, double eps, int32_t max_iter,
+                      double* mats, double* trans_t, double* heatmaps, int32_t* n_iter_dev,
+                      void* stream);
 
 /* Normalisation only (scoring_prob, action_prob, move_transition_matrix of
  * xthreat.py:74-218): mats[3*C] = scoring_prob | shot_prob | move_prob, trans_t as in
@@ -484,6 +492,15 @@ const char* sa_build_id(void);
  * owned by the library (mutex-guarded, reused in stream order); sa_shutdown() waits for the
  * last use of every slot and frees the arena.  The library stays usable afterwards. */
 int sa_shutdown(void);
+/* Device memory for output blocks: flags bit 0 = physically contiguous VRAM
+ * (hipDeviceMallocContiguous: the largest translation fragments).  Free with sa_device_free. */
+int sa_device_alloc(int64_t bytes, int32_t flags, void** out);
+int sa_device_free(void* p);
+/* A stream whose kernels run on every CU but the last n_reserved (hipExtStreamCreateWithCUMask):
+ * the VAEP passes on such a stream leave whole CUs to a side stream's latency-bound work (the
+ * xT solve's one workgroup).  Destroy with sa_stream_destroy. */
+int sa_stream_create_cu_masked(int32_t n_reserved, void** out);
+int sa_stream_destroy(void* s);
 /* Debug build (-DSA_DEBUG=1, libsocceraction_amd_debug.so): kernels check tile offsets,
  * column indices, segment cursors, LDS and grid-cell indices and record the first failure
  * instead of accessing out of bounds.  sa_debug_check() synchronises the device and returns

@@ -135,6 +135,9 @@ _SIGNATURES = {
     'sa_xt_solve': (ctypes.c_int, [_p, _p, _p, _p, ctypes.c_int32, ctypes.c_int32,
                                    ctypes.c_double, ctypes.c_int32, _p, _p, _p,
                                    ctypes.POINTER(ctypes.c_int32), _p]),
+    'sa_xt_solve_async': (ctypes.c_int, [_p, _p, _p, _p, ctypes.c_int32, ctypes.c_int32,
+                                   ctypes.c_double, ctypes.c_int32, _p, _p, _p,
+                                   _p, _p]),
     'sa_xt_normalize': (ctypes.c_int, [_p, _p, _p, _p, ctypes.c_int32, ctypes.c_int32, _p, _p,
                                        _p]),
     'sa_xt_probabilities': (ctypes.c_int, [_p, _p, _p, ctypes.c_int32, _p, _p, _p, _p]),
@@ -169,6 +172,10 @@ _SIGNATURES = {
                                               ctypes.POINTER(SaBlock), _p, ctypes.c_int64,
                                               ctypes.POINTER(SaBlock), ctypes.POINTER(SaBlock),
                                               ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, _p]),
+    'sa_device_alloc': (ctypes.c_int, [ctypes.c_int64, ctypes.c_int32, ctypes.POINTER(ctypes.c_void_p)]),
+    'sa_device_free': (ctypes.c_int, [_p]),
+    'sa_stream_create_cu_masked': (ctypes.c_int, [ctypes.c_int32, ctypes.POINTER(ctypes.c_void_p)]),
+    'sa_stream_destroy': (ctypes.c_int, [_p]),
     'sa_abi_version': (ctypes.c_int, []),
     'sa_last_error': (ctypes.c_char_p, []),
     'sa_build_id': (ctypes.c_char_p, []),

@@ -106,6 +106,39 @@ bool register_debug_poll(debug_poll_fn fn) {
 
 using namespace sa;
 
+extern "C" int sa_device_alloc(int64_t bytes, int32_t flags, void** out) {
+  if (!out || bytes <= 0 || (flags & ~1)) return fail(SA_EINVAL, "bad allocation request");
+  *out = nullptr;
+  if (flags & 1)
+    return check_hip(hipExtMallocWithFlags(out, (size_t)bytes, hipDeviceMallocContiguous),
+                     "sa_device_alloc: hipExtMallocWithFlags(contiguous)");
+  return check_hip(hipMalloc(out, (size_t)bytes), "sa_device_alloc: hipMalloc");
+}
+
+extern "C" int sa_device_free(void* p) {
+  return p ? check_hip(hipFree(p), "sa_device_free: hipFree") : SA_OK;
+}
+
+extern "C" int sa_stream_create_cu_masked(int32_t n_reserved, void** out) {
+  if (!out || n_reserved < 0) return fail(SA_EINVAL, "bad stream request");
+  int dev = 0, cus = 0;
+  int rc = check_hip(hipGetDevice(&dev), "hipGetDevice");
+  if (!rc) rc = check_hip(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev), "CU count");
+  if (rc) return rc;
+  if (n_reserved >= cus) return fail(SA_EINVAL, "cannot reserve %d of %d CUs", n_reserved, cus);
+  std::vector<uint32_t> mask((cus + 31) / 32, 0u);
+  for (int c = 0; c < cus - n_reserved; ++c) mask[c / 32] |= 1u << (c % 32);  // the last n_reserved left out
+  hipStream_t s = nullptr;
+  rc = check_hip(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()),
+                 "hipExtStreamCreateWithCUMask");
+  *out = rc ? nullptr : (void*)s;
+  return rc;
+}
+
+extern "C" int sa_stream_destroy(void* s) {
+  return s ? check_hip(hipStreamDestroy((hipStream_t)s), "hipStreamDestroy") : SA_OK;
+}
+
 extern "C" int sa_abi_version(void) { return SA_ABI_VERSION; }
 extern "C" const char* sa_last_error(void) { return sa::g_err; }
 

@@ -838,6 +838,41 @@ extern "C" int sa_xt_count_cells(const uint32_t* cells, int64_t n, int32_t l, in
                       (hipStream_t)stream);
 }
 
+extern "C" int sa_xt_solve_async(const int64_t* shot, const int64_t* goal, const int64_t* move,
+                                 const int32_t* trans, int32_t l, int32_t w, double eps, int32_t max_iter,
+                                 double* mats, double* trans_t, double* heatmaps, int32_t* n_iter_dev,
+                                 void* stream) {
+  if (l < 1 || w < 1 || max_iter < 0) return fail(SA_EINVAL, "bad l, w or max_iter");
+  const int C = l * w;
+  if (C > XT_SOLVE_MAX_C) return fail(SA_EINVAL, "the asynchronous solve takes grids of <= %d cells", XT_SOLVE_MAX_C);
+  if (!shot || !goal || !move || !trans || !mats || !trans_t || !heatmaps || !n_iter_dev)
+    return fail(SA_EINVAL, "null pointer");
+  hipStream_t st = (hipStream_t)stream;
+  auto* us = reinterpret_cast<const unsigned long long*>(shot);
+  auto* ug = reinterpret_cast<const unsigned long long*>(goal);
+  auto* um = reinterpret_cast<const unsigned long long*>(move);
+  Scratch sc;  // gs[C] | pmove[C]
+  int rc = scratch_acquire(sizeof(double) * 2 * C, st, &sc);
+  if (rc) return rc;
+  double* gs = static_cast<double*>(sc.ptr);
+  double* pm = gs + C;
+  hipLaunchKernelGGL(xt_prob_kernel, dim3((C + 255) / 256), dim3(256), 0, st, us, ug, um, C, mats, gs, pm);
+  const dim3 tgrid((C + 31) / 32, (C + 31) / 32);
+  hipLaunchKernelGGL(xt_transpose_kernel, tgrid, dim3(256), 0, st, trans, um, C, trans_t);
+  rc = check_launch("xt normalise");
+  if (!rc && C <= XR_MAX_C) {
+    hipLaunchKernelGGL(xt_solve_reg_kernel<SA_XR_PARTS>, dim3(1), dim3(SA_XR_PARTS * XR_MAX_C), 0, st, trans_t, gs,
+                       pm, C, eps, max_iter, heatmaps, mats + 3 * C, n_iter_dev);
+    rc = check_launch("xt_solve_reg_kernel");
+  } else if (!rc) {
+    hipLaunchKernelGGL(xt_solve_small_kernel, dim3(1), dim3(((C + 63) / 64) * 64), 0, st, trans_t, gs, pm, C, eps,
+                       max_iter, heatmaps, mats + 3 * C, n_iter_dev);
+    rc = check_launch("xt_solve_small_kernel");
+  }
+  scratch_release(sc, st);
+  return rc;
+}
+
 extern "C" int sa_xt_solve(const int64_t* shot, const int64_t* goal, const int64_t* move,
                            const int32_t* trans, int32_t l, int32_t w, double eps, int32_t max_iter,
                            double* mats, double* trans_t, double* heatmaps, int32_t* n_iter,

@@ -589,3 +589,21 @@ def test_step_matches_separate_launches(sa, atomic):
                             np.testing.assert_array_equal(a, b)
                         for c in ('scores', 'concedes', 'goal_from_shot'):
                             assert torch.equal(getattr(lab2, c)[:n], getattr(lref, c)[:n]), (bi, nr, c)
+
+
+@pytest.mark.parametrize('l,w', [(16, 12), (8, 6), (30, 20)])
+def test_xt_solve_async_matches_solve(sa, l, w):
+    """sa_xt_solve_async (no host round trip; the iteration count stays on the device) == the
+    synchronised sa_xt_solve: every matrix, the surface, the heatmaps and the iteration count,
+    bit for bit (the register solve at 16 x 12 and 8 x 6, the one-workgroup solve at 30 x 20)."""
+    B, ops, syn = sa['batch'], sa['ops'], sa['synthetic']
+    ab = B.ActionBatch.from_columns(syn.spadl_games(40, seed=12))
+    acc = ops.xt_count(ab, l, w)
+    ref = ops.xt_solve(acc)
+    got = ops.xt_solve_async(acc)
+    torch.cuda.synchronize()
+    n = int(got.n_iter.item())
+    assert n == ref.n_iter > 0
+    assert torch.equal(got.mats, ref.mats)
+    assert torch.equal(got.trans_t, ref.trans_t)
+    assert torch.equal(got.heatmaps[:n + 1], ref.heatmaps)
