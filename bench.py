@@ -16,7 +16,6 @@ from __future__ import annotations
 
 import argparse
 import copy
-import ctypes
 import json
 import os
 import sys
@@ -543,8 +542,6 @@ def main() -> None:
                          '3.24 - 3.31 ms per step, profiles/r02_step_ab.md), or on the side stream')
     ap.add_argument('--num-tile', type=int, default=128,
                     help='rows per f64/i64-block tile (0 = one tile: plain column-major)')
-    ap.add_argument('--reserve-cu', type=int, default=0,
-                    help='dev knob: run the step on a stream masked off the last N CUs')
     ap.add_argument('--alloc-order', default='contig',
                     choices=('contig', 'bool-first', 'num-first', 'single', 'single-bool-first'),
                     help='output blocks: contig = the bool block in physically contiguous VRAM '
@@ -613,12 +610,6 @@ def main() -> None:
 
     def cells():
         return ring['bufs'][ring['k']]
-    if args.reserve_cu > 0:  # dev knob: the VAEP passes on a CU-masked stream (xT side stream free)
-        from socceraction_amd import _native as NN
-        hs = ctypes.c_void_p()
-        NN.check(NN.lib().sa_stream_create_cu_masked(args.reserve_cu, ctypes.byref(hs)))
-        main_s = torch.cuda.ExternalStream(hs.value)
-        torch.cuda.set_stream(main_s)
     main_s = torch.cuda.current_stream()
     overlap = not args.serial
     # the xT side stream; --side-priority high: a high-priority HIP stream, so its few

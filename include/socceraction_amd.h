@@ -496,11 +496,6 @@ int sa_shutdown(void);
  * (hipDeviceMallocContiguous: the largest translation fragments).  Free with sa_device_free. */
 int sa_device_alloc(int64_t bytes, int32_t flags, void** out);
 int sa_device_free(void* p);
-/* A stream whose kernels run on every CU but the last n_reserved (hipExtStreamCreateWithCUMask):
- * the VAEP passes on such a stream leave whole CUs to a side stream's latency-bound work (the
- * xT solve's one workgroup).  Destroy with sa_stream_destroy. */
-int sa_stream_create_cu_masked(int32_t n_reserved, void** out);
-int sa_stream_destroy(void* s);
 /* Debug build (-DSA_DEBUG=1, libsocceraction_amd_debug.so): kernels check tile offsets,
  * column indices, segment cursors, LDS and grid-cell indices and record the first failure
  * instead of accessing out of bounds.  sa_debug_check() synchronises the device and returns

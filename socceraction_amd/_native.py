@@ -174,8 +174,6 @@ _SIGNATURES = {
                                               ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, _p]),
     'sa_device_alloc': (ctypes.c_int, [ctypes.c_int64, ctypes.c_int32, ctypes.POINTER(ctypes.c_void_p)]),
     'sa_device_free': (ctypes.c_int, [_p]),
-    'sa_stream_create_cu_masked': (ctypes.c_int, [ctypes.c_int32, ctypes.POINTER(ctypes.c_void_p)]),
-    'sa_stream_destroy': (ctypes.c_int, [_p]),
     'sa_abi_version': (ctypes.c_int, []),
     'sa_last_error': (ctypes.c_char_p, []),
     'sa_build_id': (ctypes.c_char_p, []),

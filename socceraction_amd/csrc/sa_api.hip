@@ -119,26 +119,6 @@ extern "C" int sa_device_free(void* p) {
   return p ? check_hip(hipFree(p), "sa_device_free: hipFree") : SA_OK;
 }
 
-extern "C" int sa_stream_create_cu_masked(int32_t n_reserved, void** out) {
-  if (!out || n_reserved < 0) return fail(SA_EINVAL, "bad stream request");
-  int dev = 0, cus = 0;
-  int rc = check_hip(hipGetDevice(&dev), "hipGetDevice");
-  if (!rc) rc = check_hip(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev), "CU count");
-  if (rc) return rc;
-  if (n_reserved >= cus) return fail(SA_EINVAL, "cannot reserve %d of %d CUs", n_reserved, cus);
-  std::vector<uint32_t> mask((cus + 31) / 32, 0u);
-  for (int c = 0; c < cus - n_reserved; ++c) mask[c / 32] |= 1u << (c % 32);  // the last n_reserved left out
-  hipStream_t s = nullptr;
-  rc = check_hip(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()),
-                 "hipExtStreamCreateWithCUMask");
-  *out = rc ? nullptr : (void*)s;
-  return rc;
-}
-
-extern "C" int sa_stream_destroy(void* s) {
-  return s ? check_hip(hipStreamDestroy((hipStream_t)s), "hipStreamDestroy") : SA_OK;
-}
-
 extern "C" int sa_abi_version(void) { return SA_ABI_VERSION; }
 extern "C" const char* sa_last_error(void) { return sa::g_err; }
 

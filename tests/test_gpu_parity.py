@@ -607,3 +607,25 @@ def test_xt_solve_async_matches_solve(sa, l, w):
     assert torch.equal(got.mats, ref.mats)
     assert torch.equal(got.trans_t, ref.trans_t)
     assert torch.equal(got.heatmaps[:n + 1], ref.heatmaps)
+
+
+def test_contiguous_bool_block_matches(sa):
+    """Feature blocks whose bool block lives in physically contiguous VRAM (sa_device_alloc,
+    viewed through __cuda_array_interface__) hold the same bytes as caching-allocator blocks, and
+    the allocation outlives the DeviceBuffer's last Python reference held by the blocks."""
+    import gc
+    B, ops, syn = sa['batch'], sa['ops'], sa['synthetic']
+    ab = B.ActionBatch.from_columns(syn.spadl_games(30, seed=4))
+    plan = ops.build_plan(vo.SPADL_DEFAULT, 3, False)
+    ref = ops.alloc_feature_blocks(plan, ab.n, ab.device, 1024, 128)
+    got = ops.alloc_feature_blocks(plan, ab.n, ab.device, 1024, 128, contiguous=True)
+    assert got._arena is not None and got.bool_block.data_ptr() == got._arena.ptr
+    gc.collect()
+    for fb in (ref, got):
+        ops.features_into(ab.struct(), fb)
+    for a, b in zip(got.to_numpy(), ref.to_numpy()):
+        np.testing.assert_array_equal(a, b)
+    buf = ops.DeviceBuffer(1 << 20, contiguous=False)
+    t = buf.tensor((256, 1024), torch.float32)
+    t.fill_(2.0)
+    assert float(t.sum()) == 2.0 * 256 * 1024
