@@ -373,6 +373,10 @@ def rate_extra(ab, out, n, dev, reps: int = 5) -> dict:
     val = torch.empty((3, (n + 15) // 16 * 16), dtype=torch.float32, device=dev)
     ms_feat = _events_ms(lambda: ops.features(ab, SPADL_DEFAULT, 3, out=fbits), reps)
     ms_tree = _events_ms(lambda: models[0].predict_blocks(fbits, out=ps), reps)
+    # VAEP.rate's default for xgboost learners: the split conditions evaluated in the feature
+    # passes (sa_vaep_features_conditions), both walks over bitmaps only
+    from socceraction_amd import trees as T
+    ms_cond = _events_ms(lambda: T.predict_pair_conditions(ab, out.plan, models), reps)
     f64bits = ops.features(ab, SPADL_DEFAULT, 3, num_tile=out.Rn, bool_bits=True)
     ms_feat64 = _events_ms(lambda: ops.features(ab, SPADL_DEFAULT, 3, out=f64bits), reps)
     ms_tree64 = _events_ms(lambda: models[0].predict_blocks(f64bits, out=ps), reps)
@@ -386,6 +390,8 @@ def rate_extra(ab, out, n, dev, reps: int = 5) -> dict:
                         'depth 3) + formula (float32 probabilities), cfg2 actions',
             'method': 'staged condition walk (sa_tree_predict_staged) over the bitmaps and the '
                       'float32 numeric blocks',
+            'ms_features_and_both_models_conditions': round(ms_cond, 4),
+            'ms_rate_total_conditions': round(ms_cond + ms_formula, 4),
             'ms_features_bitmap_form': round(ms_feat, 4), 'ms_per_model': round(ms_tree, 4),
             'ms_features_bitmap_f64_form': round(ms_feat64, 4),
             'ms_per_model_f64_numeric': round(ms_tree64, 4),

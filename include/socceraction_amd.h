@@ -160,6 +160,20 @@ int sa_vaep_features_bits_f32(const sa_actions* a, const sa_feature_plan* plan, 
                               int64_t bits_stride, int32_t n_bool_cols, const sa_block* f32_out,
                               const sa_block* i32f_out, void* stream);
 
+/* VAEP.rate's features for xgboost learners as CONDITION bitmaps: bitmap rows [0, n_bool_cols)
+ * = the bool features (as sa_vaep_features_bits), rows n_bool_cols + c = split condition c of
+ * the learners (bit set = goes right: xgboost's float32 `x < thr` goes left, NaN follows
+ * cond_dl[c]); the numeric columns are evaluated in the numeric pass and never written.
+ * Condition c belongs to f64 column j for cond_fstart[j] <= c < cond_fstart[j+1] (j < n_f64_cols)
+ * or i64 column j for cond_istart[j] <= c < cond_istart[j+1]; bits 16-byte aligned, bits_stride
+ * a multiple of 16 bytes >= 16 * ceil(n / 128).  k <= 3.  The staged walk then reads every
+ * condition from these bitmaps (sa_tree_predict_staged with n_num = 0). */
+int sa_vaep_features_conditions(const sa_actions* a, const sa_feature_plan* plan, uint8_t* bits,
+                                int64_t bits_stride, int32_t n_bool_cols, int32_t n_f64_cols,
+                                int32_t n_i64_cols, const int32_t* cond_fstart,
+                                const int32_t* cond_istart, const float* cond_thr,
+                                const int32_t* cond_dl, int32_t n_cond, void* stream);
+
 /* goalscore alone (vaep/features.py:505-539; atomic/vaep/features.py:229-260): writes the
  * goalscore_team / _opponent / _diff columns col, col+1, col+2 of the i64 block (one wave per
  * segment).  sa_vaep_features computes the columns inside its numeric pass in windowed mode

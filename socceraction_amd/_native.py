@@ -122,6 +122,9 @@ _SIGNATURES = {
     'sa_vaep_features_bits_f32': (ctypes.c_int, [ctypes.POINTER(SaActions), ctypes.POINTER(SaFeaturePlan),
                                                  _p, ctypes.c_int64, ctypes.c_int32, ctypes.POINTER(SaBlock),
                                                  ctypes.POINTER(SaBlock), _p]),
+    'sa_vaep_features_conditions': (ctypes.c_int, [ctypes.POINTER(SaActions), ctypes.POINTER(SaFeaturePlan),
+                                                   _p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
+                                                   ctypes.c_int32, _p, _p, _p, _p, ctypes.c_int32, _p]),
     'sa_vaep_features_xt': (ctypes.c_int, [ctypes.POINTER(SaActions),
                                            ctypes.POINTER(SaFeaturePlan), ctypes.POINTER(SaBlock),
                                            ctypes.POINTER(SaBlock), ctypes.POINTER(SaBlock),

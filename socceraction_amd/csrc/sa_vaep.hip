@@ -69,8 +69,48 @@ struct FeatArgs {
   const double *ps, *pc;
   double *off, *def, *val;
   bool vec_ok;
+  // optional (sa_vaep_features_conditions): the numeric columns become split-condition bitmaps
+  const int32_t *cond_fstart, *cond_istart;  // [Cf + 1], [Ci + 1]: conditions of each column
+  const float* cond_thr;                     // per condition: float32 threshold (`x < thr` goes left)
+  const int32_t* cond_dl;                    // per condition: NaN goes left
+  int32_t cond_row0;                         // bitmap row of condition 0 (after the bool columns)
 };
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// COND mode of the numeric pass: a store of column `col` (rows jb, jb+1 of the lane) evaluates
+// that column's split conditions of a learner instead -- bit = goes right, xgboost's float32
+// compare (`x < thr` left, NaN -> default) -- and the wave's 128 bits of each condition go to
+// bitmap row cond_row0 + c (Arrow layout).  Both learners of VAEP.rate read these bitmaps like
+// bool features, so the numeric values never reach HBM.
+struct CondSink {
+  const int32_t* start;
+  const float* thr;
+  const int32_t* dl;
+  uint16_t* bits;
+  int64_t stride16;  // u16 per bitmap row
+  int32_t row0;
+  int64_t wb, n;
+};
+
+__device__ __forceinline__ void cond_store(const CondSink* s, int64_t col, float x0, float x1) {
+  const int lane = threadIdx.x & 63;
+  const int64_t jb = s->wb + 2 * lane;
+  const bool v0 = jb < s->n, v1 = jb + 1 < s->n;
+  const int c0 = s->start[col], c1 = s->start[col + 1];
+  for (int c = c0; c < c1; ++c) {
+    const float thr = s->thr[c];
+    const bool dl = s->dl[c] != 0;
+    const bool r0 = isnan(x0) ? !dl : !(x0 < thr);
+    const bool r1 = isnan(x1) ? !dl : !(x1 < thr);
+    // the 16 row bits of each 8-lane group (rows 16g .. 16g+15 of the wave) by three xor
+    // shuffles; the group's first lane stores them: one 16-B run per wave and condition
+    uint32_t b = ((uint32_t)(v0 && r0) | ((uint32_t)(v1 && r1) << 1)) << (2 * (lane & 7));
+    b |= __shfl_xor(b, 1, 64);
+    b |= __shfl_xor(b, 2, 64);
+    b |= __shfl_xor(b, 4, 64);
+    if ((lane & 7) == 0) s->bits[(int64_t)(s->row0 + c) * s->stride16 + s->wb / 16 + (lane >> 3)] = (uint16_t)b;
+  }
+}
 
 // Workgroups are dispatched round-robin over the 8 XCDs (XCD = blockIdx % 8).  Writing the
 // output front to back in blockIdx order leaves every XCD's concurrent stores scattered over
@@ -220,6 +260,14 @@ __device__ __forceinline__ void st_i64x2(int64_t* __restrict__ base, int64_t col
   i64x2 v = {(long long)v0, (long long)v1};
   SA_DGUARD(col >= 0 && col < C, col, return);
   st16(base + col * R, v);
+}
+
+__device__ __forceinline__ void st_f64x2(CondSink* s, int64_t col, int64_t, int64_t, double v0, double v1) {
+  cond_store(s, col, (float)v0, (float)v1);
+}
+
+__device__ __forceinline__ void st_i64x2(CondSink* s, int64_t col, int64_t, int64_t, int64_t v0, int64_t v1) {
+  cond_store(s, col, (float)v0, (float)v1);
 }
 
 // float32 form of the numeric blocks (sa_vaep_features_bits_f32: what xgboost learners compare,
@@ -904,11 +952,12 @@ __device__ __forceinline__ void labels_pair(const sa_actions& A, int nr, uint8_t
 // KF = 3: windowed mode with nb_prev_actions <= 3.  The pair's rows jb-2 .. jb+1 are read
 // once (16-B loads) and the windows are formed in registers (see the loop below).
 // KF = 0: any mode / any k (explicit frames, k <= 8): per-window row loads.
-template <bool ATOMIC, bool EXPLICIT, int KF, bool TAIL = false, bool N32 = false>
+template <bool ATOMIC, bool EXPLICIT, int KF, bool TAIL = false, bool N32 = false, bool COND = false>
 __global__ __launch_bounds__(256) void num_features_kernel(FeatArgs args) {
-  // N32: the f64 and i64 blocks hold float32 values (sa_vaep_features_bits_f32)
-  using FT = typename std::conditional<N32, float, double>::type;
-  using IT = typename std::conditional<N32, float, int64_t>::type;
+  // N32: the f64 and i64 blocks hold float32 values (sa_vaep_features_bits_f32); COND: no blocks,
+  // the columns' split conditions as bitmaps (sa_vaep_features_conditions)
+  using FT = typename std::conditional<COND, CondSink, typename std::conditional<N32, float, double>::type>::type;
+  using IT = typename std::conditional<COND, CondSink, typename std::conditional<N32, float, int64_t>::type>::type;
   const int lane = threadIdx.x & (WAVE - 1);
   const int wv = threadIdx.x / WAVE;
   const sa_actions& A = args.a;
@@ -919,6 +968,18 @@ __global__ __launch_bounds__(256) void num_features_kernel(FeatArgs args) {
   const int64_t wave_base = (xcd_logical_block() * BLOCK_WAVES + wv) * WAVE_ACTS;
   const sa_frame& F0 = A.frames[0];
   if (wave_base >= n) return;  // whole wave past the end (uniform: the goalscore ballots need every lane)
+  CondSink sink_f{args.cond_fstart, args.cond_thr, args.cond_dl, args.bbits, args.bstride, args.cond_row0,
+                  wave_base, n};
+  CondSink sink_i{args.cond_istart, args.cond_thr, args.cond_dl, args.bbits, args.bstride, args.cond_row0,
+                  wave_base, n};
+  auto fblock = [&](int64_t j) -> FT* {
+    if constexpr (COND) return &sink_f;
+    else return reinterpret_cast<FT*>(args.fout) + tile_off(j, 0, args.Cf, Rf);
+  };
+  auto iblock = [&](int64_t j) -> IT* {
+    if constexpr (COND) return &sink_i;
+    else return reinterpret_cast<IT*>(args.iout) + tile_off(j, 0, args.Ci, Ri);
+  };
   SegCursor cur = {0, 0, 0};
   const int gcol = EXPLICIT ? -1 : P.i64_col[SA_XFN_GOALSCORE];
   if (!EXPLICIT) {
@@ -927,7 +988,7 @@ __global__ __launch_bounds__(256) void num_features_kernel(FeatArgs args) {
     seg_advance(A, cur, jl);
     if (gcol >= 0)
       goalscore_pair<ATOMIC, IT>(A, wave_base, wave_base + 2 * lane, cur,
-                                 reinterpret_cast<IT*>(args.iout) + tile_off(jl & ~(int64_t)1, 0, args.Ci, Ri),
+                                 iblock(jl & ~(int64_t)1),
                                  gcol, (int)args.Ci, Ri);
     if (TAIL) {  // labels + formula of the same rows (every lane of the wave present)
       labels_pair<ATOMIC>(A, args.nr, args.sc, args.co, args.gfs, wave_base + 2 * lane, cur);
@@ -962,8 +1023,8 @@ __global__ __launch_bounds__(256) void num_features_kernel(FeatArgs args) {
   for (int pr = 0; pr < NUM_PAIRS; ++pr) {
     const int64_t jb = wave_base + pr * 2 * WAVE + 2 * lane;
     if (jb >= n) break;
-    FT* fb = reinterpret_cast<FT*>(args.fout) + tile_off(jb, 0, args.Cf, Rf);  // column 0 of rows jb, jb+1
-    IT* ib = reinterpret_cast<IT*>(args.iout) + tile_off(jb, 0, args.Ci, Ri);
+    FT* fb = fblock(jb);  // column 0 of rows jb, jb+1 (COND: the condition sinks)
+    IT* ib = iblock(jb);
     int64_t jr[2];
     int dd[2];
     bool away[2];
@@ -1500,7 +1561,7 @@ static int launch_features(const sa_actions* a, const sa_feature_plan* plan, con
                            const sa_block* f64_out, const sa_block* i64_out, int32_t xt_l,
                            int32_t xt_w, uint32_t* xt_cells, void* stream, uint8_t* bits = nullptr,
                            int64_t bits_stride = 0, int32_t n_bits = 0, const TailArgs* tail = nullptr,
-                           bool num32 = false);
+                           bool num32 = false, const FeatArgs* cond = nullptr);
 
 extern "C" int sa_vaep_features(const sa_actions* a, const sa_feature_plan* plan,
                                 const sa_block* bool_out, const sa_block* f64_out,
@@ -1546,6 +1607,31 @@ extern "C" int sa_vaep_features_bits_f32(const sa_actions* a, const sa_feature_p
                          n_bool_cols, nullptr, true);
 }
 
+extern "C" int sa_vaep_features_conditions(const sa_actions* a, const sa_feature_plan* plan, uint8_t* bits,
+                                           int64_t bits_stride, int32_t n_bool_cols, int32_t n_f64_cols,
+                                           int32_t n_i64_cols, const int32_t* cond_fstart,
+                                           const int32_t* cond_istart, const float* cond_thr,
+                                           const int32_t* cond_dl, int32_t n_cond, void* stream) {
+  if (!a) return fail(SA_EINVAL, "null sa_actions");
+  if (a->n_frames != 1) return fail(SA_EINVAL, "condition bitmaps: windowed mode only");
+  if (!plan || plan->nb_prev_actions > 3) return fail(SA_EINVAL, "condition bitmaps: nb_prev_actions <= 3");
+  if (!bits || n_bool_cols < 1 || n_cond < 0 || n_f64_cols < 0 || n_i64_cols < 0 || bits_stride % 16 ||
+      bits_stride < 16 * ((a->n + 127) / 128) || !aligned16(bits))
+    return fail(SA_EINVAL, "condition bitmaps: 16-byte aligned rows of at least ceil(n/128)*16 bytes");
+  if (!cond_fstart || !cond_istart || (n_cond > 0 && (!cond_thr || !cond_dl)))
+    return fail(SA_EINVAL, "null condition table");
+  // stand-in descriptors: the numeric pass writes no block in this mode, only the bitmaps
+  const sa_block fz{bits, n_f64_cols, 0, 128}, iz{bits, n_i64_cols, 0, 128};
+  FeatArgs c{};
+  c.cond_fstart = cond_fstart;
+  c.cond_istart = cond_istart;
+  c.cond_thr = cond_thr;
+  c.cond_dl = cond_dl;
+  c.cond_row0 = n_bool_cols;
+  return launch_features(a, plan, nullptr, &fz, &iz, 0, 0, nullptr, stream, bits, bits_stride, n_bool_cols, nullptr,
+                         false, &c);
+}
+
 extern "C" int sa_vaep_step_f64(const sa_actions* a, const sa_feature_plan* plan, const sa_block* bool_out,
                                 const sa_block* f64_out, const sa_block* i64_out, int32_t xt_l, int32_t xt_w,
                                 uint32_t* xt_cells, int32_t nr_actions, uint8_t* scores, uint8_t* concedes,
@@ -1584,7 +1670,8 @@ extern "C" int sa_vaep_step_f64(const sa_actions* a, const sa_feature_plan* plan
 static int launch_features(const sa_actions* a, const sa_feature_plan* plan, const sa_block* bool_out,
                            const sa_block* f64_out, const sa_block* i64_out, int32_t xt_l,
                            int32_t xt_w, uint32_t* xt_cells, void* stream, uint8_t* bits,
-                           int64_t bits_stride, int32_t n_bits, const TailArgs* tail, bool num32) {
+                           int64_t bits_stride, int32_t n_bits, const TailArgs* tail, bool num32,
+                           const FeatArgs* cond) {
   int rc = check_actions(a, true);
   if (rc) return rc;
   if (!plan) return fail(SA_EINVAL, "null plan");
@@ -1647,7 +1734,12 @@ static int launch_features(const sa_actions* a, const sa_feature_plan* plan, con
                 tail ? tail->off : nullptr,
                 tail ? tail->def : nullptr,
                 tail ? tail->val : nullptr,
-                tail ? (aligned16(tail->ps) && aligned16(tail->pc)) : false};
+                tail ? (aligned16(tail->ps) && aligned16(tail->pc)) : false,
+                cond ? cond->cond_fstart : nullptr,
+                cond ? cond->cond_istart : nullptr,
+                cond ? cond->cond_thr : nullptr,
+                cond ? cond->cond_dl : nullptr,
+                cond ? cond->cond_row0 : 0};
   const dim3 grid(xcd_grid((a->n + BLOCK_ACTS - 1) / BLOCK_ACTS)), block(BLOCK_WAVES * WAVE);
   const bool expl = a->n_frames > 1;
   if (wb) {  // one wave per (tile, group of ~32 columns), XCD-contiguous sweep order
@@ -1677,7 +1769,12 @@ static int launch_features(const sa_actions* a, const sa_feature_plan* plan, con
   const int gc = plan->i64_col[SA_XFN_GOALSCORE];
   if (wn || xt_cells || tail || (gc >= 0 && !expl)) {  // windowed mode: goalscore fused into this pass
     const bool fast = !expl && K <= 3;  // register-resident windows (KF = 3)
-    if (num32) {  // windowed, K <= 3 (checked by sa_vaep_features_bits_f32)
+    if (cond) {  // windowed, K <= 3 (checked by sa_vaep_features_conditions)
+      if (a->atomic)
+        hipLaunchKernelGGL((num_features_kernel<true, false, 3, false, false, true>), grid, block, 0, st, args);
+      else
+        hipLaunchKernelGGL((num_features_kernel<false, false, 3, false, false, true>), grid, block, 0, st, args);
+    } else if (num32) {  // windowed, K <= 3 (checked by sa_vaep_features_bits_f32)
       if (a->atomic)
         hipLaunchKernelGGL((num_features_kernel<true, false, 3, false, true>), grid, block, 0, st, args);
       else

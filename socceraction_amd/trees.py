@@ -334,6 +334,78 @@ class TreeEnsemble:
         return out[:n]
 
 
+def _conditions_prep(plan, models: Sequence[TreeEnsemble], dev) -> dict:
+    """Device tables of predict_pair_conditions for these learners on blocks of ``plan``, cached
+    on the first learner (the entry holds the learners themselves, compared by identity)."""
+    key = (tuple(plan.names), plan.n_bool, plan.n_f64, plan.n_i64, str(dev))
+    cache = getattr(models[0], '_cond_cache', None)
+    if cache is not None and cache['key'] == key and len(cache['models']) == len(models) and \
+            all(a is b for a, b in zip(cache['models'], models)):
+        return cache
+    slots = [m.feature_slots(plan) for m in models]
+    lay = staged_layout(models, slots)
+    nb = plan.n_bool
+    num_slots = lay['num_slots'].astype(np.int64)
+    n_num = len(num_slots)
+    kind, col = num_slots >> 24, num_slots & 0xFFFFFF
+    fstart = np.searchsorted(np.where(kind == 1, col, 1 << 30), np.arange(plan.n_f64 + 1), 'left')
+    istart = np.count_nonzero(kind == 1) + np.searchsorted(col[kind == 2], np.arange(plan.n_i64 + 1), 'left')
+    t = lambda v, dt: torch.from_numpy(np.ascontiguousarray(v, dt)).to(dev)  # noqa: E731
+    bool_cols = np.concatenate([lay['bool_cols'], nb + np.arange(n_num)]).astype(np.int32)
+    walks = []
+    for m, ml in zip(models, lay['models']):
+        n_cond = 1 + len(bool_cols)
+        lds = _native.lib().sa_tree_staged_lds_bytes(len(ml['nodes']), n_cond, 1)
+        if lds > 160 * 1024 or n_cond > 65536 or len(ml['nodes']) >= 65536:
+            raise ValueError('the staged form of this model does not fit LDS')
+        walks.append((t(ml['nodes'].view(np.int32), np.int32), t(ml['leaf'], np.float32),
+                      t(ml['roots'], np.int32), m._device(dev)['depth']))
+    cache = {'key': key, 'models': list(models), 'n_num': n_num, 'fstart': t(fstart, np.int32),
+             'istart': t(istart, np.int32),
+             'thr': t(lay['num_thr'] if n_num else np.zeros(1), np.float32),
+             'dl': t(lay['num_dl'] if n_num else np.zeros(1), np.int32),
+             'bool_cols': t(bool_cols, np.int32) if len(bool_cols) else None, 'n_cond_bool': len(bool_cols),
+             'walks': walks}
+    models[0]._cond_cache = cache
+    return cache
+
+
+def predict_pair_conditions(batch, plan, models: Sequence[TreeEnsemble], flip: bool = True):
+    """``VAEP.rate``'s xgboost learners on ``batch`` through condition bitmaps: the union of
+    their split conditions is evaluated inside the feature passes (``sa_vaep_features_conditions``:
+    bool features and numeric split outcomes as bitmaps, the numeric values never written), then
+    each learner's staged walk reads every condition as a bitmap (``sa_tree_predict_staged``,
+    n_num = 0).  The same float32 probabilities as :meth:`TreeEnsemble.predict_blocks`, bit for
+    bit.  Raises ValueError when a learner is not float32 (xgboost) or its walk does not fit LDS."""
+    from .batch import stream_handle
+    if not all(m.f32 and not m.le for m in models):
+        raise ValueError('condition bitmaps are for xgboost (float32, `<`) learners')
+    dev = batch.device
+    prep = _conditions_prep(plan, models, dev)
+    n, nb, n_num = batch.n, plan.n_bool, prep['n_num']
+    words = max(2, -(-n // 128) * 2)  # int64 words per row: a whole number of 16-B runs
+    bits = torch.empty((nb + n_num, words), dtype=torch.int64, device=dev)
+    s = batch.struct(flip=flip)
+    _native.check(_native.lib().sa_vaep_features_conditions(
+        ctypes.byref(s), ctypes.byref(plan.struct), bits.data_ptr(), words * 8, max(nb, 1), plan.n_f64,
+        plan.n_i64, prep['fstart'].data_ptr(), prep['istart'].data_ptr(), prep['thr'].data_ptr(),
+        prep['dl'].data_ptr(), n_num, stream_handle()))
+    z = _native.SaBlock()
+    z.data, z.n_cols, z.tile_rows = None, 0, 16
+    bc = prep['bool_cols']
+    outs = []
+    for m, (nodes, leaf, roots, depth) in zip(models, prep['walks']):
+        out = torch.empty(max(n, 1), dtype=torch.float32, device=dev)
+        rec = _native.SaTreeModel(nodes.data_ptr(), leaf.data_ptr(), roots.data_ptr(), depth.data_ptr(),
+                                  nodes.numel(), m.n_trees, float(m.base_margin), out.data_ptr())
+        _native.check(_native.lib().sa_tree_predict_staged(
+            ctypes.byref(rec), bc.data_ptr() if bc is not None else None, prep['n_cond_bool'], None, None,
+            0, None, None, 0, ctypes.byref(z), bits.data_ptr(), words * 8, ctypes.byref(z), ctypes.byref(z),
+            n, 0, 1, stream_handle()))
+        outs.append(out[:n])
+    return outs
+
+
 def staged_layout(models: Sequence[TreeEnsemble], slots: Sequence[np.ndarray]) -> dict:
     """The staged condition walk's conditions for models evaluated on the same blocks -- 0 never
     set, then the used bool columns, then the distinct numeric (slot, threshold, default

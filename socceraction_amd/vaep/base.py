@@ -279,16 +279,25 @@ class VAEP:
         known, _ = self._split_xfns()
         # the learners read the bool features as bitmaps (64 instead of 515 B/action written);
         # xgboost learners compare float32 values, so their numeric features are written and
-        # staged in float32 (half the bytes, the same probabilities bit for bit)
+        # staged in float32 (half the bytes, the same probabilities bit for bit); better still,
+        # their split conditions are evaluated in the numeric pass and only bitmaps are written
         n32 = self.nb_prev_actions <= 3 and all(t.f32 for t in trees.values())
-        fb = ops.features(ab, known, self.nb_prev_actions, bool_bits=True, num32=n32)
-        try:
-            ps = trees['scores'].predict_blocks(fb)
-            pc = trees['concedes'].predict_blocks(fb)
-        except ValueError:
-            if not n32:
-                raise
-            # a learner whose staged form does not fit LDS: the gather walk reads float64 blocks
+        ps = pc = None
+        if n32 and not any(t.le for t in trees.values()):  # xgboost learners: their split conditions evaluated inside the feature passes
+            from ..trees import predict_pair_conditions
+            try:
+                plan = ops.build_plan(known, self.nb_prev_actions, ab.atomic)
+                ps, pc = predict_pair_conditions(ab, plan, [trees['scores'], trees['concedes']])
+            except ValueError:
+                ps = pc = None
+        if ps is None and n32:  # float32 numeric blocks, the staged walk over them
+            fb = ops.features(ab, known, self.nb_prev_actions, bool_bits=True, num32=True)
+            try:
+                ps = trees['scores'].predict_blocks(fb)
+                pc = trees['concedes'].predict_blocks(fb)
+            except ValueError:
+                ps = pc = None
+        if ps is None:  # a learner whose staged form does not fit LDS: the gather walk, float64 blocks
             fb = ops.features(ab, known, self.nb_prev_actions, bool_bits=True)
             ps = trees['scores'].predict_blocks(fb)
             pc = trees['concedes'].predict_blocks(fb)
