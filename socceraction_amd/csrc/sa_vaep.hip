@@ -82,6 +82,16 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 // compare (`x < thr` left, NaN -> default) -- and the wave's 128 bits of each condition go to
 // bitmap row cond_row0 + c (Arrow layout).  Both learners of VAEP.rate read these bitmaps like
 // bool features, so the numeric values never reach HBM.
+// The wave's outcome of condition c is two ballots (rows wb + 2l and wb + 2l + 1 of lane l); lane
+// c % 64 of the wave keeps them until the wave moves to another chunk of 64 conditions, then
+// every holding lane interleaves its pair into the 128-bit run of its bitmap row and stores it
+// in one 16-B store: one store instruction per chunk instead of one per condition.
+struct CondAcc {
+  uint64_t even, odd;  // this lane's condition (chunk + lane): ballots over even / odd rows
+  uint64_t held;       // uniform: lanes holding a condition of the chunk
+  int32_t chunk;       // uniform: first condition of the chunk
+};
+
 struct CondSink {
   const int32_t* start;
   const float* thr;
@@ -90,25 +100,58 @@ struct CondSink {
   int64_t stride16;  // u16 per bitmap row
   int32_t row0;
   int64_t wb, n;
+  CondAcc* acc;
 };
 
+__device__ __forceinline__ uint64_t spread32(uint32_t v) {  // bit i -> bit 2i
+  uint64_t x = v;
+  x = (x | (x << 16)) & 0x0000FFFF0000FFFFull;
+  x = (x | (x << 8)) & 0x00FF00FF00FF00FFull;
+  x = (x | (x << 4)) & 0x0F0F0F0F0F0F0F0Full;
+  x = (x | (x << 2)) & 0x3333333333333333ull;
+  x = (x | (x << 1)) & 0x5555555555555555ull;
+  return x;
+}
+
+__device__ __forceinline__ void cond_flush(const CondSink* s) {
+  CondAcc* a = s->acc;
+  const int lane = threadIdx.x & 63;
+  if ((a->held >> lane) & 1) {
+    const uint64_t lo = spread32((uint32_t)a->even) | (spread32((uint32_t)a->odd) << 1);
+    const uint64_t hi = spread32((uint32_t)(a->even >> 32)) | (spread32((uint32_t)(a->odd >> 32)) << 1);
+    uint4* dst = reinterpret_cast<uint4*>(s->bits + (int64_t)(s->row0 + a->chunk + lane) * s->stride16 + s->wb / 16);
+    *dst = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+  }
+  a->held = 0;
+}
+
 __device__ __forceinline__ void cond_store(const CondSink* s, int64_t col, float x0, float x1) {
+  CondAcc* a = s->acc;
   const int lane = threadIdx.x & 63;
   const int64_t jb = s->wb + 2 * lane;
-  const bool v0 = jb < s->n, v1 = jb + 1 < s->n;
+  // per column: the rows present and the NaN rows as wave masks; per condition two compares,
+  // the rest is scalar (`!(x < thr)` is true for NaN: right unless NaN goes left)
+  const uint64_t ok0 = __ballot(jb < s->n), ok1 = __ballot(jb + 1 < s->n);
+  const uint64_t nan0 = __ballot(isnan(x0)), nan1 = __ballot(isnan(x1));
   const int c0 = s->start[col], c1 = s->start[col + 1];
   for (int c = c0; c < c1; ++c) {
     const float thr = s->thr[c];
     const bool dl = s->dl[c] != 0;
-    const bool r0 = isnan(x0) ? !dl : !(x0 < thr);
-    const bool r1 = isnan(x1) ? !dl : !(x1 < thr);
-    // the 16 row bits of each 8-lane group (rows 16g .. 16g+15 of the wave) by three xor
-    // shuffles; the group's first lane stores them: one 16-B run per wave and condition
-    uint32_t b = ((uint32_t)(v0 && r0) | ((uint32_t)(v1 && r1) << 1)) << (2 * (lane & 7));
-    b |= __shfl_xor(b, 1, 64);
-    b |= __shfl_xor(b, 2, 64);
-    b |= __shfl_xor(b, 4, 64);
-    if ((lane & 7) == 0) s->bits[(int64_t)(s->row0 + c) * s->stride16 + s->wb / 16 + (lane >> 3)] = (uint16_t)b;
+    uint64_t m0 = __ballot(!(x0 < thr)) & ok0, m1 = __ballot(!(x1 < thr)) & ok1;
+    if (dl) {
+      m0 &= ~nan0;
+      m1 &= ~nan1;
+    }
+    if ((c & ~63) != a->chunk) {
+      if (a->held) cond_flush(s);
+      a->chunk = c & ~63;
+    }
+    const int k = c & 63;  // the holding lane
+    if (lane == k) {
+      a->even = m0;
+      a->odd = m1;
+    }
+    a->held |= 1ull << k;
   }
 }
 
@@ -844,7 +887,7 @@ __device__ __forceinline__ void goalscore_pair(const sa_actions& A, int64_t wb, 
     v[1][e] = op;
     v[2][e] = tm - op;
   }
-  if (jb < n) {
+  if (jb < n || std::is_same<IT, CondSink>::value) {  // condition sinks: the whole wave, tail rows masked
 #pragma unroll
     for (int k = 0; k < 3; ++k) st_i64x2(ib, gcol + k, ni, Ri, v[k][0], v[k][1]);
   }
@@ -968,10 +1011,11 @@ __global__ __launch_bounds__(256) void num_features_kernel(FeatArgs args) {
   const int64_t wave_base = (xcd_logical_block() * BLOCK_WAVES + wv) * WAVE_ACTS;
   const sa_frame& F0 = A.frames[0];
   if (wave_base >= n) return;  // whole wave past the end (uniform: the goalscore ballots need every lane)
+  CondAcc acc{0, 0, 0, -64};
   CondSink sink_f{args.cond_fstart, args.cond_thr, args.cond_dl, args.bbits, args.bstride, args.cond_row0,
-                  wave_base, n};
+                  wave_base, n, &acc};
   CondSink sink_i{args.cond_istart, args.cond_thr, args.cond_dl, args.bbits, args.bstride, args.cond_row0,
-                  wave_base, n};
+                  wave_base, n, &acc};
   auto fblock = [&](int64_t j) -> FT* {
     if constexpr (COND) return &sink_f;
     else return reinterpret_cast<FT*>(args.fout) + tile_off(j, 0, args.Cf, Rf);
@@ -999,7 +1043,9 @@ __global__ __launch_bounds__(256) void num_features_kernel(FeatArgs args) {
       }
     }
   }
-  if (wave_base + 2 * lane >= n) return;
+  // COND: every lane stays (the ballots and the chunk stores need the whole wave); lanes past the
+  // end recompute the last pair and their bits are masked off in cond_store
+  if (!COND && wave_base + 2 * lane >= n) return;
   NumCols C;
   C.at = P.i64_col[SA_XFN_ACTIONTYPE];
   C.re = P.i64_col[SA_XFN_RESULT];
@@ -1021,7 +1067,8 @@ __global__ __launch_bounds__(256) void num_features_kernel(FeatArgs args) {
   C.ni = (int)args.Ci;
 
   for (int pr = 0; pr < NUM_PAIRS; ++pr) {
-    const int64_t jb = wave_base + pr * 2 * WAVE + 2 * lane;
+    int64_t jb = wave_base + pr * 2 * WAVE + 2 * lane;
+    if (COND && jb >= n) jb = (n - 1) & ~(int64_t)1;
     if (jb >= n) break;
     FT* fb = fblock(jb);  // column 0 of rows jb, jb+1 (COND: the condition sinks)
     IT* ib = iblock(jb);
@@ -1115,6 +1162,9 @@ __global__ __launch_bounds__(256) void num_features_kernel(FeatArgs args) {
         emit_window<ATOMIC, FT, IT>(C, i, w, sx0, sy0, t0, fb, ib, Rf, Ri);
       }
     }
+  }
+  if constexpr (COND) {
+    if (acc.held) cond_flush(&sink_f);
   }
 }
 
