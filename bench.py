@@ -129,6 +129,15 @@ def _reduce(dist, value, op, dev):
     return float(t.item())
 
 
+def allreduce_counts(dist, acc) -> None:
+    """The xT fit's one exchange: every rank's count buffers summed by ONE all-reduce (RCCL; a
+    gloo rehearsal sums the same buffer through host memory)."""
+    from socceraction_amd import shard
+    if dist is None:
+        return
+    shard.allreduce_xt_counts(acc)  # ONE all-reduce of the whole count allocation
+
+
 def xt_step(ab, dist, source: str = 'cells', cells=None, shared: bool = True, sync_solve: bool = False):
     """BASELINE cfg4 inside the step: xT 16x12 fit on the step's actions (count pass, RCCL
     all-reduce of the counts across ranks, value iteration to eps=1e-5; the solve synchronises
@@ -161,14 +170,7 @@ def xt_step(ab, dist, source: str = 'cells', cells=None, shared: bool = True, sy
     def reduce():
         if source == 'none':
             return
-        acc = state['acc']
-        if dist is not None and dist.get_backend() == 'nccl':
-            shard.allreduce_xt_counts(acc.shot, acc.goal, acc.move, acc.trans, acc.err)
-        elif dist is not None:  # gloo rehearsal: the same sum through host memory
-            for t in (acc.shot, acc.goal, acc.move, acc.trans):
-                h = t.cpu()
-                dist.all_reduce(h)
-                t.copy_(h)
+        allreduce_counts(dist, state['acc'])
 
     def start():
         count()
@@ -188,7 +190,156 @@ def xt_step(ab, dist, source: str = 'cells', cells=None, shared: bool = True, sy
             ops.xt_rate(ab, sol.mats[3].reshape(12, 16), 16, 12)
         state['sol'] = sol
     start.count, start.reduce, start.zero = count, reduce, zero
+    state['acc_buf'], state['rate'] = acc0, rate_out  # the parity check reads the last step's
     return start, finish, state
+
+
+class Parity:
+    """The line's own correctness check, OUTSIDE the timed region: the timed step's output
+    buffers for sampled games against the numpy oracle (the checker; never the thing measured).
+    Bit-exact for bools, ints, counts, iteration counts and the xT surface; floats within
+    |a - b| <= 1e-6 |ref| + 1e-12 (north_star's bar), NaN / inf in the same places."""
+
+    def __init__(self):
+        self.ok, self.max_rel_err, self.failures, self.games, self.values = True, 0.0, [], 0, 0
+
+    def _fail(self, what: str) -> None:
+        self.ok = False
+        if len(self.failures) < 20:
+            self.failures.append(what)
+
+    def exact(self, name: str, got, ref) -> None:
+        got, ref = np.asarray(got), np.asarray(ref)
+        self.values += ref.size
+        if got.shape != ref.shape or not np.array_equal(got.astype(np.int64), ref.astype(np.int64)):
+            self._fail(name)
+
+    def close(self, name: str, got, ref) -> None:
+        a, b = np.asarray(got, np.float64), np.asarray(ref, np.float64)
+        self.values += b.size
+        if a.shape != b.shape or (np.isnan(a) != np.isnan(b)).any():
+            return self._fail(name + ' (shape / NaN pattern)')
+        fin = np.isfinite(b)
+        if (a[~fin & ~np.isnan(b)] != b[~fin & ~np.isnan(b)]).any():
+            return self._fail(name + ' (inf)')
+        err = np.abs(a[fin] - b[fin])
+        if err.size:
+            rel = err / np.maximum(np.abs(b[fin]), 1e-300)
+            self.max_rel_err = max(self.max_rel_err, float(np.max(np.where(err == 0, 0.0, rel))))
+            if (err > 1e-6 * np.abs(b[fin]) + 1e-12).any():
+                self._fail(name)
+
+    def merge(self, dist, dev) -> None:
+        """Every rank checked its own games: the line reports the worst rank."""
+        if dist is None:
+            return
+        bad = _reduce(dist, 0.0 if self.ok else 1.0, dist.ReduceOp.MAX, dev)
+        self.max_rel_err = _reduce(dist, self.max_rel_err, dist.ReduceOp.MAX, dev)
+        self.games = int(_reduce(dist, self.games, dist.ReduceOp.SUM, dev))
+        self.values = int(_reduce(dist, self.values, dist.ReduceOp.SUM, dev))
+        if bad and self.ok:
+            self._fail('another rank')
+
+    def record(self) -> dict:
+        return {'games': self.games, 'values_checked': self.values, 'ok': self.ok,
+                'max_rel_err': float(f'{self.max_rel_err:.3e}'), 'failures': self.failures,
+                'oracle': 'oracle/vaep_oracle.py, oracle/xt_oracle.py (numpy restatement pinned '
+                          'by reference goldens), outside the timed region'}
+
+
+SPADL_COLS = ('period_id', 'time_seconds', 'team_id', 'start_x', 'start_y', 'end_x', 'end_y',
+              'type_id', 'result_id', 'bodypart_id')
+ATOMIC_COLS = ('period_id', 'time_seconds', 'team_id', 'x', 'y', 'dx', 'dy', 'type_id',
+               'bodypart_id')
+
+
+def sample_games(n_games: int, k: int = 12, seed: int = 2026) -> list:
+    """The checked games: the first, the last and k - 2 seeded random ones."""
+    if n_games <= k:
+        return list(range(n_games))
+    rest = np.random.default_rng(seed).choice(np.arange(1, n_games - 1), k - 2, replace=False)
+    return [0, n_games - 1] + sorted(int(g) for g in rest)
+
+
+def check_vaep(par: Parity, d, out, scores, concedes, val, probs, atomic: bool = False,
+               games=None) -> None:
+    """Features (every column), labels and (when ``val``) the f64 formula of sampled games of
+    the batch ``d`` in the device buffers vs the oracle, per game as the reference's
+    compute_features / compute_labels / formula.value (vaep/base.py:97-137, formula.py:116-151)."""
+    from oracle import vaep_oracle as vo
+    off = d['game_off']
+    xfns = vo.ATOMIC_DEFAULT if atomic else vo.SPADL_DEFAULT
+    for g in (sample_games(len(off) - 1) if games is None else games):
+        s, e = int(off[g]), int(off[g + 1])
+        cols = {c: d[c][s:e] for c in (ATOMIC_COLS if atomic else SPADL_COLS)}
+        ref = vo.features(cols, 3, xfns, atomic=atomic, home=[d['home_team_id'][g]])
+        if [r[0] for r in ref] != out.plan.names:
+            par._fail(f'game {g}: column names')
+            continue
+        blocks = {k: out.rows(k, s, e).cpu().numpy() for k in 'bfi'}
+        for (name, kind, col), (_, _, rv) in zip(out.plan.order, ref):
+            (par.close if kind == 'f' else par.exact)(f'game {g} {name}', blocks[kind][col], rv)
+        lab = vo.labels(cols, atomic=atomic)
+        par.exact(f'game {g} scores', scores[s:e].cpu().numpy().astype(bool), lab['scores'])
+        par.exact(f'game {g} concedes', concedes[s:e].cpu().numpy().astype(bool), lab['concedes'])
+        if val is not None:
+            fo = vo.formula(cols, probs['scores'][s:e], probs['concedes'][s:e], atomic=atomic)
+            v = val[:, s:e].cpu().numpy()
+            for r, c in enumerate(('offensive_value', 'defensive_value', 'vaep_value')):
+                par.close(f'game {g} {c}', v[r], fo[c])
+        par.games += 1
+
+
+def oracle_counts(d, l: int, w: int, dist=None, dev=None, acc: dict = None) -> dict:
+    """The oracle's xT counts of the batch ``d`` (added to ``acc`` when given), summed over the
+    ranks when ``dist`` (the same exchange the device counts go through)."""
+    from oracle import xt_oracle as xo
+    cnt = xo.counts({c: d[c] for c in ('start_x', 'start_y', 'end_x', 'end_y', 'type_id',
+                                        'result_id')}, l, w) if d is not None else None
+    if acc is not None and cnt is not None:
+        cnt = {k: acc[k] + cnt[k] for k in cnt}
+    elif cnt is None:
+        cnt = acc
+    if dist is not None:
+        on_dev = dist.get_backend() == 'nccl'
+        for k in cnt:
+            t = torch.from_numpy(np.ascontiguousarray(cnt[k])).to(dev if on_dev else 'cpu')
+            dist.all_reduce(t)
+            cnt[k] = t.cpu().numpy()
+    return cnt
+
+
+def check_xt(par: Parity, cnt: dict, acc, xT_dev, n_iter: int, l: int, w: int) -> np.ndarray:
+    """xT fit (xthreat.py:322-345): the counts the device solved from (all ranks' counts after
+    the all-reduce) == the oracle's counts of the same actions, bit for bit; the device surface
+    and iteration count == the oracle's value iteration over them (xthreat.py:278-320), bit for
+    bit. Returns the oracle surface."""
+    from oracle import xt_oracle as xo
+    tag = f'xT {l}x{w}'
+    for k, t in (('shot', acc.shot), ('goal', acc.goal), ('move', acc.move)):
+        par.exact(f'{tag} {k} counts', t.cpu().numpy(), cnt[k].reshape(-1))
+    tr = acc.trans.cpu().numpy().astype(np.int64)
+    par.exact(f'{tag} transition counts', tr, cnt['trans'].reshape(-1))
+    fit = xo.solve(cnt, l, w)
+    par.exact(f'{tag} iterations', n_iter + 1, len(fit['heatmaps']))
+    got = xT_dev.cpu().numpy().reshape(w, l)
+    par.values += got.size
+    if not np.array_equal(got, fit['xT']):
+        par._fail(f'{tag} surface')
+    return fit['xT']
+
+
+def check_xt_rate(par: Parity, d, rate_dev, xT: np.ndarray, interp: bool = False,
+                  games=None) -> None:
+    """ExpectedThreat.rate (xthreat.py:408-465) of sampled games: the device values == the
+    oracle's rate on the same surface (NaN for every action but successful moves)."""
+    from oracle import xt_oracle as xo
+    off = d['game_off']
+    for g in (sample_games(len(off) - 1) if games is None else games):
+        s, e = int(off[g]), int(off[g + 1])
+        cols = {c: d[c][s:e] for c in ('start_x', 'start_y', 'end_x', 'end_y', 'type_id', 'result_id')}
+        par.close(f'xT rate game {g}', rate_dev[s:e].cpu().numpy(),
+                  xo.rate(cols, xT, use_interpolation=interp))
 
 
 ATOMIC_DEFAULT = ['actiontype', 'actiontype_onehot', 'bodypart', 'bodypart_onehot', 'time',
@@ -228,7 +379,7 @@ def _events_ms(fn, reps: int) -> float:
     return a.elapsed_time(b) / reps
 
 
-def atomic_extra(dist, rank, world, dev, games: int, reps: int = 5) -> dict:
+def atomic_extra(dist, rank, world, dev, games: int, reps: int = 5, check: bool = True) -> dict:
     """BASELINE cfg3 alongside the main line: Atomic-VAEP features (k=3, default xfns, 154
     columns) + labels of cfg3's ``games`` synthetic atomic games (10,000 ≈ 4.0e7 atomic
     actions), sharded by game over the ranks (this entry scales strongly)."""
@@ -244,6 +395,11 @@ def atomic_extra(dist, rank, world, dev, games: int, reps: int = 5) -> dict:
     def step():  # features + labels in two launches: the labels ride in the numeric pass
         ops.step_into(s, out, None, None, 10, lab, None)
     ms = _events_ms(step, reps)
+    par = Parity()
+    if check:  # the timed launches' own buffers: sampled atomic games vs the oracle
+        torch.cuda.synchronize()
+        check_vaep(par, d, out, lab.scores, lab.concedes, None, None, atomic=True)
+        par.merge(dist, dev)
     n, total, wall = ab.n, ab.n, ms
     if dist is not None:
         wall = _reduce(dist, ms, dist.ReduceOp.MAX, dev)
@@ -255,11 +411,13 @@ def atomic_extra(dist, rank, world, dev, games: int, reps: int = 5) -> dict:
             'atomic_actions_per_gpu': n, 'atomic_actions_total': total, 'scaling': 'strong',
             'ms_per_step': round(wall, 4),
             'atomic_actions_per_s': round(total / wall * 1e3, 1), 'bytes_per_action': bpa,
-            'frac_of_8TBs_per_gpu': round(bpa * n / ms * 1e-6 / HBM_PEAK_GBS, 4)}
+            'frac_of_8TBs_per_gpu': round(bpa * n / ms * 1e-6 / HBM_PEAK_GBS, 4),
+            **({'parity': par.record()} if check else {})}
 
 
 def xt105_extra(ab, dist, dev, sharded: bool = False, cfg5_games: int = 62500,
-                rank: int = 0, world: int = 1, step_games: int = 10000) -> dict:
+                rank: int = 0, world: int = 1, step_games: int = 10000, d=None,
+                check: bool = True) -> dict:
     """BASELINE cfg5 alongside the main line: xT 105x68 fit of cfg5's 62,500 games (≈1.0e8
     actions; split over the ranks, so this entry scales strongly) -- count pass over this
     rank's games, RCCL all-reduce of the 7140-cell count vectors and 204 MB transition counts,
@@ -270,15 +428,24 @@ def xt105_extra(ab, dist, dev, sharded: bool = False, cfg5_games: int = 62500,
     from socceraction_amd import shard
     l, w = 105, 68
     batches = [ab]
+    first = d  # host columns of the first batch (its rate is checked game by game)
+    # the oracle's counts of every batch, accumulated while the batches are generated (the
+    # host columns are not kept): the checker of the fit below
+    ocnt = oracle_counts(d, l, w) if check and d is not None else None
     if cfg5_games > 0:
         mine = cfg5_games // world + (1 if rank < cfg5_games % world else 0)
         batches = [ab] if mine >= step_games else []
+        if not batches:
+            first, ocnt = None, None
         left = mine - (step_games if batches else 0)
         gid = 10_000_000 + rank * (cfg5_games + 1)  # ids disjoint from the step's games
         while left > 0:
             c = min(left, step_games)
-            batches.append(B.ActionBatch.from_columns(synthetic.spadl_games(c, game_id0=gid),
-                                                      dev=dev))
+            dc = synthetic.spadl_games(c, game_id0=gid)
+            batches.append(B.ActionBatch.from_columns(dc, dev=dev))
+            if check:
+                ocnt = oracle_counts(dc, l, w, acc=ocnt)
+                first = dc if first is None else first
             gid += c
             left -= c
 
@@ -288,24 +455,43 @@ def xt105_extra(ab, dist, dev, sharded: bool = False, cfg5_games: int = 62500,
             for b in batches:
                 ops.xt_count(b, l, w, acc)
             mats, _, n_iter = shard.xt_solve_sharded(acc)
+            acc = None  # each rank holds only its row block of the transition counts
         else:  # one all-reduce of the counts, replicated solve
             acc = ops.xt_zero_counts(l, w, dev)
             for b in batches:
                 ops.xt_count(b, l, w, acc)
-            if dist is not None and dist.get_backend() == 'nccl':
-                shard.allreduce_xt_counts(acc.shot, acc.goal, acc.move, acc.trans, acc.err)
+            allreduce_counts(dist, acc)
             sol = ops.xt_solve(acc, transition=False)  # synchronises; ExpectedThreat.fit's
             mats, n_iter = sol.mats, sol.n_iter           # call above 1024 cells
-        grid = ops.xt_interp_grid(mats[3].reshape(w, l), l, w)
-        for b in batches:
-            ops.xt_rate(b, grid, 1050, 680)
-        return n_iter
+        # rate(use_interpolation=True): each action's two node values evaluated in place from
+        # the 105 x 68 surface (sa_xt_rate_interp), bit-identical to the 1050 x 680 grid gather
+        xT = mats[3].reshape(w, l)
+        rates = [ops.xt_rate_interp(b, xT, l, w, 1050, 680, axes=axes)[0] for b in batches]
+        return n_iter, acc, mats, rates
+    axes = ops.xt_interp_axes(l, w, dev)  # node positions (constants of the reference's grid)
     once()  # warm-up (allocator, first launches)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    n_iter = once()
+    n_iter, acc, mats, rates = once()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    par = Parity()
+    if check:  # the timed call's counts, surface, iterations and the first batch's rates
+        ocnt = oracle_counts(None, l, w, dist, dev, acc=ocnt)
+        if acc is None:  # row-sharded solve: the surface is checked, the counts are not held
+            from oracle import xt_oracle as xo
+            fit = xo.solve(ocnt, l, w)
+            xT = fit['xT']
+            par.exact('xT 105x68 iterations', n_iter + 1, len(fit['heatmaps']))
+            if not np.array_equal(mats[3].cpu().numpy().reshape(w, l), xT):
+                par._fail('xT 105x68 surface')
+        else:
+            xT = check_xt(par, ocnt, acc, mats[3], n_iter, l, w)
+        del ocnt
+        if first is not None:
+            check_xt_rate(par, first, rates[0], xT, interp=True)
+            par.games += len(sample_games(len(first['game_off']) - 1))
+        par.merge(dist, dev)
     n = sum(b.n for b in batches)
     total = n
     if dist is not None:
@@ -318,7 +504,8 @@ def xt105_extra(ab, dist, dev, sharded: bool = False, cfg5_games: int = 62500,
             'actions_per_gpu': n, 'actions_total': total, 'iterations': n_iter,
             'ms_fit_and_rate': round(dt * 1e3, 3), 'actions_per_s': round(total / dt, 1),
             'scaling': 'strong' if cfg5_games > 0 else 'weak',
-            'solve': 'row-sharded' if (sharded and dist is not None) else 'replicated'}
+            'solve': 'row-sharded' if (sharded and dist is not None) else 'replicated',
+            **({'parity': par.record()} if check else {})}
 
 
 def convert_extra(d, dist, dev, reps: int = 3) -> dict:
@@ -504,6 +691,9 @@ def main() -> None:
     ap.add_argument('--e2e-games', type=int, default=1000,
                     help='games of the end-to-end (pandas in -> pandas out) side entry (0: skip)')
     ap.add_argument('--no-cpu', action='store_true')
+    ap.add_argument('--no-check', action='store_true',
+                    help='dev A/B only: skip the parity check of the timed buffers (the line '
+                         'then carries no "parity" field)')
     ap.add_argument('--no-side', action='store_true',
                     help='skip the cfg3 (atomic) and cfg5 (xT 105x68) side measurements')
     ap.add_argument('--cfg5-games', type=int, default=62500,
@@ -794,18 +984,37 @@ def main() -> None:
     if dist:
         wall = _reduce(dist, wall, dist.ReduceOp.MAX, dev)
         total_actions = int(_reduce(dist, n, dist.ReduceOp.SUM, dev))
+    check = not args.no_check
+    par = Parity()
+    if check:  # outside the timed region: the last timed step's own buffers vs the oracle
+        tc = time.perf_counter()
+        check_vaep(par, d, out, lab_buf[0], lab_buf[1], val, p)
+        if base['xt'] in ('cells', 'codes', 'coords'):
+            sol = xt_last['sol']
+            cnt = oracle_counts(d, 16, 12, dist, dev)
+            xT_ref = check_xt(par, cnt, xt_last['acc_buf'], sol.mats[3], _iterations(sol), 16, 12)
+            check_xt_rate(par, d, xt_last['rate'], xT_ref)
+        par.merge(dist, dev)
+        check_s = time.perf_counter() - tc
     extra_side = {}
     if not args.no_side:
         extra_side['xt105_cfg5'] = xt105_extra(ab, dist, dev, args.xt_sharded, args.cfg5_games,
-                                               rank, world, args.games)
-        extra_side['atomic_cfg3'] = atomic_extra(dist, rank, world, dev, args.atomic_games)
+                                               rank, world, args.games, d=d, check=check)
+        extra_side['atomic_cfg3'] = atomic_extra(dist, rank, world, dev, args.atomic_games,
+                                                 check=check)
         extra_side['convert_to_atomic'] = convert_extra(d, dist, dev)
         extra_side['rate_on_device'] = rate_extra(ab, out, n, dev)
         if args.e2e_games > 0 and rank == 0:
             extra_side['end_to_end'] = e2e_extra(d, min(args.e2e_games, args.games))
+    side_ok = all(v.get('parity', {}).get('ok', True) for v in extra_side.values())
     if rank != 0:
         if dist:
             dist.destroy_process_group()
+        if not (par.ok and side_ok):
+            print(f'bench.py rank {rank}: PARITY FAILED: ' + json.dumps(
+                {'step': par.failures, **{k: v['parity']['failures'] for k, v in extra_side.items()
+                                          if 'parity' in v}}), file=sys.stderr)
+            raise SystemExit(3)
         return
     ms_per_step = wall / args.steps * 1e3
     value = total_actions * args.steps / wall
@@ -869,6 +1078,12 @@ def main() -> None:
                        'VAEP kernels on the main stream, xT solve + rate on a side stream without a '
                        'host round trip, pipelined: step k\'s xT work may finish during step k+1 (two '
                        'cell-code buffers); the timed region ends after every stream is synchronised')
+    if check:
+        line['parity'] = dict(par.record(), seconds=round(check_s, 2),
+                              what='the last timed step\'s buffers: every feature column, both '
+                                   'labels and the f64 formula of 12 sampled games per rank; the '
+                                   'xT 16x12 counts the step solved from, its surface and '
+                                   'iteration count, and its rate of the sampled games')
     line.update(extra_side)
     if not args.no_cpu and world == 1:  # the CPU comparator runs on rank 0 at N = 1 only
         line['cpu_baseline'] = cpu_baseline(d, args.cpu_seconds)
@@ -878,6 +1093,11 @@ def main() -> None:
     print(json.dumps(line), flush=True)
     if dist:
         dist.destroy_process_group()
+    if not (par.ok and side_ok):
+        print('bench.py: PARITY FAILED: ' + json.dumps(
+            {'step': par.failures, **{k: v['parity']['failures'] for k, v in extra_side.items()
+                                      if 'parity' in v}}), file=sys.stderr)
+        raise SystemExit(3)
 
 
 if __name__ == '__main__':

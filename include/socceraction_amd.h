@@ -229,10 +229,12 @@ int sa_vaep_step_f64(const sa_actions* a, const sa_feature_plan* plan, const sa_
  * trans[s*C+e] += successful moves s->e  (xthreat.py:40-67, 74-98, 144-218).
  * Accumulates into the caller's zeroed buffers (RCCL-reducible), C = l*w.
  * NaN start coordinates are dropped from shot/goal/move counts (`_count`); a
- * non-finite coordinate that the reference would cast to int64 sets a bit in
- * *err_flags (device int32): 1 = infinite shot start (scoring_prob, action_prob, fit raise),
- * 2 = infinite move start (action_prob, move_transition_matrix, fit raise), 8 = NaN move start
- * or non-finite move end (only move_transition_matrix and fit, which cast every move
+ * non-finite coordinate that the reference would cast to int64 sets a flag in
+ * *err_flags (device int32), ONE BYTE per flag so that the ranks' flags add up in the same
+ * sum all-reduce as the counts (<= 255 ranks; a flag is set when its byte is non-zero):
+ * 0x1 = infinite shot start (scoring_prob, action_prob, fit raise), 0x100 = infinite move
+ * start (action_prob, move_transition_matrix, fit raise), 0x10000 = NaN move start or
+ * non-finite move end (only move_transition_matrix and fit, which cast every move
  * coordinate, raise; such a move is left out of the transition counts). */
 int sa_xt_count(const sa_actions* a, int32_t l, int32_t w, int64_t* shot, int64_t* goal,
                 int64_t* move, int32_t* trans, int32_t* err_flags, void* stream);
@@ -320,6 +322,18 @@ int sa_xt_iterate_rows(const int32_t* cnt_rows, const int64_t* move, const doubl
 int sa_xt_interp_grid(const double* xT, const double* cx, const double* cy, int32_t l, int32_t w,
                       const double* xs, int32_t L, const double* ys, int32_t W, double* grid,
                       void* stream);
+
+/* ExpectedThreat.rate(use_interpolation=True) (xthreat.py:443-464) WITHOUT materialising the
+ * L x W surface: a successful move's start and end node values are evaluated per action from
+ * the (w x l) xT surface -- each node's bracket (i, tx) / (j, ty) tabulated once per call by the
+ * device function sa_xt_interp_grid uses, then its bilinear expression in the same order -- so
+ * out[] equals sa_xt_interp_grid(xT, cx, cy, l, w, xs, L, ys, W) + sa_xt_rate(..., L, W) bit for
+ * bit, NaN pattern and err_flags bit 4 included.  Reads 34 B and writes 8 B per action; the
+ * surface (w*l doubles) and the (L + W) node tables stay cache-resident.  Replaces the grid
+ * gather of `grid[w - 1 - yj, xi]` (xthreat.py:456-464). */
+int sa_xt_rate_interp(const sa_actions* a, const double* xT, const double* cx, const double* cy,
+                      int32_t l, int32_t w, const double* xs, int32_t L, const double* ys, int32_t W,
+                      double* out, int32_t* err_flags, void* stream);
 
 /* ExpectedThreat.rate (xthreat.py:408-465): out[j] = grid[W-1-yj(end), xi(end)] -
  * grid[W-1-yj(start), xi(start)] for successful moves, NaN otherwise.  A non-finite

@@ -51,25 +51,37 @@ def _safe_divide(a, b):
     return np.divide(a, b, out=np.zeros_like(a), where=b != 0)
 
 
-def fit(cols: Dict[str, np.ndarray], l: int = 16, w: int = 12, eps: float = 1e-5) -> dict:
+def counts(cols: Dict[str, np.ndarray], l: int = 16, w: int = 12) -> dict:
+    """The fit's integer counts (xthreat.py:74-218): shots, goals and moves per start cell,
+    moves per start cell for the transition rows, and the C x C successful-move counts
+    (int64). Counts of disjoint action sets add, so shards can be summed before ``solve``."""
     t, r = cols['type_id'], cols['result_id']
     sx, sy, ex, ey = cols['start_x'], cols['start_y'], cols['end_x'], cols['end_y']
     shot = t == 11
     goal = shot & (r == 1)
     move = (t == 0) | (t == 21) | (t == 1)
-    shotm = count(sx[shot], sy[shot], l, w)
-    goalm = count(sx[goal], sy[goal], l, w)
-    scoring = _safe_divide(goalm, shotm)
-    movem = count(sx[move], sy[move], l, w)
-    total = movem + shotm
-    pshot, pmove = _safe_divide(shotm, total), _safe_divide(movem, total)
     C = l * w
     s_cell = flat_indexes(sx[move], sy[move], l, w)
     e_cell = flat_indexes(ex[move], ey[move], l, w)
     succ = r[move] == 1
-    start_counts = np.bincount(s_cell, minlength=C).astype(np.float64)
-    tc = np.zeros((C, C), dtype=np.int64)
-    np.add.at(tc, (s_cell[succ], e_cell[succ]), 1)
+    tc = np.bincount(s_cell[succ] * C + e_cell[succ], minlength=C * C).astype(np.int64)
+    return dict(shot=count(sx[shot], sy[shot], l, w).astype(np.int64),
+                goal=count(sx[goal], sy[goal], l, w).astype(np.int64),
+                move=count(sx[move], sy[move], l, w).astype(np.int64),
+                start=np.bincount(s_cell, minlength=C).astype(np.int64),
+                trans=tc.reshape(C, C))
+
+
+def solve(cnt: dict, l: int = 16, w: int = 12, eps: float = 1e-5) -> dict:
+    """Probabilities, transition matrix and value iteration from ``counts`` (xthreat.py:74-218,
+    278-320): the same float64 operations as the reference on its float64 count matrices."""
+    shotm, goalm, movem = (cnt[k].astype(np.float64).reshape((w, l)) for k in ('shot', 'goal', 'move'))
+    scoring = _safe_divide(goalm, shotm)
+    total = movem + shotm
+    pshot, pmove = _safe_divide(shotm, total), _safe_divide(movem, total)
+    C = l * w
+    start_counts = cnt['start'].astype(np.float64).reshape(-1)
+    tc = cnt['trans'].reshape(C, C)
     T = np.zeros((C, C))
     nz = tc != 0
     rows = np.nonzero(nz)[0]
@@ -92,6 +104,11 @@ def fit(cols: Dict[str, np.ndarray], l: int = 16, w: int = 12, eps: float = 1e-5
             break
     return dict(scoring_prob=scoring, shot_prob=pshot, move_prob=pmove, transition=T, xT=xT,
                 heatmaps=np.stack(heat))
+
+
+def fit(cols: Dict[str, np.ndarray], l: int = 16, w: int = 12, eps: float = 1e-5) -> dict:
+    """ExpectedThreat.fit (xthreat.py:322-345): ``solve(counts(cols))``."""
+    return solve(counts(cols, l, w), l, w, eps)
 
 
 def centres(extent: float, cells: int) -> np.ndarray:

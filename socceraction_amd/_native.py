@@ -150,6 +150,9 @@ _SIGNATURES = {
                                          ctypes.c_int32, _p, ctypes.c_int32, _p, _p]),
     'sa_xt_rate': (ctypes.c_int, [ctypes.POINTER(SaActions), _p, ctypes.c_int32, ctypes.c_int32,
                                   _p, _p, _p]),
+    'sa_xt_rate_interp': (ctypes.c_int, [ctypes.POINTER(SaActions), _p, _p, _p, ctypes.c_int32,
+                                         ctypes.c_int32, _p, ctypes.c_int32, _p, ctypes.c_int32,
+                                         _p, _p, _p]),
     'sa_atomic_scratch_bytes': (ctypes.c_int64, [ctypes.c_int64]),
     'sa_atomic_count': (ctypes.c_int, [ctypes.POINTER(SaSpadlFrame), _p,
                                        ctypes.POINTER(ctypes.c_int64), _p]),

@@ -138,8 +138,9 @@ def build_plan(xfns: Sequence[str], k: int, atomic: bool = False) -> FeaturePlan
 @lru_cache(maxsize=128)
 def _build_plan(xfns: Tuple[str, ...], k: int, atomic: bool) -> FeaturePlan:
     valid = ATOMIC_XFNS if atomic else SPADL_XFNS
-    if not 1 <= k <= 8:
-        raise ValueError('nb_prev_actions must be between 1 and 8 on this backend')
+    if k < 1:
+        # the reference's gamestates(actions, 0) is [actions]: one frame, as k = 1
+        k = 1
     base = {'b': {}, 'f': {}, 'i': {}}
     count = {'b': 0, 'f': 0, 'i': 0}
     order = []

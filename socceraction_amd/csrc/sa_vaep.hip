@@ -92,6 +92,10 @@ struct CondAcc {
   int32_t chunk;       // uniform: first condition of the chunk
 };
 
+// the sinks take the wave's first row (wb) and the ok / NaN masks from wave_base: one 128-row
+// pair per lane.  More pairs per lane would need a flush and a new wb per pair.
+static_assert(NUM_PAIRS == 1, "COND sinks assume one 2-row pair per lane (CondSink::wb)");
+
 struct CondSink {
   const int32_t* start;
   const float* thr;
@@ -404,7 +408,12 @@ constexpr int BOOL_TILE = 1024;  // rows per tile of the bool block image
 constexpr int CG_WAVES = 4;  // waves per workgroup
 #define CG_EQ(w, v) bytes_eq((w), (v))
 
-template <bool ATOMIC, bool EXPLICIT, bool BITS>
+// WIDE (windowed mode, nb_prev_actions > 9: windows reach past the 8-row halo): each window's
+// rows are gathered per action, row j - min(i, j - segment start), with the uncapped distance.
+constexpr int BOOL_HALO = 8;  // rows before j0 held in registers: windows i <= 8 (k <= 9)
+constexpr int WIDE_D_MAX = 1 << 30;
+
+template <bool ATOMIC, bool EXPLICIT, bool BITS, bool WIDE = false>
 __global__ __launch_bounds__(64 * CG_WAVES) void bool_colgroup_kernel(FeatArgs args, int ngroups,
                                                                       int gcols) {
   const int lane = threadIdx.x & (WAVE - 1);
@@ -429,6 +438,9 @@ __global__ __launch_bounds__(64 * CG_WAVES) void bool_colgroup_kernel(FeatArgs a
   // d = min(j - seg_start, 15) per action: segment of the tile start (same for all lanes),
   // then each lane advances to its own rows
   uint32_t dw[4] = {0, 0, 0, 0};
+  int32_t dm[WIDE ? LANE_ACTS : 1];  // WIDE: j - seg_start per action, uncapped (up to 2^30)
+#pragma unroll
+  for (int m = 0; m < (WIDE ? LANE_ACTS : 1); ++m) dm[m] = 0;
   if (!EXPLICIT && K > 1) {
     SegCursor c = seg_at(A, tile0);
 #pragma unroll
@@ -437,14 +449,18 @@ __global__ __launch_bounds__(64 * CG_WAVES) void bool_colgroup_kernel(FeatArgs a
       if (j < n) {
         seg_advance(A, c, j);
         const int64_t dd = j - c.s;
-        const int d = dd > 15 ? 15 : (int)dd;
-        dw[m >> 2] |= (uint32_t)d << (8 * (m & 3));
+        if (WIDE) {
+          dm[m] = dd > WIDE_D_MAX ? WIDE_D_MAX : (int32_t)dd;
+        } else {
+          const int d = dd > 15 ? 15 : (int)dd;
+          dw[m >> 2] |= (uint32_t)d << (8 * (m & 3));
+        }
       }
     }
   }
   uint32_t TR[6], RR[6], BR[6];  // rows j0-8 .. j0+15 (windowed mode)
   uint32_t tw[4], rw[4], bw[4];  // window i of the lane's 16 actions
-  if (!EXPLICIT) {
+  if (!EXPLICIT && !WIDE) {
     const int64_t wbase = j0 / 4 - 2;
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
@@ -471,6 +487,20 @@ __global__ __launch_bounds__(64 * CG_WAVES) void bool_colgroup_kernel(FeatArgs a
         tw[q] = ld_u8x4(Fi.type_id, j0 / 4 + q, n);
         rw[q] = ATOMIC ? 0u : ld_u8x4(Fi.result_id, j0 / 4 + q, n);
         bw[q] = ld_u8x4(Fi.bodypart_id, j0 / 4 + q, n);
+      }
+    } else if (WIDE) {  // window i gathered per action: row j - min(i, d) (features.py:83-88)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) tw[q] = rw[q] = bw[q] = 0;
+#pragma unroll
+      for (int m = 0; m < LANE_ACTS; ++m) {
+        const int64_t j = j0 + m;
+        if (j < n) {
+          const int64_t r = j - (dm[m] < i ? dm[m] : i);
+          SA_DCHECK(r >= 0 && r <= j, r);
+          tw[m >> 2] |= (uint32_t)F0.type_id[r] << (8 * (m & 3));
+          if (!ATOMIC) rw[m >> 2] |= (uint32_t)F0.result_id[r] << (8 * (m & 3));
+          bw[m >> 2] |= (uint32_t)F0.bodypart_id[r] << (8 * (m & 3));
+        }
       }
     } else if (i == 0) {
 #pragma unroll
@@ -565,9 +595,9 @@ __global__ __launch_bounds__(64 * CG_WAVES) void bool_colgroup_kernel(FeatArgs a
           t0 = ld_or0(A.frames[0].team, j0 + mm, n);
           ti = ld_or0(A.frames[i].team, j0 + mm, n);
         } else {
-          const int d = (int)byte_of(dw[mm >> 2], mm & 3);
+          const int d = WIDE ? dm[mm] : (int)byte_of(dw[mm >> 2], mm & 3);
           const int s = d < i ? d : i;
-          SA_DCHECK(s >= 0 && s <= 8, s);
+          SA_DCHECK(s >= 0 && (WIDE || s <= BOOL_HALO), s);
           // team codes straight from L1/L2 (a few waves per tile need them): the kernel keeps
           // no LDS, so xT workgroups with large LDS footprints co-reside with it
           t0 = ld_or0(F0.team, j0 + mm, n);
@@ -994,7 +1024,8 @@ __device__ __forceinline__ void labels_pair(const sa_actions& A, int nr, uint8_t
 
 // KF = 3: windowed mode with nb_prev_actions <= 3.  The pair's rows jb-2 .. jb+1 are read
 // once (16-B loads) and the windows are formed in registers (see the loop below).
-// KF = 0: any mode / any k (explicit frames, k <= 8): per-window row loads.
+// KF = 0: any mode / any k (explicit frames: k <= SA_MAX_FRAMES; windowed: any k): per-window
+// row loads.
 template <bool ATOMIC, bool EXPLICIT, int KF, bool TAIL = false, bool N32 = false, bool COND = false>
 __global__ __launch_bounds__(256) void num_features_kernel(FeatArgs args) {
   // N32: the f64 and i64 blocks hold float32 values (sa_vaep_features_bits_f32); COND: no blocks,
@@ -1084,7 +1115,7 @@ __global__ __launch_bounds__(256) void num_features_kernel(FeatArgs args) {
       if (!EXPLICIT) {
         seg_advance(A, cur, j);
         const int64_t d = j - cur.s;
-        dd[e] = d > 15 ? 15 : (int)d;
+        dd[e] = d > WIDE_D_MAX ? WIDE_D_MAX : (int)d;  // compared with the window index only
         away[e] = A.home_team != nullptr && F0.team[j] != A.home_team[cur.g];
       }
     }
@@ -1665,7 +1696,7 @@ extern "C" int sa_vaep_features_conditions(const sa_actions* a, const sa_feature
   if (!a) return fail(SA_EINVAL, "null sa_actions");
   if (a->n_frames != 1) return fail(SA_EINVAL, "condition bitmaps: windowed mode only");
   if (!plan || plan->nb_prev_actions > 3) return fail(SA_EINVAL, "condition bitmaps: nb_prev_actions <= 3");
-  if (!bits || n_bool_cols < 1 || n_cond < 0 || n_f64_cols < 0 || n_i64_cols < 0 || bits_stride % 16 ||
+  if (!bits || n_bool_cols < 0 || n_cond < 0 || n_f64_cols < 0 || n_i64_cols < 0 || bits_stride % 16 ||
       bits_stride < 16 * ((a->n + 127) / 128) || !aligned16(bits))
     return fail(SA_EINVAL, "condition bitmaps: 16-byte aligned rows of at least ceil(n/128)*16 bytes");
   if (!cond_fstart || !cond_istart || (n_cond > 0 && (!cond_thr || !cond_dl)))
@@ -1726,7 +1757,7 @@ static int launch_features(const sa_actions* a, const sa_feature_plan* plan, con
   if (rc) return rc;
   if (!plan) return fail(SA_EINVAL, "null plan");
   const int K = plan->nb_prev_actions;
-  if (K < 1 || K > SA_MAX_FRAMES) return fail(SA_EINVAL, "nb_prev_actions must be in [1, 8]");
+  if (K < 1) return fail(SA_EINVAL, "nb_prev_actions must be >= 1");
   if (a->n_frames > 1 && a->n_frames != K)
     return fail(SA_EINVAL, "explicit mode needs n_frames == nb_prev_actions");
   bool wb = false, wf = false, wi = false, wn = false;
@@ -1773,7 +1804,7 @@ static int launch_features(const sa_actions* a, const sa_feature_plan* plan, con
                 xt_cells,
                 xt_l,
                 xt_w,
-                wb ? (uint16_t*)bits : nullptr,
+                (wb || cond) ? (uint16_t*)bits : nullptr,  // COND: the condition rows even with no bool column
                 bits_stride / 2,
                 tail ? tail->nr : 0,
                 tail ? tail->sc : nullptr,
@@ -1797,19 +1828,30 @@ static int launch_features(const sa_actions* a, const sa_feature_plan* plan, con
     const int gc = (int)((args.Cb + ng - 1) / ng);
     const int64_t waves = (a->n + BOOL_TILE - 1) / BOOL_TILE * ng;
     const dim3 cgrid(xcd_grid((waves + CG_WAVES - 1) / CG_WAVES)), cblock(WAVE * CG_WAVES);
-    if (bits) {  // the on-device VAEP.rate: SPADL or atomic, windowed or explicit, as bitmaps
-      if (a->atomic)
+    const bool wide = !expl && K > BOOL_HALO + 1;  // windows past the register halo
+    if (bits) {  // the on-device VAEP.rate: SPADL or atomic, windowed, as bitmaps
+      if (wide) {
+        if (a->atomic)
+          hipLaunchKernelGGL((bool_colgroup_kernel<true, false, true, true>), cgrid, cblock, 0, st, args, ng, gc);
+        else
+          hipLaunchKernelGGL((bool_colgroup_kernel<false, false, true, true>), cgrid, cblock, 0, st, args, ng, gc);
+      } else if (a->atomic) {
         hipLaunchKernelGGL((bool_colgroup_kernel<true, false, true>), cgrid, cblock, 0, st, args, ng, gc);
-      else
+      } else {
         hipLaunchKernelGGL((bool_colgroup_kernel<false, false, true>), cgrid, cblock, 0, st, args, ng, gc);
+      }
     } else if (a->atomic) {
       if (expl)
         hipLaunchKernelGGL((bool_colgroup_kernel<true, true, false>), cgrid, cblock, 0, st, args, ng, gc);
+      else if (wide)
+        hipLaunchKernelGGL((bool_colgroup_kernel<true, false, false, true>), cgrid, cblock, 0, st, args, ng, gc);
       else
         hipLaunchKernelGGL((bool_colgroup_kernel<true, false, false>), cgrid, cblock, 0, st, args, ng, gc);
     } else {
       if (expl)
         hipLaunchKernelGGL((bool_colgroup_kernel<false, true, false>), cgrid, cblock, 0, st, args, ng, gc);
+      else if (wide)
+        hipLaunchKernelGGL((bool_colgroup_kernel<false, false, false, true>), cgrid, cblock, 0, st, args, ng, gc);
       else
         hipLaunchKernelGGL((bool_colgroup_kernel<false, false, false>), cgrid, cblock, 0, st, args, ng, gc);
     }

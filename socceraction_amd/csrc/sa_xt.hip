@@ -56,8 +56,11 @@ enum { XC_GLOBAL = 0, XC_VEC = 1, XC_SMALL = 2, XC_WIDE = 3 };
 // One action's part of the count pass: shot/goal/move histograms and the successful-move
 // transition count, with the reference's non-finite rules (xthreat.py:40-67: _count drops rows
 // with a NaN start, casts the rest; :177-218: move_transition_matrix casts every move
-// coordinate).  Error bits: 1 = infinite shot start, 2 = infinite move start, 8 = NaN move start
+// coordinate).  Error flags, one byte each so that a sum all-reduce of the ranks' flags keeps
+// them apart: 0x1 = infinite shot start, 0x100 = infinite move start, 0x10000 = NaN move start
 // or non-finite move end (see sa_xt_count).
+constexpr int32_t XT_ERRB_SHOT = 0x1, XT_ERRB_MOVE_START = 0x100, XT_ERRB_MOVE_OTHER = 0x10000;
+
 struct XtAct {
   uint32_t cls;            // 0, XT_CELL_SHOT, XT_CELL_MOVE
   bool succ, snan, sfin, efin;
@@ -73,7 +76,7 @@ __device__ __forceinline__ void count_one(const XtAct& a, int C, uint32_t* hs, u
   if (a.cls == XT_CELL_SHOT) {
     if (a.snan) return;  // _count drops NaN rows (xthreat.py:60-61)
     if (!a.sfin) {
-      bad |= 1;
+      bad |= XT_ERRB_SHOT;
       return;
     }
     SA_DGUARD(a.cs >= 0 && a.cs < C, a.cs, return);
@@ -86,11 +89,11 @@ __device__ __forceinline__ void count_one(const XtAct& a, int C, uint32_t* hs, u
     }
   } else if (a.cls == XT_CELL_MOVE) {
     if (a.snan) {  // dropped by action_prob's _count; move_transition_matrix's cast raises
-      bad |= 8;
+      bad |= XT_ERRB_MOVE_OTHER;
       return;
     }
     if (!a.sfin) {
-      bad |= 2;
+      bad |= XT_ERRB_MOVE_START;
       return;
     }
     SA_DGUARD(a.cs >= 0 && a.cs < C, a.cs, return);
@@ -99,7 +102,7 @@ __device__ __forceinline__ void count_one(const XtAct& a, int C, uint32_t* hs, u
     else
       atomicAdd(&move[a.cs], 1ull);
     if (!a.efin) {
-      bad |= 8;  // only move_transition_matrix reads the end coordinates
+      bad |= XT_ERRB_MOVE_OTHER;  // only move_transition_matrix reads the end coordinates
       return;
     }
     if (a.succ) {
@@ -628,6 +631,37 @@ __global__ void xt_interp_kernel(const double* __restrict__ xT, const double* __
   grid[k] = (ux * z00 + tx * z01) * uy + (ux * z10 + tx * z11) * ty;
 }
 
+// The interpolated surface's node brackets, one table entry per node column h (x axis, entries
+// [0, L)) and node row r (y axis, entries [L, L + W)): the (i, tx) / (j, ty) xt_interp_kernel
+// computes for that node, by the same bracket().  With them the rate evaluates a node's value
+// in the same operations as the grid -- bit for bit -- without the L x W grid.
+__global__ void xt_axes_kernel(const double* __restrict__ cx, const double* __restrict__ cy, int l, int w,
+                               const double* __restrict__ xs, int L, const double* __restrict__ ys, int W,
+                               int32_t* __restrict__ idx, double* __restrict__ frac) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= L + W) return;
+  int i;
+  double t;
+  if (k < L)
+    bracket(cx, l, xs[k], i, t);
+  else
+    bracket(cy, w, ys[k - L], i, t);
+  idx[k] = i;
+  frac[k] = t;
+}
+
+// B(xs[h], ys[r]) of node k = r * L + h: xt_interp_kernel's expression on the (w x l) surface
+__device__ __forceinline__ double node_value(const double* __restrict__ xT, int l, int L, int k,
+                                             const int32_t* __restrict__ idx, const double* __restrict__ frac) {
+  const int r = k / L, h = k - r * L;
+  const int i = idx[h], j = idx[L + r];
+  const double tx = frac[h], ty = frac[L + r];
+  const double z00 = xT[j * l + i], z01 = xT[j * l + i + 1];
+  const double z10 = xT[(j + 1) * l + i], z11 = xT[(j + 1) * l + i + 1];
+  const double ux = 1.0 - tx, uy = 1.0 - ty;
+  return (ux * z00 + tx * z01) * uy + (ux * z10 + tx * z11) * ty;
+}
+
 // rate (xthreat.py:408-465): successful moves get grid[end] - grid[start], others NaN.
 __device__ __forceinline__ double rate_one(int t, int r, double sx, double sy, double ex, double ey,
                                            const double* __restrict__ grid, int L, int W, int32_t& bad) {
@@ -668,6 +702,54 @@ __global__ __launch_bounds__(256) void xt_rate_kernel(sa_actions A, const double
   } else {
     for (int64_t j = j0; j < j0 + 2 && j < A.n; ++j)
       out[j] = rate_one(F.type_id[j], F.result_id[j], F.c0[j], F.c1[j], F.c2[j], F.c3[j], grid, L, W, bad);
+  }
+  if (bad && err) atomicOr(err, bad);
+}
+
+// rate(use_interpolation=True) from the (w x l) surface and the node tables (sa_xt_rate_interp):
+// xt_rate_kernel's layout (2 actions per thread, 16-B loads and store), each node value evaluated
+// in place (node_value) instead of gathered from the 5.7 MB L x W grid.
+__device__ __forceinline__ double rate_interp_one(int t, int r, double sx, double sy, double ex, double ey,
+                                                  const double* __restrict__ xT, int l, int L, int W,
+                                                  const int32_t* __restrict__ idx,
+                                                  const double* __restrict__ frac, int32_t& bad) {
+  double v = __builtin_nan("");
+  if (is_move(t) && r == R_SUCCESS) {
+    if (!isfinite(sx) || !isfinite(sy) || !isfinite(ex) || !isfinite(ey)) {
+      bad = 4;
+    } else {
+      const int s = flat_index(sx, sy, L, W), e = flat_index(ex, ey, L, W);
+      SA_DGUARD(s >= 0 && s < L * W && e >= 0 && e < L * W, s, return v);
+      v = node_value(xT, l, L, e, idx, frac) - node_value(xT, l, L, s, idx, frac);
+    }
+  }
+  return v;
+}
+
+__global__ __launch_bounds__(256) void xt_rate_interp_kernel(sa_actions A, const double* __restrict__ xT, int l,
+                                                             int L, int W, const int32_t* __restrict__ idx,
+                                                             const double* __restrict__ frac,
+                                                             double* __restrict__ out, int32_t* __restrict__ err,
+                                                             int vec) {
+  const int64_t j0 = 2 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x);
+  if (j0 >= A.n) return;
+  const sa_frame& F = A.frames[0];
+  int32_t bad = 0;
+  if (vec && j0 + 1 < A.n) {
+    const f64x2 sx = *reinterpret_cast<const f64x2*>(F.c0 + j0);
+    const f64x2 sy = *reinterpret_cast<const f64x2*>(F.c1 + j0);
+    const f64x2 ex = *reinterpret_cast<const f64x2*>(F.c2 + j0);
+    const f64x2 ey = *reinterpret_cast<const f64x2*>(F.c3 + j0);
+    const uint32_t ty = *reinterpret_cast<const uint16_t*>(F.type_id + j0);
+    const uint32_t rs = *reinterpret_cast<const uint16_t*>(F.result_id + j0);
+    f64x2 v;
+    v[0] = rate_interp_one(ty & 0xFF, rs & 0xFF, sx[0], sy[0], ex[0], ey[0], xT, l, L, W, idx, frac, bad);
+    v[1] = rate_interp_one(ty >> 8, rs >> 8, sx[1], sy[1], ex[1], ey[1], xT, l, L, W, idx, frac, bad);
+    __builtin_nontemporal_store(v, reinterpret_cast<f64x2*>(out + j0));
+  } else {
+    for (int64_t j = j0; j < j0 + 2 && j < A.n; ++j)
+      out[j] = rate_interp_one(F.type_id[j], F.result_id[j], F.c0[j], F.c1[j], F.c2[j], F.c3[j], xT, l, L, W,
+                               idx, frac, bad);
   }
   if (bad && err) atomicOr(err, bad);
 }
@@ -995,6 +1077,33 @@ extern "C" int sa_xt_rate(const sa_actions* a, const double* grid, int32_t L, in
   hipLaunchKernelGGL(xt_rate_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
                      (hipStream_t)stream, *a, grid, L, W, out, err_flags, vec);
   return check_launch("xt_rate_kernel");
+}
+
+extern "C" int sa_xt_rate_interp(const sa_actions* a, const double* xT, const double* cx, const double* cy,
+                                 int32_t l, int32_t w, const double* xs, int32_t L, const double* ys, int32_t W,
+                                 double* out, int32_t* err_flags, void* stream) {
+  if (!a || a->n < 0 || !xT || !cx || !cy || !xs || !ys || !out || L < 1 || W < 1)
+    return fail(SA_EINVAL, "bad xt_rate_interp args");
+  if (l < 2 || w < 2) return fail(SA_EINVAL, "interpolation needs at least 2 cells per axis");
+  if ((int64_t)L * W > INT32_MAX) return fail(SA_EINVAL, "interpolated grid too large");
+  if (a->n == 0) return SA_OK;
+  hipStream_t st = (hipStream_t)stream;
+  Scratch sc;  // frac[L + W] | idx[L + W]
+  int rc = scratch_acquire((sizeof(double) + sizeof(int32_t)) * (size_t)(L + W), st, &sc);
+  if (rc) return rc;
+  double* frac = static_cast<double*>(sc.ptr);
+  int32_t* idx = reinterpret_cast<int32_t*>(frac + (L + W));
+  hipLaunchKernelGGL(xt_axes_kernel, dim3((unsigned)((L + W + 255) / 256)), dim3(256), 0, st, cx, cy, l, w, xs, L,
+                     ys, W, idx, frac);
+  const sa_frame& F = a->frames[0];
+  const int vec = aligned16(F.c0) && aligned16(F.c1) && aligned16(F.c2) && aligned16(F.c3) && aligned16(out) &&
+                  ((uintptr_t)F.type_id & 1u) == 0 && ((uintptr_t)F.result_id & 1u) == 0;
+  const int64_t threads = (a->n + 1) / 2;
+  hipLaunchKernelGGL(xt_rate_interp_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, *a, xT, l, L,
+                     W, idx, frac, out, err_flags, vec);
+  rc = check_launch("xt_rate_interp_kernel");
+  scratch_release(sc, st);
+  return rc;
 }
 
 extern "C" int sa_xt_probabilities(const int64_t* shot, const int64_t* goal, const int64_t* move, int32_t C,

@@ -75,6 +75,15 @@ class FeatureBlocks:
     def column(self, kind: str, col: int) -> torch.Tensor:
         return self._blk(kind)[:, col, :].reshape(-1)[:self.n]
 
+    def rows(self, kind: str, start: int, stop: int) -> torch.Tensor:
+        """``[n_cols, stop - start]`` copy of a row range (one game), on device: only the tiles
+        that hold those rows are untiled."""
+        t = self._blk(kind)
+        R = t.shape[2]
+        t0, t1 = start // R, max(start, stop - 1) // R + 1
+        sub = t[t0:t1].permute(1, 0, 2).reshape(t.shape[1], -1)
+        return sub[:, start - t0 * R:stop - t0 * R]
+
     def to_numpy(self):
         """Host copies ``[n_cols, >= n]`` of the three blocks: whole tiles are copied (one
         contiguous D2H per block into pinned memory, all three in flight together) and the
@@ -361,20 +370,23 @@ class XTCounts:
 
 
 def xt_zero_counts(l: int, w: int, dev, row_blocks: int = 1) -> XTCounts:
-    """Zeroed count buffers, carved from ONE allocation (one fill kernel). ``row_blocks`` > 1
-    pads the C x C transition counts to a whole number of equal row blocks
-    (``XTCounts.trans_padded``) so they can be reduce-scattered by rows across that many ranks;
-    ``trans`` is the C*C view the count kernel fills."""
+    """Zeroed count buffers, carved from ONE allocation (one fill kernel, one all-reduce):
+    ``[shot | goal | move]`` (3 x C int64), the error flags (int32), then the C x C transition
+    counts (int32). ``row_blocks`` > 1 pads the transition counts to a whole number of equal row
+    blocks (``XTCounts.trans_padded``) so they can be reduce-scattered by rows across that many
+    ranks; ``trans`` is the C*C view the count kernel fills. ``XTCounts.head`` is the vectors +
+    flags part, ``XTCounts.buf`` the whole allocation."""
     C = l * w
     rows = -(-C // row_blocks) * row_blocks
     a = lambda b: -(-b // 256) * 256  # noqa: E731  (256-B aligned parts)
-    o_tr = a(3 * C * 8)
-    o_err = o_tr + a(rows * C * 4)
-    buf = torch.zeros(o_err + 256, dtype=torch.uint8, device=dev)
+    o_err = a(3 * C * 8)
+    o_tr = o_err + 256
+    buf = torch.zeros(o_tr + a(rows * C * 4), dtype=torch.uint8, device=dev)
     vec = buf[:3 * C * 8].view(torch.int64).view(3, C)
     padded = buf[o_tr:o_tr + rows * C * 4].view(torch.int32)
     acc = XTCounts(l, w, vec[0], vec[1], vec[2], padded[:C * C], buf[o_err:o_err + 4].view(torch.int32))
     acc.trans_padded = padded
+    acc.head = buf[:o_tr]
     acc.buf = buf
     return acc
 
@@ -419,7 +431,10 @@ def xt_rate_codes(codes: torch.Tensor, n: int, grid: torch.Tensor,
     return out[:n], err
 
 
-XT_ERR_SHOT, XT_ERR_MOVE_START, XT_ERR_MOVE_OTHER = 1, 2, 8
+# the count pass's error flags, one BYTE each (sa_xt_count: 0x1 / 0x100 / 0x10000 per rank), so
+# the flags of up to 255 ranks add up in the counts' one sum all-reduce without carrying into
+# each other; a flag is set when its byte is non-zero
+XT_ERR_SHOT, XT_ERR_MOVE_START, XT_ERR_MOVE_OTHER = 0xFF, 0xFF00, 0xFF0000
 XT_ERR_FIT = XT_ERR_SHOT | XT_ERR_MOVE_START | XT_ERR_MOVE_OTHER
 
 
@@ -468,10 +483,10 @@ def xt_check_errors(acc: XTCounts, mask: int = XT_ERR_FIT) -> None:
     if e & XT_ERR_MOVE_OTHER:
         raise ValueError('Cannot convert non-finite values (NA or inf) to integer '
                          '(move coordinates)')
-    if e & 1:
+    if e & XT_ERR_SHOT:
         raise ValueError('Cannot convert non-finite values (NA or inf) to integer '
                          '(shot start coordinates)')
-    if e & 2:
+    if e & XT_ERR_MOVE_START:
         raise ValueError('Cannot convert non-finite values (NA or inf) to integer '
                          '(move coordinates)')
 
@@ -570,6 +585,37 @@ def xt_normalize(acc: XTCounts) -> Tuple[torch.Tensor, torch.Tensor]:
                                                 _ptr(acc.trans), acc.l, acc.w, _ptr(mats), _ptr(tt),
                                                 stream_handle()))
     return mats, tt
+
+
+def xt_interp_axes(l: int, w: int, dev, L: int = 1050, W: int = 680) -> torch.Tensor:
+    """The node positions of the interpolated rate on the device, ``[cx | cy | xs | ys]``: the
+    cell centres (xthreat.py:372-376) and the reference's ``linspace`` nodes (:443-451)."""
+    cx, cy = _centres(105.0, l), _centres(68.0, w)
+    if len(cx) != l or len(cy) != w:
+        raise ValueError('x and y must have the lengths of the xT surface')  # as interp2d
+    c = np.concatenate([cx, cy, np.linspace(0, 105.0, L), np.linspace(0, 68.0, W)])
+    return torch.from_numpy(c).to(dev)
+
+
+def xt_rate_interp(batch: ActionBatch, xT: torch.Tensor, l: int, w: int, L: int = 1050,
+                   W: int = 680, axes: Optional[torch.Tensor] = None,
+                   out: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """ExpectedThreat.rate(use_interpolation=True) of ``batch`` from the (w, l) surface ``xT``
+    without the L x W grid (``sa_xt_rate_interp``): bit-identical to
+    ``xt_rate(batch, xt_interp_grid(xT, l, w, L=L, W=W), L, W)``. ``axes``: a cached
+    :func:`xt_interp_axes` tensor."""
+    dev = batch.device
+    axes = xt_interp_axes(l, w, dev, L, W) if axes is None else axes
+    if axes.numel() != l + w + L + W:
+        raise ValueError('axes must hold l + w + L + W node positions')
+    out = torch.empty(max(_ld(batch.n), 16), dtype=torch.float64, device=dev) if out is None else out
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    s = batch.struct()
+    o = l + w
+    _native.check(_native.lib().sa_xt_rate_interp(
+        ctypes.byref(s), _ptr(xT.contiguous()), _ptr(axes[:l]), _ptr(axes[l:o]), l, w,
+        _ptr(axes[o:o + L]), L, _ptr(axes[o + L:]), W, _ptr(out), _ptr(err), stream_handle()))
+    return out[:batch.n], err
 
 
 def xt_rate(batch: ActionBatch, grid: torch.Tensor, L: int, W: int) -> Tuple[torch.Tensor, torch.Tensor]:

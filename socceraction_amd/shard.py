@@ -30,18 +30,15 @@ def partition_games(game_off: np.ndarray, world: int) -> List[Tuple[int, int]]:
     return [(cuts[r], cuts[r + 1]) for r in range(world)]
 
 
-def allreduce_xt_counts(shot: torch.Tensor, goal: torch.Tensor, move: torch.Tensor,
-                        trans: torch.Tensor, err: torch.Tensor, group=None) -> None:
-    """Sum the xT count buffers over the ranks of ``group`` in place (2 all-reduces + 1 max)."""
-    import torch.distributed as dist
-    C = shot.numel()
-    vec = torch.cat([shot, goal, move])
-    dist.all_reduce(vec, group=group)
-    dist.all_reduce(trans, group=group)
-    dist.all_reduce(err, op=dist.ReduceOp.MAX, group=group)
-    shot.copy_(vec[:C])
-    goal.copy_(vec[C:2 * C])
-    move.copy_(vec[2 * C:])
+def allreduce_xt_counts(acc, group=None) -> None:
+    """Sum the xT count buffers of ``acc`` (``ops.xt_zero_counts``) over the ranks of ``group``
+    in place with ONE all-reduce: the whole allocation -- shot / goal / move (int64), the error
+    flags and the C x C transition counts (int32) -- summed as int32 words.  Exact while every
+    summed count is below 2**31 (the bound the int32 transition counts already carry, SURVEY
+    §8(e)): the int64 counts' high words stay 0 and their low words cannot carry; the error
+    flags are one byte each (``ops.XT_ERR_*``), so up to 255 ranks' flags add without
+    overlapping.  No staging copy, no ``torch.cat``."""
+    _all_reduce(acc.buf.view(torch.int32), group=group)
 
 
 # ----------------------------------------------------------------------------- collectives
@@ -89,7 +86,8 @@ def xt_solve_sharded(acc, eps: float = 1e-5, max_iter: int = 1000, group=None, b
     """Row-sharded xT fit over the ranks of ``group``: each rank passes
     its OWN shard's counts (``ops.xt_zero_counts(..., row_blocks=world)`` + ``ops.xt_count``).
 
-    1. all-reduce of the shot / goal / move vectors (3 x C int64) and the error flags;
+    1. one all-reduce of the shot / goal / move vectors (3 x C int64) and the error flags (the
+       head of the count allocation, summed as int32 words like ``allreduce_xt_counts``);
     2. reduce-scatter of the C x C transition counts by row blocks: rank r keeps the summed
        count rows [r*B, (r+1)*B), B = ceil(C / world) (half the traffic of an all-reduce);
     3. per iteration, each rank updates its B rows (``sa_xt_iterate_rows``, the reference's
@@ -114,10 +112,8 @@ def xt_solve_sharded(acc, eps: float = 1e-5, max_iter: int = 1000, group=None, b
     dev = acc.shot.device
     if acc.trans_padded.numel() != W * B * C:
         raise ValueError('counts must be allocated with xt_zero_counts(..., row_blocks=world)')
-    vec = torch.cat([acc.shot, acc.goal, acc.move])
-    _all_reduce(vec, group=group)
-    _all_reduce(acc.err, dist.ReduceOp.MAX, group=group)
-    shot, goal, move = vec[:C], vec[C:2 * C], vec[2 * C:]
+    _all_reduce(acc.head.view(torch.int32), group=group)  # the vectors + flags: one all-reduce
+    shot, goal, move = acc.shot, acc.goal, acc.move
     rows = torch.empty(B * C, dtype=torch.int32, device=dev)
     _reduce_scatter(rows, acc.trans_padded, group=group)
     lib = _native.lib()

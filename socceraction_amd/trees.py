@@ -384,10 +384,10 @@ def predict_pair_conditions(batch, plan, models: Sequence[TreeEnsemble], flip: b
     prep = _conditions_prep(plan, models, dev)
     n, nb, n_num = batch.n, plan.n_bool, prep['n_num']
     words = max(2, -(-n // 128) * 2)  # int64 words per row: a whole number of 16-B runs
-    bits = torch.empty((nb + n_num, words), dtype=torch.int64, device=dev)
+    bits = torch.empty((max(nb + n_num, 1), words), dtype=torch.int64, device=dev)
     s = batch.struct(flip=flip)
     _native.check(_native.lib().sa_vaep_features_conditions(
-        ctypes.byref(s), ctypes.byref(plan.struct), bits.data_ptr(), words * 8, max(nb, 1), plan.n_f64,
+        ctypes.byref(s), ctypes.byref(plan.struct), bits.data_ptr(), words * 8, nb, plan.n_f64,
         plan.n_i64, prep['fstart'].data_ptr(), prep['istart'].data_ptr(), prep['thr'].data_ptr(),
         prep['dl'].data_ptr(), n_num, stream_handle()))
     z = _native.SaBlock()

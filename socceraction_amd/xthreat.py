@@ -90,7 +90,7 @@ def _fit_counts(actions: pd.DataFrame, l: int, w: int, process_group=None,
         acc = ops.xt_zero_counts(l, w, device())
     if process_group is not None:
         from .shard import allreduce_xt_counts
-        allreduce_xt_counts(acc.shot, acc.goal, acc.move, acc.trans, acc.err, process_group)
+        allreduce_xt_counts(acc, process_group)
     ops.xt_check_errors(acc, mask)
     return acc
 
@@ -188,8 +188,13 @@ class ExpectedThreat:
     @property
     def transition_matrix(self) -> Optional[np.ndarray]:
         if self._transition is None and getattr(self, '_transition_counts', None) is not None:
-            _, tt = ops.xt_normalize(self._transition_counts)
-            self._transition = np.ascontiguousarray(tt.cpu().numpy().T)
+            # host-side from the compact counts fit kept: T[s, e] = count(s -> e) / moves from s,
+            # the reference's `vc2 / start_counts[i]` (one f64 division per non-zero bin)
+            move, idx, cnt = self._transition_counts
+            C = self.l * self.w
+            t = np.zeros(C * C)
+            t[idx] = cnt.astype(np.float64) / move[idx // C].astype(np.float64)
+            self._transition = t.reshape(C, C)
             self._transition_counts = None
         return self._transition
 
@@ -234,7 +239,11 @@ class ExpectedThreat:
         self.move_prob_matrix = m[2].reshape((w, l))
         self.transition_matrix = trans
         if trans is None and not (shard_solve and process_group is not None):
-            self._transition_counts = acc  # normalised on first access
+            # normalised on first access from a compact HOST copy (move counts + the non-zero
+            # transition bins), so the 4*C*C-byte device count buffer is not kept alive
+            nz = torch.nonzero(acc.trans).reshape(-1)
+            self._transition_counts = (acc.move.cpu().numpy(), nz.cpu().numpy(),
+                                       acc.trans[nz].cpu().numpy())
         self.xT = m[3].reshape((w, l)).copy()
         heat = heat_t.cpu().numpy().reshape((-1, w, l))
         self.heatmaps = [h.copy() for h in heat]
@@ -271,7 +280,9 @@ class ExpectedThreat:
                 raise ImportError('Interpolation requires scipy to be installed.')
             L = int(spadlconfig.field_length * 10)
             W = int(spadlconfig.field_width * 10)
-            res = (ops.xt_interp_grid(xT, l, w, L=L, W=W), L, W)
+            # the surface + its node positions: the rate evaluates each node in place
+            # (sa_xt_rate_interp), the 1050 x 680 grid is never formed
+            res = (xT, L, W, ops.xt_interp_axes(l, w, device(), L, W))
         self._grid_cache = (key, res)
         return res
 
@@ -279,11 +290,15 @@ class ExpectedThreat:
         """xT value of every successful move, NaN elsewhere (reference xthreat.py:408-465)."""
         if not np.any(self.xT):
             raise NotFittedError()
-        grid, L, W = self._grid(use_interpolation)
+        g = self._grid(use_interpolation)
         if len(actions) == 0:
             return np.empty(0)
         ab = ActionBatch.from_frame(actions)
-        out, err = ops.xt_rate(ab, grid, L, W)
+        if use_interpolation:
+            xT, L, W, axes = g
+            out, err = ops.xt_rate_interp(ab, xT, self.l, self.w, L, W, axes=axes)
+        else:
+            out, err = ops.xt_rate(ab, *g)
         if int(err.item()):
             raise ValueError('Cannot convert non-finite values (NA or inf) to integer')
         return out.cpu().numpy()

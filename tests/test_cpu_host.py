@@ -130,8 +130,10 @@ def test_default_plan_block_sizes():
         catalog.build_plan(['location'], 3, atomic=False)
     with pytest.raises(ValueError):
         catalog.build_plan(['movement'], 3, atomic=True)
-    with pytest.raises(ValueError):
-        catalog.build_plan(['time'], 9)
+    # any nb_prev_actions (vaep/features.py:62-88); 0 gives the one frame of gamestates(a, 0)
+    p = catalog.build_plan(list(catalog.SPADL_XFNS[:1]) + ['time', 'team', 'space_delta'], 17)
+    assert p.struct.nb_prev_actions == 17 and p.names[-1] == 'mov_a016'
+    assert catalog.build_plan(['time'], 0).names == catalog.build_plan(['time'], 1).names
 
 
 def test_feature_column_names_with_user_transformer():
@@ -233,18 +235,22 @@ def _gloo_worker(rank, world, port, q):
     move = (t == 0) | (t == 21) | (t == 1)
     succ = move & (cols['result_id'] == 1)
     cnt = lambda m, x, y: np.bincount(xo.flat_indexes(x[m], y[m], l, w), minlength=C)  # noqa: E731
-    sh = torch.tensor(cnt(shot, cols['start_x'], cols['start_y']), dtype=torch.int64)
-    go = torch.tensor(cnt(shot & (cols['result_id'] == 1), cols['start_x'], cols['start_y']),
-                      dtype=torch.int64)
-    mv = torch.tensor(cnt(move, cols['start_x'], cols['start_y']), dtype=torch.int64)
+    from socceraction_amd import ops
+    acc = ops.xt_zero_counts(l, w, 'cpu')  # the device layout, on the host for gloo
+    acc.shot.copy_(torch.tensor(cnt(shot, cols['start_x'], cols['start_y'])))
+    acc.goal.copy_(torch.tensor(cnt(shot & (cols['result_id'] == 1), cols['start_x'], cols['start_y'])))
+    acc.move.copy_(torch.tensor(cnt(move, cols['start_x'], cols['start_y'])))
     tr = np.zeros(C * C, np.int32)
     np.add.at(tr, xo.flat_indexes(cols['start_x'][succ], cols['start_y'][succ], l, w) * C +
               xo.flat_indexes(cols['end_x'][succ], cols['end_y'][succ], l, w), 1)
-    tr = torch.tensor(tr)
-    err = torch.tensor([rank], dtype=torch.int32)
-    shard.allreduce_xt_counts(sh, go, mv, tr, err)
+    acc.trans.copy_(torch.tensor(tr))
+    # rank 0 flags an infinite shot start, rank 1 that and an infinite move start: the byte
+    # lanes add up without touching each other
+    acc.err.fill_(ops.XT_ERR_SHOT & 0x1 if rank == 0 else 0x101)
+    shard.allreduce_xt_counts(acc)  # ONE all-reduce
     if rank == 0:
-        q.put((sh.numpy(), go.numpy(), mv.numpy(), tr.numpy(), int(err.item())))
+        q.put((acc.shot.numpy().copy(), acc.goal.numpy().copy(), acc.move.numpy().copy(),
+               acc.trans.numpy().copy(), int(acc.err.item())))
     dist.destroy_process_group()
 
 
@@ -267,7 +273,9 @@ def test_xt_count_allreduce_gloo_world2():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert err == 1
+    assert err == 0x102  # shot flag from both ranks (2), move-start flag from rank 1 (1)
+    from socceraction_amd import ops
+    assert err & ops.XT_ERR_SHOT and err & ops.XT_ERR_MOVE_START and not err & ops.XT_ERR_MOVE_OTHER
     d = synthetic.spadl_games(6, seed=9)
     f = xo.fit({c: d[c] for c in ('start_x', 'start_y', 'end_x', 'end_y', 'type_id',
                                   'result_id')}, 8, 6)

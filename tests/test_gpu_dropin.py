@@ -102,8 +102,10 @@ def test_rate_errors():
 
 
 @pytest.mark.parametrize('atomic', [False, True])
-def test_module_level_transformers(atomic):
-    """Each transformer called on a user-built game-state list equals the reference."""
+@pytest.mark.parametrize('case,k', [('n300', 3), ('widek_n300', 12), ('widek_fixture', 17)])
+def test_module_level_transformers(atomic, case, k):
+    """Each transformer called on a user-built game-state list equals the reference, including
+    game states of more frames than one launch takes (k = 12, 17: the frames go in groups)."""
     if atomic:
         from socceraction_amd.atomic.vaep import base, features as fs
         from socceraction_amd.atomic import spadl as sp
@@ -112,11 +114,11 @@ def test_module_level_transformers(atomic):
         from socceraction_amd.vaep import base, features as fs
         from socceraction_amd import spadl as sp
         prefix = 'spadl'
-    g = load(prefix, 'n300')
+    g = load(prefix, case)
     df = sp.add_names(frame(g, atomic))
-    gs = fs.play_left_to_right(fs.gamestates(df, 3), g['home_team_id'][0])
+    gs = fs.play_left_to_right(fs.gamestates(df, k), g['home_team_id'][0])
     X = pd.concat([f(gs) for f in base.xfns_default], axis=1)
-    _frame_equal(X.reset_index(drop=True), g, 3)
+    _frame_equal(X.reset_index(drop=True), g, k)
     one = fs.actiontype_onehot.__wrapped__(df)
     assert one.columns[0] == 'type_pass'
 

@@ -228,6 +228,41 @@ def test_explicit_frames_match_windowed(sa):
     _blocks_match(fb, g, k, n)
 
 
+def _same_rate(got, ref):
+    """Two rate vectors bit for bit: the same NaN rows, equal values elsewhere."""
+    a, b = got.cpu().numpy(), ref.cpu().numpy()
+    np.testing.assert_array_equal(np.isnan(a), np.isnan(b))
+    np.testing.assert_array_equal(a[~np.isnan(b)], b[~np.isnan(b)])
+
+
+def test_xt_rate_interp_equals_grid_gather(sa):
+    """sa_xt_rate_interp (node values evaluated per action from the surface) == the 1050 x 680
+    grid + gather, bit for bit, on random surfaces at 105 x 68, 16 x 12 and 2 x 2 (a row of
+    nodes clamped at each edge), with exact-edge and NaN / inf coordinates (error bit 4)."""
+    B, ops, syn = sa['batch'], sa['ops'], sa['synthetic']
+    d = syn.spadl_games(40, game_id0=3)
+    n = len(d['type_id'])
+    rng = np.random.default_rng(8)
+    for col, v in (('start_x', 0.0), ('end_x', 105.0), ('start_y', 68.0), ('end_y', 0.0),
+                   ('start_x', 104.99999999999999), ('end_y', 34.0)):
+        d[col][rng.choice(n, 50, replace=False)] = v
+    ab = B.ActionBatch.from_columns(d)
+    for l, w in ((105, 68), (16, 12), (2, 2)):
+        xT = torch.rand((w, l), dtype=torch.float64, device=ab.device)
+        r, e = ops.xt_rate(ab, ops.xt_interp_grid(xT, l, w), 1050, 680)
+        ri, ei = ops.xt_rate_interp(ab, xT, l, w)
+        _same_rate(ri, r)
+        assert int(ei.item()) == int(e.item()) == 0
+    for col, v in (('start_x', np.nan), ('end_y', np.inf)):
+        d[col][rng.choice(n, 9, replace=False)] = v
+    ab = B.ActionBatch.from_columns(d)
+    xT = torch.rand((68, 105), dtype=torch.float64, device=ab.device)
+    r, e = ops.xt_rate(ab, ops.xt_interp_grid(xT, 105, 68), 1050, 680)
+    ri, ei = ops.xt_rate_interp(ab, xT, 105, 68)
+    _same_rate(ri, r)
+    assert int(ei.item()) == int(e.item()) == 4
+
+
 def test_xt_goldens(sa):
     B, ops = sa['batch'], sa['ops']
     for name in cases('xt'):
@@ -259,6 +294,9 @@ def test_xt_goldens(sa):
                 assert_close(grid.cpu().numpy(), xo.interp_grid(g[f'{tag}_xT']), 'interp grid')
                 r, _ = ops.xt_rate(ab, grid, 1050, 680)
                 assert_close(r.cpu().numpy(), g[f'{tag}_rate_interp'], f'{name} {tag} interp rate')
+                ri, ei = ops.xt_rate_interp(ab, xT, l, w)  # per-action nodes, no grid: same bits
+                _same_rate(ri, r)
+                assert int(ei.item()) == 0
 
 
 def test_xt105_interpolated_rate_golden(sa):
@@ -283,6 +321,9 @@ def test_xt105_interpolated_rate_golden(sa):
         r, err = ops.xt_rate(ab, grid, 1050, 680)
         assert int(err.item()) == 0
         assert_close(r.cpu().numpy(), g[f'{tag}_rate_interp'], f'{tag} interp rate')
+        ri, ei = ops.xt_rate_interp(ab, xT, 105, 68)  # per-action nodes, no grid: same bits
+        _same_rate(ri, r)
+        assert int(ei.item()) == 0
         m = xthreat.ExpectedThreat(l=105, w=68)
         m.xT = g[f'{tag}_xT'].copy()
         assert_close(m.rate(df, use_interpolation=True), g[f'{tag}_rate_interp'], f'{tag} drop-in')

@@ -276,26 +276,32 @@ def test_float32_numeric_blocks_and_trees(sa, atomic):
         ops.features(ab, xfns, 4, bool_bits=True, num32=True)
 
 
-@pytest.mark.parametrize('atomic', [False, True])
-def test_condition_bitmaps_match_staged_walk(sa, atomic):
+@pytest.mark.parametrize('case', ['spadl', 'atomic', 'numeric_only'])
+def test_condition_bitmaps_match_staged_walk(sa, case):
     """sa_vaep_features_conditions + the staged walk over bitmaps only (trees.predict_pair_conditions:
     the learners' numeric split conditions evaluated inside the numeric feature pass) == each
     learner's staged walk over the feature blocks, bit for bit: two xgboost-shaped learners over
     bool and numeric (f64 and i64) features with NaN-free and NaN-routed splits, several tiles and
-    a batch whose length is not a multiple of 128."""
+    a batch whose length is not a multiple of 128; and a plan with no bool column at all
+    (numeric-only xfns: the condition rows start at bitmap row 0)."""
     from socceraction_amd import synthetic, catalog
     from oracle import vaep_oracle as vo
     B, ops, trees = sa['batch'], sa['ops'], sa['trees']
+    atomic = case == 'atomic'
     if atomic:
         d = synthetic.atomic_games(120, seed=8)
         xfns = ['actiontype', 'actiontype_onehot', 'bodypart', 'bodypart_onehot', 'time', 'team',
                 'time_delta', 'location', 'polar', 'movement_polar', 'direction', 'goalscore']
     else:
         d = synthetic.spadl_games(120, seed=8)
-        xfns = vo.SPADL_DEFAULT
+        xfns = ['time', 'startlocation', 'goalscore'] if case == 'numeric_only' else vo.SPADL_DEFAULT
     ab = B.ActionBatch.from_columns(d, atomic=atomic)
     assert ab.n % 128
-    ref = ops.features(ab, xfns, 3, num_tile=128, bool_bits=True)
+    if case == 'numeric_only':
+        ref = ops.features(ab, xfns, 3, num_tile=128)
+        assert ref.plan.n_bool == 0
+    else:
+        ref = ops.features(ab, xfns, 3, num_tile=128, bool_bits=True)
     kinds = [k for _, k, _ in ref.plan.order]
     models = [trees.TreeEnsemble.from_model(trees.synthetic_xgboost_json(
         len(kinds), n_trees=60, depth=3, seed=sd, feature_kinds=kinds)) for sd in (41, 42)]
