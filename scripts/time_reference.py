@@ -86,36 +86,56 @@ def cpu_model() -> str:
     return platform.processor() or 'unknown'
 
 
+def _load() -> dict:
+    """Host load (1 / 5 / 15-minute averages and runnable processes) at a point in time."""
+    try:
+        l1, l5, l15 = os.getloadavg()
+        return {'loadavg_1_5_15': [round(l1, 2), round(l5, 2), round(l15, 2)]}
+    except OSError:
+        return {}
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument('--games', type=int, default=64)
     ap.add_argument('--procs', type=int, default=0, help='pool size (0 = os.cpu_count())')
+    ap.add_argument('--repeats', type=int, default=3, help='timed runs per measurement (median kept)')
     ap.add_argument('--out', default=os.path.join(ROOT, 'profiles', 'reference_cpu.json'))
     args = ap.parse_args()
     _setup()
     d, df, games = _games(args.games)
     n = len(df)
+    load_before = _load()
     _value_games(games[:1])  # warm-up (imports, first merges)
 
-    t = time.perf_counter()
-    done = _value_games(games)
-    t1 = time.perf_counter() - t
+    t1s = []
+    for _ in range(args.repeats):
+        t = time.perf_counter()
+        done = _value_games(games)
+        t1s.append(time.perf_counter() - t)
+        assert done == n
     procs = args.procs or os.cpu_count() or 1
     chunks = [games[i::procs] for i in range(procs)]
+    tps = []
     with mp.get_context('fork').Pool(procs) as pool:
         pool.map(_value_games, [games[:1]] * procs)  # warm the workers
-        t = time.perf_counter()
-        done_p = sum(pool.map(_value_games, chunks))
-        tp = time.perf_counter() - t
-    assert done == done_p == n
+        for _ in range(args.repeats):
+            t = time.perf_counter()
+            done_p = sum(pool.map(_value_games, chunks))
+            tps.append(time.perf_counter() - t)
+            assert done_p == n
 
     mg = _G['mg']
-    t = time.perf_counter()
-    m = mg.ref_xt.ExpectedThreat(l=16, w=12)
-    with redirect_stdout(io.StringIO()):
-        m.fit(df)
-    m.rate(df)
-    txt = time.perf_counter() - t
+    txts = []
+    for _ in range(args.repeats):
+        t = time.perf_counter()
+        m = mg.ref_xt.ExpectedThreat(l=16, w=12)
+        with redirect_stdout(io.StringIO()):
+            m.fit(df)
+        m.rate(df)
+        txts.append(time.perf_counter() - t)
+    load_after = _load()
+    t1, tp, txt = (float(np.median(v)) for v in (t1s, tps, txts))
     rec = {
         'what': 'reference CPU path (rtelmore/socceraction, pandas), timed in the build container '
                 '(the reference never travels to the GPU host)',
@@ -123,14 +143,19 @@ def main() -> None:
                     'VAEP.compute_features (k=3, default xfns, 568 cols) + compute_labels + '
                     'formula.value (seeded probabilities)',
         'actions': n,
-        'one_process': {'seconds': round(t1, 3), 'actions_per_s': round(n / t1, 1), 'cores': 1},
-        'pool': {'seconds': round(tp, 3), 'actions_per_s': round(n / tp, 1), 'processes': procs},
+        'statistic': f'median of {args.repeats} timed runs (every run listed in "runs_s")',
+        'one_process': {'seconds': round(t1, 3), 'actions_per_s': round(n / t1, 1), 'cores': 1,
+                        'runs_s': [round(x, 3) for x in t1s]},
+        'pool': {'seconds': round(tp, 3), 'actions_per_s': round(n / tp, 1), 'processes': procs,
+                 'runs_s': [round(x, 3) for x in tps]},
         'xt_16x12_fit_rate_one_process': {'seconds': round(txt, 3),
                                           'actions_per_s': round(n / txt, 1),
-                                          'iterations': len(m.heatmaps) - 1},
+                                          'iterations': len(m.heatmaps) - 1,
+                                          'runs_s': [round(x, 3) for x in txts]},
         'step_one_process_actions_per_s': round(n / (t1 + txt), 1),
         'host': {'cpu': cpu_model(), 'os_cpu_count': os.cpu_count(),
-                 'python': platform.python_version()},
+                 'python': platform.python_version(), 'load_before': load_before,
+                 'load_after': load_after},
         'script': 'scripts/time_reference.py',
     }
     os.makedirs(os.path.dirname(args.out), exist_ok=True)

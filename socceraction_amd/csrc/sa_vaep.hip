@@ -334,10 +334,25 @@ __device__ __forceinline__ void st_i64x2(float* __restrict__ base, int64_t col, 
   st16(base + col * R, v);
 }
 
+// SA_NUM_PROBE (diagnostic builds only, wrong values): bit 0 = no transcendental math in the
+// numeric pass (sqrt / atan / division replaced by an add), bit 1 = no goalscore carry pass.
+#ifndef SA_NUM_PROBE
+#define SA_NUM_PROBE 0
+#endif
+#if SA_NUM_PROBE & 1
+#define NUM_SQRT(x) (x)
+#else
+#define NUM_SQRT(x) sqrt(x)
+#endif
+
 // nan_to_num(arctan(dy / dx)) of vaep/features.py:376 (atan(+-inf) = +-pi/2, 0/0 -> 0)
 __device__ __forceinline__ double polar_angle(double dy, double dx) {
+#if SA_NUM_PROBE & 1
+  return dy + dx;
+#else
   const double a = atan(dy / dx);
   return isnan(a) ? 0.0 : a;
+#endif
 }
 
 
@@ -657,7 +672,7 @@ __device__ __forceinline__ void emit_window(const NumCols& C, int i, const Win& 
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
         const double dx = fabs(FIELD_L - w.c0[e]), dy = fabs(GOAL_Y - w.c1[e]);
-        dist[e] = sqrt(dx * dx + dy * dy);
+        dist[e] = NUM_SQRT(dx * dx + dy * dy);
         ang[e] = polar_angle(dy, dx);
       }
       st_f64x2(fb, C.sp + 2 * i, C.nf, Rf, dist[0], dist[1]);
@@ -668,7 +683,7 @@ __device__ __forceinline__ void emit_window(const NumCols& C, int i, const Win& 
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
         const double dx = fabs(FIELD_L - w.c2[e]), dy = fabs(GOAL_Y - w.c3[e]);
-        dist[e] = sqrt(dx * dx + dy * dy);
+        dist[e] = NUM_SQRT(dx * dx + dy * dy);
         ang[e] = polar_angle(dy, dx);
       }
       st_f64x2(fb, C.ep + 2 * i, C.nf, Rf, dist[0], dist[1]);
@@ -680,7 +695,7 @@ __device__ __forceinline__ void emit_window(const NumCols& C, int i, const Win& 
       for (int e = 0; e < 2; ++e) {
         mdx[e] = w.c2[e] - w.c0[e];
         mdy[e] = w.c3[e] - w.c1[e];
-        mv[e] = sqrt(mdx[e] * mdx[e] + mdy[e] * mdy[e]);
+        mv[e] = NUM_SQRT(mdx[e] * mdx[e] + mdy[e] * mdy[e]);
       }
       st_f64x2(fb, C.mv + 3 * i, C.nf, Rf, mdx[0], mdx[1]);
       st_f64x2(fb, C.mv + 3 * i + 1, C.nf, Rf, mdy[0], mdy[1]);
@@ -692,7 +707,7 @@ __device__ __forceinline__ void emit_window(const NumCols& C, int i, const Win& 
       for (int e = 0; e < 2; ++e) {
         sdx[e] = w.c2[e] - sx0[e];
         sdy[e] = w.c3[e] - sy0[e];
-        sm[e] = sqrt(sdx[e] * sdx[e] + sdy[e] * sdy[e]);
+        sm[e] = NUM_SQRT(sdx[e] * sdx[e] + sdy[e] * sdy[e]);
       }
       st_f64x2(fb, C.sd + 3 * (i - 1), C.nf, Rf, sdx[0], sdx[1]);
       st_f64x2(fb, C.sd + 3 * (i - 1) + 1, C.nf, Rf, sdy[0], sdy[1]);
@@ -708,7 +723,7 @@ __device__ __forceinline__ void emit_window(const NumCols& C, int i, const Win& 
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
         const double dx = fabs(FIELD_L - w.c0[e]), dy = fabs(GOAL_Y - w.c1[e]);
-        dist[e] = sqrt(dx * dx + dy * dy);
+        dist[e] = NUM_SQRT(dx * dx + dy * dy);
         ang[e] = polar_angle(dy, dx);
       }
       st_f64x2(fb, C.po + 2 * i, C.nf, Rf, dist[0], dist[1]);
@@ -873,7 +888,7 @@ __device__ __forceinline__ void goalscore_pair(const sa_actions& A, int64_t wb, 
   const int lane = threadIdx.x & (WAVE - 1);
   const SegCursor c0 = wave_cursor(A, wb);  // segment of the wave's first row (uniform)
   uint64_t carry = 0;
-  if (c0.s < wb) carry = wave_goals<ATOMIC>(F, n, c0.s, wb, F.team[c0.s]);
+  if (c0.s < wb && !(SA_NUM_PROBE & 2)) carry = wave_goals<ATOMIC>(F, n, c0.s, wb, F.team[c0.s]);
   bool gA[2], gB[2], isA[2];
   int64_t s[2];
 #pragma unroll
@@ -1738,7 +1753,11 @@ extern "C" int sa_vaep_step_f64(const sa_actions* a, const sa_feature_plan* plan
       return fail(SA_EINVAL, "xT cell codes need 1 <= l * w <= %d", SA_XT_CELLS_MAX_C);
     if (!aligned16(xt_cells)) return fail(SA_EINVAL, "xt_cells must be 16-byte aligned");
   }
-  if (plan->nb_prev_actions > 3 || nr_actions > SA_STEP_MAX_NR) {  // no fused form: the separate launches
+  // no fused form: the separate launches.  Atomic actions always take them: their numeric pass
+  // (136 VGPRs, 3 waves per SIMD) loses more to the tail's registers than the tail's launch
+  // costs (cfg3, 4.0e7 atomic actions: 3.89 ms separate vs 4.35 ms fused, scripts/atomic_ab.py,
+  // profiles/r03_atomic_ab.json)
+  if (a->atomic || plan->nb_prev_actions > 3 || nr_actions > SA_STEP_MAX_NR) {
     if ((rc = launch_features(a, plan, bool_out, f64_out, i64_out, xt_l, xt_w, xt_cells, stream))) return rc;
     if (!formula) return sa_vaep_labels(a, nr_actions, scores, concedes, goal_from_shot, ld, stream);
     return sa_vaep_labels_formula_f64(a, nr_actions, scores, concedes, goal_from_shot, ld, p_scores,
