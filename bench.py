@@ -739,7 +739,7 @@ def main() -> None:
     ap.add_argument('--num-tile', type=int, default=128,
                     help='rows per f64/i64-block tile (0 = one tile: plain column-major)')
     ap.add_argument('--alloc-order', default='contig',
-                    choices=('contig', 'bool-first', 'num-first', 'single', 'single-bool-first'),
+                    choices=('contig', 'contig-all', 'bool-first', 'num-first', 'single', 'single-bool-first'),
                     help='output blocks: contig = the bool block in physically contiguous VRAM '
                          '(default; profiles/r02u_goalscore_fused_ab.md r02aq - r02au), else '
                          'placement A/B knobs (bool-first = three caching-allocator blocks)')
@@ -756,9 +756,10 @@ def main() -> None:
     ab = B.ActionBatch.from_columns(d, dev=dev)
     n = ab.n
     plan = catalog.build_plan(SPADL_DEFAULT, 3)
-    if args.alloc_order == 'contig':  # the bool block in physically contiguous VRAM (default)
+    if args.alloc_order in ('contig', 'contig-all'):  # the bool block (or all three) in contiguous VRAM
         out = ops.alloc_feature_blocks(plan, n, dev, bool_tile=args.bool_tile or None,
-                                       num_tile=args.num_tile or None, contiguous=True)
+                                       num_tile=args.num_tile or None,
+                                       contiguous='all' if args.alloc_order == 'contig-all' else True)
     elif args.alloc_order in ('num-first', 'single', 'single-bool-first'):  # dev knob: block placement A/B
         Rb, Rn = args.bool_tile or (n + 15) // 16 * 16, args.num_tile or (n + 15) // 16 * 16
         shapes = [((-(-n // Rn), plan.n_f64, Rn), torch.float64), ((-(-n // Rn), plan.n_i64, Rn), torch.int64),

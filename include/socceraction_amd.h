@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define SA_ABI_VERSION 2
+#define SA_ABI_VERSION 3
 #define SA_MAX_FRAMES 8 /* max nb_prev_actions (window frames) */
 #define SA_BOOL_TILE_QUANTUM 1024 /* bool block: rows per tile must be a multiple of this */
 #define SA_NUM_TILE_QUANTUM 128   /* f64 / i64 blocks: rows per tile must be a multiple of this */
@@ -82,7 +82,19 @@ typedef struct sa_actions {
   int32_t n_frames;
   int32_t atomic;           /* 0 = SPADL, 1 = Atomic-SPADL */
   sa_frame frames[SA_MAX_FRAMES];
+  /* optional (NULL = binary search of seg_off): segment of row b * SA_SEG_BLOCK for every
+   * block b < ceil(n / SA_SEG_BLOCK), written once per batch by sa_segment_blocks.  The kernels
+   * start every wave's segment cursor from it instead of a ~log2(n_segments)-deep chain of
+   * dependent loads. */
+  const int32_t* seg_of_block;
 } sa_actions;
+
+#define SA_SEG_BLOCK 128
+
+/* seg_of_block[b] = the segment holding row b * SA_SEG_BLOCK, b < ceil(n / SA_SEG_BLOCK), from
+ * the segment offsets (seg_off[0] = 0 <= ... <= seg_off[n_segments] = n). Asynchronous. */
+int sa_segment_blocks(const int64_t* seg_off, int64_t n_segments, int64_t n, int32_t* seg_of_block,
+                      void* stream);
 
 /* Feature transformers (reference vaep/features.py, atomic/vaep/features.py). */
 enum sa_xfn {

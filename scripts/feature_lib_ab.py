@@ -52,10 +52,34 @@ def main():
     bb, fb, ib = out.sa_blocks()
     res = {'n': ab.n, 'atomic': args.atomic, 'ms': {}, 'equal': {}}
     ref = None
+    # the bench step's numeric pass (sa_vaep_step_f64: + xT cell codes, labels, f64 formula)
+    ld = (ab.n + 15) // 16 * 16
+    lab = torch.empty((3, ld), dtype=torch.uint8, device=ab.device)
+    val = torch.empty((3, ld), dtype=torch.float64, device=ab.device)
+    ps = torch.rand(ab.n, dtype=torch.float64, device=ab.device)
+    pc = torch.rand(ab.n, dtype=torch.float64, device=ab.device)
+    cells = ops.xt_cells_buffer(ab.n, ab.device)
+    tags = (('num', num), ('all', plan)) + ((('step', num), ('step_nocells', num), ('step_labels', num),
+                                             ('num_cells', num)) if not args.atomic else ())
     for rnd in range(3):
         for name, lib in libs.items():
-            for tag, p in (('num', num), ('all', plan)):
+            for tag, p in tags:
                 def run():
+                    if tag.startswith('step'):  # step: cells + labels + formula; the parts dropped
+                        nc, lo = tag == 'step_nocells', tag == 'step_labels'
+                        N.check(lib.sa_vaep_step_f64(
+                            ctypes.byref(s), ctypes.byref(p.struct), ctypes.byref(bb), ctypes.byref(fb),
+                            ctypes.byref(ib), 0 if nc else 16, 0 if nc else 12, None if nc else cells.data_ptr(),
+                            10, lab[0].data_ptr(), lab[1].data_ptr(), None, ld,
+                            None if lo else ps.data_ptr(), None if lo else pc.data_ptr(),
+                            None if lo else val[0].data_ptr(), None if lo else val[1].data_ptr(),
+                            None if lo else val[2].data_ptr(), stream))
+                        return
+                    if tag == 'num_cells':
+                        N.check(lib.sa_vaep_features_xt(ctypes.byref(s), ctypes.byref(p.struct), ctypes.byref(bb),
+                                                        ctypes.byref(fb), ctypes.byref(ib), 16, 12,
+                                                        cells.data_ptr(), stream))
+                        return
                     N.check(lib.sa_vaep_features(ctypes.byref(s), ctypes.byref(p.struct), ctypes.byref(bb),
                                                  ctypes.byref(fb), ctypes.byref(ib), stream))
                 run()

@@ -20,6 +20,7 @@ DEBUG_LIB = os.path.join(HERE, '_lib', 'libsocceraction_amd_debug.so')
 LIB_PATH = os.environ.get('SOCCERACTION_AMD_LIB') or (DEBUG_LIB if DEBUG else DEFAULT_LIB)
 
 SA_MAX_FRAMES = 8
+SA_SEG_BLOCK = 128  # rows per entry of sa_actions.seg_of_block
 SA_XT_SOLVE_MAX_C = 1024  # sa_xt_solve: larger grids may pass trans_t = NULL
 SA_XT_CELLS_MAX_C = 4096
 SA_BOOL_TILE_QUANTUM = 1024
@@ -48,7 +49,7 @@ class SaFrame(ctypes.Structure):
 class SaActions(ctypes.Structure):
     _fields_ = [('n', ctypes.c_int64), ('n_segments', ctypes.c_int64), ('seg_off', _p),
                 ('home_team', _p), ('n_frames', ctypes.c_int32), ('atomic', ctypes.c_int32),
-                ('frames', SaFrame * SA_MAX_FRAMES)]
+                ('frames', SaFrame * SA_MAX_FRAMES), ('seg_of_block', _p)]
 
 
 class SaFeaturePlan(ctypes.Structure):
@@ -181,6 +182,7 @@ _SIGNATURES = {
     'sa_device_alloc': (ctypes.c_int, [ctypes.c_int64, ctypes.c_int32, ctypes.POINTER(ctypes.c_void_p)]),
     'sa_device_free': (ctypes.c_int, [_p]),
     'sa_abi_version': (ctypes.c_int, []),
+    'sa_segment_blocks': (ctypes.c_int, [_p, ctypes.c_int64, ctypes.c_int64, _p, _p]),
     'sa_last_error': (ctypes.c_char_p, []),
     'sa_build_id': (ctypes.c_char_p, []),
     'sa_debug_enabled': (ctypes.c_int, []),
@@ -216,7 +218,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.sa_abi_version() != 2:
+    if lib.sa_abi_version() != 3:
         raise ImportError('libsocceraction_amd ABI version mismatch')
     _check_build_id(lib, path)
     if path == LIB_PATH:

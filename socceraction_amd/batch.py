@@ -222,11 +222,28 @@ class ActionBatch:
         fr.type_id, fr.result_id = ptr('type_id'), ptr('result_id')
         fr.bodypart_id, fr.period_id, fr.team = ptr('bodypart_id'), ptr('period_id'), ptr('team')
 
+    def _seg_blocks(self) -> Optional[int]:
+        """Device pointer of the segment of every SA_SEG_BLOCK-row block (``sa_segment_blocks``),
+        built once per batch, or None for a single segment (nothing to search)."""
+        if self.n_segments <= 1 or self.n == 0:
+            return None
+        t = self.cols.get('seg_of_block')
+        if t is None:
+            from . import _native
+            t = torch.empty(-(-self.n // _native.SA_SEG_BLOCK), dtype=torch.int32, device=self.device)
+            st = torch.cuda.current_stream()
+            _native.check(_native.lib().sa_segment_blocks(self.cols['seg_off'].data_ptr(), self.n_segments,
+                                                          self.n, t.data_ptr(), st.cuda_stream))
+            st.synchronize()  # once per batch: every stream may use the table afterwards
+            self.cols['seg_of_block'] = t
+        return t.data_ptr()
+
     def struct(self, flip: bool = True) -> SaActions:
         s = SaActions()
         s.n = self.n
         s.n_segments = self.n_segments
         s.seg_off = self.cols['seg_off'].data_ptr()
+        s.seg_of_block = self._seg_blocks()
         s.home_team = self.cols['home'].data_ptr() if (flip and 'home' in self.cols) else None
         s.n_frames = 1
         s.atomic = int(self.atomic)

@@ -120,6 +120,25 @@ extern "C" int sa_device_free(void* p) {
 }
 
 extern "C" int sa_abi_version(void) { return SA_ABI_VERSION; }
+
+// one thread per segment: the blocks whose first row lies in [seg_off[g], seg_off[g+1])
+__global__ void segment_blocks_kernel(const int64_t* __restrict__ seg_off, int64_t nseg,
+                                      int32_t* __restrict__ seg_of_block) {
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= nseg) return;
+  const int64_t s = seg_off[g], e = seg_off[g + 1];
+  for (int64_t b = (s + SA_SEG_BLOCK - 1) / SA_SEG_BLOCK; b * SA_SEG_BLOCK < e; ++b) seg_of_block[b] = (int32_t)g;
+}
+
+extern "C" int sa_segment_blocks(const int64_t* seg_off, int64_t n_segments, int64_t n, int32_t* seg_of_block,
+                                 void* stream) {
+  if (!seg_off || !seg_of_block || n_segments < 1 || n < 0 || n_segments > INT32_MAX)
+    return fail(SA_EINVAL, "bad segment block args");
+  if (n == 0) return SA_OK;
+  hipLaunchKernelGGL(segment_blocks_kernel, dim3((unsigned)((n_segments + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, seg_off, n_segments, seg_of_block);
+  return check_launch("segment_blocks_kernel");
+}
 extern "C" const char* sa_last_error(void) { return sa::g_err; }
 
 // The build id is also kept as a plain marker string, so a build script can tell which sources

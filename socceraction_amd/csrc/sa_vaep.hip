@@ -193,6 +193,19 @@ struct SegCursor {
 
 __device__ __forceinline__ SegCursor seg_at(const sa_actions& A, int64_t j) {
   SegCursor c;
+  if (A.seg_of_block) {  // the segment of the row's block start, then forward to the row
+    c.g = A.seg_of_block[j / SA_SEG_BLOCK];
+    SA_DCHECK(c.g >= 0 && c.g < A.n_segments, c.g);
+    c.s = A.seg_off[c.g];
+    c.e = A.seg_off[c.g + 1];
+    while (j >= c.e) {
+      ++c.g;
+      SA_DGUARD(c.g < A.n_segments, j, --c.g; break);
+      c.s = c.e;
+      c.e = A.seg_off[c.g + 1];
+    }
+    return c;
+  }
   c.g = find_segment(A.seg_off, A.n_segments, j);
   c.s = A.seg_off[c.g];
   c.e = A.seg_off[c.g + 1];
@@ -299,7 +312,11 @@ __device__ __forceinline__ void st_f64x2(double* __restrict__ base, int64_t col,
                                          double v0, double v1) {
   f64x2 v = {v0, v1};
   SA_DGUARD(col >= 0 && col < C, col, return);
+#if SA_NUM_PROBE & 8  // probe: the f64 block is not written (wrong outputs)
+  if (v0 == 1.2345e300) st16(base + col * R, v);
+#else
   st16(base + col * R, v);
+#endif
 }
 
 __device__ __forceinline__ void st_i64x2(int64_t* __restrict__ base, int64_t col, int64_t C, int64_t R,
@@ -335,9 +352,14 @@ __device__ __forceinline__ void st_i64x2(float* __restrict__ base, int64_t col, 
 }
 
 // SA_NUM_PROBE (diagnostic builds only, wrong values): bit 0 = no transcendental math in the
-// numeric pass (sqrt / atan / division replaced by an add), bit 1 = no goalscore carry pass.
+// numeric pass (sqrt / atan / division replaced by an add), bit 1 = no goalscore carry pass,
+// bit 2 = no coordinate / time reads, bit 3 = no f64-block stores, bit 5 = no goalscore /
+// label / formula stores (the stores that precede the main row loads).
 #ifndef SA_NUM_PROBE
 #define SA_NUM_PROBE 0
+#endif
+#ifndef SA_NUM_FAMILY_MAJOR
+#define SA_NUM_FAMILY_MAJOR 0  // numeric pass store order (num_features_kernel, KF = 3)
 #endif
 #if SA_NUM_PROBE & 1
 #define NUM_SQRT(x) (x)
@@ -642,32 +664,42 @@ struct Win {  // one game-state window of the lane's 2 actions (flipped coordina
   int32_t per[2], typ[2], res[2], bp[2];
 };
 
-// Every f64 / i64 column of window i (features.py:151-499, atomic/vaep/features.py:135-226).
+// Column families of the numeric pass (emit_window's `fam`): FAM_ALL = every family of window
+// i; otherwise one family, so a caller can write the columns family by family (each family's
+// windows are adjacent block columns).
+enum { FAM_ALL = -1, FAM_IDS = 0, FAM_TIME, FAM_SL, FAM_EL, FAM_SP, FAM_EP, FAM_MV, FAM_TD, FAM_SD,
+       FAM_LO, FAM_PO, FAM_MP, FAM_DI };
+#define FAM_ON(f) (fam == FAM_ALL || fam == (f))
+
+// Every f64 / i64 column of window i (features.py:151-499, atomic/vaep/features.py:135-226), or
+// only family `fam`'s.
 template <bool ATOMIC, typename FT, typename IT>
 __device__ __forceinline__ void emit_window(const NumCols& C, int i, const Win& w,
                                             const double (&sx0)[2], const double (&sy0)[2],
                                             const double (&t0)[2], FT* __restrict__ fb,
-                                            IT* __restrict__ ib, int64_t Rf, int64_t Ri) {
-  if (C.at >= 0) st_i64x2(ib, C.at + i, C.ni, Ri, w.typ[0], w.typ[1]);
-  if (C.re >= 0) st_i64x2(ib, C.re + i, C.ni, Ri, w.res[0], w.res[1]);
-  if (C.bi >= 0) st_i64x2(ib, C.bi + i, C.ni, Ri, w.bp[0], w.bp[1]);
-  if (C.ti >= 0) st_i64x2(ib, C.ti + i, C.ni, Ri, w.per[0], w.per[1]);
-  if (C.tf >= 0) {
+                                            IT* __restrict__ ib, int64_t Rf, int64_t Ri, int fam = FAM_ALL) {
+  if (FAM_ON(FAM_IDS)) {
+    if (C.at >= 0) st_i64x2(ib, C.at + i, C.ni, Ri, w.typ[0], w.typ[1]);
+    if (C.re >= 0) st_i64x2(ib, C.re + i, C.ni, Ri, w.res[0], w.res[1]);
+    if (C.bi >= 0) st_i64x2(ib, C.bi + i, C.ni, Ri, w.bp[0], w.bp[1]);
+  }
+  if (FAM_ON(FAM_TIME) && C.ti >= 0) st_i64x2(ib, C.ti + i, C.ni, Ri, w.per[0], w.per[1]);
+  if (FAM_ON(FAM_TIME) && C.tf >= 0) {
     st_f64x2(fb, C.tf + 2 * i, C.nf, Rf, w.ts[0], w.ts[1]);
     // ((period_id - 1) * 45 * 60) + time_seconds   (features.py:313)
     st_f64x2(fb, C.tf + 2 * i + 1, C.nf, Rf, (double)((w.per[0] - 1) * 2700) + w.ts[0],
              (double)((w.per[1] - 1) * 2700) + w.ts[1]);
   }
   if (!ATOMIC) {
-    if (C.sl >= 0) {
+    if (FAM_ON(FAM_SL) && C.sl >= 0) {
       st_f64x2(fb, C.sl + 2 * i, C.nf, Rf, w.c0[0], w.c0[1]);
       st_f64x2(fb, C.sl + 2 * i + 1, C.nf, Rf, w.c1[0], w.c1[1]);
     }
-    if (C.el >= 0) {
+    if (FAM_ON(FAM_EL) && C.el >= 0) {
       st_f64x2(fb, C.el + 2 * i, C.nf, Rf, w.c2[0], w.c2[1]);
       st_f64x2(fb, C.el + 2 * i + 1, C.nf, Rf, w.c3[0], w.c3[1]);
     }
-    if (C.sp >= 0) {
+    if (FAM_ON(FAM_SP) && C.sp >= 0) {
       double dist[2], ang[2];
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
@@ -678,7 +710,7 @@ __device__ __forceinline__ void emit_window(const NumCols& C, int i, const Win& 
       st_f64x2(fb, C.sp + 2 * i, C.nf, Rf, dist[0], dist[1]);
       st_f64x2(fb, C.sp + 2 * i + 1, C.nf, Rf, ang[0], ang[1]);
     }
-    if (C.ep >= 0) {
+    if (FAM_ON(FAM_EP) && C.ep >= 0) {
       double dist[2], ang[2];
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
@@ -689,7 +721,7 @@ __device__ __forceinline__ void emit_window(const NumCols& C, int i, const Win& 
       st_f64x2(fb, C.ep + 2 * i, C.nf, Rf, dist[0], dist[1]);
       st_f64x2(fb, C.ep + 2 * i + 1, C.nf, Rf, ang[0], ang[1]);
     }
-    if (C.mv >= 0) {
+    if (FAM_ON(FAM_MV) && C.mv >= 0) {
       double mdx[2], mdy[2], mv[2];
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
@@ -701,7 +733,7 @@ __device__ __forceinline__ void emit_window(const NumCols& C, int i, const Win& 
       st_f64x2(fb, C.mv + 3 * i + 1, C.nf, Rf, mdy[0], mdy[1]);
       st_f64x2(fb, C.mv + 3 * i + 2, C.nf, Rf, mv[0], mv[1]);
     }
-    if (i >= 1 && C.sd >= 0) {  // space_delta: a_i end - a0 start (features.py:491-499)
+    if (FAM_ON(FAM_SD) && i >= 1 && C.sd >= 0) {  // space_delta: a_i end - a0 start (features.py:491-499)
       double sdx[2], sdy[2], sm[2];
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
@@ -714,11 +746,11 @@ __device__ __forceinline__ void emit_window(const NumCols& C, int i, const Win& 
       st_f64x2(fb, C.sd + 3 * (i - 1) + 2, C.nf, Rf, sm[0], sm[1]);
     }
   } else {
-    if (C.lo >= 0) {
+    if (FAM_ON(FAM_LO) && C.lo >= 0) {
       st_f64x2(fb, C.lo + 2 * i, C.nf, Rf, w.c0[0], w.c0[1]);
       st_f64x2(fb, C.lo + 2 * i + 1, C.nf, Rf, w.c1[0], w.c1[1]);
     }
-    if (C.po >= 0) {
+    if (FAM_ON(FAM_PO) && C.po >= 0) {
       double dist[2], ang[2];
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
@@ -729,7 +761,7 @@ __device__ __forceinline__ void emit_window(const NumCols& C, int i, const Win& 
       st_f64x2(fb, C.po + 2 * i, C.nf, Rf, dist[0], dist[1]);
       st_f64x2(fb, C.po + 2 * i + 1, C.nf, Rf, ang[0], ang[1]);
     }
-    if (C.mp >= 0) {  // atomic/vaep/features.py:196-199
+    if (FAM_ON(FAM_MP) && C.mp >= 0) {  // atomic/vaep/features.py:196-199
       double md[2], ma[2];
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
@@ -739,7 +771,7 @@ __device__ __forceinline__ void emit_window(const NumCols& C, int i, const Win& 
       st_f64x2(fb, C.mp + 2 * i, C.nf, Rf, md[0], md[1]);
       st_f64x2(fb, C.mp + 2 * i + 1, C.nf, Rf, ma[0], ma[1]);
     }
-    if (C.di >= 0) {  // atomic/vaep/features.py:219-224
+    if (FAM_ON(FAM_DI) && C.di >= 0) {  // atomic/vaep/features.py:219-224
       double ox[2], oy[2];
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
@@ -751,7 +783,7 @@ __device__ __forceinline__ void emit_window(const NumCols& C, int i, const Win& 
       st_f64x2(fb, C.di + 2 * i + 1, C.nf, Rf, oy[0], oy[1]);
     }
   }
-  if (i >= 1 && C.td >= 0)  // time_delta: a0 time - a_i time (features.py:469-473)
+  if (FAM_ON(FAM_TD) && i >= 1 && C.td >= 0)  // time_delta: a0 time - a_i time (features.py:469-473)
     st_f64x2(fb, C.td + (i - 1), C.nf, Rf, t0[0] - w.ts[0], t0[1] - w.ts[1]);
 }
 
@@ -798,11 +830,16 @@ __device__ __forceinline__ void load_row1(const sa_frame& F, int64_t r, bool ato
 
 // rows r, r+1 (r even: 16-B aligned f64 pairs, 2-B aligned id pairs)
 __device__ __forceinline__ void load_pair(const sa_frame& F, int64_t r, bool atomic, Row& a, Row& b) {
+#if SA_NUM_PROBE & 4  // probe: no coordinate / time reads (wrong values)
+  const double q = (double)(r & 1023);
+  const f64x2 x0 = {q, q + 1}, x1 = {q * 0.5, q}, x2 = {q + 3, q}, x3 = {q, q * 0.25}, x4 = {q, q + 2};
+#else
   const f64x2 x0 = *reinterpret_cast<const f64x2*>(F.c0 + r);
   const f64x2 x1 = *reinterpret_cast<const f64x2*>(F.c1 + r);
   const f64x2 x2 = *reinterpret_cast<const f64x2*>(F.c2 + r);
   const f64x2 x3 = *reinterpret_cast<const f64x2*>(F.c3 + r);
   const f64x2 x4 = *reinterpret_cast<const f64x2*>(F.time_seconds + r);
+#endif
   const uint32_t pe = *reinterpret_cast<const uint16_t*>(F.period_id + r);
   const uint32_t ty = *reinterpret_cast<const uint16_t*>(F.type_id + r);
   const uint32_t rs = atomic ? 0u : *reinterpret_cast<const uint16_t*>(F.result_id + r);
@@ -878,11 +915,12 @@ __device__ __forceinline__ uint64_t lane_range(int a, int b) {
 }
 
 // goalscore_team / _opponent / _diff of the lane's rows jb, jb+1 (wave rows wb .. wb+127, rows
-// >= n write don't-care padding like the other columns).  Every lane of the wave must call it;
-// `c` = a segment cursor at or before row jb (clamped to n - 1).
-template <bool ATOMIC, typename IT>
+// >= n get don't-care padding like the other columns) into v[column][row].  Loads only: the
+// caller stores after the wave's last load (see num_features_kernel).  Every lane of the wave
+// must call it; `c` = a segment cursor at or before row jb (clamped to n - 1).
+template <bool ATOMIC>
 __device__ __forceinline__ void goalscore_pair(const sa_actions& A, int64_t wb, int64_t jb, SegCursor c,
-                                               IT* __restrict__ ib, int gcol, int ni, int64_t Ri) {
+                                               int64_t (&v)[3][2]) {
   const int64_t n = A.n;
   const sa_frame& F = A.frames[0];
   const int lane = threadIdx.x & (WAVE - 1);
@@ -914,7 +952,6 @@ __device__ __forceinline__ void goalscore_pair(const sa_actions& A, int64_t wb, 
   }
   const uint64_t EA = __ballot(gA[0]), OA = __ballot(gA[1]);
   const uint64_t EB = __ballot(gB[0]), OB = __ballot(gB[1]);
-  int64_t v[3][2];
 #pragma unroll
   for (int e = 0; e < 2; ++e) {
     const int t = 2 * lane + e;                           // row offset in the wave
@@ -932,10 +969,6 @@ __device__ __forceinline__ void goalscore_pair(const sa_actions& A, int64_t wb, 
     v[1][e] = op;
     v[2][e] = tm - op;
   }
-  if (jb < n || std::is_same<IT, CondSink>::value) {  // condition sinks: the whole wave, tail rows masked
-#pragma unroll
-    for (int k = 0; k < 3; ++k) st_i64x2(ib, gcol + k, ni, Ri, v[k][0], v[k][1]);
-  }
 }
 
 // ------------------------------------------------------------------------------ tail in the
@@ -945,6 +978,10 @@ __device__ __forceinline__ void formula_rows(const sa_actions& A, const T* __res
                                              const T* __restrict__ pc, T* __restrict__ off,
                                              T* __restrict__ def, T* __restrict__ val, bool vec_ok,
                                              int64_t j0, SegCursor& cur);
+template <bool ATOMIC, typename T, typename V>
+__device__ __forceinline__ bool formula_vals(const sa_actions& A, const T* __restrict__ ps,
+                                             const T* __restrict__ pc, bool vec_ok, int64_t j0, SegCursor& cur,
+                                             V& vo, V& vd, V& vv);
 
 // goal (bit 0) / owngoal (bit 1) / shot (bit 2, atomic goal_from_shot) of row j
 template <bool ATOMIC>
@@ -963,9 +1000,8 @@ __device__ __forceinline__ uint32_t label_bits(const sa_frame& F, int64_t j) {
 // must call it; `c` = a segment cursor at or before row jb (clamped to n - 1).
 constexpr int SA_STEP_MAX_NR = 11;
 template <bool ATOMIC>
-__device__ __forceinline__ void labels_pair(const sa_actions& A, int nr, uint8_t* __restrict__ sc,
-                                            uint8_t* __restrict__ co, uint8_t* __restrict__ gfs, int64_t jb,
-                                            SegCursor c) {
+__device__ __forceinline__ void labels_pair(const sa_actions& A, int nr, int64_t jb, SegCursor c,
+                                            uint32_t& so, uint32_t& cout, uint32_t& go) {
   const int64_t n = A.n;
   const sa_frame& F = A.frames[0];
   const int lane = threadIdx.x & (WAVE - 1);
@@ -993,7 +1029,7 @@ __device__ __forceinline__ void labels_pair(const sa_actions& A, int nr, uint8_t
       bits[k] = b;
     }
   }
-  uint32_t so = 0, cout = 0, go = 0;
+  so = cout = go = 0;
 #pragma unroll
   for (int e = 0; e < 2; ++e) {
     const int64_t j = jb + e;
@@ -1024,7 +1060,13 @@ __device__ __forceinline__ void labels_pair(const sa_actions& A, int nr, uint8_t
       go |= (uint32_t)gf << (8 * e);
     }
   }
-  if (jb < n) {
+}
+
+// the labels of rows jb, jb+1 (labels_pair's bytes) into the label columns
+__device__ __forceinline__ void labels_store(int64_t n, uint8_t* __restrict__ sc, uint8_t* __restrict__ co,
+                                             uint8_t* __restrict__ gfs, int64_t jb, uint32_t so, uint32_t cout,
+                                             uint32_t go) {
+  if (jb < n && !(SA_NUM_PROBE & 32)) {
     if (jb + 1 < n) {
       if (sc) *reinterpret_cast<uint16_t*>(sc + jb) = (uint16_t)so;
       if (co) *reinterpret_cast<uint16_t*>(co + jb) = (uint16_t)cout;
@@ -1041,8 +1083,16 @@ __device__ __forceinline__ void labels_pair(const sa_actions& A, int nr, uint8_t
 // once (16-B loads) and the windows are formed in registers (see the loop below).
 // KF = 0: any mode / any k (explicit frames: k <= SA_MAX_FRAMES; windowed: any k): per-window
 // row loads.
+#ifndef SA_NUM_WAVES
+#define SA_NUM_WAVES 0  // > 0: ask the compiler for that many waves per SIMD (register cap)
+#endif
+#if SA_NUM_WAVES > 0
+#define NUM_OCCUPANCY __attribute__((amdgpu_waves_per_eu(SA_NUM_WAVES, 8)))
+#else
+#define NUM_OCCUPANCY
+#endif
 template <bool ATOMIC, bool EXPLICIT, int KF, bool TAIL = false, bool N32 = false, bool COND = false>
-__global__ __launch_bounds__(256) void num_features_kernel(FeatArgs args) {
+__global__ __launch_bounds__(256) NUM_OCCUPANCY void num_features_kernel(FeatArgs args) {
   // N32: the f64 and i64 blocks hold float32 values (sa_vaep_features_bits_f32); COND: no blocks,
   // the columns' split conditions as bitmaps (sa_vaep_features_conditions)
   using FT = typename std::conditional<COND, CondSink, typename std::conditional<N32, float, double>::type>::type;
@@ -1072,26 +1122,86 @@ __global__ __launch_bounds__(256) void num_features_kernel(FeatArgs args) {
   };
   SegCursor cur = {0, 0, 0};
   const int gcol = EXPLICIT ? -1 : P.i64_col[SA_XFN_GOALSCORE];
+  // A lane owns rows jb, jb+1 (NUM_PAIRS == 1).  Every load of the wave -- its rows, the goal
+  // credits, the label look-ahead, the probabilities -- is issued before its first store: on
+  // gfx950 a wait for a load also waits for every store issued before it (one vmcnt), so a
+  // store-then-load order made each wave sit out several write round trips.
+  const int64_t jw = wave_base + 2 * lane;  // this lane's first row (may be >= n in the last wave)
+  int64_t jb = jw;
+  if (COND && jb >= n) jb = (n - 1) & ~(int64_t)1;
+  const int64_t jq = jb < n ? jb : ((n - 1) & ~(int64_t)1);  // rows this lane loads (clamped)
+  int64_t jr[2];
+  jr[0] = jq;
+  jr[1] = jq + 1 < n ? jq + 1 : n - 1;  // padded tail rows recompute row n-1
+  Row cand[2], pool[2];
+  if (KF == 3) {
+    // the pair's window rows: cand = rows jb, jb+1, pool = the older rows jb-1, jb-2
+    if (jq >= 2 && jq + 2 <= n) {
+      load_pair(F0, jq, ATOMIC, cand[0], cand[1]);
+      load_pair(F0, jq - 2, ATOMIC, pool[1], pool[0]);
+    } else {  // first rows of the batch or the tail: guarded scalar loads
+      load_row1(F0, jr[0], ATOMIC, cand[0]);
+      load_row1(F0, jr[1], ATOMIC, cand[1]);
+      load_row1(F0, jq - 1 < 0 ? 0 : jq - 1, ATOMIC, pool[0]);
+      load_row1(F0, jq - 2 < 0 ? 0 : jq - 2, ATOMIC, pool[1]);
+    }
+  }
+  // the block addresses of rows jb, jb+1 (column 0; COND: the condition sinks), before any store
+  // so that no address arithmetic waits behind one
+  FT* fb = fblock(jq);
+  IT* ib = iblock(jq);
+  IT* gib = iblock((jw < n ? jw : n - 1) & ~(int64_t)1);
+  int64_t gs[3][2];
+  uint32_t lso = 0, lco = 0, lgo = 0;
+  f64x2 fo, fd, fv;
+  bool fok = false;
+  int dd[2] = {0, 0};
+  bool away[2] = {false, false};
   if (!EXPLICIT) {
-    const int64_t jl = wave_base + 2 * lane < n ? wave_base + 2 * lane : n - 1;
+    const int64_t jl = jw < n ? jw : n - 1;
     cur = wave_cursor(A, wave_base);
     seg_advance(A, cur, jl);
-    if (gcol >= 0)
-      goalscore_pair<ATOMIC, IT>(A, wave_base, wave_base + 2 * lane, cur,
-                                 iblock(jl & ~(int64_t)1),
-                                 gcol, (int)args.Ci, Ri);
+    if (gcol >= 0) goalscore_pair<ATOMIC>(A, wave_base, jw, cur, gs);
     if (TAIL) {  // labels + formula of the same rows (every lane of the wave present)
-      labels_pair<ATOMIC>(A, args.nr, args.sc, args.co, args.gfs, wave_base + 2 * lane, cur);
+      labels_pair<ATOMIC>(A, args.nr, jw, cur, lso, lco, lgo);
       if (args.ps) {  // uniform: labels only when no probabilities are given
         SegCursor fc = cur;
-        formula_rows<ATOMIC, double>(A, args.ps, args.pc, args.off, args.def, args.val, args.vec_ok,
-                                     wave_base + 2 * lane, fc);
+        fok = formula_vals<ATOMIC, double>(A, args.ps, args.pc, args.vec_ok, jw, fc, fo, fd, fv);
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int64_t j = jr[e];
+      seg_advance(A, cur, j);
+      const int64_t d = j - cur.s;
+      dd[e] = d > WIDE_D_MAX ? WIDE_D_MAX : (int)d;  // compared with the window index only
+      away[e] = A.home_team != nullptr && F0.team[j] != A.home_team[cur.g];
+    }
+    // -- every load is out; the stores follow
+    if (gcol >= 0 && (jw < n || COND) && !(SA_NUM_PROBE & 32)) {  // condition sinks: whole wave, tail masked
+#pragma unroll
+      for (int k = 0; k < 3; ++k) st_i64x2(gib, gcol + k, (int)args.Ci, Ri, gs[k][0], gs[k][1]);
+    }
+    if (TAIL) {
+      labels_store(n, args.sc, args.co, args.gfs, jw, lso, lco, lgo);
+      if (fok && !(SA_NUM_PROBE & 32)) {
+#if SA_NUM_PROBE & 64  // probe: the formula values into the f64 tile's last three columns
+        if constexpr (!COND && !N32) {
+          st16(fb + (args.Cf - 3) * Rf, fo);
+          st16(fb + (args.Cf - 2) * Rf, fd);
+          st16(fb + (args.Cf - 1) * Rf, fv);
+        }
+#else
+        st16(args.off + jw, fo);
+        st16(args.def + jw, fd);
+        st16(args.val + jw, fv);
+#endif
       }
     }
   }
   // COND: every lane stays (the ballots and the chunk stores need the whole wave); lanes past the
   // end recompute the last pair and their bits are masked off in cond_store
-  if (!COND && wave_base + 2 * lane >= n) return;
+  if (!COND && jw >= n) return;
   NumCols C;
   C.at = P.i64_col[SA_XFN_ACTIONTYPE];
   C.re = P.i64_col[SA_XFN_RESULT];
@@ -1112,45 +1222,13 @@ __global__ __launch_bounds__(256) void num_features_kernel(FeatArgs args) {
   C.nf = (int)args.Cf;
   C.ni = (int)args.Ci;
 
-  for (int pr = 0; pr < NUM_PAIRS; ++pr) {
-    int64_t jb = wave_base + pr * 2 * WAVE + 2 * lane;
-    if (COND && jb >= n) jb = (n - 1) & ~(int64_t)1;
-    if (jb >= n) break;
-    FT* fb = fblock(jb);  // column 0 of rows jb, jb+1 (COND: the condition sinks)
-    IT* ib = iblock(jb);
-    int64_t jr[2];
-    int dd[2];
-    bool away[2];
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int64_t j = jb + e < n ? jb + e : n - 1;  // padded tail rows recompute row n-1
-      jr[e] = j;
-      dd[e] = 0;
-      away[e] = false;
-      if (!EXPLICIT) {
-        seg_advance(A, cur, j);
-        const int64_t d = j - cur.s;
-        dd[e] = d > WIDE_D_MAX ? WIDE_D_MAX : (int)d;  // compared with the window index only
-        away[e] = A.home_team != nullptr && F0.team[j] != A.home_team[cur.g];
-      }
-    }
+  {
     double sx0[2], sy0[2], t0[2];
     if (KF == 3) {
-      // Rows of the pair's windows: cand = current window rows of actions 0/1 (raw),
-      // pool = the next older rows jb-1, jb-2.  Moving from window i-1 to i, action 1 takes
-      // action 0's previous row and action 0 takes the next pool row, unless the action's
-      // window already reached its segment start (d < i): then it keeps its row.  (If
-      // action 0 is clamped so is action 1, whose d is at most d0 + 1.)
-      Row cand[2], pool[2];
-      if (jb >= 2 && jb + 2 <= n) {
-        load_pair(F0, jb, ATOMIC, cand[0], cand[1]);
-        load_pair(F0, jb - 2, ATOMIC, pool[1], pool[0]);
-      } else {  // first rows of the batch or the tail: guarded scalar loads
-        load_row1(F0, jr[0], ATOMIC, cand[0]);
-        load_row1(F0, jr[1], ATOMIC, cand[1]);
-        load_row1(F0, jb - 1 < 0 ? 0 : jb - 1, ATOMIC, pool[0]);
-        load_row1(F0, jb - 2 < 0 ? 0 : jb - 2, ATOMIC, pool[1]);
-      }
+      // Moving from window i-1 to i, action 1 takes action 0's previous row and action 0 takes
+      // the next pool row, unless the action's window already reached its segment start
+      // (d < i): then it keeps its row.  (If action 0 is clamped so is action 1, whose d is at
+      // most d0 + 1.)
       if (!ATOMIC && args.xt_cells) {  // the raw (unflipped) rows jb, jb+1: xT cell codes
         uint32_t cc[2];
 #pragma unroll
@@ -1163,6 +1241,59 @@ __global__ __launch_bounds__(256) void num_features_kernel(FeatArgs args) {
           args.xt_cells[jb] = cc[0];
         }
       }
+#if SA_NUM_FAMILY_MAJOR
+      // family by family, each family's windows back to back: the block columns are
+      // family-major with the windows adjacent, so the wave writes its [C x 128] slab front to
+      // back instead of jumping by the family width for every window.  Window i of action e
+      // is row jb + e - min(i, d_e) of the four held rows jb-2 .. jb+1 (selected, not shifted).
+      // the three windows' rows (the shift of the window-major loop below, unrolled): window 1
+      // of action 0 is row jb-1 unless d0 < 1, of action 1 row jb unless d1 < 1; and so on
+      Win w0, w1, w2;
+      {
+        const Row y0 = dd[0] >= 1 ? pool[0] : cand[0], y1 = dd[1] >= 1 ? cand[0] : cand[1];
+        const Row z0 = dd[0] >= 2 ? pool[1] : y0, z1 = dd[1] >= 2 ? y0 : y1;
+        row_to_win(cand[0], w0, 0);
+        row_to_win(cand[1], w0, 1);
+        row_to_win(y0, w1, 0);
+        row_to_win(y1, w1, 1);
+        row_to_win(z0, w2, 0);
+        row_to_win(z1, w2, 1);
+      }
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        if (!EXPLICIT && away[e]) {
+          flip<ATOMIC>(w0, e);
+          flip<ATOMIC>(w1, e);
+          flip<ATOMIC>(w2, e);
+        }
+        sx0[e] = w0.c0[e];
+        sy0[e] = w0.c1[e];
+        t0[e] = w0.ts[e];
+      }
+      auto family = [&](int fam) __attribute__((always_inline)) {
+        emit_window<ATOMIC, FT, IT>(C, 0, w0, sx0, sy0, t0, fb, ib, Rf, Ri, fam);
+        if (K > 1) emit_window<ATOMIC, FT, IT>(C, 1, w1, sx0, sy0, t0, fb, ib, Rf, Ri, fam);
+        if (K > 2) emit_window<ATOMIC, FT, IT>(C, 2, w2, sx0, sy0, t0, fb, ib, Rf, Ri, fam);
+      };
+      // the default plans' block order (catalog.py: xfns order)
+      family(FAM_IDS);
+      family(FAM_TIME);
+      if (ATOMIC) {
+        family(FAM_TD);
+        family(FAM_LO);
+        family(FAM_PO);
+        family(FAM_MP);
+        family(FAM_DI);
+      } else {
+        family(FAM_SL);
+        family(FAM_EL);
+        family(FAM_SP);
+        family(FAM_EP);
+        family(FAM_MV);
+        family(FAM_TD);
+        family(FAM_SD);
+      }
+#else
 #pragma unroll 1
       for (int i = 0; i < K; ++i) {
         if (i > 0) {
@@ -1187,6 +1318,7 @@ __global__ __launch_bounds__(256) void num_features_kernel(FeatArgs args) {
         }
         emit_window<ATOMIC, FT, IT>(C, i, wf, sx0, sy0, t0, fb, ib, Rf, Ri);
       }
+#endif
     } else {
       for (int i = 0; i < K; ++i) {
         const sa_frame& Fi = EXPLICIT ? A.frames[i] : F0;
@@ -1437,11 +1569,10 @@ __global__ __launch_bounds__(256) void labels_kernel(sa_actions A, int nr, uint8
 // Rows j0 .. j0+V-1 of one lane (V = 16 / sizeof(T)); every lane of the wave calls it with
 // consecutive j0 (the previous row comes from the neighbouring lane); `cur` = a segment cursor
 // at or before row j0, advanced by the call.
-template <bool ATOMIC, typename T>
-__device__ __forceinline__ void formula_rows(const sa_actions& A, const T* __restrict__ ps,
-                                             const T* __restrict__ pc, T* __restrict__ off,
-                                             T* __restrict__ def, T* __restrict__ val, bool vec_ok,
-                                             int64_t j0, SegCursor& cur) {
+template <bool ATOMIC, typename T, typename VT>
+__device__ __forceinline__ bool formula_vals(const sa_actions& A, const T* __restrict__ ps,
+                                             const T* __restrict__ pc, bool vec_ok, int64_t j0, SegCursor& cur,
+                                             VT& vo, VT& vd, VT& vv) {
   constexpr int V = 16 / sizeof(T);
   const int64_t n = A.n;
   const int lane = threadIdx.x & (WAVE - 1);
@@ -1500,7 +1631,7 @@ __device__ __forceinline__ void formula_rows(const sa_actions& A, const T* __res
   double tp = __shfl_up(t_[V - 1], 1, WAVE);
   int32_t tmp = __shfl_up(tm_[V - 1], 1, WAVE), typ = __shfl_up(ty_[V - 1], 1, WAVE),
           rsp = __shfl_up(rs_[V - 1], 1, WAVE);
-  if (!active) return;
+  if (!active) return false;
   if (lane == 0 && j0 > 0) {
     const int64_t p = j0 - 1;
     sp = ps[p];
@@ -1510,7 +1641,6 @@ __device__ __forceinline__ void formula_rows(const sa_actions& A, const T* __res
     typ = F.type_id[p];
     rsp = ATOMIC ? 0 : F.result_id[p];
   }
-  vec_t vo, vd, vv;
 #pragma unroll
   for (int q = 0; q < V; ++q) {
     const int64_t j = j0 + q < n ? j0 + q : n - 1;
@@ -1557,6 +1687,19 @@ __device__ __forceinline__ void formula_rows(const sa_actions& A, const T* __res
     vd[q] = d;
     vv[q] = o + d;
   }
+  return true;
+}
+
+// formula_vals of rows j0 .. j0+V-1, stored (one 16-B store per output column)
+template <bool ATOMIC, typename T>
+__device__ __forceinline__ void formula_rows(const sa_actions& A, const T* __restrict__ ps,
+                                             const T* __restrict__ pc, T* __restrict__ off,
+                                             T* __restrict__ def, T* __restrict__ val, bool vec_ok,
+                                             int64_t j0, SegCursor& cur) {
+  constexpr int V = 16 / sizeof(T);
+  typedef T vec_t __attribute__((ext_vector_type(V)));
+  vec_t vo, vd, vv;
+  if (!formula_vals<ATOMIC, T>(A, ps, pc, vec_ok, j0, cur, vo, vd, vv)) return;
   st16(off + j0, vo);
   st16(def + j0, vd);
   st16(val + j0, vv);

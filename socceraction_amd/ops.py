@@ -136,6 +136,20 @@ def alloc_feature_blocks(plan: FeaturePlan, n: int, dev, bool_tile: Optional[int
     Rn = _ld(n) if num_tile is None else int(num_tile)
     tb, tn = max(1, -(-n // Rb)), max(1, -(-n // Rn))
     bshape = (tb, plan.n_bool, Rb)
+    if contiguous == 'all':  # A/B knob: the three blocks in ONE physically contiguous range
+        fshape, ishape = (tn, plan.n_f64, Rn), (tn, plan.n_i64, Rn)
+        al = lambda b: -(-b // (2 << 20)) * (2 << 20)  # noqa: E731  (2 MiB aligned parts)
+        sizes = [int(np.prod(bshape)), 8 * int(np.prod(fshape)), 8 * int(np.prod(ishape))]
+        try:
+            arena = DeviceBuffer(al(sizes[0]) + al(sizes[1]) + max(sizes[2], 16), contiguous=True)
+        except (RuntimeError, ValueError, _native.NativeError):
+            arena = None
+        if arena is not None:
+            out = FeatureBlocks(plan, n, Rb, Rn, arena.tensor(bshape, torch.uint8),
+                                arena.tensor(fshape, torch.float64, al(sizes[0])),
+                                arena.tensor(ishape, torch.int64, al(sizes[0]) + al(sizes[1])))
+            out._arena = arena
+            return out
     arena = None
     if contiguous and plan.n_bool:
         try:

@@ -30,7 +30,7 @@ def test_library_builds_and_exports_every_declared_symbol():
     for sym in declared:
         assert hasattr(lib, sym), sym
     assert set(declared) == set(_native.EXPORTED_SYMBOLS)
-    assert lib.sa_abi_version() == 2
+    assert lib.sa_abi_version() == 3
     assert lib.sa_debug_enabled() == 0
     assert lib.sa_debug_check() == 0  # default build: no device checks, no device call
 
@@ -76,7 +76,7 @@ def test_ctypes_struct_layout_matches_header():
 
     from socceraction_amd import _native
     assert ctypes.sizeof(_native.SaFrame) == 80
-    assert ctypes.sizeof(_native.SaActions) == 40 + 8 * 80
+    assert ctypes.sizeof(_native.SaActions) == 40 + 8 * 80 + 8
     assert ctypes.sizeof(_native.SaFeaturePlan) == 4 * (1 + 3 * _native.SA_XFN_COUNT)
     assert ctypes.sizeof(_native.SaBlock) == 24
     assert ctypes.sizeof(_native.SaTreeModel) == 4 * 8 + 2 * 4 + 8 + 8  # sa_tree_model

@@ -152,6 +152,45 @@ def _small_games(syn, atomic, seed, n_small=300):
 
 
 @pytest.mark.parametrize('atomic', [False, True])
+def test_segment_block_table(sa, atomic):
+    """sa_segment_blocks: the segment of every 128-row block start equals numpy's search of the
+    offsets (one-row games, games of exactly 128 rows, a block start on a game start); and the
+    kernels started from the table (features at k = 1, 3, 12, labels, the fused step) write the
+    same bytes as the binary-search start (seg_of_block = NULL)."""
+    B, ops, syn = sa['batch'], sa['ops'], sa['synthetic']
+    from socceraction_amd import _native
+    default = vo.ATOMIC_DEFAULT if atomic else vo.SPADL_DEFAULT
+    d = _small_games(syn, atomic, 23)
+    n0 = int(d['game_off'][-1])
+    extra = np.array([128, 1, 1, 128, 256, 3, 127, 129])  # exact-block and one-row games
+    rows = {c: v for c, v in d.items() if isinstance(v, np.ndarray) and v.shape == (n0,)}
+    d = dict(d, **{c: np.concatenate([v, v[:extra.sum()]]) for c, v in rows.items()})
+    offs = n0 + np.cumsum(extra)
+    d['game_off'] = np.concatenate([d['game_off'], offs])
+    d['home_team_id'] = np.concatenate([d['home_team_id'], d['team_id'][offs - extra]])
+    ab = B.ActionBatch.from_columns(d, atomic=atomic)
+    s = ab.struct()
+    assert s.seg_of_block
+    table = ab.cols['seg_of_block'].cpu().numpy()
+    starts = np.arange(len(table)) * _native.SA_SEG_BLOCK
+    np.testing.assert_array_equal(table, np.searchsorted(d['game_off'], starts, 'right') - 1)
+    s0 = ab.struct()
+    s0.seg_of_block = None
+    for k in (1, 3, 12):
+        plan = sa['catalog'].build_plan(default, k, atomic)
+        got = [ops.alloc_feature_blocks(plan, ab.n, ab.device, 1024, 128) for _ in range(2)]
+        labs = [ops.labels(ab) for _ in range(2)]
+        for st, out, lab in zip((s, s0), got, labs):
+            for t in (out.bool_block, out.f64_block, out.i64_block, lab.scores, lab.concedes):
+                t.zero_()
+            ops.step_into(st, out, None, None, 10, lab, None)
+        for a, b in zip(got[0].__dict__.values(), got[1].__dict__.values()):
+            if isinstance(a, torch.Tensor):
+                assert torch.equal(a, b), k
+        assert torch.equal(labs[0].scores, labs[1].scores) and torch.equal(labs[0].concedes, labs[1].concedes)
+
+
+@pytest.mark.parametrize('atomic', [False, True])
 def test_many_small_segments_vs_oracle(sa, atomic):
     """Full games + 300 games of 1..40 actions in one batch: features at k = 1, 3, 5 (both
     layouts), labels at nr_actions 10 and 20 (the > 17 path reloads rows) and the formula with
