@@ -21,7 +21,7 @@ import pandas as pd
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def main(tag: str, n_actions: int, dominant: str = 'bool_colgroup_kernel') -> None:
+def main(tag: str, n_actions: int, dominant=None) -> None:
     out = os.path.join(ROOT, 'profiles')
     src = os.path.join(ROOT, 'gpurun_out')
     shutil.copy(os.path.join(src, f'prof_{tag}_trace', 'run_kernel_stats.csv'),
@@ -40,16 +40,24 @@ def main(tag: str, n_actions: int, dominant: str = 'bool_colgroup_kernel') -> No
     df['hbm_bytes_per_action'] = df['hbm_bytes'] / n_actions
     df.index.name = 'kernel'
     df.to_csv(os.path.join(out, f'{tag}_pmc.csv'))
+    if dominant is None:  # the step kernel with the longest total duration in the trace
+        st = pd.read_csv(os.path.join(out, f'{tag}_kernel_stats.csv'))
+        st = st[st.Name.str.contains('bool_colgroup_kernel|num_features_kernel')]
+        dominant = st.sort_values('TotalDurationNs').Name.iloc[-1]
     feat = [k for k in df.index if dominant in k][0]
+    rec = {'tag': tag, 'kernel': feat, 'n_actions': n_actions,
+           'fetch_kib': float(df.loc[feat, 'FETCH_SIZE']),
+           'write_kib': float(df.loc[feat, 'WRITE_SIZE']),
+           'hbm_bytes_per_launch_per_action': float(df.loc[feat, 'hbm_bytes_per_action']),
+           # every step kernel's PMC bytes, so bench.py can quote whichever its HIP events
+           # find dominant
+           'per_kernel': {k: float(df.loc[k, 'hbm_bytes_per_action']) for k in df.index
+                          if 'bool_colgroup_kernel' in k or 'num_features_kernel' in k}}
     with open(os.path.join(out, 'pmc_dominant_kernel.json'), 'w') as f:
-        json.dump({'tag': tag, 'kernel': feat, 'n_actions': n_actions,
-                   'fetch_kib': float(df.loc[feat, 'FETCH_SIZE']),
-                   'write_kib': float(df.loc[feat, 'WRITE_SIZE']),
-                   'hbm_bytes_per_launch_per_action': float(df.loc[feat, 'hbm_bytes_per_action'])},
-                  f, indent=1)
+        json.dump(rec, f, indent=1)
     print(df.to_string())
 
 
 if __name__ == '__main__':
     main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 15992198,
-         sys.argv[3] if len(sys.argv) > 3 else 'bool_colgroup_kernel')
+         sys.argv[3] if len(sys.argv) > 3 else None)
