@@ -360,8 +360,21 @@ def _num_index(order) -> int:
     return next(i for i, k in enumerate(order) if k.startswith('num_'))
 
 
-def _record(stream) -> 'torch.cuda.Event':
-    e = torch.cuda.Event()
+# the event class of the step's stream forks / joins and per-kernel timings: 'native' =
+# socceraction_amd.events.DeviceEvent (no system-scope fence on record), 'torch' =
+# torch.cuda.Event (set by --events; --ab variants may override it with ev=...)
+EVENTS = {'kind': 'native'}
+
+
+def _event(enable_timing: bool = False, kind: str = None):
+    if (kind or EVENTS['kind']) == 'native':
+        from socceraction_amd.events import DeviceEvent
+        return DeviceEvent(enable_timing)
+    return torch.cuda.Event(enable_timing=enable_timing)
+
+
+def _record(stream, kind: str = None):
+    e = _event(kind=kind)
     e.record(stream)
     return e
 
@@ -738,12 +751,17 @@ def main() -> None:
                          '3.24 - 3.31 ms per step, profiles/r02_step_ab.md), or on the side stream')
     ap.add_argument('--num-tile', type=int, default=128,
                     help='rows per f64/i64-block tile (0 = one tile: plain column-major)')
+    ap.add_argument('--events', default='native', choices=('native', 'torch'),
+                    help='event kind of the step\'s stream forks / joins and per-kernel timings: '
+                         'native = sa_event_* without the system-scope fence (default), torch = '
+                         'torch.cuda.Event')
     ap.add_argument('--alloc-order', default='contig',
                     choices=('contig', 'contig-all', 'bool-first', 'num-first', 'single', 'single-bool-first'),
                     help='output blocks: contig = the bool block in physically contiguous VRAM '
                          '(default; profiles/r02u_goalscore_fused_ab.md r02aq - r02au), else '
                          'placement A/B knobs (bool-first = three caching-allocator blocks)')
     args = ap.parse_args()
+    EVENTS['kind'] = args.events
     if args.gpus < 1:
         raise SystemExit('--gpus must be >= 1')
     if 'WORLD_SIZE' not in os.environ and args.gpus > 1:
@@ -853,6 +871,7 @@ def main() -> None:
         ib = order.index('bool_features') if par else -1
 
         pipe = int(spec.get('pipe', 1)) and overlap
+        ek = spec.get('ev', EVENTS['kind'])  # event kind of this variant
 
         def step(ev=None):
             # ev[i] = (start, end) of VAEP call i on the main stream, ev[nv] = the xT side
@@ -861,32 +880,27 @@ def main() -> None:
             pj = None
             if pipe and ring['done'][ring['k']] is not None:
                 # this step's cell-code buffer was last read by the xT rate two steps ago
-                main_s.wait_event(ring['done'][ring['k']])
+                ring['done'][ring['k']].wait(main_s)
             # zero the xT counts on the side stream (idle until the fork) while the first VAEP
             # call runs; the count pass waits for it
             zs = side if overlap else main_s
-            zs.wait_event(_record(main_s))  # after the previous step's use of the counts
+            _record(main_s, ek).wait(zs)  # after the previous step's use of the counts
             with torch.cuda.stream(zs):
                 xt_start.zero()
-            zev = _record(zs)
+            zev = _record(zs, ek)
             if par:
-                pf = torch.cuda.Event()
-                pf.record(main_s)
-                par_s.wait_event(pf)
+                _record(main_s, ek).wait(par_s)
                 with torch.cuda.stream(par_s):
                     calls[ib]()
-                pj = torch.cuda.Event()
-                pj.record(par_s)
+                pj = _record(par_s, ek)
             for i, call in enumerate(calls):
                 if overlap and i == fork:
                     if cm:  # the count pass on the main stream; its all-reduce on the side
                         if ev is not None:
                             ev[nv][0].record(main_s)
-                        main_s.wait_event(zev)
+                        zev.wait(main_s)
                         xt_start.count()
-                    fk = torch.cuda.Event()
-                    fk.record(main_s)
-                    side.wait_event(fk)
+                    _record(main_s, ek).wait(side)
                     with torch.cuda.stream(side):
                         if ev is not None and not cm:
                             ev[nv][0].record(side)
@@ -895,7 +909,7 @@ def main() -> None:
                         else:
                             xt_start()
                 if par and i == ib:
-                    main_s.wait_event(pj)
+                    pj.wait(main_s)
                     continue
                 if ev is not None:
                     ev[i][0].record(main_s)
@@ -903,7 +917,7 @@ def main() -> None:
                 if ev is not None:
                     ev[i][1].record(main_s)
             if not overlap or fork >= nv:  # serial, or forked after the last VAEP call
-                (side if overlap else main_s).wait_event(_record(main_s))
+                _record(main_s, ek).wait(side if overlap else main_s)
                 with torch.cuda.stream(side):
                     if ev is not None:
                         ev[nv][0].record(side)
@@ -913,12 +927,11 @@ def main() -> None:
                 if ev is not None:
                     ev[nv][1].record(side)
             if pipe:  # pipelined: the xT work of this step overlaps the next step's passes
-                ring['done'][ring['k']] = _record(side)
+                ring['done'][ring['k']] = _record(side, ek)
                 ring['k'] ^= 1
             elif overlap:
-                join = torch.cuda.Event()
-                join.record(side)
-                main_s.wait_event(join)
+                _record(side, ek).wait(main_s)
+        step.ev_kind = ek
         return step, xt_last
 
     base = {'xt': args.xt_source, 'order': args.order.split(','), 'fork': args.xt_fork,
@@ -933,7 +946,7 @@ def main() -> None:
             v = dict(base)
             for kv in [o for o in opts.split('/') if o]:
                 k_, _, v_ = kv.partition('=')
-                v[k_] = v_.split('+') if k_ == 'order' else (int(v_) if k_ in ('fork', 'par', 'cm', 'diag', 'xsync', 'pipe') else v_)
+                v[k_] = v_.split('+') if k_ == 'order' else (int(v_) if k_ in ('fork', 'par', 'cm', 'diag', 'xsync', 'pipe', 'tev') else v_)
             variants[name] = (make_step(v)[0], v['order'])
         ab_ms = {k: [] for k in variants}
         ab_kern = {}
@@ -950,7 +963,7 @@ def main() -> None:
                 torch.cuda.synchronize()
                 ab_ms[k].append(round((time.perf_counter() - t) / args.steps * 1e3, 4))
         for k, (fn, vorder) in variants.items():  # per-call HIP event means, one more round
-            evs = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            evs = [[(_event(True, fn.ev_kind), _event(True, fn.ev_kind))
                     for _ in range(len(vorder) + 1)] for _ in range(args.steps)]
             for e in evs:
                 fn(e)
@@ -966,8 +979,7 @@ def main() -> None:
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    evs = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-            for _ in range(nv + 1)] for _ in range(args.steps)]
+    evs = [[(_event(True), _event(True)) for _ in range(nv + 1)] for _ in range(args.steps)]
     if dist:
         dist.barrier()
     torch.cuda.synchronize()

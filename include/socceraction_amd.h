@@ -457,6 +457,29 @@ int sa_dribble_count(const sa_spadl_frame* in, double min_len2, double max_len2,
 int sa_dribble_emit(const sa_spadl_frame* in, double min_len2, double max_len2, double max_dt,
                     const void* scratch, const int64_t* dest, const sa_spadl_out* out, void* stream);
 
+/* ---- convert_to_atomic, general form ----------------------------------------------
+ * For frames whose (game_id, period_id, action_id) keys repeat or lie no more than 0.1 apart inside a game and period (then the rows _extra_from_passes inserts do not all
+ * sort directly after their parents; base.py:82,109-110).  The first pass runs on its own:
+ *   sa_atomic_passes_flags: flags[j] (device u8 [n]) = 1 when input row j gets a receival /
+ *     interception / out / offside row (its INPUT-order successor decides, base.py:39-73);
+ *     in->order must be NULL.
+ *   sa_atomic_passes_emit: writes the n + m rows of the reference's concat (the n inputs, then
+ *     the m inserted rows of `parents` [device, the flagged rows in input order]) as SPADL rows
+ *     at dest[k] (device int64 [n + m]: the position of concatenated row k in the stable sort
+ *     of (game, period, action_id / action_id + 0.1), from the host).  Inserted rows carry
+ *     start = end = the parent's end, the midpoint time, bodypart foot, result 255 (the
+ *     reference's -1) and the atomic type id; src = input row, or ~parent for an inserted row.
+ *   sa_atomic_count_after_passes / sa_atomic_emit_after_passes: sa_atomic_count / emit of that
+ *     sorted output (order NULL) without the first pass -- the reference's remaining passes
+ *     (_add_dribbles, _extra_from_shots, _extra_from_fouls) and the column conversion. */
+int sa_atomic_passes_flags(const sa_spadl_frame* in, uint8_t* flags, void* stream);
+int sa_atomic_passes_emit(const sa_spadl_frame* in, const int64_t* parents, int64_t m,
+                          const int64_t* dest, const sa_spadl_out* out, void* stream);
+int sa_atomic_count_after_passes(const sa_spadl_frame* in, void* scratch, int64_t* n_out,
+                                 void* stream);
+int sa_atomic_emit_after_passes(const sa_spadl_frame* in, const void* scratch,
+                                const sa_atomic_frame* out, void* stream);
+
 /* Segment (game) offsets of a row-sorted key column whose values are exactly 0..n_segments-1,
  * each present -- e.g. the game codes of sa_atomic_emit's output:
  * seg_off[g] = first row of g, seg_off[n_segments] = n. */
@@ -536,6 +559,18 @@ int sa_shutdown(void);
  * (hipDeviceMallocContiguous: the largest translation fragments).  Free with sa_device_free. */
 int sa_device_alloc(int64_t bytes, int32_t flags, void** out);
 int sa_device_free(void* p);
+/* Stream-ordering and timing events for device-local work: created with
+ * hipEventDisableSystemFence, so recording one does not write back and invalidate the GPU's
+ * caches the way a default event does (its system-scope release is what a host or peer reader
+ * needs, not another stream of the same device: kernel boundaries already release to the
+ * device).  timing = 0 also sets hipEventDisableTiming.  The bench step records its stream
+ * forks / joins and per-kernel timings with these (torch.cuda.Event has no such flag). */
+int sa_event_create(int32_t timing, void** ev);
+int sa_event_destroy(void* ev);
+int sa_event_record(void* ev, void* stream);
+int sa_stream_wait_event(void* stream, void* ev);
+int sa_event_synchronize(void* ev);
+int sa_event_elapsed(void* start, void* end, float* ms);
 /* Debug build (-DSA_DEBUG=1, libsocceraction_amd_debug.so): kernels check tile offsets,
  * column indices, segment cursors, LDS and grid-cell indices and record the first failure
  * instead of accessing out of bounds.  sa_debug_check() synchronises the device and returns

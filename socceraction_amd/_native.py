@@ -163,6 +163,13 @@ _SIGNATURES = {
                                         ctypes.c_double, ctypes.c_double, _p, _p, _p,
                                         ctypes.POINTER(ctypes.c_int64),
                                         ctypes.POINTER(ctypes.c_int64), _p]),
+    'sa_atomic_passes_flags': (ctypes.c_int, [ctypes.POINTER(SaSpadlFrame), _p, _p]),
+    'sa_atomic_passes_emit': (ctypes.c_int, [ctypes.POINTER(SaSpadlFrame), _p, ctypes.c_int64, _p,
+                                             ctypes.POINTER(SaSpadlOut), _p]),
+    'sa_atomic_count_after_passes': (ctypes.c_int, [ctypes.POINTER(SaSpadlFrame), _p,
+                                                    ctypes.POINTER(ctypes.c_int64), _p]),
+    'sa_atomic_emit_after_passes': (ctypes.c_int, [ctypes.POINTER(SaSpadlFrame), _p,
+                                                   ctypes.POINTER(SaAtomicFrame), _p]),
     'sa_dribble_emit': (ctypes.c_int, [ctypes.POINTER(SaSpadlFrame), ctypes.c_double,
                                        ctypes.c_double, ctypes.c_double, _p, _p,
                                        ctypes.POINTER(SaSpadlOut), _p]),
@@ -181,6 +188,12 @@ _SIGNATURES = {
                                               ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, _p]),
     'sa_device_alloc': (ctypes.c_int, [ctypes.c_int64, ctypes.c_int32, ctypes.POINTER(ctypes.c_void_p)]),
     'sa_device_free': (ctypes.c_int, [_p]),
+    'sa_event_create': (ctypes.c_int, [ctypes.c_int32, ctypes.POINTER(ctypes.c_void_p)]),
+    'sa_event_destroy': (ctypes.c_int, [_p]),
+    'sa_event_record': (ctypes.c_int, [_p, _p]),
+    'sa_stream_wait_event': (ctypes.c_int, [_p, _p]),
+    'sa_event_synchronize': (ctypes.c_int, [_p]),
+    'sa_event_elapsed': (ctypes.c_int, [_p, _p, ctypes.POINTER(ctypes.c_float)]),
     'sa_abi_version': (ctypes.c_int, []),
     'sa_segment_blocks': (ctypes.c_int, [_p, ctypes.c_int64, ctypes.c_int64, _p, _p]),
     'sa_last_error': (ctypes.c_char_p, []),

@@ -83,27 +83,34 @@ def _ids(df: pd.DataFrame, col: str, lo: int, hi: int) -> np.ndarray:
     return v.astype(np.uint8)
 
 
-def _sorted_order(g: np.ndarray, per: np.ndarray, aid: np.ndarray) -> Optional[np.ndarray]:
-    """None when the rows already are in (game_id, period_id, action_id) order, else the
-    stable sort permutation the reference's sort_values applies (base.py:110). Equal keys
-    would let the reference interleave inserted rows of different parents: rejected."""
+def _key_layout(g: np.ndarray, per: np.ndarray, aid) -> Tuple[Optional[np.ndarray], bool]:
+    """(order, general) for the rows' (game, period, action_id) keys.  ``order`` is None when the
+    rows already are in that order, else the stable sort permutation the reference's
+    sort_values applies (base.py:110).  ``general`` is True when the single expansion's layout
+    -- every row _extra_from_passes inserts (key action_id + 0.1, base.py:82) sorts directly
+    after its parent -- may not be the reference's order: keys that repeat, or two consecutive
+    keys of one game and period no more than 0.1 apart.  Such frames take the general path
+    (the first pass on its own, placed by the host's stable lexsort; ``convert_device``)."""
     n = len(g)
     if n < 2:
-        return None
+        return None, False
     aid = np.asarray(aid)
     if aid.dtype.kind not in 'iuf':
         raise ValueError('action_id must be numeric')
+
+    def tight(gg, pp, aa):  # any consecutive pair of one game and period with a + 0.1 >= next
+        same = (np.diff(gg.astype(np.int64)) == 0) & (np.diff(pp.astype(np.int64)) == 0)
+        a = aa.astype(np.float64)
+        return bool((same & ~(a[:-1] + 0.1 < a[1:])).any())
 
     def strictly_increasing(gg, pp, aa):
         d_g, d_p, d_a = np.diff(gg.astype(np.int64)), np.diff(pp.astype(np.int64)), np.diff(aa)
         return bool(((d_g > 0) | ((d_g == 0) & ((d_p > 0) | ((d_p == 0) & (d_a > 0))))).all())
 
     if strictly_increasing(g, per, aid):
-        return None
+        return None, tight(g, per, aid)
     order = np.lexsort((aid, per, g)).astype(np.int64)
-    if not strictly_increasing(g[order], per[order], aid[order]):
-        raise ValueError('duplicate (game_id, period_id, action_id) keys are not supported')
-    return order
+    return order, tight(g[order], per[order], aid[order])
 
 
 @dataclass
@@ -115,6 +122,11 @@ class SpadlFrame:
     cols: Dict[str, torch.Tensor]
     uniques: Dict[str, pd.Index]
     dtypes: Dict[str, np.dtype]
+    # general path (see _key_layout): the host keys (game codes, period, action_id as f64) the
+    # first pass sorts on; None on the single-expansion path
+    keys: Optional[Tuple[np.ndarray, np.ndarray, np.ndarray]] = None
+    # True for the first pass's sorted output (sa_atomic_passes_emit): converted without it
+    after_passes: bool = False
 
     @classmethod
     def from_frame(cls, actions: pd.DataFrame, dev=None, sort: bool = True) -> 'SpadlFrame':
@@ -143,12 +155,14 @@ class SpadlFrame:
             'result_id': _ids(actions, 'result_id', 0, 5),
             'bodypart_id': _ids(actions, 'bodypart_id', 0, 3),
         }
-        order = _sorted_order(g, per, actions['action_id'].to_numpy()) if sort else None
-        if order is not None:
+        aid = actions['action_id'].to_numpy()
+        order, general = _key_layout(g, per, aid) if sort else (None, False)
+        if order is not None and not general:
             arrays['order'] = order
         buf, views = _pack(arrays, dev)
         dtypes = {c: actions[c].dtype for c in ('game_id', 'team_id', 'player_id')}
-        return cls(n, buf, views, {'game': gu, 'team': tu, 'player': pu, 'event': eu}, dtypes)
+        keys = (g, per, aid.astype(np.float64)) if general else None
+        return cls(n, buf, views, {'game': gu, 'team': tu, 'player': pu, 'event': eu}, dtypes, keys)
 
     @classmethod
     def from_columns(cls, d: Dict[str, np.ndarray], dev=None) -> 'SpadlFrame':
@@ -167,15 +181,16 @@ class SpadlFrame:
         arrays.update(game=g, team=t, player=p, event=np.full(n, -1, np.int32))
         for c in ('period_id', 'type_id', 'result_id', 'bodypart_id'):
             arrays[c] = np.asarray(d[c]).astype(np.uint8)
-        aid = d['pos'] if 'pos' in d else np.arange(n)
-        order = _sorted_order(g, arrays['period_id'], np.asarray(aid))
-        if order is not None:
+        aid = np.asarray(d['pos'] if 'pos' in d else np.arange(n))
+        order, general = _key_layout(g, arrays['period_id'], aid)
+        if order is not None and not general:
             arrays['order'] = order
         buf, views = _pack(arrays, dev)
         dtypes = {'game_id': np.dtype(np.int64), 'team_id': np.dtype(np.int64),
                   'player_id': np.dtype(np.int64)}
+        keys = (g, arrays['period_id'], aid.astype(np.float64)) if general else None
         return cls(n, buf, views, {'game': gu, 'team': tu, 'player': pu,
-                                   'event': pd.Index([])}, dtypes)
+                                   'event': pd.Index([])}, dtypes, keys)
 
     def struct(self) -> _native.SaSpadlFrame:
         s = _native.SaSpadlFrame()
@@ -223,16 +238,56 @@ class AtomicColumns:
         return s
 
 
+def first_pass_device(frame: SpadlFrame) -> SpadlFrame:
+    """The general path's first pass (``_extra_from_passes``, base.py:38-112) on its own: the
+    device flags the rows that get an inserted row (input-order successor), the host places the
+    reference's concat [inputs, inserted rows] by the stable lexsort of their keys
+    (base.py:109-110), and the device writes the sorted rows.  Returns them as a frame in sorted
+    order (no ``order``) for the remaining passes."""
+    from ...spadl.base import SpadlRows, _F64, _U8
+    lib = _native.lib()
+    dev = frame.buffer.device
+    n = frame.n
+    s = frame.struct()
+    flags = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
+    _native.check(lib.sa_atomic_passes_flags(ctypes.byref(s), flags.data_ptr(), stream_handle()))
+    j = np.flatnonzero(flags[:n].cpu().numpy()).astype(np.int64)
+    m = len(j)
+    g, per, aid = frame.keys
+    kg = np.concatenate([g, g[j]]).astype(np.int64)
+    kp = np.concatenate([per, per[j]]).astype(np.int64)
+    ka = np.concatenate([aid, aid[j] + 0.1])
+    order = np.lexsort((ka, kp, kg))  # stable, like sort_values on several keys
+    pos = np.empty(n + m, np.int64)
+    pos[order] = np.arange(n + m, dtype=np.int64)
+    dest = torch.from_numpy(pos).to(dev)
+    parents = torch.from_numpy(j if m else np.zeros(1, np.int64)).to(dev)
+    spec = {c: np.float64 for c in _F64}
+    spec.update(game=np.int32, team=np.int32, player=np.int32, event=np.int32)
+    spec.update({c: np.uint8 for c in _U8})
+    buf, cols = _alloc(spec, n + m, dev)
+    cols['src'] = torch.empty(n + m, dtype=torch.int64, device=dev)
+    rows = SpadlRows(n + m, m, buf, cols)
+    o = rows.struct()
+    _native.check(lib.sa_atomic_passes_emit(ctypes.byref(s), parents.data_ptr(), m, dest.data_ptr(),
+                                            ctypes.byref(o), stream_handle()))
+    keep = dict(cols, _dest=dest, _parents=parents)  # alive until the stream has used them
+    return SpadlFrame(n + m, buf, keep, frame.uniques, frame.dtypes, None, True)
+
+
 def convert_device(frame: SpadlFrame) -> AtomicColumns:
     """Run the conversion on device; the result stays in HBM."""
     lib = _native.lib()
+    if frame.keys is not None and not frame.after_passes:
+        frame = first_pass_device(frame)
+    count, emit = ((lib.sa_atomic_count_after_passes, lib.sa_atomic_emit_after_passes)
+                   if frame.after_passes else (lib.sa_atomic_count, lib.sa_atomic_emit))
     dev = frame.buffer.device
     s = frame.struct()
     scratch = torch.empty(max(int(lib.sa_atomic_scratch_bytes(frame.n)), 16), dtype=torch.uint8,
                           device=dev)
     n_out = ctypes.c_int64(0)
-    _native.check(lib.sa_atomic_count(ctypes.byref(s), scratch.data_ptr(), ctypes.byref(n_out),
-                                      stream_handle()))
+    _native.check(count(ctypes.byref(s), scratch.data_ptr(), ctypes.byref(n_out), stream_handle()))
     m = int(n_out.value)
     spec = {'time_seconds': np.float64, 'x': np.float64, 'y': np.float64, 'dx': np.float64,
             'dy': np.float64, 'game': np.int32, 'team': np.int32, 'player': np.int32,
@@ -241,8 +296,7 @@ def convert_device(frame: SpadlFrame) -> AtomicColumns:
     out = AtomicColumns(m, buf, cols)
     if m:
         o = out.struct()
-        _native.check(lib.sa_atomic_emit(ctypes.byref(s), scratch.data_ptr(), ctypes.byref(o),
-                                         stream_handle()))
+        _native.check(emit(ctypes.byref(s), scratch.data_ptr(), ctypes.byref(o), stream_handle()))
     return out
 
 

@@ -69,7 +69,7 @@ int scratch_acquire(size_t bytes, hipStream_t st, Scratch* out) {
     (void)hipGetLastError();
     return fail(SA_ENOMEM, "scratch arena: hipMalloc of %zu bytes failed", cap);
   }
-  if ((rc = check_hip(hipEventCreateWithFlags(&s.done, hipEventDisableTiming), "hipEventCreate"))) {
+  if ((rc = check_hip(hipEventCreateWithFlags(&s.done, hipEventDisableTiming | hipEventDisableSystemFence), "hipEventCreate"))) {
     (void)hipFree(s.ptr);
     return rc;
   }
@@ -117,6 +117,37 @@ extern "C" int sa_device_alloc(int64_t bytes, int32_t flags, void** out) {
 
 extern "C" int sa_device_free(void* p) {
   return p ? check_hip(hipFree(p), "sa_device_free: hipFree") : SA_OK;
+}
+
+extern "C" int sa_event_create(int32_t timing, void** ev) {
+  if (!ev) return fail(SA_EINVAL, "sa_event_create: null output");
+  *ev = nullptr;
+  const unsigned flags = hipEventDisableSystemFence | (timing ? 0u : (unsigned)hipEventDisableTiming);
+  return check_hip(hipEventCreateWithFlags(reinterpret_cast<hipEvent_t*>(ev), flags), "sa_event_create");
+}
+
+extern "C" int sa_event_destroy(void* ev) {
+  return ev ? check_hip(hipEventDestroy((hipEvent_t)ev), "sa_event_destroy") : SA_OK;
+}
+
+extern "C" int sa_event_record(void* ev, void* stream) {
+  if (!ev) return fail(SA_EINVAL, "sa_event_record: null event");
+  return check_hip(hipEventRecord((hipEvent_t)ev, (hipStream_t)stream), "sa_event_record");
+}
+
+extern "C" int sa_stream_wait_event(void* stream, void* ev) {
+  if (!ev) return fail(SA_EINVAL, "sa_stream_wait_event: null event");
+  return check_hip(hipStreamWaitEvent((hipStream_t)stream, (hipEvent_t)ev, 0), "sa_stream_wait_event");
+}
+
+extern "C" int sa_event_synchronize(void* ev) {
+  if (!ev) return fail(SA_EINVAL, "sa_event_synchronize: null event");
+  return check_hip(hipEventSynchronize((hipEvent_t)ev), "sa_event_synchronize");
+}
+
+extern "C" int sa_event_elapsed(void* start, void* end, float* ms) {
+  if (!start || !end || !ms) return fail(SA_EINVAL, "sa_event_elapsed: null argument");
+  return check_hip(hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)end), "sa_event_elapsed");
 }
 
 extern "C" int sa_abi_version(void) { return SA_ABI_VERSION; }

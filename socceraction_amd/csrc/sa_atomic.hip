@@ -93,6 +93,28 @@ struct Group {
   double e1_t;
 };
 
+// e1 of row R followed in INPUT order by Q (base.py:65-107): a pass-like action followed by a
+// non-interception in the same game and period gets a receival / interception / out / offside
+// row at its end; false when it gets none
+__device__ __forceinline__ bool e1_of(const SRow& R, const SRow& Q, int& type, int32_t& team, int32_t& player,
+                                      double& t) {
+  if (!is_passlike(R.type) || Q.game != R.game || Q.per != R.per || is_interceptionlike(Q.type)) return false;
+  const bool st = Q.team == R.team;
+  const bool out = (Q.type == T_GOALKICK && !st) || Q.type == T_THROW_IN;
+  const bool offside = R.res == 2;
+  int ty = st ? A_RECEIVAL : A_INTERCEPTION;
+  if (out) ty = A_OUT;
+  if (offside) ty = A_OFFSIDE;
+  type = ty;
+  team = ty == A_INTERCEPTION ? Q.team : R.team;
+  player = (out || offside) ? R.player : Q.player;
+  t = (R.t + Q.t) / 2;
+  return true;
+}
+
+// PASSES = false: the frame already went through _extra_from_passes (the general first pass,
+// sa_atomic_passes_emit), so no row gets an e1 here
+template <bool PASSES = true>
 __device__ __forceinline__ Group group_at(const sa_spadl_frame& F, int64_t p) {
   const int64_t n = F.n;
   Group G;
@@ -104,22 +126,9 @@ __device__ __forceinline__ Group group_at(const sa_spadl_frame& F, int64_t p) {
   G.mask = 0;
   // e1: pass-like action followed (in INPUT order) by a non-interception in the same game
   // and period
-  const bool has_q = r + 1 < n;
-  if (has_q && is_passlike(R.type)) {
+  if (PASSES && r + 1 < n && is_passlike(R.type)) {
     const SRow Q = (F.order == nullptr && has_rp) ? G.rp : load_srow(F, r + 1);
-    if (Q.game == R.game && Q.per == R.per && !is_interceptionlike(Q.type)) {
-      const bool st = Q.team == R.team;
-      const bool out = (Q.type == T_GOALKICK && !st) || Q.type == T_THROW_IN;
-      const bool offside = R.res == 2;
-      int t = st ? A_RECEIVAL : A_INTERCEPTION;
-      if (out) t = A_OUT;
-      if (offside) t = A_OFFSIDE;
-      G.mask |= G_E1;
-      G.e1_type = t;
-      G.e1_team = t == A_INTERCEPTION ? Q.team : R.team;
-      G.e1_player = (out || offside) ? R.player : Q.player;
-      G.e1_t = (R.t + Q.t) / 2;
-    }
+    if (e1_of(R, Q, G.e1_type, G.e1_team, G.e1_player, G.e1_t)) G.mask |= G_E1;
   }
   if (has_rp) {
     if (G.mask & G_E1) {
@@ -221,10 +230,11 @@ __device__ __forceinline__ int64_t block_excl_scan(int64_t v, int64_t* wsum, int
   return pre + incl - v;
 }
 
+template <bool PASSES>
 __global__ __launch_bounds__(AC_THREADS) void atomic_count_kernel(sa_spadl_frame F, int64_t* __restrict__ bsum) {
   __shared__ int64_t wsum[AC_THREADS / 64];
   const int64_t p = (int64_t)blockIdx.x * AC_BLOCK_ROWS + threadIdx.x;
-  const int64_t c = p < F.n ? group_size(group_at(F, p).mask) : 0;
+  const int64_t c = p < F.n ? group_size(group_at<PASSES>(F, p).mask) : 0;
   int64_t total;
   block_excl_scan(c, wsum, total);
   if (threadIdx.x == 0) bsum[blockIdx.x] = total;
@@ -288,6 +298,7 @@ __global__ __launch_bounds__(SC_THREADS) void atomic_scan_kernel(int64_t* __rest
 // columns) and copied out with consecutive threads on consecutive rows, so every global
 // store instruction is a contiguous run instead of 64 scattered 8-B writes (16M SPADL rows:
 // 4.2 -> 0.61 ms).
+template <bool PASSES>
 __global__ __launch_bounds__(AC_THREADS) void atomic_emit_kernel(sa_spadl_frame F, const int64_t* __restrict__ bpre,
                                                                 sa_atomic_frame O) {
   __shared__ double lds[5 * AC_MAX_OUT];  // 51,200 B
@@ -297,7 +308,7 @@ __global__ __launch_bounds__(AC_THREADS) void atomic_emit_kernel(sa_spadl_frame 
   Group G;
   int c = 0;
   if (live) {
-    G = group_at(F, p);
+    G = group_at<PASSES>(F, p);
     c = group_size(G.mask);
   }
   int64_t total;
@@ -524,6 +535,54 @@ __global__ __launch_bounds__(AC_THREADS) void dribble_emit_kernel(sa_spadl_frame
     for (int k = threadIdx.x; k < tot; k += AC_THREADS) uo[col][base + k] = lu[col * DE_MAX_OUT + k];
 }
 
+// ---- the general first pass (base.py:38-112) ---------------------------------------------
+// For frames whose (game, period, action_id) keys repeat, or lie less than 0.1 apart, the e1
+// rows do not all land right after their parents, so the first pass runs on its own: flags of
+// the rows that get one (INPUT-order successor, as the reference's shift(-1)), then every row of
+// the reference's concat [inputs, e1 rows in input order] is written at its position in the
+// stable sort (dest, from the host).  After it the keys are 0..n+m-1 (the reference resets
+// action_id), and the remaining passes run as the single expansion without e1 (PASSES = false).
+__global__ __launch_bounds__(AC_THREADS) void atomic_passes_flags_kernel(sa_spadl_frame F,
+                                                                        uint8_t* __restrict__ flags) {
+  const int64_t j = (int64_t)blockIdx.x * AC_THREADS + threadIdx.x;
+  if (j >= F.n) return;
+  bool on = false;
+  if (j + 1 < F.n) {
+    const SRow R = load_srow(F, j);
+    if (is_passlike(R.type)) {
+      int ty;
+      int32_t tm, pl;
+      double t;
+      on = e1_of(R, load_srow(F, j + 1), ty, tm, pl, t);
+    }
+  }
+  flags[j] = on;
+}
+
+__global__ __launch_bounds__(AC_THREADS) void atomic_passes_emit_kernel(sa_spadl_frame F,
+                                                                       const int64_t* __restrict__ parents,
+                                                                       int64_t m, const int64_t* __restrict__ dest,
+                                                                       sa_spadl_out O) {
+  const int64_t i = (int64_t)blockIdx.x * AC_THREADS + threadIdx.x;
+  if (i >= F.n + m) return;
+  if (i < F.n) {
+    const SRow R = load_srow(F, i);
+    put_spadl_row(O, dest[i], R.t, R.sx, R.sy, R.ex, R.ey, R.game, R.team, R.player, R.event, R.per, R.type,
+                  R.res, R.bp, i);
+    return;
+  }
+  const int64_t p = parents[i - F.n];
+  SA_DGUARD(p >= 0 && p + 1 < F.n, p, return);
+  const SRow R = load_srow(F, p);
+  int ty = 0;
+  int32_t tm = 0, pl = 0;
+  double t = 0.0;
+  e1_of(R, load_srow(F, p + 1), ty, tm, pl, t);
+  // start = end = the parent's end; bodypart foot; result -1 (kept as 255: no later pass reads
+  // it as a result the reference would match); the parent's event
+  put_spadl_row(O, dest[i], t, R.ex, R.ey, R.ex, R.ey, R.game, tm, pl, R.event, R.per, ty, 255, 0, ~p);
+}
+
 // seg_off[key[k]] = k at every run start of the sorted keys 0..n_seg-1 (each present)
 __global__ __launch_bounds__(256) void segment_offsets_kernel(const int32_t* __restrict__ key, int64_t n,
                                                               int64_t n_seg, int64_t* __restrict__ seg_off) {
@@ -554,7 +613,8 @@ static int check_spadl_frame(const sa_spadl_frame* F) {
   return SA_OK;
 }
 
-extern "C" int sa_atomic_count(const sa_spadl_frame* in, void* scratch, int64_t* n_out, void* stream) {
+template <bool PASSES>
+static int atomic_count(const sa_spadl_frame* in, void* scratch, int64_t* n_out, void* stream) {
   int rc = check_spadl_frame(in);
   if (rc) return rc;
   if (!n_out || (in->n > 0 && !scratch)) return fail(SA_EINVAL, "null scratch or n_out");
@@ -563,7 +623,7 @@ extern "C" int sa_atomic_count(const sa_spadl_frame* in, void* scratch, int64_t*
   hipStream_t st = (hipStream_t)stream;
   const int64_t nb = n_blocks(in->n);
   int64_t* bsum = (int64_t*)scratch;
-  hipLaunchKernelGGL(atomic_count_kernel, dim3((unsigned)nb), dim3(AC_THREADS), 0, st, *in, bsum);
+  hipLaunchKernelGGL(atomic_count_kernel<PASSES>, dim3((unsigned)nb), dim3(AC_THREADS), 0, st, *in, bsum);
   if ((rc = check_launch("atomic_count_kernel"))) return rc;
   hipLaunchKernelGGL(atomic_scan_kernel, dim3(1), dim3(SC_THREADS), 0, st, bsum, nb);
   if ((rc = check_launch("atomic_scan_kernel"))) return rc;
@@ -573,8 +633,8 @@ extern "C" int sa_atomic_count(const sa_spadl_frame* in, void* scratch, int64_t*
   return check_hip(hipStreamSynchronize(st), "hipStreamSynchronize");
 }
 
-extern "C" int sa_atomic_emit(const sa_spadl_frame* in, const void* scratch, const sa_atomic_frame* out,
-                              void* stream) {
+template <bool PASSES>
+static int atomic_emit(const sa_spadl_frame* in, const void* scratch, const sa_atomic_frame* out, void* stream) {
   int rc = check_spadl_frame(in);
   if (rc) return rc;
   if (in->n == 0) return SA_OK;
@@ -583,9 +643,60 @@ extern "C" int sa_atomic_emit(const sa_spadl_frame* in, const void* scratch, con
       !out->bodypart_id)
     return fail(SA_EINVAL, "null scratch or output column");
   const int64_t nb = n_blocks(in->n);
-  hipLaunchKernelGGL(atomic_emit_kernel, dim3((unsigned)nb), dim3(AC_THREADS), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(atomic_emit_kernel<PASSES>, dim3((unsigned)nb), dim3(AC_THREADS), 0, (hipStream_t)stream,
                      *in, (const int64_t*)scratch, *out);
   return check_launch("atomic_emit_kernel");
+}
+
+extern "C" int sa_atomic_count(const sa_spadl_frame* in, void* scratch, int64_t* n_out, void* stream) {
+  return atomic_count<true>(in, scratch, n_out, stream);
+}
+
+extern "C" int sa_atomic_emit(const sa_spadl_frame* in, const void* scratch, const sa_atomic_frame* out,
+                              void* stream) {
+  return atomic_emit<true>(in, scratch, out, stream);
+}
+
+extern "C" int sa_atomic_count_after_passes(const sa_spadl_frame* in, void* scratch, int64_t* n_out,
+                                            void* stream) {
+  if (in && in->order) return fail(SA_EINVAL, "the first pass's output is sorted: order must be NULL");
+  return atomic_count<false>(in, scratch, n_out, stream);
+}
+
+extern "C" int sa_atomic_emit_after_passes(const sa_spadl_frame* in, const void* scratch,
+                                           const sa_atomic_frame* out, void* stream) {
+  if (in && in->order) return fail(SA_EINVAL, "the first pass's output is sorted: order must be NULL");
+  return atomic_emit<false>(in, scratch, out, stream);
+}
+
+static bool spadl_out_ok(const sa_spadl_out* out) {
+  return out && out->time_seconds && out->start_x && out->start_y && out->end_x && out->end_y && out->game &&
+         out->team && out->player && out->event && out->period_id && out->type_id && out->result_id &&
+         out->bodypart_id && out->src;
+}
+
+extern "C" int sa_atomic_passes_flags(const sa_spadl_frame* in, uint8_t* flags, void* stream) {
+  int rc = check_spadl_frame(in);
+  if (rc) return rc;
+  if (in->order) return fail(SA_EINVAL, "_extra_from_passes reads rows in input order: order must be NULL");
+  if (in->n == 0) return SA_OK;
+  if (!flags) return fail(SA_EINVAL, "null flags");
+  hipLaunchKernelGGL(atomic_passes_flags_kernel, dim3((unsigned)n_blocks(in->n)), dim3(AC_THREADS), 0,
+                     (hipStream_t)stream, *in, flags);
+  return check_launch("atomic_passes_flags_kernel");
+}
+
+extern "C" int sa_atomic_passes_emit(const sa_spadl_frame* in, const int64_t* parents, int64_t m,
+                                     const int64_t* dest, const sa_spadl_out* out, void* stream) {
+  int rc = check_spadl_frame(in);
+  if (rc) return rc;
+  if (in->order) return fail(SA_EINVAL, "_extra_from_passes reads rows in input order: order must be NULL");
+  if (m < 0 || m > in->n || (m > 0 && !parents)) return fail(SA_EINVAL, "bad parents");
+  if (in->n == 0) return SA_OK;
+  if (!dest || !spadl_out_ok(out)) return fail(SA_EINVAL, "null dest or output column");
+  hipLaunchKernelGGL(atomic_passes_emit_kernel, dim3((unsigned)n_blocks(in->n + m)), dim3(AC_THREADS), 0,
+                     (hipStream_t)stream, *in, parents, m, dest, *out);
+  return check_launch("atomic_passes_emit_kernel");
 }
 
 static int check_dribble_rule(double min2, double max2, double max_dt) {

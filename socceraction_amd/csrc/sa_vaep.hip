@@ -353,7 +353,8 @@ __device__ __forceinline__ void st_i64x2(float* __restrict__ base, int64_t col, 
 
 // SA_NUM_PROBE (diagnostic builds only, wrong values): bit 0 = no transcendental math in the
 // numeric pass (sqrt / atan / division replaced by an add), bit 1 = no goalscore carry pass,
-// bit 2 = no coordinate / time reads, bit 3 = no f64-block stores, bit 5 = no goalscore /
+// bit 2 = no coordinate / time reads, bit 3 = no f64-block stores, bit 7 = coordinate / time
+// reads from the first 8192 rows (L2 hits), bit 5 = no goalscore /
 // label / formula stores (the stores that precede the main row loads).
 #ifndef SA_NUM_PROBE
 #define SA_NUM_PROBE 0
@@ -833,6 +834,13 @@ __device__ __forceinline__ void load_pair(const sa_frame& F, int64_t r, bool ato
 #if SA_NUM_PROBE & 4  // probe: no coordinate / time reads (wrong values)
   const double q = (double)(r & 1023);
   const f64x2 x0 = {q, q + 1}, x1 = {q * 0.5, q}, x2 = {q + 3, q}, x3 = {q, q * 0.25}, x4 = {q, q + 2};
+#elif SA_NUM_PROBE & 128  // probe: coordinate / time reads from the first 8192 rows (L2 hits; wrong values)
+  const int64_t rq = r & 8190;
+  const f64x2 x0 = *reinterpret_cast<const f64x2*>(F.c0 + rq);
+  const f64x2 x1 = *reinterpret_cast<const f64x2*>(F.c1 + rq);
+  const f64x2 x2 = *reinterpret_cast<const f64x2*>(F.c2 + rq);
+  const f64x2 x3 = *reinterpret_cast<const f64x2*>(F.c3 + rq);
+  const f64x2 x4 = *reinterpret_cast<const f64x2*>(F.time_seconds + rq);
 #else
   const f64x2 x0 = *reinterpret_cast<const f64x2*>(F.c0 + r);
   const f64x2 x1 = *reinterpret_cast<const f64x2*>(F.c1 + r);

@@ -75,14 +75,32 @@ def test_convert_unsorted_and_errors(conv):
     assert_convert_equal(_cols(out), co.convert_to_atomic(_cols(shuffled)), 'shuffled')
     with pytest.raises(AttributeError):
         conv.convert_to_atomic(df.drop(columns=['player_id']))
+    # a repeated key takes the general path (first pass placed by the stable lexsort)
     dup = df.copy()
     dup.loc[5, 'action_id'] = dup.loc[4, 'action_id']
-    with pytest.raises(ValueError):
-        conv.convert_to_atomic(dup)
+    assert_convert_equal(_cols(conv.convert_to_atomic(dup)), co.convert_to_atomic(_cols(dup)), 'dup')
     bad = df.copy()
     bad.loc[3, 'type_id'] = 23
     with pytest.raises(ValueError):
         conv.convert_to_atomic(bad)
+
+
+def test_convert_duplicate_keys_vs_oracle(conv):
+    """Repeated (game_id, period_id, action_id) keys at scale (general path: the first pass
+    on its own, then the single expansion without it) == the four-pass restatement, sorted
+    and shuffled; the reference-generated dupkeys goldens pin the small cases."""
+    from oracle import atomic_convert_oracle as co
+    from socceraction_amd.atomic.spadl import base as cb
+    df = _synthetic_frame(200, 93)
+    df['action_id'] = (df.groupby('game_id').cumcount() // 3).astype(np.int64)
+    frame = cb.SpadlFrame.from_frame(df)
+    assert frame.keys is not None  # the general path
+    out = conv.convert_to_atomic(df)
+    assert_convert_equal(_cols(out), co.convert_to_atomic(_cols(df)), 'dup-200')
+    rng = np.random.default_rng(5)
+    sh = df.iloc[rng.permutation(len(df))].reset_index(drop=True)
+    assert_convert_equal(_cols(conv.convert_to_atomic(sh)), co.convert_to_atomic(_cols(sh)),
+                         'dup-200-shuffled')
 
 
 def test_convert_then_atomic_vaep(conv):
