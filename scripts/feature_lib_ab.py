@@ -46,6 +46,11 @@ def main():
     num.struct = copy.deepcopy(plan.struct)
     for x in range(len(num.struct.bool_col)):
         num.struct.bool_col[x] = -1
+    bonly = copy.copy(plan)  # the bool pass alone
+    bonly.struct = copy.deepcopy(plan.struct)
+    for x in range(len(bonly.struct.bool_col)):
+        bonly.struct.f64_col[x] = -1
+        bonly.struct.i64_col[x] = -1
     out = ops.alloc_feature_blocks(plan, ab.n, ab.device, 1024, 128)
     s = ab.struct()
     stream = torch.cuda.current_stream().cuda_stream
@@ -59,7 +64,7 @@ def main():
     ps = torch.rand(ab.n, dtype=torch.float64, device=ab.device)
     pc = torch.rand(ab.n, dtype=torch.float64, device=ab.device)
     cells = ops.xt_cells_buffer(ab.n, ab.device)
-    tags = (('num', num), ('all', plan)) + ((('step', num), ('step_nocells', num), ('step_labels', num),
+    tags = (('num', num), ('bool', bonly), ('all', plan)) + ((('step', num), ('step_nocells', num), ('step_labels', num),
                                              ('num_cells', num)) if not args.atomic else ())
     for rnd in range(3):
         for name, lib in libs.items():

@@ -24,6 +24,7 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument('--games', type=int, default=10000)
     ap.add_argument('--reps', type=int, default=10)
+    ap.add_argument('--variants', default='', help='library variant tags (socceraction_amd.build --variant)')
     args = ap.parse_args()
     dev = B.device()
     ab = B.ActionBatch.from_columns(synthetic.spadl_games(args.games), dev=dev)
@@ -34,10 +35,28 @@ def main() -> None:
     forms = {'grid_gather': lambda: ops.xt_rate(ab, ops.xt_interp_grid(xT, 105, 68), 1050, 680),
              'gather_only': lambda: ops.xt_rate(ab, grid, 1050, 680),
              'per_action': lambda: ops.xt_rate_interp(ab, xT, 105, 68, axes=axes, out=out)}
+    import ctypes
+    from socceraction_amd import _native as N
+    s_act = ab.struct()
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    for v in [x for x in args.variants.split(',') if x]:  # the same call through a variant build
+        lib = N.load_library(os.path.join(ROOT, 'socceraction_amd', '_lib', f'libsocceraction_amd_{v}.so'))
+
+        def run(lib=lib):
+            o = 105 + 68
+            N.check(lib.sa_xt_rate_interp(ctypes.byref(s_act), xT.data_ptr(), axes[:105].data_ptr(),
+                                          axes[105:o].data_ptr(), 105, 68, axes[o:o + 1050].data_ptr(), 1050,
+                                          axes[o + 1050:].data_ptr(), 680, out.data_ptr(), err.data_ptr(),
+                                          torch.cuda.current_stream().cuda_stream))
+        forms['per_action_' + v] = run
     a, _ = forms['grid_gather']()
     b, _ = forms['per_action']()
     x, y = a.cpu().numpy(), b.cpu().numpy()
     equal = bool((np.isnan(x) == np.isnan(y)).all() and (x[~np.isnan(x)] == y[~np.isnan(x)]).all())
+    for k in [k for k in forms if k.startswith('per_action_')]:
+        forms[k]()
+        y = out[:ab.n].cpu().numpy()
+        equal &= bool((np.isnan(x) == np.isnan(y)).all() and (x[~np.isnan(x)] == y[~np.isnan(x)]).all())
     ms = {k: [] for k in forms}
     for _ in range(4):
         for k, fn in forms.items():

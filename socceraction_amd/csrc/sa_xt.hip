@@ -754,6 +754,99 @@ __global__ __launch_bounds__(256) void xt_rate_interp_kernel(sa_actions A, const
   if (bad && err) atomicOr(err, bad);
 }
 
+// The same rate with the (w x l) surface and the node tables staged in LDS (the 105 x 68 surface
+// and its 1050 + 680 node brackets: 78 KB): persistent workgroups load them once, then stream the
+// actions two pairs per thread per pass (every load before the first store), so every node value
+// is eight LDS reads instead of a chain of L2 gathers.  Same node_value operations: bit-identical.
+// 16M actions: 0.145 ms (42 B/action: 4.6 TB/s) vs 0.32 ms for L2 gathers of the node tables and
+// 0.235 ms for gathers from the materialised 1050 x 680 grid; a software-pipelined loop (next
+// pass's loads before this pass's node values) and 4 pairs per pass were not faster
+// (profiles/r03_xt_rate_interp_ab.md).
+#ifndef SA_XRI_THREADS
+#define SA_XRI_THREADS 1024  // 16 waves per CU (82 VGPRs); 512: 0.157 ms, 1024: 0.145 ms per 16M actions
+#endif
+#ifndef SA_XRI_U
+#define SA_XRI_U 2
+#endif
+#ifndef SA_XRI_BPC
+#define SA_XRI_BPC 4  // workgroups per CU in the grid (one resident at a time): 1 / 2 / 4 / 8 / 16: 0.156 / 0.150 / 0.147 / 0.160 / 0.185 ms
+#endif
+constexpr int XRI_THREADS = SA_XRI_THREADS;
+constexpr size_t XRI_LDS_MAX = 78 * 1024;
+
+__device__ __forceinline__ void rate_interp_pair(const sa_frame& F, int64_t n, int64_t j0, int vec,
+                                                 const double* __restrict__ xT, int l, int L, int W,
+                                                 const int32_t* __restrict__ idx, const double* __restrict__ frac,
+                                                 double* __restrict__ out, int32_t& bad) {
+  if (vec && j0 + 1 < n) {
+    const f64x2 sx = *reinterpret_cast<const f64x2*>(F.c0 + j0);
+    const f64x2 sy = *reinterpret_cast<const f64x2*>(F.c1 + j0);
+    const f64x2 ex = *reinterpret_cast<const f64x2*>(F.c2 + j0);
+    const f64x2 ey = *reinterpret_cast<const f64x2*>(F.c3 + j0);
+    const uint32_t ty = *reinterpret_cast<const uint16_t*>(F.type_id + j0);
+    const uint32_t rs = *reinterpret_cast<const uint16_t*>(F.result_id + j0);
+    f64x2 v;
+    v[0] = rate_interp_one(ty & 0xFF, rs & 0xFF, sx[0], sy[0], ex[0], ey[0], xT, l, L, W, idx, frac, bad);
+    v[1] = rate_interp_one(ty >> 8, rs >> 8, sx[1], sy[1], ex[1], ey[1], xT, l, L, W, idx, frac, bad);
+    __builtin_nontemporal_store(v, reinterpret_cast<f64x2*>(out + j0));
+  } else {
+    for (int64_t j = j0; j < j0 + 2 && j < n; ++j)
+      out[j] = rate_interp_one(F.type_id[j], F.result_id[j], F.c0[j], F.c1[j], F.c2[j], F.c3[j], xT, l, L, W, idx,
+                               frac, bad);
+  }
+}
+
+__global__ __launch_bounds__(XRI_THREADS) void xt_rate_interp_lds_kernel(sa_actions A, const double* __restrict__ xT,
+                                                                        int l, int w, int L, int W,
+                                                                        const int32_t* __restrict__ idx,
+                                                                        const double* __restrict__ frac,
+                                                                        double* __restrict__ out,
+                                                                        int32_t* __restrict__ err, int vec) {
+  extern __shared__ __attribute__((aligned(16))) double xri_lds[];
+  double* sxT = xri_lds;                                        // [w * l]
+  double* sfrac = sxT + w * l;                                  // [L + W]
+  int32_t* sidx = reinterpret_cast<int32_t*>(sfrac + (L + W));  // [L + W]
+  for (int k = threadIdx.x; k < w * l; k += blockDim.x) sxT[k] = xT[k];
+  for (int k = threadIdx.x; k < L + W; k += blockDim.x) {
+    sfrac[k] = frac[k];
+    sidx[k] = idx[k];
+  }
+  __syncthreads();
+  const sa_frame& F = A.frames[0];
+  const int64_t n = A.n, pairs = (n + 1) / 2, stride = (int64_t)gridDim.x * blockDim.x;
+  int32_t bad = 0;
+  constexpr int U = SA_XRI_U;  // pairs per thread per pass, every load issued before the first store
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < pairs; p += U * stride) {
+    if (vec && 2 * (p + (U - 1) * stride) + 1 < n) {
+      f64x2 sx[U], sy[U], ex[U], ey[U];
+      uint32_t ty[U], rs[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t j0 = 2 * (p + u * stride);
+        sx[u] = *reinterpret_cast<const f64x2*>(F.c0 + j0);
+        sy[u] = *reinterpret_cast<const f64x2*>(F.c1 + j0);
+        ex[u] = *reinterpret_cast<const f64x2*>(F.c2 + j0);
+        ey[u] = *reinterpret_cast<const f64x2*>(F.c3 + j0);
+        ty[u] = *reinterpret_cast<const uint16_t*>(F.type_id + j0);
+        rs[u] = *reinterpret_cast<const uint16_t*>(F.result_id + j0);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        f64x2 v;
+        v[0] = rate_interp_one(ty[u] & 0xFF, rs[u] & 0xFF, sx[u][0], sy[u][0], ex[u][0], ey[u][0], sxT, l, L, W,
+                               sidx, sfrac, bad);
+        v[1] = rate_interp_one(ty[u] >> 8, rs[u] >> 8, sx[u][1], sy[u][1], ex[u][1], ey[u][1], sxT, l, L, W, sidx,
+                               sfrac, bad);
+        __builtin_nontemporal_store(v, reinterpret_cast<f64x2*>(out + 2 * (p + u * stride)));
+      }
+    } else {
+      for (int u = 0; u < U && p + u * stride < pairs; ++u)
+        rate_interp_pair(F, n, 2 * (p + u * stride), vec, sxT, l, L, W, sidx, sfrac, out, bad);
+    }
+  }
+  if (bad && err) atomicOr(err, bad);
+}
+
 // rate() from the count pass's codes: a thread rates 4 actions (one 16-B code load, two 16-B
 // stores) -- 12 B per action instead of 42.
 __global__ __launch_bounds__(256) void xt_rate_codes_kernel(const uint32_t* __restrict__ codes, int64_t n,
@@ -1099,9 +1192,26 @@ extern "C" int sa_xt_rate_interp(const sa_actions* a, const double* xT, const do
   const int vec = aligned16(F.c0) && aligned16(F.c1) && aligned16(F.c2) && aligned16(F.c3) && aligned16(out) &&
                   ((uintptr_t)F.type_id & 1u) == 0 && ((uintptr_t)F.result_id & 1u) == 0;
   const int64_t threads = (a->n + 1) / 2;
-  hipLaunchKernelGGL(xt_rate_interp_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, *a, xT, l, L,
-                     W, idx, frac, out, err_flags, vec);
-  rc = check_launch("xt_rate_interp_kernel");
+  const size_t lds = sizeof(double) * ((size_t)l * w + L + W) + sizeof(int32_t) * (size_t)(L + W);
+  if (lds <= XRI_LDS_MAX) {  // the surface and node tables in LDS, persistent workgroups
+    static int cus = 0;
+    if (!cus) {
+      int dev = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+        cus = 256;
+    }
+    const int64_t need = (threads + XRI_THREADS - 1) / XRI_THREADS;
+    const int64_t most = (int64_t)cus * SA_XRI_BPC;
+    const unsigned blocks = (unsigned)(need < most ? need : most);
+    hipLaunchKernelGGL(xt_rate_interp_lds_kernel, dim3(blocks), dim3(XRI_THREADS), lds, st, *a, xT, l, w, L, W, idx,
+                       frac, out, err_flags, vec);
+    rc = check_launch("xt_rate_interp_lds_kernel");
+  } else {
+    hipLaunchKernelGGL(xt_rate_interp_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, *a, xT, l,
+                       L, W, idx, frac, out, err_flags, vec);
+    rc = check_launch("xt_rate_interp_kernel");
+  }
   scratch_release(sc, st);
   return rc;
 }
