@@ -1,5 +1,6 @@
 """VAEP.rate's two xgboost-shaped learners (100 trees, depth 3) on cfg2 through condition bitmaps
 (trees.predict_pair_conditions) vs the float32-block path, HIP events; for rocprofv3 traces.
+Both paths' probabilities are compared (torch.equal) before any timing; exit 3 on a mismatch.
 
     python scripts/cond_probe.py
 """
@@ -42,9 +43,16 @@ def main():
     def blocks():
         ops.features(ab, SPADL_DEFAULT, 3, out=f32)
         return [m.predict_blocks(f32) for m in models]
-    res = {'n': ab.n, 'conditions_ms': _ms(lambda: trees.predict_pair_conditions(ab, plan, models)),
+    # parity before timing: both paths give the same probabilities bit for bit
+    cond = trees.predict_pair_conditions(ab, plan, models)
+    ref = blocks()
+    equal = all(torch.equal(a, b) for a, b in zip(cond, ref))
+    res = {'n': ab.n, 'equal': equal,
+           'conditions_ms': _ms(lambda: trees.predict_pair_conditions(ab, plan, models)),
            'f32_blocks_ms': _ms(blocks)}
     print(json.dumps(res), flush=True)
+    if not equal:
+        raise SystemExit(3)
 
 
 if __name__ == '__main__':

@@ -102,6 +102,34 @@ def main():
                 b.record()
                 torch.cuda.synchronize()
                 res['ms'].setdefault(f'{name}:{tag}', []).append(round(a.elapsed_time(b) / args.reps, 4))
+    # the bench step's two VAEP launches back to back (numeric step pass, then the bool pass),
+    # each timed by its own events: what one pass costs right after the other
+    if not args.atomic:
+        for rnd in range(3):
+            for name, lib in libs.items():
+                def step():
+                    N.check(lib.sa_vaep_step_f64(
+                        ctypes.byref(s), ctypes.byref(num.struct), ctypes.byref(bb), ctypes.byref(fb),
+                        ctypes.byref(ib), 16, 12, cells.data_ptr(), 10, lab[0].data_ptr(), lab[1].data_ptr(), None,
+                        ld, ps.data_ptr(), pc.data_ptr(), val[0].data_ptr(), val[1].data_ptr(), val[2].data_ptr(),
+                        stream))
+
+                def boolp():
+                    N.check(lib.sa_vaep_features(ctypes.byref(s), ctypes.byref(bonly.struct), ctypes.byref(bb),
+                                                 ctypes.byref(fb), ctypes.byref(ib), stream))
+                step()
+                boolp()
+                ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.reps)]
+                for e in ev:
+                    e[0].record()
+                    step()
+                    e[1].record()
+                    boolp()
+                    e[2].record()
+                torch.cuda.synchronize()
+                for part, (x, y) in (('pair_step', (0, 1)), ('pair_bool', (1, 2)), ('pair_total', (0, 2))):
+                    res['ms'].setdefault(f'{name}:{part}', []).append(
+                        round(sum(e[x].elapsed_time(e[y]) for e in ev) / args.reps, 4))
     print(json.dumps(res), flush=True)
 
 

@@ -444,6 +444,9 @@ constexpr int BOOL_TILE = 1024;  // rows per tile of the bool block image
 // windows from the id columns (L2 hits: a tile's groups run back to back on one XCD) and
 // writes only the (family, window, value) columns inside its range.
 constexpr int CG_WAVES = 4;  // waves per workgroup
+#ifndef SA_BOOL_PROBE
+#define SA_BOOL_PROBE 0
+#endif
 #define CG_EQ(w, v) bytes_eq((w), (v))
 
 // WIDE (windowed mode, nb_prev_actions > 9: windows reach past the 8-row halo): each window's
@@ -499,7 +502,11 @@ __global__ __launch_bounds__(64 * CG_WAVES) void bool_colgroup_kernel(FeatArgs a
   uint32_t TR[6], RR[6], BR[6];  // rows j0-8 .. j0+15 (windowed mode)
   uint32_t tw[4], rw[4], bw[4];  // window i of the lane's 16 actions
   if (!EXPLICIT && !WIDE) {
+#if SA_BOOL_PROBE & 1  // probe: the id words from the first 8K rows (L2 hits; wrong values)
+    const int64_t wbase = ((j0 / 4) & 2047) + 2 - 2;
+#else
     const int64_t wbase = j0 / 4 - 2;
+#endif
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
       TR[k] = ld_u8x4(F0.type_id, wbase + k, n);
@@ -638,8 +645,13 @@ __global__ __launch_bounds__(64 * CG_WAVES) void bool_colgroup_kernel(FeatArgs a
           SA_DCHECK(s >= 0 && (WIDE || s <= BOOL_HALO), s);
           // team codes straight from L1/L2 (a few waves per tile need them): the kernel keeps
           // no LDS, so xT workgroups with large LDS footprints co-reside with it
+#if SA_BOOL_PROBE & 1
+          t0 = ld_or0(F0.team, ((j0 + mm) & 8191) + 16, n);
+          ti = ld_or0(F0.team, ((j0 + mm) & 8191) + 16 - s, n);
+#else
           t0 = ld_or0(F0.team, j0 + mm, n);
           ti = ld_or0(F0.team, j0 + mm - s, n);
+#endif
         }
         if (BITS)  // strided order: word mm & 3, byte mm >> 2
           m[mm & 3] |= (uint32_t)(t0 == ti) << (8 * (mm >> 2));
@@ -829,6 +841,17 @@ __device__ __forceinline__ void load_row1(const sa_frame& F, int64_t r, bool ato
           ((uint32_t)(atomic ? 0 : F.result_id[r]) << 16) | ((uint32_t)F.bodypart_id[r] << 24);
 }
 
+// SA_NUM_NTL: the numeric pass's streamed inputs (coordinates, time, probabilities) loaded
+// non-temporally, so they do not displace the id / team columns the bool pass reads next
+#ifndef SA_NUM_NTL
+#define SA_NUM_NTL 0
+#endif
+template <int BIT = 1, typename V>
+__device__ __forceinline__ V ld_stream(const V* p) {  // BIT 1: coordinates / time, 2: probabilities
+  if constexpr ((SA_NUM_NTL & BIT) != 0) return __builtin_nontemporal_load(p);
+  return *p;
+}
+
 // rows r, r+1 (r even: 16-B aligned f64 pairs, 2-B aligned id pairs)
 __device__ __forceinline__ void load_pair(const sa_frame& F, int64_t r, bool atomic, Row& a, Row& b) {
 #if SA_NUM_PROBE & 4  // probe: no coordinate / time reads (wrong values)
@@ -842,11 +865,11 @@ __device__ __forceinline__ void load_pair(const sa_frame& F, int64_t r, bool ato
   const f64x2 x3 = *reinterpret_cast<const f64x2*>(F.c3 + rq);
   const f64x2 x4 = *reinterpret_cast<const f64x2*>(F.time_seconds + rq);
 #else
-  const f64x2 x0 = *reinterpret_cast<const f64x2*>(F.c0 + r);
-  const f64x2 x1 = *reinterpret_cast<const f64x2*>(F.c1 + r);
-  const f64x2 x2 = *reinterpret_cast<const f64x2*>(F.c2 + r);
-  const f64x2 x3 = *reinterpret_cast<const f64x2*>(F.c3 + r);
-  const f64x2 x4 = *reinterpret_cast<const f64x2*>(F.time_seconds + r);
+  const f64x2 x0 = ld_stream(reinterpret_cast<const f64x2*>(F.c0 + r));
+  const f64x2 x1 = ld_stream(reinterpret_cast<const f64x2*>(F.c1 + r));
+  const f64x2 x2 = ld_stream(reinterpret_cast<const f64x2*>(F.c2 + r));
+  const f64x2 x3 = ld_stream(reinterpret_cast<const f64x2*>(F.c3 + r));
+  const f64x2 x4 = ld_stream(reinterpret_cast<const f64x2*>(F.time_seconds + r));
 #endif
   const uint32_t pe = *reinterpret_cast<const uint16_t*>(F.period_id + r);
   const uint32_t ty = *reinterpret_cast<const uint16_t*>(F.type_id + r);
@@ -856,6 +879,17 @@ __device__ __forceinline__ void load_pair(const sa_frame& F, int64_t r, bool ato
           (pe & 0xFF) | ((ty & 0xFF) << 8) | ((rs & 0xFF) << 16) | ((bo & 0xFF) << 24)};
   b = Row{x0[1], x1[1], x2[1], x3[1], x4[1],
           (pe >> 8) | ((ty >> 8) << 8) | ((rs >> 8) << 16) | ((bo >> 8) << 24)};
+}
+
+__device__ __forceinline__ Row shfl_up_row(const Row& r) {  // lane l gets lane l-1's row
+  Row o;
+  o.c0 = __shfl_up(r.c0, 1, WAVE);
+  o.c1 = __shfl_up(r.c1, 1, WAVE);
+  o.c2 = __shfl_up(r.c2, 1, WAVE);
+  o.c3 = __shfl_up(r.c3, 1, WAVE);
+  o.ts = __shfl_up(r.ts, 1, WAVE);
+  o.ids = __shfl_up(r.ids, 1, WAVE);
+  return o;
 }
 
 __device__ __forceinline__ void row_to_win(const Row& r, Win& w, int e) {
@@ -989,7 +1023,7 @@ __device__ __forceinline__ void formula_rows(const sa_actions& A, const T* __res
 template <bool ATOMIC, typename T, typename V>
 __device__ __forceinline__ bool formula_vals(const sa_actions& A, const T* __restrict__ ps,
                                              const T* __restrict__ pc, bool vec_ok, int64_t j0, SegCursor& cur,
-                                             V& vo, V& vd, V& vv);
+                                             V& vo, V& vd, V& vv, const double* t_in = nullptr);
 
 // goal (bit 0) / owngoal (bit 1) / shot (bit 2, atomic goal_from_shot) of row j
 template <bool ATOMIC>
@@ -1143,15 +1177,26 @@ __global__ __launch_bounds__(256) NUM_OCCUPANCY void num_features_kernel(FeatArg
   jr[1] = jq + 1 < n ? jq + 1 : n - 1;  // padded tail rows recompute row n-1
   Row cand[2], pool[2];
   if (KF == 3) {
-    // the pair's window rows: cand = rows jb, jb+1, pool = the older rows jb-1, jb-2
-    if (jq >= 2 && jq + 2 <= n) {
+    // the pair's window rows: cand = rows jb, jb+1 (each input row is loaded by ONE lane:
+    // streamed, read once from HBM), pool = the older rows jb-1, jb-2 = the previous lane's
+    // cand rows, by shuffles; lane 0 loads its own (the previous tile's last rows).  Lanes
+    // clamped past the batch end (jw >= n) get don't-care pool rows: their outputs are not
+    // stored (COND: masked off in cond_store)
+    if (jq + 2 <= n) {
       load_pair(F0, jq, ATOMIC, cand[0], cand[1]);
-      load_pair(F0, jq - 2, ATOMIC, pool[1], pool[0]);
-    } else {  // first rows of the batch or the tail: guarded scalar loads
+    } else {  // the batch's last row: guarded scalar loads
       load_row1(F0, jr[0], ATOMIC, cand[0]);
       load_row1(F0, jr[1], ATOMIC, cand[1]);
-      load_row1(F0, jq - 1 < 0 ? 0 : jq - 1, ATOMIC, pool[0]);
-      load_row1(F0, jq - 2 < 0 ? 0 : jq - 2, ATOMIC, pool[1]);
+    }
+    pool[0] = shfl_up_row(cand[1]);
+    pool[1] = shfl_up_row(cand[0]);
+    if (lane == 0) {
+      if (jq >= 2) {
+        load_pair(F0, jq - 2, ATOMIC, pool[1], pool[0]);
+      } else {  // the batch's first rows: windows clamp to row 0
+        load_row1(F0, jq - 1 < 0 ? 0 : jq - 1, ATOMIC, pool[0]);
+        load_row1(F0, 0, ATOMIC, pool[1]);
+      }
     }
   }
   // the block addresses of rows jb, jb+1 (column 0; COND: the condition sinks), before any store
@@ -1174,7 +1219,9 @@ __global__ __launch_bounds__(256) NUM_OCCUPANCY void num_features_kernel(FeatArg
       labels_pair<ATOMIC>(A, args.nr, jw, cur, lso, lco, lgo);
       if (args.ps) {  // uniform: labels only when no probabilities are given
         SegCursor fc = cur;
-        fok = formula_vals<ATOMIC, double>(A, args.ps, args.pc, args.vec_ok, jw, fc, fo, fd, fv);
+        const double t_rows[2] = {cand[0].ts, cand[1].ts};  // rows jw, jw+1 (KF = 3)
+        fok = formula_vals<ATOMIC, double>(A, args.ps, args.pc, args.vec_ok, jw, fc, fo, fd, fv,
+                                           KF == 3 ? t_rows : nullptr);
       }
     }
 #pragma unroll
@@ -1577,10 +1624,12 @@ __global__ __launch_bounds__(256) void labels_kernel(sa_actions A, int nr, uint8
 // Rows j0 .. j0+V-1 of one lane (V = 16 / sizeof(T)); every lane of the wave calls it with
 // consecutive j0 (the previous row comes from the neighbouring lane); `cur` = a segment cursor
 // at or before row j0, advanced by the call.
+// t_in (optional, vector path): the rows' time_seconds the caller already holds (the numeric
+// step pass loaded them with its window rows), so they are not read a second time
 template <bool ATOMIC, typename T, typename VT>
 __device__ __forceinline__ bool formula_vals(const sa_actions& A, const T* __restrict__ ps,
                                              const T* __restrict__ pc, bool vec_ok, int64_t j0, SegCursor& cur,
-                                             VT& vo, VT& vd, VT& vv) {
+                                             VT& vo, VT& vd, VT& vv, const double* t_in) {
   constexpr int V = 16 / sizeof(T);
   const int64_t n = A.n;
   const int lane = threadIdx.x & (WAVE - 1);
@@ -1591,13 +1640,18 @@ __device__ __forceinline__ bool formula_vals(const sa_actions& A, const T* __res
   int32_t tm_[V], ty_[V], rs_[V];
   typedef T vec_t __attribute__((ext_vector_type(V)));
   if (vec_ok && active && j0 + V <= n) {  // whole 16-B vectors (vec_ok: 16-B aligned probabilities)
-    const vec_t vs = *reinterpret_cast<const vec_t*>(ps + j0);
-    const vec_t vc = *reinterpret_cast<const vec_t*>(pc + j0);
+    const vec_t vs = ld_stream<2>(reinterpret_cast<const vec_t*>(ps + j0));
+    const vec_t vc = ld_stream<2>(reinterpret_cast<const vec_t*>(pc + j0));
 #pragma unroll
     for (int q = 0; q < V; q += 2) {
-      const f64x2 tv = *reinterpret_cast<const f64x2*>(F.time_seconds + j0 + q);
-      t_[q] = tv[0];
-      t_[q + 1] = tv[1];
+      if (t_in) {
+        t_[q] = t_in[q];
+        t_[q + 1] = t_in[q + 1];
+      } else {
+        const f64x2 tv = *reinterpret_cast<const f64x2*>(F.time_seconds + j0 + q);
+        t_[q] = tv[0];
+        t_[q + 1] = tv[1];
+      }
     }
     uint32_t tyw, rsw = 0;
     if (V == 4) {

@@ -44,3 +44,27 @@ def test_bench_gpus_2_side_entries():
     assert x['actions_total'] > x['actions_per_gpu'] > 0 and x['iterations'] > 0
     a = out['atomic_cfg3']
     assert a['atomic_actions_total'] > a['atomic_actions_per_gpu'] > 0
+
+
+def test_device_events_order_streams_and_time():
+    """socceraction_amd.events.DeviceEvent (sa_event_*, no system-scope fence): a side stream
+    that waits on an event recorded after a producer kernel sees the producer's writes, and a
+    timing pair measures a positive duration, like torch.cuda.Event."""
+    import torch
+    from socceraction_amd import events
+    main, side = torch.cuda.current_stream(), torch.cuda.Stream()
+    x = torch.zeros(1 << 24, dtype=torch.float32, device='cuda')
+    for _ in range(5):
+        a, b = events.DeviceEvent(True), events.DeviceEvent(True)
+        a.record(main)
+        x.add_(1.0)  # producer on the main stream
+        b.record(main)
+        done = events.DeviceEvent().record(main)
+        done.wait(side)
+        with torch.cuda.stream(side):
+            y = x.sum()  # consumer on the side stream
+        events.DeviceEvent().record(side).wait(main)
+        b.synchronize()
+        assert a.elapsed_time(b) > 0
+    torch.cuda.synchronize()
+    assert float(y.item()) == 5.0 * (1 << 24)
