@@ -841,10 +841,15 @@ __device__ __forceinline__ void load_row1(const sa_frame& F, int64_t r, bool ato
           ((uint32_t)(atomic ? 0 : F.result_id[r]) << 16) | ((uint32_t)F.bodypart_id[r] << 24);
 }
 
-// SA_NUM_NTL: the numeric pass's streamed inputs (coordinates, time, probabilities) loaded
-// non-temporally, so they do not displace the id / team columns the bool pass reads next
+// SA_NUM_NTL: the numeric pass's streamed inputs -- bit 0 the coordinates and times, bit 1 the
+// probabilities -- loaded non-temporally, so the ~1 GB they stream per pass does not push the
+// id / team columns (7 B/action) the bool pass reads next out of the Infinity Cache.  Every
+// streamed byte is loaded once (the pool rows come from the neighbour lane), so nothing is
+// lost by not caching them.  Pair A/B (profiles/r03_numeric_pass_ab.md): numeric step pass +
+// bool pass 3.035 -> 2.940 ms (slow box), 2.591 -> 2.541 ms (fast box); coordinates or
+// probabilities alone keep the columns only partly resident
 #ifndef SA_NUM_NTL
-#define SA_NUM_NTL 0
+#define SA_NUM_NTL 3
 #endif
 template <int BIT = 1, typename V>
 __device__ __forceinline__ V ld_stream(const V* p) {  // BIT 1: coordinates / time, 2: probabilities
