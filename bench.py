@@ -727,8 +727,11 @@ def main() -> None:
                          'else 0)')
     ap.add_argument('--bool-tile', type=int, default=1024,
                     help='rows per bool-block tile (0 = one tile: plain column-major)')
-    ap.add_argument('--order', default='num_step,bool_features',
-                    help='launch order of the VAEP kernels in the step; num_step = the numeric '
+    ap.add_argument('--order', default='bool_features,num_step',
+                    help='launch order of the VAEP kernels in the step (default bool first: the xT '
+                         'count, solve and rate of step k then run on the side stream beside step '
+                         'k+1\'s bool pass, 2.955 - 2.970 vs 2.975 - 2.993 ms with num first and '
+                         'the count on the main stream, profiles/r03_numeric_pass_ab.md); num_step = the numeric '
                          'pass with goalscore, labels and the f64 formula in it (sa_vaep_step_f64; '
                          '3.115 vs 3.195 ms, profiles/r02u_goalscore_fused_ab.md); num_features = '
                          'the numeric pass with goalscore; num_features_nogs + goalscore: the '
@@ -751,6 +754,9 @@ def main() -> None:
                          '3.24 - 3.31 ms per step, profiles/r02_step_ab.md), or on the side stream')
     ap.add_argument('--num-tile', type=int, default=128,
                     help='rows per f64/i64-block tile (0 = one tile: plain column-major)')
+    ap.add_argument('--event-every', type=int, default=4,
+                    help='per-launch HIP events on every Nth timed step (1 = every step); the '
+                         'kernels\' mean durations come from those steps')
     ap.add_argument('--events', default='native', choices=('native', 'torch'),
                     help='event kind of the step\'s stream forks / joins and per-kernel timings: '
                          'native = sa_event_* without the system-scope fence (default), torch = '
@@ -884,8 +890,9 @@ def main() -> None:
             # zero the xT counts on the side stream (idle until the fork) while the first VAEP
             # call runs; the count pass waits for it
             zs = side if overlap else main_s
-            _record(main_s, ek).wait(zs)  # after the previous step's use of the counts
-            with torch.cuda.stream(zs):
+            if cm and overlap and fork < nv:  # the count runs on the main stream: after its last use
+                _record(main_s, ek).wait(zs)
+            with torch.cuda.stream(zs):  # (else the side stream's own order covers the counts)
                 xt_start.zero()
             zev = _record(zs, ek)
             if par:
@@ -912,7 +919,10 @@ def main() -> None:
                     pj.wait(main_s)
                     continue
                 if ev is not None:
-                    ev[i][0].record(main_s)
+                    if i > 0 and not (overlap and i == fork) and not par:
+                        ev[i][0] = ev[i - 1][1]  # back to back on the main stream: one event
+                    else:
+                        ev[i][0].record(main_s)
                 call()
                 if ev is not None:
                     ev[i][1].record(main_s)
@@ -963,7 +973,7 @@ def main() -> None:
                 torch.cuda.synchronize()
                 ab_ms[k].append(round((time.perf_counter() - t) / args.steps * 1e3, 4))
         for k, (fn, vorder) in variants.items():  # per-call HIP event means, one more round
-            evs = [[(_event(True, fn.ev_kind), _event(True, fn.ev_kind))
+            evs = [[[_event(True, fn.ev_kind), _event(True, fn.ev_kind)]
                     for _ in range(len(vorder) + 1)] for _ in range(args.steps)]
             for e in evs:
                 fn(e)
@@ -979,17 +989,22 @@ def main() -> None:
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    evs = [[(_event(True), _event(True)) for _ in range(nv + 1)] for _ in range(args.steps)]
+    evs = [[[_event(True), _event(True)] for _ in range(nv + 1)] for _ in range(args.steps)]
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    # per-launch HIP events on every `--event-every`-th step of the timed region (each record is
+    # a marker between the kernels; the step's own launches keep their back-to-back order on the
+    # other steps): the kernels' mean durations are the mean over the sampled steps
+    sampled = [k for k in range(args.steps) if k % max(1, args.event_every) == 0]
     for k in range(args.steps):
-        step(evs[k])
+        step(evs[k] if k in sampled else None)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     wall = time.perf_counter() - t0
+    evs = [evs[k] for k in sampled]
     kern = {name: float(np.mean([e[i][0].elapsed_time(e[i][1]) for e in evs]))
             for i, name in enumerate(order)}
     kern['xt_fit_rate'] = float(np.mean([e[nv][0].elapsed_time(e[nv][1]) for e in evs]))
@@ -1065,6 +1080,8 @@ def main() -> None:
                                                    if getattr(out, '_arena', None) is not None else ''),
                    'parallelism': f'games sharded over {world} GPU(s)'},
         'kernels': per_kernel,
+        'kernel_events': f'HIP events around each launch on {len(evs)} of the {args.steps} timed steps '
+                         f'(every {max(1, args.event_every)}th)',
         'roofline': {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS,
                      'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 4),
                      'traffic': traffic, 'traffic_unit': 'HBM bytes per launch (rocprofv3 PMC)',
@@ -1086,7 +1103,10 @@ def main() -> None:
                                   'codes': 'coordinates (count) + rate operands',
                                   'coords': 'coordinates'}[base['xt']],
                        'stream': 'main (serial)' if args.serial else
-                       (f"count pass on the main stream after {base['fork']} VAEP call(s); all-reduce, "
+                       (f"count, all-reduce, solve and rate on a {base['prio']}-priority side stream "
+                        'forked after the last VAEP call, overlapping the next step\'s first pass'
+                        if base['fork'] >= len(order) else
+                        f"count pass on the main stream after {base['fork']} VAEP call(s); all-reduce, "
                         f"solve and rate on a {base['prio']}-priority side stream overlapped with the rest"
                         if base['cm'] else
                         f"{base['prio']}-priority side stream, forked after {base['fork']} VAEP "

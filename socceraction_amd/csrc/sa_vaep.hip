@@ -1130,16 +1130,20 @@ __device__ __forceinline__ void labels_store(int64_t n, uint8_t* __restrict__ sc
 // once (16-B loads) and the windows are formed in registers (see the loop below).
 // KF = 0: any mode / any k (explicit frames: k <= SA_MAX_FRAMES; windowed: any k): per-window
 // row loads.
+// Waves per SIMD the compiler must leave room for (a VGPR cap; SA_NUM_WAVES, A/B builds).  The
+// SPADL step form fits 128 VGPRs without spills at 4 waves (its pool rows come by shuffles),
+// but whether that helps depends on the box: the step's pair 1.336 vs 1.389 ms on a fast box,
+// 1.592 vs 1.549 ms on a slow one (profiles/r03_numeric_pass_ab.md), so no form is capped.
 #ifndef SA_NUM_WAVES
-#define SA_NUM_WAVES 0  // > 0: ask the compiler for that many waves per SIMD (register cap)
+#define SA_NUM_WAVES 0
 #endif
-#if SA_NUM_WAVES > 0
-#define NUM_OCCUPANCY __attribute__((amdgpu_waves_per_eu(SA_NUM_WAVES, 8)))
-#else
-#define NUM_OCCUPANCY
-#endif
+template <bool ATOMIC, bool TAIL>
+constexpr int num_min_waves() {
+  return SA_NUM_WAVES > 0 ? SA_NUM_WAVES : 1;
+}
 template <bool ATOMIC, bool EXPLICIT, int KF, bool TAIL = false, bool N32 = false, bool COND = false>
-__global__ __launch_bounds__(256) NUM_OCCUPANCY void num_features_kernel(FeatArgs args) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(num_min_waves<ATOMIC, TAIL>(), 8)))
+void num_features_kernel(FeatArgs args) {
   // N32: the f64 and i64 blocks hold float32 values (sa_vaep_features_bits_f32); COND: no blocks,
   // the columns' split conditions as bitmaps (sa_vaep_features_conditions)
   using FT = typename std::conditional<COND, CondSink, typename std::conditional<N32, float, double>::type>::type;
