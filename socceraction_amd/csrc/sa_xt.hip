@@ -464,17 +464,27 @@ __global__ __launch_bounds__(H * XR_MAX_C) void xt_solve_reg_kernel(const double
 #ifndef SA_XI_LOADERS
 #define SA_XI_LOADERS 8
 #endif
-constexpr int XI_ROWS = 16;
+#ifndef SA_XI_ROWS
+#define SA_XI_ROWS 16  // rows per workgroup = chain lanes (16, 32 or 64)
+#endif
+#ifndef SA_XI_CH
+#define SA_XI_CH 128  // columns per chunk (64 or 128)
+#endif
+constexpr int XI_ROWS = SA_XI_ROWS;
 constexpr int XI_LOADERS = SA_XI_LOADERS;        // loader waves; one more wave runs the chains
 constexpr int XI_RQ = XI_ROWS / XI_LOADERS;      // rows per loader wave
 constexpr int XI_THREADS = (XI_LOADERS + 1) * 64;
-constexpr int XI_CH = 128;             // columns per chunk = 2 per loader lane per row
+constexpr int XI_CH = SA_XI_CH;        // columns per chunk = XI_NI per loader lane per row
+constexpr int XI_NI = XI_CH / 64;
+static_assert(XI_RQ >= 1 && XI_RQ * XI_LOADERS == XI_ROWS && XI_NI >= 1 && XI_NI * 64 == XI_CH &&
+                  (XI_ROWS & (XI_ROWS - 1)) == 0 && XI_ROWS <= 64,
+              "xt_iter_kernel shape");
 constexpr int XI_DEPTH = SA_XI_DEPTH;  // chunks in flight per loader lane
 constexpr int XI_LST = XI_CH + 1;      // list row stride (doubles): chain reads hit 16 banks
 
 struct XiChunk {
-  int32_t cnt[XI_RQ][2];  // [row q][column i]
-  double xv[2];       // x[c] of column i
+  int32_t cnt[XI_RQ][XI_NI];  // [row q][column i]
+  double xv[XI_NI];           // x[c] of column i
 };
 
 // Rows [rb, rb + nrows) of the system: `trans` points at the count row of row rb (row rb + i
@@ -513,7 +523,7 @@ __global__ __launch_bounds__(XI_THREADS) void xt_iter_kernel(const int32_t* __re
     }
     auto issue = [&](XiChunk& R, int k) {  // unconditional loads from clamped addresses
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
+      for (int i = 0; i < XI_NI; ++i) {
         const int c = k * XI_CH + 64 * i + lane;
         const int cc = c < C ? c : C - 1;
         R.xv[i] = x[cc];
@@ -528,7 +538,7 @@ __global__ __launch_bounds__(XI_THREADS) void xt_iter_kernel(const int32_t* __re
         const int row = XI_RQ * wv + q;
         int base = 0;
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {  // compact the non-zero columns, in column order
+        for (int i = 0; i < XI_NI; ++i) {  // compact the non-zero columns, in column order
           const bool cok = k * XI_CH + 64 * i + lane < C;
           const int32_t cnt = (cok && rowok[q]) ? R.cnt[q][i] : 0;
           const uint64_t m = __ballot(cnt != 0);
