@@ -127,11 +127,42 @@ def move_transition_matrix(actions: pd.DataFrame, l: int = N, w: int = M) -> np.
     return np.ascontiguousarray(tt.cpu().numpy().T)
 
 
+_SPLINE_DEGREE = {'linear': 1, 'cubic': 3, 'quintic': 5}
+
+
+def _spline_interp2d(x, y, z, k):
+    """``interp2d(x, y, z, kind='cubic' | 'quintic')`` on a regular grid, as scipy < 1.14 computes
+    it: the interpolating tensor-product spline of degree k (FITPACK ``regrid_smth`` with s = 0,
+    i.e. ``RectBivariateSpline(x, y, z.T, kx=k, ky=k, s=0)``) evaluated by ``bisplev`` on the
+    sorted query axes, points outside the node hull clamped to it (bounds_error=False,
+    fill_value=None), result shape (len(ys), len(xs)).  A host delegation to scipy like the
+    reference's own (xthreat.py:347-378); off the rating path (``rate`` interpolates linearly on
+    the device).  scipy >= 1.14 dropped interp2d itself, so this is pinned to the same
+    RectBivariateSpline stand-in the linear golden was produced with."""
+    from scipy.interpolate import RectBivariateSpline
+    z = np.asarray(z, dtype=np.float64)
+    x = np.asarray(x, np.float64).reshape(-1)
+    y = np.asarray(y, np.float64).reshape(-1)
+    if len(x) <= k or len(y) <= k:
+        raise ValueError(f'{k + 1} nodes per axis are needed for a degree-{k} spline')
+    spl = RectBivariateSpline(x, y, z.T, kx=k, ky=k, s=0)
+
+    def f(xs, ys):
+        xs = np.clip(np.sort(np.atleast_1d(np.asarray(xs, np.float64))), x[0], x[-1])
+        ys = np.clip(np.sort(np.atleast_1d(np.asarray(ys, np.float64))), y[0], y[-1])
+        return spl(xs, ys).T
+
+    return f
+
+
 def _gpu_interp2d(x, y, z, kind='linear', bounds_error=False):
     """GPU stand-in for ``scipy.interpolate.interp2d(x, y, z, kind='linear')`` on a regular
-    grid: z[j, i] sits at (x[i], y[j]); queries are clamped to the node hull."""
+    grid: z[j, i] sits at (x[i], y[j]); queries are clamped to the node hull.  ``kind`` 'cubic'
+    and 'quintic' delegate to scipy's spline (:func:`_spline_interp2d`)."""
+    if kind not in _SPLINE_DEGREE:
+        raise ValueError(f'Unsupported interpolation type {kind!r}.')
     if kind != 'linear':
-        raise NotImplementedError("only kind='linear' is implemented on this backend")
+        return _spline_interp2d(x, y, z, _SPLINE_DEGREE[kind])
     z = np.asarray(z, dtype=np.float64)
     w, l = z.shape
     x = np.asarray(x, np.float64).reshape(-1)

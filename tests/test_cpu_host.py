@@ -377,6 +377,31 @@ class TestModelPersistency:
         with pytest.raises(NotFittedError):
             m.rate(pd.DataFrame({'type_id': [0]}))
 
+    @pytest.mark.parametrize('kind,k', [('cubic', 3), ('quintic', 5)])
+    def test_interpolator_spline_kinds(self, kind, k):
+        """interpolator(kind='cubic' | 'quintic') (xthreat.py:347-378): interp2d's regular-grid
+        spline as scipy < 1.14 computed it -- RectBivariateSpline(kx=ky=k, s=0), sorted query
+        axes, out-of-hull points clamped, (len(ys), len(xs)) -- incl. interpolation at the nodes.
+        Parity against interp2d itself is unpinned (scipy here no longer has it)."""
+        from scipy.interpolate import RectBivariateSpline
+
+        from socceraction_amd import xthreat as xt
+        m = xt.ExpectedThreat(l=16, w=12)
+        rng = np.random.default_rng(3)
+        m.xT = rng.random((12, 16)) * 0.3
+        f = m.interpolator(kind)
+        cx = np.arange(0.0, 105.0, 105.0 / 16) + 0.5 * 105.0 / 16
+        cy = np.arange(0.0, 68.0, 68.0 / 12) + 0.5 * 68.0 / 12
+        np.testing.assert_allclose(f(cx, cy), m.xT, rtol=1e-10, atol=1e-12)  # through the nodes
+        xs, ys = np.array([104.0, -3.0, 50.2, 7.5]), np.array([30.0, 70.0, 1.0])
+        got = f(xs, ys)
+        spl = RectBivariateSpline(cx, cy, m.xT.T, kx=k, ky=k, s=0)
+        ref = spl(np.clip(np.sort(xs), cx[0], cx[-1]), np.clip(np.sort(ys), cy[0], cy[-1])).T
+        assert got.shape == (3, 4)
+        np.testing.assert_array_equal(got, ref)
+        with pytest.raises(ValueError):
+            m.interpolator('nearest')
+
     def test_interpolate_without_interp2d(self, monkeypatch):
         from socceraction_amd import xthreat as xt
         monkeypatch.setattr(xt, 'interp2d', None)
