@@ -17,6 +17,9 @@
 #include "sa_common.h"
 #include "sa_internal.h"
 
+#ifndef SA_XC_UC
+#define SA_XC_UC 8  // count pass from cell codes: codes per thread per pass, all loaded first
+#endif
 #ifndef SA_XT_WIDE
 #define SA_XT_WIDE 1  // C <= 197: XC_WIDE count pass (0: the 32k-action XC_SMALL workgroups)
 #endif
@@ -166,7 +169,7 @@ __global__ __launch_bounds__(XT_WIDE_THREADS) void xt_count_kernel(sa_actions A,
   int32_t bad = 0;
   // XC_U actions per thread per pass, every load issued before any is used (the loop is
   // otherwise one HBM round trip per action); rows past `end` are clamped and skipped
-  constexpr int XC_U = CELLS ? 8 : 4;
+  constexpr int XC_U = CELLS ? SA_XC_UC : 4;
   for (int64_t j0 = begin; j0 < end; j0 += XC_U * stride) {
     XtAct act[XC_U];
     if (CELLS) {
