@@ -20,6 +20,7 @@ import json
 import os
 import sys
 import time
+from typing import Tuple
 
 import numpy as np
 import torch
@@ -28,7 +29,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from socceraction_amd import batch as B  # noqa: E402
-from socceraction_amd import catalog, ops, synthetic  # noqa: E402
+from socceraction_amd import _native, catalog, ops, synthetic  # noqa: E402
 from socceraction_amd._native import XFN  # noqa: E402
 
 SPADL_DEFAULT = ['actiontype_onehot', 'result_onehot', 'actiontype_result_onehot',
@@ -379,6 +380,22 @@ def _record(stream, kind: str = None):
     return e
 
 
+def _events_median_ms(fn, reps: int) -> Tuple[float, float, float]:
+    """(median, min, max) ms of ``reps`` back-to-back calls of ``fn``, one HIP event pair per
+    call on the current stream, after one untimed call."""
+    fn()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(reps)]
+    for a, b in ev:
+        a.record()
+        fn()
+        b.record()
+    torch.cuda.synchronize()
+    t = [a.elapsed_time(b) for a, b in ev]
+    return float(np.median(t)), float(np.min(t)), float(np.max(t))
+
+
 def _events_ms(fn, reps: int) -> float:
     """Mean ms of ``fn`` over ``reps`` back-to-back calls (HIP events, current stream)."""
     fn()
@@ -392,7 +409,7 @@ def _events_ms(fn, reps: int) -> float:
     return a.elapsed_time(b) / reps
 
 
-def atomic_extra(dist, rank, world, dev, games: int, reps: int = 5, check: bool = True) -> dict:
+def atomic_extra(dist, rank, world, dev, games: int, reps: int = 21, check: bool = True) -> dict:
     """BASELINE cfg3 alongside the main line: Atomic-VAEP features (k=3, default xfns, 154
     columns) + labels of cfg3's ``games`` synthetic atomic games (10,000 ≈ 4.0e7 atomic
     actions), sharded by game over the ranks (this entry scales strongly)."""
@@ -405,9 +422,9 @@ def atomic_extra(dist, rank, world, dev, games: int, reps: int = 5, check: bool 
 
     s = ab.struct()
 
-    def step():  # features + labels in two launches: the labels ride in the numeric pass
-        ops.step_into(s, out, None, None, 10, lab, None)
-    ms = _events_ms(step, reps)
+    def step():  # features, then the labels as their own launch (sa_vaep_step_f64 routes every
+        ops.step_into(s, out, None, None, 10, lab, None)  # atomic step to separate launches)
+    ms, ms_lo, ms_hi = _events_median_ms(step, reps)
     par = Parity()
     if check:  # the timed launches' own buffers: sampled atomic games vs the oracle
         torch.cuda.synchronize()
@@ -423,6 +440,8 @@ def atomic_extra(dist, rank, world, dev, games: int, reps: int = 5, check: bool 
                         f'{games:,} synthetic atomic games over {world} rank(s)',
             'atomic_actions_per_gpu': n, 'atomic_actions_total': total, 'scaling': 'strong',
             'ms_per_step': round(wall, 4),
+            'timing': f'median of {reps} steps (HIP events per step; min {ms_lo:.4f}, max '
+                      f'{ms_hi:.4f} ms on rank {rank})',
             'atomic_actions_per_s': round(total / wall * 1e3, 1), 'bytes_per_action': bpa,
             'frac_of_8TBs_per_gpu': round(bpa * n / ms * 1e-6 / HBM_PEAK_GBS, 4),
             **({'parity': par.record()} if check else {})}
@@ -430,7 +449,7 @@ def atomic_extra(dist, rank, world, dev, games: int, reps: int = 5, check: bool 
 
 def xt105_extra(ab, dist, dev, sharded: bool = False, cfg5_games: int = 62500,
                 rank: int = 0, world: int = 1, step_games: int = 10000, d=None,
-                check: bool = True) -> dict:
+                check: bool = True, reps: int = 21) -> dict:
     """BASELINE cfg5 alongside the main line: xT 105x68 fit of cfg5's 62,500 games (≈1.0e8
     actions; split over the ranks, so this entry scales strongly) -- count pass over this
     rank's games, RCCL all-reduce of the 7140-cell count vectors and 204 MB transition counts,
@@ -462,34 +481,62 @@ def xt105_extra(ab, dist, dev, sharded: bool = False, cfg5_games: int = 62500,
             gid += c
             left -= c
 
-    def once():
+    def once(marks=None):
+        def mark():  # the instrumented call only: phase boundaries (synchronised)
+            if marks is not None:
+                torch.cuda.synchronize()
+                marks.append(time.perf_counter())
+        mark()
+        # the count of every batch: band-owned (sa_xt_count_bucket per batch, the C x C table
+        # written once by sa_xt_count_from_buckets; no global atomics), into a fresh accumulator
+        # and, per action, the operand of the interpolated rate below (start / end node of the
+        # 1050 x 680 grid: 8 B read by the rate instead of 34 B of coordinates and ids)
         if sharded and dist is not None:  # reduce-scatter of count rows + row-sharded solve
             acc = ops.xt_zero_counts(l, w, dev, row_blocks=dist.get_world_size())
-            for b in batches:
-                ops.xt_count(b, l, w, acc)
+            ops.xt_count_many(batches, l, w, acc, overwrite=True, interp_codes=icodes)
+            mark()
+            mark()  # (the exchange happens inside the sharded solve)
             mats, _, n_iter = shard.xt_solve_sharded(acc)
             acc = None  # each rank holds only its row block of the transition counts
         else:  # one all-reduce of the counts, replicated solve
-            acc = ops.xt_zero_counts(l, w, dev)
-            for b in batches:
-                ops.xt_count(b, l, w, acc)
+            acc = ops.xt_count_many(batches, l, w, interp_codes=icodes)
+            mark()
             allreduce_counts(dist, acc)
+            mark()
             sol = ops.xt_solve(acc, transition=False)  # synchronises; ExpectedThreat.fit's
             mats, n_iter = sol.mats, sol.n_iter           # call above 1024 cells
+        mark()
         # rate(use_interpolation=True): each action's two node values evaluated in place from
-        # the 105 x 68 surface (sa_xt_rate_interp), bit-identical to the 1050 x 680 grid gather
+        # the 105 x 68 surface staged in LDS (sa_xt_rate_interp_codes), bit-identical to the
+        # 1050 x 680 grid gather
         xT = mats[3].reshape(w, l)
-        rates = [ops.xt_rate_interp(b, xT, l, w, 1050, 680, axes=axes)[0] for b in batches]
+        rates = [ops.xt_rate_interp_codes(c, b.n, xT, l, w, 1050, 680, axes=axes, out=o)[0]
+                 for b, c, o in zip(batches, icodes, rate_out)]
+        mark()
         return n_iter, acc, mats, rates
     axes = ops.xt_interp_axes(l, w, dev)  # node positions (constants of the reference's grid)
+    icodes = [ops.xt_interp_codes_buffer(b.n, dev) for b in batches]
+    rate_out = [torch.empty(max(b.n, 16), dtype=torch.float64, device=dev) for b in batches]
     once()  # warm-up (allocator, first launches)
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    n_iter, acc, mats, rates = once()
+    times = []
+    for _ in range(reps):  # each call wall-timed alone (the solve synchronises with the host)
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        n_iter, acc, mats, rates = once()
+        torch.cuda.synchronize()
+        times.append(time.perf_counter() - t0)
+    dt = float(np.median(times))
+    marks = []
+    once(marks)  # one more call, synchronised between phases: where the time goes
+    phases = dict(zip(('count', 'exchange', 'solve', 'rate'),
+                      (round((b - a) * 1e3, 3) for a, b in zip(marks, marks[1:]))))
+    n_iter, acc, mats, rates = once()  # the checked outputs come from an untouched call
     torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
     par = Parity()
-    if check:  # the timed call's counts, surface, iterations and the first batch's rates
+    if check:  # the last call's counts, surface, iterations and the first batch's rates
         ocnt = oracle_counts(None, l, w, dist, dev, acc=ocnt)
         if acc is None:  # row-sharded solve: the surface is checked, the counts are not held
             from oracle import xt_oracle as xo
@@ -516,8 +563,19 @@ def xt105_extra(ab, dist, dev, sharded: bool = False, cfg5_games: int = 62500,
                         f'rate(use_interpolation=True) of {games}',
             'actions_per_gpu': n, 'actions_total': total, 'iterations': n_iter,
             'ms_fit_and_rate': round(dt * 1e3, 3), 'actions_per_s': round(total / dt, 1),
+            'timing': f'median of {reps} calls (wall clock around each, after a warm-up call; '
+                      f'min {min(times) * 1e3:.3f}, max {max(times) * 1e3:.3f} ms on rank {rank})'
+                      + ('; max over ranks' if dist is not None else ''),
             'scaling': 'strong' if cfg5_games > 0 else 'weak',
             'solve': 'row-sharded' if (sharded and dist is not None) else 'replicated',
+            'phases_ms': dict(phases, note='one extra call synchronised between phases (rank '
+                              f'{rank}): count = band buckets + table; exchange = the counts\' '
+                              'all-reduce (sharded: inside solve); solve = normalise + value '
+                              'iteration incl. its host syncs; rate'),
+            'pipeline': 'band-owned count (per batch: one key per counted action, bucketed by '
+                        'start-cell band; the 7140^2 table written once, no global atomics) '
+                        'writing each action\'s 8-B interpolated-rate operand; value iteration '
+                        'over the compact count rows; rate from the operands (LDS surface)',
             **({'parity': par.record()} if check else {})}
 
 
@@ -1056,14 +1114,20 @@ def main() -> None:
                       'achieved_GBs': round(bts[k] * n / (kern[k] * 1e-3) / 1e9, 1),
                       'frac': round(bts[k] * n / (kern[k] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
                   for k in vaep}
-    traffic = None
+    traffic, traffic_src = None, 'no PMC record (profiles/pmc_dominant_kernel.json)'
     pmc = os.path.join(ROOT, 'profiles', 'pmc_dominant_kernel.json')
+    lib_id = (_native.lib().sa_build_id() or b'').decode()
     if os.path.exists(pmc):
         with open(pmc) as f:
             rec = json.load(f)
-        for k, v in rec.get('per_kernel', {rec.get('kernel', ''): rec.get('hbm_bytes_per_launch_per_action')}).items():
-            if KERNEL_NAMES[dom] in k and v is not None:
-                traffic = round(v * n)
+        if rec.get('build_id') != lib_id:  # counted on another build: not this kernel's bytes
+            traffic_src = (f"PMC record {rec.get('tag')} was counted on build "
+                           f"{rec.get('build_id')}, not the loaded {lib_id}: traffic omitted")
+        else:
+            for k, v in rec.get('per_kernel', {}).items():
+                if KERNEL_NAMES[dom] in k and v is not None:
+                    traffic = round(v * n)
+                    traffic_src = f"rocprofv3 PMC, record {rec.get('tag')}, build {lib_id}"
     line = {
         'metric': 'SPADL actions/sec valued (VAEP feat+labels+formula, xT fit+rate) at 1/2/4/8 GPUs',
         'value': round(value, 1), 'unit': 'actions/s', 'n_gpus': world, 'steps': args.steps,
@@ -1085,6 +1149,7 @@ def main() -> None:
         'roofline': {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS,
                      'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 4),
                      'traffic': traffic, 'traffic_unit': 'HBM bytes per launch (rocprofv3 PMC)',
+                     'traffic_source': traffic_src,
                      'algorithmic_bytes': bts[dom] * n, 'kernel': KERNEL_NAMES[dom],
                      'bytes_per_action': bts[dom],
                      # the whole step against the roofline: the VAEP path's 1,029 B/action

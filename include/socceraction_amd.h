@@ -83,7 +83,8 @@ typedef struct sa_actions {
   int32_t atomic;           /* 0 = SPADL, 1 = Atomic-SPADL */
   sa_frame frames[SA_MAX_FRAMES];
   /* optional (NULL = binary search of seg_off): segment of row b * SA_SEG_BLOCK for every
-   * block b < ceil(n / SA_SEG_BLOCK), written once per batch by sa_segment_blocks.  The kernels
+   * block b < ceil(n / SA_SEG_BLOCK), written once per batch by sa_segment_blocks for THIS
+   * seg_off and n (a table of another batch gives wrong segments).  The kernels
    * start every wave's segment cursor from it instead of a ~log2(n_segments)-deep chain of
    * dependent loads. */
   const int32_t* seg_of_block;
@@ -125,7 +126,8 @@ enum sa_xfn {
 /* Where each requested transformer writes: first column index inside the bool,
  * f64 and i64 output blocks (-1 = not requested / no columns of that dtype). */
 typedef struct sa_feature_plan {
-  int32_t nb_prev_actions;            /* k, 1..SA_MAX_FRAMES */
+  int32_t nb_prev_actions;            /* k: any k >= 1 in windowed mode (n_frames == 1);
+                                         explicit mode needs n_frames == k <= SA_MAX_FRAMES */
   int32_t bool_col[SA_XFN_COUNT];
   int32_t f64_col[SA_XFN_COUNT];
   int32_t i64_col[SA_XFN_COUNT];
@@ -280,6 +282,38 @@ int sa_xt_count_cells(const uint32_t* cells, int64_t n, int32_t l, int32_t w, in
 int sa_xt_rate_cells(const uint32_t* cells, int64_t n, int32_t l, int32_t w, const double* grid,
                      double* out, int32_t* err_flags, void* stream);
 
+/* Band-owned count of large grids (203 <= C <= ~12000 cells, e.g. 105 x 68; sa_xt_band_shape
+ * says whether a grid takes it): the transition counts without global atomics.  sa_xt_count,
+ * sa_xt_count_codes and sa_xt_count_cells use it internally for such grids; a fit over several
+ * device batches calls, per batch, sa_xt_count_bucket -- one 4-B key per counted action
+ * (start cell << 16 | end cell, or C / C+1 / C+2 for a shot / scored shot / move without a
+ * transition), sorted by start-cell band into buckets[n] (u32) with band_off[NB + 1] (int64,
+ * device) -- then ONCE sa_xt_count_from_buckets over every batch's buckets, which adds (or with
+ * SA_XT_COUNT_OVERWRITE writes) shot / goal / move and the C x C transition counts exactly as
+ * sa_xt_count over all the batches would; err_flags as sa_xt_count, set by the bucket call.
+ * `cells` (C <= SA_XT_CELLS_MAX_C) replaces the coordinates of `a` when not NULL (then `a` may
+ * be NULL and n is the action count); `codes` as in sa_xt_count_codes (coordinates only).
+ * buckets / band_off are plain device arrays the caller keeps until the count call.
+ * Replaces xthreat.py:40-67 (`_count`) and :177-218 (`move_transition_matrix` counts). */
+#define SA_XT_COUNT_OVERWRITE 2
+int sa_xt_band_shape(int32_t l, int32_t w, int32_t* rows_per_band, int32_t* n_bands);
+int sa_xt_count_bucket(const sa_actions* a, const uint32_t* cells, int64_t n, int32_t l, int32_t w,
+                       uint32_t* buckets, int64_t* band_off, int32_t* err_flags, uint32_t* codes,
+                       uint64_t* interp_codes, int32_t L, int32_t W, void* stream);
+/* interp_codes (coordinates only; [n] u64, 16-byte aligned, or NULL): per action the operand of a
+ * later rate(use_interpolation=True) of the SAME actions on the L x W node grid -- start node |
+ * end node << 32 of a successful move, 2^64 - 2 for one with a non-finite coordinate, 2^64 - 1
+ * otherwise -- consumed by sa_xt_rate_interp_codes, which then equals sa_xt_rate_interp on those
+ * actions bit for bit (values, NaN pattern, err_flags bit 4) reading 8 B per action. */
+int sa_xt_rate_interp_codes(const uint64_t* interp_codes, int64_t n, const double* xT,
+                            const double* cx, const double* cy, int32_t l, int32_t w,
+                            const double* xs, int32_t L, const double* ys, int32_t W, double* out,
+                            int32_t* err_flags, void* stream);
+int sa_xt_count_from_buckets(int32_t nsets, const uint32_t* const* buckets,
+                             const int64_t* const* band_off, int32_t l, int32_t w, int64_t* shot,
+                             int64_t* goal, int64_t* move, int32_t* trans, int32_t flags,
+                             void* stream);
+
 /* Grids up to SA_XT_SOLVE_MAX_C cells solve in one workgroup from the transposed matrix. */
 #define SA_XT_SOLVE_MAX_C 1024
 
@@ -326,6 +360,20 @@ int sa_xt_iterate_rows(const int32_t* cnt_rows, const int64_t* move, const doubl
                        const double* pmove, int32_t C, int32_t r0, int32_t nrows, const double* x,
                        double eps, double* x_next_rows, const int32_t* flag_prev, int32_t* flag_out,
                        void* stream);
+/* The same iteration over a compact form of the count rows built once (C <= 10240; sa_xt_solve
+ * uses it for C > SA_XT_SOLVE_MAX_C): sa_xt_compact_rows writes, per slice of 32 rows, each
+ * row's non-zero counts in column order (4 B each) into ell (u32, 16-byte aligned,
+ * sa_xt_compact_bytes(C, nrows) bytes) and the slice lengths into slice_len[(nrows + 31) / 32]
+ * (int32, device); sa_xt_iterate_compact then equals sa_xt_iterate_rows bit for bit (cnt_rows:
+ * the same dense rows, read only for counts >= 65535).  Asynchronous. */
+int64_t sa_xt_compact_bytes(int32_t C, int32_t nrows);
+int sa_xt_compact_rows(const int32_t* cnt_rows, int32_t C, int32_t nrows, uint32_t* ell,
+                       int32_t* slice_len, void* stream);
+int sa_xt_iterate_compact(const uint32_t* ell, const int32_t* slice_len, const int32_t* cnt_rows,
+                          const int64_t* move, const double* gs, const double* pmove, int32_t C,
+                          int32_t r0, int32_t nrows, const double* x, double eps,
+                          double* x_next_rows, const int32_t* flag_prev, int32_t* flag_out,
+                          void* stream);
 
 /* interp2d(x=cx, y=cy, z=xT, kind='linear')(xs, ys) of ExpectedThreat.interpolator
  * (xthreat.py:347-378): grid[r*L + h] = bilinear(xT; xs[h], ys[r]) through the cell

@@ -8,6 +8,9 @@ export TMPDIR=/tmp
 tag=${1:-r01}
 steps=${2:-10}
 mkdir -p gpurun_out
+# the build the counters are taken on (bench.py quotes roofline.traffic only for this build)
+python3 -c "import sys; sys.path.insert(0, '.'); from socceraction_amd.build import file_build_id, OUT; print(file_build_id(OUT))" \
+  > gpurun_out/prof_${tag}_build_id.txt
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${tag}_trace -o run \
   -- python3 bench.py --steps "$steps" --warmup 2 --no-cpu --no-side > gpurun_out/prof_${tag}_trace.log 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${tag}_side -o run \

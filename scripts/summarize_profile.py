@@ -6,7 +6,9 @@ Reads gpurun_out/prof_<tag>_{trace,fetch,write}/ (see scripts/profile_round.sh) 
   profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary of the step alone
   profiles/<tag>_side_kernel_stats.csv   the same with bench.py's side entries
   profiles/<tag>_pmc.csv            per-kernel mean FETCH_SIZE / WRITE_SIZE (KiB) + HBM bytes
-  profiles/pmc_dominant_kernel.json HBM bytes per action of the dominant kernel (read by bench.py)
+  profiles/pmc_dominant_kernel.json HBM bytes per action of the dominant kernel (read by bench.py,
+                                    which quotes them only while the loaded library's build id
+                                    equals the profiled one, gpurun_out/prof_<tag>_build_id.txt)
 HBM bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024: on gfx950 FETCH_SIZE reports half the
 bytes of wide streaming reads (MI355X_MICROARCH.md, HBM section); WRITE_SIZE is exact for
 16-byte-per-lane streaming stores.
@@ -45,7 +47,9 @@ def main(tag: str, n_actions: int, dominant=None) -> None:
         st = st[st.Name.str.contains('bool_colgroup_kernel|num_features_kernel')]
         dominant = st.sort_values('TotalDurationNs').Name.iloc[-1]
     feat = [k for k in df.index if dominant in k][0]
-    rec = {'tag': tag, 'kernel': feat, 'n_actions': n_actions,
+    bid = os.path.join(src, f'prof_{tag}_build_id.txt')
+    build_id = open(bid).read().strip() if os.path.exists(bid) else None
+    rec = {'tag': tag, 'build_id': build_id, 'kernel': feat, 'n_actions': n_actions,
            'fetch_kib': float(df.loc[feat, 'FETCH_SIZE']),
            'write_kib': float(df.loc[feat, 'WRITE_SIZE']),
            'hbm_bytes_per_launch_per_action': float(df.loc[feat, 'hbm_bytes_per_action']),

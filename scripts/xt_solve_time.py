@@ -52,7 +52,19 @@ def main():
     out['rate_cells_ms'] = _ms(lambda: ops.xt_rate_cells(cells, ab.n, 16, 12, grid), args.reps)
     if args.large:
         big = ops.xt_count(ab, 105, 68)
+        # sa_xt_count of one batch into a zeroed accumulator (band-owned: buckets + the table
+        # read and written once; the atomics variant build: XC_VEC global atomics)
         out['count_105x68_ms'] = _ms(lambda: ops.xt_count(ab, 105, 68), args.reps)
+        # the fit's form (bench cfg5): a fresh accumulator, the table written without a read
+        out['count_many_105x68_ms'] = _ms(lambda: ops.xt_count_many([ab], 105, 68), args.reps)
+        # random int32 atomics of the same number and spread into a 105x68 transition table
+        # (torch index_add_: one global atomic per element), the old pass's ceiling
+        C = 105 * 68
+        tbl = torch.zeros(C * C, dtype=torch.int32, device=ab.device)
+        idx = torch.randint(0, C * C, (int(big.trans.sum().item()),), device=ab.device)
+        one = torch.ones(idx.numel(), dtype=torch.int32, device=ab.device)
+        out['random_int32_atomics'] = idx.numel()
+        out['random_int32_atomics_ms'] = _ms(lambda: tbl.index_add_(0, idx, one), args.reps)
         sol = ops.xt_solve(big)
         out['iterations_105x68'] = sol.n_iter
         out['solve_105x68_ms_incl_host_sync'] = _ms(lambda: ops.xt_solve(big), args.reps)

@@ -23,6 +23,8 @@ SA_MAX_FRAMES = 8
 SA_SEG_BLOCK = 128  # rows per entry of sa_actions.seg_of_block
 SA_XT_SOLVE_MAX_C = 1024  # sa_xt_solve: larger grids may pass trans_t = NULL
 SA_XT_CELLS_MAX_C = 4096
+SA_XT_COUNT_SHARED, SA_XT_COUNT_OVERWRITE = 1, 2
+SA_XT_COMPACT_MAX_C = 10240  # sa_xt_compact_rows / sa_xt_iterate_compact
 SA_BOOL_TILE_QUANTUM = 1024
 SA_NUM_TILE_QUANTUM = 128
 SA_OK, SA_EINVAL, SA_EHIP, SA_EDATA, SA_ENOMEM = 0, -1, -2, -3, -4
@@ -147,6 +149,21 @@ _SIGNATURES = {
     'sa_xt_probabilities': (ctypes.c_int, [_p, _p, _p, ctypes.c_int32, _p, _p, _p, _p]),
     'sa_xt_iterate_rows': (ctypes.c_int, [_p, _p, _p, _p, ctypes.c_int32, ctypes.c_int32,
                                           ctypes.c_int32, _p, ctypes.c_double, _p, _p, _p, _p]),
+    'sa_xt_band_shape': (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32),
+                                        ctypes.POINTER(ctypes.c_int32)]),
+    'sa_xt_count_bucket': (ctypes.c_int, [ctypes.POINTER(SaActions), _p, ctypes.c_int64, ctypes.c_int32,
+                                          ctypes.c_int32, _p, _p, _p, _p, _p, ctypes.c_int32,
+                                          ctypes.c_int32, _p]),
+    'sa_xt_rate_interp_codes': (ctypes.c_int, [_p, ctypes.c_int64, _p, _p, _p, ctypes.c_int32,
+                                               ctypes.c_int32, _p, ctypes.c_int32, _p, ctypes.c_int32,
+                                               _p, _p, _p]),
+    'sa_xt_count_from_buckets': (ctypes.c_int, [ctypes.c_int32, ctypes.POINTER(_p), ctypes.POINTER(_p),
+                                                ctypes.c_int32, ctypes.c_int32, _p, _p, _p, _p,
+                                                ctypes.c_int32, _p]),
+    'sa_xt_compact_bytes': (ctypes.c_int64, [ctypes.c_int32, ctypes.c_int32]),
+    'sa_xt_compact_rows': (ctypes.c_int, [_p, ctypes.c_int32, ctypes.c_int32, _p, _p, _p]),
+    'sa_xt_iterate_compact': (ctypes.c_int, [_p, _p, _p, _p, _p, _p, ctypes.c_int32, ctypes.c_int32,
+                                             ctypes.c_int32, _p, ctypes.c_double, _p, _p, _p, _p]),
     'sa_xt_interp_grid': (ctypes.c_int, [_p, _p, _p, ctypes.c_int32, ctypes.c_int32, _p,
                                          ctypes.c_int32, _p, ctypes.c_int32, _p, _p]),
     'sa_xt_rate': (ctypes.c_int, [ctypes.POINTER(SaActions), _p, ctypes.c_int32, ctypes.c_int32,

@@ -26,7 +26,7 @@ CSRC = os.path.join(HERE, 'csrc')
 LIBDIR = os.path.join(HERE, '_lib')
 OUT = os.path.join(LIBDIR, 'libsocceraction_amd.so')
 DEBUG_OUT = os.path.join(LIBDIR, 'libsocceraction_amd_debug.so')
-SOURCES = ['sa_api.hip', 'sa_vaep.hip', 'sa_xt.hip', 'sa_atomic.hip', 'sa_trees.hip', 'sa_store.hip']
+SOURCES = ['sa_api.hip', 'sa_vaep.hip', 'sa_xt.hip', 'sa_xt_large.hip', 'sa_atomic.hip', 'sa_trees.hip', 'sa_store.hip']
 HEADERS = ['sa_common.h', 'sa_internal.h', 'sa_debug.h',
            os.path.join('..', '..', 'include', 'socceraction_amd.h')]
 FLAGS = ['-O3', '--offload-arch=gfx950', '-ffp-contract=off', '-fPIC', '-shared', '-std=c++17',

@@ -88,6 +88,39 @@ void scratch_release(const Scratch& s, hipStream_t st) {
   sl.busy = false;
 }
 
+// ------------------------------------------------------------------------ device attributes
+namespace {
+constexpr int MAX_DEVICES = 64;
+std::mutex g_attr_mu;
+int g_cus[MAX_DEVICES], g_lds[MAX_DEVICES];
+}  // namespace
+
+int current_device() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return dev;
+}
+
+static int device_attr(int dev, int* cache, hipDeviceAttribute_t attr, int fallback) {
+  if (dev < 0 || dev >= MAX_DEVICES) return fallback;
+  std::lock_guard<std::mutex> lk(g_attr_mu);
+  if (!cache[dev]) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, attr, dev) != hipSuccess || v < 1) {
+      (void)hipGetLastError();
+      v = fallback;
+    }
+    cache[dev] = v;
+  }
+  return cache[dev];
+}
+
+int device_cus(int dev) { return device_attr(dev, g_cus, hipDeviceAttributeMultiprocessorCount, 256); }
+int device_lds_max(int dev) { return device_attr(dev, g_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, 64 * 1024); }
+
 // ------------------------------------------------------------------------ debug collector
 namespace {
 std::mutex g_dbg_mu;

@@ -15,6 +15,8 @@
 namespace sa {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
+typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 typedef double f64x2 __attribute__((ext_vector_type(2)));
 typedef long long i64x2 __attribute__((ext_vector_type(2)));
 
@@ -112,6 +114,75 @@ __device__ __forceinline__ uint32_t xt_cell_code(int t, int r, double sx, double
   if (cls != 0 && sfin) c |= (uint32_t)flat_index(sx, sy, l, w);
   if (cls == XT_CELL_MOVE && efin) c |= (uint32_t)flat_index(ex, ey, l, w) << 12;
   return c;
+}
+
+
+// ---- shared by the xT count passes (sa_xt.hip, sa_xt_large.hip) ----
+// Rate operand of one action for a later rate() on the same (l, w) grid, written by the count
+// pass so the rate pass reads 4 B instead of the 34 B of coordinates and ids again
+// (xthreat.py:440-465 without interpolation): start cell | end cell << 16 for a successful
+// move with finite coordinates, XT_CODE_BAD for a successful move with a non-finite one (the
+// reference's int64 cast raises), XT_CODE_NAN for every other action (rated NaN).
+constexpr uint32_t XT_CODE_NAN = 0xFFFFFFFFu, XT_CODE_BAD = 0xFFFFFFFEu;
+
+__device__ __forceinline__ uint32_t rate_code(int t, int r, double sx, double sy, double ex, double ey,
+                                              int l, int w) {
+  if (!is_move(t) || r != R_SUCCESS) return XT_CODE_NAN;
+  if (!isfinite(sx) || !isfinite(sy) || !isfinite(ex) || !isfinite(ey)) return XT_CODE_BAD;
+  return (uint32_t)flat_index(sx, sy, l, w) | ((uint32_t)flat_index(ex, ey, l, w) << 16);
+}
+
+// The operand of a rate(use_interpolation=True) of the same action on the L x W node grid
+// (xthreat.py:443-464: the start and end node of a successful move), u64 so that L * W up to 2^31
+// fits: start node | end node << 32; markers as rate_code.
+constexpr uint64_t XT_ICODE_NAN = ~0ull, XT_ICODE_BAD = ~0ull - 1;
+
+__device__ __forceinline__ uint64_t rate_icode(int t, int r, double sx, double sy, double ex, double ey,
+                                               int L, int W) {
+  if (!is_move(t) || r != R_SUCCESS) return XT_ICODE_NAN;
+  if (!isfinite(sx) || !isfinite(sy) || !isfinite(ex) || !isfinite(ey)) return XT_ICODE_BAD;
+  return (uint64_t)(uint32_t)flat_index(sx, sy, L, W) | ((uint64_t)(uint32_t)flat_index(ex, ey, L, W) << 32);
+}
+
+// One action's part of the count pass: shot/goal/move histograms and the successful-move
+// transition count, with the reference's non-finite rules (xthreat.py:40-67: _count drops rows
+// with a NaN start, casts the rest; :177-218: move_transition_matrix casts every move
+// coordinate).  Error flags, one byte each so that a sum all-reduce of the ranks' flags keeps
+// them apart: 0x1 = infinite shot start, 0x100 = infinite move start, 0x10000 = NaN move start
+// or non-finite move end (see sa_xt_count).
+constexpr int32_t XT_ERRB_SHOT = 0x1, XT_ERRB_MOVE_START = 0x100, XT_ERRB_MOVE_OTHER = 0x10000;
+
+struct XtAct {
+  uint32_t cls;            // 0, XT_CELL_SHOT, XT_CELL_MOVE
+  bool succ, snan, sfin, efin;
+  int cs, ce;              // start / end cell (valid when binned)
+};
+
+__device__ __forceinline__ XtAct decode_cell(uint32_t c) {
+  XtAct a;
+  a.cls = (c >> 24) & 3u;
+  a.succ = (c >> 26) & 1u;
+  a.snan = (c >> 27) & 1u;
+  a.sfin = !((c >> 28) & 1u);
+  a.efin = !((c >> 29) & 1u);
+  a.cs = (int)(c & 0xFFFu);
+  a.ce = (int)((c >> 12) & 0xFFFu);
+  return a;
+}
+
+
+// The XtAct of one action from its row (the coordinate form of decode_cell; t < 0: not counted).
+__device__ __forceinline__ XtAct act_from_row(int t, int r, double sx, double sy, double ex, double ey, int l,
+                                              int w) {
+  XtAct a;
+  a.cls = t == T_SHOT ? XT_CELL_SHOT : (is_move(t) ? XT_CELL_MOVE : 0u);
+  a.succ = r == R_SUCCESS;
+  a.snan = isnan(sx) || isnan(sy);
+  a.sfin = isfinite(sx) && isfinite(sy);
+  a.efin = isfinite(ex) && isfinite(ey);
+  a.cs = (a.cls && a.sfin) ? flat_index(sx, sy, l, w) : 0;
+  a.ce = (a.cls == XT_CELL_MOVE && a.succ && a.efin) ? flat_index(ex, ey, l, w) : 0;
+  return a;
 }
 
 }  // namespace sa

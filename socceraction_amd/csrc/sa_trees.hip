@@ -44,6 +44,7 @@ constexpr int TR_LDS_SLOTS = 2048;  // 8 KB
 #define SA_TREE_FIXED 1  // tree_depth given: fixed-depth walk over self-looping leaves
 #endif
 constexpr int TG = SA_TREE_TG;      // trees walked together per thread
+static_assert(TG >= 1 && TG <= 32, "SA_TREE_TG: trees per thread");
 
 // Row j's element of column `col` in each tiled block is base[kind] + col * R[kind]; the
 // per-row bases are computed once (one division per block) instead of per feature read.

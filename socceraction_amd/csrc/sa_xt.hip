@@ -20,25 +20,17 @@
 #ifndef SA_XC_UC
 #define SA_XC_UC 8  // count pass from cell codes: codes per thread per pass, all loaded first
 #endif
+#ifndef SA_XT_BANDS
+#define SA_XT_BANDS 1  // grids the band-owned count holds (sa_xt_large.hip); 0: XC_VEC / XC_GLOBAL atomics
+#endif
+#ifndef SA_XT_COMPACT
+#define SA_XT_COMPACT 1  // large-grid solve over the compact count rows (0: xt_iter_kernel on the dense rows)
+#endif
 #ifndef SA_XT_WIDE
 #define SA_XT_WIDE 1  // C <= 197: XC_WIDE count pass (0: the 32k-action XC_SMALL workgroups)
 #endif
 
 namespace sa {
-
-// Rate operand of one action for a later rate() on the same (l, w) grid, written by the count
-// pass so the rate pass reads 4 B instead of the 34 B of coordinates and ids again
-// (xthreat.py:440-465 without interpolation): start cell | end cell << 16 for a successful
-// move with finite coordinates, XT_CODE_BAD for a successful move with a non-finite one (the
-// reference's int64 cast raises), XT_CODE_NAN for every other action (rated NaN).
-constexpr uint32_t XT_CODE_NAN = 0xFFFFFFFFu, XT_CODE_BAD = 0xFFFFFFFEu;
-
-__device__ __forceinline__ uint32_t rate_code(int t, int r, double sx, double sy, double ex, double ey,
-                                              int l, int w) {
-  if (!is_move(t) || r != R_SUCCESS) return XT_CODE_NAN;
-  if (!isfinite(sx) || !isfinite(sy) || !isfinite(ex) || !isfinite(ey)) return XT_CODE_BAD;
-  return (uint32_t)flat_index(sx, sy, l, w) | ((uint32_t)flat_index(ex, ey, l, w) << 16);
-}
 
 // ---------------------------------------------------------------------------------------------
 // Count pass.  XC_SMALL: per-workgroup LDS histograms (u32 for the three C-vectors, the C x C
@@ -55,20 +47,6 @@ constexpr int XT_THREADS = 256;
 constexpr int XT_WIDE_THREADS = 1024;
 constexpr int XT_SMALL_ACTS = 32768;  // actions per workgroup in XC_SMALL / XC_VEC
 enum { XC_GLOBAL = 0, XC_VEC = 1, XC_SMALL = 2, XC_WIDE = 3 };
-
-// One action's part of the count pass: shot/goal/move histograms and the successful-move
-// transition count, with the reference's non-finite rules (xthreat.py:40-67: _count drops rows
-// with a NaN start, casts the rest; :177-218: move_transition_matrix casts every move
-// coordinate).  Error flags, one byte each so that a sum all-reduce of the ranks' flags keeps
-// them apart: 0x1 = infinite shot start, 0x100 = infinite move start, 0x10000 = NaN move start
-// or non-finite move end (see sa_xt_count).
-constexpr int32_t XT_ERRB_SHOT = 0x1, XT_ERRB_MOVE_START = 0x100, XT_ERRB_MOVE_OTHER = 0x10000;
-
-struct XtAct {
-  uint32_t cls;            // 0, XT_CELL_SHOT, XT_CELL_MOVE
-  bool succ, snan, sfin, efin;
-  int cs, ce;              // start / end cell (valid when binned)
-};
 
 template <int MODE>
 __device__ __forceinline__ void count_one(const XtAct& a, int C, uint32_t* hs, uint32_t* hg, uint32_t* hm,
@@ -119,18 +97,6 @@ __device__ __forceinline__ void count_one(const XtAct& a, int C, uint32_t* hs, u
         atomicAdd(&trans[k], 1);
     }
   }
-}
-
-__device__ __forceinline__ XtAct decode_cell(uint32_t c) {
-  XtAct a;
-  a.cls = (c >> 24) & 3u;
-  a.succ = (c >> 26) & 1u;
-  a.snan = (c >> 27) & 1u;
-  a.sfin = !((c >> 28) & 1u);
-  a.efin = !((c >> 29) & 1u);
-  a.cs = (int)(c & 0xFFFu);
-  a.ce = (int)((c >> 12) & 0xFFFu);
-  return a;
 }
 
 // CELLS = false: reads the actions' coordinates and ids (34 B per action) and may write each
@@ -482,6 +448,7 @@ constexpr int XI_NI = XI_CH / 64;
 static_assert(XI_RQ >= 1 && XI_RQ * XI_LOADERS == XI_ROWS && XI_NI >= 1 && XI_NI * 64 == XI_CH &&
                   (XI_ROWS & (XI_ROWS - 1)) == 0 && XI_ROWS <= 64,
               "xt_iter_kernel shape");
+static_assert(XI_THREADS <= 1024, "xt_iter_kernel: SA_XI_LOADERS + 1 waves must fit one workgroup");
 constexpr int XI_DEPTH = SA_XI_DEPTH;  // chunks in flight per loader lane
 constexpr int XI_LST = XI_CH + 1;      // list row stride (doubles): chain reads hit 16 banks
 
@@ -785,6 +752,8 @@ __global__ __launch_bounds__(256) void xt_rate_interp_kernel(sa_actions A, const
 #define SA_XRI_BPC 4  // workgroups per CU in the grid (one resident at a time): 1 / 2 / 4 / 8 / 16: 0.156 / 0.150 / 0.147 / 0.160 / 0.185 ms
 #endif
 constexpr int XRI_THREADS = SA_XRI_THREADS;
+static_assert(XRI_THREADS % 64 == 0 && XRI_THREADS <= 1024 && SA_XRI_U >= 1 && SA_XRI_BPC >= 1,
+              "xt_rate_interp_lds_kernel shape (SA_XRI_THREADS / SA_XRI_U / SA_XRI_BPC)");
 constexpr size_t XRI_LDS_MAX = 78 * 1024;
 
 __device__ __forceinline__ void rate_interp_pair(const sa_frame& F, int64_t n, int64_t j0, int vec,
@@ -855,6 +824,59 @@ __global__ __launch_bounds__(XRI_THREADS) void xt_rate_interp_lds_kernel(sa_acti
     } else {
       for (int u = 0; u < U && p + u * stride < pairs; ++u)
         rate_interp_pair(F, n, 2 * (p + u * stride), vec, sxT, l, L, W, sidx, sfrac, out, bad);
+    }
+  }
+  if (bad && err) atomicOr(err, bad);
+}
+
+// rate(use_interpolation=True) from the u64 node operands the count pass wrote (rate_icode,
+// sa_xt_count_bucket): xt_rate_interp_lds_kernel's LDS-staged surface and node tables and its
+// node_value operations -- bit-identical values, NaN pattern and error bit 4 -- reading 8 B per
+// action instead of the 34 B of coordinates and ids.  A thread rates 2 consecutive actions per
+// pass (one 16-B code load, one 16-B store), U pairs per pass, every load before the stores.
+__global__ __launch_bounds__(XRI_THREADS) void xt_rate_icodes_lds_kernel(const uint64_t* __restrict__ icodes,
+                                                                        int64_t n, const double* __restrict__ xT,
+                                                                        int l, int w, int L, int W,
+                                                                        const int32_t* __restrict__ idx,
+                                                                        const double* __restrict__ frac,
+                                                                        double* __restrict__ out,
+                                                                        int32_t* __restrict__ err) {
+  extern __shared__ __attribute__((aligned(16))) double xri_lds[];
+  double* sxT = xri_lds;                                        // [w * l]
+  double* sfrac = sxT + w * l;                                  // [L + W]
+  int32_t* sidx = reinterpret_cast<int32_t*>(sfrac + (L + W));  // [L + W]
+  for (int k = threadIdx.x; k < w * l; k += blockDim.x) sxT[k] = xT[k];
+  for (int k = threadIdx.x; k < L + W; k += blockDim.x) {
+    sfrac[k] = frac[k];
+    sidx[k] = idx[k];
+  }
+  __syncthreads();
+  const int64_t pairs = (n + 1) / 2, stride = (int64_t)gridDim.x * blockDim.x;
+  int32_t bad = 0;
+  auto one = [&](uint64_t c) -> double {
+    if (c == XT_ICODE_NAN) return __builtin_nan("");
+    if (c == XT_ICODE_BAD) {
+      bad = 4;
+      return __builtin_nan("");
+    }
+    const int s = (int)(uint32_t)c, e = (int)(c >> 32);
+    SA_DGUARD(s >= 0 && s < L * W && e >= 0 && e < L * W, s, return __builtin_nan(""));
+    return node_value(sxT, l, L, e, sidx, sfrac) - node_value(sxT, l, L, s, sidx, sfrac);
+  };
+  constexpr int U = SA_XRI_U;
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < pairs; p += U * stride) {
+    if (2 * (p + (U - 1) * stride) + 1 < n) {
+      u64x2 c[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) c[u] = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(icodes + 2 * (p + u * stride)));
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const f64x2 v = {one(c[u][0]), one(c[u][1])};
+        __builtin_nontemporal_store(v, reinterpret_cast<f64x2*>(out + 2 * (p + u * stride)));
+      }
+    } else {
+      for (int u = 0; u < U && p + u * stride < pairs; ++u)
+        for (int64_t j = 2 * (p + u * stride); j < 2 * (p + u * stride) + 2 && j < n; ++j) out[j] = one(icodes[j]);
     }
   }
   if (bad && err) atomicOr(err, bad);
@@ -956,19 +978,16 @@ static int launch_count(const sa_actions& A, const uint32_t* cells, int64_t n, i
   } while (0)
   if (SA_XT_WIDE && wide_lds <= 150 * 1024 && !shared) {
     // one workgroup per CU (or fewer when there are few actions: >= 4096 actions each)
-    static int cus = 0;
-    if (!cus) {
-      int dev = 0;
-      if (hipGetDevice(&dev) != hipSuccess ||
-          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
-        cus = 256;
-    }
+    const int cus = device_cus(current_device());
     int64_t blocks = (n + 4095) / 4096;
     if (blocks > cus) blocks = cus;
     const int64_t chunk = (n + blocks - 1) / blocks;
     SA_COUNT_LAUNCH(XC_WIDE, dim3((unsigned)blocks), dim3(XT_WIDE_THREADS), wide_lds, chunk);
   } else if (small_lds <= 80 * 1024) {
     SA_COUNT_LAUNCH(XC_SMALL, dim3(wg_blocks), dim3(XT_THREADS), small_lds, XT_SMALL_ACTS);
+  } else if (SA_XT_BANDS && xt_band_ok(C) && n <= INT32_MAX) {
+    // band-owned count (sa_xt_large.hip): no global atomics into the C x C table
+    return xt_count_bands(A, cells, n, l, w, shot, goal, move, trans, err_flags, codes, st);
   } else if (vec_lds <= 120 * 1024) {
     SA_COUNT_LAUNCH(XC_VEC, dim3(wg_blocks), dim3(XT_THREADS), vec_lds, XT_SMALL_ACTS);
   } else {
@@ -1104,16 +1123,35 @@ extern "C" int sa_xt_solve(const int64_t* shot, const int64_t* goal, const int64
   } else if (!rc) {
     rc = check_hip(hipMemsetAsync(dflags, 0, sizeof(int32_t) * (max_iter + 1), st), "memset");
     if (!rc) rc = check_hip(hipMemsetAsync(heatmaps, 0, sizeof(double) * C, st), "memset");
+    // the compact form of the count rows, built once (sa_xt_large.hip): [ell | slice_len]
+    const bool compact = SA_XT_COMPACT && xt_compact_ok(C);
+    Scratch ce;
+    uint32_t* ell = nullptr;
+    int32_t* slen = nullptr;
+    if (!rc && compact) {
+      const size_t eb = (xt_compact_bytes(C, C) + 255) & ~(size_t)255;
+      rc = scratch_acquire(eb + sizeof(int32_t) * (size_t)C, st, &ce);
+      if (!rc) {
+        ell = static_cast<uint32_t*>(ce.ptr);
+        slen = reinterpret_cast<int32_t*>(static_cast<char*>(ce.ptr) + eb);
+        rc = xt_compact_build(trans, C, C, ell, slen, st);
+      }
+    }
     std::vector<int32_t> hflags(max_iter + 1, 0);
     const int batch = 8;
     for (int it0 = 0; !rc && it0 < max_iter && iters < 0; it0 += batch) {
       const int it1 = it0 + batch < max_iter ? it0 + batch : max_iter;
-      for (int it = it0; it < it1; ++it)
-        hipLaunchKernelGGL(xt_iter_kernel, dim3((C + XI_ROWS - 1) / XI_ROWS), dim3(XI_THREADS), 0, st,
-                           trans, um, gs, pm, C, 0, C, eps, heatmaps + (int64_t)it * C,
-                           heatmaps + (int64_t)(it + 1) * C, it > 0 ? dflags + it - 1 : nullptr,
-                           dflags + it);
-      rc = check_launch("xt_iter_kernel");
+      for (int it = it0; it < it1 && !rc; ++it) {
+        double* xi = heatmaps + (int64_t)it * C;
+        const int32_t* fp = it > 0 ? dflags + it - 1 : nullptr;
+        if (compact) {
+          rc = xt_compact_iterate(ell, slen, trans, move, gs, pm, C, 0, C, xi, eps, xi + C, fp, dflags + it, st);
+        } else {
+          hipLaunchKernelGGL(xt_iter_kernel, dim3((C + XI_ROWS - 1) / XI_ROWS), dim3(XI_THREADS), 0, st, trans, um,
+                             gs, pm, C, 0, C, eps, xi, xi + C, fp, dflags + it);
+          rc = check_launch("xt_iter_kernel");
+        }
+      }
       if (!rc) rc = check_hip(hipMemcpyAsync(hflags.data() + it0, dflags + it0,
                                              sizeof(int32_t) * (it1 - it0), hipMemcpyDeviceToHost, st),
                               "copy flags");
@@ -1131,6 +1169,7 @@ extern "C" int sa_xt_solve(const int64_t* shot, const int64_t* goal, const int64
                      "copy xT");
       if (!rc) rc = check_hip(hipStreamSynchronize(st), "hipStreamSynchronize");
     }
+    if (compact) scratch_release(ce, st);
   }
   scratch_release(sc, st);
   *n_iter = iters;
@@ -1206,14 +1245,9 @@ extern "C" int sa_xt_rate_interp(const sa_actions* a, const double* xT, const do
                   ((uintptr_t)F.type_id & 1u) == 0 && ((uintptr_t)F.result_id & 1u) == 0;
   const int64_t threads = (a->n + 1) / 2;
   const size_t lds = sizeof(double) * ((size_t)l * w + L + W) + sizeof(int32_t) * (size_t)(L + W);
-  if (lds <= XRI_LDS_MAX) {  // the surface and node tables in LDS, persistent workgroups
-    static int cus = 0;
-    if (!cus) {
-      int dev = 0;
-      if (hipGetDevice(&dev) != hipSuccess ||
-          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
-        cus = 256;
-    }
+  const int dev = current_device();
+  if (lds <= XRI_LDS_MAX && lds <= (size_t)device_lds_max(dev)) {  // surface + node tables in LDS
+    const int cus = device_cus(dev);
     const int64_t need = (threads + XRI_THREADS - 1) / XRI_THREADS;
     const int64_t most = (int64_t)cus * SA_XRI_BPC;
     const unsigned blocks = (unsigned)(need < most ? need : most);
@@ -1225,6 +1259,37 @@ extern "C" int sa_xt_rate_interp(const sa_actions* a, const double* xT, const do
                        L, W, idx, frac, out, err_flags, vec);
     rc = check_launch("xt_rate_interp_kernel");
   }
+  scratch_release(sc, st);
+  return rc;
+}
+
+extern "C" int sa_xt_rate_interp_codes(const uint64_t* interp_codes, int64_t n, const double* xT, const double* cx,
+                                       const double* cy, int32_t l, int32_t w, const double* xs, int32_t L,
+                                       const double* ys, int32_t W, double* out, int32_t* err_flags, void* stream) {
+  if (n < 0 || !xT || !cx || !cy || !xs || !ys || L < 1 || W < 1 || (n > 0 && (!interp_codes || !out)))
+    return fail(SA_EINVAL, "bad xt_rate_interp_codes args");
+  if (l < 2 || w < 2) return fail(SA_EINVAL, "interpolation needs at least 2 cells per axis");
+  if ((int64_t)L * W > INT32_MAX) return fail(SA_EINVAL, "interpolated grid too large");
+  if (n > 0 && (!aligned16(interp_codes) || !aligned16(out))) return fail(SA_EINVAL, "codes and out must be 16-byte aligned");
+  const size_t lds = sizeof(double) * ((size_t)l * w + L + W) + sizeof(int32_t) * (size_t)(L + W);
+  const int dev = current_device();
+  if (lds > XRI_LDS_MAX || lds > (size_t)device_lds_max(dev))
+    return fail(SA_EINVAL, "surface and node tables exceed the LDS");
+  if (n == 0) return SA_OK;
+  hipStream_t st = (hipStream_t)stream;
+  Scratch sc;  // frac[L + W] | idx[L + W]
+  int rc = scratch_acquire((sizeof(double) + sizeof(int32_t)) * (size_t)(L + W), st, &sc);
+  if (rc) return rc;
+  double* frac = static_cast<double*>(sc.ptr);
+  int32_t* idx = reinterpret_cast<int32_t*>(frac + (L + W));
+  hipLaunchKernelGGL(xt_axes_kernel, dim3((unsigned)((L + W + 255) / 256)), dim3(256), 0, st, cx, cy, l, w, xs, L,
+                     ys, W, idx, frac);
+  const int64_t threads = (n + 1) / 2;
+  const int64_t need = (threads + XRI_THREADS - 1) / XRI_THREADS;
+  const int64_t most = (int64_t)device_cus(dev) * SA_XRI_BPC;
+  hipLaunchKernelGGL(xt_rate_icodes_lds_kernel, dim3((unsigned)(need < most ? need : most)), dim3(XRI_THREADS), lds,
+                     st, interp_codes, n, xT, l, w, L, W, idx, frac, out, err_flags);
+  rc = check_launch("xt_rate_icodes_lds_kernel");
   scratch_release(sc, st);
   return rc;
 }

@@ -1,0 +1,774 @@
+// Expected Threat (xT) fit on large grids -- e.g. the 105 x 68 grid of BASELINE cfg5: C = 7140
+// cells, 51M transition bins -- for gfx950.  Reference: socceraction/xthreat.py.
+//
+// 1. Band-owned transition count (xthreat.py:40-67 `_count`, :177-218 `move_transition_matrix`)
+//    without global atomics.  Random int32 atomics into the 204 MB transition table execute at
+//    the memory side, one uncached request per lane (MI355X_MICROARCH.md "Global float atomics":
+//    64 lanes in 64 rows ~0.08 TB/s); the round-3 XC_VEC pass sat on that ceiling (0.446 ms per
+//    16M actions).  Here the start cells are cut into bands of R consecutive cells and every
+//    counted action becomes one 4-B key (start cell << 16 | slot):
+//      K1 xt_keys_kernel        reads the actions once, writes each workgroup's keys contiguously
+//                               (wave ballots) and the keys per band;
+//      K2 xt_band_scan_kernel   band offsets (exclusive scan);
+//      K3 xt_keys_scatter_kernel  a counting sort of each workgroup's keys by band in LDS, then
+//                               runs of keys into the band buckets;
+//      K4 xt_band_count_kernel  one workgroup per band: its R rows x (C + 3) bins as u32 in LDS
+//                               (143 KB at 105 x 68), filled from the band's bucket(s), flushed
+//                               once with coalesced stores -- the shot / goal / move counts of
+//                               the band's cells come from the same bins (slots C, C + 1, C + 2).
+//    K1-K3 run per batch of actions (sa_xt_count_bucket); K4 runs once over the buckets of every
+//    batch (sa_xt_count_from_buckets), so the 204 MB table is written once per fit.
+// 2. Value iteration (xthreat.py:278-320) over a compact form of the counts built once per solve
+//    (sa_xt_compact_rows): per slice of 32 rows the non-zero counts of each row in column order,
+//    4 B each (column | count << 16), interleaved by row (entry k of row i at k * 32 + i) so a
+//    wave reads 256 contiguous bytes.  Per iteration (xt_iter_ell_kernel) eight product waves form
+//    T[r, c] * x[c] = (cnt / move[r]) * x[c] -- the quotient tabulated in LDS for counts < 64, the
+//    same correctly rounded division -- and one chain wave adds each row's products strictly left
+//    to right (the reference's loop order; zero terms add +0 to a non-negative sum, so skipping
+//    them keeps every bit).  84 MB per iteration instead of the 204 MB dense int32 rows.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <vector>
+
+#include "sa_common.h"
+#include "sa_internal.h"
+
+namespace sa {
+
+// ============================================================================ band-owned count
+constexpr int XK_THREADS = 256;     // K1 workgroup
+constexpr int XK_CHUNK = 32768;     // actions per K1 workgroup = key capacity of its region
+constexpr int XS_THREADS = 1024;    // K3 workgroup
+constexpr int XS_PER = XK_CHUNK / XS_THREADS;
+constexpr int XB_THREADS = 1024;    // K4 workgroup
+constexpr int XB_MAX_ROWS = 8;      // start cells per band
+constexpr int XB_NB_MAX = 4000;     // bands (K3 holds 2 words per band + a region's keys in LDS)
+constexpr size_t XB_LDS_MAX = 160 * 1024;
+constexpr int XB_MAX_SETS = 24;     // buckets per K4 launch
+constexpr uint32_t XB_NONE = 0xFFFFFFFFu;
+static_assert(XS_PER * XS_THREADS == XK_CHUNK, "K3 holds one K1 region");
+static_assert(XK_CHUNK * 4 + 2 * XB_NB_MAX * 4 + 256 <= XB_LDS_MAX, "K3 LDS");
+
+struct XbShape {
+  int C;           // cells
+  int R;           // start cells per band
+  int NB;          // bands
+  int P;           // LDS pitch of a band row in K4 (>= C + 3, multiple of 4)
+  uint64_t magic;  // band of start cell cs = (cs * magic) >> 32 = cs / R for cs < 2^16
+};
+
+__device__ __forceinline__ uint32_t band_of(uint32_t key, uint64_t magic) {
+  return (uint32_t)(((uint64_t)(key >> 16) * magic) >> 32);
+}
+
+// One action -> its key (false: not counted).  Slots: the end cell of a successful move with
+// finite coordinates (a transition; also counted in move), C = shot, C + 1 = scored shot,
+// C + 2 = a move without a transition.  Same non-finite rules and error bytes as count_one
+// (sa_xt.hip): a NaN start drops the action from _count, a cast of a non-finite coordinate
+// raises in the reference.
+__device__ __forceinline__ bool band_key(const XtAct& a, int C, uint32_t& key, int32_t& bad) {
+  uint32_t slot;
+  if (a.cls == XT_CELL_SHOT) {
+    if (a.snan) return false;
+    if (!a.sfin) {
+      bad |= XT_ERRB_SHOT;
+      return false;
+    }
+    slot = (uint32_t)C + (a.succ ? 1u : 0u);
+  } else if (a.cls == XT_CELL_MOVE) {
+    if (a.snan) {
+      bad |= XT_ERRB_MOVE_OTHER;
+      return false;
+    }
+    if (!a.sfin) {
+      bad |= XT_ERRB_MOVE_START;
+      return false;
+    }
+    if (!a.efin) {
+      bad |= XT_ERRB_MOVE_OTHER;
+      slot = (uint32_t)C + 2u;
+    } else {
+      slot = a.succ ? (uint32_t)a.ce : (uint32_t)C + 2u;
+    }
+  } else {
+    return false;
+  }
+  key = ((uint32_t)a.cs << 16) | slot;
+  return true;
+}
+
+__device__ __forceinline__ uint32_t lane_rank(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// Per-action rate operands the coordinate pass can write while it holds the coordinates:
+// codes = sa_xt_count_codes' u32 operand of a rate on the (l, w) grid; icodes = the u64 operand
+// of a rate(use_interpolation=True) on the L x W node grid (start node | end node << 32 of a
+// successful move, XT_ICODE_BAD / XT_ICODE_NAN as rate_code's markers).
+struct XkRate {
+  uint32_t* codes;
+  uint64_t* icodes;
+  int L, W;
+};
+
+// K1: region r = actions [r * XK_CHUNK, (r + 1) * XK_CHUNK) -> keys[r * XK_CHUNK + i], i <
+// region_cnt[r]; band_cnt[b] += the region's keys of band b.  CELLS: 4-B cell codes
+// (sa_xt_cells, C <= SA_XT_CELLS_MAX_C) instead of the coordinates (no rate operands then).
+template <bool CELLS>
+__global__ __launch_bounds__(XK_THREADS) void xt_keys_kernel(sa_actions A, const uint32_t* __restrict__ cells,
+                                                             int64_t n, int l, int w, XbShape S,
+                                                             uint32_t* __restrict__ keys,
+                                                             uint32_t* __restrict__ region_cnt,
+                                                             uint32_t* __restrict__ band_cnt,
+                                                             int32_t* __restrict__ err, XkRate RO) {
+  extern __shared__ uint32_t bh[];  // [NB]
+  __shared__ uint32_t cursor;
+  for (int b = threadIdx.x; b < S.NB; b += XK_THREADS) bh[b] = 0;
+  if (threadIdx.x == 0) cursor = 0;
+  __syncthreads();
+  const int64_t begin = (int64_t)blockIdx.x * XK_CHUNK;
+  const int64_t end = min(n, begin + XK_CHUNK);
+  uint32_t* out = keys + begin;
+  const sa_frame& F = A.frames[0];
+  const int lane = threadIdx.x & 63;
+  int32_t bad = 0;
+  constexpr int U = CELLS ? 8 : 4;  // actions per thread per pass, every load issued first
+  for (int64_t base = begin; base < end; base += (int64_t)U * XK_THREADS) {  // wave-uniform bound
+    XtAct act[U];
+    if (CELLS) {
+      uint32_t cv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t j = base + u * XK_THREADS + threadIdx.x;
+        cv[u] = cells[j < end ? j : end - 1];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        act[u] = decode_cell(cv[u]);
+        if (base + u * XK_THREADS + threadIdx.x >= end) act[u].cls = 0;
+      }
+    } else {
+      int tt[U], rr[U];
+      double sx[U], sy[U], ex[U], ey[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t j = base + u * XK_THREADS + threadIdx.x;
+        const int64_t jc = j < end ? j : end - 1;
+        tt[u] = j < end ? F.type_id[jc] : -1;
+        rr[u] = F.result_id[jc];
+        sx[u] = F.c0[jc];
+        sy[u] = F.c1[jc];
+        ex[u] = F.c2[jc];
+        ey[u] = F.c3[jc];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t j = base + u * XK_THREADS + threadIdx.x;
+        if (RO.codes && tt[u] >= 0) RO.codes[j] = rate_code(tt[u], rr[u], sx[u], sy[u], ex[u], ey[u], l, w);
+        if (RO.icodes && tt[u] >= 0)
+          RO.icodes[j] = rate_icode(tt[u], rr[u], sx[u], sy[u], ex[u], ey[u], RO.L, RO.W);
+        act[u] = act_from_row(tt[u], rr[u], sx[u], sy[u], ex[u], ey[u], l, w);
+      }
+    }
+    uint32_t key[U];
+    bool has[U];
+    uint64_t m[U];
+    uint32_t tot = 0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      has[u] = band_key(act[u], S.C, key[u], bad);
+      m[u] = __ballot(has[u]);
+      tot += (uint32_t)__popcll(m[u]);
+    }
+    uint32_t wbase = 0;
+    if (lane == 0 && tot) wbase = atomicAdd(&cursor, tot);
+    wbase = __shfl(wbase, 0);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (has[u]) {
+        const uint32_t pos = wbase + lane_rank(m[u]);
+        SA_DGUARD(pos < XK_CHUNK, pos, continue);
+        out[pos] = key[u];
+        atomicAdd(&bh[band_of(key[u], S.magic)], 1u);
+      }
+      wbase += (uint32_t)__popcll(m[u]);
+    }
+  }
+  if (bad) atomicOr(err, bad);
+  __syncthreads();
+  for (int b = threadIdx.x; b < S.NB; b += XK_THREADS)
+    if (bh[b]) atomicAdd(&band_cnt[b], bh[b]);
+  if (threadIdx.x == 0) region_cnt[blockIdx.x] = cursor;
+}
+
+// Exclusive scan of a[0, n) in place by one 1024-thread workgroup; returns the total (to every
+// thread).  ws: 17 words of LDS.
+__device__ uint32_t block_scan_1024(uint32_t* a, int n, uint32_t* ws) {
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int per = (n + 1023) / 1024;
+  const int lo = min(n, t * per), hi = min(n, lo + per);
+  uint32_t s = 0;
+  for (int i = lo; i < hi; ++i) s += a[i];
+  uint32_t inc = s;  // inclusive wave scan
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t v = __shfl_up(inc, d);
+    if (lane >= d) inc += v;
+  }
+  if (lane == 63) ws[wv] = inc;
+  __syncthreads();
+  if (t == 0) {
+    uint32_t run = 0;
+    for (int k = 0; k < 16; ++k) {
+      const uint32_t v = ws[k];
+      ws[k] = run;
+      run += v;
+    }
+    ws[16] = run;
+  }
+  __syncthreads();
+  uint32_t run = ws[wv] + inc - s;
+  for (int i = lo; i < hi; ++i) {
+    const uint32_t v = a[i];
+    a[i] = run;
+    run += v;
+  }
+  const uint32_t total = ws[16];
+  __syncthreads();
+  return total;
+}
+
+// K2: band_off[b] = keys of bands < b (int64, [NB + 1]); cursor[b] = band_off[b].
+__global__ __launch_bounds__(1024) void xt_band_scan_kernel(uint32_t* __restrict__ band_cnt, int NB,
+                                                            int64_t* __restrict__ band_off,
+                                                            uint32_t* __restrict__ cursor) {
+  __shared__ uint32_t ws[17];
+  const uint32_t total = block_scan_1024(band_cnt, NB, ws);
+  for (int b = threadIdx.x; b < NB; b += 1024) {
+    band_off[b] = band_cnt[b];
+    cursor[b] = band_cnt[b];
+  }
+  if (threadIdx.x == 0) band_off[NB] = total;
+}
+
+// K3: one workgroup per K1 region.  Its keys (<= XK_CHUNK, 32 per thread in registers) are ranked
+// within their band by LDS atomics, each band's run gets its place in the band's bucket by ONE
+// global atomic on the band cursor, the keys are sorted by band in LDS, and thread i writes the
+// sorted key i -- consecutive threads of a run write consecutive words.
+__global__ __launch_bounds__(XS_THREADS) void xt_keys_scatter_kernel(const uint32_t* __restrict__ keys,
+                                                                     const uint32_t* __restrict__ region_cnt,
+                                                                     XbShape S, uint32_t* __restrict__ cursor,
+                                                                     uint32_t* __restrict__ buckets) {
+  extern __shared__ uint32_t sm[];
+  uint32_t* bh = sm;              // [NB] keys per band, then the local run offsets
+  uint32_t* bb = sm + S.NB;       // [NB] the runs' places in the buckets
+  uint32_t* sorted = sm + 2 * S.NB;  // [XK_CHUNK]
+  __shared__ uint32_t ws[17];
+  const uint32_t cnt = region_cnt[blockIdx.x];
+  const uint32_t* in = keys + (int64_t)blockIdx.x * XK_CHUNK;
+  for (int b = threadIdx.x; b < S.NB; b += XS_THREADS) bh[b] = 0;
+  uint32_t k[XS_PER], rk[XS_PER];
+#pragma unroll
+  for (int u = 0; u < XS_PER; ++u) {
+    const uint32_t i = u * XS_THREADS + threadIdx.x;
+    k[u] = i < cnt ? in[i] : XB_NONE;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < XS_PER; ++u) {
+    rk[u] = 0;
+    if (k[u] != XB_NONE) {
+      const uint32_t b = band_of(k[u], S.magic);
+      SA_DGUARD(b < (uint32_t)S.NB, b, continue);
+      rk[u] = atomicAdd(&bh[b], 1u);
+    }
+  }
+  __syncthreads();
+  for (int b = threadIdx.x; b < S.NB; b += XS_THREADS) {
+    const uint32_t c = bh[b];
+    bb[b] = c ? atomicAdd(&cursor[b], c) : 0u;
+  }
+  __syncthreads();
+  block_scan_1024(bh, S.NB, ws);
+#pragma unroll
+  for (int u = 0; u < XS_PER; ++u)
+    if (k[u] != XB_NONE) {
+      const uint32_t b = band_of(k[u], S.magic);
+      SA_DGUARD(b < (uint32_t)S.NB, b, continue);
+      sorted[bh[b] + rk[u]] = k[u];
+    }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < cnt; i += XS_THREADS) {
+    const uint32_t key = sorted[i];
+    const uint32_t b = band_of(key, S.magic);
+    SA_DGUARD(b < (uint32_t)S.NB, b, continue);
+    buckets[bb[b] + (i - bh[b])] = key;
+  }
+}
+
+struct XbSets {
+  const uint32_t* keys[XB_MAX_SETS];
+  const int64_t* off[XB_MAX_SETS];
+  int n;
+};
+
+// K4: band b = start cells [b R, b R + R).  Bins h[i][slot] (i < R, slot < C + 3) as u32 in LDS,
+// filled by LDS atomics from every set's bucket of the band, then flushed: the transition rows
+// with coalesced 16-B stores (vec) or 4-B stores, the shot / goal / move counts of each cell
+// from slots C, C + 1, C + 2 and the row sum.  overwrite: the rows and counts are written, not
+// added to (a fresh accumulator: no read of the old rows).
+__global__ __launch_bounds__(XB_THREADS) void xt_band_count_kernel(XbSets sets, XbShape S,
+                                                                   unsigned long long* __restrict__ shot,
+                                                                   unsigned long long* __restrict__ goal,
+                                                                   unsigned long long* __restrict__ move,
+                                                                   int32_t* __restrict__ trans, int overwrite,
+                                                                   int vec) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t h[];  // [R][P]
+  __shared__ unsigned long long msum[XB_MAX_ROWS];
+  const int b = blockIdx.x, C = S.C, P = S.P;
+  const int r0 = b * S.R, nr = min(S.R, C - r0);
+  for (int e = 4 * threadIdx.x; e < nr * P; e += 4 * XB_THREADS) *reinterpret_cast<u32x4*>(h + e) = u32x4{0, 0, 0, 0};
+  if (threadIdx.x < XB_MAX_ROWS) msum[threadIdx.x] = 0;
+  __syncthreads();
+  for (int s = 0; s < sets.n; ++s) {
+    const uint32_t* kp = sets.keys[s];
+    const int64_t lo = sets.off[s][b], hi = sets.off[s][b + 1];
+    for (int64_t i = lo + threadIdx.x; i < hi; i += 4 * XB_THREADS) {
+      uint32_t v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t j = i + u * XB_THREADS;
+        v[u] = j < hi ? kp[j] : XB_NONE;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (v[u] != XB_NONE) {
+          const int row = (int)(v[u] >> 16) - r0, slot = (int)(v[u] & 0xFFFFu);
+          SA_DGUARD(row >= 0 && row < nr && slot < C + 3, v[u], continue);
+          atomicAdd(&h[row * P + slot], 1u);
+        }
+    }
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  for (int i = 0; i < nr; ++i) {
+    const uint32_t* hr = h + i * P;
+    int32_t* dst = trans + (int64_t)(r0 + i) * C;
+    unsigned long long ms = 0;
+    if (vec) {  // C % 4 == 0 and trans 16-byte aligned: every row starts 16-byte aligned
+      for (int c = 4 * threadIdx.x; c < C; c += 4 * XB_THREADS) {
+        const u32x4 v = *reinterpret_cast<const u32x4*>(hr + c);
+        ms += (unsigned long long)v[0] + v[1] + v[2] + v[3];
+        i32x4 o = {(int32_t)v[0], (int32_t)v[1], (int32_t)v[2], (int32_t)v[3]};
+        if (!overwrite) {
+          const i32x4 old = *reinterpret_cast<const i32x4*>(dst + c);
+          o += old;
+        }
+        *reinterpret_cast<i32x4*>(dst + c) = o;
+      }
+    } else {
+      for (int c = threadIdx.x; c < C; c += XB_THREADS) {
+        const uint32_t v = hr[c];
+        ms += v;
+        dst[c] = overwrite ? (int32_t)v : dst[c] + (int32_t)v;
+      }
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) ms += __shfl_xor(ms, d);
+    if (lane == 0 && ms) atomicAdd(&msum[i], ms);
+  }
+  __syncthreads();
+  if (threadIdx.x < nr) {
+    const int i = threadIdx.x, r = r0 + i;
+    const uint32_t* hr = h + i * P;
+    const unsigned long long sh = (unsigned long long)hr[C] + hr[C + 1], gl = hr[C + 1];
+    const unsigned long long mv = msum[i] + hr[C + 2];
+    if (overwrite) {
+      shot[r] = sh;
+      goal[r] = gl;
+      move[r] = mv;
+    } else {
+      shot[r] += sh;
+      goal[r] += gl;
+      move[r] += mv;
+    }
+  }
+}
+
+// ============================================================================ compact iteration
+constexpr int XE_S = 32;                     // rows per slice = chain lanes
+constexpr int XE_P = 8;                      // product waves
+constexpr int XE_KC = 64;                    // entries per row per chunk
+constexpr int XE_CT = 64;                    // counts whose quotient is tabulated
+constexpr int XE_THREADS = (XE_P + 1) * 64;  // + the chain wave
+constexpr int XE_XMAX = 10240;               // x (C doubles) staged in LDS
+constexpr int XE_BUILD_THREADS = 1024;
+constexpr uint32_t XE_CNT_ESC = 0xFFFFu;     // count >= 65535: read from the dense row
+static_assert(XE_KC * XE_S == 4 * XE_P * 64, "one 16-B entry quad per product lane per chunk");
+static_assert(XE_THREADS <= 1024 && XE_S <= 64 && (XE_S & 3) == 0, "xt_iter_ell_kernel shape");
+static_assert((size_t)XE_XMAX * 8 + (XE_CT + 2 * XE_KC + 1) * XE_S * 8 <= 160 * 1024, "xt_iter_ell_kernel LDS");
+
+// Compact form of rows [0, nrows) of a count block (row i at cnt_rows + i*C): slice s = rows
+// [32 s, 32 s + 32) at ell + s * 32 * C (room for a dense slice); entry k of row i (the row's
+// k-th non-zero count in column order, column | min(count, 0xFFFF) << 16) at k * 32 + i; every
+// row padded with 0 entries to slice_len[s] = the slice's longest row.
+__global__ __launch_bounds__(XE_BUILD_THREADS) void xt_ell_build_kernel(const int32_t* __restrict__ cnt_rows, int C,
+                                                                        int nrows, uint32_t* __restrict__ ell,
+                                                                        int32_t* __restrict__ slice_len) {
+  __shared__ int lens[XE_S];
+  __shared__ int mx;
+  const int s = blockIdx.x, row0 = s * XE_S;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  constexpr int NW = XE_BUILD_THREADS / 64;
+  uint32_t* E = ell + (int64_t)s * XE_S * C;
+  for (int i = wv; i < XE_S; i += NW) {
+    const int r = row0 + i;
+    int base = 0;
+    if (r < nrows) {
+      const int32_t* row = cnt_rows + (int64_t)r * C;
+      for (int c0 = 0; c0 < C; c0 += 64 * 8) {
+        int32_t v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int c = c0 + 64 * u + lane;
+          v[u] = c < C ? row[c] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const uint64_t m = __ballot(v[u] != 0);
+          if (v[u] != 0) {
+            const uint32_t cnt = (uint32_t)v[u] < XE_CNT_ESC ? (uint32_t)v[u] : XE_CNT_ESC;
+            E[(int64_t)(base + (int)lane_rank(m)) * XE_S + i] = (uint32_t)(c0 + 64 * u + lane) | (cnt << 16);
+          }
+          base += (int)__popcll(m);
+        }
+      }
+    }
+    if (lane == 0) lens[i] = base;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int m = 0;
+    for (int i = 0; i < XE_S; ++i) m = max(m, lens[i]);
+    mx = m;
+    slice_len[s] = m;
+  }
+  __syncthreads();
+  for (int i = wv; i < XE_S; i += NW)
+    for (int k = lens[i] + lane; k < mx; k += 64) E[(int64_t)k * XE_S + i] = 0u;
+}
+
+// One iteration of rows [rb, rb + nrows) from their compact form (xt_ell_build_kernel of the same
+// rows; cnt_rows: the dense rows, read only for counts >= 65535): xo[i] = gs + pmove * sum over
+// the row's non-zero columns c, in column order, of (cnt / move[r]) * x[c] -- xt_iter_kernel's
+// operations (sa_xt.hip), without its per-chunk compaction of the dense rows.  One workgroup per
+// slice; per chunk of 64 entries per row the product waves write the 64 x 32 products to LDS and
+// the chain wave (lane = row) adds them in order, one barrier per chunk, two buffers.
+__global__ __launch_bounds__(XE_THREADS) void xt_iter_ell_kernel(const uint32_t* __restrict__ ell,
+                                                                 const int32_t* __restrict__ slice_len,
+                                                                 const int32_t* __restrict__ cnt_rows,
+                                                                 const unsigned long long* __restrict__ move,
+                                                                 const double* __restrict__ gs,
+                                                                 const double* __restrict__ pmove, int C, int rb,
+                                                                 int nrows, double eps, const double* __restrict__ x,
+                                                                 double* __restrict__ xo, const int32_t* flag_prev,
+                                                                 int32_t* __restrict__ flag_out) {
+  if (flag_prev && __hip_atomic_load(flag_prev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
+  extern __shared__ __attribute__((aligned(16))) double xs[];  // [C]
+  __shared__ double tq[XE_CT * XE_S];                          // tq[q * S + i] = q / move[row i]
+  __shared__ double prod[2][XE_KC * XE_S];
+  __shared__ double mvs[XE_S];
+  const int s = blockIdx.x, row0 = s * XE_S, nr = min(XE_S, nrows - row0);
+  const int len = slice_len[s];
+  for (int c = threadIdx.x; c < C; c += XE_THREADS) xs[c] = x[c];
+  for (int e = threadIdx.x; e < XE_CT * XE_S; e += XE_THREADS) {
+    const int q = e / XE_S, i = e % XE_S;
+    const double mv = i < nr ? (double)move[rb + row0 + i] : 1.0;
+    tq[e] = q == 0 ? 0.0 : (double)q / mv;  // a count of 0 is a zero term (T = 0)
+    if (q == 0) mvs[i] = mv;
+  }
+  __syncthreads();
+  const uint32_t* E = ell + (int64_t)s * XE_S * C;
+  const int nch = (len + XE_KC - 1) / XE_KC;
+  const int wv = threadIdx.x >> 6;
+  if (wv < XE_P) {  // ---- product waves: quad t = entries (k = t / 8, rows 4 (t % 8) .. + 3) of a chunk
+    const int t = threadIdx.x, kk = t >> 3, i0 = (t & 7) * 4;
+    auto ld = [&](int j) -> u32x4 {
+      const int k = j * XE_KC + kk;
+      return k < len ? *reinterpret_cast<const u32x4*>(E + (int64_t)k * XE_S + i0) : u32x4{0, 0, 0, 0};
+    };
+    u32x4 qa = ld(0), qb = ld(1);
+    asm volatile("" ::: "memory");
+    for (int j = 0; j < nch; ++j) {
+      const u32x4 q = qa;
+      qa = qb;
+      qb = ld(j + 2);  // two chunks ahead (past the end: zero, no load)
+      asm volatile("" ::: "memory");
+      double* pr = prod[j & 1] + kk * XE_S + i0;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint32_t e = q[u], cnt = e >> 16, col = e & 0xFFFFu;
+        SA_DGUARD((int)col < C, col, continue);
+        double tv;
+        if (cnt < (uint32_t)XE_CT) {
+          tv = tq[cnt * XE_S + i0 + u];
+        } else {
+          const int32_t c32 = cnt == XE_CNT_ESC ? cnt_rows[(int64_t)(row0 + i0 + u) * C + col] : (int32_t)cnt;
+          tv = (double)c32 / mvs[i0 + u];
+        }
+        pr[u] = tv * xs[col];
+      }
+      __syncthreads();
+    }
+  } else {  // ---- chain wave: lane i adds row i's products strictly left to right
+    const int i = threadIdx.x & (XE_S - 1);
+    double acc = 0.0;
+    for (int j = 0; j < nch; ++j) {
+      __syncthreads();
+      const double* pr = prod[j & 1] + i;
+      double v[XE_KC];
+#pragma unroll
+      for (int k = 0; k < XE_KC; ++k) v[k] = pr[k * XE_S];
+#pragma unroll
+      for (int k = 0; k < XE_KC; ++k) acc = acc + v[k];
+    }
+    const int lane = threadIdx.x & 63;
+    if (lane < nr) {
+      const int rr = rb + row0 + lane;
+      const double mv = pmove[rr] * acc;
+      const double nx = gs[rr] + mv;
+      xo[row0 + lane] = nx;
+      if ((nx - x[rr]) > eps) atomicOr(flag_out, 1);  // np.any(diff > eps): NaN is False
+    }
+  }
+}
+
+}  // namespace sa
+
+// ================================== C ABI =================================================
+using namespace sa;
+
+namespace sa {
+// The band shape of a grid, false when the band path cannot hold it (then the caller counts with
+// the global-atomic pass).  R = C / 256 (>= 256 bands to fill the chip), at most what 160 KB of
+// LDS holds and at most 8.
+static bool xt_band_shape(int C, XbShape* s);
+bool xt_band_ok(int C) {
+  XbShape s;
+  return xt_band_shape(C, &s);
+}
+
+static bool xt_band_shape(int C, XbShape* s) {
+  if (C < 1 || C + 3 > 65536) return false;
+  const int P = (C + 3 + 3) & ~3;
+  int rmax = (int)(XB_LDS_MAX / ((size_t)P * 4));
+  if (rmax > XB_MAX_ROWS) rmax = XB_MAX_ROWS;
+  if (rmax < 1) return false;
+  int r = C / 256;
+  if (r < 1) r = 1;
+  if (r > rmax) r = rmax;
+  const int nb = (C + r - 1) / r;
+  if (nb > XB_NB_MAX) return false;
+  s->C = C;
+  s->R = r;
+  s->NB = nb;
+  s->P = P;
+  s->magic = ((1ull << 32) + (uint64_t)r - 1) / (uint64_t)r;
+  return true;
+}
+
+// K1 -> K2 -> K3 of one batch: its keys sorted into buckets[] by band, band_off[NB + 1].
+static int bucket_batch(const sa_actions& A, const uint32_t* cells, int64_t n, int l, int w, const XbShape& S,
+                        uint32_t* buckets, int64_t* band_off, int32_t* err, const XkRate& RO, hipStream_t st) {
+  const int64_t regions = (n + XK_CHUNK - 1) / XK_CHUNK;
+  // scratch: keys [regions * XK_CHUNK] | region_cnt [regions] | band_cnt [NB] | cursor [NB]
+  const size_t kb = (size_t)regions * XK_CHUNK * 4;
+  const size_t bytes = kb + ((size_t)regions + 2 * (size_t)S.NB) * 4 + 256;
+  Scratch sc;
+  int rc = scratch_acquire(bytes, st, &sc);
+  if (rc) return rc;
+  uint32_t* keys = static_cast<uint32_t*>(sc.ptr);
+  uint32_t* region_cnt = keys + (size_t)regions * XK_CHUNK;
+  uint32_t* band_cnt = region_cnt + regions;
+  uint32_t* cursor = band_cnt + S.NB;
+  rc = check_hip(hipMemsetAsync(band_cnt, 0, (size_t)S.NB * 4, st), "memset band counts");
+  if (!rc) {
+    sa_actions none;
+    memset(&none, 0, sizeof(none));
+    if (cells)
+      hipLaunchKernelGGL((xt_keys_kernel<true>), dim3((unsigned)regions), dim3(XK_THREADS), (size_t)S.NB * 4, st, none,
+                         cells, n, l, w, S, keys, region_cnt, band_cnt, err, XkRate{nullptr, nullptr, 0, 0});
+    else
+      hipLaunchKernelGGL((xt_keys_kernel<false>), dim3((unsigned)regions), dim3(XK_THREADS), (size_t)S.NB * 4, st, A,
+                         nullptr, n, l, w, S, keys, region_cnt, band_cnt, err, RO);
+    rc = check_launch("xt_keys_kernel");
+  }
+  if (!rc) {
+    hipLaunchKernelGGL(xt_band_scan_kernel, dim3(1), dim3(1024), 0, st, band_cnt, S.NB, band_off, cursor);
+    rc = check_launch("xt_band_scan_kernel");
+  }
+  if (!rc) {
+    const size_t lds = ((size_t)2 * S.NB + XK_CHUNK) * 4;
+    hipLaunchKernelGGL(xt_keys_scatter_kernel, dim3((unsigned)regions), dim3(XS_THREADS), lds, st, keys, region_cnt,
+                       S, cursor, buckets);
+    rc = check_launch("xt_keys_scatter_kernel");
+  }
+  scratch_release(sc, st);
+  return rc;
+}
+
+static int count_from_buckets(int nsets, const uint32_t* const* buckets, const int64_t* const* band_off,
+                              const XbShape& S, int64_t* shot, int64_t* goal, int64_t* move, int32_t* trans,
+                              int overwrite, hipStream_t st) {
+  const int vec = (S.C % 4 == 0) && aligned16(trans);
+  const size_t lds = (size_t)S.R * S.P * 4;
+  for (int s0 = 0; s0 < nsets || (s0 == 0 && nsets == 0); s0 += XB_MAX_SETS) {
+    XbSets sets;
+    memset(&sets, 0, sizeof(sets));
+    sets.n = nsets - s0 < XB_MAX_SETS ? nsets - s0 : XB_MAX_SETS;
+    for (int k = 0; k < sets.n; ++k) {
+      sets.keys[k] = buckets[s0 + k];
+      sets.off[k] = band_off[s0 + k];
+    }
+    // later launches add to what the first one wrote
+    hipLaunchKernelGGL(xt_band_count_kernel, dim3((unsigned)S.NB), dim3(XB_THREADS), lds, st, sets, S,
+                       reinterpret_cast<unsigned long long*>(shot), reinterpret_cast<unsigned long long*>(goal),
+                       reinterpret_cast<unsigned long long*>(move), trans, (overwrite && s0 == 0) ? 1 : 0, vec);
+    int rc = check_launch("xt_band_count_kernel");
+    if (rc) return rc;
+    if (nsets == 0) break;
+  }
+  return SA_OK;
+}
+
+// The whole band-owned count of one batch (sa_xt_count / sa_xt_count_codes / sa_xt_count_cells
+// for grids the band path holds): buckets in scratch, added into the caller's counts.
+int xt_count_bands(const sa_actions& A, const uint32_t* cells, int64_t n, int l, int w, int64_t* shot,
+                   int64_t* goal, int64_t* move, int32_t* trans, int32_t* err, uint32_t* codes, hipStream_t st) {
+  XbShape S;
+  if (!xt_band_shape(l * w, &S)) return fail(SA_EINVAL, "grid outside the band-owned count");
+  Scratch sc;  // buckets [n] | band_off [NB + 1]
+  const size_t bb = ((size_t)n * 4 + 255) & ~(size_t)255;
+  int rc = scratch_acquire(bb + ((size_t)S.NB + 1) * 8, st, &sc);
+  if (rc) return rc;
+  uint32_t* buckets = static_cast<uint32_t*>(sc.ptr);
+  int64_t* band_off = reinterpret_cast<int64_t*>(static_cast<char*>(sc.ptr) + bb);
+  rc = bucket_batch(A, cells, n, l, w, S, buckets, band_off, err, XkRate{codes, nullptr, 0, 0}, st);
+  if (!rc) {
+    const uint32_t* bk[1] = {buckets};
+    const int64_t* bo[1] = {band_off};
+    rc = count_from_buckets(1, bk, bo, S, shot, goal, move, trans, 0, st);
+  }
+  scratch_release(sc, st);
+  return rc;
+}
+
+// Compact form + iteration used by sa_xt_solve for C > SA_XT_SOLVE_MAX_C.
+bool xt_compact_ok(int C) { return C >= 1 && C <= XE_XMAX; }
+size_t xt_compact_bytes(int C, int nrows) {
+  const size_t ns = (size_t)(nrows + XE_S - 1) / XE_S;
+  return ns * XE_S * (size_t)C * 4;
+}
+int xt_compact_build(const int32_t* cnt_rows, int C, int nrows, uint32_t* ell, int32_t* slice_len, hipStream_t st) {
+  const int ns = (nrows + XE_S - 1) / XE_S;
+  if (ns == 0) return SA_OK;
+  hipLaunchKernelGGL(xt_ell_build_kernel, dim3((unsigned)ns), dim3(XE_BUILD_THREADS), 0, st, cnt_rows, C, nrows, ell,
+                     slice_len);
+  return check_launch("xt_ell_build_kernel");
+}
+int xt_compact_iterate(const uint32_t* ell, const int32_t* slice_len, const int32_t* cnt_rows, const int64_t* move,
+                       const double* gs, const double* pmove, int C, int rb, int nrows, const double* x, double eps,
+                       double* xo, const int32_t* flag_prev, int32_t* flag_out, hipStream_t st) {
+  const int ns = (nrows + XE_S - 1) / XE_S;
+  if (ns == 0) return SA_OK;
+  hipLaunchKernelGGL(xt_iter_ell_kernel, dim3((unsigned)ns), dim3(XE_THREADS), (size_t)C * 8, st, ell, slice_len,
+                     cnt_rows, reinterpret_cast<const unsigned long long*>(move), gs, pmove, C, rb, nrows, eps, x, xo,
+                     flag_prev, flag_out);
+  return check_launch("xt_iter_ell_kernel");
+}
+}  // namespace sa
+
+extern "C" int sa_xt_band_shape(int32_t l, int32_t w, int32_t* rows_per_band, int32_t* n_bands) {
+  if (l < 1 || w < 1 || (int64_t)l * w > 46340) return fail(SA_EINVAL, "bad l or w");
+  XbShape S;
+  if (!xt_band_shape(l * w, &S)) return fail(SA_EINVAL, "the band-owned count does not hold %d cells", l * w);
+  if (rows_per_band) *rows_per_band = S.R;
+  if (n_bands) *n_bands = S.NB;
+  return SA_OK;
+}
+
+extern "C" int sa_xt_count_bucket(const sa_actions* a, const uint32_t* cells, int64_t n, int32_t l, int32_t w,
+                                  uint32_t* buckets, int64_t* band_off, int32_t* err_flags, uint32_t* codes,
+                                  uint64_t* interp_codes, int32_t L, int32_t W, void* stream) {
+  if (l < 1 || w < 1 || (int64_t)l * w > 46340) return fail(SA_EINVAL, "bad l or w");
+  XbShape S;
+  if (!xt_band_shape(l * w, &S)) return fail(SA_EINVAL, "the band-owned count does not hold %d cells", l * w);
+  if (!band_off || !err_flags) return fail(SA_EINVAL, "null output");
+  if (cells) {
+    if (n < 0 || (int64_t)l * w > SA_XT_CELLS_MAX_C) return fail(SA_EINVAL, "cell codes need l * w <= %d", SA_XT_CELLS_MAX_C);
+    if (codes || interp_codes) return fail(SA_EINVAL, "rate codes come from the coordinate pass");
+  } else {
+    if (!a || a->n < 0 || a->atomic) return fail(SA_EINVAL, "bad sa_actions (SPADL actions required)");
+    n = a->n;
+    const sa_frame& F = a->frames[0];
+    if (n > 0 && (!F.type_id || !F.result_id || !F.c0 || !F.c1 || !F.c2 || !F.c3))
+      return fail(SA_EINVAL, "null input column");
+    if (codes && !aligned16(codes)) return fail(SA_EINVAL, "codes must be 16-byte aligned");
+    if (codes && (int64_t)l * w > 65535) return fail(SA_EINVAL, "rate codes need l * w <= 65535");
+    if (interp_codes && (!aligned16(interp_codes) || L < 1 || W < 1 || (int64_t)L * W > INT32_MAX))
+      return fail(SA_EINVAL, "interp_codes: 16-byte aligned, 1 <= L * W < 2^31");
+  }
+  if (n > INT32_MAX) return fail(SA_EINVAL, "at most 2^31 - 1 actions per batch");
+  if (n > 0 && !buckets) return fail(SA_EINVAL, "null buckets");
+  hipStream_t st = (hipStream_t)stream;
+  if (n == 0)
+    return check_hip(hipMemsetAsync(band_off, 0, sizeof(int64_t) * ((size_t)S.NB + 1), st), "memset band offsets");
+  sa_actions none;
+  memset(&none, 0, sizeof(none));
+  return bucket_batch(cells ? none : *a, cells, n, l, w, S, buckets, band_off, err_flags,
+                      XkRate{codes, interp_codes, L, W}, st);
+}
+
+extern "C" int sa_xt_count_from_buckets(int32_t nsets, const uint32_t* const* buckets, const int64_t* const* band_off,
+                                        int32_t l, int32_t w, int64_t* shot, int64_t* goal, int64_t* move,
+                                        int32_t* trans, int32_t flags, void* stream) {
+  if (l < 1 || w < 1 || (int64_t)l * w > 46340) return fail(SA_EINVAL, "bad l or w");
+  XbShape S;
+  if (!xt_band_shape(l * w, &S)) return fail(SA_EINVAL, "the band-owned count does not hold %d cells", l * w);
+  if (nsets < 0 || (nsets > 0 && (!buckets || !band_off))) return fail(SA_EINVAL, "bad bucket sets");
+  for (int k = 0; k < nsets; ++k)
+    if (!band_off[k]) return fail(SA_EINVAL, "null band offsets");
+  if (!shot || !goal || !move || !trans) return fail(SA_EINVAL, "null count buffer");
+  if (flags & ~SA_XT_COUNT_OVERWRITE) return fail(SA_EINVAL, "unknown flags");
+  if (nsets == 0 && !(flags & SA_XT_COUNT_OVERWRITE)) return SA_OK;
+  return count_from_buckets(nsets, buckets, band_off, S, shot, goal, move, trans,
+                            (flags & SA_XT_COUNT_OVERWRITE) != 0, (hipStream_t)stream);
+}
+
+extern "C" int sa_xt_compact_rows(const int32_t* cnt_rows, int32_t C, int32_t nrows, uint32_t* ell,
+                                  int32_t* slice_len, void* stream) {
+  if (!xt_compact_ok(C) || nrows < 0) return fail(SA_EINVAL, "the compact form takes 1 <= C <= %d", XE_XMAX);
+  if (nrows > 0 && (!cnt_rows || !ell || !slice_len)) return fail(SA_EINVAL, "null pointer");
+  if (nrows > 0 && !aligned16(ell)) return fail(SA_EINVAL, "ell must be 16-byte aligned");
+  return xt_compact_build(cnt_rows, C, nrows, ell, slice_len, (hipStream_t)stream);
+}
+
+extern "C" int sa_xt_iterate_compact(const uint32_t* ell, const int32_t* slice_len, const int32_t* cnt_rows,
+                                     const int64_t* move, const double* gs, const double* pmove, int32_t C, int32_t r0,
+                                     int32_t nrows, const double* x, double eps, double* x_next_rows,
+                                     const int32_t* flag_prev, int32_t* flag_out, void* stream) {
+  if (!xt_compact_ok(C)) return fail(SA_EINVAL, "the compact form takes 1 <= C <= %d", XE_XMAX);
+  if (r0 < 0 || nrows < 0 || r0 + nrows > C) return fail(SA_EINVAL, "row range outside [0, C)");
+  if (!move || !gs || !pmove || !x || !flag_out ||
+      (nrows > 0 && (!ell || !slice_len || !cnt_rows || !x_next_rows)))
+    return fail(SA_EINVAL, "null xt iteration pointer");
+  if (nrows > 0 && !aligned16(ell)) return fail(SA_EINVAL, "ell must be 16-byte aligned");
+  return xt_compact_iterate(ell, slice_len, cnt_rows, move, gs, pmove, C, r0, nrows, x, eps, x_next_rows, flag_prev,
+                            flag_out, (hipStream_t)stream);
+}
+
+extern "C" int64_t sa_xt_compact_bytes(int32_t C, int32_t nrows) {
+  if (!xt_compact_ok(C) || nrows < 0) return -1;
+  return (int64_t)xt_compact_bytes(C, nrows);
+}

@@ -428,6 +428,114 @@ def xt_count(batch: ActionBatch, l: int, w: int, acc: Optional[XTCounts] = None,
     return acc
 
 
+def xt_band_shape(l: int, w: int) -> Optional[Tuple[int, int]]:
+    """(start cells per band, bands) of the band-owned count of an (l, w) grid, or None when
+    the grid takes the LDS-histogram (small) or global-atomic (very large) count instead."""
+    C = l * w
+    if C <= 202 or C > 46340:  # the XC_WIDE / XC_SMALL LDS passes hold these whole
+        return None
+    r, nb = ctypes.c_int32(0), ctypes.c_int32(0)
+    if _native.lib().sa_xt_band_shape(int(l), int(w), ctypes.byref(r), ctypes.byref(nb)) != 0:
+        return None
+    return r.value, nb.value
+
+
+@dataclass
+class XTBuckets:
+    """One batch's counted actions sorted by start-cell band (``sa_xt_count_bucket``)."""
+    keys: torch.Tensor      # u32 (as int32) [n]
+    band_off: torch.Tensor  # int64 [n_bands + 1]
+
+
+def xt_bucket(batch: Optional[ActionBatch], l: int, w: int, err: torch.Tensor,
+              cells: Optional[torch.Tensor] = None, n: Optional[int] = None,
+              codes: Optional[torch.Tensor] = None,
+              interp_codes: Optional[torch.Tensor] = None, L: int = 1050,
+              W: int = 680) -> XTBuckets:
+    """The per-batch half of the band-owned count: every counted action of ``batch`` (or of
+    ``n`` cell codes) as a 4-B key, sorted by start-cell band; error bytes into ``err``.
+    ``interp_codes`` (int64 [>= n], :func:`xt_interp_codes_buffer`): each action's operand of a
+    later :func:`xt_rate_interp_codes` of the same actions on the L x W node grid."""
+    if interp_codes is not None and (interp_codes.dtype != torch.int64 or
+                                     interp_codes.numel() < batch.n):
+        raise ValueError('interp_codes must be an int64 tensor of at least n elements')
+    shape = xt_band_shape(l, w)
+    if shape is None:
+        raise ValueError(f'the band-owned count does not take a {l} x {w} grid')
+    dev = err.device
+    n = batch.n if cells is None else int(n)
+    keys = torch.empty(max(n, 16), dtype=torch.int32, device=dev)
+    off = torch.empty(shape[1] + 1, dtype=torch.int64, device=dev)
+    s = batch.struct() if cells is None else None
+    if codes is not None and (codes.dtype != torch.int32 or codes.numel() < n):
+        raise ValueError('codes must be an int32 tensor of at least n elements')
+    _native.check(_native.lib().sa_xt_count_bucket(
+        ctypes.byref(s) if s is not None else None, _ptr(cells), int(n), int(l), int(w), _ptr(keys),
+        _ptr(off), _ptr(err), _ptr(codes), _ptr(interp_codes), int(L), int(W), stream_handle()))
+    return XTBuckets(keys, off)
+
+
+def xt_interp_codes_buffer(n: int, dev) -> torch.Tensor:
+    """u64 interpolated-rate operands (stored as int64) for n actions."""
+    return torch.empty(max(_ld(n), 16), dtype=torch.int64, device=dev)
+
+
+def xt_rate_interp_codes(icodes: torch.Tensor, n: int, xT: torch.Tensor, l: int, w: int,
+                         L: int = 1050, W: int = 680, axes: Optional[torch.Tensor] = None,
+                         out: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """:func:`xt_rate_interp` of the actions whose bucket pass wrote ``icodes``: the same
+    values, NaN pattern and error bit, reading 8 B per action."""
+    dev = icodes.device
+    axes = xt_interp_axes(l, w, dev, L, W) if axes is None else axes
+    if axes.numel() != l + w + L + W:
+        raise ValueError('axes must hold l + w + L + W node positions')
+    out = torch.empty(max(_ld(n), 16), dtype=torch.float64, device=dev) if out is None else out
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    o = l + w
+    _native.check(_native.lib().sa_xt_rate_interp_codes(
+        _ptr(icodes), int(n), _ptr(xT.contiguous()), _ptr(axes[:l]), _ptr(axes[l:o]), l, w,
+        _ptr(axes[o:o + L]), L, _ptr(axes[o + L:]), W, _ptr(out), _ptr(err), stream_handle()))
+    return out[:n], err
+
+
+def xt_count_buckets(parts: Sequence[XTBuckets], l: int, w: int, acc: XTCounts,
+                     overwrite: bool = False) -> XTCounts:
+    """The once-per-fit half of the band-owned count: every batch's buckets into ``acc`` (added;
+    ``overwrite``: written, the rows' old values never read)."""
+    k = len(parts)
+    keys = (ctypes.c_void_p * max(k, 1))(*[p.keys.data_ptr() for p in parts])
+    offs = (ctypes.c_void_p * max(k, 1))(*[p.band_off.data_ptr() for p in parts])
+    _native.check(_native.lib().sa_xt_count_from_buckets(
+        k, keys, offs, int(l), int(w), _ptr(acc.shot), _ptr(acc.goal), _ptr(acc.move),
+        _ptr(acc.trans), _native.SA_XT_COUNT_OVERWRITE if overwrite else 0, stream_handle()))
+    return acc
+
+
+def xt_count_many(batches: Sequence[ActionBatch], l: int, w: int,
+                  acc: Optional[XTCounts] = None, overwrite: Optional[bool] = None,
+                  interp_codes: Optional[Sequence[torch.Tensor]] = None) -> XTCounts:
+    """The count pass of ONE fit over several device batches (e.g. cfg5's 1e8 actions in
+    batches of <= 10k games): equal to :func:`xt_count` of every batch into one accumulator.
+    Band-owned grids bucket each batch and write the C x C table once. ``overwrite`` (default:
+    ``acc`` is None, a fresh accumulator): the counts are written, not added to the old ones
+    (``acc``'s error flags still accumulate). ``interp_codes``: one :func:`xt_interp_codes_buffer`
+    per batch (band-owned grids only), filled for a later :func:`xt_rate_interp_codes`."""
+    if xt_band_shape(l, w) is None or not batches:
+        if interp_codes is not None:
+            raise ValueError('interp_codes come from the band-owned count')
+        if overwrite and acc is not None:
+            acc.zero_()
+        for b in batches:
+            acc = xt_count(b, l, w, acc)
+        return acc if acc is not None else xt_zero_counts(l, w, torch.device('cuda'))
+    if overwrite is None:
+        overwrite = acc is None
+    acc = acc or xt_zero_counts(l, w, batches[0].device)
+    ic = list(interp_codes) if interp_codes is not None else [None] * len(batches)
+    parts = [xt_bucket(b, l, w, acc.err, interp_codes=c) for b, c in zip(batches, ic)]
+    return xt_count_buckets(parts, l, w, acc, overwrite=overwrite)
+
+
 def xt_rate_codes_buffer(n: int, dev) -> torch.Tensor:
     """u32 rate operands (stored as int32) for n actions."""
     return torch.empty(max(_ld(n), 16), dtype=torch.int32, device=dev)

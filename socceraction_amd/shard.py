@@ -38,7 +38,15 @@ def allreduce_xt_counts(acc, group=None) -> None:
     §8(e)): the int64 counts' high words stay 0 and their low words cannot carry; the error
     flags are one byte each (``ops.XT_ERR_*``), so up to 255 ranks' flags add without
     overlapping.  No staging copy, no ``torch.cat``."""
+    _check_world(group)
     _all_reduce(acc.buf.view(torch.int32), group=group)
+
+
+def _check_world(group) -> None:
+    """The counts' int32-word sum keeps the error bytes apart for at most 255 ranks."""
+    import torch.distributed as dist
+    if dist.get_world_size(group) > 255:
+        raise ValueError('the xT count all-reduce sums one error byte per flag: at most 255 ranks')
 
 
 # ----------------------------------------------------------------------------- collectives
@@ -90,9 +98,11 @@ def xt_solve_sharded(acc, eps: float = 1e-5, max_iter: int = 1000, group=None, b
        head of the count allocation, summed as int32 words like ``allreduce_xt_counts``);
     2. reduce-scatter of the C x C transition counts by row blocks: rank r keeps the summed
        count rows [r*B, (r+1)*B), B = ceil(C / world) (half the traffic of an all-reduce);
-    3. per iteration, each rank updates its B rows (``sa_xt_iterate_rows``, the reference's
-       summation order, so every value is bit-identical to the single-GPU solve) and one
-       all-gather of the B-row slices rebuilds the full x on every rank;
+    3. per iteration, each rank updates its B rows (``sa_xt_iterate_compact`` over the compact
+       form of its rows built once, ``sa_xt_iterate_rows`` above 10240 cells; the reference's
+       summation order, so every value is bit-identical to the single-GPU solve) into one
+       persistent B-row buffer, and one all-gather of those buffers rebuilds the full x on
+       every rank;
     4. convergence flags are combined (max) every ``batch`` iterations; iterations past the
        first converged one are computed and discarded.
 
@@ -105,6 +115,7 @@ def xt_solve_sharded(acc, eps: float = 1e-5, max_iter: int = 1000, group=None, b
 
     from . import _native
     from .batch import stream_handle
+    _check_world(group)
     W = dist.get_world_size(group)
     r = dist.get_rank(group)
     C = acc.C
@@ -126,16 +137,31 @@ def xt_solve_sharded(acc, eps: float = 1e-5, max_iter: int = 1000, group=None, b
     flags = torch.zeros(max_iter + 1, dtype=torch.int32, device=dev)
     r0 = r * B
     nrows = max(0, min(B, C - r0))
+    mine = torch.zeros(B, dtype=torch.float64, device=dev)  # this rank's rows, all-gathered
+    # the compact form of this rank's count rows, built once (sa_xt_compact_rows)
+    compact = C <= _native.SA_XT_COMPACT_MAX_C
+    if compact:
+        ell = torch.empty(max(int(lib.sa_xt_compact_bytes(C, nrows)) // 4, 4), dtype=torch.int32,
+                          device=dev)
+        slen = torch.empty(max(-(-nrows // 32), 1), dtype=torch.int32, device=dev)
+        _native.check(lib.sa_xt_compact_rows(ptr(rows), C, nrows, ptr(ell), ptr(slen),
+                                             stream_handle()))
     iters = -1
     it0 = 0
     while it0 < max_iter and iters < 0:
         it1 = min(it0 + batch, max_iter)
         for it in range(it0, it1):
-            _native.check(lib.sa_xt_iterate_rows(
-                ptr(rows), ptr(move), ptr(gp[0]), ptr(gp[1]), C, min(r0, C), nrows,
-                ptr(heat[it]), float(eps), ptr(heat[it + 1][r0:]), None, ptr(flags[it:]),
-                stream_handle()))
-            _all_gather(heat[it + 1], heat[it + 1][r0:r0 + B].clone(), group=group)
+            if compact:
+                _native.check(lib.sa_xt_iterate_compact(
+                    ptr(ell), ptr(slen), ptr(rows), ptr(move), ptr(gp[0]), ptr(gp[1]), C,
+                    min(r0, C), nrows, ptr(heat[it]), float(eps), ptr(mine), None,
+                    ptr(flags[it:]), stream_handle()))
+            else:
+                _native.check(lib.sa_xt_iterate_rows(
+                    ptr(rows), ptr(move), ptr(gp[0]), ptr(gp[1]), C, min(r0, C), nrows,
+                    ptr(heat[it]), float(eps), ptr(mine), None, ptr(flags[it:]),
+                    stream_handle()))
+            _all_gather(heat[it + 1], mine, group=group)
         f = flags[it0:it1]
         _all_reduce(f, dist.ReduceOp.MAX, group=group)
         hf = f.cpu().numpy()

@@ -38,8 +38,9 @@ print('ok')
 
 
 def _run(args, timeout=600):
-    env = dict(os.environ, SOCCERACTION_AMD_DEBUG='1', PYTHONPATH=ROOT + os.pathsep +
-               os.path.join(ROOT, 'tests'))
+    # prepend: whatever PYTHONPATH the harness set (e.g. its library-mapping hook) stays
+    path = [ROOT, os.path.join(ROOT, 'tests')] + [p for p in os.environ.get('PYTHONPATH', '').split(os.pathsep) if p]
+    env = dict(os.environ, SOCCERACTION_AMD_DEBUG='1', PYTHONPATH=os.pathsep.join(path))
     p = subprocess.run([sys.executable] + args, cwd=ROOT, env=env, capture_output=True, text=True,
                        timeout=timeout)
     assert p.returncode == 0, (p.stdout[-3000:], p.stderr[-3000:])

@@ -1,0 +1,205 @@
+"""GPU parity of the large-grid xT fit (sa_xt_large.hip): the band-owned count (no global
+atomics) against the oracle's counts, and the compact-form value iteration against the dense
+count-row iteration (sa_xt_iterate_rows), bit for bit.  Reference: xthreat.py:40-67, 177-218
+(counts), 278-320 (value iteration)."""
+import numpy as np
+import pytest
+
+from oracle import xt_oracle as xo
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip('torch')
+
+
+@pytest.fixture(scope='module')
+def sa():
+    from socceraction_amd import _native, batch, ops, synthetic
+    _native.load_library()
+    return dict(_native=_native, batch=batch, ops=ops, synthetic=synthetic)
+
+
+def _oracle(d, l, w):
+    return xo.counts({c: d[c] for c in ('start_x', 'start_y', 'end_x', 'end_y', 'type_id',
+                                         'result_id')}, l, w)
+
+
+def _same_counts(acc, ref, l, w):
+    C = l * w
+    np.testing.assert_array_equal(acc.shot.cpu().numpy(), ref['shot'].reshape(-1))
+    np.testing.assert_array_equal(acc.goal.cpu().numpy(), ref['goal'].reshape(-1))
+    np.testing.assert_array_equal(acc.move.cpu().numpy(), ref['move'].reshape(-1))
+    np.testing.assert_array_equal(acc.trans.cpu().numpy().reshape(C, C), ref['trans'])
+
+
+def _cat(parts):
+    out = {}
+    for k, v in parts[0].items():
+        if isinstance(v, np.ndarray) and k not in ('game_off', 'home_team_id'):
+            out[k] = np.concatenate([p[k] for p in parts])
+    return out
+
+
+@pytest.mark.parametrize('l,w', [(105, 68), (40, 30), (15, 14)])
+def test_band_count_many_batches_vs_oracle(sa, l, w):
+    """xt_count_many over three device batches (fresh accumulator: the band count writes the
+    table once, never reading it) == the oracle's counts of all their actions; the same batches
+    added into an accumulator that already holds counts (one xt_count first) == the sum."""
+    B, ops, syn = sa['batch'], sa['ops'], sa['synthetic']
+    assert ops.xt_band_shape(l, w) is not None
+    ds = [syn.spadl_games(g, game_id0=100 * i + 7) for i, g in enumerate((40, 55, 23))]
+    abs_ = [B.ActionBatch.from_columns(d) for d in ds]
+    acc = ops.xt_count_many(abs_, l, w)
+    ops.xt_check_errors(acc)
+    _same_counts(acc, _oracle(_cat(ds), l, w), l, w)
+    acc2 = ops.xt_count(abs_[0], l, w)
+    ops.xt_count_many(abs_[1:], l, w, acc2)  # accumulate (read-modify-write of the rows)
+    _same_counts(acc2, _oracle(_cat(ds), l, w), l, w)
+
+
+def test_band_count_hot_cells_and_edges(sa):
+    """Adversarial key distributions: every move between two cells (one bin far above 65535
+    counts, one band holding almost every key), actions on the exact pitch edges, NaN / inf
+    coordinates (error bytes as sa_xt_count's coordinate path) and a batch shorter than one
+    workgroup's chunk."""
+    B, ops, syn = sa['batch'], sa['ops'], sa['synthetic']
+    l, w = 105, 68
+    d = syn.spadl_games(80, game_id0=11)
+    n = len(d['type_id'])
+    mv = np.isin(d['type_id'], (0, 1, 21))
+    d['start_x'][mv], d['start_y'][mv] = 52.2, 33.3
+    d['end_x'][mv], d['end_y'][mv] = 104.999, 0.0
+    ab = B.ActionBatch.from_columns(d)
+    acc = ops.xt_count(ab, l, w)
+    ops.xt_check_errors(acc)
+    ref = _oracle(d, l, w)
+    assert ref['trans'].max() > 65535
+    _same_counts(acc, ref, l, w)
+    rng = np.random.default_rng(4)
+    e = syn.spadl_games(3, game_id0=19)
+    m = len(e['type_id'])
+    for col, v in (('start_x', 0.0), ('end_x', 105.0), ('start_y', 68.0), ('end_y', 0.0)):
+        e[col][rng.choice(m, 40, replace=False)] = v
+    ab = B.ActionBatch.from_columns(e)
+    _same_counts(ops.xt_count_many([ab], l, w), _oracle(e, l, w), l, w)
+    for col, v, bit in (('start_x', np.nan, 0x10000), ('end_y', np.inf, 0x10000)):
+        f = {k: (v2.copy() if isinstance(v2, np.ndarray) else v2) for k, v2 in e.items()}
+        f[col][np.flatnonzero(np.isin(f['type_id'], (0, 1, 21)))[:5]] = v
+        ab = B.ActionBatch.from_columns(f)
+        got = ops.xt_count_many([ab], l, w)
+        old = ops.xt_count(ab, l, w)  # the one-batch entry point: the same band path
+        assert int(got.err.item()) & bit and int(got.err.item()) == int(old.err.item())
+        for a, b in ((got.shot, old.shot), (got.goal, old.goal), (got.move, old.move),
+                     (got.trans, old.trans)):
+            assert torch.equal(a, b)
+    # a shot with an infinite start: byte 0x1
+    f = {k: (v2.copy() if isinstance(v2, np.ndarray) else v2) for k, v2 in e.items()}
+    f['start_x'][np.flatnonzero(f['type_id'] == 11)[:2]] = -np.inf
+    got = ops.xt_count_many([B.ActionBatch.from_columns(f)], l, w)
+    assert int(got.err.item()) & 0xFF
+
+
+def _random_rows(rng, C, nrows, zero_rows=3):
+    """Count rows shaped like a fit's: ~40 % non-zero, mostly small counts, some >= 64 (the
+    division path), a few >= 65535 (the escape to the dense row), some empty rows."""
+    cnt = np.zeros((nrows, C), np.int32)
+    nz = rng.random((nrows, C)) < 0.4
+    cnt[nz] = rng.geometric(0.3, nz.sum())
+    big = rng.random((nrows, C)) < 0.002
+    cnt[big] = rng.integers(64, 5000, big.sum())
+    cnt[rng.integers(0, nrows, 4), rng.integers(0, C, 4)] = rng.integers(65535, 300000, 4)
+    cnt[rng.choice(nrows, zero_rows, replace=False)] = 0
+    return cnt
+
+
+@pytest.mark.parametrize('C,r0,nrows', [(7140, 0, 7140), (7140, 1785, 1785), (1200, 1170, 30),
+                                        (203, 0, 203)])
+def test_compact_iteration_equals_dense(sa, C, r0, nrows):
+    """sa_xt_iterate_compact over sa_xt_compact_rows == sa_xt_iterate_rows (the dense count-row
+    kernel), bit for bit, on random count rows (tabulated quotients, divided counts, escaped
+    counts >= 65535, empty rows), a sub-range of rows (the row-sharded solve), x with zeros;
+    the convergence flag and the no-op when the previous flag is 0."""
+    _native, ops = sa['_native'], sa['ops']
+    from socceraction_amd.batch import stream_handle
+    lib = _native.lib()
+    dev = torch.device('cuda')
+    rng = np.random.default_rng(C + r0)
+    rows = torch.from_numpy(_random_rows(rng, C, nrows)).to(dev)
+    move_all = rng.integers(1, 10, C).astype(np.int64)
+    move_all[r0:r0 + nrows] += rows.sum(dim=1, dtype=torch.int64).cpu().numpy()
+    move = torch.from_numpy(move_all).to(dev)
+    gs = torch.rand(C, dtype=torch.float64, device=dev) * 0.1
+    pm = torch.rand(C, dtype=torch.float64, device=dev)
+    ell = torch.empty(int(lib.sa_xt_compact_bytes(C, nrows)) // 4, dtype=torch.int32, device=dev)
+    slen = torch.empty(-(-nrows // 32), dtype=torch.int32, device=dev)
+    p = lambda t: t.data_ptr()  # noqa: E731
+    _native.check(lib.sa_xt_compact_rows(p(rows), C, nrows, p(ell), p(slen), stream_handle()))
+    lens = slen.cpu().numpy()
+    nnz = (rows.cpu().numpy() != 0).sum(axis=1)
+    np.testing.assert_array_equal(lens, [nnz[i:i + 32].max() for i in range(0, nrows, 32)])
+    for trial in range(3):
+        x = torch.rand(C, dtype=torch.float64, device=dev)
+        x[torch.from_numpy(rng.random(C) < 0.2).to(dev)] = 0.0
+        a = torch.empty(nrows, dtype=torch.float64, device=dev)
+        b = torch.empty(nrows, dtype=torch.float64, device=dev)
+        fa = torch.zeros(1, dtype=torch.int32, device=dev)
+        fb = torch.zeros(1, dtype=torch.int32, device=dev)
+        eps = 1e-5 if trial < 2 else 10.0
+        _native.check(lib.sa_xt_iterate_rows(p(rows), p(move), p(gs), p(pm), C, r0, nrows, p(x),
+                                             eps, p(a), None, p(fa), stream_handle()))
+        _native.check(lib.sa_xt_iterate_compact(p(ell), p(slen), p(rows), p(move), p(gs), p(pm), C,
+                                                r0, nrows, p(x), eps, p(b), None, p(fb),
+                                                stream_handle()))
+        assert torch.equal(a, b), trial
+        assert int(fa.item()) == int(fb.item()) == (1 if trial < 2 else 0)
+    zero = torch.zeros(1, dtype=torch.int32, device=dev)
+    b.fill_(-1.0)
+    _native.check(lib.sa_xt_iterate_compact(p(ell), p(slen), p(rows), p(move), p(gs), p(pm), C, r0,
+                                            nrows, p(x), 1e-5, p(b), p(zero), p(fb), stream_handle()))
+    assert bool((b == -1.0).all())
+
+
+def test_full_cfg4_batch_large_grid_solve(sa):
+    """One full cfg2/cfg4 batch (10k games, ~16M actions) at 105 x 68: band count == the oracle's
+    counts, and the solve over the compact rows gives the oracle's iteration count and surface."""
+    B, ops, syn = sa['batch'], sa['ops'], sa['synthetic']
+    d = syn.spadl_games(10000)
+    ab = B.ActionBatch.from_columns(d)
+    acc = ops.xt_count_many([ab], 105, 68)
+    ref = _oracle(d, 105, 68)
+    _same_counts(acc, ref, 105, 68)
+    sol = ops.xt_solve(acc, transition=False)
+    fit = xo.solve(ref, 105, 68)
+    assert sol.n_iter + 1 == len(fit['heatmaps'])
+    np.testing.assert_array_equal(sol.mats[3].cpu().numpy().reshape(68, 105), fit['xT'])
+
+
+def test_interp_codes_rate_equals_rate_interp(sa):
+    """The bucket pass's per-action interpolated-rate operands + sa_xt_rate_interp_codes ==
+    sa_xt_rate_interp on the coordinates, bit for bit: values, NaN pattern and error bit 4
+    (NaN / inf coordinates on successful moves, exact pitch edges, an odd-length batch)."""
+    B, ops, syn = sa['batch'], sa['ops'], sa['synthetic']
+    d = syn.spadl_games(31, game_id0=23)
+    n = len(d['type_id'])
+    d = {k: (v[:n - 1].copy() if isinstance(v, np.ndarray) and v.shape == (n,) else v)
+         for k, v in d.items()}
+    d['game_off'] = np.minimum(d['game_off'], n - 1)
+    rng = np.random.default_rng(12)
+    for col, v in (('start_x', 0.0), ('end_x', 105.0), ('start_y', 68.0), ('end_y', 0.0),
+                   ('start_x', 104.99999999999999)):
+        d[col][rng.choice(n - 1, 30, replace=False)] = v
+    for bad in (False, True):
+        if bad:
+            for col, v in (('start_x', np.nan), ('end_y', np.inf), ('end_x', -np.inf)):
+                d[col][rng.choice(n - 1, 5, replace=False)] = v
+        ab = B.ActionBatch.from_columns(d)
+        ic = ops.xt_interp_codes_buffer(ab.n, ab.device)
+        acc = ops.xt_count_many([ab], 105, 68, interp_codes=[ic])
+        xT = torch.rand((68, 105), dtype=torch.float64, device=ab.device)
+        ref, e0 = ops.xt_rate_interp(ab, xT, 105, 68)
+        got, e1 = ops.xt_rate_interp_codes(ic, ab.n, xT, 105, 68)
+        a, b = ref.cpu().numpy(), got.cpu().numpy()
+        np.testing.assert_array_equal(np.isnan(a), np.isnan(b))
+        np.testing.assert_array_equal(a[~np.isnan(a)], b[~np.isnan(a)])
+        assert int(e0.item()) == int(e1.item()) == (4 if bad else 0)
+        assert bool(acc.err.item()) == bad
