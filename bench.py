@@ -491,12 +491,10 @@ def xt105_extra(ab, dist, dev, sharded: bool = False, cfg5_games: int = 62500,
         # written once by sa_xt_count_from_buckets; no global atomics), into a fresh accumulator
         # and, per action, the operand of the interpolated rate below (start / end node of the
         # 1050 x 680 grid: 8 B read by the rate instead of 34 B of coordinates and ids)
-        if sharded and dist is not None:  # reduce-scatter of count rows + row-sharded solve
-            acc = ops.xt_zero_counts(l, w, dev, row_blocks=dist.get_world_size())
-            ops.xt_count_many(batches, l, w, acc, overwrite=True, interp_codes=icodes)
-            mark()
-            mark()  # (the exchange happens inside the sharded solve)
-            mats, _, n_iter = shard.xt_solve_sharded(acc)
+        if sharded and dist is not None:  # band-sharded: all-to-all of the counted actions,
+            mark()                         # each rank counts its bands; row-sharded iteration
+            mark()  # (count and exchange happen inside the sharded fit)
+            mats, _, n_iter, err = shard.xt_fit_bands_sharded(batches, l, w, interp_codes=icodes)
             acc = None  # each rank holds only its row block of the transition counts
         else:  # one all-reduce of the counts, replicated solve
             acc = ops.xt_count_many(batches, l, w, interp_codes=icodes)
@@ -567,10 +565,12 @@ def xt105_extra(ab, dist, dev, sharded: bool = False, cfg5_games: int = 62500,
                       f'min {min(times) * 1e3:.3f}, max {max(times) * 1e3:.3f} ms on rank {rank})'
                       + ('; max over ranks' if dist is not None else ''),
             'scaling': 'strong' if cfg5_games > 0 else 'weak',
-            'solve': 'row-sharded' if (sharded and dist is not None) else 'replicated',
+            'solve': ('band-sharded (all-to-all of counted actions, row-sharded iteration)'
+                      if (sharded and dist is not None) else 'replicated'),
             'phases_ms': dict(phases, note='one extra call synchronised between phases (rank '
                               f'{rank}): count = band buckets + table; exchange = the counts\' '
-                              'all-reduce (sharded: inside solve); solve = normalise + value '
+                              'all-reduce (band-sharded: count and exchange inside solve); '
+                              'solve = normalise + value '
                               'iteration incl. its host syncs; rate'),
             'pipeline': 'band-owned count (per batch: one key per counted action, bucketed by '
                         'start-cell band; the 7140^2 table written once, no global atomics) '
@@ -770,9 +770,13 @@ def main() -> None:
     ap.add_argument('--cfg5-games', type=int, default=62500,
                     help='games of the cfg5 side entry (BASELINE cfg5: 62,500 = 1.0e8 actions, '
                          'split over the ranks; 0 = the step batch)')
-    ap.add_argument('--xt-sharded', action='store_true',
-                    help='cfg5 with N > 1: reduce-scatter the count rows and row-shard the value '
-                         'iteration (default: one all-reduce, replicated solve)')
+    ap.add_argument('--cfg5-solve', default='auto', choices=('auto', 'sharded', 'replicated'),
+                    help='cfg5 with N > 1: "sharded" = each rank counts and iterates its own '
+                         'start-cell bands after ONE all-to-all of the counted actions '
+                         '(shard.xt_fit_bands_sharded); "replicated" = one all-reduce of the '
+                         '204 MB count table and the whole solve on every rank; auto = sharded '
+                         '(the projection in DESIGN.md §6)')
+    ap.add_argument('--xt-sharded', action='store_true', help='same as --cfg5-solve sharded')
     ap.add_argument('--atomic-games', type=int, default=10000,
                     help='atomic games of the cfg3 side entry, split over the ranks (BASELINE '
                          'cfg3: 10,000 = 4.0e7 atomic actions)')
@@ -1084,7 +1088,8 @@ def main() -> None:
         check_s = time.perf_counter() - tc
     extra_side = {}
     if not args.no_side:
-        extra_side['xt105_cfg5'] = xt105_extra(ab, dist, dev, args.xt_sharded, args.cfg5_games,
+        cfg5_sharded = args.xt_sharded or args.cfg5_solve in ('auto', 'sharded')
+        extra_side['xt105_cfg5'] = xt105_extra(ab, dist, dev, cfg5_sharded, args.cfg5_games,
                                                rank, world, args.games, d=d, check=check)
         extra_side['atomic_cfg3'] = atomic_extra(dist, rank, world, dev, args.atomic_games,
                                                  check=check)

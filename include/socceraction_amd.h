@@ -300,6 +300,16 @@ int sa_xt_band_shape(int32_t l, int32_t w, int32_t* rows_per_band, int32_t* n_ba
 int sa_xt_count_bucket(const sa_actions* a, const uint32_t* cells, int64_t n, int32_t l, int32_t w,
                        uint32_t* buckets, int64_t* band_off, int32_t* err_flags, uint32_t* codes,
                        uint64_t* interp_codes, int32_t L, int32_t W, void* stream);
+/* The band-owned count of bands [band0, band0 + nbands) only (a rank's row block in the
+ * row-sharded multi-GPU fit: its bands' keys gathered from every rank by an all-to-all).  Set k's
+ * keys of local band lb (band band0 + lb) are buckets[k][band_off[k][lb] .. band_off[k][lb + 1]),
+ * band_off[k] holding nbands + 1 entries; the outputs hold the rows from band0 * R on (R from
+ * sa_xt_band_shape): shot / goal / move_rows [min(nbands R, C - band0 R)], trans_rows
+ * [that many rows x C].  flags: SA_XT_COUNT_OVERWRITE or 0 (add). */
+int sa_xt_count_band_rows(int32_t nsets, const uint32_t* const* buckets,
+                          const int64_t* const* band_off, int32_t l, int32_t w, int32_t band0,
+                          int32_t nbands, int64_t* shot_rows, int64_t* goal_rows,
+                          int64_t* move_rows, int32_t* trans_rows, int32_t flags, void* stream);
 /* interp_codes (coordinates only; [n] u64, 16-byte aligned, or NULL): per action the operand of a
  * later rate(use_interpolation=True) of the SAME actions on the L x W node grid -- start node |
  * end node << 32 of a successful move, 2^64 - 2 for one with a non-finite coordinate, 2^64 - 1
@@ -360,16 +370,17 @@ int sa_xt_iterate_rows(const int32_t* cnt_rows, const int64_t* move, const doubl
                        const double* pmove, int32_t C, int32_t r0, int32_t nrows, const double* x,
                        double eps, double* x_next_rows, const int32_t* flag_prev, int32_t* flag_out,
                        void* stream);
-/* The same iteration over a compact form of the count rows built once (C <= 10240; sa_xt_solve
- * uses it for C > SA_XT_SOLVE_MAX_C): sa_xt_compact_rows writes, per slice of 32 rows, each
- * row's non-zero counts in column order (4 B each) into ell (u32, 16-byte aligned,
- * sa_xt_compact_bytes(C, nrows) bytes) and the slice lengths into slice_len[(nrows + 31) / 32]
- * (int32, device); sa_xt_iterate_compact then equals sa_xt_iterate_rows bit for bit (cnt_rows:
- * the same dense rows, read only for counts >= 65535).  Asynchronous. */
+/* The same iteration over a compact form of the count rows built once (C <= 9472; sa_xt_solve
+ * uses it for C > SA_XT_SOLVE_MAX_C): sa_xt_compact_rows writes each row's non-zero counts in
+ * column order (4 B each: column | min(count, 65535) << 16) at ell[i * pe ..], pe = C rounded up
+ * to a multiple of 4 (u32, 16-byte aligned, sa_xt_compact_bytes(C, nrows) bytes), and their
+ * number at row_len[i] (int32 [nrows], device);
+ * sa_xt_iterate_compact then equals sa_xt_iterate_rows bit for bit (cnt_rows: the same dense
+ * rows, read only for counts >= 65535).  Asynchronous. */
 int64_t sa_xt_compact_bytes(int32_t C, int32_t nrows);
 int sa_xt_compact_rows(const int32_t* cnt_rows, int32_t C, int32_t nrows, uint32_t* ell,
-                       int32_t* slice_len, void* stream);
-int sa_xt_iterate_compact(const uint32_t* ell, const int32_t* slice_len, const int32_t* cnt_rows,
+                       int32_t* row_len, void* stream);
+int sa_xt_iterate_compact(const uint32_t* ell, const int32_t* row_len, const int32_t* cnt_rows,
                           const int64_t* move, const double* gs, const double* pmove, int32_t C,
                           int32_t r0, int32_t nrows, const double* x, double eps,
                           double* x_next_rows, const int32_t* flag_prev, int32_t* flag_out,

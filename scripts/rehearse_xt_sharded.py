@@ -31,6 +31,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--games', type=int, default=400, help='games per rank')
     ap.add_argument('--grid', default='105x68', help='l x w cells')
+    ap.add_argument('--mode', default='auto', choices=('auto', 'bands', 'rows'),
+                    help='bands: shard.xt_fit_bands_sharded (all-to-all of the counted actions); '
+                         'rows: xt_solve_sharded (reduce-scatter of the count table); auto: bands '
+                         'where the band-owned count holds the grid')
     args = ap.parse_args()
     backend = os.environ.get('SA_DIST_BACKEND', 'nccl')
     lr = int(os.environ.get('LOCAL_RANK', '0'))
@@ -45,7 +49,15 @@ def main():
     d = synthetic.spadl_games(args.games, game_id0=rank * args.games)
     ab = B.ActionBatch.from_columns(d, dev=dev)
 
+    mode = args.mode
+    if mode == 'auto':
+        mode = 'bands' if ops.xt_band_shape(l, w) is not None else 'rows'
+
     def fit():
+        if mode == 'bands':
+            mats, heat, iters, err = shard.xt_fit_bands_sharded([ab], l, w)
+            assert int(err.item()) == 0
+            return mats, heat, iters
         acc = ops.xt_zero_counts(l, w, dev, row_blocks=world)
         ops.xt_count(ab, l, w, acc)
         return shard.xt_solve_sharded(acc)
@@ -56,7 +68,7 @@ def main():
     mats, heat, iters = fit()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    out = {'rank': rank, 'world': world, 'backend': backend, 'grid': f'{l}x{w}',
+    out = {'rank': rank, 'world': world, 'backend': backend, 'grid': f'{l}x{w}', 'mode': mode,
            'actions_this_rank': ab.n, 'iterations': iters, 'ms_sharded_fit': round(dt * 1e3, 3)}
     if rank == 0:
         cols = [synthetic.spadl_games(args.games, game_id0=r * args.games) for r in range(world)]

@@ -24,7 +24,7 @@ SA_SEG_BLOCK = 128  # rows per entry of sa_actions.seg_of_block
 SA_XT_SOLVE_MAX_C = 1024  # sa_xt_solve: larger grids may pass trans_t = NULL
 SA_XT_CELLS_MAX_C = 4096
 SA_XT_COUNT_SHARED, SA_XT_COUNT_OVERWRITE = 1, 2
-SA_XT_COMPACT_MAX_C = 10240  # sa_xt_compact_rows / sa_xt_iterate_compact
+SA_XT_COMPACT_MAX_C = 9472  # sa_xt_compact_rows / sa_xt_iterate_compact
 SA_BOOL_TILE_QUANTUM = 1024
 SA_NUM_TILE_QUANTUM = 128
 SA_OK, SA_EINVAL, SA_EHIP, SA_EDATA, SA_ENOMEM = 0, -1, -2, -3, -4
@@ -160,6 +160,9 @@ _SIGNATURES = {
     'sa_xt_count_from_buckets': (ctypes.c_int, [ctypes.c_int32, ctypes.POINTER(_p), ctypes.POINTER(_p),
                                                 ctypes.c_int32, ctypes.c_int32, _p, _p, _p, _p,
                                                 ctypes.c_int32, _p]),
+    'sa_xt_count_band_rows': (ctypes.c_int, [ctypes.c_int32, ctypes.POINTER(_p), ctypes.POINTER(_p),
+                                             ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                             ctypes.c_int32, _p, _p, _p, _p, ctypes.c_int32, _p]),
     'sa_xt_compact_bytes': (ctypes.c_int64, [ctypes.c_int32, ctypes.c_int32]),
     'sa_xt_compact_rows': (ctypes.c_int, [_p, ctypes.c_int32, ctypes.c_int32, _p, _p, _p]),
     'sa_xt_iterate_compact': (ctypes.c_int, [_p, _p, _p, _p, _p, _p, ctypes.c_int32, ctypes.c_int32,

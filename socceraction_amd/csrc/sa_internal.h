@@ -34,14 +34,14 @@ void scratch_release(const Scratch& s, hipStream_t st);
 
 // Large-grid xT (sa_xt_large.hip).  xt_band_ok: the band-owned count holds a grid of C cells;
 // xt_count_bands: that count of one batch, added into the caller's counts.  xt_compact_*: the
-// compact form of count rows and one value iteration over it (C <= 10240).
+// compact form of count rows and one value iteration over it (C <= 9472).
 bool xt_band_ok(int C);
 int xt_count_bands(const sa_actions& A, const uint32_t* cells, int64_t n, int l, int w, int64_t* shot,
                    int64_t* goal, int64_t* move, int32_t* trans, int32_t* err, uint32_t* codes, hipStream_t st);
 bool xt_compact_ok(int C);
 size_t xt_compact_bytes(int C, int nrows);
-int xt_compact_build(const int32_t* cnt_rows, int C, int nrows, uint32_t* ell, int32_t* slice_len, hipStream_t st);
-int xt_compact_iterate(const uint32_t* ell, const int32_t* slice_len, const int32_t* cnt_rows, const int64_t* move,
+int xt_compact_build(const int32_t* cnt_rows, int C, int nrows, uint32_t* ell, int32_t* row_len, hipStream_t st);
+int xt_compact_iterate(const uint32_t* ell, const int32_t* row_len, const int32_t* cnt_rows, const int64_t* move,
                        const double* gs, const double* pmove, int C, int rb, int nrows, const double* x, double eps,
                        double* xo, const int32_t* flag_prev, int32_t* flag_out, hipStream_t st);
 }  // namespace sa

@@ -1123,7 +1123,7 @@ extern "C" int sa_xt_solve(const int64_t* shot, const int64_t* goal, const int64
   } else if (!rc) {
     rc = check_hip(hipMemsetAsync(dflags, 0, sizeof(int32_t) * (max_iter + 1), st), "memset");
     if (!rc) rc = check_hip(hipMemsetAsync(heatmaps, 0, sizeof(double) * C, st), "memset");
-    // the compact form of the count rows, built once (sa_xt_large.hip): [ell | slice_len]
+    // the compact form of the count rows, built once (sa_xt_large.hip): [ell | row_len]
     const bool compact = SA_XT_COMPACT && xt_compact_ok(C);
     Scratch ce;
     uint32_t* ell = nullptr;

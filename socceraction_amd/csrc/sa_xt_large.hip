@@ -19,10 +19,9 @@
 //    K1-K3 run per batch of actions (sa_xt_count_bucket); K4 runs once over the buckets of every
 //    batch (sa_xt_count_from_buckets), so the 204 MB table is written once per fit.
 // 2. Value iteration (xthreat.py:278-320) over a compact form of the counts built once per solve
-//    (sa_xt_compact_rows): per slice of 32 rows the non-zero counts of each row in column order,
-//    4 B each (column | count << 16), interleaved by row (entry k of row i at k * 32 + i) so a
-//    wave reads 256 contiguous bytes.  Per iteration (xt_iter_ell_kernel) eight product waves form
-//    T[r, c] * x[c] = (cnt / move[r]) * x[c] -- the quotient tabulated in LDS for counts < 64, the
+//    (sa_xt_compact_rows): each row's non-zero counts in column order, 4 B each (column | count
+//    << 16), contiguous per row.  Per iteration (xt_iter_ell_kernel) eight product waves form
+//    T[r, c] * x[c] = (cnt / move[r]) * x[c] -- the quotient tabulated in LDS for small counts, the
 //    same correctly rounded division -- and one chain wave adds each row's products strictly left
 //    to right (the reference's loop order; zero terms add +0 to a non-negative sum, so skipping
 //    them keeps every bit).  84 MB per iteration instead of the 204 MB dense int32 rows.
@@ -37,12 +36,19 @@
 namespace sa {
 
 // ============================================================================ band-owned count
-constexpr int XK_THREADS = 256;     // K1 workgroup
+#ifndef SA_XK_THREADS
+#define SA_XK_THREADS 1024  // K1 workgroup (two per CU at cfg5: 32 waves of loads in flight)
+#endif
+constexpr int XK_THREADS = SA_XK_THREADS;
 constexpr int XK_CHUNK = 32768;     // actions per K1 workgroup = key capacity of its region
 constexpr int XS_THREADS = 1024;    // K3 workgroup
 constexpr int XS_PER = XK_CHUNK / XS_THREADS;
 constexpr int XB_THREADS = 1024;    // K4 workgroup
-constexpr int XB_MAX_ROWS = 8;      // start cells per band
+#ifndef SA_XB_RMAX
+#define SA_XB_RMAX 8  // start cells per band at most (105 x 68: 5 = the most 160 KB of LDS holds)
+#endif
+constexpr int XB_MAX_ROWS = 8;      // start cells per band (LDS row sums)
+static_assert(SA_XB_RMAX >= 1 && SA_XB_RMAX <= XB_MAX_ROWS, "SA_XB_RMAX");
 constexpr int XB_NB_MAX = 4000;     // bands (K3 holds 2 words per band + a region's keys in LDS)
 constexpr size_t XB_LDS_MAX = 160 * 1024;
 constexpr int XB_MAX_SETS = 24;     // buckets per K4 launch
@@ -115,13 +121,15 @@ struct XkRate {
 // K1: region r = actions [r * XK_CHUNK, (r + 1) * XK_CHUNK) -> keys[r * XK_CHUNK + i], i <
 // region_cnt[r]; band_cnt[b] += the region's keys of band b.  CELLS: 4-B cell codes
 // (sa_xt_cells, C <= SA_XT_CELLS_MAX_C) instead of the coordinates (no rate operands then).
+// vec (coordinates): the columns are 16-byte (f64) / 2-byte (ids) aligned, so a lane loads two
+// consecutive actions per column instruction (16-B and 2-B loads, half the load instructions).
 template <bool CELLS>
 __global__ __launch_bounds__(XK_THREADS) void xt_keys_kernel(sa_actions A, const uint32_t* __restrict__ cells,
                                                              int64_t n, int l, int w, XbShape S,
                                                              uint32_t* __restrict__ keys,
                                                              uint32_t* __restrict__ region_cnt,
                                                              uint32_t* __restrict__ band_cnt,
-                                                             int32_t* __restrict__ err, XkRate RO) {
+                                                             int32_t* __restrict__ err, XkRate RO, int vec) {
   extern __shared__ uint32_t bh[];  // [NB]
   __shared__ uint32_t cursor;
   for (int b = threadIdx.x; b < S.NB; b += XK_THREADS) bh[b] = 0;
@@ -149,22 +157,59 @@ __global__ __launch_bounds__(XK_THREADS) void xt_keys_kernel(sa_actions A, const
         if (base + u * XK_THREADS + threadIdx.x >= end) act[u].cls = 0;
       }
     } else {
+      // action u of the pass: j = base + 2 (p * XK_THREADS + tid) + e, u = 2 p + e (vec), or
+      // j = base + u * XK_THREADS + tid; rows past `end` are clamped and not counted
       int tt[U], rr[U];
       double sx[U], sy[U], ex[U], ey[U];
+      int64_t jj[U];
+      if (vec) {
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int64_t j = base + u * XK_THREADS + threadIdx.x;
-        const int64_t jc = j < end ? j : end - 1;
-        tt[u] = j < end ? F.type_id[jc] : -1;
-        rr[u] = F.result_id[jc];
-        sx[u] = F.c0[jc];
-        sy[u] = F.c1[jc];
-        ex[u] = F.c2[jc];
-        ey[u] = F.c3[jc];
+        for (int q = 0; q < U / 2; ++q) {
+          const int64_t j = base + 2 * ((int64_t)q * XK_THREADS + threadIdx.x);
+          const int64_t jc = j + 1 < end ? j : ((end - 2) & ~(int64_t)1);  // a whole aligned pair
+          const f64x2 a = *reinterpret_cast<const f64x2*>(F.c0 + jc), b = *reinterpret_cast<const f64x2*>(F.c1 + jc);
+          const f64x2 c = *reinterpret_cast<const f64x2*>(F.c2 + jc), d = *reinterpret_cast<const f64x2*>(F.c3 + jc);
+          const uint32_t ty = *reinterpret_cast<const uint16_t*>(F.type_id + jc);
+          const uint32_t rs = *reinterpret_cast<const uint16_t*>(F.result_id + jc);
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const int u = 2 * q + e;
+            jj[u] = j + e;
+            sx[u] = a[e];
+            sy[u] = b[e];
+            ex[u] = c[e];
+            ey[u] = d[e];
+            tt[u] = (int)((ty >> (8 * e)) & 0xFF);
+            rr[u] = (int)((rs >> (8 * e)) & 0xFF);
+          }
+          if (j + 1 >= end) {  // the batch's odd last action (or none): scalar, the rest not counted
+            const int64_t k = j < end ? j : end - 1;
+            sx[2 * q] = F.c0[k];
+            sy[2 * q] = F.c1[k];
+            ex[2 * q] = F.c2[k];
+            ey[2 * q] = F.c3[k];
+            tt[2 * q] = j < end ? (int)F.type_id[k] : -1;
+            rr[2 * q] = F.result_id[k];
+            tt[2 * q + 1] = -1;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int64_t j = base + u * XK_THREADS + threadIdx.x;
+          const int64_t jc = j < end ? j : end - 1;
+          jj[u] = j;
+          tt[u] = j < end ? F.type_id[jc] : -1;
+          rr[u] = F.result_id[jc];
+          sx[u] = F.c0[jc];
+          sy[u] = F.c1[jc];
+          ex[u] = F.c2[jc];
+          ey[u] = F.c3[jc];
+        }
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int64_t j = base + u * XK_THREADS + threadIdx.x;
+        const int64_t j = jj[u];
         if (RO.codes && tt[u] >= 0) RO.codes[j] = rate_code(tt[u], rr[u], sx[u], sy[u], ex[u], ey[u], l, w);
         if (RO.icodes && tt[u] >= 0)
           RO.icodes[j] = rate_icode(tt[u], rr[u], sx[u], sy[u], ex[u], ey[u], RO.L, RO.W);
@@ -313,12 +358,14 @@ struct XbSets {
   int n;
 };
 
-// K4: band b = start cells [b R, b R + R).  Bins h[i][slot] (i < R, slot < C + 3) as u32 in LDS,
-// filled by LDS atomics from every set's bucket of the band, then flushed: the transition rows
-// with coalesced 16-B stores (vec) or 4-B stores, the shot / goal / move counts of each cell
-// from slots C, C + 1, C + 2 and the row sum.  overwrite: the rows and counts are written, not
-// added to (a fresh accumulator: no read of the old rows).
-__global__ __launch_bounds__(XB_THREADS) void xt_band_count_kernel(XbSets sets, XbShape S,
+// K4: workgroup lb = band b = band0 + lb = start cells [b R, b R + R).  Bins h[i][slot] (i < R,
+// slot < C + 3) as u32 in LDS, filled by LDS atomics from every set's bucket of the band (set s:
+// keys[s][off[s][lb] .. off[s][lb + 1])), then flushed: the transition rows with coalesced 16-B
+// stores (vec) or 4-B stores, the shot / goal / move counts of each cell from slots C, C + 1,
+// C + 2 and the row sum.  The outputs hold rows from band0 * R on (a rank's row block, or the
+// whole table with band0 = 0).  overwrite: the rows and counts are written, not added to (a
+// fresh accumulator: no read of the old rows).
+__global__ __launch_bounds__(XB_THREADS) void xt_band_count_kernel(XbSets sets, XbShape S, int band0,
                                                                    unsigned long long* __restrict__ shot,
                                                                    unsigned long long* __restrict__ goal,
                                                                    unsigned long long* __restrict__ move,
@@ -326,14 +373,15 @@ __global__ __launch_bounds__(XB_THREADS) void xt_band_count_kernel(XbSets sets, 
                                                                    int vec) {
   extern __shared__ __attribute__((aligned(16))) uint32_t h[];  // [R][P]
   __shared__ unsigned long long msum[XB_MAX_ROWS];
-  const int b = blockIdx.x, C = S.C, P = S.P;
+  const int lb = blockIdx.x, b = band0 + lb, C = S.C, P = S.P;
   const int r0 = b * S.R, nr = min(S.R, C - r0);
+  const int orow = r0 - band0 * S.R;  // the band's first row in the outputs
   for (int e = 4 * threadIdx.x; e < nr * P; e += 4 * XB_THREADS) *reinterpret_cast<u32x4*>(h + e) = u32x4{0, 0, 0, 0};
   if (threadIdx.x < XB_MAX_ROWS) msum[threadIdx.x] = 0;
   __syncthreads();
   for (int s = 0; s < sets.n; ++s) {
     const uint32_t* kp = sets.keys[s];
-    const int64_t lo = sets.off[s][b], hi = sets.off[s][b + 1];
+    const int64_t lo = sets.off[s][lb], hi = sets.off[s][lb + 1];
     for (int64_t i = lo + threadIdx.x; i < hi; i += 4 * XB_THREADS) {
       uint32_t v[4];
 #pragma unroll
@@ -354,7 +402,7 @@ __global__ __launch_bounds__(XB_THREADS) void xt_band_count_kernel(XbSets sets, 
   const int lane = threadIdx.x & 63;
   for (int i = 0; i < nr; ++i) {
     const uint32_t* hr = h + i * P;
-    int32_t* dst = trans + (int64_t)(r0 + i) * C;
+    int32_t* dst = trans + (int64_t)(orow + i) * C;
     unsigned long long ms = 0;
     if (vec) {  // C % 4 == 0 and trans 16-byte aligned: every row starts 16-byte aligned
       for (int c = 4 * threadIdx.x; c < C; c += 4 * XB_THREADS) {
@@ -380,7 +428,7 @@ __global__ __launch_bounds__(XB_THREADS) void xt_band_count_kernel(XbSets sets, 
   }
   __syncthreads();
   if (threadIdx.x < nr) {
-    const int i = threadIdx.x, r = r0 + i;
+    const int i = threadIdx.x, r = orow + i;
     const uint32_t* hr = h + i * P;
     const unsigned long long sh = (unsigned long long)hr[C] + hr[C + 1], gl = hr[C + 1];
     const unsigned long long mv = msum[i] + hr[C + 2];
@@ -397,143 +445,239 @@ __global__ __launch_bounds__(XB_THREADS) void xt_band_count_kernel(XbSets sets, 
 }
 
 // ============================================================================ compact iteration
-constexpr int XE_S = 32;                     // rows per slice = chain lanes
-constexpr int XE_P = 8;                      // product waves
-constexpr int XE_KC = 64;                    // entries per row per chunk
-constexpr int XE_CT = 64;                    // counts whose quotient is tabulated
+constexpr int XE_S = 32;                     // rows per workgroup (slice) = chain lanes
+constexpr int XE_P = 8;                      // product waves: rows p, p + 8, p + 16, p + 24
+constexpr int XE_RPW = XE_S / XE_P;          // rows per product wave
+constexpr int XE_KC = 128;                   // entries per row per chunk
+constexpr int XE_PAIRS = XE_RPW / 2;         // row pairs per product wave (a 16-B load per pair)
+constexpr int XE_PITCH = XE_KC + 2;          // prod row pitch (doubles): 16-B aligned rows whose
+                                             // 16-B chain reads hit every bank once per 16 lanes
+constexpr int XE_CT_MAX = 256;               // counts whose quotient is tabulated: CT = the largest
+                                             // power of two <= 256 whose table fits next to x
+#ifndef SA_XE_DEPTH
+#define SA_XE_DEPTH 4                        // chunks of entries in flight per product lane
+#endif
+#ifndef SA_XE_NTL
+#define SA_XE_NTL 0                          // 1: non-temporal entry loads
+#endif
+constexpr int XE_DEPTH = SA_XE_DEPTH;
 constexpr int XE_THREADS = (XE_P + 1) * 64;  // + the chain wave
-constexpr int XE_XMAX = 10240;               // x (C doubles) staged in LDS
-constexpr int XE_BUILD_THREADS = 1024;
+constexpr int XE_XMAX = 9472;                // x (C doubles) staged in LDS
+constexpr int XE_BUILD_ROWS = 16;            // build: rows per workgroup (one wave each)
 constexpr uint32_t XE_CNT_ESC = 0xFFFFu;     // count >= 65535: read from the dense row
-static_assert(XE_KC * XE_S == 4 * XE_P * 64, "one 16-B entry quad per product lane per chunk");
-static_assert(XE_THREADS <= 1024 && XE_S <= 64 && (XE_S & 3) == 0, "xt_iter_ell_kernel shape");
-static_assert((size_t)XE_XMAX * 8 + (XE_CT + 2 * XE_KC + 1) * XE_S * 8 <= 160 * 1024, "xt_iter_ell_kernel LDS");
+#ifndef SA_XE_PROBE
+#define SA_XE_PROBE 0  // diagnostic builds (wrong values): 1 = no products, 2 = no chain adds,
+#endif                 // 4 = idle product waves (no loads, no LDS writes)
+static_assert(XE_KC == 128 && XE_PAIRS * 2 * XE_P == XE_S, "xt_iter_ell_kernel shape: 32 lanes x 4 entries per row chunk");
+static_assert(XE_THREADS <= 1024 && XE_S <= 64, "xt_iter_ell_kernel shape");
+constexpr size_t XE_LDS_STATIC = (size_t)XE_S * (2 * XE_PITCH + 1) * 8 + XE_S * 4;
+constexpr size_t XE_LDS_MAX = 160 * 1024;
+static_assert((size_t)XE_XMAX * 8 + (size_t)XE_S * 16 * 8 + XE_LDS_STATIC <= XE_LDS_MAX,
+              "xt_iter_ell_kernel LDS: x and a 16-count quotient table");
+static_assert(XE_DEPTH >= 1 && XE_DEPTH <= 8, "SA_XE_DEPTH");
 
-// Compact form of rows [0, nrows) of a count block (row i at cnt_rows + i*C): slice s = rows
-// [32 s, 32 s + 32) at ell + s * 32 * C (room for a dense slice); entry k of row i (the row's
-// k-th non-zero count in column order, column | min(count, 0xFFFF) << 16) at k * 32 + i; every
-// row padded with 0 entries to slice_len[s] = the slice's longest row.
-__global__ __launch_bounds__(XE_BUILD_THREADS) void xt_ell_build_kernel(const int32_t* __restrict__ cnt_rows, int C,
-                                                                        int nrows, uint32_t* __restrict__ ell,
-                                                                        int32_t* __restrict__ slice_len) {
-  __shared__ int lens[XE_S];
-  __shared__ int mx;
-  const int s = blockIdx.x, row0 = s * XE_S;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  constexpr int NW = XE_BUILD_THREADS / 64;
-  uint32_t* E = ell + (int64_t)s * XE_S * C;
-  for (int i = wv; i < XE_S; i += NW) {
-    const int r = row0 + i;
-    int base = 0;
-    if (r < nrows) {
-      const int32_t* row = cnt_rows + (int64_t)r * C;
-      for (int c0 = 0; c0 < C; c0 += 64 * 8) {
-        int32_t v[8];
+// Compact form of rows [0, nrows) of a count block (row i at cnt_rows + i*C): row i's non-zero
+// counts in column order, column | min(count, 0xFFFF) << 16, at ell[i*pe + k] (pe = C rounded up
+// to a multiple of 4: room for a dense row, 16-byte aligned rows), and their number at row_len[i].  One wave per row: 8 loads of 64 columns in flight,
+// ballot + mbcnt, so each instruction stores one contiguous run.
+__global__ __launch_bounds__(XE_BUILD_ROWS * 64) void xt_ell_build_kernel(const int32_t* __restrict__ cnt_rows, int C,
+                                                                          int nrows, uint32_t* __restrict__ ell,
+                                                                          int32_t* __restrict__ row_len) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * XE_BUILD_ROWS + (threadIdx.x >> 6);
+  if (r >= nrows) return;  // whole wave
+  const int32_t* row = cnt_rows + (int64_t)r * C;
+  uint32_t* E = ell + (int64_t)r * ((C + 3) & ~3);  // rows 16-byte aligned
+  int base = 0;
+  for (int c0 = 0; c0 < C; c0 += 64 * 8) {
+    int32_t v[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const int c = c0 + 64 * u + lane;
-          v[u] = c < C ? row[c] : 0;
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const uint64_t m = __ballot(v[u] != 0);
-          if (v[u] != 0) {
-            const uint32_t cnt = (uint32_t)v[u] < XE_CNT_ESC ? (uint32_t)v[u] : XE_CNT_ESC;
-            E[(int64_t)(base + (int)lane_rank(m)) * XE_S + i] = (uint32_t)(c0 + 64 * u + lane) | (cnt << 16);
-          }
-          base += (int)__popcll(m);
-        }
-      }
+    for (int u = 0; u < 8; ++u) {
+      const int c = c0 + 64 * u + lane;
+      v[u] = c < C ? __builtin_nontemporal_load(row + c) : 0;
     }
-    if (lane == 0) lens[i] = base;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const uint64_t m = __ballot(v[u] != 0);
+      if (v[u] != 0) {
+        const uint32_t cnt = (uint32_t)v[u] < XE_CNT_ESC ? (uint32_t)v[u] : XE_CNT_ESC;
+        E[base + (int)lane_rank(m)] = (uint32_t)(c0 + 64 * u + lane) | (cnt << 16);
+      }
+      base += (int)__popcll(m);
+    }
   }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int m = 0;
-    for (int i = 0; i < XE_S; ++i) m = max(m, lens[i]);
-    mx = m;
-    slice_len[s] = m;
-  }
-  __syncthreads();
-  for (int i = wv; i < XE_S; i += NW)
-    for (int k = lens[i] + lane; k < mx; k += 64) E[(int64_t)k * XE_S + i] = 0u;
+  if (lane == 0) row_len[r] = base;
 }
 
 // One iteration of rows [rb, rb + nrows) from their compact form (xt_ell_build_kernel of the same
 // rows; cnt_rows: the dense rows, read only for counts >= 65535): xo[i] = gs + pmove * sum over
 // the row's non-zero columns c, in column order, of (cnt / move[r]) * x[c] -- xt_iter_kernel's
 // operations (sa_xt.hip), without its per-chunk compaction of the dense rows.  One workgroup per
-// slice; per chunk of 64 entries per row the product waves write the 64 x 32 products to LDS and
-// the chain wave (lane = row) adds them in order, one barrier per chunk, two buffers.
+// slice of 32 rows.  Per chunk of KC entries per row, each product wave loads its 4 rows'
+// entries (256 contiguous bytes per load; DEPTH - 1 chunks ahead), forms the products -- the
+// quotient from a per-row LDS table for counts < ct, else the same division -- and writes them
+// to prod[row][k]; the
+// chain wave (lane = row) then adds its row's products strictly in order.  One barrier per
+// chunk, two buffers; rows shorter than the slice's longest add +0 terms (exact: the sums are
+// non-negative).
 __global__ __launch_bounds__(XE_THREADS) void xt_iter_ell_kernel(const uint32_t* __restrict__ ell,
-                                                                 const int32_t* __restrict__ slice_len,
+                                                                 const int32_t* __restrict__ row_len,
                                                                  const int32_t* __restrict__ cnt_rows,
                                                                  const unsigned long long* __restrict__ move,
                                                                  const double* __restrict__ gs,
                                                                  const double* __restrict__ pmove, int C, int rb,
-                                                                 int nrows, double eps, const double* __restrict__ x,
+                                                                 int nrows, int ct, double eps,
+                                                                 const double* __restrict__ x,
                                                                  double* __restrict__ xo, const int32_t* flag_prev,
                                                                  int32_t* __restrict__ flag_out) {
   if (flag_prev && __hip_atomic_load(flag_prev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
-  extern __shared__ __attribute__((aligned(16))) double xs[];  // [C]
-  __shared__ double tq[XE_CT * XE_S];                          // tq[q * S + i] = q / move[row i]
-  __shared__ double prod[2][XE_KC * XE_S];
+  extern __shared__ __attribute__((aligned(16))) double xs[];  // [C] x, then tq [S][ct]
+  double* tq = xs + C;                                         // tq[i * ct + q] = q / move[row i]
+  __shared__ double prod[2][XE_S * XE_PITCH];
   __shared__ double mvs[XE_S];
-  const int s = blockIdx.x, row0 = s * XE_S, nr = min(XE_S, nrows - row0);
-  const int len = slice_len[s];
+  __shared__ int lens[XE_S];
+  const int row0 = blockIdx.x * XE_S, nr = min(XE_S, nrows - row0);
+  const int pe = (C + 3) & ~3;  // the compact rows' pitch (16-byte aligned rows)
   for (int c = threadIdx.x; c < C; c += XE_THREADS) xs[c] = x[c];
-  for (int e = threadIdx.x; e < XE_CT * XE_S; e += XE_THREADS) {
-    const int q = e / XE_S, i = e % XE_S;
+  for (int e = threadIdx.x; e < XE_S * ct; e += XE_THREADS) {
+    const int i = e / ct, q = e % ct;
     const double mv = i < nr ? (double)move[rb + row0 + i] : 1.0;
     tq[e] = q == 0 ? 0.0 : (double)q / mv;  // a count of 0 is a zero term (T = 0)
-    if (q == 0) mvs[i] = mv;
+    if (q == 0) {
+      mvs[i] = mv;
+      lens[i] = i < nr ? row_len[row0 + i] : 0;
+    }
   }
   __syncthreads();
-  const uint32_t* E = ell + (int64_t)s * XE_S * C;
-  const int nch = (len + XE_KC - 1) / XE_KC;
-  const int wv = threadIdx.x >> 6;
-  if (wv < XE_P) {  // ---- product waves: quad t = entries (k = t / 8, rows 4 (t % 8) .. + 3) of a chunk
-    const int t = threadIdx.x, kk = t >> 3, i0 = (t & 7) * 4;
-    auto ld = [&](int j) -> u32x4 {
-      const int k = j * XE_KC + kk;
-      return k < len ? *reinterpret_cast<const u32x4*>(E + (int64_t)k * XE_S + i0) : u32x4{0, 0, 0, 0};
-    };
-    u32x4 qa = ld(0), qb = ld(1);
-    asm volatile("" ::: "memory");
-    for (int j = 0; j < nch; ++j) {
-      const u32x4 q = qa;
-      qa = qb;
-      qb = ld(j + 2);  // two chunks ahead (past the end: zero, no load)
-      asm volatile("" ::: "memory");
-      double* pr = prod[j & 1] + kk * XE_S + i0;
+  int len = 0;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const uint32_t e = q[u], cnt = e >> 16, col = e & 0xFFFFu;
-        SA_DGUARD((int)col < C, col, continue);
-        double tv;
-        if (cnt < (uint32_t)XE_CT) {
-          tv = tq[cnt * XE_S + i0 + u];
-        } else {
-          const int32_t c32 = cnt == XE_CNT_ESC ? cnt_rows[(int64_t)(row0 + i0 + u) * C + col] : (int32_t)cnt;
-          tv = (double)c32 / mvs[i0 + u];
-        }
-        pr[u] = tv * xs[col];
+  for (int i = 0; i < XE_S; ++i) len = max(len, lens[i]);
+  const int nch = (len + XE_KC - 1) / XE_KC;
+  const int nchp = (nch + XE_DEPTH - 1) / XE_DEPTH * XE_DEPTH;  // chunks past nch: +0 terms
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (wv < XE_P) {  // ---- product waves
+#if SA_XE_PROBE & 4
+    for (int j = 0; j < nchp; ++j) __syncthreads();
+    return;
+#endif
+    // wave wv owns rows wv + 8 q (q < 4) as two pairs: half = lane / 32 takes row
+    // wv + 8 (2 p + half) of pair p, a lane 4 consecutive entries of it per chunk (one 16-B load:
+    // a wave instruction fetches 1 KiB, two rows' chunks)
+    const int half = lane >> 5, k4 = 4 * (lane & 31);
+    const uint32_t* Er[XE_PAIRS];
+    int lr[XE_PAIRS], ir[XE_PAIRS];
+#pragma unroll
+    for (int p = 0; p < XE_PAIRS; ++p) {
+      const int i = wv + XE_P * (2 * p + half);
+      ir[p] = i;
+      Er[p] = ell + (int64_t)(row0 + min(i, nr - 1)) * pe;
+      lr[p] = lens[i];
+    }
+    // DEPTH register slots of entries, slot d holding chunk j with j % DEPTH == d: the loop is
+    // unrolled by DEPTH so a slot's loads are refilled right after its products are formed and
+    // no register is copied while its load is in flight (a copy waits for the load); loads are
+    // unconditional from clamped addresses, entries past a row's end zeroed at their use
+    u32x4 e[XE_DEPTH][XE_PAIRS];
+    auto ld = [&](u32x4 (&d)[XE_PAIRS], int j) {
+#pragma unroll
+      for (int p = 0; p < XE_PAIRS; ++p) {
+        const int k = min(j * XE_KC + k4, pe - 4);
+#if SA_XE_NTL
+        d[p] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(Er[p] + k));
+#else  // default policy: the compact rows (~70 MB at cfg5) stay in the Infinity Cache across iterations
+        d[p] = *reinterpret_cast<const u32x4*>(Er[p] + k);
+#endif
       }
-      __syncthreads();
+    };
+    auto products = [&](const u32x4 (&E)[XE_PAIRS], int j) {
+      double* pr = prod[j & 1];
+      // every LDS read of the chunk first (the quotient from the table at min(cnt, ct - 1), x at
+      // the column; entries past a row's end are 0: T = 0, x[0]), then the rare counts >= ct,
+      // then the products: no branch between a read and its use, so the reads overlap
+      double tv[XE_PAIRS][4], xv[XE_PAIRS][4];
+      uint32_t en[XE_PAIRS][4];
+      bool big = false;
+#pragma unroll
+      for (int p = 0; p < XE_PAIRS; ++p)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          en[p][u] = j * XE_KC + k4 + u < lr[p] ? E[p][u] : 0u;
+          const uint32_t cnt = en[p][u] >> 16, col = en[p][u] & 0xFFFFu;
+          SA_DCHECK((int)col < C, col);
+          tv[p][u] = tq[ir[p] * ct + min(cnt, (uint32_t)ct - 1u)];
+          xv[p][u] = xs[col < (uint32_t)C ? col : 0u];
+          big |= cnt >= (uint32_t)ct;
+        }
+      if (__builtin_expect(__ballot(big) != 0, 0)) {
+#pragma unroll
+        for (int p = 0; p < XE_PAIRS; ++p)
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const uint32_t cnt = en[p][u] >> 16, col = en[p][u] & 0xFFFFu;
+            if (cnt >= (uint32_t)ct) {
+              const int32_t c32 = cnt == XE_CNT_ESC ? cnt_rows[(int64_t)(row0 + ir[p]) * C + col] : (int32_t)cnt;
+              tv[p][u] = (double)c32 / mvs[ir[p]];
+            }
+          }
+      }
+#pragma unroll
+      for (int p = 0; p < XE_PAIRS; ++p) {
+        f64x2 v0, v1;
+#if SA_XE_PROBE & 1
+        v0 = f64x2{0.0 * tv[p][0], 0.0 * tv[p][1]};
+        v1 = f64x2{0.0 * tv[p][2], 0.0 * tv[p][3]};
+#else
+        v0 = f64x2{tv[p][0] * xv[p][0], tv[p][1] * xv[p][1]};
+        v1 = f64x2{tv[p][2] * xv[p][2], tv[p][3] * xv[p][3]};
+#endif
+        f64x2* dst = reinterpret_cast<f64x2*>(pr + ir[p] * XE_PITCH + k4);
+        dst[0] = v0;
+        dst[1] = v1;
+      }
+    };
+#pragma unroll
+    for (int d = 0; d < XE_DEPTH; ++d) ld(e[d], d);
+    asm volatile("" ::: "memory");
+    for (int j0 = 0; j0 < nchp; j0 += XE_DEPTH) {
+#pragma unroll
+      for (int d = 0; d < XE_DEPTH; ++d) {
+        products(e[d], j0 + d);
+        ld(e[d], j0 + d + XE_DEPTH);  // past the last chunk: harmless clamped re-reads
+        asm volatile("" ::: "memory");
+        __syncthreads();
+      }
     }
   } else {  // ---- chain wave: lane i adds row i's products strictly left to right
-    const int i = threadIdx.x & (XE_S - 1);
+    // the critical path of the launch (the longest row's adds): first claim on its SIMD's issue
+    // slots over the two product waves sharing it (MI355X_MICROARCH.md: priority, then age)
+    __builtin_amdgcn_s_setprio(3);
+    const int i = lane & (XE_S - 1);
     double acc = 0.0;
-    for (int j = 0; j < nch; ++j) {
+    for (int j = 0; j < nchp; ++j) {
       __syncthreads();
-      const double* pr = prod[j & 1] + i;
-      double v[XE_KC];
+      const f64x2* pr = reinterpret_cast<const f64x2*>(prod[j & 1] + i * XE_PITCH);
+#if !(SA_XE_PROBE & 2)
+      constexpr int G = 16;  // 16-B reads (two products each) issued a group ahead of their adds
+      f64x2 v[G];
 #pragma unroll
-      for (int k = 0; k < XE_KC; ++k) v[k] = pr[k * XE_S];
+      for (int k = 0; k < G; ++k) v[k] = pr[k];
 #pragma unroll
-      for (int k = 0; k < XE_KC; ++k) acc = acc + v[k];
+      for (int k0 = 0; k0 < XE_KC / 2; k0 += G) {
+        f64x2 nx[G];
+#pragma unroll
+        for (int k = 0; k < G; ++k) nx[k] = k0 + G + k < XE_KC / 2 ? pr[k0 + G + k] : f64x2{0.0, 0.0};
+#pragma unroll
+        for (int k = 0; k < G; ++k) {
+          acc = acc + v[k][0];
+          acc = acc + v[k][1];
+        }
+#pragma unroll
+        for (int k = 0; k < G; ++k) v[k] = nx[k];
+      }
+#else
+      acc += pr[0][0];
+#endif
     }
-    const int lane = threadIdx.x & 63;
     if (lane < nr) {
       const int rr = rb + row0 + lane;
       const double mv = pmove[rr] * acc;
@@ -563,7 +707,7 @@ static bool xt_band_shape(int C, XbShape* s) {
   if (C < 1 || C + 3 > 65536) return false;
   const int P = (C + 3 + 3) & ~3;
   int rmax = (int)(XB_LDS_MAX / ((size_t)P * 4));
-  if (rmax > XB_MAX_ROWS) rmax = XB_MAX_ROWS;
+  if (rmax > SA_XB_RMAX) rmax = SA_XB_RMAX;
   if (rmax < 1) return false;
   int r = C / 256;
   if (r < 1) r = 1;
@@ -596,12 +740,15 @@ static int bucket_batch(const sa_actions& A, const uint32_t* cells, int64_t n, i
   if (!rc) {
     sa_actions none;
     memset(&none, 0, sizeof(none));
+    const sa_frame& F = A.frames[0];
+    const int vec = !cells && n >= 2 && aligned16(F.c0) && aligned16(F.c1) && aligned16(F.c2) && aligned16(F.c3) &&
+                    ((uintptr_t)F.type_id & 1u) == 0 && ((uintptr_t)F.result_id & 1u) == 0;
     if (cells)
       hipLaunchKernelGGL((xt_keys_kernel<true>), dim3((unsigned)regions), dim3(XK_THREADS), (size_t)S.NB * 4, st, none,
-                         cells, n, l, w, S, keys, region_cnt, band_cnt, err, XkRate{nullptr, nullptr, 0, 0});
+                         cells, n, l, w, S, keys, region_cnt, band_cnt, err, XkRate{nullptr, nullptr, 0, 0}, 0);
     else
       hipLaunchKernelGGL((xt_keys_kernel<false>), dim3((unsigned)regions), dim3(XK_THREADS), (size_t)S.NB * 4, st, A,
-                         nullptr, n, l, w, S, keys, region_cnt, band_cnt, err, RO);
+                         nullptr, n, l, w, S, keys, region_cnt, band_cnt, err, RO, vec);
     rc = check_launch("xt_keys_kernel");
   }
   if (!rc) {
@@ -619,8 +766,9 @@ static int bucket_batch(const sa_actions& A, const uint32_t* cells, int64_t n, i
 }
 
 static int count_from_buckets(int nsets, const uint32_t* const* buckets, const int64_t* const* band_off,
-                              const XbShape& S, int64_t* shot, int64_t* goal, int64_t* move, int32_t* trans,
-                              int overwrite, hipStream_t st) {
+                              const XbShape& S, int band0, int nbands, int64_t* shot, int64_t* goal, int64_t* move,
+                              int32_t* trans, int overwrite, hipStream_t st) {
+  if (nbands <= 0) return SA_OK;
   const int vec = (S.C % 4 == 0) && aligned16(trans);
   const size_t lds = (size_t)S.R * S.P * 4;
   for (int s0 = 0; s0 < nsets || (s0 == 0 && nsets == 0); s0 += XB_MAX_SETS) {
@@ -632,7 +780,7 @@ static int count_from_buckets(int nsets, const uint32_t* const* buckets, const i
       sets.off[k] = band_off[s0 + k];
     }
     // later launches add to what the first one wrote
-    hipLaunchKernelGGL(xt_band_count_kernel, dim3((unsigned)S.NB), dim3(XB_THREADS), lds, st, sets, S,
+    hipLaunchKernelGGL(xt_band_count_kernel, dim3((unsigned)nbands), dim3(XB_THREADS), lds, st, sets, S, band0,
                        reinterpret_cast<unsigned long long*>(shot), reinterpret_cast<unsigned long long*>(goal),
                        reinterpret_cast<unsigned long long*>(move), trans, (overwrite && s0 == 0) ? 1 : 0, vec);
     int rc = check_launch("xt_band_count_kernel");
@@ -658,7 +806,7 @@ int xt_count_bands(const sa_actions& A, const uint32_t* cells, int64_t n, int l,
   if (!rc) {
     const uint32_t* bk[1] = {buckets};
     const int64_t* bo[1] = {band_off};
-    rc = count_from_buckets(1, bk, bo, S, shot, goal, move, trans, 0, st);
+    rc = count_from_buckets(1, bk, bo, S, 0, S.NB, shot, goal, move, trans, 0, st);
   }
   scratch_release(sc, st);
   return rc;
@@ -666,25 +814,23 @@ int xt_count_bands(const sa_actions& A, const uint32_t* cells, int64_t n, int l,
 
 // Compact form + iteration used by sa_xt_solve for C > SA_XT_SOLVE_MAX_C.
 bool xt_compact_ok(int C) { return C >= 1 && C <= XE_XMAX; }
-size_t xt_compact_bytes(int C, int nrows) {
-  const size_t ns = (size_t)(nrows + XE_S - 1) / XE_S;
-  return ns * XE_S * (size_t)C * 4;
-}
-int xt_compact_build(const int32_t* cnt_rows, int C, int nrows, uint32_t* ell, int32_t* slice_len, hipStream_t st) {
-  const int ns = (nrows + XE_S - 1) / XE_S;
-  if (ns == 0) return SA_OK;
-  hipLaunchKernelGGL(xt_ell_build_kernel, dim3((unsigned)ns), dim3(XE_BUILD_THREADS), 0, st, cnt_rows, C, nrows, ell,
-                     slice_len);
+size_t xt_compact_bytes(int C, int nrows) { return (size_t)(nrows > 0 ? nrows : 0) * (size_t)((C + 3) & ~3) * 4; }
+int xt_compact_build(const int32_t* cnt_rows, int C, int nrows, uint32_t* ell, int32_t* row_len, hipStream_t st) {
+  if (nrows <= 0) return SA_OK;
+  hipLaunchKernelGGL(xt_ell_build_kernel, dim3((unsigned)((nrows + XE_BUILD_ROWS - 1) / XE_BUILD_ROWS)),
+                     dim3(XE_BUILD_ROWS * 64), 0, st, cnt_rows, C, nrows, ell, row_len);
   return check_launch("xt_ell_build_kernel");
 }
-int xt_compact_iterate(const uint32_t* ell, const int32_t* slice_len, const int32_t* cnt_rows, const int64_t* move,
+int xt_compact_iterate(const uint32_t* ell, const int32_t* row_len, const int32_t* cnt_rows, const int64_t* move,
                        const double* gs, const double* pmove, int C, int rb, int nrows, const double* x, double eps,
                        double* xo, const int32_t* flag_prev, int32_t* flag_out, hipStream_t st) {
   const int ns = (nrows + XE_S - 1) / XE_S;
   if (ns == 0) return SA_OK;
-  hipLaunchKernelGGL(xt_iter_ell_kernel, dim3((unsigned)ns), dim3(XE_THREADS), (size_t)C * 8, st, ell, slice_len,
-                     cnt_rows, reinterpret_cast<const unsigned long long*>(move), gs, pmove, C, rb, nrows, eps, x, xo,
-                     flag_prev, flag_out);
+  int ct = XE_CT_MAX;  // the quotient table: as many counts as fit next to x
+  while (ct > 16 && (size_t)C * 8 + (size_t)XE_S * ct * 8 + XE_LDS_STATIC > XE_LDS_MAX) ct >>= 1;
+  hipLaunchKernelGGL(xt_iter_ell_kernel, dim3((unsigned)ns), dim3(XE_THREADS), ((size_t)C + (size_t)XE_S * ct) * 8, st,
+                     ell, row_len, cnt_rows, reinterpret_cast<const unsigned long long*>(move), gs, pmove, C, rb,
+                     nrows, ct, eps, x, xo, flag_prev, flag_out);
   return check_launch("xt_iter_ell_kernel");
 }
 }  // namespace sa
@@ -742,29 +888,48 @@ extern "C" int sa_xt_count_from_buckets(int32_t nsets, const uint32_t* const* bu
   if (!shot || !goal || !move || !trans) return fail(SA_EINVAL, "null count buffer");
   if (flags & ~SA_XT_COUNT_OVERWRITE) return fail(SA_EINVAL, "unknown flags");
   if (nsets == 0 && !(flags & SA_XT_COUNT_OVERWRITE)) return SA_OK;
-  return count_from_buckets(nsets, buckets, band_off, S, shot, goal, move, trans,
+  return count_from_buckets(nsets, buckets, band_off, S, 0, S.NB, shot, goal, move, trans,
+                            (flags & SA_XT_COUNT_OVERWRITE) != 0, (hipStream_t)stream);
+}
+
+extern "C" int sa_xt_count_band_rows(int32_t nsets, const uint32_t* const* buckets, const int64_t* const* band_off,
+                                     int32_t l, int32_t w, int32_t band0, int32_t nbands, int64_t* shot_rows,
+                                     int64_t* goal_rows, int64_t* move_rows, int32_t* trans_rows, int32_t flags,
+                                     void* stream) {
+  if (l < 1 || w < 1 || (int64_t)l * w > 46340) return fail(SA_EINVAL, "bad l or w");
+  XbShape S;
+  if (!xt_band_shape(l * w, &S)) return fail(SA_EINVAL, "the band-owned count does not hold %d cells", l * w);
+  if (band0 < 0 || nbands < 0 || band0 + nbands > S.NB) return fail(SA_EINVAL, "band range outside [0, %d)", S.NB);
+  if (nsets < 0 || (nsets > 0 && (!buckets || !band_off))) return fail(SA_EINVAL, "bad bucket sets");
+  for (int k = 0; k < nsets; ++k)
+    if (!band_off[k]) return fail(SA_EINVAL, "null band offsets");
+  if (nbands > 0 && (!shot_rows || !goal_rows || !move_rows || !trans_rows))
+    return fail(SA_EINVAL, "null count buffer");
+  if (flags & ~SA_XT_COUNT_OVERWRITE) return fail(SA_EINVAL, "unknown flags");
+  if (nsets == 0 && !(flags & SA_XT_COUNT_OVERWRITE)) return SA_OK;
+  return count_from_buckets(nsets, buckets, band_off, S, band0, nbands, shot_rows, goal_rows, move_rows, trans_rows,
                             (flags & SA_XT_COUNT_OVERWRITE) != 0, (hipStream_t)stream);
 }
 
 extern "C" int sa_xt_compact_rows(const int32_t* cnt_rows, int32_t C, int32_t nrows, uint32_t* ell,
-                                  int32_t* slice_len, void* stream) {
+                                  int32_t* row_len, void* stream) {
   if (!xt_compact_ok(C) || nrows < 0) return fail(SA_EINVAL, "the compact form takes 1 <= C <= %d", XE_XMAX);
-  if (nrows > 0 && (!cnt_rows || !ell || !slice_len)) return fail(SA_EINVAL, "null pointer");
+  if (nrows > 0 && (!cnt_rows || !ell || !row_len)) return fail(SA_EINVAL, "null pointer");
   if (nrows > 0 && !aligned16(ell)) return fail(SA_EINVAL, "ell must be 16-byte aligned");
-  return xt_compact_build(cnt_rows, C, nrows, ell, slice_len, (hipStream_t)stream);
+  return xt_compact_build(cnt_rows, C, nrows, ell, row_len, (hipStream_t)stream);
 }
 
-extern "C" int sa_xt_iterate_compact(const uint32_t* ell, const int32_t* slice_len, const int32_t* cnt_rows,
+extern "C" int sa_xt_iterate_compact(const uint32_t* ell, const int32_t* row_len, const int32_t* cnt_rows,
                                      const int64_t* move, const double* gs, const double* pmove, int32_t C, int32_t r0,
                                      int32_t nrows, const double* x, double eps, double* x_next_rows,
                                      const int32_t* flag_prev, int32_t* flag_out, void* stream) {
   if (!xt_compact_ok(C)) return fail(SA_EINVAL, "the compact form takes 1 <= C <= %d", XE_XMAX);
   if (r0 < 0 || nrows < 0 || r0 + nrows > C) return fail(SA_EINVAL, "row range outside [0, C)");
   if (!move || !gs || !pmove || !x || !flag_out ||
-      (nrows > 0 && (!ell || !slice_len || !cnt_rows || !x_next_rows)))
+      (nrows > 0 && (!ell || !row_len || !cnt_rows || !x_next_rows)))
     return fail(SA_EINVAL, "null xt iteration pointer");
   if (nrows > 0 && !aligned16(ell)) return fail(SA_EINVAL, "ell must be 16-byte aligned");
-  return xt_compact_iterate(ell, slice_len, cnt_rows, move, gs, pmove, C, r0, nrows, x, eps, x_next_rows, flag_prev,
+  return xt_compact_iterate(ell, row_len, cnt_rows, move, gs, pmove, C, r0, nrows, x, eps, x_next_rows, flag_prev,
                             flag_out, (hipStream_t)stream);
 }
 

@@ -90,6 +90,26 @@ def _all_gather(out: torch.Tensor, inp: torch.Tensor, group=None) -> None:
         out.copy_(torch.cat(parts))
 
 
+def _all_to_all(out: torch.Tensor, inp: torch.Tensor, out_splits=None, in_splits=None,
+                group=None) -> None:
+    """out = the concatenation over ranks q of the part of q's ``inp`` meant for this rank
+    (``in_splits`` / ``out_splits``: element counts per rank; None: equal parts)."""
+    import torch.distributed as dist
+    if _on_device(group):
+        dist.all_to_all_single(out, inp, out_splits, in_splits, group=group)
+    else:
+        h = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_to_all_single(h, inp.cpu(), out_splits, in_splits, group=group)
+        out.copy_(h)
+
+
+def band_ranges(n_bands: int, world: int) -> List[Tuple[int, int]]:
+    """Bands [b0, b1) owned by each rank in the band-sharded fit: ceil(NB / world) consecutive
+    bands per rank (the last ranks may own fewer, or none)."""
+    per = -(-n_bands // world)
+    return [(min(n_bands, q * per), min(n_bands, (q + 1) * per)) for q in range(world)]
+
+
 def xt_solve_sharded(acc, eps: float = 1e-5, max_iter: int = 1000, group=None, batch: int = 8):
     """Row-sharded xT fit over the ranks of ``group``: each rank passes
     its OWN shard's counts (``ops.xt_zero_counts(..., row_blocks=world)`` + ``ops.xt_count``).
@@ -99,7 +119,7 @@ def xt_solve_sharded(acc, eps: float = 1e-5, max_iter: int = 1000, group=None, b
     2. reduce-scatter of the C x C transition counts by row blocks: rank r keeps the summed
        count rows [r*B, (r+1)*B), B = ceil(C / world) (half the traffic of an all-reduce);
     3. per iteration, each rank updates its B rows (``sa_xt_iterate_compact`` over the compact
-       form of its rows built once, ``sa_xt_iterate_rows`` above 10240 cells; the reference's
+       form of its rows built once, ``sa_xt_iterate_rows`` above 9472 cells; the reference's
        summation order, so every value is bit-identical to the single-GPU solve) into one
        persistent B-row buffer, and one all-gather of those buffers rebuilds the full x on
        every rank;
@@ -109,12 +129,7 @@ def xt_solve_sharded(acc, eps: float = 1e-5, max_iter: int = 1000, group=None, b
     Returns ``(mats [4, C] = scoring | shot | move | xT, heatmaps [n_iter + 1, C], n_iter)``;
     the normalised C x C transition matrix is never materialised on this path.
     """
-    import ctypes
-
     import torch.distributed as dist
-
-    from . import _native
-    from .batch import stream_handle
     _check_world(group)
     W = dist.get_world_size(group)
     r = dist.get_rank(group)
@@ -127,6 +142,20 @@ def xt_solve_sharded(acc, eps: float = 1e-5, max_iter: int = 1000, group=None, b
     shot, goal, move = acc.shot, acc.goal, acc.move
     rows = torch.empty(B * C, dtype=torch.int32, device=dev)
     _reduce_scatter(rows, acc.trans_padded, group=group)
+    return _solve_row_block(rows, shot, goal, move, C, B, eps, max_iter, group, batch)
+
+
+def _solve_row_block(rows, shot, goal, move, C: int, B: int, eps: float, max_iter: int, group,
+                     batch: int):
+    """The row-sharded value iteration: this rank holds the summed count rows [r B, r B + B)
+    (``rows``, B x C int32) and the full shot / goal / move vectors."""
+    import torch.distributed as dist
+
+    from . import _native
+    from .batch import stream_handle
+    W = dist.get_world_size(group)
+    r = dist.get_rank(group)
+    dev = rows.device
     lib = _native.lib()
     mats = torch.empty((4, C), dtype=torch.float64, device=dev)
     gp = torch.empty((2, C), dtype=torch.float64, device=dev)
@@ -143,7 +172,7 @@ def xt_solve_sharded(acc, eps: float = 1e-5, max_iter: int = 1000, group=None, b
     if compact:
         ell = torch.empty(max(int(lib.sa_xt_compact_bytes(C, nrows)) // 4, 4), dtype=torch.int32,
                           device=dev)
-        slen = torch.empty(max(-(-nrows // 32), 1), dtype=torch.int32, device=dev)
+        slen = torch.empty(max(nrows, 1), dtype=torch.int32, device=dev)  # row lengths
         _native.check(lib.sa_xt_compact_rows(ptr(rows), C, nrows, ptr(ell), ptr(slen),
                                              stream_handle()))
     iters = -1
@@ -173,3 +202,115 @@ def xt_solve_sharded(acc, eps: float = 1e-5, max_iter: int = 1000, group=None, b
         raise RuntimeError(f'xT value iteration did not converge within {max_iter} iterations')
     mats[3].copy_(heat[iters, :C])
     return mats, heat[:iters + 1, :C], iters
+
+
+def xt_fit_bands_sharded(batches, l: int, w: int, eps: float = 1e-5, max_iter: int = 1000,
+                         group=None, batch: int = 8, interp_codes=None):
+    """Band-sharded xT fit (cfg5 over several GPUs) for grids the band-owned count holds
+    (``ops.xt_band_shape``, e.g. 105 x 68): the ranks exchange their COUNTED ACTIONS, not count
+    tables.  Rank r owns the start-cell bands [b0, b1) = ``band_ranges(NB, world)[r]``, i.e.
+    the count rows [b0 R, b1 R).
+
+    1. every rank buckets its own batches (``sa_xt_count_bucket``: one 4-B key per counted
+       action, sorted by band, so each destination's keys are one contiguous range);
+    2. one all-to-all of the keys (about 3.4 B per action: ~37 MB per rank at 1e8 actions over 8
+       ranks, against 204 MB x 2 (W-1) / W for the table's all-reduce) and one of the band offsets;
+    3. each rank counts its own bands from every rank's keys (``sa_xt_count_band_rows``: the B x C
+       rows written once from LDS, no global atomics) -- the same row block the reduce-scatter of
+       ``xt_solve_sharded`` would leave it;
+    4. one all-gather of the shot / goal / move counts of every rank's rows and a max all-reduce
+       of the error flags;
+    5. the row-sharded value iteration of ``xt_solve_sharded`` (compact rows, one all-gather of x
+       per iteration): every value bit-identical to the single-GPU fit of all ranks' actions.
+
+    ``interp_codes``: one ``ops.xt_interp_codes_buffer`` per batch, filled for the rate.
+    Returns ``(mats [4, C], heatmaps [n_iter + 1, C], n_iter, err)``; ``err`` is the error-flag
+    word of ``sa_xt_count`` (check with ``ops.xt_check_errors(types.SimpleNamespace(err=err))``).
+    """
+    import ctypes
+
+    import torch.distributed as dist
+
+    from . import _native, ops
+    from .batch import stream_handle
+    _check_world(group)
+    shape = ops.xt_band_shape(l, w)
+    if shape is None:
+        raise ValueError(f'the band-owned count does not take a {l} x {w} grid')
+    R, NB = shape
+    C = l * w
+    W = dist.get_world_size(group)
+    r = dist.get_rank(group)
+    ranges = band_ranges(NB, W)
+    per = -(-NB // W)  # bands per rank (equal row blocks for the iteration's all-gather)
+    B = per * R
+    b0, b1 = ranges[r]
+    dev = batches[0].device if batches else torch.device('cuda', torch.cuda.current_device())
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    ic = list(interp_codes) if interp_codes is not None else [None] * len(batches)
+    parts = [ops.xt_bucket(b, l, w, err, interp_codes=c) for b, c in zip(batches, ic)]
+    sets_keys, sets_off = exchange_band_keys([(p.keys, p.band_off) for p in parts], NB, group, dev)
+    nb = b1 - b0
+    rows = torch.zeros(B * C, dtype=torch.int32, device=dev)
+    vec = torch.zeros((3, B), dtype=torch.int64, device=dev)
+    kp = (ctypes.c_void_p * len(sets_keys))(*[t.data_ptr() for t in sets_keys])
+    op = (ctypes.c_void_p * len(sets_off))(*[t.data_ptr() for t in sets_off])
+    _native.check(_native.lib().sa_xt_count_band_rows(
+        len(sets_keys), kp, op, l, w, b0, nb, vec[0].data_ptr(), vec[1].data_ptr(),
+        vec[2].data_ptr(), rows.data_ptr(), _native.SA_XT_COUNT_OVERWRITE, stream_handle()))
+    allv = torch.empty((W, 3, B), dtype=torch.int64, device=dev)
+    _all_gather(allv.reshape(-1), vec.reshape(-1), group=group)
+    full = allv.permute(1, 0, 2).reshape(3, W * B)[:, :C].contiguous()
+    _all_reduce(err, dist.ReduceOp.MAX, group=group)  # the error bytes of every rank
+    mats, heat, iters = _solve_row_block(rows, full[0], full[1], full[2], C, B, eps, max_iter,
+                                         group, batch)
+    return mats, heat, iters, err
+
+
+def exchange_band_keys(parts, n_bands: int, group=None, dev=None):
+    """Step 2 of :func:`xt_fit_bands_sharded`: ``parts`` = this rank's ``(keys, band_off)`` per
+    local batch (keys sorted by band, ``band_off`` [NB + 1]); returns the key sets of THIS rank's
+    bands, one per (local batch index, source rank): ``(keys list, band offsets list)`` where set
+    k holds its band lb's keys at ``keys[k][off[k][lb] .. off[k][lb + 1])``.  Every rank runs
+    the same number of exchanges (max local batches over the ranks; a rank with fewer sends
+    nothing in the extra ones)."""
+    import torch.distributed as dist
+    W = dist.get_world_size(group)
+    NB = n_bands
+    ranges = band_ranges(NB, W)
+    per = -(-NB // W)
+    dev = dev if dev is not None else (parts[0][0].device if parts else torch.device('cpu'))
+    rounds = torch.tensor([len(parts)], dtype=torch.int64, device=dev)
+    _all_reduce(rounds, dist.ReduceOp.MAX, group=group)
+    cuts = torch.tensor([q0 for q0, _ in ranges] + [NB], dtype=torch.int64, device=dev)
+    # the band offsets each destination needs: its bands q0 .. q0 + per (clamped), [W, per + 1]
+    want = torch.tensor([[min(NB, q0 + k) for k in range(per + 1)] for q0, _ in ranges],
+                        dtype=torch.int64, device=dev)
+    hcuts = (torch.stack([off[cuts] for _, off in parts]).cpu().numpy() if parts else
+             np.zeros((0, W + 1), np.int64))
+    sets_keys, sets_off = [], []
+    for k in range(int(rounds.item())):
+        if k < len(parts):
+            keys_k, off_k = parts[k]
+            send = (hcuts[k, 1:] - hcuts[k, :-1]).astype(np.int64)
+            keys = keys_k[int(hcuts[k, 0]):int(hcuts[k, W])]
+            offs = off_k[want.reshape(-1)].reshape(W, per + 1)
+            offs = offs - offs[:, :1]  # relative to each destination's first band
+        else:  # nothing of this round here, but every rank takes part in every exchange
+            send = np.zeros(W, np.int64)
+            keys = torch.zeros(0, dtype=torch.int32, device=dev)
+            offs = torch.zeros((W, per + 1), dtype=torch.int64, device=dev)
+        cnt = torch.from_numpy(send).to(dev)
+        rcnt = torch.empty(W, dtype=torch.int64, device=dev)
+        _all_to_all(rcnt, cnt, group=group)
+        recv_n = rcnt.cpu().numpy()
+        total = int(recv_n.sum())
+        recv = torch.empty(max(total, 1), dtype=torch.int32, device=dev)
+        _all_to_all(recv[:total], keys.contiguous(), recv_n.tolist(), send.tolist(), group=group)
+        roff = torch.empty((W, per + 1), dtype=torch.int64, device=dev)
+        _all_to_all(roff.reshape(-1), offs.contiguous().reshape(-1), group=group)
+        starts = np.concatenate([[0], np.cumsum(recv_n)])
+        for q in range(W):
+            sets_keys.append(recv[int(starts[q]):])
+            sets_off.append(roff[q])
+    return sets_keys, sets_off

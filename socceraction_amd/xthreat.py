@@ -240,12 +240,25 @@ class ExpectedThreat:
 
         With ``process_group`` each rank passes its own shard of games; counts are summed
         with one RCCL all-reduce and every rank solves the same system. ``shard_solve=True``
-        instead reduce-scatters the transition counts by rows and splits the value iteration
-        over the ranks (one all-gather of x per iteration; bit-identical results) for large
-        grids; the C x C ``transition_matrix`` is then not materialised (left ``None``).
+        instead splits the count rows and the value iteration over the ranks (one all-gather of x
+        per iteration; bit-identical results) for large grids -- grids the band-owned count holds
+        (``ops.xt_band_shape``, e.g. 105 x 68) exchange the ranks' counted actions by one
+        all-to-all, others reduce-scatter the count table; the C x C ``transition_matrix`` is
+        then not materialised (left ``None``).
         """
         w, l = self.w, self.l
-        if shard_solve and process_group is not None:
+        if shard_solve and process_group is not None and ops.xt_band_shape(l, w) is not None:
+            # band-owned grids: the ranks exchange their counted actions (an all-to-all of 4-B
+            # keys) instead of reduce-scattering the C x C count table
+            import types
+
+            from .shard import xt_fit_bands_sharded
+            batches = [ActionBatch.from_frame(actions)] if len(actions) else []
+            mats, heat_t, n_iter, err = xt_fit_bands_sharded(batches, l, w, self.eps, max_iter,
+                                                             process_group)
+            ops.xt_check_errors(types.SimpleNamespace(err=err))
+            trans = None
+        elif shard_solve and process_group is not None:
             import torch.distributed as dist
 
             from .shard import xt_solve_sharded

@@ -289,6 +289,74 @@ def test_xt_count_allreduce_gloo_world2():
     np.testing.assert_array_equal(T, f['transition'])
 
 
+def _band_keys(rank, part, R, NB):
+    """Synthetic bucketed keys of one local batch: start cell << 16 | slot, sorted by band."""
+    rng = np.random.default_rng([rank, part, 5])
+    n = int(rng.integers(0, 400))
+    cs = rng.integers(0, NB * R - 2, n)  # the last band is partial (C = NB R - 2)
+    keys = ((cs << 16) | rng.integers(0, 50, n)).astype(np.int64)
+    band = cs // R
+    order = np.argsort(band, kind='stable')
+    off = np.concatenate([[0], np.cumsum(np.bincount(band, minlength=NB))])
+    return keys[order].astype(np.uint32).view(np.int32), off.astype(np.int64)
+
+
+def _band_exchange_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+
+    from socceraction_amd import shard
+    dist.init_process_group('gloo', init_method=f'tcp://127.0.0.1:{port}', rank=rank,
+                            world_size=world)
+    R, NB = 3, 11
+    nparts = 2 if rank == 0 else 1  # the ranks run different numbers of local batches
+    parts = [tuple(torch.from_numpy(a) for a in _band_keys(rank, k, R, NB)) for k in range(nparts)]
+    keys, offs = shard.exchange_band_keys(parts, NB, dev=torch.device('cpu'))
+    b0, b1 = shard.band_ranges(NB, world)[rank]
+    got = []
+    for k, o in zip(keys, offs):
+        o = o.numpy()
+        kk = k.numpy().view(np.uint32).astype(np.int64)
+        for lb in range(b1 - b0):  # every key of local band lb belongs to band b0 + lb
+            seg = kk[o[lb]:o[lb + 1]]
+            assert ((seg >> 16) // R == b0 + lb).all()
+            got.append(seg)
+    q.put((rank, np.sort(np.concatenate(got)) if got else np.zeros(0, np.int64), len(keys)))
+    dist.destroy_process_group()
+
+
+def test_band_key_exchange_gloo_world2():
+    """shard.exchange_band_keys (the band-sharded xT fit's all-to-all) over gloo, world 2, with
+    a different number of local batches per rank: each rank receives exactly the keys of its own
+    bands from every rank's every batch, with band offsets relative to its first band."""
+    import multiprocessing as mp
+    import socket
+
+    from socceraction_amd import shard
+    assert shard.band_ranges(11, 2) == [(0, 6), (6, 11)]
+    assert shard.band_ranges(3, 4) == [(0, 1), (1, 2), (2, 3), (3, 3)]
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_band_exchange_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict((r, (keys, n)) for r, keys, n in (q.get(timeout=120) for _ in range(2)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    R, NB = 3, 11
+    every = np.concatenate([_band_keys(r, k, R, NB)[0].view(np.uint32).astype(np.int64)
+                            for r, nparts in ((0, 2), (1, 1)) for k in range(nparts)])
+    for r, (b0, b1) in enumerate(shard.band_ranges(NB, 2)):
+        band = (every >> 16) // R
+        want = np.sort(every[(band >= b0) & (band < b1)])
+        np.testing.assert_array_equal(res[r][0], want)
+        assert res[r][1] == 2 * 2  # two rounds (rank 0's batches) x two source ranks
+
+
 # ----------------------------------------------------------------------------- synthetic data
 def test_synthetic_generator_shape_and_determinism():
     from socceraction_amd import synthetic

@@ -28,22 +28,29 @@ def test_bench_gpus_2_launches_two_ranks():
     assert 0 < out['roofline']['step_frac'] < 1
 
 
-def test_bench_gpus_2_side_entries():
-    """The side entries under two ranks: cfg5's and cfg3's games split over the ranks."""
+@pytest.mark.parametrize('solve', ['sharded', 'replicated'])
+def test_bench_gpus_2_side_entries(solve):
+    """The side entries under two ranks: cfg5's and cfg3's games split over the ranks; cfg5's
+    fit band-sharded (the default for N > 1: all-to-all of the counted actions, each rank counting
+    and iterating its own bands) or replicated (all-reduce of the count table), its parity block
+    (counts or surface, iterations, rates vs the oracle) ok either way."""
     env = dict(os.environ, SA_DIST_BACKEND='gloo')
     env.pop('WORLD_SIZE', None)
     p = subprocess.run([sys.executable, 'bench.py', '--gpus', '2', '--games', '20', '--steps', '2',
                         '--warmup', '1', '--no-cpu', '--cfg5-games', '45', '--atomic-games', '30',
-                        '--e2e-games', '5'], cwd=ROOT, env=env, capture_output=True, text=True,
-                       timeout=240)
+                        '--e2e-games', '5', '--cfg5-solve', solve], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=240)
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith('{')]
     assert p.returncode == 0 and len(lines) == 1, p.stdout[-2000:] + p.stderr[-3000:]
     out = json.loads(lines[0])
     assert out['n_gpus'] == 2
     x = out['xt105_cfg5']
     assert x['actions_total'] > x['actions_per_gpu'] > 0 and x['iterations'] > 0
+    assert x['solve'].startswith('band-sharded' if solve == 'sharded' else 'replicated')
+    assert x['parity']['ok'] and x['parity']['values_checked'] > 0
     a = out['atomic_cfg3']
     assert a['atomic_actions_total'] > a['atomic_actions_per_gpu'] > 0
+    assert a['parity']['ok']
 
 
 def test_device_events_order_streams_and_time():

@@ -113,10 +113,11 @@ def _random_rows(rng, C, nrows, zero_rows=3):
 
 
 @pytest.mark.parametrize('C,r0,nrows', [(7140, 0, 7140), (7140, 1785, 1785), (1200, 1170, 30),
-                                        (203, 0, 203)])
+                                        (203, 0, 203), (1201, 7, 100)])
 def test_compact_iteration_equals_dense(sa, C, r0, nrows):
-    """sa_xt_iterate_compact over sa_xt_compact_rows == sa_xt_iterate_rows (the dense count-row
-    kernel), bit for bit, on random count rows (tabulated quotients, divided counts, escaped
+    """sa_xt_compact_rows holds each row's non-zero columns and counts in order, and
+    sa_xt_iterate_compact over it == sa_xt_iterate_rows (the dense count-row kernel), bit for
+    bit, on random count rows (tabulated quotients, divided counts, escaped
     counts >= 65535, empty rows), a sub-range of rows (the row-sharded solve), x with zeros;
     the convergence flag and the no-op when the previous flag is 0."""
     _native, ops = sa['_native'], sa['ops']
@@ -131,12 +132,17 @@ def test_compact_iteration_equals_dense(sa, C, r0, nrows):
     gs = torch.rand(C, dtype=torch.float64, device=dev) * 0.1
     pm = torch.rand(C, dtype=torch.float64, device=dev)
     ell = torch.empty(int(lib.sa_xt_compact_bytes(C, nrows)) // 4, dtype=torch.int32, device=dev)
-    slen = torch.empty(-(-nrows // 32), dtype=torch.int32, device=dev)
+    slen = torch.empty(nrows, dtype=torch.int32, device=dev)
     p = lambda t: t.data_ptr()  # noqa: E731
     _native.check(lib.sa_xt_compact_rows(p(rows), C, nrows, p(ell), p(slen), stream_handle()))
-    lens = slen.cpu().numpy()
-    nnz = (rows.cpu().numpy() != 0).sum(axis=1)
-    np.testing.assert_array_equal(lens, [nnz[i:i + 32].max() for i in range(0, nrows, 32)])
+    h = rows.cpu().numpy()
+    np.testing.assert_array_equal(slen.cpu().numpy(), (h != 0).sum(axis=1))
+    pe = (C + 3) // 4 * 4  # the compact rows' pitch
+    e = ell.cpu().numpy().view(np.uint32).reshape(nrows, pe)
+    for i in rng.choice(nrows, 5, replace=False):  # row i: its non-zero columns in order, counts
+        nz = np.flatnonzero(h[i])
+        np.testing.assert_array_equal(e[i, :len(nz)] & 0xFFFF, nz)
+        np.testing.assert_array_equal(e[i, :len(nz)] >> 16, np.minimum(h[i, nz], 0xFFFF))
     for trial in range(3):
         x = torch.rand(C, dtype=torch.float64, device=dev)
         x[torch.from_numpy(rng.random(C) < 0.2).to(dev)] = 0.0
