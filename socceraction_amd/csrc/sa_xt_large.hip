@@ -36,6 +36,9 @@
 namespace sa {
 
 // ============================================================================ band-owned count
+#ifndef SA_XK_PROBE
+#define SA_XK_PROBE 0  // diagnostic builds (wrong counts): 1 = no band histogram, 2 = no key stores
+#endif
 #ifndef SA_XK_THREADS
 #define SA_XK_THREADS 1024  // K1 workgroup (two per CU at cfg5: 32 waves of loads in flight)
 #endif
@@ -207,14 +210,39 @@ __global__ __launch_bounds__(XK_THREADS) void xt_keys_kernel(sa_actions A, const
           ey[u] = F.c3[jc];
         }
       }
+      if (vec) {  // a pair's two operands in one store (16 B: whole lines per instruction)
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int64_t j = jj[u];
-        if (RO.codes && tt[u] >= 0) RO.codes[j] = rate_code(tt[u], rr[u], sx[u], sy[u], ex[u], ey[u], l, w);
-        if (RO.icodes && tt[u] >= 0)
-          RO.icodes[j] = rate_icode(tt[u], rr[u], sx[u], sy[u], ex[u], ey[u], RO.L, RO.W);
-        act[u] = act_from_row(tt[u], rr[u], sx[u], sy[u], ex[u], ey[u], l, w);
+        for (int q = 0; q < U / 2; ++q) {
+          const int u = 2 * q;
+          const int64_t j = jj[u];
+          if (RO.codes && tt[u] >= 0) {
+            const uint32_t c0 = rate_code(tt[u], rr[u], sx[u], sy[u], ex[u], ey[u], l, w);
+            if (tt[u + 1] >= 0)
+              *reinterpret_cast<uint2*>(RO.codes + j) =
+                  make_uint2(c0, rate_code(tt[u + 1], rr[u + 1], sx[u + 1], sy[u + 1], ex[u + 1], ey[u + 1], l, w));
+            else
+              RO.codes[j] = c0;
+          }
+          if (RO.icodes && tt[u] >= 0) {
+            const uint64_t c0 = rate_icode(tt[u], rr[u], sx[u], sy[u], ex[u], ey[u], RO.L, RO.W);
+            if (tt[u + 1] >= 0)
+              *reinterpret_cast<u64x2*>(RO.icodes + j) =
+                  u64x2{c0, rate_icode(tt[u + 1], rr[u + 1], sx[u + 1], sy[u + 1], ex[u + 1], ey[u + 1], RO.L, RO.W)};
+            else
+              RO.icodes[j] = c0;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int64_t j = jj[u];
+          if (RO.codes && tt[u] >= 0) RO.codes[j] = rate_code(tt[u], rr[u], sx[u], sy[u], ex[u], ey[u], l, w);
+          if (RO.icodes && tt[u] >= 0)
+            RO.icodes[j] = rate_icode(tt[u], rr[u], sx[u], sy[u], ex[u], ey[u], RO.L, RO.W);
+        }
       }
+#pragma unroll
+      for (int u = 0; u < U; ++u) act[u] = act_from_row(tt[u], rr[u], sx[u], sy[u], ex[u], ey[u], l, w);
     }
     uint32_t key[U];
     bool has[U];
@@ -234,8 +262,8 @@ __global__ __launch_bounds__(XK_THREADS) void xt_keys_kernel(sa_actions A, const
       if (has[u]) {
         const uint32_t pos = wbase + lane_rank(m[u]);
         SA_DGUARD(pos < XK_CHUNK, pos, continue);
-        out[pos] = key[u];
-        atomicAdd(&bh[band_of(key[u], S.magic)], 1u);
+        if (!(SA_XK_PROBE & 2)) out[pos] = key[u];
+        if (!(SA_XK_PROBE & 1)) atomicAdd(&bh[band_of(key[u], S.magic)], 1u);
       }
       wbase += (uint32_t)__popcll(m[u]);
     }
@@ -467,7 +495,7 @@ constexpr int XE_BUILD_ROWS = 16;            // build: rows per workgroup (one w
 constexpr uint32_t XE_CNT_ESC = 0xFFFFu;     // count >= 65535: read from the dense row
 #ifndef SA_XE_PROBE
 #define SA_XE_PROBE 0  // diagnostic builds (wrong values): 1 = no products, 2 = no chain adds,
-#endif                 // 4 = idle product waves (no loads, no LDS writes)
+#endif                 // 4 = idle product waves (no loads, no LDS writes), 8 = no division path
 static_assert(XE_KC == 128 && XE_PAIRS * 2 * XE_P == XE_S, "xt_iter_ell_kernel shape: 32 lanes x 4 entries per row chunk");
 static_assert(XE_THREADS <= 1024 && XE_S <= 64, "xt_iter_ell_kernel shape");
 constexpr size_t XE_LDS_STATIC = (size_t)XE_S * (2 * XE_PITCH + 1) * 8 + XE_S * 4;
@@ -576,12 +604,18 @@ __global__ __launch_bounds__(XE_THREADS) void xt_iter_ell_kernel(const uint32_t*
     // DEPTH register slots of entries, slot d holding chunk j with j % DEPTH == d: the loop is
     // unrolled by DEPTH so a slot's loads are refilled right after its products are formed and
     // no register is copied while its load is in flight (a copy waits for the load); loads are
-    // unconditional from clamped addresses, entries past a row's end zeroed at their use
+    // unconditional from addresses clamped to the row's last entries (a slice's HBM / Infinity
+    // Cache bytes are its rows' entries only: one CU pulls ~30-70 GB/s, so the slice holding the
+    // longest row would otherwise stream every row to that length), entries past a row's end
+    // zeroed at their use
     u32x4 e[XE_DEPTH][XE_PAIRS];
+    int kmax[XE_PAIRS];  // the last 16-B group of each row: an ended row's loads re-read it (cache hits)
+#pragma unroll
+    for (int p = 0; p < XE_PAIRS; ++p) kmax[p] = lr[p] > 0 ? (lr[p] - 1) & ~3 : 0;
     auto ld = [&](u32x4 (&d)[XE_PAIRS], int j) {
 #pragma unroll
       for (int p = 0; p < XE_PAIRS; ++p) {
-        const int k = min(j * XE_KC + k4, pe - 4);
+        const int k = min(j * XE_KC + k4, kmax[p]);
 #if SA_XE_NTL
         d[p] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(Er[p] + k));
 #else  // default policy: the compact rows (~70 MB at cfg5) stay in the Infinity Cache across iterations
@@ -608,7 +642,7 @@ __global__ __launch_bounds__(XE_THREADS) void xt_iter_ell_kernel(const uint32_t*
           xv[p][u] = xs[col < (uint32_t)C ? col : 0u];
           big |= cnt >= (uint32_t)ct;
         }
-      if (__builtin_expect(__ballot(big) != 0, 0)) {
+      if (__builtin_expect(__ballot(big) != 0, 0) && !(SA_XE_PROBE & 8)) {
 #pragma unroll
         for (int p = 0; p < XE_PAIRS; ++p)
 #pragma unroll
