@@ -372,9 +372,9 @@ int sa_xt_iterate_rows(const int32_t* cnt_rows, const int64_t* move, const doubl
                        void* stream);
 /* The same iteration over a compact form of the count rows built once (C <= 9472; sa_xt_solve
  * uses it for C > SA_XT_SOLVE_MAX_C): sa_xt_compact_rows writes each row's non-zero counts in
- * column order (4 B each: column | min(count, 65535) << 16) at ell[i * pe ..], pe = C rounded up
- * to a multiple of 4 (u32, 16-byte aligned, sa_xt_compact_bytes(C, nrows) bytes), and their
- * number at row_len[i] (int32 [nrows], device);
+ * column order (4 B each: column | min(count, 65535) << 16) in row i's pe = C rounded up to a
+ * multiple of 128 slots, the k-th at slot (k & ~127) | (k % 32) << 2 | (k / 32) % 4 (u32,
+ * sa_xt_compact_bytes(C, nrows) bytes), and their number at row_len[i] (int32 [nrows], device);
  * sa_xt_iterate_compact then equals sa_xt_iterate_rows bit for bit (cnt_rows: the same dense
  * rows, read only for counts >= 65535).  Asynchronous. */
 int64_t sa_xt_compact_bytes(int32_t C, int32_t nrows);

@@ -489,25 +489,41 @@ constexpr int XE_CT_MAX = 256;               // counts whose quotient is tabulat
 #define SA_XE_NTL 0                          // 1: non-temporal entry loads
 #endif
 constexpr int XE_DEPTH = SA_XE_DEPTH;
+#ifndef SA_XE_QDIV
+#define SA_XE_QDIV 1                         // 1: quotients cnt / move by a corrected product with
+#endif                                       //    the row's reciprocal; 0: per-row LDS table
 constexpr int XE_THREADS = (XE_P + 1) * 64;  // + the chain wave
 constexpr int XE_XMAX = 9472;                // x (C doubles) staged in LDS
 constexpr int XE_BUILD_ROWS = 16;            // build: rows per workgroup (one wave each)
 constexpr uint32_t XE_CNT_ESC = 0xFFFFu;     // count >= 65535: read from the dense row
 #ifndef SA_XE_PROBE
-#define SA_XE_PROBE 0  // diagnostic builds (wrong values): 1 = no products, 2 = no chain adds,
-#endif                 // 4 = idle product waves (no loads, no LDS writes), 8 = no division path
+#define SA_XE_PROBE 0  // diagnostic builds (wrong values): 1 = no products,
+#endif                 // 4 = idle product waves (no loads, no LDS writes; the chain then reads LDS
+                       // nobody wrote and may be folded away: no chain timing), 8 = no division path,
+                       // 16 = workgroup 0's phase times (wall clock ticks) in x_next[0..3],
+                       // 32 = its work / barrier clocks per wave in x_next[40..43], 64 = product
+                       // waves without LDS traffic (x = the column, no product stores)
 static_assert(XE_KC == 128 && XE_PAIRS * 2 * XE_P == XE_S, "xt_iter_ell_kernel shape: 32 lanes x 4 entries per row chunk");
 static_assert(XE_THREADS <= 1024 && XE_S <= 64, "xt_iter_ell_kernel shape");
-constexpr size_t XE_LDS_STATIC = (size_t)XE_S * (2 * XE_PITCH + 1) * 8 + XE_S * 4;
+constexpr size_t XE_LDS_STATIC = (size_t)XE_S * (2 * XE_PITCH + 2) * 8 + XE_S * 4;
 constexpr size_t XE_LDS_MAX = 160 * 1024;
 static_assert((size_t)XE_XMAX * 8 + (size_t)XE_S * 16 * 8 + XE_LDS_STATIC <= XE_LDS_MAX,
               "xt_iter_ell_kernel LDS: x and a 16-count quotient table");
 static_assert(XE_DEPTH >= 1 && XE_DEPTH <= 8, "SA_XE_DEPTH");
 
+// A compact row's pitch in entries: C rounded up to whole chunks (room for a dense row).
+__host__ __device__ constexpr int xe_pitch(int C) { return (C + XE_KC - 1) / XE_KC * XE_KC; }
+// Storage slot of a row's k-th entry: chunk-interleaved, so the 16-B group at slot 4 l of a chunk
+// holds its entries l, l + 32, l + 64, l + 96 -- one 16-B load per lane, yet each LDS instruction
+// of the products (x at the columns, the product stores) spans 32 consecutive entries: columns
+// close together, distinct banks (entries 4 apart would put a dense row's columns 32 B apart,
+// eight lanes on a bank pair).
+__device__ __forceinline__ int xe_slot(int k) { return (k & ~(XE_KC - 1)) | ((k & 31) << 2) | ((k >> 5) & 3); }
+
 // Compact form of rows [0, nrows) of a count block (row i at cnt_rows + i*C): row i's non-zero
-// counts in column order, column | min(count, 0xFFFF) << 16, at ell[i*pe + k] (pe = C rounded up
-// to a multiple of 4: room for a dense row, 16-byte aligned rows), and their number at row_len[i].  One wave per row: 8 loads of 64 columns in flight,
-// ballot + mbcnt, so each instruction stores one contiguous run.
+// counts in column order, column | min(count, 0xFFFF) << 16, the k-th at ell[i*pe + xe_slot(k)]
+// (pe = xe_pitch(C)), and their number at row_len[i].  One wave per row: 8 loads of 64 columns
+// in flight, ballot + mbcnt for each entry's rank.
 __global__ __launch_bounds__(XE_BUILD_ROWS * 64) void xt_ell_build_kernel(const int32_t* __restrict__ cnt_rows, int C,
                                                                           int nrows, uint32_t* __restrict__ ell,
                                                                           int32_t* __restrict__ row_len) {
@@ -515,7 +531,7 @@ __global__ __launch_bounds__(XE_BUILD_ROWS * 64) void xt_ell_build_kernel(const 
   const int r = blockIdx.x * XE_BUILD_ROWS + (threadIdx.x >> 6);
   if (r >= nrows) return;  // whole wave
   const int32_t* row = cnt_rows + (int64_t)r * C;
-  uint32_t* E = ell + (int64_t)r * ((C + 3) & ~3);  // rows 16-byte aligned
+  uint32_t* E = ell + (int64_t)r * xe_pitch(C);
   int base = 0;
   for (int c0 = 0; c0 < C; c0 += 64 * 8) {
     int32_t v[8];
@@ -529,7 +545,7 @@ __global__ __launch_bounds__(XE_BUILD_ROWS * 64) void xt_ell_build_kernel(const 
       const uint64_t m = __ballot(v[u] != 0);
       if (v[u] != 0) {
         const uint32_t cnt = (uint32_t)v[u] < XE_CNT_ESC ? (uint32_t)v[u] : XE_CNT_ESC;
-        E[base + (int)lane_rank(m)] = (uint32_t)(c0 + 64 * u + lane) | (cnt << 16);
+        E[xe_slot(base + (int)lane_rank(m))] = (uint32_t)(c0 + 64 * u + lane) | (cnt << 16);
       }
       base += (int)__popcll(m);
     }
@@ -543,11 +559,13 @@ __global__ __launch_bounds__(XE_BUILD_ROWS * 64) void xt_ell_build_kernel(const 
 // operations (sa_xt.hip), without its per-chunk compaction of the dense rows.  One workgroup per
 // slice of 32 rows.  Per chunk of KC entries per row, each product wave loads its 4 rows'
 // entries (256 contiguous bytes per load; DEPTH - 1 chunks ahead), forms the products -- the
-// quotient from a per-row LDS table for counts < ct, else the same division -- and writes them
-// to prod[row][k]; the
-// chain wave (lane = row) then adds its row's products strictly in order.  One barrier per
-// chunk, two buffers; rows shorter than the slice's longest add +0 terms (exact: the sums are
-// non-negative).
+// quotient cnt / move[row] (QDIV: y = cnt * r, r = 1 / move[row] rounded; then
+// y + r * (cnt - y * move) by two fmas, Markstein's correction: the correctly rounded quotient, the
+// division's own bits -- scripts/check_quotient.c checks it exhaustively for cnt < 65536 against
+// 6000 + 6001 divisors and on 4e8 random pairs up to 2^53; no LDS read, no table), times x at
+// the column -- and writes them to prod[row][k]; the chain wave (lane = row) then adds its row's products strictly in order.  One barrier per
+// chunk, two buffers; a row shorter than the slice's longest costs nothing past its end (its
+// product lanes and its chain lane skip those chunks).
 __global__ __launch_bounds__(XE_THREADS) void xt_iter_ell_kernel(const uint32_t* __restrict__ ell,
                                                                  const int32_t* __restrict__ row_len,
                                                                  const int32_t* __restrict__ cnt_rows,
@@ -559,27 +577,48 @@ __global__ __launch_bounds__(XE_THREADS) void xt_iter_ell_kernel(const uint32_t*
                                                                  double* __restrict__ xo, const int32_t* flag_prev,
                                                                  int32_t* __restrict__ flag_out) {
   if (flag_prev && __hip_atomic_load(flag_prev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
+#if SA_XE_PROBE & 16
+  const long long t_entry = wall_clock64();
+#endif
   extern __shared__ __attribute__((aligned(16))) double xs[];  // [C] x, then tq [S][ct]
-  double* tq = xs + C;                                         // tq[i * ct + q] = q / move[row i]
+  [[maybe_unused]] double* tq = xs + C;                        // tq[i * ct + q] = q / move[row i]
   __shared__ double prod[2][XE_S * XE_PITCH];
-  __shared__ double mvs[XE_S];
+  __shared__ double mvs[XE_S], rcp[XE_S];
   __shared__ int lens[XE_S];
   const int row0 = blockIdx.x * XE_S, nr = min(XE_S, nrows - row0);
-  const int pe = (C + 3) & ~3;  // the compact rows' pitch (16-byte aligned rows)
-  for (int c = threadIdx.x; c < C; c += XE_THREADS) xs[c] = x[c];
-  for (int e = threadIdx.x; e < XE_S * ct; e += XE_THREADS) {
-    const int i = e / ct, q = e % ct;
-    const double mv = i < nr ? (double)move[rb + row0 + i] : 1.0;
-    tq[e] = q == 0 ? 0.0 : (double)q / mv;  // a count of 0 is a zero term (T = 0)
-    if (q == 0) {
-      mvs[i] = mv;
-      lens[i] = i < nr ? row_len[row0 + i] : 0;
-    }
+  const int pe = xe_pitch(C);
+  // staging: every global load of x, move and row_len issued before the first LDS store (a
+  // load-store loop would wait out one memory latency per 576 elements: ~13 at C = 7140)
+  constexpr int XR = (XE_XMAX + XE_THREADS - 1) / XE_THREADS;
+  double xr[XR];
+#pragma unroll
+  for (int u = 0; u < XR; ++u) xr[u] = x[min((int)threadIdx.x + u * XE_THREADS, C - 1)];
+  const int t = threadIdx.x;
+  const double mv0 = t < nr ? (double)move[rb + row0 + min(t, nr - 1)] : 1.0;
+  const int len0 = t < nr ? row_len[row0 + min(t, nr - 1)] : 0;
+#pragma unroll
+  for (int u = 0; u < XR; ++u)
+    if (t + u * XE_THREADS < C) xs[t + u * XE_THREADS] = xr[u];
+  if (t < XE_S) {
+    mvs[t] = mv0;
+    rcp[t] = 1.0 / mv0;
+    lens[t] = len0;
   }
   __syncthreads();
+#if !SA_XE_QDIV
+  const int lct = __builtin_ctz(ct);  // ct: a power of two
+  for (int e = t; e < XE_S * ct; e += XE_THREADS) {
+    const int q = e & (ct - 1);
+    tq[e] = q == 0 ? 0.0 : (double)q / mvs[e >> lct];  // a count of 0 is a zero term (T = 0)
+  }
+  __syncthreads();
+#endif
   int len = 0;
 #pragma unroll
   for (int i = 0; i < XE_S; ++i) len = max(len, lens[i]);
+#if SA_XE_PROBE & 16
+  const long long t_setup = wall_clock64();
+#endif
   const int nch = (len + XE_KC - 1) / XE_KC;
   const int nchp = (nch + XE_DEPTH - 1) / XE_DEPTH * XE_DEPTH;  // chunks past nch: +0 terms
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -589,15 +628,19 @@ __global__ __launch_bounds__(XE_THREADS) void xt_iter_ell_kernel(const uint32_t*
     return;
 #endif
     // wave wv owns rows wv + 8 q (q < 4) as two pairs: half = lane / 32 takes row
-    // wv + 8 (2 p + half) of pair p, a lane 4 consecutive entries of it per chunk (one 16-B load:
-    // a wave instruction fetches 1 KiB, two rows' chunks)
-    const int half = lane >> 5, k4 = 4 * (lane & 31);
+    // wv + 8 (2 p + half) of pair p, lane l = lane % 32 its entries l + 32 u (u < 4) of each
+    // chunk (one 16-B load of slots 4 l..4 l + 3: a wave instruction fetches 1 KiB, two rows'
+    // chunks)
+    const int half = lane >> 5, l32 = lane & 31;
     const uint32_t* Er[XE_PAIRS];
     int lr[XE_PAIRS], ir[XE_PAIRS];
+    double mq[XE_PAIRS], rq[XE_PAIRS];  // the rows' move count and its rounded reciprocal
 #pragma unroll
     for (int p = 0; p < XE_PAIRS; ++p) {
       const int i = wv + XE_P * (2 * p + half);
       ir[p] = i;
+      mq[p] = mvs[i];
+      rq[p] = rcp[i];
       Er[p] = ell + (int64_t)(row0 + min(i, nr - 1)) * pe;
       lr[p] = lens[i];
     }
@@ -609,13 +652,13 @@ __global__ __launch_bounds__(XE_THREADS) void xt_iter_ell_kernel(const uint32_t*
     // longest row would otherwise stream every row to that length), entries past a row's end
     // zeroed at their use
     u32x4 e[XE_DEPTH][XE_PAIRS];
-    int kmax[XE_PAIRS];  // the last 16-B group of each row: an ended row's loads re-read it (cache hits)
+    int jmax[XE_PAIRS];  // each row's last chunk: an ended row's loads re-read it (cache hits)
 #pragma unroll
-    for (int p = 0; p < XE_PAIRS; ++p) kmax[p] = lr[p] > 0 ? (lr[p] - 1) & ~3 : 0;
+    for (int p = 0; p < XE_PAIRS; ++p) jmax[p] = lr[p] > 0 ? (lr[p] - 1) / XE_KC : 0;
     auto ld = [&](u32x4 (&d)[XE_PAIRS], int j) {
 #pragma unroll
       for (int p = 0; p < XE_PAIRS; ++p) {
-        const int k = min(j * XE_KC + k4, kmax[p]);
+        const int k = min(j, jmax[p]) * XE_KC + 4 * l32;
 #if SA_XE_NTL
         d[p] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(Er[p] + k));
 #else  // default policy: the compact rows (~70 MB at cfg5) stay in the Infinity Cache across iterations
@@ -625,22 +668,36 @@ __global__ __launch_bounds__(XE_THREADS) void xt_iter_ell_kernel(const uint32_t*
     };
     auto products = [&](const u32x4 (&E)[XE_PAIRS], int j) {
       double* pr = prod[j & 1];
-      // every LDS read of the chunk first (the quotient from the table at min(cnt, ct - 1), x at
-      // the column; entries past a row's end are 0: T = 0, x[0]), then the rare counts >= ct,
-      // then the products: no branch between a read and its use, so the reads overlap
+      // every LDS read of the chunk first (x at the column; without QDIV the quotient from the
+      // table at min(cnt, ct - 1); entries past a row's end are 0: T = 0, x[0]), then the rare
+      // escaped counts (without QDIV: counts >= ct), then the products: no branch between a read
+      // and its use, so the reads overlap
       double tv[XE_PAIRS][4], xv[XE_PAIRS][4];
       uint32_t en[XE_PAIRS][4];
-      bool big = false;
+      bool big = false, live[XE_PAIRS];
+#pragma unroll
+      for (int p = 0; p < XE_PAIRS; ++p) live[p] = j * XE_KC < lr[p];  // the row has entries in chunk j
 #pragma unroll
       for (int p = 0; p < XE_PAIRS; ++p)
+        if (live[p])  // an ended row costs no LDS traffic: its chain lane skips the chunk
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          en[p][u] = j * XE_KC + k4 + u < lr[p] ? E[p][u] : 0u;
+          en[p][u] = j * XE_KC + 32 * u + l32 < lr[p] ? E[p][u] : 0u;
           const uint32_t cnt = en[p][u] >> 16, col = en[p][u] & 0xFFFFu;
           SA_DCHECK((int)col < C, col);
-          tv[p][u] = tq[ir[p] * ct + min(cnt, (uint32_t)ct - 1u)];
+#if SA_XE_PROBE & 64
+          xv[p][u] = (double)col;
+#else
           xv[p][u] = xs[col < (uint32_t)C ? col : 0u];
+#endif
+#if SA_XE_QDIV
+          const double q = (double)cnt, y = q * rq[p];  // a count of 0 is a zero term (T = 0)
+          tv[p][u] = __builtin_fma(__builtin_fma(-y, mq[p], q), rq[p], y);
+          big |= cnt == XE_CNT_ESC;
+#else
+          tv[p][u] = tq[ir[p] * ct + min(cnt, (uint32_t)ct - 1u)];
           big |= cnt >= (uint32_t)ct;
+#endif
         }
       if (__builtin_expect(__ballot(big) != 0, 0) && !(SA_XE_PROBE & 8)) {
 #pragma unroll
@@ -648,49 +705,86 @@ __global__ __launch_bounds__(XE_THREADS) void xt_iter_ell_kernel(const uint32_t*
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             const uint32_t cnt = en[p][u] >> 16, col = en[p][u] & 0xFFFFu;
-            if (cnt >= (uint32_t)ct) {
+            if (live[p] && cnt >= (uint32_t)(SA_XE_QDIV ? XE_CNT_ESC : ct)) {
               const int32_t c32 = cnt == XE_CNT_ESC ? cnt_rows[(int64_t)(row0 + ir[p]) * C + col] : (int32_t)cnt;
-              tv[p][u] = (double)c32 / mvs[ir[p]];
+              tv[p][u] = (double)c32 / mq[p];
             }
           }
       }
 #pragma unroll
       for (int p = 0; p < XE_PAIRS; ++p) {
-        f64x2 v0, v1;
-#if SA_XE_PROBE & 1
-        v0 = f64x2{0.0 * tv[p][0], 0.0 * tv[p][1]};
-        v1 = f64x2{0.0 * tv[p][2], 0.0 * tv[p][3]};
+        if (!live[p]) continue;
+        double* dst = pr + ir[p] * XE_PITCH + l32;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#if SA_XE_PROBE & 64
+          if (tv[p][u] * xv[p][u] == -1.0) dst[32 * u] = 0.0;
+#elif SA_XE_PROBE & 1
+          dst[32 * u] = 0.0 * tv[p][u];
 #else
-        v0 = f64x2{tv[p][0] * xv[p][0], tv[p][1] * xv[p][1]};
-        v1 = f64x2{tv[p][2] * xv[p][2], tv[p][3] * xv[p][3]};
+          dst[32 * u] = tv[p][u] * xv[p][u];
 #endif
-        f64x2* dst = reinterpret_cast<f64x2*>(pr + ir[p] * XE_PITCH + k4);
-        dst[0] = v0;
-        dst[1] = v1;
       }
     };
 #pragma unroll
     for (int d = 0; d < XE_DEPTH; ++d) ld(e[d], d);
     asm volatile("" ::: "memory");
+#if SA_XE_PROBE & 32
+    long long pw_work = 0, pw_bar = 0, pw_t = clock64();
+#endif
     for (int j0 = 0; j0 < nchp; j0 += XE_DEPTH) {
 #pragma unroll
       for (int d = 0; d < XE_DEPTH; ++d) {
         products(e[d], j0 + d);
         ld(e[d], j0 + d + XE_DEPTH);  // past the last chunk: harmless clamped re-reads
         asm volatile("" ::: "memory");
+#if SA_XE_PROBE & 32
+        const long long t1 = clock64();
+        pw_work += t1 - pw_t;
+#endif
         __syncthreads();
+#if SA_XE_PROBE & 32
+        pw_t = clock64();
+        pw_bar += pw_t - t1;
+#endif
       }
     }
+#if SA_XE_PROBE & 32
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      xo[40] = (double)pw_work;
+      xo[41] = (double)pw_bar;
+    }
+#endif
+#if SA_XE_PROBE & 16
+    if (blockIdx.x == 0 && threadIdx.x == 0) xo[3] = (double)(wall_clock64() - t_entry);
+#endif
   } else {  // ---- chain wave: lane i adds row i's products strictly left to right
     // the critical path of the launch (the longest row's adds): first claim on its SIMD's issue
     // slots over the two product waves sharing it (MI355X_MICROARCH.md: priority, then age)
     __builtin_amdgcn_s_setprio(3);
-    const int i = lane & (XE_S - 1);
+    const int i = lane & (XE_S - 1), li = lane < XE_S ? lens[i] : 0;  // lanes >= S idle
+    // the adds are LDS-fed: each 16-B read (2 products) costs the wave ~5 clocks of issue
+    // whatever its active lanes and however far ahead it is issued, on top of the ~5-clock
+    // dependent f64 add (scratch microbenchmarks: 10.35 clocks per add fed from LDS, 5.2 from
+    // registers) -- the longest row's ~6000 adds bound the launch
     double acc = 0.0;
+#if SA_XE_PROBE & 32
+    long long cw_work = 0, cw_bar = 0, cw_t = clock64();
+#endif
     for (int j = 0; j < nchp; ++j) {
+#if SA_XE_PROBE & 32
+      {
+        const long long t1 = clock64();
+        cw_work += t1 - cw_t;
+        __syncthreads();
+        cw_t = clock64();
+        cw_bar += cw_t - t1;
+      }
+#else
       __syncthreads();
+#endif
+      if (j * XE_KC >= li) continue;  // row ended (or idle lane): no reads, no +0 adds
       const f64x2* pr = reinterpret_cast<const f64x2*>(prod[j & 1] + i * XE_PITCH);
-#if !(SA_XE_PROBE & 2)
       constexpr int G = 16;  // 16-B reads (two products each) issued a group ahead of their adds
       f64x2 v[G];
 #pragma unroll
@@ -708,9 +802,6 @@ __global__ __launch_bounds__(XE_THREADS) void xt_iter_ell_kernel(const uint32_t*
 #pragma unroll
         for (int k = 0; k < G; ++k) v[k] = nx[k];
       }
-#else
-      acc += pr[0][0];
-#endif
     }
     if (lane < nr) {
       const int rr = rb + row0 + lane;
@@ -719,6 +810,19 @@ __global__ __launch_bounds__(XE_THREADS) void xt_iter_ell_kernel(const uint32_t*
       xo[row0 + lane] = nx;
       if ((nx - x[rr]) > eps) atomicOr(flag_out, 1);  // np.any(diff > eps): NaN is False
     }
+#if SA_XE_PROBE & 32  // shader clocks of work / barrier wait, chain wave (42, 43), product wave 0 (40, 41)
+    if (blockIdx.x == 0 && lane == 0) {
+      xo[42] = (double)(cw_work + (clock64() - cw_t));
+      xo[43] = (double)cw_bar;
+    }
+#endif
+#if SA_XE_PROBE & 16  // wall clock (100 MHz) ticks from entry: setup done, chain done, (3) products done
+    if (blockIdx.x == 0 && lane == 0) {
+      xo[0] = (double)nchp;
+      xo[1] = (double)(t_setup - t_entry);
+      xo[2] = (double)(wall_clock64() - t_entry);
+    }
+#endif
   }
 }
 
@@ -848,7 +952,7 @@ int xt_count_bands(const sa_actions& A, const uint32_t* cells, int64_t n, int l,
 
 // Compact form + iteration used by sa_xt_solve for C > SA_XT_SOLVE_MAX_C.
 bool xt_compact_ok(int C) { return C >= 1 && C <= XE_XMAX; }
-size_t xt_compact_bytes(int C, int nrows) { return (size_t)(nrows > 0 ? nrows : 0) * (size_t)((C + 3) & ~3) * 4; }
+size_t xt_compact_bytes(int C, int nrows) { return (size_t)(nrows > 0 ? nrows : 0) * (size_t)xe_pitch(C) * 4; }
 int xt_compact_build(const int32_t* cnt_rows, int C, int nrows, uint32_t* ell, int32_t* row_len, hipStream_t st) {
   if (nrows <= 0) return SA_OK;
   hipLaunchKernelGGL(xt_ell_build_kernel, dim3((unsigned)((nrows + XE_BUILD_ROWS - 1) / XE_BUILD_ROWS)),
@@ -860,7 +964,7 @@ int xt_compact_iterate(const uint32_t* ell, const int32_t* row_len, const int32_
                        double* xo, const int32_t* flag_prev, int32_t* flag_out, hipStream_t st) {
   const int ns = (nrows + XE_S - 1) / XE_S;
   if (ns == 0) return SA_OK;
-  int ct = XE_CT_MAX;  // the quotient table: as many counts as fit next to x
+  int ct = SA_XE_QDIV ? 0 : XE_CT_MAX;  // the quotient table: as many counts as fit next to x
   while (ct > 16 && (size_t)C * 8 + (size_t)XE_S * ct * 8 + XE_LDS_STATIC > XE_LDS_MAX) ct >>= 1;
   hipLaunchKernelGGL(xt_iter_ell_kernel, dim3((unsigned)ns), dim3(XE_THREADS), ((size_t)C + (size_t)XE_S * ct) * 8, st,
                      ell, row_len, cnt_rows, reinterpret_cast<const unsigned long long*>(move), gs, pmove, C, rb,

@@ -137,12 +137,16 @@ def test_compact_iteration_equals_dense(sa, C, r0, nrows):
     _native.check(lib.sa_xt_compact_rows(p(rows), C, nrows, p(ell), p(slen), stream_handle()))
     h = rows.cpu().numpy()
     np.testing.assert_array_equal(slen.cpu().numpy(), (h != 0).sum(axis=1))
-    pe = (C + 3) // 4 * 4  # the compact rows' pitch
+    pe = (C + 127) // 128 * 128  # the compact rows' pitch (whole 128-entry chunks)
     e = ell.cpu().numpy().view(np.uint32).reshape(nrows, pe)
+    k = np.arange(pe)
+    slot = (k & ~127) | (k % 32) << 2 | (k // 32) % 4  # chunk-interleaved: entry k's slot
+    assert np.array_equal(np.sort(slot), k)
     for i in rng.choice(nrows, 5, replace=False):  # row i: its non-zero columns in order, counts
         nz = np.flatnonzero(h[i])
-        np.testing.assert_array_equal(e[i, :len(nz)] & 0xFFFF, nz)
-        np.testing.assert_array_equal(e[i, :len(nz)] >> 16, np.minimum(h[i, nz], 0xFFFF))
+        ei = e[i, slot[:len(nz)]]
+        np.testing.assert_array_equal(ei & 0xFFFF, nz)
+        np.testing.assert_array_equal(ei >> 16, np.minimum(h[i, nz], 0xFFFF))
     for trial in range(3):
         x = torch.rand(C, dtype=torch.float64, device=dev)
         x[torch.from_numpy(rng.random(C) < 0.2).to(dev)] = 0.0
