@@ -213,3 +213,19 @@ def test_interp_codes_rate_equals_rate_interp(sa):
         np.testing.assert_array_equal(a[~np.isnan(a)], b[~np.isnan(a)])
         assert int(e0.item()) == int(e1.item()) == (4 if bad else 0)
         assert bool(acc.err.item()) == bad
+
+
+def test_coresident_16x12_count_full_batch_vs_oracle(sa):
+    """The co-resident count (shared=True: the workgroup shape the bench step's side stream
+    uses next to the VAEP passes) over cfg2's whole 10k-game batch (~16M actions) == the
+    oracle's counts, and == the default launch shape's."""
+    B, ops, syn = sa['batch'], sa['ops'], sa['synthetic']
+    l, w = 16, 12
+    d = syn.spadl_games(10000)
+    ab = B.ActionBatch.from_columns(d)
+    acc = ops.xt_count(ab, l, w, shared=True)
+    ops.xt_check_errors(acc)
+    _same_counts(acc, _oracle(d, l, w), l, w)
+    ref = ops.xt_count(ab, l, w)
+    for a, b in ((acc.shot, ref.shot), (acc.goal, ref.goal), (acc.move, ref.move), (acc.trans, ref.trans)):
+        assert torch.equal(a, b)
