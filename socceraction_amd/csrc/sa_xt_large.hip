@@ -20,11 +20,12 @@
 //    batch (sa_xt_count_from_buckets), so the 204 MB table is written once per fit.
 // 2. Value iteration (xthreat.py:278-320) over a compact form of the counts built once per solve
 //    (sa_xt_compact_rows): each row's non-zero counts in column order, 4 B each (column | count
-//    << 16), contiguous per row.  Per iteration (xt_iter_ell_kernel) eight product waves form
-//    T[r, c] * x[c] = (cnt / move[r]) * x[c] -- the quotient tabulated in LDS for small counts, the
-//    same correctly rounded division -- and one chain wave adds each row's products strictly left
-//    to right (the reference's loop order; zero terms add +0 to a non-negative sum, so skipping
-//    them keeps every bit).  84 MB per iteration instead of the 204 MB dense int32 rows.
+//    << 16), chunk-interleaved per row.  Per iteration (xt_iter_ell_kernel) eight product waves
+//    form T[r, c] * x[c] = (cnt / move[r]) * x[c] -- the correctly rounded quotient from the
+//    row's reciprocal and one fma correction -- and one chain wave adds each row's products
+//    strictly left to right (the reference's loop order; zero terms add +0 to a non-negative sum,
+//    so skipping them keeps every bit).  62.5 MB per cfg5 iteration instead of the 204 MB dense
+//    int32 rows.
 #include <hip/hip_runtime.h>
 
 #include <cstring>
