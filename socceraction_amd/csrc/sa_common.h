@@ -94,6 +94,31 @@ __device__ __forceinline__ int flat_index(double x, double y, int l, int w) {
 
 __device__ __forceinline__ bool is_move(int t) { return t == T_PASS || t == T_DRIBBLE || t == T_CROSS; }
 
+// The binning's quotients x / 105 and y / 68 without a division: y = x * r, r = RN(1 / b), then
+// Markstein's correction y + r * (x - y * b) by two fmas -- the correctly rounded quotient for
+// every x whose quotient is a normal number (scripts/check_quotient.c; 1e9 random doubles over
+// 2^-960..2^960 and [0, 128) against x / b, no mismatch).  Elsewhere it may differ from x / b
+// only where the int64 cast cannot tell (|q| < 2^-1000: cell 0 either way; x = +-inf gives NaN
+// instead of +-inf: both cast to INT64_MIN), so flat_index_q(bin_q...) == flat_index for every
+// double input.
+struct BinQ {
+  double sx, sy, ex, ey;  // start / end coordinates over the field's extent
+};
+__device__ __forceinline__ double bin_quot(double x, double b, double rb) {
+  const double y = x * rb;
+  return __builtin_fma(__builtin_fma(-y, b, x), rb, y);
+}
+__device__ __forceinline__ BinQ bin_q(double sx, double sy, double ex, double ey) {
+  constexpr double RL = 1.0 / FIELD_L, RW = 1.0 / FIELD_W;
+  return BinQ{bin_quot(sx, FIELD_L, RL), bin_quot(sy, FIELD_W, RW), bin_quot(ex, FIELD_L, RL),
+              bin_quot(ey, FIELD_W, RW)};
+}
+__device__ __forceinline__ int flat_index_q(double qx, double qy, int l, int w) {
+  int xi = cell_index(qx * (double)l, l);
+  int yj = cell_index(qy * (double)w, w);
+  return (w - 1 - yj) * l + xi;
+}
+
 // xT cell code of one SPADL action for a fit + rate of the same actions on an (l, w) grid with
 // l * w <= SA_XT_CELLS_MAX_C (include/socceraction_amd.h): written once per action where the
 // coordinates are already in registers (the VAEP feature pass, or sa_xt_cells), read by the
@@ -171,6 +196,20 @@ __device__ __forceinline__ XtAct decode_cell(uint32_t c) {
 }
 
 
+// rate_code / rate_icode from the binning quotients (bin_q of the same coordinates).
+__device__ __forceinline__ uint32_t rate_code_q(int t, int r, double sx, double sy, double ex, double ey,
+                                                const BinQ& q, int l, int w) {
+  if (!is_move(t) || r != R_SUCCESS) return XT_CODE_NAN;
+  if (!isfinite(sx) || !isfinite(sy) || !isfinite(ex) || !isfinite(ey)) return XT_CODE_BAD;
+  return (uint32_t)flat_index_q(q.sx, q.sy, l, w) | ((uint32_t)flat_index_q(q.ex, q.ey, l, w) << 16);
+}
+__device__ __forceinline__ uint64_t rate_icode_q(int t, int r, double sx, double sy, double ex, double ey,
+                                                 const BinQ& q, int L, int W) {
+  if (!is_move(t) || r != R_SUCCESS) return XT_ICODE_NAN;
+  if (!isfinite(sx) || !isfinite(sy) || !isfinite(ex) || !isfinite(ey)) return XT_ICODE_BAD;
+  return (uint64_t)(uint32_t)flat_index_q(q.sx, q.sy, L, W) | ((uint64_t)(uint32_t)flat_index_q(q.ex, q.ey, L, W) << 32);
+}
+
 // The XtAct of one action from its row (the coordinate form of decode_cell; t < 0: not counted).
 __device__ __forceinline__ XtAct act_from_row(int t, int r, double sx, double sy, double ex, double ey, int l,
                                               int w) {
@@ -182,6 +221,20 @@ __device__ __forceinline__ XtAct act_from_row(int t, int r, double sx, double sy
   a.efin = isfinite(ex) && isfinite(ey);
   a.cs = (a.cls && a.sfin) ? flat_index(sx, sy, l, w) : 0;
   a.ce = (a.cls == XT_CELL_MOVE && a.succ && a.efin) ? flat_index(ex, ey, l, w) : 0;
+  return a;
+}
+
+// act_from_row from the binning quotients (bin_q of the same coordinates).
+__device__ __forceinline__ XtAct act_from_row_q(int t, int r, double sx, double sy, double ex, double ey,
+                                                const BinQ& q, int l, int w) {
+  XtAct a;
+  a.cls = t == T_SHOT ? XT_CELL_SHOT : (is_move(t) ? XT_CELL_MOVE : 0u);
+  a.succ = r == R_SUCCESS;
+  a.snan = isnan(sx) || isnan(sy);
+  a.sfin = isfinite(sx) && isfinite(sy);
+  a.efin = isfinite(ex) && isfinite(ey);
+  a.cs = (a.cls && a.sfin) ? flat_index_q(q.sx, q.sy, l, w) : 0;
+  a.ce = (a.cls == XT_CELL_MOVE && a.succ && a.efin) ? flat_index_q(q.ex, q.ey, l, w) : 0;
   return a;
 }
 

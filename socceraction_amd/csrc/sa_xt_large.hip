@@ -44,6 +44,20 @@ namespace sa {
 #define SA_XK_THREADS 1024  // K1 workgroup (two per CU at cfg5: 32 waves of loads in flight)
 #endif
 constexpr int XK_THREADS = SA_XK_THREADS;
+#ifndef SA_XK_NT
+#define SA_XK_NT 3  // bit 0: non-temporal coordinate / id loads in K1, bit 1: non-temporal operand stores
+                    // (read once per fit; cfg5 batch 0.263 -> 0.251 ms, profiles/r04_xt_count_ab.md)
+#endif
+template <typename T>
+__device__ __forceinline__ T xk_ld(const T* p) {
+  if constexpr ((SA_XK_NT & 1) != 0) return __builtin_nontemporal_load(p);
+  return *p;
+}
+template <typename T>
+__device__ __forceinline__ void xk_st(T* p, T v) {
+  if constexpr ((SA_XK_NT & 2) != 0) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
 constexpr int XK_CHUNK = 32768;     // actions per K1 workgroup = key capacity of its region
 constexpr int XS_THREADS = 1024;    // K3 workgroup
 constexpr int XS_PER = XK_CHUNK / XS_THREADS;
@@ -171,10 +185,10 @@ __global__ __launch_bounds__(XK_THREADS) void xt_keys_kernel(sa_actions A, const
         for (int q = 0; q < U / 2; ++q) {
           const int64_t j = base + 2 * ((int64_t)q * XK_THREADS + threadIdx.x);
           const int64_t jc = j + 1 < end ? j : ((end - 2) & ~(int64_t)1);  // a whole aligned pair
-          const f64x2 a = *reinterpret_cast<const f64x2*>(F.c0 + jc), b = *reinterpret_cast<const f64x2*>(F.c1 + jc);
-          const f64x2 c = *reinterpret_cast<const f64x2*>(F.c2 + jc), d = *reinterpret_cast<const f64x2*>(F.c3 + jc);
-          const uint32_t ty = *reinterpret_cast<const uint16_t*>(F.type_id + jc);
-          const uint32_t rs = *reinterpret_cast<const uint16_t*>(F.result_id + jc);
+          const f64x2 a = xk_ld(reinterpret_cast<const f64x2*>(F.c0 + jc)), b = xk_ld(reinterpret_cast<const f64x2*>(F.c1 + jc));
+          const f64x2 c = xk_ld(reinterpret_cast<const f64x2*>(F.c2 + jc)), d = xk_ld(reinterpret_cast<const f64x2*>(F.c3 + jc));
+          const uint32_t ty = xk_ld(reinterpret_cast<const uint16_t*>(F.type_id + jc));
+          const uint32_t rs = xk_ld(reinterpret_cast<const uint16_t*>(F.result_id + jc));
 #pragma unroll
           for (int e = 0; e < 2; ++e) {
             const int u = 2 * q + e;
@@ -211,24 +225,28 @@ __global__ __launch_bounds__(XK_THREADS) void xt_keys_kernel(sa_actions A, const
           ey[u] = F.c3[jc];
         }
       }
+      BinQ bq[U];  // the binning's quotients, once per action for the count and the rate operands
+#pragma unroll
+      for (int u = 0; u < U; ++u) bq[u] = bin_q(sx[u], sy[u], ex[u], ey[u]);
       if (vec) {  // a pair's two operands in one store (16 B: whole lines per instruction)
 #pragma unroll
         for (int q = 0; q < U / 2; ++q) {
           const int u = 2 * q;
           const int64_t j = jj[u];
           if (RO.codes && tt[u] >= 0) {
-            const uint32_t c0 = rate_code(tt[u], rr[u], sx[u], sy[u], ex[u], ey[u], l, w);
+            const uint32_t c0 = rate_code_q(tt[u], rr[u], sx[u], sy[u], ex[u], ey[u], bq[u], l, w);
             if (tt[u + 1] >= 0)
-              *reinterpret_cast<uint2*>(RO.codes + j) =
-                  make_uint2(c0, rate_code(tt[u + 1], rr[u + 1], sx[u + 1], sy[u + 1], ex[u + 1], ey[u + 1], l, w));
+              *reinterpret_cast<uint2*>(RO.codes + j) = make_uint2(
+                  c0, rate_code_q(tt[u + 1], rr[u + 1], sx[u + 1], sy[u + 1], ex[u + 1], ey[u + 1], bq[u + 1], l, w));
             else
               RO.codes[j] = c0;
           }
           if (RO.icodes && tt[u] >= 0) {
-            const uint64_t c0 = rate_icode(tt[u], rr[u], sx[u], sy[u], ex[u], ey[u], RO.L, RO.W);
+            const uint64_t c0 = rate_icode_q(tt[u], rr[u], sx[u], sy[u], ex[u], ey[u], bq[u], RO.L, RO.W);
             if (tt[u + 1] >= 0)
-              *reinterpret_cast<u64x2*>(RO.icodes + j) =
-                  u64x2{c0, rate_icode(tt[u + 1], rr[u + 1], sx[u + 1], sy[u + 1], ex[u + 1], ey[u + 1], RO.L, RO.W)};
+              xk_st(reinterpret_cast<u64x2*>(RO.icodes + j),
+                    u64x2{c0, rate_icode_q(tt[u + 1], rr[u + 1], sx[u + 1], sy[u + 1], ex[u + 1], ey[u + 1], bq[u + 1],
+                                           RO.L, RO.W)});
             else
               RO.icodes[j] = c0;
           }
@@ -237,13 +255,13 @@ __global__ __launch_bounds__(XK_THREADS) void xt_keys_kernel(sa_actions A, const
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           const int64_t j = jj[u];
-          if (RO.codes && tt[u] >= 0) RO.codes[j] = rate_code(tt[u], rr[u], sx[u], sy[u], ex[u], ey[u], l, w);
+          if (RO.codes && tt[u] >= 0) RO.codes[j] = rate_code_q(tt[u], rr[u], sx[u], sy[u], ex[u], ey[u], bq[u], l, w);
           if (RO.icodes && tt[u] >= 0)
-            RO.icodes[j] = rate_icode(tt[u], rr[u], sx[u], sy[u], ex[u], ey[u], RO.L, RO.W);
+            RO.icodes[j] = rate_icode_q(tt[u], rr[u], sx[u], sy[u], ex[u], ey[u], bq[u], RO.L, RO.W);
         }
       }
 #pragma unroll
-      for (int u = 0; u < U; ++u) act[u] = act_from_row(tt[u], rr[u], sx[u], sy[u], ex[u], ey[u], l, w);
+      for (int u = 0; u < U; ++u) act[u] = act_from_row_q(tt[u], rr[u], sx[u], sy[u], ex[u], ey[u], bq[u], l, w);
     }
     uint32_t key[U];
     bool has[U];
@@ -407,25 +425,80 @@ __global__ __launch_bounds__(XB_THREADS) void xt_band_count_kernel(XbSets sets, 
   const int orow = r0 - band0 * S.R;  // the band's first row in the outputs
   for (int e = 4 * threadIdx.x; e < nr * P; e += 4 * XB_THREADS) *reinterpret_cast<u32x4*>(h + e) = u32x4{0, 0, 0, 0};
   if (threadIdx.x < XB_MAX_ROWS) msum[threadIdx.x] = 0;
+  // the band's keys, set after set, in tiles of XB_U keys per thread, two tiles in flight (the
+  // next tile's loads are issued before the current tile's LDS atomics; one tile at a time
+  // waited out a memory latency per 4 keys and per set: 148 us per cfg5 table pass).  Set
+  // bounds and key pointers in LDS (global address space: no FLAT loads, whose lgkmcnt would
+  // tie them to the LDS reads)
+  typedef const uint32_t __attribute__((address_space(1)))* gkeys;
+  __shared__ gkeys kb[XB_MAX_SETS];
+  __shared__ int64_t klo[XB_MAX_SETS], khi[XB_MAX_SETS];
+  const int ns = sets.n;
+  if (threadIdx.x < ns) {
+    kb[threadIdx.x] = (gkeys)sets.keys[threadIdx.x];
+    klo[threadIdx.x] = sets.off[threadIdx.x][lb];
+    khi[threadIdx.x] = sets.off[threadIdx.x][lb + 1];
+  }
   __syncthreads();
-  for (int s = 0; s < sets.n; ++s) {
-    const uint32_t* kp = sets.keys[s];
-    const int64_t lo = sets.off[s][lb], hi = sets.off[s][lb + 1];
-    for (int64_t i = lo + threadIdx.x; i < hi; i += 4 * XB_THREADS) {
-      uint32_t v[4];
+  constexpr int XB_U = 16;
+  constexpr int64_t XB_TILE = (int64_t)XB_U * XB_THREADS;
+  auto skip_empty = [&](int& ts, int64_t& ti) {  // (ts, ti): a tile of set ts from key ti; ts == ns: none
+    while (ts < ns && klo[ts] >= khi[ts]) ++ts;
+    if (ts < ns) ti = klo[ts];
+  };
+  auto next_tile = [&](int& ts, int64_t& ti) {
+    if (ts >= ns) return;
+    ti += XB_TILE;
+    if (ti >= khi[ts]) {
+      ++ts;
+      skip_empty(ts, ti);
+    }
+  };
+  auto load = [&](uint32_t (&v)[XB_U], int ts, int64_t ti) {
+    if (ts >= ns) {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int64_t j = i + u * XB_THREADS;
-        v[u] = j < hi ? kp[j] : XB_NONE;
-      }
+      for (int u = 0; u < XB_U; ++u) v[u] = XB_NONE;
+      return;
+    }
+    const gkeys kp = kb[ts];
+    const int64_t hi = khi[ts];
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
-        if (v[u] != XB_NONE) {
+    for (int u = 0; u < XB_U; ++u) {
+      const int64_t j = ti + u * XB_THREADS + threadIdx.x;
+      v[u] = j < hi ? kp[j] : XB_NONE;
+    }
+  };
+  auto count = [&](const uint32_t (&v)[XB_U]) {
+#pragma unroll
+    for (int u = 0; u < XB_U; ++u)
+      if (v[u] != XB_NONE) {
           const int row = (int)(v[u] >> 16) - r0, slot = (int)(v[u] & 0xFFFFu);
           SA_DGUARD(row >= 0 && row < nr && slot < C + 3, v[u], continue);
           atomicAdd(&h[row * P + slot], 1u);
         }
-    }
+  };
+  int sa = 0, sb;
+  int64_t ia = 0, ib;
+  skip_empty(sa, ia);
+  sb = sa;
+  ib = ia;
+  next_tile(sb, ib);
+  uint32_t va[XB_U], vb[XB_U];
+  load(va, sa, ia);
+  load(vb, sb, ib);
+  for (;;) {  // slots a / b alternate (no register copy of a load in flight)
+    if (sa >= ns) break;
+    count(va);
+    sa = sb;
+    ia = ib;
+    next_tile(sa, ia);
+    load(va, sa, ia);
+    if (sb >= ns) break;
+    count(vb);
+    sb = sa;
+    ib = ia;
+    next_tile(sb, ib);
+    load(vb, sb, ib);
   }
   __syncthreads();
   const int lane = threadIdx.x & 63;

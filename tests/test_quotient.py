@@ -1,6 +1,7 @@
 """The compact xT iteration's quotient (xt_iter_ell_kernel, SA_XE_QDIV): cnt / move formed as a
 reciprocal product plus one fma correction must be the IEEE quotient bit for bit (the reference
-divides, xthreat.py:_get_transition_matrix).  scripts/check_quotient.c checks the identity on
+divides, xthreat.py:_get_transition_matrix); so must the binning's x / 105 and y / 68 (bin_quot,
+sa_common.h; xthreat.py:_get_cell_indexes).  scripts/check_quotient.c checks the identity on
 the host in double arithmetic -- the same operations the kernel issues (v_rcp-free division for
 the reciprocal, v_mul_f64, two v_fma_f64).  A reduced sweep here; the full one (every count
 < 65536 x 12001 divisors + 4e8 random pairs) is the program's default."""
