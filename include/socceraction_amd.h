@@ -37,7 +37,7 @@ extern "C" {
 #endif
 
 #define SA_ABI_VERSION 3
-#define SA_MAX_FRAMES 8 /* max nb_prev_actions (window frames) */
+#define SA_MAX_FRAMES 8 /* max frames n_frames == k of explicit-frame mode (windowed mode: any k) */
 #define SA_BOOL_TILE_QUANTUM 1024 /* bool block: rows per tile must be a multiple of this */
 #define SA_NUM_TILE_QUANTUM 128   /* f64 / i64 blocks: rows per tile must be a multiple of this */
 

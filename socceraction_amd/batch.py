@@ -142,6 +142,7 @@ class ActionBatch:
             self.cols[k] = self.buffer[o:o + a.nbytes].view(torch.from_numpy(a[:0]).dtype) \
                 if a.nbytes else torch.empty(0, dtype=torch.from_numpy(a[:0]).dtype, device=dev)
         self.device = dev
+        self._seg_blocks()  # now, on the stream that copied seg_off: struct() never launches
 
     # ------------------------------------------------------------------ constructors
     @classmethod
@@ -211,6 +212,7 @@ class ActionBatch:
             self.cols['home'] = home
         self.buffer = None
         self.device = seg_off.device
+        self._seg_blocks()  # now, on the stream that wrote seg_off (the caller's current one)
         return self
 
     # ------------------------------------------------------------------ C structs
@@ -224,7 +226,10 @@ class ActionBatch:
 
     def _seg_blocks(self) -> Optional[int]:
         """Device pointer of the segment of every SA_SEG_BLOCK-row block (``sa_segment_blocks``),
-        built once per batch, or None for a single segment (nothing to search)."""
+        or None for a single segment (nothing to search).  Built once, when the batch is made, on
+        the stream current then (the one that wrote seg_off), and host-synchronised there, so any
+        stream may read it and struct() -- called inside timed regions and under other streams --
+        never launches or synchronises."""
         if self.n_segments <= 1 or self.n == 0:
             return None
         t = self.cols.get('seg_of_block')
