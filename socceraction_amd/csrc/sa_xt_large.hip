@@ -60,7 +60,12 @@ __device__ __forceinline__ void xk_st(T* p, T v) {
 }
 constexpr int XK_CHUNK = 32768;     // actions per K1 workgroup = key capacity of its region
 constexpr int XS_THREADS = 1024;    // K3 workgroup
-constexpr int XS_PER = XK_CHUNK / XS_THREADS;
+#ifndef SA_XS_SPLIT
+#define SA_XS_SPLIT 1  // K3 workgroups per K1 region (2 / 4 parts: two per CU, slower; r04_xt_count_ab.md)
+#endif
+constexpr int XS_SPLIT = SA_XS_SPLIT;
+constexpr int XS_PART = XK_CHUNK / XS_SPLIT;  // keys per K3 workgroup
+constexpr int XS_PER = XS_PART / XS_THREADS;
 constexpr int XB_THREADS = 1024;    // K4 workgroup
 #ifndef SA_XB_RMAX
 #define SA_XB_RMAX 8  // start cells per band at most (105 x 68: 5 = the most 160 KB of LDS holds)
@@ -71,8 +76,8 @@ constexpr int XB_NB_MAX = 4000;     // bands (K3 holds 2 words per band + a regi
 constexpr size_t XB_LDS_MAX = 160 * 1024;
 constexpr int XB_MAX_SETS = 24;     // buckets per K4 launch
 constexpr uint32_t XB_NONE = 0xFFFFFFFFu;
-static_assert(XS_PER * XS_THREADS == XK_CHUNK, "K3 holds one K1 region");
-static_assert(XK_CHUNK * 4 + 2 * XB_NB_MAX * 4 + 256 <= XB_LDS_MAX, "K3 LDS");
+static_assert(XS_PER * XS_THREADS * XS_SPLIT == XK_CHUNK && XS_PER >= 1, "K3 holds one part of a K1 region");
+static_assert(XS_PART * 4 + 2 * XB_NB_MAX * 4 + 256 <= XB_LDS_MAX, "K3 LDS");
 
 struct XbShape {
   int C;           // cells
@@ -344,7 +349,7 @@ __global__ __launch_bounds__(1024) void xt_band_scan_kernel(uint32_t* __restrict
   if (threadIdx.x == 0) band_off[NB] = total;
 }
 
-// K3: one workgroup per K1 region.  Its keys (<= XK_CHUNK, 32 per thread in registers) are ranked
+// K3: XS_SPLIT workgroups per K1 region, one per part of its keys (<= XS_PART, XS_PER per thread in registers), ranked
 // within their band by LDS atomics, each band's run gets its place in the band's bucket by ONE
 // global atomic on the band cursor, the keys are sorted by band in LDS, and thread i writes the
 // sorted key i -- consecutive threads of a run write consecutive words.
@@ -355,10 +360,12 @@ __global__ __launch_bounds__(XS_THREADS) void xt_keys_scatter_kernel(const uint3
   extern __shared__ uint32_t sm[];
   uint32_t* bh = sm;              // [NB] keys per band, then the local run offsets
   uint32_t* bb = sm + S.NB;       // [NB] the runs' places in the buckets
-  uint32_t* sorted = sm + 2 * S.NB;  // [XK_CHUNK]
+  uint32_t* sorted = sm + 2 * S.NB;  // [XS_PART]
   __shared__ uint32_t ws[17];
-  const uint32_t cnt = region_cnt[blockIdx.x];
-  const uint32_t* in = keys + (int64_t)blockIdx.x * XK_CHUNK;
+  const int region = blockIdx.x / XS_SPLIT, part = blockIdx.x % XS_SPLIT;
+  const uint32_t rc = region_cnt[region], p0 = (uint32_t)part * XS_PART;
+  const uint32_t cnt = rc > p0 ? min(rc - p0, (uint32_t)XS_PART) : 0u;
+  const uint32_t* in = keys + (int64_t)region * XK_CHUNK + p0;
   for (int b = threadIdx.x; b < S.NB; b += XS_THREADS) bh[b] = 0;
   uint32_t k[XS_PER], rk[XS_PER];
 #pragma unroll
@@ -968,9 +975,9 @@ static int bucket_batch(const sa_actions& A, const uint32_t* cells, int64_t n, i
     rc = check_launch("xt_band_scan_kernel");
   }
   if (!rc) {
-    const size_t lds = ((size_t)2 * S.NB + XK_CHUNK) * 4;
-    hipLaunchKernelGGL(xt_keys_scatter_kernel, dim3((unsigned)regions), dim3(XS_THREADS), lds, st, keys, region_cnt,
-                       S, cursor, buckets);
+    const size_t lds = ((size_t)2 * S.NB + XS_PART) * 4;
+    hipLaunchKernelGGL(xt_keys_scatter_kernel, dim3((unsigned)(regions * XS_SPLIT)), dim3(XS_THREADS), lds, st, keys,
+                       region_cnt, S, cursor, buckets);
     rc = check_launch("xt_keys_scatter_kernel");
   }
   scratch_release(sc, st);
