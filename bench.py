@@ -449,7 +449,7 @@ def atomic_extra(dist, rank, world, dev, games: int, reps: int = 21, check: bool
 
 def xt105_extra(ab, dist, dev, sharded: bool = False, cfg5_games: int = 62500,
                 rank: int = 0, world: int = 1, step_games: int = 10000, d=None,
-                check: bool = True, reps: int = 21) -> dict:
+                check: bool = True, reps: int = 21, solve: str = 'compact') -> dict:
     """BASELINE cfg5 alongside the main line: xT 105x68 fit of cfg5's 62,500 games (≈1.0e8
     actions; split over the ranks, so this entry scales strongly) -- count pass over this
     rank's games, RCCL all-reduce of the 7140-cell count vectors and 204 MB transition counts,
@@ -494,7 +494,8 @@ def xt105_extra(ab, dist, dev, sharded: bool = False, cfg5_games: int = 62500,
         if sharded and dist is not None:  # band-sharded: all-to-all of the counted actions,
             mark()                         # each rank counts its bands; row-sharded iteration
             mark()  # (count and exchange happen inside the sharded fit)
-            mats, _, n_iter, err = shard.xt_fit_bands_sharded(batches, l, w, interp_codes=icodes)
+            mats, _, n_iter, err = shard.xt_fit_bands_sharded(batches, l, w, interp_codes=icodes,
+                                                              solve=solve)
             acc = None  # each rank holds only its row block of the transition counts
         else:  # one all-reduce of the counts, replicated solve
             acc = ops.xt_count_many(batches, l, w, interp_codes=icodes)
@@ -565,7 +566,9 @@ def xt105_extra(ab, dist, dev, sharded: bool = False, cfg5_games: int = 62500,
                       f'min {min(times) * 1e3:.3f}, max {max(times) * 1e3:.3f} ms on rank {rank})'
                       + ('; max over ranks' if dist is not None else ''),
             'scaling': 'strong' if cfg5_games > 0 else 'weak',
-            'solve': ('band-sharded (all-to-all of counted actions, row-sharded iteration)'
+            'solve': (('band-sharded (all-to-all of counted actions, '
+                       + ('compact rows all-gathered once, replicated iteration)' if solve == 'compact'
+                          else 'row-sharded iteration)'))
                       if (sharded and dist is not None) else 'replicated'),
             'phases_ms': dict(phases, note='one extra call synchronised between phases (rank '
                               f'{rank}): count = band buckets + table; exchange = the counts\' '
@@ -770,12 +773,14 @@ def main() -> None:
     ap.add_argument('--cfg5-games', type=int, default=62500,
                     help='games of the cfg5 side entry (BASELINE cfg5: 62,500 = 1.0e8 actions, '
                          'split over the ranks; 0 = the step batch)')
-    ap.add_argument('--cfg5-solve', default='auto', choices=('auto', 'sharded', 'replicated'),
-                    help='cfg5 with N > 1: "sharded" = each rank counts and iterates its own '
-                         'start-cell bands after ONE all-to-all of the counted actions '
-                         '(shard.xt_fit_bands_sharded); "replicated" = one all-reduce of the '
-                         '204 MB count table and the whole solve on every rank; auto = sharded '
-                         '(the projection in DESIGN.md §6)')
+    ap.add_argument('--cfg5-solve', default='auto', choices=('auto', 'sharded', 'sharded-rows', 'replicated'),
+                    help='cfg5 with N > 1: "sharded" = each rank counts its own start-cell bands '
+                         'after ONE all-to-all of the counted actions, then one all-gather of the '
+                         'compact count rows and the iteration on every rank '
+                         '(shard.xt_fit_bands_sharded); "sharded-rows" = the same count, each rank '
+                         'iterating its own rows with an all-gather of x per iteration; '
+                         '"replicated" = one all-reduce of the 204 MB count table and the whole '
+                         'solve on every rank; auto = sharded (the projection in DESIGN.md §6)')
     ap.add_argument('--xt-sharded', action='store_true', help='same as --cfg5-solve sharded')
     ap.add_argument('--atomic-games', type=int, default=10000,
                     help='atomic games of the cfg3 side entry, split over the ranks (BASELINE '
@@ -1088,9 +1093,11 @@ def main() -> None:
         check_s = time.perf_counter() - tc
     extra_side = {}
     if not args.no_side:
-        cfg5_sharded = args.xt_sharded or args.cfg5_solve in ('auto', 'sharded')
+        cfg5_sharded = args.xt_sharded or args.cfg5_solve in ('auto', 'sharded', 'sharded-rows')
         extra_side['xt105_cfg5'] = xt105_extra(ab, dist, dev, cfg5_sharded, args.cfg5_games,
-                                               rank, world, args.games, d=d, check=check)
+                                               rank, world, args.games, d=d, check=check,
+                                               solve='rows' if args.cfg5_solve == 'sharded-rows'
+                                               else 'compact')
         extra_side['atomic_cfg3'] = atomic_extra(dist, rank, world, dev, args.atomic_games,
                                                  check=check)
         extra_side['convert_to_atomic'] = convert_extra(d, dist, dev)

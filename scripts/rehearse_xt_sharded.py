@@ -31,8 +31,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--games', type=int, default=400, help='games per rank')
     ap.add_argument('--grid', default='105x68', help='l x w cells')
-    ap.add_argument('--mode', default='auto', choices=('auto', 'bands', 'rows'),
-                    help='bands: shard.xt_fit_bands_sharded (all-to-all of the counted actions); '
+    ap.add_argument('--mode', default='auto', choices=('auto', 'bands', 'bands-rows', 'rows'),
+                    help='bands: shard.xt_fit_bands_sharded (all-to-all of the counted actions, '
+                         'the compact rows all-gathered once); bands-rows: the same count, '
+                         'row-sharded iteration; '
                          'rows: xt_solve_sharded (reduce-scatter of the count table); auto: bands '
                          'where the band-owned count holds the grid')
     args = ap.parse_args()
@@ -54,8 +56,9 @@ def main():
         mode = 'bands' if ops.xt_band_shape(l, w) is not None else 'rows'
 
     def fit():
-        if mode == 'bands':
-            mats, heat, iters, err = shard.xt_fit_bands_sharded([ab], l, w)
+        if mode in ('bands', 'bands-rows'):
+            mats, heat, iters, err = shard.xt_fit_bands_sharded(
+                [ab], l, w, solve='rows' if mode == 'bands-rows' else 'compact')
             assert int(err.item()) == 0
             return mats, heat, iters
         acc = ops.xt_zero_counts(l, w, dev, row_blocks=world)

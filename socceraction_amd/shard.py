@@ -205,7 +205,7 @@ def _solve_row_block(rows, shot, goal, move, C: int, B: int, eps: float, max_ite
 
 
 def xt_fit_bands_sharded(batches, l: int, w: int, eps: float = 1e-5, max_iter: int = 1000,
-                         group=None, batch: int = 8, interp_codes=None):
+                         group=None, batch: int = 8, interp_codes=None, solve: str = 'compact'):
     """Band-sharded xT fit (cfg5 over several GPUs) for grids the band-owned count holds
     (``ops.xt_band_shape``, e.g. 105 x 68): the ranks exchange their COUNTED ACTIONS, not count
     tables.  Rank r owns the start-cell bands [b0, b1) = ``band_ranges(NB, world)[r]``, i.e.
@@ -220,8 +220,14 @@ def xt_fit_bands_sharded(batches, l: int, w: int, eps: float = 1e-5, max_iter: i
        ``xt_solve_sharded`` would leave it;
     4. one all-gather of the shot / goal / move counts of every rank's rows and a max all-reduce
        of the error flags;
-    5. the row-sharded value iteration of ``xt_solve_sharded`` (compact rows, one all-gather of x
-       per iteration): every value bit-identical to the single-GPU fit of all ranks' actions.
+    5. ``solve='compact'`` (default): each rank builds the compact form of its rows
+       (``sa_xt_compact_rows``), one all-gather of those rows' non-zero entries (62.5 MB in all at
+       cfg5) gives every rank the whole compact form, and every rank iterates all rows with no
+       further exchange (``_solve_compact_exchange``; falls back to 'rows' when some count
+       reaches 65535: escaped entries are read from the dense row, which only its owner holds);
+       ``solve='rows'``: the row-sharded value iteration of ``xt_solve_sharded`` (one
+       all-gather of x per iteration).  Either way every value is bit-identical to the
+       single-GPU fit of all ranks' actions.
 
     ``interp_codes``: one ``ops.xt_interp_codes_buffer`` per batch, filled for the rate.
     Returns ``(mats [4, C], heatmaps [n_iter + 1, C], n_iter, err)``; ``err`` is the error-flag
@@ -262,9 +268,91 @@ def xt_fit_bands_sharded(batches, l: int, w: int, eps: float = 1e-5, max_iter: i
     _all_gather(allv.reshape(-1), vec.reshape(-1), group=group)
     full = allv.permute(1, 0, 2).reshape(3, W * B)[:, :C].contiguous()
     _all_reduce(err, dist.ReduceOp.MAX, group=group)  # the error bytes of every rank
-    mats, heat, iters = _solve_row_block(rows, full[0], full[1], full[2], C, B, eps, max_iter,
-                                         group, batch)
+    if solve not in ('compact', 'rows'):
+        raise ValueError("solve must be 'compact' or 'rows'")
+    res = None
+    if solve == 'compact' and C <= _native.SA_XT_COMPACT_MAX_C:
+        res = _solve_compact_exchange(rows, full[0], full[1], full[2], C, B, eps, max_iter, group, batch)
+    if res is None:
+        res = _solve_row_block(rows, full[0], full[1], full[2], C, B, eps, max_iter, group, batch)
+    mats, heat, iters = res
     return mats, heat, iters, err
+
+
+def _solve_compact_exchange(rows, shot, goal, move, C: int, B: int, eps: float, max_iter: int,
+                            group, batch: int):
+    """Step 5 of :func:`xt_fit_bands_sharded` with ``solve='compact'``: this rank holds the
+    count rows [r B, r B + B) (``rows``); returns None (nothing exchanged) when a count of any
+    rank reaches 65535, else ``(mats, heatmaps, n_iter)`` of the replicated iteration over the
+    gathered compact form.  The compact rows are exchanged as their used chunks only: row i's
+    first ceil(len_i / 128) * 128 slots (the chunk-interleaved layout of ``sa_xt_compact_rows``,
+    header), packed per rank in row order; the ranks' row blocks are consecutive, so the
+    gathered packs unpack into the full form in rank order."""
+    import torch.distributed as dist
+
+    from . import _native
+    from .batch import stream_handle
+    W = dist.get_world_size(group)
+    r = dist.get_rank(group)
+    dev = rows.device
+    lib = _native.lib()
+    ptr = lambda t: t.data_ptr()  # noqa: E731
+    r0 = r * B
+    nrows = max(0, min(B, C - r0))
+    big = torch.zeros(1, dtype=torch.int32, device=dev)
+    if nrows:
+        big[0] = (rows[:nrows * C].max() >= 65535).to(torch.int32)
+    _all_reduce(big, dist.ReduceOp.MAX, group=group)
+    if int(big.item()):
+        return None
+    pe = int(lib.sa_xt_compact_bytes(C, 1)) // 4  # slots per compact row
+    ell = torch.empty(max(nrows, 1) * pe, dtype=torch.int32, device=dev)
+    slen = torch.zeros(B, dtype=torch.int32, device=dev)
+    if nrows:
+        _native.check(lib.sa_xt_compact_rows(ptr(rows), C, nrows, ptr(ell), ptr(slen), stream_handle()))
+    lens = torch.empty(W * B, dtype=torch.int32, device=dev)
+    _all_gather(lens, slen, group=group)
+    lens = lens[:C].contiguous()
+    used = (lens.to(torch.int64) + 127) // 128 * 128  # slots each row occupies
+    per_rank = torch.nn.functional.pad(used, (0, W * B - C)).view(W, B).sum(dim=1)
+    tot = per_rank.cpu().numpy()
+    mx = max(int(tot.max()), 1)
+    k = torch.arange(pe, device=dev)
+    send = torch.zeros(mx, dtype=torch.int32, device=dev)
+    if nrows:
+        packed = ell[:nrows * pe].view(nrows, pe)[k[None, :] < used[r0:r0 + nrows, None]]
+        send[:packed.numel()] = packed
+    recv = torch.empty(W * mx, dtype=torch.int32, device=dev)
+    _all_gather(recv, send, group=group)
+    full = torch.zeros(C * pe, dtype=torch.int32, device=dev)
+    full.view(C, pe)[k[None, :] < used[:, None]] = torch.cat(
+        [recv[q * mx:q * mx + int(tot[q])] for q in range(W)])
+    del recv, send, ell
+    mats = torch.empty((4, C), dtype=torch.float64, device=dev)
+    gp = torch.empty((2, C), dtype=torch.float64, device=dev)
+    _native.check(lib.sa_xt_probabilities(ptr(shot), ptr(goal), ptr(move), C, ptr(mats), ptr(gp[0]),
+                                          ptr(gp[1]), stream_handle()))
+    heat = torch.zeros((max_iter + 1, C), dtype=torch.float64, device=dev)
+    flags = torch.zeros(max_iter + 1, dtype=torch.int32, device=dev)
+    iters = -1
+    it0 = 0
+    while it0 < max_iter and iters < 0:
+        it1 = min(it0 + batch, max_iter)
+        for it in range(it0, it1):
+            # cnt_rows: read for counts >= 65535 only, which no rank has (checked above)
+            _native.check(lib.sa_xt_iterate_compact(
+                ptr(full), ptr(lens), ptr(rows), ptr(move), ptr(gp[0]), ptr(gp[1]), C, 0, C,
+                ptr(heat[it]), float(eps), ptr(heat[it + 1]), ptr(flags[it - 1:]) if it else None,
+                ptr(flags[it:]), stream_handle()))
+        hf = flags[it0:it1].cpu().numpy()
+        done = np.flatnonzero(hf == 0)
+        if len(done):
+            iters = it0 + int(done[0]) + 1
+        it0 = it1
+    if iters < 0:
+        raise RuntimeError(f'xT value iteration did not converge within {max_iter} iterations')
+    mats[3].copy_(heat[iters])
+    return mats, heat[:iters + 1], iters
 
 
 def exchange_band_keys(parts, n_bands: int, group=None, dev=None):

@@ -28,11 +28,12 @@ def test_bench_gpus_2_launches_two_ranks():
     assert 0 < out['roofline']['step_frac'] < 1
 
 
-@pytest.mark.parametrize('solve', ['sharded', 'replicated'])
+@pytest.mark.parametrize('solve', ['sharded', 'sharded-rows', 'replicated'])
 def test_bench_gpus_2_side_entries(solve):
     """The side entries under two ranks: cfg5's and cfg3's games split over the ranks; cfg5's
     fit band-sharded (the default for N > 1: all-to-all of the counted actions, each rank counting
-    and iterating its own bands) or replicated (all-reduce of the count table), its parity block
+    its own bands, then the compact rows all-gathered once, or each rank iterating its own rows)
+    or replicated (all-reduce of the count table), its parity block
     (counts or surface, iterations, rates vs the oracle) ok either way."""
     env = dict(os.environ, SA_DIST_BACKEND='gloo')
     env.pop('WORLD_SIZE', None)
@@ -46,7 +47,9 @@ def test_bench_gpus_2_side_entries(solve):
     assert out['n_gpus'] == 2
     x = out['xt105_cfg5']
     assert x['actions_total'] > x['actions_per_gpu'] > 0 and x['iterations'] > 0
-    assert x['solve'].startswith('band-sharded' if solve == 'sharded' else 'replicated')
+    assert x['solve'].startswith('replicated' if solve == 'replicated' else 'band-sharded')
+    if solve != 'replicated':
+        assert ('row-sharded' in x['solve']) == (solve == 'sharded-rows')
     assert x['parity']['ok'] and x['parity']['values_checked'] > 0
     a = out['atomic_cfg3']
     assert a['atomic_actions_total'] > a['atomic_actions_per_gpu'] > 0

@@ -279,14 +279,15 @@ def test_xt_large_grid_multi_launch_solver():
         np.testing.assert_array_equal(m.xT, f['xT'])
 
 
-@pytest.mark.parametrize('grid,mode', [('105x68', 'bands'), ('105x68', 'rows'), ('40x30', 'bands'),
-                                       ('16x12', 'rows')])
+@pytest.mark.parametrize('grid,mode', [('105x68', 'bands'), ('105x68', 'bands-rows'), ('105x68', 'rows'),
+                                       ('40x30', 'bands'), ('16x12', 'rows')])
 def test_xt_row_sharded_solve_two_ranks(grid, mode):
     """The row-sharded fits with two ranks over gloo on this GPU, each counting its own games,
     reproduce bit for bit the single-GPU fit of all the games (matrices, heatmaps, iteration
     count): shard.xt_solve_sharded (rows: all-reduce of the count vectors, reduce-scatter of the
-    transition rows) and shard.xt_fit_bands_sharded (bands: all-to-all of the counted actions,
-    each rank counting its own bands), both with a per-iteration all-gather of x.  The ranks run
+    transition rows) and shard.xt_fit_bands_sharded (all-to-all of the counted actions, each
+    rank counting its own bands; bands: the compact rows all-gathered once and every rank
+    iterating all rows; bands-rows: a per-iteration all-gather of x).  The ranks run
     as child processes of torch.distributed.run (scripts/rehearse_xt_sharded.py checks and
     prints the verdict)."""
     import json
@@ -296,7 +297,7 @@ def test_xt_row_sharded_solve_two_ranks(grid, mode):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ, SA_DIST_BACKEND='gloo', MASTER_ADDR='127.0.0.1')
     port = 29600 + (os.getpid() % 200) + 211 * ['105x68bands', '105x68rows', '40x30bands',
-                                                '16x12rows'].index(grid + mode)
+                                                '16x12rows', '105x68bands-rows'].index(grid + mode)
     cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '2',
            '--master-addr', '127.0.0.1', '--master-port', str(port),
            os.path.join(root, 'scripts', 'rehearse_xt_sharded.py'), '--games', '40', '--grid', grid,
