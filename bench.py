@@ -417,7 +417,13 @@ def atomic_extra(dist, rank, world, dev, games: int, reps: int = 21, check: bool
     first = rank * (games // world) + min(rank, games % world)
     d = synthetic.atomic_games(mine, game_id0=first)
     ab = B.ActionBatch.from_columns(d, atomic=True, dev=dev)
-    out = ops.features(ab, ATOMIC_DEFAULT, 3, bool_tile=1024, num_tile=128)
+    # the bool block in physically contiguous VRAM, as the main step's (the bool
+    # pass is sensitive to its address translations; from the caching allocator its time
+    # followed the allocations placed before it: 3.80 vs 3.41 - 3.43 ms per step on one box,
+    # profiles/r04_cfg3_contig_ab.json)
+    plan = catalog.build_plan(ATOMIC_DEFAULT, 3, True)
+    out = ops.alloc_feature_blocks(plan, ab.n, dev, 1024, 128, contiguous=True)
+    ops.features(ab, ATOMIC_DEFAULT, 3, out=out, bool_tile=1024, num_tile=128)
     lab = ops.labels(ab)
 
     s = ab.struct()
