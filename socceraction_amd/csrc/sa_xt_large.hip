@@ -44,6 +44,10 @@ namespace sa {
 #define SA_XK_THREADS 1024  // K1 workgroup (two per CU at cfg5: 32 waves of loads in flight)
 #endif
 constexpr int XK_THREADS = SA_XK_THREADS;
+#ifndef SA_XK_U
+#define SA_XK_U 4  // K1 actions per thread per pass (coordinates; even)
+#endif
+static_assert(SA_XK_U >= 2 && SA_XK_U % 2 == 0 && SA_XK_U <= 16, "SA_XK_U");
 #ifndef SA_XK_NT
 #define SA_XK_NT 3  // bit 0: non-temporal coordinate / id loads in K1, bit 1: non-temporal operand stores
                     // (read once per fit; cfg5 batch 0.263 -> 0.251 ms, profiles/r04_xt_count_ab.md)
@@ -164,7 +168,7 @@ __global__ __launch_bounds__(XK_THREADS) void xt_keys_kernel(sa_actions A, const
   const sa_frame& F = A.frames[0];
   const int lane = threadIdx.x & 63;
   int32_t bad = 0;
-  constexpr int U = CELLS ? 8 : 4;  // actions per thread per pass, every load issued first
+  constexpr int U = CELLS ? 8 : SA_XK_U;  // actions per thread per pass, every load issued first
   for (int64_t base = begin; base < end; base += (int64_t)U * XK_THREADS) {  // wave-uniform bound
     XtAct act[U];
     if (CELLS) {
