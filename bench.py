@@ -310,11 +310,24 @@ def oracle_counts(d, l: int, w: int, dist=None, dev=None, acc: dict = None) -> d
     return cnt
 
 
-def check_xt(par: Parity, cnt: dict, acc, xT_dev, n_iter: int, l: int, w: int) -> np.ndarray:
+def check_surface(par: Parity, tag: str, got: np.ndarray, ref: np.ndarray, rtol: float) -> None:
+    """The xT surface: bit for bit (rtol 0: the reference's summation order), or within rtol
+    relative (the large grids' reordered sums, whose iteration count is still checked exactly);
+    the largest relative difference goes into the parity record."""
+    par.values += ref.size
+    err = np.abs(got - ref)
+    rel = float(np.max(np.where(err == 0, 0.0, err / np.maximum(np.abs(ref), 1e-300)))) if ref.size else 0.0
+    par.surface_rel_err = max(getattr(par, 'surface_rel_err', 0.0), rel)
+    if got.shape != ref.shape or (np.isnan(got) != np.isnan(ref)).any() or rel > rtol:
+        par._fail(f'{tag} surface')
+
+
+def check_xt(par: Parity, cnt: dict, acc, xT_dev, n_iter: int, l: int, w: int,
+             rtol: float = 0.0) -> np.ndarray:
     """xT fit (xthreat.py:322-345): the counts the device solved from (all ranks' counts after
-    the all-reduce) == the oracle's counts of the same actions, bit for bit; the device surface
-    and iteration count == the oracle's value iteration over them (xthreat.py:278-320), bit for
-    bit. Returns the oracle surface."""
+    the all-reduce) == the oracle's counts of the same actions, bit for bit; the iteration count
+    == the oracle's value iteration over them (xthreat.py:278-320), the surface bit for bit
+    (``rtol`` 0) or within ``rtol`` relative. Returns the oracle surface."""
     from oracle import xt_oracle as xo
     tag = f'xT {l}x{w}'
     for k, t in (('shot', acc.shot), ('goal', acc.goal), ('move', acc.move)):
@@ -323,10 +336,7 @@ def check_xt(par: Parity, cnt: dict, acc, xT_dev, n_iter: int, l: int, w: int) -
     par.exact(f'{tag} transition counts', tr, cnt['trans'].reshape(-1))
     fit = xo.solve(cnt, l, w)
     par.exact(f'{tag} iterations', n_iter + 1, len(fit['heatmaps']))
-    got = xT_dev.cpu().numpy().reshape(w, l)
-    par.values += got.size
-    if not np.array_equal(got, fit['xT']):
-        par._fail(f'{tag} surface')
+    check_surface(par, tag, xT_dev.cpu().numpy().reshape(w, l), fit['xT'], rtol)
     return fit['xT']
 
 
@@ -422,7 +432,9 @@ def atomic_extra(dist, rank, world, dev, games: int, reps: int = 21, check: bool
     # followed the allocations placed before it: 3.80 vs 3.41 - 3.43 ms per step on one box,
     # profiles/r04_cfg3_contig_ab.json)
     plan = catalog.build_plan(ATOMIC_DEFAULT, 3, True)
-    out = ops.alloc_feature_blocks(plan, ab.n, dev, 1024, 128, contiguous=True)
+    torch.cuda.empty_cache()  # cached blocks of earlier entries out of the way of the range
+    # 'require': no silent fall-back to the caching allocator (the line says which served it)
+    out = ops.alloc_feature_blocks(plan, ab.n, dev, 1024, 128, contiguous='require')
     ops.features(ab, ATOMIC_DEFAULT, 3, out=out, bool_tile=1024, num_tile=128)
     lab = ops.labels(ab)
 
@@ -445,6 +457,7 @@ def atomic_extra(dist, rank, world, dev, games: int, reps: int = 21, check: bool
     return {'workload': f'cfg3: Atomic-VAEP features (k=3, default xfns, 154 cols) + labels of '
                         f'{games:,} synthetic atomic games over {world} rank(s)',
             'atomic_actions_per_gpu': n, 'atomic_actions_total': total, 'scaling': 'strong',
+            'bool_block': out.bool_alloc,
             'ms_per_step': round(wall, 4),
             'timing': f'median of {reps} steps (HIP events per step; min {ms_lo:.4f}, max '
                       f'{ms_hi:.4f} ms on rank {rank})',
@@ -503,6 +516,7 @@ def xt105_extra(ab, dist, dev, sharded: bool = False, cfg5_games: int = 62500,
             mats, _, n_iter, err = shard.xt_fit_bands_sharded(batches, l, w, interp_codes=icodes,
                                                               solve=solve)
             acc = None  # each rank holds only its row block of the transition counts
+            path[0] = 'sequential' if solve == 'rows' else 'reordered'
         else:  # one all-reduce of the counts, replicated solve
             acc = ops.xt_count_many(batches, l, w, interp_codes=icodes)
             mark()
@@ -510,6 +524,7 @@ def xt105_extra(ab, dist, dev, sharded: bool = False, cfg5_games: int = 62500,
             mark()
             sol = ops.xt_solve(acc, transition=False)  # synchronises; ExpectedThreat.fit's
             mats, n_iter = sol.mats, sol.n_iter           # call above 1024 cells
+            path[0] = sol.path
         mark()
         # rate(use_interpolation=True): each action's two node values evaluated in place from
         # the 105 x 68 surface staged in LDS (sa_xt_rate_interp_codes), bit-identical to the
@@ -519,6 +534,7 @@ def xt105_extra(ab, dist, dev, sharded: bool = False, cfg5_games: int = 62500,
                  for b, c, o in zip(batches, icodes, rate_out)]
         mark()
         return n_iter, acc, mats, rates
+    path = ['sequential']  # the value iteration's summation path of the last call
     axes = ops.xt_interp_axes(l, w, dev)  # node positions (constants of the reference's grid)
     icodes = [ops.xt_interp_codes_buffer(b.n, dev) for b in batches]
     rate_out = [torch.empty(max(b.n, 16), dtype=torch.float64, device=dev) for b in batches]
@@ -541,6 +557,9 @@ def xt105_extra(ab, dist, dev, sharded: bool = False, cfg5_games: int = 62500,
     n_iter, acc, mats, rates = once()  # the checked outputs come from an untouched call
     torch.cuda.synchronize()
     par = Parity()
+    # reordered sums: the iteration count exact, the surface within 1e-12 relative (the error
+    # bound allows 4e-11 after 26 iterations; north_star's bar is 1e-6); in order: bit for bit
+    rtol = 0.0 if path[0] == 'sequential' else 1e-12
     if check:  # the last call's counts, surface, iterations and the first batch's rates
         ocnt = oracle_counts(None, l, w, dist, dev, acc=ocnt)
         if acc is None:  # row-sharded solve: the surface is checked, the counts are not held
@@ -548,10 +567,9 @@ def xt105_extra(ab, dist, dev, sharded: bool = False, cfg5_games: int = 62500,
             fit = xo.solve(ocnt, l, w)
             xT = fit['xT']
             par.exact('xT 105x68 iterations', n_iter + 1, len(fit['heatmaps']))
-            if not np.array_equal(mats[3].cpu().numpy().reshape(w, l), xT):
-                par._fail('xT 105x68 surface')
+            check_surface(par, 'xT 105x68', mats[3].cpu().numpy().reshape(w, l), xT, rtol)
         else:
-            xT = check_xt(par, ocnt, acc, mats[3], n_iter, l, w)
+            xT = check_xt(par, ocnt, acc, mats[3], n_iter, l, w, rtol)
         del ocnt
         if first is not None:
             check_xt_rate(par, first, rates[0], xT, interp=True)
@@ -585,7 +603,14 @@ def xt105_extra(ab, dist, dev, sharded: bool = False, cfg5_games: int = 62500,
                         'start-cell band; the 7140^2 table written once, no global atomics) '
                         'writing each action\'s 8-B interpolated-rate operand; value iteration '
                         'over the compact count rows; rate from the operands (LDS surface)',
-            **({'parity': par.record()} if check else {})}
+            'solve_path': path[0] + (' (one launch, rows summed in a fixed parallel order under '
+                                     'an error bound that keeps every convergence decision)'
+                                     if path[0] == 'reordered' else ''),
+            **({'parity': dict(par.record(),
+                               surface_tolerance=('bit-exact' if rtol == 0 else
+                                                  f'{rtol:g} relative, iteration count exact'),
+                               surface_max_rel_err=float(f"{getattr(par, 'surface_rel_err', 0.0):.3e}"))}
+               if check else {})}
 
 
 def convert_extra(d, dist, dev, reps: int = 3) -> dict:
@@ -1099,13 +1124,16 @@ def main() -> None:
         check_s = time.perf_counter() - tc
     extra_side = {}
     if not args.no_side:
+        # cfg3 first: its bool block wants a physically contiguous range, which cfg5's ~1e8
+        # actions of device batches (allocated and freed by its entry) would fragment
+        extra_side['atomic_cfg3'] = atomic_extra(dist, rank, world, dev, args.atomic_games,
+                                                 check=check)
+        torch.cuda.empty_cache()
         cfg5_sharded = args.xt_sharded or args.cfg5_solve in ('auto', 'sharded', 'sharded-rows')
         extra_side['xt105_cfg5'] = xt105_extra(ab, dist, dev, cfg5_sharded, args.cfg5_games,
                                                rank, world, args.games, d=d, check=check,
                                                solve='rows' if args.cfg5_solve == 'sharded-rows'
                                                else 'compact')
-        extra_side['atomic_cfg3'] = atomic_extra(dist, rank, world, dev, args.atomic_games,
-                                                 check=check)
         extra_side['convert_to_atomic'] = convert_extra(d, dist, dev)
         extra_side['rate_on_device'] = rate_extra(ab, out, n, dev)
         if args.e2e_games > 0 and rank == 0:

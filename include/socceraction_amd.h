@@ -339,6 +339,24 @@ int sa_xt_count_from_buckets(int32_t nsets, const uint32_t* const* buckets,
 int sa_xt_solve(const int64_t* shot, const int64_t* goal, const int64_t* move,
                 const int32_t* trans, int32_t l, int32_t w, double eps, int32_t max_iter,
                 double* mats, double* trans_t, double* heatmaps, int32_t* n_iter, void* stream);
+/* sa_xt_solve with a choice of summation order for grids above SA_XT_SOLVE_MAX_C cells (smaller
+ * grids always sum in the reference's order, bit-exact).  Large grids by default solve in ONE
+ * launch with each row's sum reordered into a fixed parallel tree (run-to-run reproducible)
+ * under a rigorous error bound: every `diff > eps` decision, and so the iteration count, is the
+ * reference's, and the iterates are within 4e-11 relative of the reference's (26 iterations at
+ * 105 x 68); when some cell's diff falls inside the bound the system is re-solved in the
+ * reference's order.  flags: SA_XT_SOLVE_EXACT = always the reference's order (bit-exact
+ * iterates, one launch per iteration).  *path (may be NULL) receives which path produced the
+ * result (SA_XT_PATH_*).  Same outputs and synchronisation as sa_xt_solve. */
+#define SA_XT_SOLVE_EXACT 1
+#define SA_XT_PATH_SEQUENTIAL 0   /* the reference's order (small grid, or SA_XT_SOLVE_EXACT) */
+#define SA_XT_PATH_REORDERED 1    /* reordered sums, every decision outside the error bound */
+#define SA_XT_PATH_INSIDE_BOUND 2 /* reordered, a decision inside the bound: re-solved in order */
+#define SA_XT_PATH_UNAVAILABLE 3  /* reordered solve not launchable here: solved in order */
+int sa_xt_solve_ex(const int64_t* shot, const int64_t* goal, const int64_t* move,
+                   const int32_t* trans, int32_t l, int32_t w, double eps, int32_t max_iter,
+                   int32_t flags, double* mats, double* trans_t, double* heatmaps, int32_t* n_iter,
+                   int32_t* path, void* stream);
 /* sa_xt_solve for grids of <= SA_XT_SOLVE_MAX_C cells without the host round trip: the
  * iteration count (-1: max_iter reached first) is written to device memory *n_iter_dev and
  * nothing is synchronised, so a consumer of the surface (sa_xt_rate_cells) can be enqueued
@@ -385,6 +403,15 @@ int sa_xt_iterate_compact(const uint32_t* ell, const int32_t* row_len, const int
                           int32_t r0, int32_t nrows, const double* x, double eps,
                           double* x_next_rows, const int32_t* flag_prev, int32_t* flag_out,
                           void* stream);
+/* The whole value iteration of a grid from the compact form of ALL its C rows (as built by
+ * sa_xt_compact_rows; the multi-GPU fit gathers it from the ranks): heatmaps[(max_iter+1)*C]
+ * = x after 0..n_iter iterations, *n_iter [host] the count (-1: max_iter reached first), the
+ * summation order chosen by `flags` exactly as in sa_xt_solve_ex (*path may be NULL).
+ * cnt_rows: the dense count rows, read only for counts >= 65535.  Synchronises the stream. */
+int sa_xt_solve_compact(const uint32_t* ell, const int32_t* row_len, const int32_t* cnt_rows,
+                        const int64_t* move, const double* gs, const double* pmove, int32_t C,
+                        double eps, int32_t max_iter, int32_t flags, double* heatmaps,
+                        int32_t* n_iter, int32_t* path, void* stream);
 
 /* interp2d(x=cx, y=cy, z=xT, kind='linear')(xs, ys) of ExpectedThreat.interpolator
  * (xthreat.py:347-378): grid[r*L + h] = bilinear(xT; xs[h], ys[r]) through the cell

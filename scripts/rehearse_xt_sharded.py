@@ -80,7 +80,9 @@ def main():
             ops.xt_count(B.ActionBatch.from_columns(c, dev=dev), l, w, acc)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        sol = ops.xt_solve(acc)
+        # the bands mode's replicated iteration is the single-GPU solve itself (reordered sums
+        # under the error bound); the row-sharded iterations sum in the reference's order
+        sol = ops.xt_solve(acc, exact_order=mode in ('rows', 'bands-rows'))
         torch.cuda.synchronize()
         out['ms_single_solve'] = round((time.perf_counter() - t0) * 1e3, 3)
         out['single_iterations'] = sol.n_iter

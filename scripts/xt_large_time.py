@@ -70,8 +70,15 @@ def main():
     out['table_ms'] = _ms(lambda: ops.xt_count_buckets(parts, l, w, acc, overwrite=True), args.reps)
     out['count_many_ms'] = _ms(lambda: ops.xt_count_many(bs, l, w, interp_codes=ic), args.reps)
     sol = ops.xt_solve(acc, transition=False)
+    ex = ops.xt_solve(acc, transition=False, exact_order=True)
     out['iterations'] = sol.n_iter
+    out['iterations_exact_order'] = ex.n_iter
+    out['solve_path'] = sol.path
+    h, r = sol.heatmaps.cpu().numpy(), ex.heatmaps.cpu().numpy()
+    d = np.abs(h - r)
+    out['heatmaps_max_rel_diff'] = float(np.max(np.where(d == 0, 0.0, d / np.maximum(np.abs(r), 1e-300))))
     out['solve_ms'] = _ms(lambda: ops.xt_solve(acc, transition=False), args.reps)
+    out['solve_exact_order_ms'] = _ms(lambda: ops.xt_solve(acc, transition=False, exact_order=True), args.reps)
     # one value iteration alone (sa_xt_iterate_compact on the fitted counts, x = the surface)
     # and the compact form's build, HIP events
     from socceraction_amd import _native
@@ -94,6 +101,12 @@ def main():
         p(ell), p(rl), p(acc.trans), p(acc.move), p(gp[0]), p(gp[1]), C, 0, C, p(x), 1e-5, p(xo), None,
         p(fl), stream_handle()))
     out['iteration_ms'] = _ev(it, 3 * args.reps)
+    # the whole reordered iteration from the prebuilt compact form (one launch + its host sync)
+    t = lambda: ops.xt_solve_compact(ell, rl, acc.trans, acc.move, gp[0], gp[1], C)  # noqa: E731
+    out['solve_compact_reordered_ms'] = _ms(t, args.reps)
+    out['solve_compact_reordered_path'] = t()[2]
+    out['solve_compact_exact_ms'] = _ms(lambda: ops.xt_solve_compact(ell, rl, acc.trans, acc.move, gp[0], gp[1], C,
+                                                                     exact_order=True), args.reps)
     out['row_len_max'] = int(rl.max().item())
     out['row_len_mean'] = round(float(rl.float().mean().item()), 1)
     xT = sol.mats[3].reshape(w, l)

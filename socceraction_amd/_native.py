@@ -25,6 +25,9 @@ SA_XT_SOLVE_MAX_C = 1024  # sa_xt_solve: larger grids may pass trans_t = NULL
 SA_XT_CELLS_MAX_C = 4096
 SA_XT_COUNT_SHARED, SA_XT_COUNT_OVERWRITE = 1, 2
 SA_XT_COMPACT_MAX_C = 9472  # sa_xt_compact_rows / sa_xt_iterate_compact
+SA_XT_SOLVE_EXACT = 1  # sa_xt_solve_ex / sa_xt_solve_compact: the reference's summation order
+# which path produced a large-grid solve (sa_xt_solve_ex's *path)
+XT_SOLVE_PATHS = ('sequential', 'reordered', 'inside-bound', 'unavailable')
 SA_BOOL_TILE_QUANTUM = 1024
 SA_NUM_TILE_QUANTUM = 128
 SA_OK, SA_EINVAL, SA_EHIP, SA_EDATA, SA_ENOMEM = 0, -1, -2, -3, -4
@@ -141,6 +144,14 @@ _SIGNATURES = {
     'sa_xt_solve': (ctypes.c_int, [_p, _p, _p, _p, ctypes.c_int32, ctypes.c_int32,
                                    ctypes.c_double, ctypes.c_int32, _p, _p, _p,
                                    ctypes.POINTER(ctypes.c_int32), _p]),
+    'sa_xt_solve_ex': (ctypes.c_int, [_p, _p, _p, _p, ctypes.c_int32, ctypes.c_int32,
+                                      ctypes.c_double, ctypes.c_int32, ctypes.c_int32, _p, _p, _p,
+                                      ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32),
+                                      _p]),
+    'sa_xt_solve_compact': (ctypes.c_int, [_p, _p, _p, _p, _p, _p, ctypes.c_int32, ctypes.c_double,
+                                           ctypes.c_int32, ctypes.c_int32, _p,
+                                           ctypes.POINTER(ctypes.c_int32),
+                                           ctypes.POINTER(ctypes.c_int32), _p]),
     'sa_xt_solve_async': (ctypes.c_int, [_p, _p, _p, _p, ctypes.c_int32, ctypes.c_int32,
                                    ctypes.c_double, ctypes.c_int32, _p, _p, _p,
                                    _p, _p]),

@@ -1084,10 +1084,20 @@ extern "C" int sa_xt_solve(const int64_t* shot, const int64_t* goal, const int64
                            const int32_t* trans, int32_t l, int32_t w, double eps, int32_t max_iter,
                            double* mats, double* trans_t, double* heatmaps, int32_t* n_iter,
                            void* stream) {
+  return sa_xt_solve_ex(shot, goal, move, trans, l, w, eps, max_iter, 0, mats, trans_t, heatmaps, n_iter, nullptr,
+                        stream);
+}
+
+extern "C" int sa_xt_solve_ex(const int64_t* shot, const int64_t* goal, const int64_t* move,
+                              const int32_t* trans, int32_t l, int32_t w, double eps, int32_t max_iter,
+                              int32_t flags, double* mats, double* trans_t, double* heatmaps, int32_t* n_iter,
+                              int32_t* path, void* stream) {
   if (l < 1 || w < 1 || max_iter < 0) return fail(SA_EINVAL, "bad l, w or max_iter");
   const int C = l * w;
   if (!shot || !goal || !move || !trans || !mats || (!trans_t && C <= XT_SOLVE_MAX_C) || !heatmaps || !n_iter)
     return fail(SA_EINVAL, "null pointer");
+  if (flags & ~SA_XT_SOLVE_EXACT) return fail(SA_EINVAL, "unknown flags");
+  if (path) *path = SA_XT_PATH_SEQUENTIAL;
   hipStream_t st = (hipStream_t)stream;
   auto* us = reinterpret_cast<const unsigned long long*>(shot);
   auto* ug = reinterpret_cast<const unsigned long long*>(goal);
@@ -1137,20 +1147,21 @@ extern "C" int sa_xt_solve(const int64_t* shot, const int64_t* goal, const int64
         rc = xt_compact_build(trans, C, C, ell, slen, st);
       }
     }
+    if (compact && !rc) {  // reordered under the error bound, or the reference's order
+      int p = SA_XT_PATH_SEQUENTIAL;
+      rc = xt_compact_solve(ell, slen, trans, move, gs, pm, C, eps, max_iter, flags, heatmaps, &iters, &p, st);
+      if (path) *path = p;
+    }
     std::vector<int32_t> hflags(max_iter + 1, 0);
     const int batch = 8;
-    for (int it0 = 0; !rc && it0 < max_iter && iters < 0; it0 += batch) {
+    for (int it0 = 0; !compact && !rc && it0 < max_iter && iters < 0; it0 += batch) {
       const int it1 = it0 + batch < max_iter ? it0 + batch : max_iter;
-      for (int it = it0; it < it1 && !rc; ++it) {
+      for (int it = it0; it < it1 && !rc; ++it) {  // above the compact form's C: the dense rows
         double* xi = heatmaps + (int64_t)it * C;
         const int32_t* fp = it > 0 ? dflags + it - 1 : nullptr;
-        if (compact) {
-          rc = xt_compact_iterate(ell, slen, trans, move, gs, pm, C, 0, C, xi, eps, xi + C, fp, dflags + it, st);
-        } else {
-          hipLaunchKernelGGL(xt_iter_kernel, dim3((C + XI_ROWS - 1) / XI_ROWS), dim3(XI_THREADS), 0, st, trans, um,
-                             gs, pm, C, 0, C, eps, xi, xi + C, fp, dflags + it);
-          rc = check_launch("xt_iter_kernel");
-        }
+        hipLaunchKernelGGL(xt_iter_kernel, dim3((C + XI_ROWS - 1) / XI_ROWS), dim3(XI_THREADS), 0, st, trans, um,
+                           gs, pm, C, 0, C, eps, xi, xi + C, fp, dflags + it);
+        rc = check_launch("xt_iter_kernel");
       }
       if (!rc) rc = check_hip(hipMemcpyAsync(hflags.data() + it0, dflags + it0,
                                              sizeof(int32_t) * (it1 - it0), hipMemcpyDeviceToHost, st),

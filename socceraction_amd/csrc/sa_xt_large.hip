@@ -28,6 +28,7 @@
 //    int32 rows.
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
 #include <cstring>
 #include <vector>
 
@@ -79,6 +80,10 @@ static_assert(SA_XB_RMAX >= 1 && SA_XB_RMAX <= XB_MAX_ROWS, "SA_XB_RMAX");
 constexpr int XB_NB_MAX = 4000;     // bands (K3 holds 2 words per band + a region's keys in LDS)
 constexpr size_t XB_LDS_MAX = 160 * 1024;
 constexpr int XB_MAX_SETS = 24;     // buckets per K4 launch
+// K4's static LDS (row sums, set pointers and bounds), reserved out of XB_LDS_MAX before the
+// dynamic R x P bins are sized (100 x 68 at R = 6 would ask 163,296 + 640 B of 163,840)
+constexpr size_t XB_LDS_STATIC = 1024;
+static_assert(XB_MAX_ROWS * 8 + XB_MAX_SETS * 24 <= XB_LDS_STATIC, "K4 static LDS");
 constexpr uint32_t XB_NONE = 0xFFFFFFFFu;
 static_assert(XS_PER * XS_THREADS * XS_SPLIT == XK_CHUNK && XS_PER >= 1, "K3 holds one part of a K1 region");
 static_assert(XS_PART * 4 + 2 * XB_NB_MAX * 4 + 256 <= XB_LDS_MAX, "K3 LDS");
@@ -303,11 +308,13 @@ __global__ __launch_bounds__(XK_THREADS) void xt_keys_kernel(sa_actions A, const
   if (threadIdx.x == 0) region_cnt[blockIdx.x] = cursor;
 }
 
-// Exclusive scan of a[0, n) in place by one 1024-thread workgroup; returns the total (to every
-// thread).  ws: 17 words of LDS.
-__device__ uint32_t block_scan_1024(uint32_t* a, int n, uint32_t* ws) {
+// Exclusive scan of a[0, n) in place by one NT-thread workgroup; returns the total (to every
+// thread).  ws: NT / 64 + 1 words of LDS.
+template <int NT>
+__device__ uint32_t block_scan(uint32_t* a, int n, uint32_t* ws) {
+  constexpr int NW = NT / 64;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  const int per = (n + 1023) / 1024;
+  const int per = (n + NT - 1) / NT;
   const int lo = min(n, t * per), hi = min(n, lo + per);
   uint32_t s = 0;
   for (int i = lo; i < hi; ++i) s += a[i];
@@ -321,12 +328,12 @@ __device__ uint32_t block_scan_1024(uint32_t* a, int n, uint32_t* ws) {
   __syncthreads();
   if (t == 0) {
     uint32_t run = 0;
-    for (int k = 0; k < 16; ++k) {
+    for (int k = 0; k < NW; ++k) {
       const uint32_t v = ws[k];
       ws[k] = run;
       run += v;
     }
-    ws[16] = run;
+    ws[NW] = run;
   }
   __syncthreads();
   uint32_t run = ws[wv] + inc - s;
@@ -335,10 +342,11 @@ __device__ uint32_t block_scan_1024(uint32_t* a, int n, uint32_t* ws) {
     a[i] = run;
     run += v;
   }
-  const uint32_t total = ws[16];
+  const uint32_t total = ws[NW];
   __syncthreads();
   return total;
 }
+__device__ uint32_t block_scan_1024(uint32_t* a, int n, uint32_t* ws) { return block_scan<1024>(a, n, ws); }
 
 // K2: band_off[b] = keys of bands < b (int64, [NB + 1]); cursor[b] = band_off[b].
 __global__ __launch_bounds__(1024) void xt_band_scan_kernel(uint32_t* __restrict__ band_cnt, int NB,
@@ -911,6 +919,345 @@ __global__ __launch_bounds__(XE_THREADS) void xt_iter_ell_kernel(const uint32_t*
   }
 }
 
+// ============================================================================ reordered solve
+// The whole value iteration in ONE launch with the row sums reordered (xthreat.py:303-317 fixes
+// a left-to-right order; north_star allows 1e-6 relative on xT surfaces, only the iteration count
+// must be the reference's).  One 1024-thread workgroup per CU holds its rows' compact entries in
+// REGISTERS for every iteration (62.5 MB at cfg5 = 244 KB per CU of a 512 KB register file), so
+// an iteration reads no count from memory: it stages x (C doubles) into LDS, forms its rows' sums
+// and hands its new x values to every other workgroup through a grid barrier.
+//
+// Sum order (fixed, so every run gives the same bits): a row's 128-entry chunk ("unit") is summed
+// by a half-wave -- each lane its 4 entries in order by fmas of the count and x, then a fixed
+// 32-lane tree (recursive halving over 8 units at a time) -- and the row's unit sums are added in
+// unit order; the row sum is divided by the row's move count once.  Against the reference's
+// sequential sum of the correctly rounded (cnt / m) * x[c] terms, both are sums of the same
+// non-negative terms in some order, so with n <= C terms each differs from the exact sum S by at
+// most (n + 2) u S (u = 2^-53), and the two by (2 C + 8) u S.  Across iterations a relative
+// difference e_t of x becomes at most e_t + (2 C + 16) u in the next x (T substochastic,
+// everything non-negative).  The decision `diff > eps` of a cell is therefore the reference's
+// whenever |diff - eps| exceeds e_{t+1} (x_{t+1} + x_t) plus the subtraction's rounding; a cell
+// inside that margin flags the solve as ambiguous and the caller re-solves it in the reference's
+// order (xt_iter_ell_kernel).  Without an ambiguous cell every decision, and so the iteration
+// count, is the reference's; the iterates differ from the reference's by at most e_t relative
+// (26 iterations at 105 x 68: <= 4e-11; measured ~1e-15).
+//
+// Hand-off (MI355X_MICROARCH.md, visibility, Valid forms row 1): each workgroup stores its new x
+// values write-through (agent-scope atomic stores) into a FRESH 128-B aligned row of a scratch
+// history (a line is never read before it is written), every storing wave drains its stores,
+// one lane adds to a monotonic arrival counter and polls it; every load of handed-off words is an
+// agent-scope atomic load.  The poll is bounded (1 s of the wall clock): a workgroup that times
+// out sets the abort word and every workgroup leaves at its next barrier; the host then re-solves
+// in the reference's order.
+constexpr int XF_THREADS = 512;   // 2 waves per SIMD: 256 VGPRs each, half of them entries
+constexpr int XF_HALVES = XF_THREADS / 32;  // half-waves per workgroup
+constexpr int XF_G = 8;                     // units reduced together by a half-wave
+#ifndef SA_XF_PAIR
+#define SA_XF_PAIR 2  // units whose x reads may be in flight together
+#endif
+constexpr int XF_PAIR = SA_XF_PAIR;
+#ifndef SA_XF_KREG
+#define SA_XF_KREG 32  // units per half-wave held in registers (the rest re-read every iteration)
+#endif
+constexpr int XF_KREG = SA_XF_KREG;
+static_assert(XF_KREG % XF_G == 0 && XF_KREG >= XF_G && XF_KREG <= 48, "SA_XF_KREG");
+constexpr long long XF_SPIN_TICKS = 100000000;  // 1 s of the 100 MHz wall clock
+// control words (int32, zeroed before the launch): arrivals, timeout, ambiguous, iterations, then
+// one flag per iteration (some cell moved by more than eps)
+constexpr int XF_BAR = 0, XF_ABORT = 1, XF_AMB = 2, XF_NITER = 3, XF_FLAGS = 8;
+#ifndef SA_XF_PROBE
+#define SA_XF_PROBE 0  // 1: workgroup 0's wall-clock ticks per phase in control words 4..7 (stderr)
+#endif
+typedef uint32_t __attribute__((address_space(1))) xf_gu32;
+typedef unsigned long long __attribute__((address_space(1))) xf_gu64;
+
+__device__ __forceinline__ uint32_t xf_ld32(const int32_t* p) {
+  return __hip_atomic_load((xf_gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Largest i in [0, nrl) with luo[i] <= gu (luo ascending, luo[0] <= gu < luo[nrl]).
+__device__ __forceinline__ int xf_locate(const int32_t* luo, int nrl, int gu) {
+  int lo = 0, hi = nrl;
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (luo[mid] <= gu)
+      lo = mid;
+    else
+      hi = mid;
+  }
+  return lo;
+}
+
+// Lane l32's 4 entries (l32 + 32 q, q < 4) of global unit gu: row ra + i, chunk gu - luo[i];
+// entries past the row's end read as 0 (count 0, column 0: a +0 term).
+__device__ __forceinline__ u32x4 xf_unit(const uint32_t* __restrict__ ell, const int32_t* __restrict__ row_len,
+                                         const int32_t* luo, int nrl, int ra, int pe, int gu, int l32) {
+  const int i = xf_locate(luo, nrl, gu);
+  const int j = gu - luo[i];
+  const int len = row_len[ra + i];
+  u32x4 e = *reinterpret_cast<const u32x4*>(ell + (int64_t)(ra + i) * pe + j * XE_KC + 4 * l32);
+  const int k = j * XE_KC + l32;
+  e[0] = k < len ? e[0] : 0u;
+  e[1] = k + 32 < len ? e[1] : 0u;
+  e[2] = k + 64 < len ? e[2] : 0u;
+  e[3] = k + 96 < len ? e[3] : 0u;
+  return e;
+}
+
+// The lane's part of a unit's sum: its 4 entries in order, count * x by fmas.
+__device__ __forceinline__ double xf_dot(const u32x4& e, const double* xs) {
+  double s = (double)(e[0] >> 16) * xs[e[0] & 0xFFFFu];
+  s = __builtin_fma((double)(e[1] >> 16), xs[e[1] & 0xFFFFu], s);
+  s = __builtin_fma((double)(e[2] >> 16), xs[e[2] & 0xFFFFu], s);
+  return __builtin_fma((double)(e[3] >> 16), xs[e[3] & 0xFFFFu], s);
+}
+
+__device__ __forceinline__ bool xf_has_esc(const u32x4& e) {
+  return (e[0] >> 16) == XE_CNT_ESC || (e[1] >> 16) == XE_CNT_ESC || (e[2] >> 16) == XE_CNT_ESC ||
+         (e[3] >> 16) == XE_CNT_ESC;
+}
+
+// 8 unit values per lane -> the sum over the half-wave's 32 lanes of unit (l32 >> 2) & 7, in
+// lanes with l32 % 4 == 0 (and their 3 neighbours): recursive halving over lane bits 4, 3, 2, then
+// a butterfly over bits 1, 0 (a + b and b + a are the same double: the 4 copies agree).
+__device__ __forceinline__ double xf_reduce8(double (&v)[XF_G], int l32) {
+#pragma unroll
+  for (int D = 16, h = XF_G / 2; D >= 4; D >>= 1, h >>= 1) {
+    const bool hi = (l32 & D) != 0;
+#pragma unroll
+    for (int i = 0; i < h; ++i) {
+      const double send = hi ? v[i] : v[i + h];
+      const double keep = hi ? v[i + h] : v[i];
+      v[i] = keep + __shfl_xor(send, D);
+    }
+  }
+  double s = v[0];
+  s = s + __shfl_xor(s, 2);
+  return s + __shfl_xor(s, 1);
+}
+
+__global__ __launch_bounds__(XF_THREADS) void xt_solve_reordered_kernel(
+    const uint32_t* __restrict__ ell, const int32_t* __restrict__ row_len, const int32_t* __restrict__ cnt_rows,
+    const unsigned long long* __restrict__ move, const double* __restrict__ gs, const double* __restrict__ pmove,
+    int C, int hp, double eps, int max_iter, int pmax, double* xb, double* __restrict__ heat, int32_t* ctrl) {
+  extern __shared__ __attribute__((aligned(16))) double xs[];  // [C] x_t | part [pmax] | luo [C + 1]
+  double* part = xs + C;
+  int32_t* luo = reinterpret_cast<int32_t*>(part + pmax);
+  uint32_t* scan = reinterpret_cast<uint32_t*>(xs);  // prologue: units of every row, scanned
+  __shared__ uint32_t ws[XF_THREADS / 64 + 1];
+  __shared__ int s_ra, s_rb;
+#if SA_XF_PROBE
+  const long long k_entry = wall_clock64();
+#endif
+  const int t = threadIdx.x, G = gridDim.x, g = blockIdx.x;
+  const int l32 = t & 31, hw = t >> 5;
+  const int pe = xe_pitch(C);
+
+  // ---- rows of this workgroup: weight of row r = its units + 1, cut at multiples of total / G
+  for (int r = t; r < C; r += XF_THREADS) scan[r] = (uint32_t)((row_len[r] + XE_KC - 1) / XE_KC);
+  __syncthreads();
+  const uint32_t U = block_scan<XF_THREADS>(scan, C, ws);
+  if (t == 0) scan[C] = U;
+  __syncthreads();
+  const uint64_t K = (uint64_t)U + (uint64_t)C;
+  auto owner = [&](int r) -> uint64_t {  // non-decreasing in r; owner(C) = G
+    return r >= C ? (uint64_t)G : ((uint64_t)scan[r] + (uint64_t)r) * (uint64_t)G / K;
+  };
+  if (t < 2) {  // first row with owner >= g + t
+    int lo = -1, hi = C;  // owner(lo) < g + t <= owner(hi)
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (owner(mid) >= (uint64_t)(g + t))
+        hi = mid;
+      else
+        lo = mid;
+    }
+    if (t == 0)
+      s_ra = hi;
+    else
+      s_rb = hi;
+  }
+  __syncthreads();
+  const int ra = s_ra, nrl = s_rb - s_ra;
+  for (int i = t; i <= nrl; i += XF_THREADS) luo[i] = (int32_t)scan[ra + i];
+  __syncthreads();  // the scan's words are x's from here on
+  const int ua = luo[0], nu = luo[nrl] - ua;
+  if (nu > pmax) {  // the host's bound on units per workgroup was wrong: never; the others leave
+    if (t == 0)     // at their first barrier
+      __hip_atomic_store((xf_gu32*)(ctrl + XF_ABORT), 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  const int hb = (int)((int64_t)nu * hw / XF_HALVES), he = (int)((int64_t)nu * (hw + 1) / XF_HALVES);
+  const int hn = he - hb;  // this half-wave's units: local [hb, he)
+
+  // ---- the half-wave's first XF_KREG units, held in registers for the whole solve
+  u32x4 E[XF_KREG];
+  bool esc = false;
+#pragma unroll
+  for (int k = 0; k < XF_KREG; ++k) {
+    E[k] = k < hn ? xf_unit(ell, row_len, luo, nrl, ra, pe, ua + hb + k, l32) : u32x4{0u, 0u, 0u, 0u};
+    esc |= xf_has_esc(E[k]);
+  }
+  for (int k = XF_KREG; k < hn; ++k) esc |= xf_has_esc(xf_unit(ell, row_len, luo, nrl, ra, pe, ua + hb + k, l32));
+  if (__syncthreads_or(esc)) {  // a count >= 65535 (its value is in the dense row only): the host
+    if (t == 0)                 // re-solves in order; the others leave at their first barrier
+      __hip_atomic_store((xf_gu32*)(ctrl + XF_ABORT), 4u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  // this thread's first row's constants
+  double m0 = 1.0, g0 = 0.0, p0 = 0.0;
+  if (t < nrl) {
+    m0 = (double)move[ra + t];
+    g0 = gs[ra + t];
+    p0 = pmove[ra + t];
+  }
+
+#if SA_XF_PROBE
+  long long pt[5] = {0, 0, 0, 0, 0}, pc = k_entry;  // prologue, stage, units, rows, barrier
+  auto tick = [&](int ph) {
+    const long long n = wall_clock64();
+    pt[ph] += n - pc;
+    pc = n;
+  };
+  tick(0);
+#else
+  auto tick = [](int) {};
+#endif
+  constexpr double u = 0x1p-53;
+  const double delta = (2.0 * (double)C + 16.0) * u;
+  double ebound = 0.0;  // relative distance of x_t from the reference's x_t (bound)
+  int n_iter = -1;
+  for (int it = 0; it < max_iter; ++it) {
+    // the entries as the loop's own values: derived words (LDS addresses, counts as doubles)
+    // hoisted out of the loop would take three times their registers
+#pragma unroll
+    for (int k = 0; k < XF_KREG; ++k) asm volatile("" : "+v"(E[k]));
+    // ---- stage x_t (write-through stores of every workgroup, read by agent-scope loads)
+    if (it == 0) {
+      for (int c = t; c < C; c += XF_THREADS) xs[c] = 0.0;
+    } else {
+      const xf_gu64* src = (const xf_gu64*)(xb + (int64_t)it * hp);
+      constexpr int XR = 8;  // loads in flight per thread
+      for (int c0 = 0; c0 < C; c0 += XR * XF_THREADS) {
+        unsigned long long xr[XR];
+#pragma unroll
+        for (int q = 0; q < XR; ++q) {
+          const int c = c0 + t + q * XF_THREADS;
+          xr[q] = c < C ? __hip_atomic_load(src + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+        }
+#pragma unroll
+        for (int q = 0; q < XR; ++q) {
+          const int c = c0 + t + q * XF_THREADS;
+          if (c < C) xs[c] = __longlong_as_double((long long)xr[q]);
+        }
+      }
+    }
+    __syncthreads();
+    tick(1);
+    // ---- unit sums of the half-wave: registers, then any further units re-read from ell
+#pragma unroll
+    for (int k0 = 0; k0 < XF_KREG; k0 += XF_G) {
+      if (k0 < hn) {  // half-wave uniform
+        double v[XF_G];
+#pragma unroll
+        for (int k = 0; k < XF_G; ++k) {
+          v[k] = xf_dot(E[k0 + k], xs);
+          // two units' LDS reads in flight at a time: the scheduler would otherwise hoist all
+          // 32 and spill the entry registers
+          if (k % XF_PAIR == XF_PAIR - 1) __builtin_amdgcn_sched_barrier(0);
+        }
+        const double s = xf_reduce8(v, l32);
+        const int k = k0 + ((l32 >> 2) & 7);
+        if ((l32 & 3) == 0 && k < hn) part[hb + k] = s;
+      }
+    }
+    for (int k0 = XF_KREG; k0 < hn; k0 += XF_G) {
+      double v[XF_G];
+#pragma unroll
+      for (int k = 0; k < XF_G; ++k) {
+        v[k] = 0.0;
+        if (k0 + k < hn) {
+          v[k] = xf_dot(xf_unit(ell, row_len, luo, nrl, ra, pe, ua + hb + k0 + k, l32), xs);
+        }
+      }
+      const double s = xf_reduce8(v, l32);
+      const int k = k0 + ((l32 >> 2) & 7);
+      if ((l32 & 3) == 0 && k < hn) part[hb + k] = s;
+    }
+    __syncthreads();
+    tick(2);
+    // ---- rows: unit sums in order, / move, the reference's gs + pmove * (.) and its decision
+    const double enext = (ebound + delta) * (1.0 + 0x1p-20);
+    bool up = false, amb = false;
+    xf_gu64* dst = (xf_gu64*)(xb + (int64_t)(it + 1) * hp);
+    for (int i = t; i < nrl; i += XF_THREADS) {
+      const int r = ra + i;
+      double m = m0, gr = g0, pr = p0;
+      if (i != t) {
+        m = (double)move[r];
+        gr = gs[r];
+        pr = pmove[r];
+      }
+      const int u0 = luo[i] - ua, u1 = luo[i + 1] - ua;
+      double s = 0.0;
+      for (int q = u0; q < u1; ++q) s = s + part[q];
+      const double v = u1 > u0 ? s / m : 0.0;  // a row without entries sums +0 terms: 0
+      const double xn = gr + pr * v;
+      const double xo = xs[r];
+      const double d = xn - xo;
+      up |= d > eps;  // np.any(diff > eps)
+      const double margin = enext * (xn + xo) * (1.0 + 0x1p-20) + 8.0 * u * (fabs(d) + fabs(eps));
+      amb |= fabs(d - eps) <= margin;
+      __hip_atomic_store(dst + r, (unsigned long long)__double_as_longlong(xn), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+      heat[(int64_t)(it + 1) * C + r] = xn;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its stores
+    const int any_up = __syncthreads_or(up), any_amb = __syncthreads_or(amb);
+    tick(3);
+    if (t == 0) {  // ---- grid barrier: one arrival per workgroup, one lane polls
+      if (any_up) __hip_atomic_fetch_or((xf_gu32*)(ctrl + XF_FLAGS + it), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (any_amb) __hip_atomic_fetch_or((xf_gu32*)(ctrl + XF_AMB), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_fetch_add((xf_gu32*)(ctrl + XF_BAR), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t target = (uint32_t)(it + 1) * (uint32_t)G;
+      const long long t0 = wall_clock64();
+      while (xf_ld32(ctrl + XF_BAR) < target) {
+        if (xf_ld32(ctrl + XF_ABORT)) break;
+        if (wall_clock64() - t0 > XF_SPIN_TICKS) {
+          __hip_atomic_store((xf_gu32*)(ctrl + XF_ABORT), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+    }
+    __syncthreads();
+    tick(4);
+    const uint32_t flag = xf_ld32(ctrl + XF_FLAGS + it);
+    const uint32_t stop = xf_ld32(ctrl + XF_ABORT) | xf_ld32(ctrl + XF_AMB);
+    if (stop) break;  // every workgroup reads the same words behind the same barrier
+    ebound = enext;
+    if (!flag) {
+      n_iter = it + 1;
+      break;
+    }
+  }
+#if SA_XF_PROBE
+  if (t == 0) {  // the slowest workgroup's unit phase and the most units of one workgroup
+    atomicMax(ctrl + XF_FLAGS + max_iter + 1, (int32_t)pt[2]);
+    atomicMax(ctrl + XF_FLAGS + max_iter + 2, nu);
+    atomicMax(ctrl + XF_FLAGS + max_iter + 3, (int32_t)pt[1]);
+  }
+#endif
+  if (g == 0 && t == 0) {
+    ctrl[XF_NITER] = n_iter;
+#if SA_XF_PROBE
+    for (int q = 0; q < 4; ++q) ctrl[4 + q] = (int32_t)pt[q + 1];
+    ctrl[XF_FLAGS + max_iter] = (int32_t)pt[0];
+#endif
+  }
+}
+
 }  // namespace sa
 
 // ================================== C ABI =================================================
@@ -929,7 +1276,7 @@ bool xt_band_ok(int C) {
 static bool xt_band_shape(int C, XbShape* s) {
   if (C < 1 || C + 3 > 65536) return false;
   const int P = (C + 3 + 3) & ~3;
-  int rmax = (int)(XB_LDS_MAX / ((size_t)P * 4));
+  int rmax = (int)((XB_LDS_MAX - XB_LDS_STATIC) / ((size_t)P * 4));
   if (rmax > SA_XB_RMAX) rmax = SA_XB_RMAX;
   if (rmax < 1) return false;
   int r = C / 256;
@@ -1056,6 +1403,121 @@ int xt_compact_iterate(const uint32_t* ell, const int32_t* row_len, const int32_
                      nrows, ct, eps, x, xo, flag_prev, flag_out);
   return check_launch("xt_iter_ell_kernel");
 }
+
+// The reordered solve of the compact rows (xt_solve_reordered_kernel): *status 0 = solved
+// (*n_iter the reference's count, -1: max_iter reached), 1 = a decision fell inside the error
+// bound, 2 = not launched (grid, LDS, residency or scratch size), 3 = a barrier timed out.
+// heat: [(max_iter + 1) * C] f64, rows 1.. written.  Synchronises the stream.
+static int xt_solve_reordered(const uint32_t* ell, const int32_t* row_len, const int32_t* cnt_rows,
+                              const int64_t* move, const double* gs, const double* pmove, int C, double eps,
+                              int max_iter, double* heat, int* n_iter, int* status, hipStream_t st) {
+  *status = 2;
+  *n_iter = -1;
+  if (!xt_compact_ok(C) || max_iter < 1) return SA_OK;
+  const int dev = current_device();
+  const int G = device_cus(dev);
+  const int upr = (C + XE_KC - 1) / XE_KC;                 // units of a dense row
+  const int64_t kmax = (int64_t)C * upr + C;               // row weights (units + 1), at most
+  const int pmax = (int)((kmax + G - 1) / G) + upr + 2;    // units of one workgroup, at most
+  const size_t lds = (size_t)C * 8 + (size_t)pmax * 8 + ((size_t)C + 1) * 4;
+  if (lds + 1024 > (size_t)device_lds_max(dev)) return SA_OK;
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(xt_solve_reordered_kernel),
+                                                   XF_THREADS, lds) != hipSuccess) {
+    (void)hipGetLastError();
+    return SA_OK;
+  }
+  if (nb < 1) return SA_OK;  // one resident workgroup per CU is what the grid barrier needs
+  const int hp = (C + 15) & ~15;  // x history rows on whole 128-B lines
+  const size_t xbytes = (size_t)(max_iter + 1) * (size_t)hp * 8;
+  if (xbytes > ((size_t)512 << 20)) return SA_OK;
+  const size_t cbytes = ((size_t)(XF_FLAGS + max_iter + 4) * 4 + 255) & ~(size_t)255;
+  Scratch sc;
+  int rc = scratch_acquire(cbytes + xbytes, st, &sc);
+  if (rc) return rc;
+  int32_t* ctrl = static_cast<int32_t*>(sc.ptr);
+  double* xb = reinterpret_cast<double*>(static_cast<char*>(sc.ptr) + cbytes);
+  int32_t h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  rc = check_hip(hipMemsetAsync(ctrl, 0, cbytes, st), "memset solve control");
+  if (!rc) {
+    hipLaunchKernelGGL(xt_solve_reordered_kernel, dim3((unsigned)G), dim3(XF_THREADS), lds, st, ell, row_len,
+                       cnt_rows, reinterpret_cast<const unsigned long long*>(move), gs, pmove, C, hp, eps, max_iter,
+                       pmax, xb, heat, ctrl);
+    rc = check_launch("xt_solve_reordered_kernel");
+  }
+  if (!rc) rc = check_hip(hipMemcpyAsync(h, ctrl, sizeof(h), hipMemcpyDeviceToHost, st), "copy solve control");
+  if (!rc) rc = check_hip(hipStreamSynchronize(st), "hipStreamSynchronize");
+#if SA_XF_PROBE
+  int32_t pro[4] = {0, 0, 0, 0};
+  if (!rc) rc = check_hip(hipMemcpy(pro, ctrl + XF_FLAGS + max_iter, 16, hipMemcpyDeviceToHost), "copy probe");
+  fprintf(stderr,
+          "xf_probe C=%d G=%d kreg=%d iters=%d ticks(10ns) wg0: prologue %d stage %d units %d rows %d barrier %d; "
+          "max over wgs: units %d stage %d, units per wg %d (register capacity %d)\n",
+          C, G, XF_KREG, h[XF_NITER], pro[0], h[4], h[5], h[6], h[7], pro[1], pro[3], pro[2], XF_HALVES * XF_KREG);
+#endif
+  scratch_release(sc, st);
+  if (rc) return rc;
+  if (h[XF_ABORT])
+    *status = 3;
+  else if (h[XF_AMB])
+    *status = 1;
+  else {
+    *status = 0;
+    *n_iter = h[XF_NITER];
+  }
+  return SA_OK;
+}
+
+// The value iteration over the compact rows of the whole grid (heat row 0 already zero): the
+// reordered solve unless `flags` asks for the reference's order, the sequential-order kernel
+// (one launch per iteration, flags read back every 8) when asked or when the reordered solve
+// cannot decide.  *path: SA_XT_PATH_*.  Synchronises the stream.
+int xt_compact_solve(const uint32_t* ell, const int32_t* row_len, const int32_t* cnt_rows, const int64_t* move,
+                     const double* gs, const double* pmove, int C, double eps, int max_iter, int flags,
+                     double* heat, int* n_iter, int* path, hipStream_t st) {
+  *n_iter = -1;
+  *path = SA_XT_PATH_SEQUENTIAL;
+  if (!(flags & SA_XT_SOLVE_EXACT)) {
+    int status = 2, it = -1;
+    int rc = xt_solve_reordered(ell, row_len, cnt_rows, move, gs, pmove, C, eps, max_iter, heat, &it, &status, st);
+    if (rc) return rc;
+    if (status == 0) {
+      *n_iter = it;
+      *path = SA_XT_PATH_REORDERED;
+      return SA_OK;
+    }
+    *path = status == 1 ? SA_XT_PATH_INSIDE_BOUND : SA_XT_PATH_UNAVAILABLE;
+  }
+  Scratch sc;  // convergence flags [max_iter + 1]
+  int rc = scratch_acquire(sizeof(int32_t) * ((size_t)max_iter + 1), st, &sc);
+  if (rc) return rc;
+  int32_t* dflags = static_cast<int32_t*>(sc.ptr);
+  rc = check_hip(hipMemsetAsync(dflags, 0, sizeof(int32_t) * ((size_t)max_iter + 1), st), "memset");
+  std::vector<int32_t> hflags(max_iter + 1, 0);
+  const int batch = 8;
+  int iters = -1;
+  for (int it0 = 0; !rc && it0 < max_iter && iters < 0; it0 += batch) {
+    const int it1 = it0 + batch < max_iter ? it0 + batch : max_iter;
+    for (int it = it0; it < it1 && !rc; ++it) {
+      double* xi = heat + (int64_t)it * C;
+      rc = xt_compact_iterate(ell, row_len, cnt_rows, move, gs, pmove, C, 0, C, xi, eps, xi + C,
+                              it > 0 ? dflags + it - 1 : nullptr, dflags + it, st);
+    }
+    if (!rc)
+      rc = check_hip(hipMemcpyAsync(hflags.data() + it0, dflags + it0, sizeof(int32_t) * (it1 - it0),
+                                    hipMemcpyDeviceToHost, st),
+                     "copy flags");
+    if (!rc) rc = check_hip(hipStreamSynchronize(st), "hipStreamSynchronize");
+    for (int it = it0; !rc && it < it1; ++it)
+      if (hflags[it] == 0) {
+        iters = it + 1;
+        break;
+      }
+  }
+  scratch_release(sc, st);
+  *n_iter = iters;
+  return rc;
+}
 }  // namespace sa
 
 extern "C" int sa_xt_band_shape(int32_t l, int32_t w, int32_t* rows_per_band, int32_t* n_bands) {
@@ -1154,6 +1616,25 @@ extern "C" int sa_xt_iterate_compact(const uint32_t* ell, const int32_t* row_len
   if (nrows > 0 && !aligned16(ell)) return fail(SA_EINVAL, "ell must be 16-byte aligned");
   return xt_compact_iterate(ell, row_len, cnt_rows, move, gs, pmove, C, r0, nrows, x, eps, x_next_rows, flag_prev,
                             flag_out, (hipStream_t)stream);
+}
+
+extern "C" int sa_xt_solve_compact(const uint32_t* ell, const int32_t* row_len, const int32_t* cnt_rows,
+                                   const int64_t* move, const double* gs, const double* pmove, int32_t C, double eps,
+                                   int32_t max_iter, int32_t flags, double* heatmaps, int32_t* n_iter, int32_t* path,
+                                   void* stream) {
+  if (!xt_compact_ok(C)) return fail(SA_EINVAL, "the compact form takes 1 <= C <= %d", XE_XMAX);
+  if (max_iter < 0) return fail(SA_EINVAL, "bad max_iter");
+  if (!ell || !row_len || !cnt_rows || !move || !gs || !pmove || !heatmaps || !n_iter)
+    return fail(SA_EINVAL, "null pointer");
+  if (!aligned16(ell)) return fail(SA_EINVAL, "ell must be 16-byte aligned");
+  if (flags & ~SA_XT_SOLVE_EXACT) return fail(SA_EINVAL, "unknown flags");
+  hipStream_t st = (hipStream_t)stream;
+  int rc = check_hip(hipMemsetAsync(heatmaps, 0, sizeof(double) * C, st), "memset");
+  int it = -1, p = SA_XT_PATH_SEQUENTIAL;
+  if (!rc) rc = xt_compact_solve(ell, row_len, cnt_rows, move, gs, pmove, C, eps, max_iter, flags, heatmaps, &it, &p, st);
+  *n_iter = it;
+  if (path) *path = p;
+  return rc;
 }
 
 extern "C" int64_t sa_xt_compact_bytes(int32_t C, int32_t nrows) {

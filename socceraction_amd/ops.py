@@ -131,7 +131,9 @@ def alloc_feature_blocks(plan: FeaturePlan, n: int, dev, bool_tile: Optional[int
     ``contiguous``: the bool block in physically contiguous VRAM (``sa_device_alloc``, the
     largest translation fragments: a bool pass that follows another kernel refills fewer
     translations, 1.40 vs 1.50 ms at cfg2 on the boxes measured) -- for long-lived blocks (a
-    batch pipeline); falls back to the caching allocator when no contiguous range is free."""
+    batch pipeline); falls back to the caching allocator when no contiguous range is free
+    (``contiguous='require'``: raises instead).  ``FeatureBlocks.bool_alloc`` says which
+    allocator served the bool block: 'contiguous' or 'caching'."""
     Rb = _ld(n) if bool_tile is None else int(bool_tile)
     Rn = _ld(n) if num_tile is None else int(num_tile)
     tb, tn = max(1, -(-n // Rb)), max(1, -(-n // Rn))
@@ -154,7 +156,9 @@ def alloc_feature_blocks(plan: FeaturePlan, n: int, dev, bool_tile: Optional[int
     if contiguous and plan.n_bool:
         try:
             arena = DeviceBuffer(int(np.prod(bshape)), contiguous=True)
-        except (RuntimeError, ValueError, _native.NativeError):
+        except (RuntimeError, ValueError, _native.NativeError, MemoryError):
+            if contiguous == 'require':
+                raise
             arena = None
     bblk = arena.tensor(bshape, torch.uint8) if arena is not None else \
         torch.empty(bshape, dtype=torch.uint8, device=dev)
@@ -162,6 +166,7 @@ def alloc_feature_blocks(plan: FeaturePlan, n: int, dev, bool_tile: Optional[int
                         torch.empty((tn, plan.n_f64, Rn), dtype=torch.float64, device=dev),
                         torch.empty((tn, plan.n_i64, Rn), dtype=torch.int64, device=dev))
     out._arena = arena  # keeps the contiguous allocation alive with the blocks
+    out.bool_alloc = 'contiguous' if arena is not None else 'caching'
     return out
 
 
@@ -456,19 +461,23 @@ def xt_bucket(batch: Optional[ActionBatch], l: int, w: int, err: torch.Tensor,
     ``n`` cell codes) as a 4-B key, sorted by start-cell band; error bytes into ``err``.
     ``interp_codes`` (int64 [>= n], :func:`xt_interp_codes_buffer`): each action's operand of a
     later :func:`xt_rate_interp_codes` of the same actions on the L x W node grid."""
+    if cells is not None and (codes is not None or interp_codes is not None):
+        raise ValueError('rate operands come from the coordinate pass, not from cell codes')
+    if cells is None and batch is None:
+        raise ValueError('a batch or cell codes are required')
+    n = batch.n if cells is None else int(n)
     if interp_codes is not None and (interp_codes.dtype != torch.int64 or
-                                     interp_codes.numel() < batch.n):
+                                     interp_codes.numel() < n):
         raise ValueError('interp_codes must be an int64 tensor of at least n elements')
+    if codes is not None and (codes.dtype != torch.int32 or codes.numel() < n):
+        raise ValueError('codes must be an int32 tensor of at least n elements')
     shape = xt_band_shape(l, w)
     if shape is None:
         raise ValueError(f'the band-owned count does not take a {l} x {w} grid')
     dev = err.device
-    n = batch.n if cells is None else int(n)
     keys = torch.empty(max(n, 16), dtype=torch.int32, device=dev)
     off = torch.empty(shape[1] + 1, dtype=torch.int64, device=dev)
     s = batch.struct() if cells is None else None
-    if codes is not None and (codes.dtype != torch.int32 or codes.numel() < n):
-        raise ValueError('codes must be an int32 tensor of at least n elements')
     _native.check(_native.lib().sa_xt_count_bucket(
         ctypes.byref(s) if s is not None else None, _ptr(cells), int(n), int(l), int(w), _ptr(keys),
         _ptr(off), _ptr(err), _ptr(codes), _ptr(interp_codes), int(L), int(W), stream_handle()))
@@ -523,8 +532,9 @@ def xt_count_many(batches: Sequence[ActionBatch], l: int, w: int,
     if xt_band_shape(l, w) is None or not batches:
         if interp_codes is not None:
             raise ValueError('interp_codes come from the band-owned count')
-        if overwrite and acc is not None:
-            acc.zero_()
+        if overwrite and acc is not None:  # the counts only: the error flags accumulate, as on
+            for t in (acc.shot, acc.goal, acc.move, acc.trans):  # the band-owned path
+                t.zero_()
         for b in batches:
             acc = xt_count(b, l, w, acc)
         return acc if acc is not None else xt_zero_counts(l, w, torch.device('cuda'))
@@ -557,7 +567,9 @@ def xt_rate_codes(codes: torch.Tensor, n: int, grid: torch.Tensor,
 # the flags of up to 255 ranks add up in the counts' one sum all-reduce without carrying into
 # each other; a flag is set when its byte is non-zero
 XT_ERR_SHOT, XT_ERR_MOVE_START, XT_ERR_MOVE_OTHER = 0xFF, 0xFF00, 0xFF0000
-XT_ERR_FIT = XT_ERR_SHOT | XT_ERR_MOVE_START | XT_ERR_MOVE_OTHER
+# a rank's counts too large for the multi-GPU int32-word sum (shard.allreduce_xt_counts)
+XT_ERR_OVERFLOW = 0xFF000000
+XT_ERR_FIT = XT_ERR_SHOT | XT_ERR_MOVE_START | XT_ERR_MOVE_OTHER | XT_ERR_OVERFLOW
 
 
 def xt_cells_buffer(n: int, dev) -> torch.Tensor:
@@ -602,6 +614,9 @@ def xt_check_errors(acc: XTCounts, mask: int = XT_ERR_FIT) -> None:
     shots (scoring_prob), shots and move starts (action_prob), every move coordinate
     (move_transition_matrix) or everything (fit)."""
     e = int(acc.err.item()) & mask
+    if e & XT_ERR_OVERFLOW:
+        raise OverflowError('xT counts of one rank reach 2**31 / world: the multi-GPU count sum '
+                            'would overflow its int32 words')
     if e & XT_ERR_MOVE_OTHER:
         raise ValueError('Cannot convert non-finite values (NA or inf) to integer '
                          '(move coordinates)')
@@ -619,13 +634,18 @@ class XTSolution:
     trans_t: Optional[torch.Tensor]  # f64 [C, C] transposed transition matrix (or None)
     heatmaps: torch.Tensor  # f64 [n_iter + 1, C]
     n_iter: int
+    path: str = 'sequential'  # _native.XT_SOLVE_PATHS: how the value iteration summed its rows
 
 
 def xt_solve(acc: XTCounts, eps: float = 1e-5, max_iter: int = 1000,
-             transition: bool = True) -> XTSolution:
+             transition: bool = True, exact_order: bool = False) -> XTSolution:
     """Normalisation + value iteration. ``transition=False`` (grids above
     ``SA_XT_SOLVE_MAX_C`` cells only) skips forming the dense transposed transition matrix,
-    which the large-grid iteration never reads (408 MB at 105 x 68)."""
+    which the large-grid iteration never reads (408 MB at 105 x 68).  Grids above
+    ``SA_XT_SOLVE_MAX_C`` cells sum each row in a fixed parallel order under an error bound that
+    keeps every convergence decision, and so the iteration count, the reference's (iterates
+    within 4e-11 relative at 105 x 68; ``sa_xt_solve_ex``); ``exact_order=True`` sums in the
+    reference's order (bit-exact iterates).  ``XTSolution.path`` says which ran."""
     C = acc.C
     dev = acc.shot.device
     mats = torch.empty((4, C), dtype=torch.float64, device=dev)
@@ -633,14 +653,30 @@ def xt_solve(acc: XTCounts, eps: float = 1e-5, max_iter: int = 1000,
         transition = True  # the small-grid solve reads the transposed matrix
     tt = torch.empty((C, C), dtype=torch.float64, device=dev) if transition else None
     heat = torch.empty((max_iter + 1, C), dtype=torch.float64, device=dev)
-    n_iter = ctypes.c_int32(0)
-    _native.check(_native.lib().sa_xt_solve(_ptr(acc.shot), _ptr(acc.goal), _ptr(acc.move),
-                                            _ptr(acc.trans), acc.l, acc.w, float(eps),
-                                            int(max_iter), _ptr(mats), _ptr(tt), _ptr(heat),
-                                            ctypes.byref(n_iter), stream_handle()))
+    n_iter, path = ctypes.c_int32(0), ctypes.c_int32(0)
+    _native.check(_native.lib().sa_xt_solve_ex(
+        _ptr(acc.shot), _ptr(acc.goal), _ptr(acc.move), _ptr(acc.trans), acc.l, acc.w, float(eps),
+        int(max_iter), _native.SA_XT_SOLVE_EXACT if exact_order else 0, _ptr(mats), _ptr(tt),
+        _ptr(heat), ctypes.byref(n_iter), ctypes.byref(path), stream_handle()))
     if n_iter.value < 0:
         raise RuntimeError(f'xT value iteration did not converge within {max_iter} iterations')
-    return XTSolution(mats, tt, heat[:n_iter.value + 1], n_iter.value)
+    return XTSolution(mats, tt, heat[:n_iter.value + 1], n_iter.value,
+                      _native.XT_SOLVE_PATHS[path.value])
+
+
+def xt_solve_compact(ell: torch.Tensor, row_len: torch.Tensor, cnt_rows: torch.Tensor,
+                     move: torch.Tensor, gs: torch.Tensor, pmove: torch.Tensor, C: int,
+                     eps: float = 1e-5, max_iter: int = 1000,
+                     exact_order: bool = False) -> Tuple[torch.Tensor, int, str]:
+    """The whole value iteration from the compact form of every row (``sa_xt_solve_compact``):
+    ``(heatmaps [max_iter + 1, C] (rows past n_iter unused), n_iter, path)``."""
+    heat = torch.empty((max_iter + 1, C), dtype=torch.float64, device=ell.device)
+    n_iter, path = ctypes.c_int32(0), ctypes.c_int32(0)
+    _native.check(_native.lib().sa_xt_solve_compact(
+        _ptr(ell), _ptr(row_len), _ptr(cnt_rows), _ptr(move), _ptr(gs), _ptr(pmove), int(C),
+        float(eps), int(max_iter), _native.SA_XT_SOLVE_EXACT if exact_order else 0, _ptr(heat),
+        ctypes.byref(n_iter), ctypes.byref(path), stream_handle()))
+    return heat, n_iter.value, _native.XT_SOLVE_PATHS[path.value]
 
 
 def xt_solve_async(acc: XTCounts, eps: float = 1e-5, max_iter: int = 1000) -> XTSolution:

@@ -39,7 +39,22 @@ def allreduce_xt_counts(acc, group=None) -> None:
     flags are one byte each (``ops.XT_ERR_*``), so up to 255 ranks' flags add without
     overlapping.  No staging copy, no ``torch.cat``."""
     _check_world(group)
+    _flag_count_range(acc, group)
     _all_reduce(acc.buf.view(torch.int32), group=group)
+
+
+def _flag_count_range(acc, group) -> None:
+    """The int32-word sum is exact while every summed count stays below 2**31: each rank's shot
+    and move counts below 2**31 // world guarantee it (a transition count never exceeds its
+    row's move count, a goal count its shot count).  A rank over that bound sets the overflow
+    byte of the error word (``ops.XT_ERR_OVERFLOW``, raised by ``ops.xt_check_errors``) on the
+    device, before the all-reduce: no host round trip."""
+    import torch.distributed as dist
+
+    from .ops import XT_ERR_OVERFLOW
+    bound = (2 ** 31) // dist.get_world_size(group)
+    big = torch.maximum(acc.shot.max(), acc.move.max()) >= bound
+    acc.err.add_(big.to(torch.int32) * (XT_ERR_OVERFLOW & -XT_ERR_OVERFLOW))
 
 
 def _check_world(group) -> None:
@@ -138,6 +153,7 @@ def xt_solve_sharded(acc, eps: float = 1e-5, max_iter: int = 1000, group=None, b
     dev = acc.shot.device
     if acc.trans_padded.numel() != W * B * C:
         raise ValueError('counts must be allocated with xt_zero_counts(..., row_blocks=world)')
+    _flag_count_range(acc, group)
     _all_reduce(acc.head.view(torch.int32), group=group)  # the vectors + flags: one all-reduce
     shot, goal, move = acc.shot, acc.goal, acc.move
     rows = torch.empty(B * C, dtype=torch.int32, device=dev)
@@ -205,7 +221,8 @@ def _solve_row_block(rows, shot, goal, move, C: int, B: int, eps: float, max_ite
 
 
 def xt_fit_bands_sharded(batches, l: int, w: int, eps: float = 1e-5, max_iter: int = 1000,
-                         group=None, batch: int = 8, interp_codes=None, solve: str = 'compact'):
+                         group=None, batch: int = 8, interp_codes=None, solve: str = 'compact',
+                         exact_order: bool = False):
     """Band-sharded xT fit (cfg5 over several GPUs) for grids the band-owned count holds
     (``ops.xt_band_shape``, e.g. 105 x 68): the ranks exchange their COUNTED ACTIONS, not count
     tables.  Rank r owns the start-cell bands [b0, b1) = ``band_ranges(NB, world)[r]``, i.e.
@@ -223,11 +240,13 @@ def xt_fit_bands_sharded(batches, l: int, w: int, eps: float = 1e-5, max_iter: i
     5. ``solve='compact'`` (default): each rank builds the compact form of its rows
        (``sa_xt_compact_rows``), one all-gather of those rows' non-zero entries (62.5 MB in all at
        cfg5) gives every rank the whole compact form, and every rank iterates all rows with no
-       further exchange (``_solve_compact_exchange``; falls back to 'rows' when some count
-       reaches 65535: escaped entries are read from the dense row, which only its owner holds);
-       ``solve='rows'``: the row-sharded value iteration of ``xt_solve_sharded`` (one
-       all-gather of x per iteration).  Either way every value is bit-identical to the
-       single-GPU fit of all ranks' actions.
+       further exchange (``_solve_compact_exchange``: the single-GPU fit's own solve,
+       ``sa_xt_solve_compact``, reordered sums under the error bound unless ``exact_order``;
+       falls back to 'rows' when some count reaches 65535: escaped entries are read from the
+       dense row, which only its owner holds); ``solve='rows'``: the row-sharded value
+       iteration of ``xt_solve_sharded`` (the reference's order, one all-gather of x per
+       iteration).  Either way every value is bit-identical to the single-GPU fit of all ranks'
+       actions with the same ``exact_order`` ('rows': ``exact_order=True``).
 
     ``interp_codes``: one ``ops.xt_interp_codes_buffer`` per batch, filled for the rate.
     Returns ``(mats [4, C], heatmaps [n_iter + 1, C], n_iter, err)``; ``err`` is the error-flag
@@ -267,12 +286,15 @@ def xt_fit_bands_sharded(batches, l: int, w: int, eps: float = 1e-5, max_iter: i
     allv = torch.empty((W, 3, B), dtype=torch.int64, device=dev)
     _all_gather(allv.reshape(-1), vec.reshape(-1), group=group)
     full = allv.permute(1, 0, 2).reshape(3, W * B)[:, :C].contiguous()
-    _all_reduce(err, dist.ReduceOp.MAX, group=group)  # the error bytes of every rank
+    # the error bytes of every rank: summed, one byte per flag, like allreduce_xt_counts (a MAX
+    # of whole words would drop one rank's lower-byte flag behind another's higher one)
+    _all_reduce(err, group=group)
     if solve not in ('compact', 'rows'):
         raise ValueError("solve must be 'compact' or 'rows'")
     res = None
     if solve == 'compact' and C <= _native.SA_XT_COMPACT_MAX_C:
-        res = _solve_compact_exchange(rows, full[0], full[1], full[2], C, B, eps, max_iter, group, batch)
+        res = _solve_compact_exchange(rows, full[0], full[1], full[2], C, B, eps, max_iter, group,
+                                      exact_order)
     if res is None:
         res = _solve_row_block(rows, full[0], full[1], full[2], C, B, eps, max_iter, group, batch)
     mats, heat, iters = res
@@ -280,7 +302,7 @@ def xt_fit_bands_sharded(batches, l: int, w: int, eps: float = 1e-5, max_iter: i
 
 
 def _solve_compact_exchange(rows, shot, goal, move, C: int, B: int, eps: float, max_iter: int,
-                            group, batch: int):
+                            group, exact_order: bool = False):
     """Step 5 of :func:`xt_fit_bands_sharded` with ``solve='compact'``: this rank holds the
     count rows [r B, r B + B) (``rows``); returns None (nothing exchanged) when a count of any
     rank reaches 65535, else ``(mats, heatmaps, n_iter)`` of the replicated iteration over the
@@ -332,23 +354,12 @@ def _solve_compact_exchange(rows, shot, goal, move, C: int, B: int, eps: float, 
     gp = torch.empty((2, C), dtype=torch.float64, device=dev)
     _native.check(lib.sa_xt_probabilities(ptr(shot), ptr(goal), ptr(move), C, ptr(mats), ptr(gp[0]),
                                           ptr(gp[1]), stream_handle()))
-    heat = torch.zeros((max_iter + 1, C), dtype=torch.float64, device=dev)
-    flags = torch.zeros(max_iter + 1, dtype=torch.int32, device=dev)
-    iters = -1
-    it0 = 0
-    while it0 < max_iter and iters < 0:
-        it1 = min(it0 + batch, max_iter)
-        for it in range(it0, it1):
-            # cnt_rows: read for counts >= 65535 only, which no rank has (checked above)
-            _native.check(lib.sa_xt_iterate_compact(
-                ptr(full), ptr(lens), ptr(rows), ptr(move), ptr(gp[0]), ptr(gp[1]), C, 0, C,
-                ptr(heat[it]), float(eps), ptr(heat[it + 1]), ptr(flags[it - 1:]) if it else None,
-                ptr(flags[it:]), stream_handle()))
-        hf = flags[it0:it1].cpu().numpy()
-        done = np.flatnonzero(hf == 0)
-        if len(done):
-            iters = it0 + int(done[0]) + 1
-        it0 = it1
+    # the whole iteration on every rank from the same compact form (sa_xt_solve_compact: the
+    # single-GPU fit's own solve, so the same bits); cnt_rows is read for counts >= 65535 only,
+    # which no rank has (checked above)
+    from .ops import xt_solve_compact
+    heat, iters, _path = xt_solve_compact(full, lens, rows, move, gp[0], gp[1], C, eps, max_iter,
+                                          exact_order)
     if iters < 0:
         raise RuntimeError(f'xT value iteration did not converge within {max_iter} iterations')
     mats[3].copy_(heat[iters])

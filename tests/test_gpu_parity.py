@@ -380,7 +380,7 @@ def test_xt_large_grid_vs_oracle(sa, l, w, games):
     ab = B.ActionBatch.from_columns(d)
     acc = ops.xt_count(ab, l, w)
     ops.xt_check_errors(acc)
-    sol = ops.xt_solve(acc)
+    sol = ops.xt_solve(acc, exact_order=True)  # the reference's summation order: bit-exact
     ref = xo.fit(d, l, w)
     m = sol.mats.cpu().numpy()
     np.testing.assert_array_equal(m[0].reshape(w, l), ref['scoring_prob'])
@@ -393,16 +393,25 @@ def test_xt_large_grid_vs_oracle(sa, l, w, games):
     if l * w > 1024:
         # the large-grid solve without the dense transposed matrix: same results, and the
         # drop-in's transition_matrix (formed on first access) equals the oracle's
-        lean = ops.xt_solve(acc, transition=False)
+        lean = ops.xt_solve(acc, transition=False, exact_order=True)
         assert lean.trans_t is None and lean.n_iter == sol.n_iter
         np.testing.assert_array_equal(lean.mats.cpu().numpy(), m)
         np.testing.assert_array_equal(lean.heatmaps.cpu().numpy(), sol.heatmaps.cpu().numpy())
+        # the default reordered sums: the same iteration count, iterates within 1e-12 relative
+        fast = ops.xt_solve(acc, transition=False)
+        assert fast.path == 'reordered' and fast.n_iter == sol.n_iter
+        np.testing.assert_array_equal(fast.mats[:3].cpu().numpy(), m[:3])
+        h, r = fast.heatmaps.cpu().numpy(), sol.heatmaps.cpu().numpy()
+        assert np.all(np.abs(h - r) <= 1e-12 * np.abs(r))
         from socceraction_amd import xthreat
-        model = xthreat.ExpectedThreat(l=l, w=w).fit(syn.to_frame(d))
-        assert model._transition is None
+        model = xthreat.ExpectedThreat(l=l, w=w).fit(syn.to_frame(d), exact_order=True)
+        assert model._transition is None and model.solve_path == 'sequential'
         np.testing.assert_array_equal(model.xT, ref['xT'])
         np.testing.assert_array_equal(model.transition_matrix, ref['transition'])
         assert model._transition_counts is None
+        model = xthreat.ExpectedThreat(l=l, w=w).fit(syn.to_frame(d))
+        assert model.solve_path == 'reordered' and len(model.heatmaps) == len(ref['heatmaps'])
+        assert np.all(np.abs(model.xT - ref['xT']) <= 1e-12 * np.abs(ref['xT']))
 
 
 @pytest.mark.parametrize('l,w,games', [(16, 12, 400), (105, 68, 60), (1, 1, 5), (30, 20, 1)])

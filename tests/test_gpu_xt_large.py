@@ -40,7 +40,7 @@ def _cat(parts):
     return out
 
 
-@pytest.mark.parametrize('l,w', [(105, 68), (40, 30), (15, 14)])
+@pytest.mark.parametrize('l,w', [(105, 68), (40, 30), (15, 14), (100, 68), (75, 68), (120, 68)])
 def test_band_count_many_batches_vs_oracle(sa, l, w):
     """xt_count_many over three device batches (fresh accumulator: the band count writes the
     table once, never reading it) == the oracle's counts of all their actions; the same batches
@@ -169,19 +169,120 @@ def test_compact_iteration_equals_dense(sa, C, r0, nrows):
     assert bool((b == -1.0).all())
 
 
+# The reordered solve's iterates against the reference's order: the error bound allows 4e-11
+# relative after 26 iterations at 105 x 68 (sa_xt_large.hip); the bar the tests hold is 1e-12.
+REORDER_RTOL = 1e-12
+
+
+def _close_rel(a, b, rtol=REORDER_RTOL):
+    a, b = np.asarray(a), np.asarray(b)
+    assert a.shape == b.shape
+    np.testing.assert_array_equal(np.isnan(a), np.isnan(b))
+    assert np.all(np.abs(a - b) <= rtol * np.abs(b) + 1e-300), np.max(np.abs(a - b) / np.maximum(np.abs(b), 1e-300))
+
+
 def test_full_cfg4_batch_large_grid_solve(sa):
     """One full cfg2/cfg4 batch (10k games, ~16M actions) at 105 x 68: band count == the oracle's
-    counts, and the solve over the compact rows gives the oracle's iteration count and surface."""
+    counts; the solve over the compact rows in the reference's order gives the oracle's iteration
+    count and surface bit for bit, the default reordered solve the same count and every heatmap
+    within 1e-12 relative."""
     B, ops, syn = sa['batch'], sa['ops'], sa['synthetic']
     d = syn.spadl_games(10000)
     ab = B.ActionBatch.from_columns(d)
     acc = ops.xt_count_many([ab], 105, 68)
     ref = _oracle(d, 105, 68)
     _same_counts(acc, ref, 105, 68)
-    sol = ops.xt_solve(acc, transition=False)
     fit = xo.solve(ref, 105, 68)
-    assert sol.n_iter + 1 == len(fit['heatmaps'])
-    np.testing.assert_array_equal(sol.mats[3].cpu().numpy().reshape(68, 105), fit['xT'])
+    exact = ops.xt_solve(acc, transition=False, exact_order=True)
+    assert exact.path == 'sequential' and exact.n_iter + 1 == len(fit['heatmaps'])
+    np.testing.assert_array_equal(exact.mats[3].cpu().numpy().reshape(68, 105), fit['xT'])
+    sol = ops.xt_solve(acc, transition=False)
+    assert sol.path == 'reordered' and sol.n_iter == exact.n_iter
+    _close_rel(sol.heatmaps.cpu().numpy().reshape(-1, 68, 105), fit['heatmaps'])
+    again = ops.xt_solve(acc, transition=False)  # run to run: the same bits
+    assert torch.equal(again.heatmaps, sol.heatmaps) and torch.equal(again.mats, sol.mats)
+
+
+def _fit_like_rows(rng, C, dense=0.4, zero_rows=3, hot=0):
+    """Count rows of a fit without escapes (every count < 65535) and the vectors of a system
+    that converges: move[r] >= the row's transitions, gs and pmove like a fit's."""
+    cnt = np.zeros((C, C), np.int32)
+    nz = rng.random((C, C)) < dense
+    cnt[nz] = rng.geometric(0.3, nz.sum())
+    big = rng.random((C, C)) < 0.002
+    cnt[big] = rng.integers(64, 5000, big.sum())
+    if hot:
+        cnt[rng.integers(0, C, hot), rng.integers(0, C, hot)] = rng.integers(65535, 300000, hot)
+    cnt[rng.choice(C, zero_rows, replace=False)] = 0
+    move = cnt.sum(axis=1, dtype=np.int64) + rng.integers(1, 50, C)
+    gs = rng.random(C) * 0.05
+    pm = rng.random(C) * 0.95
+    return cnt, move, gs, pm
+
+
+def _compact_solve(sa, cnt, move, gs, pm, eps, max_iter=1000, exact=False):
+    _native, ops = sa['_native'], sa['ops']
+    from socceraction_amd.batch import stream_handle
+    lib = _native.lib()
+    dev = torch.device('cuda')
+    C = cnt.shape[0]
+    rows = torch.from_numpy(cnt).to(dev)
+    ell = torch.empty(int(lib.sa_xt_compact_bytes(C, C)) // 4, dtype=torch.int32, device=dev)
+    slen = torch.empty(C, dtype=torch.int32, device=dev)
+    _native.check(lib.sa_xt_compact_rows(rows.data_ptr(), C, C, ell.data_ptr(), slen.data_ptr(),
+                                         stream_handle()))
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    heat, n, path = ops.xt_solve_compact(ell, slen, rows, t(move), t(gs), t(pm), C, eps, max_iter,
+                                         exact_order=exact)
+    return heat[:max(n, max_iter) + 1 if n < 0 else n + 1].cpu().numpy(), n, path
+
+
+@pytest.mark.parametrize('C,dense', [(7140, 0.3), (1200, 0.6), (1025, 0.05), (9472, 0.1)])
+def test_reordered_solve_vs_sequential(sa, C, dense):
+    """sa_xt_solve_compact's reordered solve == the reference-order solve: the same iteration
+    count, every iterate within 1e-12 relative, path 'reordered'; two runs give the same bits;
+    max_iter reached first (-1) on both paths alike."""
+    rng = np.random.default_rng(C)
+    cnt, move, gs, pm = _fit_like_rows(rng, C, dense)
+    h0, n0, p0 = _compact_solve(sa, cnt, move, gs, pm, 1e-5, exact=True)
+    h1, n1, p1 = _compact_solve(sa, cnt, move, gs, pm, 1e-5)
+    assert p0 == 'sequential' and p1 == 'reordered'
+    assert n0 > 2 and n1 == n0
+    _close_rel(h1, h0)
+    h2, n2, _ = _compact_solve(sa, cnt, move, gs, pm, 1e-5)
+    assert n2 == n1 and np.array_equal(h2, h1)
+    m = n0 - 1  # stops one iteration short: not converged on either path
+    h3, n3, p3 = _compact_solve(sa, cnt, move, gs, pm, 1e-5, max_iter=m)
+    assert n3 == -1 and p3 == 'reordered'
+    _close_rel(h3, h0[:m + 1])
+
+
+def test_reordered_solve_inside_bound_falls_back(sa):
+    """eps set to a cell's exact diff at some iteration: the reordered decision for that cell
+    lies inside the error bound, so the solve is redone in the reference's order (path
+    'inside-bound') and its iteration count and iterates are the reference order's, bit for
+    bit."""
+    rng = np.random.default_rng(5)
+    C = 2000
+    cnt, move, gs, pm = _fit_like_rows(rng, C, 0.2)
+    h0, n0, _ = _compact_solve(sa, cnt, move, gs, pm, 1e-5, exact=True)
+    k = n0 // 2
+    eps = float(np.max(h0[k] - h0[k - 1]))  # the largest diff of iteration k: stops there
+    he, ne, _ = _compact_solve(sa, cnt, move, gs, pm, eps, exact=True)
+    hr, nr, pr = _compact_solve(sa, cnt, move, gs, pm, eps)
+    assert pr == 'inside-bound'
+    assert nr == ne and np.array_equal(hr, he)
+
+
+def test_reordered_solve_with_escaped_counts(sa):
+    """A count >= 65535 (held in the dense row only): the reordered solve declines (path
+    'unavailable') and the reference-order solve runs, bit for bit."""
+    rng = np.random.default_rng(6)
+    cnt, move, gs, pm = _fit_like_rows(rng, 1500, 0.3, hot=3)
+    assert cnt.max() >= 65535
+    h0, n0, _ = _compact_solve(sa, cnt, move, gs, pm, 1e-5, exact=True)
+    h1, n1, p1 = _compact_solve(sa, cnt, move, gs, pm, 1e-5)
+    assert p1 == 'unavailable' and n1 == n0 and np.array_equal(h1, h0)
 
 
 def test_interp_codes_rate_equals_rate_interp(sa):
