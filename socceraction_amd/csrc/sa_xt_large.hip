@@ -922,57 +922,99 @@ __global__ __launch_bounds__(XE_THREADS) void xt_iter_ell_kernel(const uint32_t*
 // ============================================================================ reordered solve
 // The whole value iteration in ONE launch with the row sums reordered (xthreat.py:303-317 fixes
 // a left-to-right order; north_star allows 1e-6 relative on xT surfaces, only the iteration count
-// must be the reference's).  One 1024-thread workgroup per CU holds its rows' compact entries in
-// REGISTERS for every iteration (62.5 MB at cfg5 = 244 KB per CU of a 512 KB register file), so
-// an iteration reads no count from memory: it stages x (C doubles) into LDS, forms its rows' sums
-// and hands its new x values to every other workgroup through a grid barrier.
+// must be the reference's).  One 512-thread workgroup per CU holds its rows' compact entries in
+// REGISTERS (and LDS for the few that do not fit) for every iteration -- 62.5 MB at cfg5 = 244 KB
+// per CU of a 512 KB register file -- so an iteration reads no count from memory: it stages x
+// (C doubles) into LDS, forms its rows' sums and hands its new x values to every other workgroup
+// through a grid barrier.
 //
 // Sum order (fixed, so every run gives the same bits): a row's 128-entry chunk ("unit") is summed
 // by a half-wave -- each lane its 4 entries in order by fmas of the count and x, then a fixed
-// 32-lane tree (recursive halving over 8 units at a time) -- and the row's unit sums are added in
-// unit order; the row sum is divided by the row's move count once.  Against the reference's
-// sequential sum of the correctly rounded (cnt / m) * x[c] terms, both are sums of the same
-// non-negative terms in some order, so with n <= C terms each differs from the exact sum S by at
-// most (n + 2) u S (u = 2^-53), and the two by (2 C + 8) u S.  Across iterations a relative
-// difference e_t of x becomes at most e_t + (2 C + 16) u in the next x (T substochastic,
-// everything non-negative).  The decision `diff > eps` of a cell is therefore the reference's
-// whenever |diff - eps| exceeds e_{t+1} (x_{t+1} + x_t) plus the subtraction's rounding; a cell
-// inside that margin flags the solve as ambiguous and the caller re-solves it in the reference's
-// order (xt_iter_ell_kernel).  Without an ambiguous cell every decision, and so the iteration
-// count, is the reference's; the iterates differ from the reference's by at most e_t relative
-// (26 iterations at 105 x 68: <= 4e-11; measured ~1e-15).
+// 32-lane tree (recursive halving over 8 units at a time) -- and the row's unit sums by 8 lanes
+// (lane j: units j, j + 8, ... in order; then a fixed 8-lane tree); the row sum is divided by the
+// row's move count once.  Against the reference's sequential sum of the correctly rounded
+// (cnt / m) * x[c] terms, both are sums of the same non-negative terms in some order, so with
+// n <= C terms each differs from the exact sum S by at most (n + 2) u S (u = 2^-53), and the two
+// by (2 C + 8) u S.  Across iterations a relative difference e_t of x becomes at most
+// e_t + (2 C + 16) u in the next x (T substochastic, everything non-negative).  The decision
+// `diff > eps` of a cell is therefore the reference's whenever |diff - eps| exceeds
+// e_{t+1} (x_{t+1} + x_t) plus the subtraction's rounding; a cell inside that margin flags the
+// solve as ambiguous and the caller re-solves it in the reference's order (xt_iter_ell_kernel).
+// Without an ambiguous cell every decision, and so the iteration count, is the reference's; the
+// iterates differ from the reference's by at most e_t relative (26 iterations at 105 x 68:
+// <= 4e-11; measured 7e-15).
 //
 // Hand-off (MI355X_MICROARCH.md, visibility, Valid forms row 1): each workgroup stores its new x
 // values write-through (agent-scope atomic stores) into a FRESH 128-B aligned row of a scratch
 // history (a line is never read before it is written), every storing wave drains its stores,
-// one lane adds to a monotonic arrival counter and polls it; every load of handed-off words is an
-// agent-scope atomic load.  The poll is bounded (1 s of the wall clock): a workgroup that times
-// out sets the abort word and every workgroup leaves at its next barrier; the host then re-solves
-// in the reference's order.
+// one lane arrives at the barrier; every load of handed-off words is an sc1 load (16-B buffer
+// loads).  The barrier is XCD-hierarchical (workgroups b and b + 8 share an XCD): one counter per
+// group, the group's last arriver adds to the top counter, the last group's last arriver writes
+// every group's generation word, which the group's workgroups poll.  Every poll is bounded (1 s
+// of the wall clock): a workgroup that times out sets the abort word and every workgroup leaves
+// at its next barrier; the host then re-solves in the reference's order.
 constexpr int XF_THREADS = 512;   // 2 waves per SIMD: 256 VGPRs each, half of them entries
 constexpr int XF_HALVES = XF_THREADS / 32;  // half-waves per workgroup
 constexpr int XF_G = 8;                     // units reduced together by a half-wave
 #ifndef SA_XF_PAIR
-#define SA_XF_PAIR 2  // units whose x reads may be in flight together
+#define SA_XF_PAIR 2  // units per pipeline stage: the next stage's x reads are in flight meanwhile
 #endif
 constexpr int XF_PAIR = SA_XF_PAIR;
+static_assert(XF_G % XF_PAIR == 0, "SA_XF_PAIR");
 #ifndef SA_XF_KREG
-#define SA_XF_KREG 32  // units per half-wave held in registers (the rest re-read every iteration)
+#define SA_XF_KREG 32  // units per half-wave held in registers
 #endif
 constexpr int XF_KREG = SA_XF_KREG;
 static_assert(XF_KREG % XF_G == 0 && XF_KREG >= XF_G && XF_KREG <= 48, "SA_XF_KREG");
+constexpr int XF_KOV_MAX = 16;  // units per half-wave held in LDS past the registers (the rest
+                                // are re-read from the compact rows every iteration)
+constexpr int XF_UNIT_BYTES = 32 * 16;      // a unit: 32 lanes x 16 B
+constexpr int XF_X16 = (XE_XMAX / 2 + XF_THREADS - 1) / XF_THREADS;  // 16-B loads of x per thread
+constexpr int XF_ROWL = 8;                  // lanes per row in the row phase
 constexpr long long XF_SPIN_TICKS = 100000000;  // 1 s of the 100 MHz wall clock
-// control words (int32, zeroed before the launch): arrivals, timeout, ambiguous, iterations, then
-// one flag per iteration (some cell moved by more than eps)
-constexpr int XF_BAR = 0, XF_ABORT = 1, XF_AMB = 2, XF_NITER = 3, XF_FLAGS = 8;
+// control words (int32, zeroed before the launch), each counter on a 128-B line of its own:
+// timeout, ambiguous, iterations (line 0), the top arrival counter (line 1), per group g & 7 its
+// arrival counter (lines 2..9) and generation (lines 10..17), then one flag per iteration (some
+// cell moved by more than eps)
+constexpr int XF_ABORT = 1, XF_AMB = 2, XF_NITER = 3, XF_TOP = 32, XF_GRP = 64, XF_GEN = 64 + 8 * 32,
+              XF_FLAGS = 64 + 16 * 32;
 #ifndef SA_XF_PROBE
-#define SA_XF_PROBE 0  // 1: workgroup 0's wall-clock ticks per phase in control words 4..7 (stderr)
+#define SA_XF_PROBE 0  // 1: workgroup 0's wall-clock ticks per phase in control words 4..7 (stderr);
+#endif                 // diagnostic builds (wrong values): 2 = conflict-free x reads, 4 = no lane tree
+__device__ __forceinline__ uint32_t xf_col(uint32_t e, int q) {
+#if SA_XF_PROBE & 2
+  return (uint32_t)((threadIdx.x & 63) + 64 * q) + (e & 0x10000u ? 1u : 0u);
+#else
+  (void)q;
+  return e & 0xFFFFu;
 #endif
+}
 typedef uint32_t __attribute__((address_space(1))) xf_gu32;
 typedef unsigned long long __attribute__((address_space(1))) xf_gu64;
 
 __device__ __forceinline__ uint32_t xf_ld32(const int32_t* p) {
   return __hip_atomic_load((xf_gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void xf_st32(int32_t* p, uint32_t v) {
+  __hip_atomic_store((xf_gu32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t xf_add32(int32_t* p, uint32_t v) {
+  return __hip_atomic_fetch_add((xf_gu32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Poll *p (relaxed sc1 loads, s_sleep between) until >= target; false on the abort word or the
+// wall-clock bound (which then sets it).
+__device__ bool xf_wait(int32_t* ctrl, int32_t* p, uint32_t target) {
+  const long long t0 = wall_clock64();
+  while (xf_ld32(p) < target) {
+    if (xf_ld32(ctrl + XF_ABORT)) return false;
+    if (wall_clock64() - t0 > XF_SPIN_TICKS) {
+      xf_st32(ctrl + XF_ABORT, 1u);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  return true;
 }
 
 // Largest i in [0, nrl) with luo[i] <= gu (luo ascending, luo[0] <= gu < luo[nrl]).
@@ -1004,44 +1046,110 @@ __device__ __forceinline__ u32x4 xf_unit(const uint32_t* __restrict__ ell, const
   return e;
 }
 
-// The lane's part of a unit's sum: its 4 entries in order, count * x by fmas.
-__device__ __forceinline__ double xf_dot(const u32x4& e, const double* xs) {
-  double s = (double)(e[0] >> 16) * xs[e[0] & 0xFFFFu];
-  s = __builtin_fma((double)(e[1] >> 16), xs[e[1] & 0xFFFFu], s);
-  s = __builtin_fma((double)(e[2] >> 16), xs[e[2] & 0xFFFFu], s);
-  return __builtin_fma((double)(e[3] >> 16), xs[e[3] & 0xFFFFu], s);
-}
-
 __device__ __forceinline__ bool xf_has_esc(const u32x4& e) {
   return (e[0] >> 16) == XE_CNT_ESC || (e[1] >> 16) == XE_CNT_ESC || (e[2] >> 16) == XE_CNT_ESC ||
          (e[3] >> 16) == XE_CNT_ESC;
 }
 
+// Cross-lane moves without LDS (DPP and gfx950's v_permlane16_swap): a reduction through
+// ds_bpermute paid the LDS latency at every one of its dependent levels (5.3 of 8.7 us per
+// iteration at cfg5, probe build SA_XF_PROBE & 4).
+template <int CTRL>
+__device__ __forceinline__ double xf_dpp(double v) {  // DPP row op on both dwords
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, false);
+  return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+constexpr int XF_DPP_QUAD_XOR1 = 0xB1, XF_DPP_QUAD_XOR2 = 0x4E, XF_DPP_ROW_MIRROR = 0x140,
+              XF_DPP_ROW_HALF_MIRROR = 0x141;
+// a's lanes 16-31 <-> b's lanes 0-15 (and 48-63 <-> 32-47): each 32-lane half with itself
+__device__ __forceinline__ void xf_swap16(double& a, double& b) {
+  const long long x = __double_as_longlong(a), y = __double_as_longlong(b);
+  const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)x, (unsigned)y, false, false);
+  const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)(x >> 32), (unsigned)(y >> 32), false, false);
+  a = __longlong_as_double((long long)(((unsigned long long)hi[0] << 32) | lo[0]));
+  b = __longlong_as_double((long long)(((unsigned long long)hi[1] << 32) | lo[1]));
+}
+
 // 8 unit values per lane -> the sum over the half-wave's 32 lanes of unit (l32 >> 2) & 7, in
-// lanes with l32 % 4 == 0 (and their 3 neighbours): recursive halving over lane bits 4, 3, 2, then
-// a butterfly over bits 1, 0 (a + b and b + a are the same double: the 4 copies agree).
+// lanes with l32 % 4 == 0 (and their 3 neighbours), by a fixed tree: recursive halving over the
+// lane pairs (l, l + 16) (row swap), (l, 15 - l) within 16 (row mirror), (l, 7 - l) within 8
+// (half mirror), then a butterfly within the quad (a + b and b + a are the same double: the 4
+// copies agree).  Every pair stays inside its 32-lane half.
 __device__ __forceinline__ double xf_reduce8(double (&v)[XF_G], int l32) {
 #pragma unroll
-  for (int D = 16, h = XF_G / 2; D >= 4; D >>= 1, h >>= 1) {
-    const bool hi = (l32 & D) != 0;
+  for (int i = 0; i < 4; ++i) {  // lanes 0-15 keep units 0-3, lanes 16-31 units 4-7
+    xf_swap16(v[i], v[i + 4]);
+    v[i] = v[i] + v[i + 4];
+  }
+  const bool b3 = (l32 & 8) != 0, b2 = (l32 & 4) != 0;
 #pragma unroll
-    for (int i = 0; i < h; ++i) {
-      const double send = hi ? v[i] : v[i + h];
-      const double keep = hi ? v[i + h] : v[i];
-      v[i] = keep + __shfl_xor(send, D);
-    }
+  for (int i = 0; i < 2; ++i) {
+    const double send = b3 ? v[i] : v[i + 2];
+    const double keep = b3 ? v[i + 2] : v[i];
+    v[i] = keep + xf_dpp<XF_DPP_ROW_MIRROR>(send);
+  }
+  {
+    const double send = b2 ? v[0] : v[1];
+    const double keep = b2 ? v[1] : v[0];
+    v[0] = keep + xf_dpp<XF_DPP_ROW_HALF_MIRROR>(send);
   }
   double s = v[0];
-  s = s + __shfl_xor(s, 2);
-  return s + __shfl_xor(s, 1);
+  s = s + xf_dpp<XF_DPP_QUAD_XOR1>(s);
+  return s + xf_dpp<XF_DPP_QUAD_XOR2>(s);
+}
+
+// 8 units' sums (registers e[8]): per lane its 4 entries of each unit, count * x by fmas in entry
+// order, software-pipelined by XF_PAIR units (the next stage's LDS reads of x issued before this
+// stage's arithmetic); then xf_reduce8.
+__device__ __forceinline__ double xf_group(const u32x4 (&e)[XF_G], const double* xs, int l32) {
+  double v[XF_G];
+  double xa[XF_PAIR][4], xb[XF_PAIR][4];
+#pragma unroll
+  for (int p = 0; p < XF_PAIR; ++p)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) xa[p][q] = xs[xf_col(e[p][q], q)];
+#pragma unroll
+  for (int s = 0; s < XF_G / XF_PAIR; ++s) {
+    double(&cur)[XF_PAIR][4] = (s & 1) ? xb : xa;
+    double(&nxt)[XF_PAIR][4] = (s & 1) ? xa : xb;
+    if (s + 1 < XF_G / XF_PAIR) {
+#pragma unroll
+      for (int p = 0; p < XF_PAIR; ++p)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) nxt[p][q] = xs[xf_col(e[(s + 1) * XF_PAIR + p][q], q)];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int p = 0; p < XF_PAIR; ++p) {
+      const u32x4& u = e[s * XF_PAIR + p];
+      double a = (double)(u[0] >> 16) * cur[p][0];
+      a = __builtin_fma((double)(u[1] >> 16), cur[p][1], a);
+      a = __builtin_fma((double)(u[2] >> 16), cur[p][2], a);
+      v[s * XF_PAIR + p] = __builtin_fma((double)(u[3] >> 16), cur[p][3], a);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+#if SA_XF_PROBE & 4
+  double z = 0.0;
+#pragma unroll
+  for (int k = 0; k < XF_G; ++k) z += v[k];
+  return z;
+#else
+  return xf_reduce8(v, l32);
+#endif
 }
 
 __global__ __launch_bounds__(XF_THREADS) void xt_solve_reordered_kernel(
-    const uint32_t* __restrict__ ell, const int32_t* __restrict__ row_len, const int32_t* __restrict__ cnt_rows,
-    const unsigned long long* __restrict__ move, const double* __restrict__ gs, const double* __restrict__ pmove,
-    int C, int hp, double eps, int max_iter, int pmax, double* xb, double* __restrict__ heat, int32_t* ctrl) {
-  extern __shared__ __attribute__((aligned(16))) double xs[];  // [C] x_t | part [pmax] | luo [C + 1]
-  double* part = xs + C;
+    const uint32_t* __restrict__ ell, const int32_t* __restrict__ row_len, const unsigned long long* __restrict__ move,
+    const double* __restrict__ gs, const double* __restrict__ pmove, int C, int hp, double eps, int max_iter,
+    int pmax, int kov, double* xb, double* __restrict__ heat, int32_t* ctrl) {
+  // LDS: ov [XF_HALVES][kov] units | xs [C] x_t | part [pmax] unit sums | luo [pmax + 1]
+  extern __shared__ __attribute__((aligned(16))) u32x4 xf_lds[];
+  u32x4* ov = xf_lds;
+  double* xs = reinterpret_cast<double*>(xf_lds + (size_t)XF_HALVES * kov * 32);
+  double* part = xs + ((C + 1) & ~1);
   int32_t* luo = reinterpret_cast<int32_t*>(part + pmax);
   uint32_t* scan = reinterpret_cast<uint32_t*>(xs);  // prologue: units of every row, scanned
   __shared__ uint32_t ws[XF_THREADS / 64 + 1];
@@ -1079,18 +1187,20 @@ __global__ __launch_bounds__(XF_THREADS) void xt_solve_reordered_kernel(
   }
   __syncthreads();
   const int ra = s_ra, nrl = s_rb - s_ra;
-  for (int i = t; i <= nrl; i += XF_THREADS) luo[i] = (int32_t)scan[ra + i];
-  __syncthreads();  // the scan's words are x's from here on
-  const int ua = luo[0], nu = luo[nrl] - ua;
-  if (nu > pmax) {  // the host's bound on units per workgroup was wrong: never; the others leave
-    if (t == 0)     // at their first barrier
-      __hip_atomic_store((xf_gu32*)(ctrl + XF_ABORT), 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int ua = (int)scan[ra], nu = (int)scan[ra + nrl] - ua;
+  // the host's bounds on units and rows per workgroup (never exceeded): the others leave at
+  // their first barrier
+  if (nu > pmax || nrl > pmax) {
+    if (t == 0) xf_st32(ctrl + XF_ABORT, 2u);
     return;
   }
+  for (int i = t; i <= nrl; i += XF_THREADS) luo[i] = (int32_t)scan[ra + i];
+  __syncthreads();  // the scan's words are x's from here on
   const int hb = (int)((int64_t)nu * hw / XF_HALVES), he = (int)((int64_t)nu * (hw + 1) / XF_HALVES);
   const int hn = he - hb;  // this half-wave's units: local [hb, he)
 
-  // ---- the half-wave's first XF_KREG units, held in registers for the whole solve
+  // ---- the half-wave's units: the first XF_KREG in registers for the whole solve, the next kov
+  // in LDS, any further ones re-read from the compact rows every iteration
   u32x4 E[XF_KREG];
   bool esc = false;
 #pragma unroll
@@ -1098,18 +1208,17 @@ __global__ __launch_bounds__(XF_THREADS) void xt_solve_reordered_kernel(
     E[k] = k < hn ? xf_unit(ell, row_len, luo, nrl, ra, pe, ua + hb + k, l32) : u32x4{0u, 0u, 0u, 0u};
     esc |= xf_has_esc(E[k]);
   }
-  for (int k = XF_KREG; k < hn; ++k) esc |= xf_has_esc(xf_unit(ell, row_len, luo, nrl, ra, pe, ua + hb + k, l32));
+  u32x4* my_ov = ov + (size_t)hw * kov * 32 + l32;
+  for (int k = XF_KREG; k < XF_KREG + kov; ++k) {
+    const u32x4 e = k < hn ? xf_unit(ell, row_len, luo, nrl, ra, pe, ua + hb + k, l32) : u32x4{0u, 0u, 0u, 0u};
+    esc |= xf_has_esc(e);
+    my_ov[(k - XF_KREG) * 32] = e;
+  }
+  for (int k = XF_KREG + kov; k < hn; ++k) esc |= xf_has_esc(xf_unit(ell, row_len, luo, nrl, ra, pe, ua + hb + k, l32));
   if (__syncthreads_or(esc)) {  // a count >= 65535 (its value is in the dense row only): the host
     if (t == 0)                 // re-solves in order; the others leave at their first barrier
-      __hip_atomic_store((xf_gu32*)(ctrl + XF_ABORT), 4u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      xf_st32(ctrl + XF_ABORT, 4u);
     return;
-  }
-  // this thread's first row's constants
-  double m0 = 1.0, g0 = 0.0, p0 = 0.0;
-  if (t < nrl) {
-    m0 = (double)move[ra + t];
-    g0 = gs[ra + t];
-    p0 = pmove[ra + t];
   }
 
 #if SA_XF_PROBE
@@ -1127,109 +1236,114 @@ __global__ __launch_bounds__(XF_THREADS) void xt_solve_reordered_kernel(
   const double delta = (2.0 * (double)C + 16.0) * u;
   double ebound = 0.0;  // relative distance of x_t from the reference's x_t (bound)
   int n_iter = -1;
+  const int grp = g & 7, ngrp = G < 8 ? G : 8, nq = (G - grp + 7) >> 3;  // barrier groups
+  const int n16 = (C + 1) >> 1;                                         // 16-B words of x
   for (int it = 0; it < max_iter; ++it) {
     // the entries as the loop's own values: derived words (LDS addresses, counts as doubles)
     // hoisted out of the loop would take three times their registers
 #pragma unroll
     for (int k = 0; k < XF_KREG; ++k) asm volatile("" : "+v"(E[k]));
-    // ---- stage x_t (write-through stores of every workgroup, read by agent-scope loads)
+    // ---- stage x_t: every 16-B word of the row loaded (sc1) before any LDS store
     if (it == 0) {
       for (int c = t; c < C; c += XF_THREADS) xs[c] = 0.0;
     } else {
-      const xf_gu64* src = (const xf_gu64*)(xb + (int64_t)it * hp);
-      constexpr int XR = 8;  // loads in flight per thread
-      for (int c0 = 0; c0 < C; c0 += XR * XF_THREADS) {
-        unsigned long long xr[XR];
+      const auto rs = __builtin_amdgcn_make_buffer_rsrc(xb + (int64_t)it * hp, 0, hp * 8, 0x00020000);
+      u32x4 xr[XF_X16];  // past the row: the descriptor's range check returns 0, no memory access
 #pragma unroll
-        for (int q = 0; q < XR; ++q) {
-          const int c = c0 + t + q * XF_THREADS;
-          xr[q] = c < C ? __hip_atomic_load(src + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
-        }
+      for (int q = 0; q < XF_X16; ++q) xr[q] = __builtin_amdgcn_raw_buffer_load_b128(rs, (t + q * XF_THREADS) * 16, 0, 16);
 #pragma unroll
-        for (int q = 0; q < XR; ++q) {
-          const int c = c0 + t + q * XF_THREADS;
-          if (c < C) xs[c] = __longlong_as_double((long long)xr[q]);
-        }
+      for (int q = 0; q < XF_X16; ++q) {
+        const int w = t + q * XF_THREADS;
+        if (w < n16) reinterpret_cast<u32x4*>(xs)[w] = xr[q];
       }
     }
     __syncthreads();
     tick(1);
-    // ---- unit sums of the half-wave: registers, then any further units re-read from ell
+    // ---- unit sums of the half-wave: registers, LDS, then re-read ones
 #pragma unroll
     for (int k0 = 0; k0 < XF_KREG; k0 += XF_G) {
       if (k0 < hn) {  // half-wave uniform
-        double v[XF_G];
+        u32x4 e8[XF_G];
 #pragma unroll
-        for (int k = 0; k < XF_G; ++k) {
-          v[k] = xf_dot(E[k0 + k], xs);
-          // two units' LDS reads in flight at a time: the scheduler would otherwise hoist all
-          // 32 and spill the entry registers
-          if (k % XF_PAIR == XF_PAIR - 1) __builtin_amdgcn_sched_barrier(0);
-        }
-        const double s = xf_reduce8(v, l32);
+        for (int k = 0; k < XF_G; ++k) e8[k] = E[k0 + k];
+        const double s = xf_group(e8, xs, l32);
         const int k = k0 + ((l32 >> 2) & 7);
         if ((l32 & 3) == 0 && k < hn) part[hb + k] = s;
       }
     }
     for (int k0 = XF_KREG; k0 < hn; k0 += XF_G) {
-      double v[XF_G];
+      u32x4 e8[XF_G];
 #pragma unroll
       for (int k = 0; k < XF_G; ++k) {
-        v[k] = 0.0;
-        if (k0 + k < hn) {
-          v[k] = xf_dot(xf_unit(ell, row_len, luo, nrl, ra, pe, ua + hb + k0 + k, l32), xs);
-        }
+        const int kk = k0 + k;
+        e8[k] = kk >= hn ? u32x4{0u, 0u, 0u, 0u}
+                         : (kk < XF_KREG + kov ? my_ov[(kk - XF_KREG) * 32]
+                                                : xf_unit(ell, row_len, luo, nrl, ra, pe, ua + hb + kk, l32));
       }
-      const double s = xf_reduce8(v, l32);
+      const double s = xf_group(e8, xs, l32);
       const int k = k0 + ((l32 >> 2) & 7);
       if ((l32 & 3) == 0 && k < hn) part[hb + k] = s;
     }
     __syncthreads();
     tick(2);
-    // ---- rows: unit sums in order, / move, the reference's gs + pmove * (.) and its decision
+    // ---- rows, 8 lanes each: lane j sums units j, j + 8, ... in order, a fixed 8-lane tree; / move,
+    // the reference's gs + pmove * (.) and its decision
     const double enext = (ebound + delta) * (1.0 + 0x1p-20);
     bool up = false, amb = false;
     xf_gu64* dst = (xf_gu64*)(xb + (int64_t)(it + 1) * hp);
-    for (int i = t; i < nrl; i += XF_THREADS) {
-      const int r = ra + i;
-      double m = m0, gr = g0, pr = p0;
-      if (i != t) {
-        m = (double)move[r];
-        gr = gs[r];
-        pr = pmove[r];
+    const int sub = t & (XF_ROWL - 1);
+    for (int i0 = 0; i0 < nrl; i0 += XF_THREADS / XF_ROWL) {  // workgroup-uniform bound
+      const int i = i0 + t / XF_ROWL;
+      const bool live = i < nrl;
+      const int r = ra + (live ? i : 0);
+      double m = 1.0, gr = 0.0, pr = 0.0, xo = 0.0;
+      int u0 = 0, u1 = 0;
+      if (live) {
+        if (sub == 0) {
+          m = (double)move[r];
+          gr = gs[r];
+          pr = pmove[r];
+          xo = xs[r];
+        }
+        u0 = luo[i] - ua;
+        u1 = luo[i + 1] - ua;
       }
-      const int u0 = luo[i] - ua, u1 = luo[i + 1] - ua;
       double s = 0.0;
-      for (int q = u0; q < u1; ++q) s = s + part[q];
-      const double v = u1 > u0 ? s / m : 0.0;  // a row without entries sums +0 terms: 0
-      const double xn = gr + pr * v;
-      const double xo = xs[r];
-      const double d = xn - xo;
-      up |= d > eps;  // np.any(diff > eps)
-      const double margin = enext * (xn + xo) * (1.0 + 0x1p-20) + 8.0 * u * (fabs(d) + fabs(eps));
-      amb |= fabs(d - eps) <= margin;
-      __hip_atomic_store(dst + r, (unsigned long long)__double_as_longlong(xn), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-      heat[(int64_t)(it + 1) * C + r] = xn;
+      for (int q = u0 + sub; q < u1; q += XF_ROWL) s = s + part[q];
+      // a fixed 8-lane tree, lane 0's result used: pairs (l, 7 - l), then the quad's butterfly
+      s = s + xf_dpp<XF_DPP_ROW_HALF_MIRROR>(s);
+      s = s + xf_dpp<XF_DPP_QUAD_XOR1>(s);
+      s = s + xf_dpp<XF_DPP_QUAD_XOR2>(s);
+      if (live && sub == 0) {
+        const double v = u1 > u0 ? s / m : 0.0;  // a row without entries sums +0 terms: 0
+        const double xn = gr + pr * v;
+        const double d = xn - xo;
+        up |= d > eps;  // np.any(diff > eps)
+        const double margin = enext * (xn + xo) * (1.0 + 0x1p-20) + 8.0 * u * (fabs(d) + fabs(eps));
+        amb |= fabs(d - eps) <= margin;
+        __hip_atomic_store(dst + r, (unsigned long long)__double_as_longlong(xn), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        heat[(int64_t)(it + 1) * C + r] = xn;
+      }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its stores
     const int any_up = __syncthreads_or(up), any_amb = __syncthreads_or(amb);
     tick(3);
-    if (t == 0) {  // ---- grid barrier: one arrival per workgroup, one lane polls
+    if (t == 0) {  // ---- grid barrier, XCD-hierarchical; one lane per workgroup
       if (any_up) __hip_atomic_fetch_or((xf_gu32*)(ctrl + XF_FLAGS + it), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (any_amb) __hip_atomic_fetch_or((xf_gu32*)(ctrl + XF_AMB), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_fetch_add((xf_gu32*)(ctrl + XF_BAR), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const uint32_t target = (uint32_t)(it + 1) * (uint32_t)G;
-      const long long t0 = wall_clock64();
-      while (xf_ld32(ctrl + XF_BAR) < target) {
-        if (xf_ld32(ctrl + XF_ABORT)) break;
-        if (wall_clock64() - t0 > XF_SPIN_TICKS) {
-          __hip_atomic_store((xf_gu32*)(ctrl + XF_ABORT), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
+      const uint32_t epoch = (uint32_t)it + 1;
+      const uint32_t old = xf_add32(ctrl + XF_GRP + 32 * grp, 1u);
+      bool go = true;
+      if (old == epoch * (uint32_t)nq - 1) {  // the group's last arriver
+        const uint32_t ot = xf_add32(ctrl + XF_TOP, 1u);
+        if (ot == epoch * (uint32_t)ngrp - 1) {  // the last group: release every group
+          for (int q = 0; q < ngrp; ++q) xf_st32(ctrl + XF_GEN + 32 * q, epoch);
+          go = false;
         }
-        __builtin_amdgcn_s_sleep(2);
       }
+      if (go) xf_wait(ctrl, ctrl + XF_GEN + 32 * grp, epoch);
     }
     __syncthreads();
     tick(4);
@@ -1418,9 +1532,13 @@ static int xt_solve_reordered(const uint32_t* ell, const int32_t* row_len, const
   const int G = device_cus(dev);
   const int upr = (C + XE_KC - 1) / XE_KC;                 // units of a dense row
   const int64_t kmax = (int64_t)C * upr + C;               // row weights (units + 1), at most
-  const int pmax = (int)((kmax + G - 1) / G) + upr + 2;    // units of one workgroup, at most
-  const size_t lds = (size_t)C * 8 + (size_t)pmax * 8 + ((size_t)C + 1) * 4;
-  if (lds + 1024 > (size_t)device_lds_max(dev)) return SA_OK;
+  const int pmax = (int)((kmax + G - 1) / G) + upr + 2;    // units (or rows) of one workgroup, at most
+  const size_t fixed = (size_t)((C + 1) & ~1) * 8 + (size_t)pmax * 8 + ((size_t)pmax + 1) * 4;
+  const size_t lmax = (size_t)device_lds_max(dev) - 1024;  // the kernel's static LDS
+  if (fixed + (size_t)C * 4 > lmax || (size_t)(C + 1) * 4 > (size_t)((C + 1) & ~1) * 8) return SA_OK;
+  int kov = (int)((lmax - fixed) / ((size_t)XF_HALVES * XF_UNIT_BYTES));
+  if (kov > XF_KOV_MAX) kov = XF_KOV_MAX;
+  const size_t lds = fixed + (size_t)XF_HALVES * kov * XF_UNIT_BYTES;
   int nb = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(xt_solve_reordered_kernel),
                                                    XF_THREADS, lds) != hipSuccess) {
@@ -1441,8 +1559,8 @@ static int xt_solve_reordered(const uint32_t* ell, const int32_t* row_len, const
   rc = check_hip(hipMemsetAsync(ctrl, 0, cbytes, st), "memset solve control");
   if (!rc) {
     hipLaunchKernelGGL(xt_solve_reordered_kernel, dim3((unsigned)G), dim3(XF_THREADS), lds, st, ell, row_len,
-                       cnt_rows, reinterpret_cast<const unsigned long long*>(move), gs, pmove, C, hp, eps, max_iter,
-                       pmax, xb, heat, ctrl);
+                       reinterpret_cast<const unsigned long long*>(move), gs, pmove, C, hp, eps, max_iter, pmax, kov,
+                       xb, heat, ctrl);
     rc = check_launch("xt_solve_reordered_kernel");
   }
   if (!rc) rc = check_hip(hipMemcpyAsync(h, ctrl, sizeof(h), hipMemcpyDeviceToHost, st), "copy solve control");
