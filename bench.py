@@ -513,10 +513,11 @@ def xt105_extra(ab, dist, dev, sharded: bool = False, cfg5_games: int = 62500,
         if sharded and dist is not None:  # band-sharded: all-to-all of the counted actions,
             mark()                         # each rank counts its bands; row-sharded iteration
             mark()  # (count and exchange happen inside the sharded fit)
+            xstats.clear()
             mats, _, n_iter, err = shard.xt_fit_bands_sharded(batches, l, w, interp_codes=icodes,
-                                                              solve=solve)
+                                                              solve=solve, stats=xstats)
             acc = None  # each rank holds only its row block of the transition counts
-            path[0] = 'sequential' if solve == 'rows' else 'reordered'
+            path[0] = xstats.get('solve_path', 'sequential')
         else:  # one all-reduce of the counts, replicated solve
             acc = ops.xt_count_many(batches, l, w, interp_codes=icodes)
             mark()
@@ -535,6 +536,7 @@ def xt105_extra(ab, dist, dev, sharded: bool = False, cfg5_games: int = 62500,
         mark()
         return n_iter, acc, mats, rates
     path = ['sequential']  # the value iteration's summation path of the last call
+    xstats = {}  # band-sharded exchange: kind, bytes and host reads of the last call (this rank)
     axes = ops.xt_interp_axes(l, w, dev)  # node positions (constants of the reference's grid)
     icodes = [ops.xt_interp_codes_buffer(b.n, dev) for b in batches]
     rate_out = [torch.empty(max(b.n, 16), dtype=torch.float64, device=dev) for b in batches]
@@ -603,6 +605,7 @@ def xt105_extra(ab, dist, dev, sharded: bool = False, cfg5_games: int = 62500,
                         'start-cell band; the 7140^2 table written once, no global atomics) '
                         'writing each action\'s 8-B interpolated-rate operand; value iteration '
                         'over the compact count rows; rate from the operands (LDS surface)',
+            **({'exchange': dict(xstats, rank=rank)} if xstats else {}),
             'solve_path': path[0] + (' (one launch, rows summed in a fixed parallel order under '
                                      'an error bound that keeps every convergence decision)'
                                      if path[0] == 'reordered' else ''),
@@ -611,6 +614,50 @@ def xt105_extra(ab, dist, dev, sharded: bool = False, cfg5_games: int = 62500,
                                                   f'{rtol:g} relative, iteration count exact'),
                                surface_max_rel_err=float(f"{getattr(par, 'surface_rel_err', 0.0):.3e}"))}
                if check else {})}
+
+
+def rotate_extra(args, dist, dev, d, ps, pc, inp, step, n, total_actions, world) -> dict:
+    """The headline step over ``--rotate`` K device copies of the batch (inputs and
+    probabilities at other addresses), used in turn: no step finds its inputs left in the 256 MB
+    Infinity Cache by the step before it, as a stream of fresh batches would not (the main
+    line's steps re-value one batch, whose id / team columns the bool pass then reads from the
+    Infinity Cache).  Same outputs, same buffers; timed like the main loop."""
+    K = int(args.rotate)
+    sets = [(inp['s'], inp['ps'], inp['pc'])]
+    keep = []
+    for _ in range(K - 1):
+        b = B.ActionBatch.from_columns(d, dev=dev)
+        keep.append(b)
+        sets.append((b.struct(), ps.clone(), pc.clone()))
+    first = dict(inp)
+
+    def use(k):
+        inp['s'], inp['ps'], inp['pc'] = sets[k % K]
+    for k in range(max(args.warmup, K)):
+        use(k)
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        use(k)
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    if dist:
+        wall = _reduce(dist, wall, dist.ReduceOp.MAX, dev)
+    inp.update(first)
+    ms = wall / args.steps * 1e3
+    return {'batches': K, 'ms_per_step': round(ms, 4),
+            'value': round(total_actions * args.steps / wall, 1),
+            'step_frac': round(STEP_BYTES * total_actions / (ms * 1e-3) / (world * HBM_PEAK_GBS * 1e9), 4),
+            'what': f'the step over {K} device copies of the batch in turn (inputs at other '
+                    'addresses each step: none left in the Infinity Cache by the step before); '
+                    'not the headline value'}
 
 
 def convert_extra(d, dist, dev, reps: int = 3) -> dict:
@@ -793,6 +840,9 @@ def main() -> None:
     ap.add_argument('--warmup', type=int, default=3)
     ap.add_argument('--games', type=int, default=10000, help='games per GPU (cfg2: 10k)')
     ap.add_argument('--cpu-seconds', type=float, default=15.0)
+    ap.add_argument('--rotate', type=int, default=2,
+                    help='also time the step over K device copies of the batch in turn (K >= 2; '
+                         '0: skip): the figure without cross-step Infinity Cache reuse')
     ap.add_argument('--e2e-games', type=int, default=1000,
                     help='games of the end-to-end (pandas in -> pandas out) side entry (0: skip)')
     ap.add_argument('--no-cpu', action='store_true')
@@ -922,7 +972,8 @@ def main() -> None:
     lab_buf = torch.empty((3, ld), dtype=torch.uint8, device=dev)
     lab = ops.LabelBlocks(n, lab_buf[0], lab_buf[1], None)
     val = torch.empty((3, ld), dtype=torch.float64, device=dev)
-    s_act = ab.struct()
+    # the step's inputs (--rotate swaps in other device copies of the same batch between steps)
+    inp = {'s': ab.struct(), 'ps': ps, 'pc': pc}
     # two cell-code buffers used by alternate steps: with the xT side stream of step k still
     # rating from its codes while step k+1's numeric pass writes the other buffer (pipelined)
     ring = {'bufs': [ops.xt_cells_buffer(n, dev), ops.xt_cells_buffer(n, dev)], 'k': 0, 'done': [None, None]}
@@ -949,18 +1000,18 @@ def main() -> None:
                              f'(fused entries: {FUSED_CALLS})')
         if xt == 'cells' and overlap and fork <= _num_index(order):
             raise SystemExit('xt=cells: the side stream forks after num_features')
-        by_name = {'bool_features': lambda: ops.features_into(s_act, bool_out),
-                   'num_features': (lambda: ops.features_into(s_act, num_out,
+        by_name = {'bool_features': lambda: ops.features_into(inp['s'], bool_out),
+                   'num_features': (lambda: ops.features_into(inp['s'], num_out,
                                                               xt_cells=(16, 12, cells())))
-                   if xt in ('cells', 'none') else (lambda: ops.features_into(s_act, num_out)),
-                   'num_features_nogs': (lambda: ops.features_into(s_act, num_nogs,
+                   if xt in ('cells', 'none') else (lambda: ops.features_into(inp['s'], num_out)),
+                   'num_features_nogs': (lambda: ops.features_into(inp['s'], num_nogs,
                                                                    xt_cells=(16, 12, cells())))
-                   if xt in ('cells', 'none') else (lambda: ops.features_into(s_act, num_nogs)),
+                   if xt in ('cells', 'none') else (lambda: ops.features_into(inp['s'], num_nogs)),
                    'goalscore': lambda: ops.goalscore_into(ab, out),
                    'labels': lambda: ops.labels(ab, 10, lab),
                    'formula': lambda: ops.formula(ab, ps, pc, val),
                    'labels_formula': lambda: ops.labels_formula(ab, ps, pc, 10, lab, val),
-                   'num_step': lambda: ops.step_into(s_act, num_out, ps, pc, 10, lab, val,
+                   'num_step': lambda: ops.step_into(inp['s'], num_out, inp['ps'], inp['pc'], 10, lab, val,
                                                      xt_cells=(16, 12, cells()) if xt in ('cells', 'none')
                                                      else None)}
         calls = tuple(by_name[k] for k in order)
@@ -1122,6 +1173,9 @@ def main() -> None:
             check_xt_rate(par, d, xt_last['rate'], xT_ref)
         par.merge(dist, dev)
         check_s = time.perf_counter() - tc
+    rotate = None
+    if args.rotate >= 2:  # the same step over K device copies of the batch, one per step in turn
+        rotate = rotate_extra(args, dist, dev, d, ps, pc, inp, step, n, total_actions, world)
     extra_side = {}
     if not args.no_side:
         # cfg3 first: its bool block wants a physically contiguous range, which cfg5's ~1e8
@@ -1222,6 +1276,8 @@ def main() -> None:
                         if base['cm'] else
                         f"{base['prio']}-priority side stream, forked after {base['fork']} VAEP "
                         'call(s), overlapped with the rest')}
+    if rotate is not None:
+        line['rotate'] = rotate
     line['vaep_order'] = order
     line['streams'] = ('one stream' if args.serial else
                        'VAEP kernels on the main stream, xT solve + rate on a side stream without a '

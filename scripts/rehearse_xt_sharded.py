@@ -55,10 +55,12 @@ def main():
     if mode == 'auto':
         mode = 'bands' if ops.xt_band_shape(l, w) is not None else 'rows'
 
+    stats = {}
+
     def fit():
         if mode in ('bands', 'bands-rows'):
             mats, heat, iters, err = shard.xt_fit_bands_sharded(
-                [ab], l, w, solve='rows' if mode == 'bands-rows' else 'compact')
+                [ab], l, w, solve='rows' if mode == 'bands-rows' else 'compact', stats=stats)
             assert int(err.item()) == 0
             return mats, heat, iters
         acc = ops.xt_zero_counts(l, w, dev, row_blocks=world)
@@ -72,7 +74,8 @@ def main():
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     out = {'rank': rank, 'world': world, 'backend': backend, 'grid': f'{l}x{w}', 'mode': mode,
-           'actions_this_rank': ab.n, 'iterations': iters, 'ms_sharded_fit': round(dt * 1e3, 3)}
+           'actions_this_rank': ab.n, 'iterations': iters, 'ms_sharded_fit': round(dt * 1e3, 3),
+           'exchange': stats}
     if rank == 0:
         cols = [synthetic.spadl_games(args.games, game_id0=r * args.games) for r in range(world)]
         acc = ops.xt_zero_counts(l, w, dev)
@@ -82,7 +85,10 @@ def main():
         t0 = time.perf_counter()
         # the bands mode's replicated iteration is the single-GPU solve itself (reordered sums
         # under the error bound); the row-sharded iterations sum in the reference's order
-        sol = ops.xt_solve(acc, exact_order=mode in ('rows', 'bands-rows'))
+        # (ranks sharing one GPU: a persistent solve that could not hold every CU falls back to
+        # the reference's order; compare with the path the sharded fit took)
+        sol = ops.xt_solve(acc, exact_order=mode in ('rows', 'bands-rows') or
+                           stats.get('solve_path', 'reordered') != 'reordered')
         torch.cuda.synchronize()
         out['ms_single_solve'] = round((time.perf_counter() - t0) * 1e3, 3)
         out['single_iterations'] = sol.n_iter

@@ -972,6 +972,10 @@ constexpr int XF_UNIT_BYTES = 32 * 16;      // a unit: 32 lanes x 16 B
 constexpr int XF_X16 = (XE_XMAX / 2 + XF_THREADS - 1) / XF_THREADS;  // 16-B loads of x per thread
 constexpr int XF_ROWL = 8;                  // lanes per row in the row phase
 constexpr long long XF_SPIN_TICKS = 100000000;  // 1 s of the 100 MHz wall clock
+// the first barrier: every workgroup of a resident grid arrives within microseconds of the
+// launch; one that waits 50 ms shares the GPU with another persistent grid (two processes on
+// one device: each may hold some CUs and wait for the rest) and gives up early
+constexpr long long XF_SPIN_TICKS_FIRST = 5000000;
 // control words (int32, zeroed before the launch), each counter on a 128-B line of its own:
 // timeout, ambiguous, iterations (line 0), the top arrival counter (line 1), per group g & 7 its
 // arrival counter (lines 2..9) and generation (lines 10..17), then one flag per iteration (some
@@ -1004,11 +1008,11 @@ __device__ __forceinline__ uint32_t xf_add32(int32_t* p, uint32_t v) {
 
 // Poll *p (relaxed sc1 loads, s_sleep between) until >= target; false on the abort word or the
 // wall-clock bound (which then sets it).
-__device__ bool xf_wait(int32_t* ctrl, int32_t* p, uint32_t target) {
+__device__ bool xf_wait(int32_t* ctrl, int32_t* p, uint32_t target, long long limit) {
   const long long t0 = wall_clock64();
   while (xf_ld32(p) < target) {
     if (xf_ld32(ctrl + XF_ABORT)) return false;
-    if (wall_clock64() - t0 > XF_SPIN_TICKS) {
+    if (wall_clock64() - t0 > limit) {
       xf_st32(ctrl + XF_ABORT, 1u);
       return false;
     }
@@ -1343,7 +1347,7 @@ __global__ __launch_bounds__(XF_THREADS) void xt_solve_reordered_kernel(
           go = false;
         }
       }
-      if (go) xf_wait(ctrl, ctrl + XF_GEN + 32 * grp, epoch);
+      if (go) xf_wait(ctrl, ctrl + XF_GEN + 32 * grp, epoch, it == 0 ? XF_SPIN_TICKS_FIRST : XF_SPIN_TICKS);
     }
     __syncthreads();
     tick(4);

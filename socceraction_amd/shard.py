@@ -118,6 +118,14 @@ def _all_to_all(out: torch.Tensor, inp: torch.Tensor, out_splits=None, in_splits
         out.copy_(h)
 
 
+def _to_host(t: torch.Tensor, stats=None) -> np.ndarray:
+    """The one place the exchange reads device values on the host (a stream synchronisation);
+    ``stats['host_reads']`` counts them."""
+    if stats is not None:
+        stats['host_reads'] = stats.get('host_reads', 0) + 1
+    return t.cpu().numpy()
+
+
 def band_ranges(n_bands: int, world: int) -> List[Tuple[int, int]]:
     """Bands [b0, b1) owned by each rank in the band-sharded fit: ceil(NB / world) consecutive
     bands per rank (the last ranks may own fewer, or none)."""
@@ -222,7 +230,7 @@ def _solve_row_block(rows, shot, goal, move, C: int, B: int, eps: float, max_ite
 
 def xt_fit_bands_sharded(batches, l: int, w: int, eps: float = 1e-5, max_iter: int = 1000,
                          group=None, batch: int = 8, interp_codes=None, solve: str = 'compact',
-                         exact_order: bool = False):
+                         exact_order: bool = False, stats=None):
     """Band-sharded xT fit (cfg5 over several GPUs) for grids the band-owned count holds
     (``ops.xt_band_shape``, e.g. 105 x 68): the ranks exchange their COUNTED ACTIONS, not count
     tables.  Rank r owns the start-cell bands [b0, b1) = ``band_ranges(NB, world)[r]``, i.e.
@@ -249,6 +257,7 @@ def xt_fit_bands_sharded(batches, l: int, w: int, eps: float = 1e-5, max_iter: i
        actions with the same ``exact_order`` ('rows': ``exact_order=True``).
 
     ``interp_codes``: one ``ops.xt_interp_codes_buffer`` per batch, filled for the rate.
+    ``stats`` (dict, optional) receives the exchange's kind, bytes and host reads.
     Returns ``(mats [4, C], heatmaps [n_iter + 1, C], n_iter, err)``; ``err`` is the error-flag
     word of ``sa_xt_count`` (check with ``ops.xt_check_errors(types.SimpleNamespace(err=err))``).
     """
@@ -274,7 +283,8 @@ def xt_fit_bands_sharded(batches, l: int, w: int, eps: float = 1e-5, max_iter: i
     err = torch.zeros(1, dtype=torch.int32, device=dev)
     ic = list(interp_codes) if interp_codes is not None else [None] * len(batches)
     parts = [ops.xt_bucket(b, l, w, err, interp_codes=c) for b, c in zip(batches, ic)]
-    sets_keys, sets_off = exchange_band_keys([(p.keys, p.band_off) for p in parts], NB, group, dev)
+    sets_keys, sets_off = exchange_band_keys([(p.keys, p.band_off) for p in parts], NB, group, dev,
+                                             stats)
     nb = b1 - b0
     rows = torch.zeros(B * C, dtype=torch.int32, device=dev)
     vec = torch.zeros((3, B), dtype=torch.int64, device=dev)
@@ -294,22 +304,72 @@ def xt_fit_bands_sharded(batches, l: int, w: int, eps: float = 1e-5, max_iter: i
     res = None
     if solve == 'compact' and C <= _native.SA_XT_COMPACT_MAX_C:
         res = _solve_compact_exchange(rows, full[0], full[1], full[2], C, B, eps, max_iter, group,
-                                      exact_order)
+                                      exact_order, stats)
+        if stats is not None:
+            stats['exchange'] = ('all-to-all of counted actions + all-gather of compact rows'
+                                 if res is not None else
+                                 'all-to-all of counted actions (escaped counts: row-sharded '
+                                 'iteration, all-gather of x per iteration)')
     if res is None:
+        if stats is not None:
+            stats['solve_path'] = 'sequential'
+        if stats is not None and solve == 'rows':
+            stats['exchange'] = 'all-to-all of counted actions + all-gather of x per iteration'
         res = _solve_row_block(rows, full[0], full[1], full[2], C, B, eps, max_iter, group, batch)
     mats, heat, iters = res
     return mats, heat, iters, err
 
 
+def pack_compact_rows(ell: torch.Tensor, row_chunks: torch.Tensor, pe: int,
+                      total: int) -> torch.Tensor:
+    """The used 128-slot chunks of compact rows (``sa_xt_compact_rows`` layout: row i at
+    ``ell[i * pe:]``, ``row_chunks[i]`` = ceil(len_i / 128) chunks used), packed in row order:
+    ``total`` (= row_chunks.sum(), host-known) chunks, int32 [total * 128].  Device ops only (a
+    prefix sum and one chunk gather): no host read."""
+    dev = ell.device
+    n = row_chunks.numel()
+    if total == 0 or n == 0:
+        return torch.zeros(0, dtype=ell.dtype, device=dev)
+    rc = row_chunks.to(torch.int64)
+    row_of = torch.repeat_interleave(torch.arange(n, device=dev), rc, output_size=total)
+    first = torch.cumsum(rc, 0) - rc
+    k = torch.arange(total, device=dev) - first[row_of]
+    return ell.view(-1, 128)[row_of * (pe // 128) + k].reshape(-1)
+
+
+def unpack_compact_rows(packs: torch.Tensor, stride: int, rank_chunks: np.ndarray,
+                        row_chunks: torch.Tensor, B: int, pe: int, out: torch.Tensor) -> torch.Tensor:
+    """The inverse for every rank at once: ``packs`` = the ranks' packs, rank q's at chunk
+    ``q * stride`` (an all-gather of equal-size buffers), ``rank_chunks[q]`` its chunk count
+    (host), ``row_chunks`` [C] every row's chunk count (device), rank q holding rows
+    [q B, (q + 1) B).  Writes the rows' used chunks into ``out`` (int32 [C * pe]; slots past a
+    row's length are left as they are: the iterations mask them by the row length)."""
+    dev = out.device
+    C = row_chunks.numel()
+    total = int(rank_chunks.sum())
+    if total == 0:
+        return out
+    rc = row_chunks.to(torch.int64)
+    row_of = torch.repeat_interleave(torch.arange(C, device=dev), rc, output_size=total)
+    first = torch.cumsum(rc, 0) - rc
+    j = torch.arange(total, device=dev)
+    k = j - first[row_of]
+    q = row_of // B
+    start = torch.from_numpy(np.concatenate([[0], np.cumsum(rank_chunks)[:-1]]).astype(np.int64)).to(dev)
+    src = q * stride + (j - start[q])
+    out.view(-1, 128)[row_of * (pe // 128) + k] = packs.view(-1, 128)[src]
+    return out
+
+
 def _solve_compact_exchange(rows, shot, goal, move, C: int, B: int, eps: float, max_iter: int,
-                            group, exact_order: bool = False):
+                            group, exact_order: bool = False, stats=None):
     """Step 5 of :func:`xt_fit_bands_sharded` with ``solve='compact'``: this rank holds the
     count rows [r B, r B + B) (``rows``); returns None (nothing exchanged) when a count of any
     rank reaches 65535, else ``(mats, heatmaps, n_iter)`` of the replicated iteration over the
-    gathered compact form.  The compact rows are exchanged as their used chunks only: row i's
-    first ceil(len_i / 128) * 128 slots (the chunk-interleaved layout of ``sa_xt_compact_rows``,
-    header), packed per rank in row order; the ranks' row blocks are consecutive, so the
-    gathered packs unpack into the full form in rank order."""
+    gathered compact form.  The compact rows are exchanged as their used 128-slot chunks only,
+    packed per rank in row order (:func:`pack_compact_rows`); the ranks' row blocks are
+    consecutive, so the gathered packs unpack into the full form (:func:`unpack_compact_rows`).
+    ONE host read: the gathered row lengths and the escaped-count flag."""
     import torch.distributed as dist
 
     from . import _native
@@ -321,34 +381,34 @@ def _solve_compact_exchange(rows, shot, goal, move, C: int, B: int, eps: float, 
     ptr = lambda t: t.data_ptr()  # noqa: E731
     r0 = r * B
     nrows = max(0, min(B, C - r0))
-    big = torch.zeros(1, dtype=torch.int32, device=dev)
-    if nrows:
-        big[0] = (rows[:nrows * C].max() >= 65535).to(torch.int32)
-    _all_reduce(big, dist.ReduceOp.MAX, group=group)
-    if int(big.item()):
-        return None
     pe = int(lib.sa_xt_compact_bytes(C, 1)) // 4  # slots per compact row
     ell = torch.empty(max(nrows, 1) * pe, dtype=torch.int32, device=dev)
-    slen = torch.zeros(B, dtype=torch.int32, device=dev)
+    slen = torch.zeros(B + 1, dtype=torch.int32, device=dev)  # [B] row lengths | escaped flag
     if nrows:
         _native.check(lib.sa_xt_compact_rows(ptr(rows), C, nrows, ptr(ell), ptr(slen), stream_handle()))
-    lens = torch.empty(W * B, dtype=torch.int32, device=dev)
+        slen[B] = (rows[:nrows * C].max() >= 65535).to(torch.int32)
+    lens = torch.empty(W * (B + 1), dtype=torch.int32, device=dev)
     _all_gather(lens, slen, group=group)
-    lens = lens[:C].contiguous()
-    used = (lens.to(torch.int64) + 127) // 128 * 128  # slots each row occupies
-    per_rank = torch.nn.functional.pad(used, (0, W * B - C)).view(W, B).sum(dim=1)
-    tot = per_rank.cpu().numpy()
-    mx = max(int(tot.max()), 1)
-    k = torch.arange(pe, device=dev)
-    send = torch.zeros(mx, dtype=torch.int32, device=dev)
+    lens = lens.view(W, B + 1)
+    h = _to_host(lens, stats)  # the compact exchange's one host read
+    if h[:, B].any():
+        return None
+    nch = (lens[:, :B].reshape(-1)[:C].to(torch.int64) + 127) // 128  # chunks of every row
+    nch_h = ((h[:, :B].reshape(-1)[:C].astype(np.int64) + 127) // 128)
+    rank_chunks = np.array([nch_h[q * B:min(C, (q + 1) * B)].sum() for q in range(W)], np.int64)
+    mx = max(int(rank_chunks.max()), 1)
+    send = torch.zeros(mx * 128, dtype=torch.int32, device=dev)
     if nrows:
-        packed = ell[:nrows * pe].view(nrows, pe)[k[None, :] < used[r0:r0 + nrows, None]]
-        send[:packed.numel()] = packed
-    recv = torch.empty(W * mx, dtype=torch.int32, device=dev)
+        mine = pack_compact_rows(ell, nch[r0:r0 + nrows], pe, int(rank_chunks[r]))
+        send[:mine.numel()] = mine
+    recv = torch.empty(W * mx * 128, dtype=torch.int32, device=dev)
     _all_gather(recv, send, group=group)
-    full = torch.zeros(C * pe, dtype=torch.int32, device=dev)
-    full.view(C, pe)[k[None, :] < used[:, None]] = torch.cat(
-        [recv[q * mx:q * mx + int(tot[q])] for q in range(W)])
+    full = torch.empty(C * pe, dtype=torch.int32, device=dev)
+    unpack_compact_rows(recv, mx, rank_chunks, nch, B, pe, full)
+    lens_c = lens[:, :B].reshape(-1)[:C].contiguous()
+    if stats is not None:
+        stats['compact_gathered_bytes'] = W * mx * 128 * 4
+        stats['compact_used_bytes'] = int(rank_chunks.sum()) * 128 * 4
     del recv, send, ell
     mats = torch.empty((4, C), dtype=torch.float64, device=dev)
     gp = torch.empty((2, C), dtype=torch.float64, device=dev)
@@ -358,38 +418,62 @@ def _solve_compact_exchange(rows, shot, goal, move, C: int, B: int, eps: float, 
     # single-GPU fit's own solve, so the same bits); cnt_rows is read for counts >= 65535 only,
     # which no rank has (checked above)
     from .ops import xt_solve_compact
-    heat, iters, _path = xt_solve_compact(full, lens, rows, move, gp[0], gp[1], C, eps, max_iter,
-                                          exact_order)
+    heat, iters, path = xt_solve_compact(full, lens_c, rows, move, gp[0], gp[1], C, eps, max_iter,
+                                         exact_order)
+    if stats is not None:
+        stats['solve_path'] = path
     if iters < 0:
         raise RuntimeError(f'xT value iteration did not converge within {max_iter} iterations')
     mats[3].copy_(heat[iters])
     return mats, heat[:iters + 1], iters
 
 
-def exchange_band_keys(parts, n_bands: int, group=None, dev=None):
+# per source rank and destination: its number of local batches, then the key count of each batch
+_MAX_ROUNDS = 64
+
+
+def exchange_band_keys(parts, n_bands: int, group=None, dev=None, stats=None):
     """Step 2 of :func:`xt_fit_bands_sharded`: ``parts`` = this rank's ``(keys, band_off)`` per
     local batch (keys sorted by band, ``band_off`` [NB + 1]); returns the key sets of THIS rank's
     bands, one per (local batch index, source rank): ``(keys list, band offsets list)`` where set
     k holds its band lb's keys at ``keys[k][off[k][lb] .. off[k][lb + 1])``.  Every rank runs
     the same number of exchanges (max local batches over the ranks; a rank with fewer sends
-    nothing in the extra ones)."""
+    nothing in the extra ones).
+
+    ONE host read for the whole exchange: a first all-to-all of fixed-size headers (every
+    rank's batch count and, per batch, the keys it sends each destination; at most
+    ``_MAX_ROUNDS`` batches per rank) gives every rank all the split sizes at once; then per
+    round one all-to-all of the keys (host-known splits, as RCCL's all_to_all_single needs) and
+    one of the band offsets (equal splits, device only).  ``stats`` (dict): host reads and bytes."""
     import torch.distributed as dist
     W = dist.get_world_size(group)
     NB = n_bands
     ranges = band_ranges(NB, W)
     per = -(-NB // W)
     dev = dev if dev is not None else (parts[0][0].device if parts else torch.device('cpu'))
-    rounds = torch.tensor([len(parts)], dtype=torch.int64, device=dev)
-    _all_reduce(rounds, dist.ReduceOp.MAX, group=group)
+    R = len(parts)
+    if R > _MAX_ROUNDS:
+        raise ValueError(f'at most {_MAX_ROUNDS} local batches per rank in one band exchange')
     cuts = torch.tensor([q0 for q0, _ in ranges] + [NB], dtype=torch.int64, device=dev)
     # the band offsets each destination needs: its bands q0 .. q0 + per (clamped), [W, per + 1]
     want = torch.tensor([[min(NB, q0 + k) for k in range(per + 1)] for q0, _ in ranges],
                         dtype=torch.int64, device=dev)
-    hcuts = (torch.stack([off[cuts] for _, off in parts]).cpu().numpy() if parts else
-             np.zeros((0, W + 1), np.int64))
+    hdr = torch.zeros((W, 1 + _MAX_ROUNDS), dtype=torch.int64, device=dev)
+    hdr[:, 0] = R
+    hc = (torch.stack([off[cuts] for _, off in parts]) if R else
+          torch.zeros((0, W + 1), dtype=torch.int64, device=dev))  # [R, W + 1] key cuts
+    if R:
+        hdr[:, 1:1 + R] = (hc[:, 1:] - hc[:, :-1]).T
+    rhdr = torch.empty_like(hdr)
+    _all_to_all(rhdr.view(-1), hdr.view(-1), group=group)
+    h = _to_host(torch.cat([rhdr.view(-1), hc.view(-1)]), stats)  # the exchange's one host read
+    rh = h[:W * (1 + _MAX_ROUNDS)].reshape(W, 1 + _MAX_ROUNDS)
+    hcuts = h[W * (1 + _MAX_ROUNDS):].reshape(R, W + 1)
+    rounds = int(rh[:, 0].max())
     sets_keys, sets_off = [], []
-    for k in range(int(rounds.item())):
-        if k < len(parts):
+    sent = recvd = 0
+    for k in range(rounds):
+        if k < R:
             keys_k, off_k = parts[k]
             send = (hcuts[k, 1:] - hcuts[k, :-1]).astype(np.int64)
             keys = keys_k[int(hcuts[k, 0]):int(hcuts[k, W])]
@@ -399,17 +483,20 @@ def exchange_band_keys(parts, n_bands: int, group=None, dev=None):
             send = np.zeros(W, np.int64)
             keys = torch.zeros(0, dtype=torch.int32, device=dev)
             offs = torch.zeros((W, per + 1), dtype=torch.int64, device=dev)
-        cnt = torch.from_numpy(send).to(dev)
-        rcnt = torch.empty(W, dtype=torch.int64, device=dev)
-        _all_to_all(rcnt, cnt, group=group)
-        recv_n = rcnt.cpu().numpy()
+        recv_n = rh[:, 1 + k].astype(np.int64)
         total = int(recv_n.sum())
         recv = torch.empty(max(total, 1), dtype=torch.int32, device=dev)
         _all_to_all(recv[:total], keys.contiguous(), recv_n.tolist(), send.tolist(), group=group)
         roff = torch.empty((W, per + 1), dtype=torch.int64, device=dev)
         _all_to_all(roff.reshape(-1), offs.contiguous().reshape(-1), group=group)
+        sent += int(send.sum())
+        recvd += total
         starts = np.concatenate([[0], np.cumsum(recv_n)])
         for q in range(W):
             sets_keys.append(recv[int(starts[q]):])
             sets_off.append(roff[q])
+    if stats is not None:
+        stats['keys_sent_bytes'] = stats.get('keys_sent_bytes', 0) + 4 * sent
+        stats['keys_recv_bytes'] = stats.get('keys_recv_bytes', 0) + 4 * recvd
+        stats['exchange_rounds'] = rounds
     return sets_keys, sets_off

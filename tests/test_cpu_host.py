@@ -301,6 +301,9 @@ def _band_keys(rank, part, R, NB):
     return keys[order].astype(np.uint32).view(np.int32), off.astype(np.int64)
 
 
+_BAND_PARTS = {2: (2, 1), 3: (2, 0, 1)}  # local batches per rank: uneven, one rank with none
+
+
 def _band_exchange_worker(rank, world, port, q):
     import torch
     import torch.distributed as dist
@@ -309,9 +312,11 @@ def _band_exchange_worker(rank, world, port, q):
     dist.init_process_group('gloo', init_method=f'tcp://127.0.0.1:{port}', rank=rank,
                             world_size=world)
     R, NB = 3, 11
-    nparts = 2 if rank == 0 else 1  # the ranks run different numbers of local batches
+    nparts = _BAND_PARTS[world][rank]  # the ranks run different numbers of local batches
     parts = [tuple(torch.from_numpy(a) for a in _band_keys(rank, k, R, NB)) for k in range(nparts)]
-    keys, offs = shard.exchange_band_keys(parts, NB, dev=torch.device('cpu'))
+    stats = {}
+    keys, offs = shard.exchange_band_keys(parts, NB, dev=torch.device('cpu'), stats=stats)
+    assert stats['host_reads'] == 1, stats  # one host read for every round's splits
     b0, b1 = shard.band_ranges(NB, world)[rank]
     got = []
     for k, o in zip(keys, offs):
@@ -325,36 +330,101 @@ def _band_exchange_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_band_key_exchange_gloo_world2():
-    """shard.exchange_band_keys (the band-sharded xT fit's all-to-all) over gloo, world 2, with
-    a different number of local batches per rank: each rank receives exactly the keys of its own
-    bands from every rank's every batch, with band offsets relative to its first band."""
+@pytest.mark.parametrize('world', [2, 3])
+def test_band_key_exchange_gloo(world):
+    """shard.exchange_band_keys (the band-sharded xT fit's all-to-all) over gloo, world 2 and 3
+    (3: uneven band ownership 4 / 4 / 3 bands, a rank with no local batch), with a different
+    number of local batches per rank: each rank receives exactly the keys of its own bands from
+    every rank's every batch, with band offsets relative to its first band, after ONE host read
+    of the split sizes (stats['host_reads'])."""
     import multiprocessing as mp
     import socket
 
     from socceraction_amd import shard
     assert shard.band_ranges(11, 2) == [(0, 6), (6, 11)]
+    assert shard.band_ranges(11, 3) == [(0, 4), (4, 8), (8, 11)]
     assert shard.band_ranges(3, 4) == [(0, 1), (1, 2), (2, 3), (3, 3)]
     with socket.socket() as s:
         s.bind(('127.0.0.1', 0))
         port = s.getsockname()[1]
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
-    procs = [ctx.Process(target=_band_exchange_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_band_exchange_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = dict((r, (keys, n)) for r, keys, n in (q.get(timeout=120) for _ in range(2)))
+    res = dict((r, (keys, n)) for r, keys, n in (q.get(timeout=120) for _ in range(world)))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
     R, NB = 3, 11
     every = np.concatenate([_band_keys(r, k, R, NB)[0].view(np.uint32).astype(np.int64)
-                            for r, nparts in ((0, 2), (1, 1)) for k in range(nparts)])
-    for r, (b0, b1) in enumerate(shard.band_ranges(NB, 2)):
+                            for r, nparts in enumerate(_BAND_PARTS[world]) for k in range(nparts)])
+    for r, (b0, b1) in enumerate(shard.band_ranges(NB, world)):
         band = (every >> 16) // R
         want = np.sort(every[(band >= b0) & (band < b1)])
         np.testing.assert_array_equal(res[r][0], want)
-        assert res[r][1] == 2 * 2  # two rounds (rank 0's batches) x two source ranks
+        assert res[r][1] == 2 * world  # two rounds (rank 0's batches) x every source rank
+
+
+def _compact_pack_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+
+    from socceraction_amd import shard
+    dist.init_process_group('gloo', init_method=f'tcp://127.0.0.1:{port}', rank=rank,
+                            world_size=world)
+    C, pe = 23, 384  # 3 chunks per row slot
+    B = -(-C // world)
+    lens = np.random.default_rng(7).integers(0, pe + 1, C)  # every rank knows every length
+    r0, nrows = rank * B, max(0, min(B, C - rank * B))
+    ell = torch.from_numpy(np.random.default_rng([rank, 8]).integers(0, 2 ** 31, max(nrows, 1) * pe)
+                           .astype(np.int32))
+    nch = torch.from_numpy((lens + 127) // 128)
+    rank_chunks = np.array([((lens[qq * B:min(C, (qq + 1) * B)] + 127) // 128).sum()
+                            for qq in range(world)], np.int64)
+    mx = int(rank_chunks.max())
+    send = torch.zeros(mx * 128, dtype=torch.int32)
+    mine = shard.pack_compact_rows(ell, nch[r0:r0 + nrows], pe, int(rank_chunks[rank]))
+    send[:mine.numel()] = mine
+    recv = torch.empty(world * mx * 128, dtype=torch.int32)
+    shard._all_gather(recv, send)
+    full = torch.full((C * pe,), -1, dtype=torch.int32)
+    shard.unpack_compact_rows(recv, mx, rank_chunks, nch, B, pe, full)
+    q.put((rank, ell.numpy(), full.numpy()))
+    dist.destroy_process_group()
+
+
+def test_compact_row_pack_unpack_gloo_world3():
+    """The band-sharded solve's compact-row exchange (shard.pack_compact_rows -> all-gather ->
+    shard.unpack_compact_rows) over gloo with 3 ranks and uneven row blocks (23 rows: 8 / 8 / 7):
+    every row's used 128-slot chunks land where the single-GPU compact form holds them, and the
+    slots past them are untouched."""
+    import multiprocessing as mp
+    import socket
+    world = 3
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_compact_pack_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {r: (e, f) for r, e, f in (q.get(timeout=120) for _ in range(world))}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    C, pe = 23, 384
+    B = -(-C // world)
+    lens = np.random.default_rng(7).integers(0, pe + 1, C)
+    for r in range(world):
+        full = res[r][1].reshape(C, pe)
+        for i in range(C):
+            owner, li = i // B, i % B
+            used = (lens[i] + 127) // 128 * 128
+            src = res[owner][0].reshape(-1, pe)[li]
+            np.testing.assert_array_equal(full[i, :used], src[:used])
+            assert (full[i, used:] == -1).all()
 
 
 # ----------------------------------------------------------------------------- synthetic data
