@@ -716,6 +716,12 @@ def rate_extra(ab, out, n, dev, reps: int = 5) -> dict:
     # passes (sa_vaep_features_conditions), both walks over bitmaps only
     from socceraction_amd import trees as T
     ms_cond = _events_ms(lambda: T.predict_pair_conditions(ab, out.plan, models), reps)
+    prep, cbits, words = T.condition_bitmaps(ab, out.plan, models)
+    ms_cond_feat = _events_ms(lambda: T.condition_bitmaps(ab, out.plan, models, bits=cbits), reps)
+    ms_cond_walk = [_events_ms(lambda k=k: T.walk_conditions(prep, k, models[k], cbits, words, n, dev,
+                                                             out=ps), reps) for k in range(2)]
+    cond_counts = {'union': prep['n_cond_union'], 'per_model': [w[5] for w in prep['walks']]}
+    del cbits
     f64bits = ops.features(ab, SPADL_DEFAULT, 3, num_tile=out.Rn, bool_bits=True)
     ms_feat64 = _events_ms(lambda: ops.features(ab, SPADL_DEFAULT, 3, out=f64bits), reps)
     ms_tree64 = _events_ms(lambda: models[0].predict_blocks(f64bits, out=ps), reps)
@@ -730,6 +736,9 @@ def rate_extra(ab, out, n, dev, reps: int = 5) -> dict:
             'method': 'staged condition walk (sa_tree_predict_staged) over the bitmaps and the '
                       'float32 numeric blocks',
             'ms_features_and_both_models_conditions': round(ms_cond, 4),
+            'ms_features_conditions': round(ms_cond_feat, 4),
+            'ms_per_model_conditions': [round(x, 4) for x in ms_cond_walk],
+            'conditions': cond_counts,
             'ms_rate_total_conditions': round(ms_cond + ms_formula, 4),
             'ms_features_bitmap_form': round(ms_feat, 4), 'ms_per_model': round(ms_tree, 4),
             'ms_features_bitmap_f64_form': round(ms_feat64, 4),
@@ -1013,7 +1022,10 @@ def main() -> None:
                    'labels_formula': lambda: ops.labels_formula(ab, ps, pc, 10, lab, val),
                    'num_step': lambda: ops.step_into(inp['s'], num_out, inp['ps'], inp['pc'], 10, lab, val,
                                                      xt_cells=(16, 12, cells()) if xt in ('cells', 'none')
-                                                     else None)}
+                                                     else None, chunk_rows=chunk, prefetch=pf)}
+        # chunk / pf (A/B probe, sa_vaep_step_f64_chunked): the numeric pass in launches of chunk
+        # rows, each after a pure-read pass pulling its inputs into the Infinity Cache (pf = 1)
+        chunk, pf = int(spec.get('chunk', 0)), bool(int(spec.get('pf', 0)))
         calls = tuple(by_name[k] for k in order)
         # cm=1: the count pass runs on the main stream right after num_features, in the fast
         # one-workgroup-per-CU shape; the side stream takes the all-reduce, solve and rate
@@ -1105,7 +1117,7 @@ def main() -> None:
             v = dict(base)
             for kv in [o for o in opts.split('/') if o]:
                 k_, _, v_ = kv.partition('=')
-                v[k_] = v_.split('+') if k_ == 'order' else (int(v_) if k_ in ('fork', 'par', 'cm', 'diag', 'xsync', 'pipe', 'tev') else v_)
+                v[k_] = v_.split('+') if k_ == 'order' else (int(v_) if k_ in ('fork', 'par', 'cm', 'diag', 'xsync', 'pipe', 'tev', 'chunk', 'pf') else v_)
             variants[name] = (make_step(v)[0], v['order'])
         ab_ms = {k: [] for k in variants}
         ab_kern = {}

@@ -235,6 +235,17 @@ int sa_vaep_step_f64(const sa_actions* a, const sa_feature_plan* plan, const sa_
                      uint32_t* xt_cells, int32_t nr_actions, uint8_t* scores, uint8_t* concedes,
                      uint8_t* goal_from_shot, int64_t ld, const double* p_scores,
                      const double* p_concedes, double* off, double* def, double* val, void* stream);
+/* sa_vaep_step_f64's numeric pass in launches of chunk_rows rows (a multiple of 512; 0: one
+ * launch), each optionally preceded (prefetch != 0) by a pure-read pass that pulls the chunk's
+ * inputs into the Infinity Cache: an A/B probe of the pass's read / write turnaround
+ * (bench.py --num-chunks).  The numeric pass only (bool_out without columns of the plan); the
+ * same outputs bit for bit. */
+int sa_vaep_step_f64_chunked(const sa_actions* a, const sa_feature_plan* plan, const sa_block* bool_out,
+                             const sa_block* f64_out, const sa_block* i64_out, int32_t xt_l, int32_t xt_w,
+                             uint32_t* xt_cells, int32_t nr_actions, uint8_t* scores, uint8_t* concedes,
+                             uint8_t* goal_from_shot, int64_t ld, const double* p_scores,
+                             const double* p_concedes, double* off, double* def, double* val,
+                             int64_t chunk_rows, int32_t prefetch, void* stream);
 
 /* ---- Expected Threat (xthreat.py) --------------------------------------------
  * Count pass over SPADL actions (frames[0] of `a`; segments ignored):

@@ -47,8 +47,15 @@ def main():
     cond = trees.predict_pair_conditions(ab, plan, models)
     ref = blocks()
     equal = all(torch.equal(a, b) for a, b in zip(cond, ref))
+    prep, bits, words = trees.condition_bitmaps(ab, plan, models)
+    out = torch.empty(ab.n, dtype=torch.float32, device=ab.device)
     res = {'n': ab.n, 'equal': equal,
            'conditions_ms': _ms(lambda: trees.predict_pair_conditions(ab, plan, models)),
+           'conditions_features_ms': _ms(lambda: trees.condition_bitmaps(ab, plan, models, bits=bits)),
+           'conditions_walk_ms': [_ms(lambda k=k: trees.walk_conditions(prep, k, models[k], bits, words, ab.n,
+                                                                        ab.device, out=out)) for k in range(2)],
+           'conditions': {'union': prep['n_cond_union'], 'per_model': [w[5] for w in prep['walks']],
+                          'nodes': [w[0].numel() for w in prep['walks']]},
            'f32_blocks_ms': _ms(blocks)}
     print(json.dumps(res), flush=True)
     if not equal:

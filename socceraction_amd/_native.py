@@ -116,6 +116,11 @@ _SIGNATURES = {
                                         ctypes.POINTER(SaBlock), ctypes.c_int32, ctypes.c_int32, _p,
                                         ctypes.c_int32, _p, _p, _p, ctypes.c_int64, _p, _p, _p, _p,
                                         _p, _p]),
+    'sa_vaep_step_f64_chunked': (ctypes.c_int, [ctypes.POINTER(SaActions), ctypes.POINTER(SaFeaturePlan),
+                                                ctypes.POINTER(SaBlock), ctypes.POINTER(SaBlock),
+                                                ctypes.POINTER(SaBlock), ctypes.c_int32, ctypes.c_int32, _p,
+                                                ctypes.c_int32, _p, _p, _p, ctypes.c_int64, _p, _p, _p, _p,
+                                                _p, ctypes.c_int64, ctypes.c_int32, _p]),
     'sa_xt_count': (ctypes.c_int, [ctypes.POINTER(SaActions), ctypes.c_int32, ctypes.c_int32,
                                    _p, _p, _p, _p, _p, _p]),
     'sa_xt_count_codes': (ctypes.c_int, [ctypes.POINTER(SaActions), ctypes.c_int32,

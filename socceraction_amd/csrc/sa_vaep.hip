@@ -74,6 +74,9 @@ struct FeatArgs {
   const float* cond_thr;                     // per condition: float32 threshold (`x < thr` goes left)
   const int32_t* cond_dl;                    // per condition: NaN goes left
   int32_t cond_row0;                         // bitmap row of condition 0 (after the bool columns)
+  // the numeric pass over rows [row0, row_end) only (row_end 0: to n); row0 a multiple of
+  // BLOCK_ACTS (sa_vaep_step_f64_chunked: one launch per chunk of the batch)
+  int64_t row0, row_end;
 };
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
@@ -1155,9 +1158,10 @@ void num_features_kernel(FeatArgs args) {
   const int64_t n = A.n;
   const int K = P.nb_prev_actions;
   const int64_t Rf = args.Rf, Ri = args.Ri;
-  const int64_t wave_base = (xcd_logical_block() * BLOCK_WAVES + wv) * WAVE_ACTS;
+  const int64_t wave_base = args.row0 + (xcd_logical_block() * BLOCK_WAVES + wv) * WAVE_ACTS;
   const sa_frame& F0 = A.frames[0];
-  if (wave_base >= n) return;  // whole wave past the end (uniform: the goalscore ballots need every lane)
+  // whole wave past the end (uniform: the goalscore ballots need every lane)
+  if (wave_base >= n || (args.row_end > 0 && wave_base >= args.row_end)) return;
   CondAcc acc{0, 0, 0, -64};
   CondSink sink_f{args.cond_fstart, args.cond_thr, args.cond_dl, args.bbits, args.bstride, args.cond_row0,
                   wave_base, n, &acc};
@@ -1865,7 +1869,40 @@ struct TailArgs {  // labels + f64 formula riding in the numeric pass (sa_vaep_s
   uint8_t *sc, *co, *gfs;
   const double *ps, *pc;
   double *off, *def, *val;
+  int64_t chunk;     // > 0: the numeric pass in launches of `chunk` rows (sa_vaep_step_f64_chunked)
+  int32_t prefetch;  // each chunk's inputs read into the Infinity Cache first
 };
+
+// sa_vaep_step_f64_chunked's probe of the numeric pass's read / write turnaround: rows [r0, r1)'s
+// inputs (coordinates, time, ids, team codes, probabilities: 64 B per row) read once with the
+// default cache policy, so the Infinity Cache holds them when the pass over the chunk runs --
+// the chunk's HBM reads happen in one pure-read burst instead of inside the pass's write stream.
+// 4 rows per thread; the values only feed a compare that never stores.
+__global__ __launch_bounds__(256) void prefetch_rows_kernel(sa_actions A, const double* __restrict__ ps,
+                                                            const double* __restrict__ pc, int64_t r0, int64_t r1,
+                                                            uint32_t* __restrict__ sink) {
+  const int64_t j = r0 + 4 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x);
+  if (j + 4 > r1) return;  // r0, r1 multiples of 4 (or r1 = n: the tail rows stay out)
+  const sa_frame& F = A.frames[0];
+  uint64_t h = 0;
+  auto f2 = [&](const double* c) {
+    if (!c) return;
+    const f64x2 a = *reinterpret_cast<const f64x2*>(c + j), b = *reinterpret_cast<const f64x2*>(c + j + 2);
+    h ^= (uint64_t)__double_as_longlong(a[0] + a[1] + b[0] + b[1]);
+  };
+  f2(F.c0);
+  f2(F.c1);
+  f2(F.c2);
+  f2(F.c3);
+  f2(F.time_seconds);
+  f2(ps);
+  f2(pc);
+  h ^= *reinterpret_cast<const uint32_t*>(F.type_id + j) ^ *reinterpret_cast<const uint32_t*>(F.result_id + j) ^
+       *reinterpret_cast<const uint32_t*>(F.bodypart_id + j) ^ *reinterpret_cast<const uint32_t*>(F.period_id + j);
+  const i32x4 tm = *reinterpret_cast<const i32x4*>(F.team + j);
+  h ^= (uint32_t)(tm[0] ^ tm[1] ^ tm[2] ^ tm[3]);
+  if (h == 0x5A5A5A5A5A5A5A5Aull) sink[0] = (uint32_t)h;  // never in practice: keeps the loads
+}
 
 static int launch_features(const sa_actions* a, const sa_feature_plan* plan, const sa_block* bool_out,
                            const sa_block* f64_out, const sa_block* i64_out, int32_t xt_l,
@@ -1977,7 +2014,39 @@ extern "C" int sa_vaep_step_f64(const sa_actions* a, const sa_feature_plan* plan
     return sa_vaep_labels_formula_f64(a, nr_actions, scores, concedes, goal_from_shot, ld, p_scores,
                                       p_concedes, off, def, val, stream);
   }
-  const TailArgs t{nr_actions, scores, concedes, goal_from_shot, p_scores, p_concedes, off, def, val};
+  const TailArgs t{nr_actions, scores, concedes, goal_from_shot, p_scores, p_concedes, off, def, val, 0, 0};
+  return launch_features(a, plan, bool_out, f64_out, i64_out, xt_l, xt_w, xt_cells, stream, nullptr, 0, 0, &t);
+}
+
+extern "C" int sa_vaep_step_f64_chunked(const sa_actions* a, const sa_feature_plan* plan, const sa_block* bool_out,
+                                        const sa_block* f64_out, const sa_block* i64_out, int32_t xt_l, int32_t xt_w,
+                                        uint32_t* xt_cells, int32_t nr_actions, uint8_t* scores, uint8_t* concedes,
+                                        uint8_t* goal_from_shot, int64_t ld, const double* p_scores,
+                                        const double* p_concedes, double* off, double* def, double* val,
+                                        int64_t chunk_rows, int32_t prefetch, void* stream) {
+  if (chunk_rows < 0 || chunk_rows % BLOCK_ACTS != 0)
+    return fail(SA_EINVAL, "chunk_rows must be a non-negative multiple of %d", BLOCK_ACTS);
+  if (!a || a->atomic || !plan || plan->nb_prev_actions > 3 || nr_actions < 1 || nr_actions > SA_STEP_MAX_NR ||
+      !p_scores || !p_concedes)
+    return fail(SA_EINVAL, "the chunked step takes the fused SPADL step form with probabilities");
+  if (bool_out && bool_out->n_cols > 0) {
+    for (int x = 0; x < SA_XFN_COUNT; ++x)
+      if (plan->bool_col[x] >= 0) return fail(SA_EINVAL, "the chunked step is the numeric pass only");
+  }
+  if (chunk_rows == 0)
+    return sa_vaep_step_f64(a, plan, bool_out, f64_out, i64_out, xt_l, xt_w, xt_cells, nr_actions, scores, concedes,
+                            goal_from_shot, ld, p_scores, p_concedes, off, def, val, stream);
+  int rc = check_actions(a, false);
+  if (rc) return rc;
+  if (ld % 16 != 0 || ld < ((a->n + 15) / 16) * 16)
+    return fail(SA_EINVAL, "ld must be a multiple of 16 and >= round_up(n, 16)");
+  if (!aligned16(scores) || !aligned16(concedes) || !aligned16(goal_from_shot) || !off || !def || !val ||
+      !aligned16(off) || !aligned16(def) || !aligned16(val))
+    return fail(SA_EINVAL, "label / formula outputs: non-null, 16-byte aligned");
+  if (xt_cells && (xt_l < 1 || xt_w < 1 || (int64_t)xt_l * xt_w > SA_XT_CELLS_MAX_C || !aligned16(xt_cells)))
+    return fail(SA_EINVAL, "bad xT cell code arguments");
+  const TailArgs t{nr_actions, scores, concedes, goal_from_shot, p_scores, p_concedes, off, def, val, chunk_rows,
+                   prefetch};
   return launch_features(a, plan, bool_out, f64_out, i64_out, xt_l, xt_w, xt_cells, stream, nullptr, 0, 0, &t);
 }
 
@@ -2104,6 +2173,19 @@ static int launch_features(const sa_actions* a, const sa_feature_plan* plan, con
         hipLaunchKernelGGL((num_features_kernel<true, false, 3, false, true>), grid, block, 0, st, args);
       else
         hipLaunchKernelGGL((num_features_kernel<false, false, 3, false, true>), grid, block, 0, st, args);
+    } else if (tail && tail->chunk > 0 && !a->atomic) {  // sa_vaep_step_f64_chunked (probe)
+      for (int64_t c0 = 0; c0 < a->n; c0 += tail->chunk) {
+        const int64_t c1 = c0 + tail->chunk < a->n ? c0 + tail->chunk : a->n;
+        if (tail->prefetch) {
+          const int64_t th = (c1 - c0 + 3) / 4;
+          hipLaunchKernelGGL(prefetch_rows_kernel, dim3((unsigned)((th + 255) / 256)), dim3(256), 0, st, *a,
+                             tail->ps, tail->pc, c0, c1, xt_cells);
+        }
+        args.row0 = c0;
+        args.row_end = c1;
+        const dim3 cg(xcd_grid((c1 - c0 + BLOCK_ACTS - 1) / BLOCK_ACTS));
+        hipLaunchKernelGGL((num_features_kernel<false, false, 3, true>), cg, block, 0, st, args);
+      }
     } else if (tail) {  // windowed, K <= 3 (checked by sa_vaep_step_f64)
       if (a->atomic)
         hipLaunchKernelGGL((num_features_kernel<true, false, 3, true>), grid, block, 0, st, args);

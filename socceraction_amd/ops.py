@@ -340,7 +340,8 @@ def labels_formula(batch: ActionBatch, p_scores: torch.Tensor, p_concedes: torch
 
 def step_into(s: _native.SaActions, out: FeatureBlocks, p_scores: Optional[torch.Tensor],
               p_concedes: Optional[torch.Tensor], nr_actions: int, labels_out: LabelBlocks,
-              values_out: Optional[torch.Tensor], xt_cells: Optional[tuple] = None) -> None:
+              values_out: Optional[torch.Tensor], xt_cells: Optional[tuple] = None,
+              chunk_rows: int = 0, prefetch: bool = False) -> None:
     """The batch valuation step in one call (``sa_vaep_step_f64``): the features of ``out``'s
     plan (and, with ``xt_cells = (l, w, cells)``, every action's xT cell code), the labels and
     the f64 formula of the same actions -- exactly :func:`features_into` followed by
@@ -360,6 +361,13 @@ def step_into(s: _native.SaActions, out: FeatureBlocks, p_scores: Optional[torch
     if cells is not None and (cells.dtype != torch.int32 or cells.numel() < s.n):
         raise ValueError('cells must be an int32 tensor of at least n elements')
     bb, fb, ib = out.sa_blocks()
+    if chunk_rows:  # A/B probe: the numeric pass in chunks, optionally prefetched (bench --num-chunks)
+        _native.check(_native.lib().sa_vaep_step_f64_chunked(
+            ctypes.byref(s), ctypes.byref(out.plan.struct), ctypes.byref(bb), ctypes.byref(fb),
+            ctypes.byref(ib), int(l), int(w), _ptr(cells), int(nr_actions), _ptr(labels_out.scores),
+            _ptr(labels_out.concedes), _ptr(labels_out.goal_from_shot), _ld(s.n), _ptr(ps), _ptr(pc),
+            _ptr(o[0]), _ptr(o[1]), _ptr(o[2]), int(chunk_rows), int(prefetch), stream_handle()))
+        return
     _native.check(_native.lib().sa_vaep_step_f64(
         ctypes.byref(s), ctypes.byref(out.plan.struct), ctypes.byref(bb), ctypes.byref(fb),
         ctypes.byref(ib), int(l), int(w), _ptr(cells), int(nr_actions), _ptr(labels_out.scores),

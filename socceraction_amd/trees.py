@@ -351,21 +351,30 @@ def _conditions_prep(plan, models: Sequence[TreeEnsemble], dev) -> dict:
     fstart = np.searchsorted(np.where(kind == 1, col, 1 << 30), np.arange(plan.n_f64 + 1), 'left')
     istart = np.count_nonzero(kind == 1) + np.searchsorted(col[kind == 2], np.arange(plan.n_i64 + 1), 'left')
     t = lambda v, dt: torch.from_numpy(np.ascontiguousarray(v, dt)).to(dev)  # noqa: E731
-    bool_cols = np.concatenate([lay['bool_cols'], nb + np.arange(n_num)]).astype(np.int32)
+    # the bitmap rows of the union's conditions: the used bool columns, then every numeric one
+    rows_all = np.concatenate([lay['bool_cols'], nb + np.arange(n_num)]).astype(np.int32)
     walks = []
     for m, ml in zip(models, lay['models']):
-        n_cond = 1 + len(bool_cols)
-        lds = _native.lib().sa_tree_staged_lds_bytes(len(ml['nodes']), n_cond, 1)
-        if lds > 160 * 1024 or n_cond > 65536 or len(ml['nodes']) >= 65536:
+        # each learner stages only the conditions ITS splits test (the union's other half is the
+        # other learner's): its nodes renumbered to its own condition list
+        cond = ml['nodes'] & 0xFFFF
+        used = np.unique(cond[cond != 0])
+        local = np.zeros(len(rows_all) + 1, np.uint32)
+        local[used] = np.arange(1, len(used) + 1, dtype=np.uint32)
+        nodes = (ml['nodes'] & np.uint32(0xFFFF0000)) | local[cond]
+        rows_m = rows_all[used - 1].astype(np.int32)
+        n_cond = 1 + len(rows_m)
+        lds = _native.lib().sa_tree_staged_lds_bytes(len(nodes), n_cond, 1)
+        if lds > 160 * 1024 or n_cond > 65536 or len(nodes) >= 65536:
             raise ValueError('the staged form of this model does not fit LDS')
-        walks.append((t(ml['nodes'].view(np.int32), np.int32), t(ml['leaf'], np.float32),
-                      t(ml['roots'], np.int32), m._device(dev)['depth']))
+        walks.append((t(nodes.view(np.int32), np.int32), t(ml['leaf'], np.float32),
+                      t(ml['roots'], np.int32), m._device(dev)['depth'],
+                      t(rows_m, np.int32) if len(rows_m) else None, len(rows_m)))
     cache = {'key': key, 'models': list(models), 'n_num': n_num, 'fstart': t(fstart, np.int32),
              'istart': t(istart, np.int32),
              'thr': t(lay['num_thr'] if n_num else np.zeros(1), np.float32),
              'dl': t(lay['num_dl'] if n_num else np.zeros(1), np.int32),
-             'bool_cols': t(bool_cols, np.int32) if len(bool_cols) else None, 'n_cond_bool': len(bool_cols),
-             'walks': walks}
+             'n_cond_union': len(rows_all), 'walks': walks}
     models[0]._cond_cache = cache
     return cache
 
@@ -377,6 +386,14 @@ def predict_pair_conditions(batch, plan, models: Sequence[TreeEnsemble], flip: b
     each learner's staged walk reads every condition as a bitmap (``sa_tree_predict_staged``,
     n_num = 0).  The same float32 probabilities as :meth:`TreeEnsemble.predict_blocks`, bit for
     bit.  Raises ValueError when a learner is not float32 (xgboost) or its walk does not fit LDS."""
+    prep, bits, words = condition_bitmaps(batch, plan, models, flip)
+    return [walk_conditions(prep, k, m, bits, words, batch.n, batch.device) for k, m in enumerate(models)]
+
+
+def condition_bitmaps(batch, plan, models: Sequence[TreeEnsemble], flip: bool = True, bits=None):
+    """predict_pair_conditions' first half: the feature passes writing the bool features and
+    the union of the learners' numeric split outcomes as bitmaps (``sa_vaep_features_conditions``).
+    Returns ``(prep, bits, words)``."""
     from .batch import stream_handle
     if not all(m.f32 and not m.le for m in models):
         raise ValueError('condition bitmaps are for xgboost (float32, `<`) learners')
@@ -384,26 +401,32 @@ def predict_pair_conditions(batch, plan, models: Sequence[TreeEnsemble], flip: b
     prep = _conditions_prep(plan, models, dev)
     n, nb, n_num = batch.n, plan.n_bool, prep['n_num']
     words = max(2, -(-n // 128) * 2)  # int64 words per row: a whole number of 16-B runs
-    bits = torch.empty((max(nb + n_num, 1), words), dtype=torch.int64, device=dev)
+    if bits is None:
+        bits = torch.empty((max(nb + n_num, 1), words), dtype=torch.int64, device=dev)
     s = batch.struct(flip=flip)
     _native.check(_native.lib().sa_vaep_features_conditions(
         ctypes.byref(s), ctypes.byref(plan.struct), bits.data_ptr(), words * 8, nb, plan.n_f64,
         plan.n_i64, prep['fstart'].data_ptr(), prep['istart'].data_ptr(), prep['thr'].data_ptr(),
         prep['dl'].data_ptr(), n_num, stream_handle()))
+    return prep, bits, words
+
+
+def walk_conditions(prep: dict, k: int, model: 'TreeEnsemble', bits: torch.Tensor, words: int,
+                    n: int, dev, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Learner k's staged walk over the condition bitmaps ``bits`` (predict_pair_conditions'
+    second half): it stages only its own conditions' bitmap rows."""
+    from .batch import stream_handle
     z = _native.SaBlock()
     z.data, z.n_cols, z.tile_rows = None, 0, 16
-    bc = prep['bool_cols']
-    outs = []
-    for m, (nodes, leaf, roots, depth) in zip(models, prep['walks']):
-        out = torch.empty(max(n, 1), dtype=torch.float32, device=dev)
-        rec = _native.SaTreeModel(nodes.data_ptr(), leaf.data_ptr(), roots.data_ptr(), depth.data_ptr(),
-                                  nodes.numel(), m.n_trees, float(m.base_margin), out.data_ptr())
-        _native.check(_native.lib().sa_tree_predict_staged(
-            ctypes.byref(rec), bc.data_ptr() if bc is not None else None, prep['n_cond_bool'], None, None,
-            0, None, None, 0, ctypes.byref(z), bits.data_ptr(), words * 8, ctypes.byref(z), ctypes.byref(z),
-            n, 0, 1, stream_handle()))
-        outs.append(out[:n])
-    return outs
+    nodes, leaf, roots, depth, rows, n_rows = prep['walks'][k]
+    out = torch.empty(max(n, 1), dtype=torch.float32, device=dev) if out is None else out
+    rec = _native.SaTreeModel(nodes.data_ptr(), leaf.data_ptr(), roots.data_ptr(), depth.data_ptr(),
+                              nodes.numel(), model.n_trees, float(model.base_margin), out.data_ptr())
+    _native.check(_native.lib().sa_tree_predict_staged(
+        ctypes.byref(rec), rows.data_ptr() if rows is not None else None, n_rows, None, None,
+        0, None, None, 0, ctypes.byref(z), bits.data_ptr(), words * 8, ctypes.byref(z), ctypes.byref(z),
+        n, 0, 1, stream_handle()))
+    return out[:n]
 
 
 def staged_layout(models: Sequence[TreeEnsemble], slots: Sequence[np.ndarray]) -> dict:

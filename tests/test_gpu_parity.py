@@ -718,3 +718,43 @@ def test_contiguous_bool_block_matches(sa):
     t = buf.tensor((256, 1024), torch.float32)
     t.fill_(2.0)
     assert float(t.sum()) == 2.0 * 256 * 1024
+
+
+def test_chunked_step_equals_step(sa):
+    """sa_vaep_step_f64_chunked (the numeric step pass in launches of whole 512-row blocks, each
+    optionally after a pure-read pass over its inputs; bench.py's --ab probe of the pass's read /
+    write turnaround) == sa_vaep_step_f64 byte for byte: f64 / i64 blocks, xT cell codes, labels
+    and formula, with a chunk that does not divide n."""
+    import copy
+    B, ops, syn = sa['batch'], sa['ops'], sa['synthetic']
+    ab = B.ActionBatch.from_columns(syn.spadl_games(700, seed=41))
+    n = ab.n
+    rng = np.random.default_rng(9)
+    ps = torch.from_numpy(rng.random(n)).to(ab.device)
+    pc = torch.from_numpy(rng.random(n)).to(ab.device)
+    plan = ops.build_plan(vo.SPADL_DEFAULT, 3, False)
+    num = copy.copy(plan)
+    num.struct = copy.deepcopy(plan.struct)
+    for x in range(len(num.struct.bool_col)):
+        num.struct.bool_col[x] = -1
+    outs = []
+    for chunk, pf in ((0, False), (131072, False), (131072, True), (512 * 997, True)):
+        blk = ops.alloc_feature_blocks(plan, n, ab.device, 1024, 128)
+        view = ops.FeatureBlocks(num, n, blk.Rb, blk.Rn, blk.bool_block, blk.f64_block, blk.i64_block)
+        blk.f64_block.fill_(float('nan'))
+        blk.i64_block.fill_(-7)
+        lab, val = ops.labels_formula(ab, ps, pc, nr_actions=10)
+        for t in (lab.scores, lab.concedes, lab.goal_from_shot):
+            t.fill_(7)
+        val.fill_(float('nan'))
+        cells = ops.xt_cells_buffer(n, ab.device)
+        ops.step_into(ab.struct(), view, ps, pc, 10, lab, val, xt_cells=(16, 12, cells), chunk_rows=chunk,
+                      prefetch=pf)
+        outs.append((blk.f64_block.clone(), blk.i64_block.clone(), cells[:n].clone(),
+                     [getattr(lab, c)[:n].clone() for c in ('scores', 'concedes', 'goal_from_shot')],
+                     val[:, :n].clone()))
+    f0, i0, c0, l0, v0 = outs[0]
+    for f, i, c, l, v in outs[1:]:
+        assert torch.equal(f.view(torch.int64), f0.view(torch.int64)) and torch.equal(i, i0)
+        assert torch.equal(c, c0) and torch.equal(v.view(torch.int64), v0.view(torch.int64))
+        assert all(torch.equal(a, b) for a, b in zip(l, l0))
