@@ -528,11 +528,11 @@ def xt105_extra(ab, dist, dev, sharded: bool = False, cfg5_games: int = 62500,
             path[0] = sol.path
         mark()
         # rate(use_interpolation=True): each action's two node values evaluated in place from
-        # the 105 x 68 surface staged in LDS (sa_xt_rate_interp_codes), bit-identical to the
-        # 1050 x 680 grid gather
+        # the 105 x 68 surface staged in LDS (sa_xt_rate_interp_codes_many: every batch in one
+        # launch), bit-identical to the 1050 x 680 grid gather
         xT = mats[3].reshape(w, l)
-        rates = [ops.xt_rate_interp_codes(c, b.n, xT, l, w, 1050, 680, axes=axes, out=o)[0]
-                 for b, c, o in zip(batches, icodes, rate_out)]
+        rates, _ = ops.xt_rate_interp_codes_many(icodes, [b.n for b in batches], xT, l, w, 1050,
+                                                 680, axes=axes, outs=rate_out)
         mark()
         return n_iter, acc, mats, rates
     path = ['sequential']  # the value iteration's summation path of the last call

@@ -330,6 +330,14 @@ int sa_xt_rate_interp_codes(const uint64_t* interp_codes, int64_t n, const doubl
                             const double* cx, const double* cy, int32_t l, int32_t w,
                             const double* xs, int32_t L, const double* ys, int32_t W, double* out,
                             int32_t* err_flags, void* stream);
+/* sa_xt_rate_interp_codes of nsets action sets (a fit's device batches) in one launch per 16
+ * sets, the surface staged once: set q's interp_codes[q] / n[q] / out[q] as above, one err_flags
+ * for all.  (The batched form of the rate loop over batches in ExpectedThreat.rate's callers.) */
+int sa_xt_rate_interp_codes_many(int32_t nsets, const uint64_t* const* interp_codes,
+                                 const int64_t* n, const double* xT, const double* cx,
+                                 const double* cy, int32_t l, int32_t w, const double* xs,
+                                 int32_t L, const double* ys, int32_t W, double* const* out,
+                                 int32_t* err_flags, void* stream);
 int sa_xt_count_from_buckets(int32_t nsets, const uint32_t* const* buckets,
                              const int64_t* const* band_off, int32_t l, int32_t w, int64_t* shot,
                              int64_t* goal, int64_t* move, int32_t* trans, int32_t flags,

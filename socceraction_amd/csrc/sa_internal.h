@@ -46,8 +46,9 @@ int xt_compact_iterate(const uint32_t* ell, const int32_t* row_len, const int32_
                        double* xo, const int32_t* flag_prev, int32_t* flag_out, hipStream_t st);
 // The whole value iteration over the compact form of every row (sa_xt_solve_compact):
 // reordered sums under an error bound, or the reference's order (SA_XT_SOLVE_EXACT, or when the
-// bound cannot decide); *path = SA_XT_PATH_*.  Synchronises the stream.
+// bound cannot decide); *path = SA_XT_PATH_*.  xt_out (optional): the reordered path also
+// writes the final iterate there (the surface).  Synchronises the stream.
 int xt_compact_solve(const uint32_t* ell, const int32_t* row_len, const int32_t* cnt_rows, const int64_t* move,
                      const double* gs, const double* pmove, int C, double eps, int max_iter, int flags,
-                     double* heat, int* n_iter, int* path, hipStream_t st);
+                     double* heat, int* n_iter, int* path, hipStream_t st, double* xt_out = nullptr);
 }  // namespace sa

@@ -834,12 +834,20 @@ __global__ __launch_bounds__(XRI_THREADS) void xt_rate_interp_lds_kernel(sa_acti
 // node_value operations -- bit-identical values, NaN pattern and error bit 4 -- reading 8 B per
 // action instead of the 34 B of coordinates and ids.  A thread rates 2 consecutive actions per
 // pass (one 16-B code load, one 16-B store), U pairs per pass, every load before the stores.
-__global__ __launch_bounds__(XRI_THREADS) void xt_rate_icodes_lds_kernel(const uint64_t* __restrict__ icodes,
-                                                                        int64_t n, const double* __restrict__ xT,
+// The sets (a fit's device batches, XRI_MAX_SETS per launch) are rated one after the other by
+// the whole grid, the surface staged once: one launch per fit instead of one per batch.
+constexpr int XRI_MAX_SETS = 16;
+struct XriSets {
+  int n;
+  const uint64_t* codes[XRI_MAX_SETS];
+  double* out[XRI_MAX_SETS];
+  int64_t cnt[XRI_MAX_SETS];
+};
+
+__global__ __launch_bounds__(XRI_THREADS) void xt_rate_icodes_lds_kernel(XriSets sets, const double* __restrict__ xT,
                                                                         int l, int w, int L, int W,
                                                                         const int32_t* __restrict__ idx,
                                                                         const double* __restrict__ frac,
-                                                                        double* __restrict__ out,
                                                                         int32_t* __restrict__ err) {
   extern __shared__ __attribute__((aligned(16))) double xri_lds[];
   double* sxT = xri_lds;                                        // [w * l]
@@ -851,7 +859,7 @@ __global__ __launch_bounds__(XRI_THREADS) void xt_rate_icodes_lds_kernel(const u
     sidx[k] = idx[k];
   }
   __syncthreads();
-  const int64_t pairs = (n + 1) / 2, stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   int32_t bad = 0;
   auto one = [&](uint64_t c) -> double {
     if (c == XT_ICODE_NAN) return __builtin_nan("");
@@ -864,19 +872,25 @@ __global__ __launch_bounds__(XRI_THREADS) void xt_rate_icodes_lds_kernel(const u
     return node_value(sxT, l, L, e, sidx, sfrac) - node_value(sxT, l, L, s, sidx, sfrac);
   };
   constexpr int U = SA_XRI_U;
-  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < pairs; p += U * stride) {
-    if (2 * (p + (U - 1) * stride) + 1 < n) {
-      u64x2 c[U];
+  for (int q = 0; q < sets.n; ++q) {
+    const uint64_t* __restrict__ icodes = sets.codes[q];
+    double* __restrict__ out = sets.out[q];
+    const int64_t n = sets.cnt[q], pairs = (n + 1) / 2;
+    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < pairs; p += U * stride) {
+      if (2 * (p + (U - 1) * stride) + 1 < n) {
+        u64x2 c[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) c[u] = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(icodes + 2 * (p + u * stride)));
+        for (int u = 0; u < U; ++u)
+          c[u] = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(icodes + 2 * (p + u * stride)));
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const f64x2 v = {one(c[u][0]), one(c[u][1])};
-        __builtin_nontemporal_store(v, reinterpret_cast<f64x2*>(out + 2 * (p + u * stride)));
+        for (int u = 0; u < U; ++u) {
+          const f64x2 v = {one(c[u][0]), one(c[u][1])};
+          __builtin_nontemporal_store(v, reinterpret_cast<f64x2*>(out + 2 * (p + u * stride)));
+        }
+      } else {
+        for (int u = 0; u < U && p + u * stride < pairs; ++u)
+          for (int64_t j = 2 * (p + u * stride); j < 2 * (p + u * stride) + 2 && j < n; ++j) out[j] = one(icodes[j]);
       }
-    } else {
-      for (int u = 0; u < U && p + u * stride < pairs; ++u)
-        for (int64_t j = 2 * (p + u * stride); j < 2 * (p + u * stride) + 2 && j < n; ++j) out[j] = one(icodes[j]);
     }
   }
   if (bad && err) atomicOr(err, bad);
@@ -1131,10 +1145,11 @@ extern "C" int sa_xt_solve_ex(const int64_t* shot, const int64_t* goal, const in
                             "copy n_iter");
     if (!rc) rc = check_hip(hipStreamSynchronize(st), "hipStreamSynchronize");
   } else if (!rc) {
-    rc = check_hip(hipMemsetAsync(dflags, 0, sizeof(int32_t) * (max_iter + 1), st), "memset");
-    if (!rc) rc = check_hip(hipMemsetAsync(heatmaps, 0, sizeof(double) * C, st), "memset");
     // the compact form of the count rows, built once (sa_xt_large.hip): [ell | row_len]
     const bool compact = SA_XT_COMPACT && xt_compact_ok(C);
+    rc = check_hip(hipMemsetAsync(heatmaps, 0, sizeof(double) * C, st), "memset");
+    if (!rc && !compact)  // the dense loop's flags (the compact solve keeps its own)
+      rc = check_hip(hipMemsetAsync(dflags, 0, sizeof(int32_t) * (max_iter + 1), st), "memset");
     Scratch ce;
     uint32_t* ell = nullptr;
     int32_t* slen = nullptr;
@@ -1147,10 +1162,13 @@ extern "C" int sa_xt_solve_ex(const int64_t* shot, const int64_t* goal, const in
         rc = xt_compact_build(trans, C, C, ell, slen, st);
       }
     }
+    bool surface_done = false;  // the reordered solve wrote the surface itself
     if (compact && !rc) {  // reordered under the error bound, or the reference's order
       int p = SA_XT_PATH_SEQUENTIAL;
-      rc = xt_compact_solve(ell, slen, trans, move, gs, pm, C, eps, max_iter, flags, heatmaps, &iters, &p, st);
+      rc = xt_compact_solve(ell, slen, trans, move, gs, pm, C, eps, max_iter, flags, heatmaps, &iters, &p, st,
+                            mats + 3 * C);
       if (path) *path = p;
+      surface_done = p == SA_XT_PATH_REORDERED;
     }
     std::vector<int32_t> hflags(max_iter + 1, 0);
     const int batch = 8;
@@ -1173,7 +1191,7 @@ extern "C" int sa_xt_solve_ex(const int64_t* shot, const int64_t* goal, const in
           break;
         }
     }
-    if (!rc) {
+    if (!rc && !surface_done) {
       const int last = iters < 0 ? max_iter : iters;
       rc = check_hip(hipMemcpyAsync(mats + 3 * C, heatmaps + (int64_t)last * C, sizeof(double) * C,
                                     hipMemcpyDeviceToDevice, st),
@@ -1274,19 +1292,27 @@ extern "C" int sa_xt_rate_interp(const sa_actions* a, const double* xT, const do
   return rc;
 }
 
-extern "C" int sa_xt_rate_interp_codes(const uint64_t* interp_codes, int64_t n, const double* xT, const double* cx,
-                                       const double* cy, int32_t l, int32_t w, const double* xs, int32_t L,
-                                       const double* ys, int32_t W, double* out, int32_t* err_flags, void* stream) {
-  if (n < 0 || !xT || !cx || !cy || !xs || !ys || L < 1 || W < 1 || (n > 0 && (!interp_codes || !out)))
+extern "C" int sa_xt_rate_interp_codes_many(int32_t nsets, const uint64_t* const* interp_codes, const int64_t* n,
+                                            const double* xT, const double* cx, const double* cy, int32_t l, int32_t w,
+                                            const double* xs, int32_t L, const double* ys, int32_t W,
+                                            double* const* out, int32_t* err_flags, void* stream) {
+  if (nsets < 0 || (nsets > 0 && (!interp_codes || !n || !out)) || !xT || !cx || !cy || !xs || !ys || L < 1 || W < 1)
     return fail(SA_EINVAL, "bad xt_rate_interp_codes args");
   if (l < 2 || w < 2) return fail(SA_EINVAL, "interpolation needs at least 2 cells per axis");
   if ((int64_t)L * W > INT32_MAX) return fail(SA_EINVAL, "interpolated grid too large");
-  if (n > 0 && (!aligned16(interp_codes) || !aligned16(out))) return fail(SA_EINVAL, "codes and out must be 16-byte aligned");
+  int64_t most_n = 0;
+  for (int q = 0; q < nsets; ++q) {
+    if (n[q] < 0) return fail(SA_EINVAL, "set %d: negative action count", q);
+    if (n[q] > 0 && (!interp_codes[q] || !out[q])) return fail(SA_EINVAL, "set %d: null codes or out", q);
+    if (n[q] > 0 && (!aligned16(interp_codes[q]) || !aligned16(out[q])))
+      return fail(SA_EINVAL, "codes and out must be 16-byte aligned");
+    most_n = n[q] > most_n ? n[q] : most_n;
+  }
   const size_t lds = sizeof(double) * ((size_t)l * w + L + W) + sizeof(int32_t) * (size_t)(L + W);
   const int dev = current_device();
   if (lds > XRI_LDS_MAX || lds > (size_t)device_lds_max(dev))
     return fail(SA_EINVAL, "surface and node tables exceed the LDS");
-  if (n == 0) return SA_OK;
+  if (most_n == 0) return SA_OK;
   hipStream_t st = (hipStream_t)stream;
   Scratch sc;  // frac[L + W] | idx[L + W]
   int rc = scratch_acquire((sizeof(double) + sizeof(int32_t)) * (size_t)(L + W), st, &sc);
@@ -1295,14 +1321,32 @@ extern "C" int sa_xt_rate_interp_codes(const uint64_t* interp_codes, int64_t n, 
   int32_t* idx = reinterpret_cast<int32_t*>(frac + (L + W));
   hipLaunchKernelGGL(xt_axes_kernel, dim3((unsigned)((L + W + 255) / 256)), dim3(256), 0, st, cx, cy, l, w, xs, L,
                      ys, W, idx, frac);
-  const int64_t threads = (n + 1) / 2;
+  const int64_t threads = (most_n + 1) / 2;
   const int64_t need = (threads + XRI_THREADS - 1) / XRI_THREADS;
   const int64_t most = (int64_t)device_cus(dev) * SA_XRI_BPC;
-  hipLaunchKernelGGL(xt_rate_icodes_lds_kernel, dim3((unsigned)(need < most ? need : most)), dim3(XRI_THREADS), lds,
-                     st, interp_codes, n, xT, l, w, L, W, idx, frac, out, err_flags);
-  rc = check_launch("xt_rate_icodes_lds_kernel");
+  for (int q0 = 0; q0 < nsets && !rc; q0 += XRI_MAX_SETS) {
+    XriSets S{};
+    for (int q = q0; q < nsets && q < q0 + XRI_MAX_SETS; ++q) {
+      if (n[q] == 0) continue;
+      S.codes[S.n] = interp_codes[q];
+      S.out[S.n] = out[q];
+      S.cnt[S.n] = n[q];
+      ++S.n;
+    }
+    if (!S.n) continue;
+    hipLaunchKernelGGL(xt_rate_icodes_lds_kernel, dim3((unsigned)(need < most ? need : most)), dim3(XRI_THREADS),
+                       lds, st, S, xT, l, w, L, W, idx, frac, err_flags);
+    rc = check_launch("xt_rate_icodes_lds_kernel");
+  }
   scratch_release(sc, st);
   return rc;
+}
+
+extern "C" int sa_xt_rate_interp_codes(const uint64_t* interp_codes, int64_t n, const double* xT, const double* cx,
+                                       const double* cy, int32_t l, int32_t w, const double* xs, int32_t L,
+                                       const double* ys, int32_t W, double* out, int32_t* err_flags, void* stream) {
+  if (n < 0 || (n > 0 && (!interp_codes || !out))) return fail(SA_EINVAL, "bad xt_rate_interp_codes args");
+  return sa_xt_rate_interp_codes_many(1, &interp_codes, &n, xT, cx, cy, l, w, xs, L, ys, W, &out, err_flags, stream);
 }
 
 extern "C" int sa_xt_probabilities(const int64_t* shot, const int64_t* goal, const int64_t* move, int32_t C,

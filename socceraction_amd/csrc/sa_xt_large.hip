@@ -1148,7 +1148,7 @@ __device__ __forceinline__ double xf_group(const u32x4 (&e)[XF_G], const double*
 __global__ __launch_bounds__(XF_THREADS) void xt_solve_reordered_kernel(
     const uint32_t* __restrict__ ell, const int32_t* __restrict__ row_len, const unsigned long long* __restrict__ move,
     const double* __restrict__ gs, const double* __restrict__ pmove, int C, int hp, double eps, int max_iter,
-    int pmax, int kov, double* xb, double* __restrict__ heat, int32_t* ctrl) {
+    int pmax, int kov, double* xb, double* __restrict__ heat, double* __restrict__ xt_out, int32_t* ctrl) {
   // LDS: ov [XF_HALVES][kov] units | xs [C] x_t | part [pmax] unit sums | luo [pmax + 1]
   extern __shared__ __attribute__((aligned(16))) u32x4 xf_lds[];
   u32x4* ov = xf_lds;
@@ -1328,6 +1328,7 @@ __global__ __launch_bounds__(XF_THREADS) void xt_solve_reordered_kernel(
         __hip_atomic_store(dst + r, (unsigned long long)__double_as_longlong(xn), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
         heat[(int64_t)(it + 1) * C + r] = xn;
+        if (xt_out) xt_out[r] = xn;  // the surface: the last iterate when the loop ends
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its stores
@@ -1414,17 +1415,21 @@ static bool xt_band_shape(int C, XbShape* s) {
 static int bucket_batch(const sa_actions& A, const uint32_t* cells, int64_t n, int l, int w, const XbShape& S,
                         uint32_t* buckets, int64_t* band_off, int32_t* err, const XkRate& RO, hipStream_t st) {
   const int64_t regions = (n + XK_CHUNK - 1) / XK_CHUNK;
-  // scratch: keys [regions * XK_CHUNK] | region_cnt [regions] | band_cnt [NB] | cursor [NB]
-  const size_t kb = (size_t)regions * XK_CHUNK * 4;
-  const size_t bytes = kb + ((size_t)regions + 2 * (size_t)S.NB) * 4 + 256;
+  // scratch: band_cnt [NB] | cursor [NB] | region_cnt [regions] | keys [regions * XK_CHUNK], each
+  // part on 256-B boundaries: the band counts' memset is ONE aligned fill (an unaligned start
+  // split it into three fill kernels, ~9 us more per batch)
+  auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  const size_t nbb = al((size_t)S.NB * 4), rcb = al((size_t)regions * 4);
+  const size_t bytes = 2 * nbb + rcb + (size_t)regions * XK_CHUNK * 4;
   Scratch sc;
   int rc = scratch_acquire(bytes, st, &sc);
   if (rc) return rc;
-  uint32_t* keys = static_cast<uint32_t*>(sc.ptr);
-  uint32_t* region_cnt = keys + (size_t)regions * XK_CHUNK;
-  uint32_t* band_cnt = region_cnt + regions;
-  uint32_t* cursor = band_cnt + S.NB;
-  rc = check_hip(hipMemsetAsync(band_cnt, 0, (size_t)S.NB * 4, st), "memset band counts");
+  char* base = static_cast<char*>(sc.ptr);
+  uint32_t* band_cnt = reinterpret_cast<uint32_t*>(base);
+  uint32_t* cursor = reinterpret_cast<uint32_t*>(base + nbb);
+  uint32_t* region_cnt = reinterpret_cast<uint32_t*>(base + 2 * nbb);
+  uint32_t* keys = reinterpret_cast<uint32_t*>(base + 2 * nbb + rcb);
+  rc = check_hip(hipMemsetAsync(band_cnt, 0, nbb, st), "memset band counts");
   if (!rc) {
     sa_actions none;
     memset(&none, 0, sizeof(none));
@@ -1526,9 +1531,20 @@ int xt_compact_iterate(const uint32_t* ell, const int32_t* row_len, const int32_
 // (*n_iter the reference's count, -1: max_iter reached), 1 = a decision fell inside the error
 // bound, 2 = not launched (grid, LDS, residency or scratch size), 3 = a barrier timed out.
 // heat: [(max_iter + 1) * C] f64, rows 1.. written.  Synchronises the stream.
+// A small pinned host buffer for the solve's control words (a pageable destination made the
+// copy a staged, synchronous one: ~70 us of the call at cfg5).
+static int32_t* pinned_ctrl() {
+  static thread_local int32_t* p = nullptr;
+  if (!p && hipHostMalloc(reinterpret_cast<void**>(&p), 64, hipHostMallocDefault) != hipSuccess) {
+    (void)hipGetLastError();
+    p = nullptr;
+  }
+  return p;
+}
+
 static int xt_solve_reordered(const uint32_t* ell, const int32_t* row_len, const int32_t* cnt_rows,
                               const int64_t* move, const double* gs, const double* pmove, int C, double eps,
-                              int max_iter, double* heat, int* n_iter, int* status, hipStream_t st) {
+                              int max_iter, double* heat, double* xt_out, int* n_iter, int* status, hipStream_t st) {
   *status = 2;
   *n_iter = -1;
   if (!xt_compact_ok(C) || max_iter < 1) return SA_OK;
@@ -1559,15 +1575,17 @@ static int xt_solve_reordered(const uint32_t* ell, const int32_t* row_len, const
   if (rc) return rc;
   int32_t* ctrl = static_cast<int32_t*>(sc.ptr);
   double* xb = reinterpret_cast<double*>(static_cast<char*>(sc.ptr) + cbytes);
-  int32_t h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  int32_t hl[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  int32_t* pin = pinned_ctrl();
+  int32_t* h = pin ? pin : hl;
   rc = check_hip(hipMemsetAsync(ctrl, 0, cbytes, st), "memset solve control");
   if (!rc) {
     hipLaunchKernelGGL(xt_solve_reordered_kernel, dim3((unsigned)G), dim3(XF_THREADS), lds, st, ell, row_len,
                        reinterpret_cast<const unsigned long long*>(move), gs, pmove, C, hp, eps, max_iter, pmax, kov,
-                       xb, heat, ctrl);
+                       xb, heat, xt_out, ctrl);
     rc = check_launch("xt_solve_reordered_kernel");
   }
-  if (!rc) rc = check_hip(hipMemcpyAsync(h, ctrl, sizeof(h), hipMemcpyDeviceToHost, st), "copy solve control");
+  if (!rc) rc = check_hip(hipMemcpyAsync(h, ctrl, 8 * sizeof(int32_t), hipMemcpyDeviceToHost, st), "copy solve control");
   if (!rc) rc = check_hip(hipStreamSynchronize(st), "hipStreamSynchronize");
 #if SA_XF_PROBE
   int32_t pro[4] = {0, 0, 0, 0};
@@ -1596,12 +1614,13 @@ static int xt_solve_reordered(const uint32_t* ell, const int32_t* row_len, const
 // cannot decide.  *path: SA_XT_PATH_*.  Synchronises the stream.
 int xt_compact_solve(const uint32_t* ell, const int32_t* row_len, const int32_t* cnt_rows, const int64_t* move,
                      const double* gs, const double* pmove, int C, double eps, int max_iter, int flags,
-                     double* heat, int* n_iter, int* path, hipStream_t st) {
+                     double* heat, int* n_iter, int* path, hipStream_t st, double* xt_out) {
   *n_iter = -1;
   *path = SA_XT_PATH_SEQUENTIAL;
   if (!(flags & SA_XT_SOLVE_EXACT)) {
     int status = 2, it = -1;
-    int rc = xt_solve_reordered(ell, row_len, cnt_rows, move, gs, pmove, C, eps, max_iter, heat, &it, &status, st);
+    int rc = xt_solve_reordered(ell, row_len, cnt_rows, move, gs, pmove, C, eps, max_iter, heat, xt_out, &it,
+                                &status, st);
     if (rc) return rc;
     if (status == 0) {
       *n_iter = it;

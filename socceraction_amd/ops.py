@@ -9,7 +9,7 @@ from __future__ import annotations
 
 import ctypes
 from dataclasses import dataclass
-from typing import Optional, Sequence, Tuple
+from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -396,19 +396,24 @@ class XTCounts:
         return self
 
 
-def xt_zero_counts(l: int, w: int, dev, row_blocks: int = 1) -> XTCounts:
+def xt_zero_counts(l: int, w: int, dev, row_blocks: int = 1, zero_counts: bool = True) -> XTCounts:
     """Zeroed count buffers, carved from ONE allocation (one fill kernel, one all-reduce):
     ``[shot | goal | move]`` (3 x C int64), the error flags (int32), then the C x C transition
     counts (int32). ``row_blocks`` > 1 pads the transition counts to a whole number of equal row
     blocks (``XTCounts.trans_padded``) so they can be reduce-scattered by rows across that many
     ranks; ``trans`` is the C*C view the count kernel fills. ``XTCounts.head`` is the vectors +
-    flags part, ``XTCounts.buf`` the whole allocation."""
+    flags part, ``XTCounts.buf`` the whole allocation. ``zero_counts=False``: only the error
+    flags are zeroed (for a count that overwrites every row, ``row_blocks`` 1)."""
     C = l * w
     rows = -(-C // row_blocks) * row_blocks
     a = lambda b: -(-b // 256) * 256  # noqa: E731  (256-B aligned parts)
     o_err = a(3 * C * 8)
     o_tr = o_err + 256
-    buf = torch.zeros(o_tr + a(rows * C * 4), dtype=torch.uint8, device=dev)
+    if zero_counts or row_blocks != 1:
+        buf = torch.zeros(o_tr + a(rows * C * 4), dtype=torch.uint8, device=dev)
+    else:
+        buf = torch.empty(o_tr + a(rows * C * 4), dtype=torch.uint8, device=dev)
+        buf[o_err:o_tr].zero_()
     vec = buf[:3 * C * 8].view(torch.int64).view(3, C)
     padded = buf[o_tr:o_tr + rows * C * 4].view(torch.int32)
     acc = XTCounts(l, w, vec[0], vec[1], vec[2], padded[:C * C], buf[o_err:o_err + 4].view(torch.int32))
@@ -515,6 +520,40 @@ def xt_rate_interp_codes(icodes: torch.Tensor, n: int, xT: torch.Tensor, l: int,
     return out[:n], err
 
 
+def xt_rate_interp_codes_many(icodes: Sequence[torch.Tensor], ns: Sequence[int], xT: torch.Tensor,
+                              l: int, w: int, L: int = 1050, W: int = 680,
+                              axes: Optional[torch.Tensor] = None,
+                              outs: Optional[Sequence[torch.Tensor]] = None
+                              ) -> Tuple[List[torch.Tensor], torch.Tensor]:
+    """:func:`xt_rate_interp_codes` of several batches (a fit's device batches) in one launch
+    (``sa_xt_rate_interp_codes_many``): the same values per batch, one error word for all."""
+    if len(icodes) != len(ns) or (outs is not None and len(outs) != len(ns)):
+        raise ValueError('one operand buffer, count (and out) per batch')
+    dev = xT.device
+    axes = xt_interp_axes(l, w, dev, L, W) if axes is None else axes
+    if axes.numel() != l + w + L + W:
+        raise ValueError('axes must hold l + w + L + W node positions')
+    ns = [int(n) for n in ns]
+    for c, n in zip(icodes, ns):
+        if n < 0 or c.numel() * c.element_size() < 8 * n:
+            raise ValueError('an operand buffer holds fewer than n codes')
+    outs = [torch.empty(max(_ld(n), 16), dtype=torch.float64, device=dev) for n in ns] \
+        if outs is None else list(outs)
+    for o, n in zip(outs, ns):
+        if o.dtype != torch.float64 or o.numel() < n:
+            raise ValueError('out must be float64 with room for n values')
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    k = len(ns)
+    cp = (ctypes.c_void_p * max(k, 1))(*[c.data_ptr() for c in icodes])
+    op = (ctypes.c_void_p * max(k, 1))(*[o.data_ptr() for o in outs])
+    nn = (ctypes.c_int64 * max(k, 1))(*ns)
+    o = l + w
+    _native.check(_native.lib().sa_xt_rate_interp_codes_many(
+        k, cp, nn, _ptr(xT.contiguous()), _ptr(axes[:l]), _ptr(axes[l:o]), l, w,
+        _ptr(axes[o:o + L]), L, _ptr(axes[o + L:]), W, op, _ptr(err), stream_handle()))
+    return [t[:n] for t, n in zip(outs, ns)], err
+
+
 def xt_count_buckets(parts: Sequence[XTBuckets], l: int, w: int, acc: XTCounts,
                      overwrite: bool = False) -> XTCounts:
     """The once-per-fit half of the band-owned count: every batch's buckets into ``acc`` (added;
@@ -548,7 +587,9 @@ def xt_count_many(batches: Sequence[ActionBatch], l: int, w: int,
         return acc if acc is not None else xt_zero_counts(l, w, torch.device('cuda'))
     if overwrite is None:
         overwrite = acc is None
-    acc = acc or xt_zero_counts(l, w, batches[0].device)
+    # a fresh accumulator the overwriting count fills whole: only its error word zeroed (the
+    # 204 MB fill of the 105 x 68 table was 27 us of cfg5's fit)
+    acc = acc or xt_zero_counts(l, w, batches[0].device, zero_counts=not overwrite)
     ic = list(interp_codes) if interp_codes is not None else [None] * len(batches)
     parts = [xt_bucket(b, l, w, acc.err, interp_codes=c) for b, c in zip(batches, ic)]
     return xt_count_buckets(parts, l, w, acc, overwrite=overwrite)

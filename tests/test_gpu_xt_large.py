@@ -316,6 +316,59 @@ def test_interp_codes_rate_equals_rate_interp(sa):
         assert bool(acc.err.item()) == bad
 
 
+def test_interp_codes_rate_many_equals_per_batch(sa):
+    """sa_xt_rate_interp_codes_many over 19 batches (two launches of <= 16 sets; odd, tiny and
+    empty batches) == sa_xt_rate_interp_codes of each batch, bit for bit, one error word."""
+    B, ops, syn = sa['batch'], sa['ops'], sa['synthetic']
+    rng = np.random.default_rng(31)
+    ns, ic, bs = [], [], []
+    for k in range(19):
+        if k % 6 == 4:  # an empty set
+            ns.append(0)
+            ic.append(ops.xt_interp_codes_buffer(0, 'cuda'))
+            continue
+        d = syn.spadl_games([1, 3, 7, 40][k % 4], game_id0=100 * k)
+        N = len(d['type_id'])
+        n = [1, 333, N, N - 1][k % 4] if N > 333 else N
+        d = {c: (v[:n].copy() if isinstance(v, np.ndarray) and v.shape == (N,) else v)
+             for c, v in d.items()}
+        d['game_off'] = np.minimum(d['game_off'], n)
+        if k == 5 and n > 10:
+            d['start_x'][rng.choice(n, 60, replace=False)] = np.nan
+        bs.append(B.ActionBatch.from_columns(d))
+        ns.append(bs[-1].n)
+        ic.append(ops.xt_interp_codes_buffer(bs[-1].n, bs[-1].device))
+    ops.xt_count_many(bs, 105, 68, interp_codes=[c for c, n in zip(ic, ns) if n])
+    xT = torch.rand((68, 105), dtype=torch.float64, device='cuda')
+    got, err = ops.xt_rate_interp_codes_many(ic, ns, xT, 105, 68)
+    want_err = 0
+    for n, c, g in zip(ns, ic, got):
+        assert g.numel() == n
+        if n == 0:
+            continue
+        ref, e = ops.xt_rate_interp_codes(c, n, xT, 105, 68)
+        want_err |= int(e.item())
+        a, r = g.cpu().numpy(), ref.cpu().numpy()
+        np.testing.assert_array_equal(np.isnan(a), np.isnan(r))
+        np.testing.assert_array_equal(a[~np.isnan(r)], r[~np.isnan(r)])
+    assert want_err == 4 and int(err.item()) == want_err
+
+
+def test_fresh_accumulator_overwrite_ignores_stale_memory(sa):
+    """xt_count_many's fresh accumulator is not zero-filled (the count overwrites every row):
+    counts equal the oracle's even when the allocator hands back memory full of junk."""
+    B, ops, syn = sa['batch'], sa['ops'], sa['synthetic']
+    l, w = 105, 68
+    C = l * w
+    junk = torch.full((3 * C * 8 + 512 + C * C * 4 + 4096,), 0x5A, dtype=torch.uint8, device='cuda')
+    del junk  # back to the caching allocator, bytes intact
+    d = syn.spadl_games(25)
+    ab = B.ActionBatch.from_columns(d)
+    acc = ops.xt_count_many([ab], l, w)
+    ops.xt_check_errors(acc)
+    _same_counts(acc, _oracle(d, l, w), l, w)
+
+
 def test_coresident_16x12_count_full_batch_vs_oracle(sa):
     """The co-resident count (shared=True: the workgroup shape the bench step's side stream
     uses next to the VAEP passes) over cfg2's whole 10k-game batch (~16M actions) == the
