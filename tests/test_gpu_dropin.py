@@ -264,8 +264,9 @@ def test_xt_reference_known_answers():
 
 
 def test_xt_large_grid_multi_launch_solver():
-    """C = 30*20 = 600 takes the persistent path; C > 1024 the per-iteration launches.
-    Both agree with the oracle's exact summation order."""
+    """C = 40*30 = 1200 > 1024 cells: the large-grid solve.  exact_order=True sums in the
+    reference's order (bit-exact with the oracle); the default reordered sums keep the oracle's
+    iteration count and every heatmap within 1e-12 relative (the error-bound guard)."""
     from oracle import xt_oracle as xo
     from socceraction_amd import synthetic
     from socceraction_amd import xthreat as xt
@@ -273,10 +274,15 @@ def test_xt_large_grid_multi_launch_solver():
     df = synthetic.to_frame(d)
     cols = {c: d[c] for c in ('start_x', 'start_y', 'end_x', 'end_y', 'type_id', 'result_id')}
     for l, w in ((40, 30),):
-        m = xt.ExpectedThreat(l=l, w=w).fit(df)
         f = xo.fit(cols, l, w)
+        m = xt.ExpectedThreat(l=l, w=w).fit(df, exact_order=True)
         assert len(m.heatmaps) == len(f['heatmaps'])
         np.testing.assert_array_equal(m.xT, f['xT'])
+        r = xt.ExpectedThreat(l=l, w=w).fit(df)
+        assert r.solve_path in ('reordered', 'sequential')
+        assert len(r.heatmaps) == len(f['heatmaps'])
+        for a, b in zip(r.heatmaps, f['heatmaps']):
+            np.testing.assert_allclose(a, b, rtol=1e-12, atol=1e-300)
 
 
 @pytest.mark.parametrize('grid,mode', [('105x68', 'bands'), ('105x68', 'bands-rows'), ('105x68', 'rows'),
