@@ -89,6 +89,13 @@ def main():
                                                  ctypes.byref(fb), ctypes.byref(ib), stream))
                 run()
                 torch.cuda.synchronize()
+                if tag == 'step':  # the step form's outputs, compared across the builds too
+                    got = [t.clone() for t in (out.f64_block, out.i64_block, lab, val, cells)]
+                    sref = res.setdefault('_sref', {})
+                    if 'v' not in sref:
+                        sref['v'] = got
+                    res['equal'][name + ':step'] = all(torch.equal(a, b) for a, b in zip(got, sref['v']))
+                    del got
                 if tag == 'all':
                     got = [t.clone() for t in (out.bool_block, out.f64_block, out.i64_block)]
                     if ref is None:
@@ -130,6 +137,7 @@ def main():
                 for part, (x, y) in (('pair_step', (0, 1)), ('pair_bool', (1, 2)), ('pair_total', (0, 2))):
                     res['ms'].setdefault(f'{name}:{part}', []).append(
                         round(sum(e[x].elapsed_time(e[y]) for e in ev) / args.reps, 4))
+    res.pop('_sref', None)
     print(json.dumps(res), flush=True)
 
 

@@ -1144,22 +1144,21 @@ template <bool ATOMIC, bool TAIL>
 constexpr int num_min_waves() {
   return SA_NUM_WAVES > 0 ? SA_NUM_WAVES : 1;
 }
+// The pass over the wave's 128 rows from wave_base.  F0: frames[0] with the streamed columns
+// (coordinates, time) where the caller wants them read from; ps / pc: the probabilities (TAIL).
 template <bool ATOMIC, bool EXPLICIT, int KF, bool TAIL = false, bool N32 = false, bool COND = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(num_min_waves<ATOMIC, TAIL>(), 8)))
-void num_features_kernel(FeatArgs args) {
+__device__ __forceinline__ void num_features_body(const FeatArgs& args, int64_t wave_base, const sa_frame& F0,
+                                                  const double* ps_in, const double* pc_in) {
   // N32: the f64 and i64 blocks hold float32 values (sa_vaep_features_bits_f32); COND: no blocks,
   // the columns' split conditions as bitmaps (sa_vaep_features_conditions)
   using FT = typename std::conditional<COND, CondSink, typename std::conditional<N32, float, double>::type>::type;
   using IT = typename std::conditional<COND, CondSink, typename std::conditional<N32, float, int64_t>::type>::type;
   const int lane = threadIdx.x & (WAVE - 1);
-  const int wv = threadIdx.x / WAVE;
   const sa_actions& A = args.a;
   const sa_feature_plan& P = args.p;
   const int64_t n = A.n;
   const int K = P.nb_prev_actions;
   const int64_t Rf = args.Rf, Ri = args.Ri;
-  const int64_t wave_base = args.row0 + (xcd_logical_block() * BLOCK_WAVES + wv) * WAVE_ACTS;
-  const sa_frame& F0 = A.frames[0];
   // whole wave past the end (uniform: the goalscore ballots need every lane)
   if (wave_base >= n || (args.row_end > 0 && wave_base >= args.row_end)) return;
   CondAcc acc{0, 0, 0, -64};
@@ -1233,7 +1232,7 @@ void num_features_kernel(FeatArgs args) {
       if (args.ps) {  // uniform: labels only when no probabilities are given
         SegCursor fc = cur;
         const double t_rows[2] = {cand[0].ts, cand[1].ts};  // rows jw, jw+1 (KF = 3)
-        fok = formula_vals<ATOMIC, double>(A, args.ps, args.pc, args.vec_ok, jw, fc, fo, fd, fv,
+        fok = formula_vals<ATOMIC, double>(A, ps_in, pc_in, args.vec_ok, jw, fc, fo, fd, fv,
                                            KF == 3 ? t_rows : nullptr);
       }
     }
@@ -1413,6 +1412,70 @@ void num_features_kernel(FeatArgs args) {
     if (acc.held) cond_flush(&sink_f);
   }
 }
+
+template <bool ATOMIC, bool EXPLICIT, int KF, bool TAIL = false, bool N32 = false, bool COND = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(num_min_waves<ATOMIC, TAIL>(), 8)))
+void num_features_kernel(FeatArgs args) {
+  const int wv = threadIdx.x / WAVE;
+  const int64_t wave_base = args.row0 + (xcd_logical_block() * BLOCK_WAVES + wv) * WAVE_ACTS;
+  num_features_body<ATOMIC, EXPLICIT, KF, TAIL, N32, COND>(args, wave_base, args.a.frames[0], args.ps, args.pc);
+}
+
+// SA_NUM_STAGE = T > 0 (probe builds): the SPADL step pass with each workgroup's streamed inputs
+// -- coordinates, time and the two probabilities of T x 512 rows (56 B per row) plus the two rows
+// before -- loaded into LDS in one burst before any of the T tiles' stores; the tiles then read
+// those columns from LDS.  The experiment on the read / write turnaround of the numeric pass
+// (profiles/r03_numeric_pass_ab.md): does separating a CU's reads from its stores in time help?
+#ifndef SA_NUM_STAGE
+#define SA_NUM_STAGE 0
+#endif
+#if SA_NUM_STAGE > 0
+constexpr int STG_T = SA_NUM_STAGE;
+constexpr int STG_ROWS = STG_T * BLOCK_ACTS + 2;
+constexpr int STG_NP = (STG_ROWS / 2 + 255) / 256;  // row pairs per thread per column
+__global__ __launch_bounds__(256) void num_staged_kernel(FeatArgs args) {
+  extern __shared__ __attribute__((aligned(16))) double stg[];  // [7][STG_ROWS]
+  const sa_frame& G = args.a.frames[0];
+  const int64_t n = args.a.n;
+  const int64_t row0 = xcd_logical_block() * (int64_t)(STG_T * BLOCK_ACTS);
+  if (row0 >= n) return;
+  const int64_t lo = row0 - 2;  // LDS row i = row lo + i
+  const int64_t hi = min(n, row0 + (int64_t)STG_T * BLOCK_ACTS);
+  const double* src[7] = {G.c0, G.c1, G.c2, G.c3, G.time_seconds, args.ps, args.pc};
+  const int ncol = args.ps ? 7 : 5;
+  for (int c = 0; c < ncol; ++c) {  // every load of the column before its LDS stores
+    f64x2 v[STG_NP];
+#pragma unroll
+    for (int q = 0; q < STG_NP; ++q) {
+      const int pr = q * 256 + threadIdx.x;
+      const int64_t r = lo + 2 * (int64_t)pr;
+      v[q] = f64x2{0.0, 0.0};
+      if (pr < STG_ROWS / 2 && r >= 0) {
+        if (r + 1 < hi) v[q] = ld_stream(reinterpret_cast<const f64x2*>(src[c] + r));
+        else if (r < hi) v[q][0] = src[c][r];
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < STG_NP; ++q) {
+      const int pr = q * 256 + threadIdx.x;
+      if (pr < STG_ROWS / 2) *reinterpret_cast<f64x2*>(stg + c * STG_ROWS + 2 * pr) = v[q];
+    }
+  }
+  __syncthreads();
+  sa_frame F = G;
+  F.c0 = stg - lo;
+  F.c1 = stg + STG_ROWS - lo;
+  F.c2 = stg + 2 * STG_ROWS - lo;
+  F.c3 = stg + 3 * STG_ROWS - lo;
+  F.time_seconds = stg + 4 * STG_ROWS - lo;
+  const double* ps = args.ps ? stg + 5 * STG_ROWS - lo : nullptr;
+  const double* pc = args.ps ? stg + 6 * STG_ROWS - lo : nullptr;
+  const int wv = threadIdx.x / WAVE;
+#pragma unroll 1
+  for (int t = 0; t < STG_T; ++t)
+    num_features_body<false, false, 3, true>(args, row0 + (int64_t)t * BLOCK_ACTS + wv * WAVE_ACTS, F, ps, pc);
+}
+#endif
 
 // ------------------------------------------------------------------------------ goalscore
 // features.py:505-539 / atomic/vaep/features.py:229-260: per segment, teamA = team of the
@@ -2187,6 +2250,12 @@ static int launch_features(const sa_actions* a, const sa_feature_plan* plan, con
         hipLaunchKernelGGL((num_features_kernel<false, false, 3, true>), cg, block, 0, st, args);
       }
     } else if (tail) {  // windowed, K <= 3 (checked by sa_vaep_step_f64)
+#if SA_NUM_STAGE > 0
+      if (!a->atomic && (!tail->ps || (aligned16(tail->ps) && aligned16(tail->pc)))) {
+        const dim3 sg(xcd_grid((a->n + STG_T * BLOCK_ACTS - 1) / (STG_T * BLOCK_ACTS)));
+        hipLaunchKernelGGL(num_staged_kernel, sg, block, sizeof(double) * 7 * STG_ROWS, st, args);
+      } else
+#endif
       if (a->atomic)
         hipLaunchKernelGGL((num_features_kernel<true, false, 3, true>), grid, block, 0, st, args);
       else
