@@ -730,23 +730,29 @@ def rate_extra(ab, out, n, dev, reps: int = 5) -> dict:
     ms_gather = _events_ms(lambda: models[0].predict_blocks(out, out=ps, method='gather'), reps)
     ms_formula = _events_ms(lambda: ops.formula(ab, ps, pc, val), reps)
     del fbits
-    return {'workload': 'VAEP.rate on device: features (bool features as bitmaps, numeric '
-                        'features in float32) + 2 x xgboost-shaped tree ensembles (100 trees, '
-                        'depth 3) + formula (float32 probabilities), cfg2 actions',
-            'method': 'staged condition walk (sa_tree_predict_staged) over the bitmaps and the '
-                      'float32 numeric blocks',
-            'ms_features_and_both_models_conditions': round(ms_cond, 4),
+    return {'workload': 'VAEP.rate on device: the feature passes + 2 x xgboost-shaped tree '
+                        'ensembles (100 trees, depth 3) + formula (float32 probabilities), cfg2 '
+                        'actions',
+            'method': 'VAEP.rate default (vaep/base.py): the split conditions evaluated inside the '
+                      'feature passes as bitmaps (sa_vaep_features_conditions), then one staged '
+                      'walk per learner over the condition bitmaps only',
             'ms_features_conditions': round(ms_cond_feat, 4),
-            'ms_per_model_conditions': [round(x, 4) for x in ms_cond_walk],
+            'ms_per_model': [round(x, 4) for x in ms_cond_walk],
             'conditions': cond_counts,
-            'ms_rate_total_conditions': round(ms_cond + ms_formula, 4),
-            'ms_features_bitmap_form': round(ms_feat, 4), 'ms_per_model': round(ms_tree, 4),
-            'ms_features_bitmap_f64_form': round(ms_feat64, 4),
-            'ms_per_model_f64_numeric': round(ms_tree64, 4),
-            'ms_per_model_from_bool_block': round(ms_block, 4),
-            'ms_per_model_gather_walk': round(ms_gather, 4), 'ms_formula_f32': round(ms_formula, 4),
-            'ms_rate_total': round(ms_feat + 2 * ms_tree + ms_formula, 4),
-            'actions_per_s_rate': round(n / (ms_feat + 2 * ms_tree + ms_formula) * 1e3, 1)}
+            'ms_features_and_both_models': round(ms_cond, 4),
+            'ms_formula_f32': round(ms_formula, 4),
+            'ms_rate_total': round(ms_cond + ms_formula, 4),
+            'actions_per_s_rate': round(n / (ms_cond + ms_formula) * 1e3, 1),
+            'staged_walk_over_feature_blocks': {
+                'what': 'the other tree path (sa_tree_predict_staged over the bool bitmaps and '
+                        'the numeric blocks: VAEP.rate for learners whose splits are not xgboost float32 `<` '
+                        'conditions, or whose conditions do not fit the condition bitmaps)',
+                'ms_features_bitmap_form': round(ms_feat, 4), 'ms_per_model': round(ms_tree, 4),
+                'ms_features_bitmap_f64_form': round(ms_feat64, 4),
+                'ms_per_model_f64_numeric': round(ms_tree64, 4),
+                'ms_per_model_from_bool_block': round(ms_block, 4),
+                'ms_per_model_gather_walk': round(ms_gather, 4),
+                'ms_rate_total': round(ms_feat + 2 * ms_tree + ms_formula, 4)}}
 
 
 def e2e_extra(d, games: int, reps: int = 2) -> dict:
