@@ -332,7 +332,8 @@ int sa_xt_rate_interp_codes(const uint64_t* interp_codes, int64_t n, const doubl
                             int32_t* err_flags, void* stream);
 /* sa_xt_rate_interp_codes of nsets action sets (a fit's device batches) in one launch per 16
  * sets, the surface staged once: set q's interp_codes[q] / n[q] / out[q] as above, one err_flags
- * for all.  (The batched form of the rate loop over batches in ExpectedThreat.rate's callers.) */
+ * for all.  (ExpectedThreat.rate(use_interpolation=True) xthreat.py:443-464 of a fit's
+ * batches.) */
 int sa_xt_rate_interp_codes_many(int32_t nsets, const uint64_t* const* interp_codes,
                                  const int64_t* n, const double* xT, const double* cx,
                                  const double* cy, int32_t l, int32_t w, const double* xs,
@@ -358,7 +359,8 @@ int sa_xt_count_from_buckets(int32_t nsets, const uint32_t* const* buckets,
 int sa_xt_solve(const int64_t* shot, const int64_t* goal, const int64_t* move,
                 const int32_t* trans, int32_t l, int32_t w, double eps, int32_t max_iter,
                 double* mats, double* trans_t, double* heatmaps, int32_t* n_iter, void* stream);
-/* sa_xt_solve with a choice of summation order for grids above SA_XT_SOLVE_MAX_C cells (smaller
+/* sa_xt_solve (ExpectedThreat.fit xthreat.py:322-345 + __solve :278-320) with a choice of
+ * summation order for grids above SA_XT_SOLVE_MAX_C cells (smaller
  * grids always sum in the reference's order, bit-exact).  Large grids by default solve in ONE
  * launch with each row's sum reordered into a fixed parallel tree (run-to-run reproducible)
  * under a rigorous error bound: every `diff > eps` decision, and so the iteration count, is the
@@ -422,7 +424,8 @@ int sa_xt_iterate_compact(const uint32_t* ell, const int32_t* row_len, const int
                           int32_t r0, int32_t nrows, const double* x, double eps,
                           double* x_next_rows, const int32_t* flag_prev, int32_t* flag_out,
                           void* stream);
-/* The whole value iteration of a grid from the compact form of ALL its C rows (as built by
+/* The whole value iteration (__solve xthreat.py:278-320) of a grid from the compact form of ALL
+ * its C rows (as built by
  * sa_xt_compact_rows; the multi-GPU fit gathers it from the ranks): heatmaps[(max_iter+1)*C]
  * = x after 0..n_iter iterations, *n_iter [host] the count (-1: max_iter reached first), the
  * summation order chosen by `flags` exactly as in sa_xt_solve_ex (*path may be NULL).
