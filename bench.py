@@ -851,7 +851,10 @@ def cpu_baseline(d, seconds: float) -> dict:
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=20)
+    # 50 timed steps by default: the last step's xT fit + rate (~0.5 ms on the side stream) is
+    # the one part of the pipeline no later step hides; over 20 steps it added ~10 us per step
+    # (profiles/r05w_steps_ab.log), over 50 about 4
+    ap.add_argument('--steps', type=int, default=50)
     ap.add_argument('--warmup', type=int, default=3)
     ap.add_argument('--games', type=int, default=10000, help='games per GPU (cfg2: 10k)')
     ap.add_argument('--cpu-seconds', type=float, default=15.0)
