@@ -343,6 +343,15 @@ int sa_xt_count_from_buckets(int32_t nsets, const uint32_t* const* buckets,
                              const int64_t* const* band_off, int32_t l, int32_t w, int64_t* shot,
                              int64_t* goal, int64_t* move, int32_t* trans, int32_t flags,
                              void* stream);
+/* sa_xt_count_from_buckets that also writes the count rows in the compact form of
+ * sa_xt_compact_rows (ell [C * sa_xt_compact_bytes(C, 1) / 4] u32, 16-byte aligned; row_len [C]),
+ * straight from the bins: the large-grid solve (sa_xt_solve_ex with ell / row_len) then skips
+ * its own build pass over the dense table.  Needs SA_XT_COUNT_OVERWRITE, at most 24 bucket sets
+ * and 1025 <= C <= 9472; ell = row_len = NULL is sa_xt_count_from_buckets. */
+int sa_xt_count_from_buckets_ex(int32_t nsets, const uint32_t* const* buckets,
+                                const int64_t* const* band_off, int32_t l, int32_t w,
+                                int64_t* shot, int64_t* goal, int64_t* move, int32_t* trans,
+                                int32_t flags, uint32_t* ell, int32_t* row_len, void* stream);
 
 /* Grids up to SA_XT_SOLVE_MAX_C cells solve in one workgroup from the transposed matrix. */
 #define SA_XT_SOLVE_MAX_C 1024
@@ -368,7 +377,9 @@ int sa_xt_solve(const int64_t* shot, const int64_t* goal, const int64_t* move,
  * 105 x 68); when some cell's diff falls inside the bound the system is re-solved in the
  * reference's order.  flags: SA_XT_SOLVE_EXACT = always the reference's order (bit-exact
  * iterates, one launch per iteration).  *path (may be NULL) receives which path produced the
- * result (SA_XT_PATH_*).  Same outputs and synchronisation as sa_xt_solve. */
+ * result (SA_XT_PATH_*).  ell / row_len (both or NULL; grids of 1025 - 9472 cells): the compact
+ * form of `trans` as sa_xt_count_from_buckets_ex or sa_xt_compact_rows wrote it, used instead of
+ * building it again.  Same outputs and synchronisation as sa_xt_solve. */
 #define SA_XT_SOLVE_EXACT 1
 #define SA_XT_PATH_SEQUENTIAL 0   /* the reference's order (small grid, or SA_XT_SOLVE_EXACT) */
 #define SA_XT_PATH_REORDERED 1    /* reordered sums, every decision outside the error bound */
@@ -377,7 +388,7 @@ int sa_xt_solve(const int64_t* shot, const int64_t* goal, const int64_t* move,
 int sa_xt_solve_ex(const int64_t* shot, const int64_t* goal, const int64_t* move,
                    const int32_t* trans, int32_t l, int32_t w, double eps, int32_t max_iter,
                    int32_t flags, double* mats, double* trans_t, double* heatmaps, int32_t* n_iter,
-                   int32_t* path, void* stream);
+                   int32_t* path, const uint32_t* ell, const int32_t* row_len, void* stream);
 /* sa_xt_solve for grids of <= SA_XT_SOLVE_MAX_C cells without the host round trip: the
  * iteration count (-1: max_iter reached first) is written to device memory *n_iter_dev and
  * nothing is synchronised, so a consumer of the surface (sa_xt_rate_cells) can be enqueued

@@ -1099,18 +1099,22 @@ extern "C" int sa_xt_solve(const int64_t* shot, const int64_t* goal, const int64
                            double* mats, double* trans_t, double* heatmaps, int32_t* n_iter,
                            void* stream) {
   return sa_xt_solve_ex(shot, goal, move, trans, l, w, eps, max_iter, 0, mats, trans_t, heatmaps, n_iter, nullptr,
-                        stream);
+                        nullptr, nullptr, stream);
 }
 
 extern "C" int sa_xt_solve_ex(const int64_t* shot, const int64_t* goal, const int64_t* move,
                               const int32_t* trans, int32_t l, int32_t w, double eps, int32_t max_iter,
                               int32_t flags, double* mats, double* trans_t, double* heatmaps, int32_t* n_iter,
-                              int32_t* path, void* stream) {
+                              int32_t* path, const uint32_t* ell_in, const int32_t* row_len_in, void* stream) {
   if (l < 1 || w < 1 || max_iter < 0) return fail(SA_EINVAL, "bad l, w or max_iter");
   const int C = l * w;
   if (!shot || !goal || !move || !trans || !mats || (!trans_t && C <= XT_SOLVE_MAX_C) || !heatmaps || !n_iter)
     return fail(SA_EINVAL, "null pointer");
   if (flags & ~SA_XT_SOLVE_EXACT) return fail(SA_EINVAL, "unknown flags");
+  if (!ell_in != !row_len_in) return fail(SA_EINVAL, "ell and row_len come together");
+  if (ell_in && (C <= XT_SOLVE_MAX_C || !SA_XT_COMPACT || !xt_compact_ok(C) || !aligned16(ell_in)))
+    return fail(SA_EINVAL, "a prebuilt compact form is for %d < C <= the compact limit (16-byte aligned)",
+                XT_SOLVE_MAX_C);
   if (path) *path = SA_XT_PATH_SEQUENTIAL;
   hipStream_t st = (hipStream_t)stream;
   auto* us = reinterpret_cast<const unsigned long long*>(shot);
@@ -1151,15 +1155,17 @@ extern "C" int sa_xt_solve_ex(const int64_t* shot, const int64_t* goal, const in
     if (!rc && !compact)  // the dense loop's flags (the compact solve keeps its own)
       rc = check_hip(hipMemsetAsync(dflags, 0, sizeof(int32_t) * (max_iter + 1), st), "memset");
     Scratch ce;
-    uint32_t* ell = nullptr;
-    int32_t* slen = nullptr;
-    if (!rc && compact) {
+    const uint32_t* ell = ell_in;  // prebuilt by the count (sa_xt_count_from_buckets_ex), or built here
+    const int32_t* slen = row_len_in;
+    if (!rc && compact && !ell) {
       const size_t eb = (xt_compact_bytes(C, C) + 255) & ~(size_t)255;
       rc = scratch_acquire(eb + sizeof(int32_t) * (size_t)C, st, &ce);
       if (!rc) {
-        ell = static_cast<uint32_t*>(ce.ptr);
-        slen = reinterpret_cast<int32_t*>(static_cast<char*>(ce.ptr) + eb);
-        rc = xt_compact_build(trans, C, C, ell, slen, st);
+        uint32_t* e = static_cast<uint32_t*>(ce.ptr);
+        int32_t* sl = reinterpret_cast<int32_t*>(static_cast<char*>(ce.ptr) + eb);
+        rc = xt_compact_build(trans, C, C, e, sl, st);
+        ell = e;
+        slen = sl;
       }
     }
     bool surface_done = false;  // the reordered solve wrote the surface itself
@@ -1198,7 +1204,7 @@ extern "C" int sa_xt_solve_ex(const int64_t* shot, const int64_t* goal, const in
                      "copy xT");
       if (!rc) rc = check_hip(hipStreamSynchronize(st), "hipStreamSynchronize");
     }
-    if (compact) scratch_release(ce, st);
+    if (compact && !ell_in) scratch_release(ce, st);
   }
   scratch_release(sc, st);
   *n_iter = iters;

@@ -82,9 +82,11 @@ constexpr size_t XB_LDS_MAX = 160 * 1024;
 constexpr int XB_MAX_SETS = 24;     // buckets per K4 launch
 // K4's static LDS (row sums, set pointers and bounds), reserved out of XB_LDS_MAX before the
 // dynamic R x P bins are sized (100 x 68 at R = 6 would ask 163,296 + 640 B of 163,840)
-constexpr size_t XB_LDS_STATIC = 1024;
-static_assert(XB_MAX_ROWS * 8 + XB_MAX_SETS * 24 <= XB_LDS_STATIC, "K4 static LDS");
+// + the compact-row staging rings (xe_emit: 256 entries per row)
+constexpr size_t XB_LDS_STATIC = 1024 + (size_t)XB_MAX_ROWS * 256 * 4;
+static_assert(XB_MAX_ROWS * 8 + XB_MAX_SETS * 24 + XB_MAX_ROWS * 256 * 4 <= XB_LDS_STATIC, "K4 static LDS");
 constexpr uint32_t XB_NONE = 0xFFFFFFFFu;
+constexpr uint32_t XE_CNT_ESC_K4 = 0xFFFFu;  // = XE_CNT_ESC: a count >= 65535 is read from the dense row
 static_assert(XS_PER * XS_THREADS * XS_SPLIT == XK_CHUNK && XS_PER >= 1, "K3 holds one part of a K1 region");
 static_assert(XS_PART * 4 + 2 * XB_NB_MAX * 4 + 256 <= XB_LDS_MAX, "K3 LDS");
 
@@ -431,12 +433,55 @@ struct XbSets {
 // C + 2 and the row sum.  The outputs hold rows from band0 * R on (a rank's row block, or the
 // whole table with band0 = 0).  overwrite: the rows and counts are written, not added to (a
 // fresh accumulator: no read of the old rows).
+// One wave writes a row's compact form (xt_ell_build_kernel's layout: the k-th non-zero count
+// of the row, column | min(count, 0xFFFF) << 16, at slot (k & ~127) | (k & 31) << 2 | (k >> 5) & 3)
+// 512 columns at a time (v[u] = the count at column c0 + 64 u + lane, 0 past the row): entries
+// are ranked by ballot + mbcnt into a 256-entry LDS ring S, and every complete chunk of 128 goes
+// out as 32 lanes x 16 B -- whole 512-B runs.  (Scattered 4-B stores left lines half written when
+// L2 evicted them: each partial line cost the memory a read-modify-write, 60 us per cfg5 table.)
+// Call with base = done = 0; after the last group, xe_emit_tail.
+__device__ __forceinline__ void xe_emit_group(const uint32_t (&v)[8], int c0, uint32_t* __restrict__ E,
+                                              uint32_t* S, int lane, int& base, int& done) {
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const uint64_t m = __ballot(v[u] != 0);
+    if (v[u] != 0) {
+      const uint32_t cnt = v[u] < XE_CNT_ESC_K4 ? v[u] : XE_CNT_ESC_K4;
+      S[(base + (int)lane_rank(m)) & 255] = (uint32_t)(c0 + 64 * u + lane) | (cnt << 16);
+    }
+    base += (int)__popcll(m);
+    if (base - done >= 128) {  // wave-uniform: a whole chunk is staged
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the ring writes land before the reads
+      if (lane < 32) {
+        const int o = done & 255;
+        const uint4 q = {S[o + lane], S[o + lane + 32], S[o + lane + 64], S[o + lane + 96]};
+        *reinterpret_cast<uint4*>(E + done + 4 * lane) = q;
+      }
+      done += 128;
+    }
+  }
+}
+__device__ __forceinline__ void xe_emit_tail(uint32_t* __restrict__ E, const uint32_t* S, int lane, int base, int done) {
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  if (lane < 32)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = done + lane + 32 * j;
+      if (k < base) E[done + 4 * lane + j] = S[k & 255];
+    }
+}
+
+// ell (optional, with overwrite): the band's rows also in the compact form of
+// xt_ell_build_kernel, emitted from the bins (ell + row * pe, row_len[row]) -- the solve then
+// skips its build pass and its 204 MB read of the table.
+__device__ __forceinline__ int xe_slot(int k);
 __global__ __launch_bounds__(XB_THREADS) void xt_band_count_kernel(XbSets sets, XbShape S, int band0,
                                                                    unsigned long long* __restrict__ shot,
                                                                    unsigned long long* __restrict__ goal,
                                                                    unsigned long long* __restrict__ move,
                                                                    int32_t* __restrict__ trans, int overwrite,
-                                                                   int vec) {
+                                                                   int vec, uint32_t* __restrict__ ell,
+                                                                   int32_t* __restrict__ row_len, int pe) {
   extern __shared__ __attribute__((aligned(16))) uint32_t h[];  // [R][P]
   __shared__ unsigned long long msum[XB_MAX_ROWS];
   const int lb = blockIdx.x, b = band0 + lb, C = S.C, P = S.P;
@@ -521,31 +566,55 @@ __global__ __launch_bounds__(XB_THREADS) void xt_band_count_kernel(XbSets sets, 
   }
   __syncthreads();
   const int lane = threadIdx.x & 63;
-  for (int i = 0; i < nr; ++i) {
-    const uint32_t* hr = h + i * P;
-    int32_t* dst = trans + (int64_t)(orow + i) * C;
-    unsigned long long ms = 0;
-    if (vec) {  // C % 4 == 0 and trans 16-byte aligned: every row starts 16-byte aligned
-      for (int c = 4 * threadIdx.x; c < C; c += 4 * XB_THREADS) {
-        const u32x4 v = *reinterpret_cast<const u32x4*>(hr + c);
-        ms += (unsigned long long)v[0] + v[1] + v[2] + v[3];
-        i32x4 o = {(int32_t)v[0], (int32_t)v[1], (int32_t)v[2], (int32_t)v[3]};
-        if (!overwrite) {
-          const i32x4 old = *reinterpret_cast<const i32x4*>(dst + c);
-          o += old;
+  // with ell, the first nr waves emit the compact rows (one row each) WHILE the others flush the
+  // dense rows: the emission is a chain of dependent LDS steps (~9 us per band) that would
+  // otherwise idle the CU after the flush
+  const int f0 = ell ? 64 * nr : 0, fth = XB_THREADS - f0;
+  if ((int)threadIdx.x >= f0) {
+    const int ft = threadIdx.x - f0;
+    for (int i = 0; i < nr; ++i) {
+      const uint32_t* hr = h + i * P;
+      int32_t* dst = trans + (int64_t)(orow + i) * C;
+      unsigned long long ms = 0;
+      if (vec) {  // C % 4 == 0 and trans 16-byte aligned: every row starts 16-byte aligned
+        for (int c = 4 * ft; c < C; c += 4 * fth) {
+          const u32x4 v = *reinterpret_cast<const u32x4*>(hr + c);
+          ms += (unsigned long long)v[0] + v[1] + v[2] + v[3];
+          i32x4 o = {(int32_t)v[0], (int32_t)v[1], (int32_t)v[2], (int32_t)v[3]};
+          if (!overwrite) {
+            const i32x4 old = *reinterpret_cast<const i32x4*>(dst + c);
+            o += old;
+          }
+          *reinterpret_cast<i32x4*>(dst + c) = o;
         }
-        *reinterpret_cast<i32x4*>(dst + c) = o;
+      } else {
+        for (int c = ft; c < C; c += fth) {
+          const uint32_t v = hr[c];
+          ms += v;
+          dst[c] = overwrite ? (int32_t)v : dst[c] + (int32_t)v;
+        }
       }
-    } else {
-      for (int c = threadIdx.x; c < C; c += XB_THREADS) {
-        const uint32_t v = hr[c];
-        ms += v;
-        dst[c] = overwrite ? (int32_t)v : dst[c] + (int32_t)v;
-      }
-    }
 #pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) ms += __shfl_xor(ms, d);
-    if (lane == 0 && ms) atomicAdd(&msum[i], ms);
+      for (int d = 32; d >= 1; d >>= 1) ms += __shfl_xor(ms, d);
+      if (lane == 0 && ms) atomicAdd(&msum[i], ms);
+    }
+  } else {  // ell: wave i emits row i (xe_emit_group)
+    __shared__ uint32_t ring[XB_MAX_ROWS][256];
+    const int i = threadIdx.x >> 6;
+    const uint32_t* hr = h + i * P;
+    uint32_t* E = ell + (int64_t)(orow + i) * pe;
+    int base = 0, done = 0;
+    for (int c0 = 0; c0 < C; c0 += 64 * 8) {
+      uint32_t v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int c = c0 + 64 * u + lane;
+        v[u] = c < C ? hr[c] : 0u;
+      }
+      xe_emit_group(v, c0, E, ring[i], lane, base, done);
+    }
+    xe_emit_tail(E, ring[i], lane, base, done);
+    if (lane == 0) row_len[orow + i] = base;
   }
   __syncthreads();
   if (threadIdx.x < nr) {
@@ -612,6 +681,7 @@ __host__ __device__ constexpr int xe_pitch(int C) { return (C + XE_KC - 1) / XE_
 // close together, distinct banks (entries 4 apart would put a dense row's columns 32 B apart,
 // eight lanes on a bank pair).
 __device__ __forceinline__ int xe_slot(int k) { return (k & ~(XE_KC - 1)) | ((k & 31) << 2) | ((k >> 5) & 3); }
+static_assert(XE_CNT_ESC_K4 == XE_CNT_ESC, "K4's compact rows escape counts like xt_ell_build_kernel");
 
 // Compact form of rows [0, nrows) of a count block (row i at cnt_rows + i*C): row i's non-zero
 // counts in column order, column | min(count, 0xFFFF) << 16, the k-th at ell[i*pe + xe_slot(k)]
@@ -625,24 +695,18 @@ __global__ __launch_bounds__(XE_BUILD_ROWS * 64) void xt_ell_build_kernel(const 
   if (r >= nrows) return;  // whole wave
   const int32_t* row = cnt_rows + (int64_t)r * C;
   uint32_t* E = ell + (int64_t)r * xe_pitch(C);
-  int base = 0;
+  __shared__ uint32_t ring[XE_BUILD_ROWS][256];
+  int base = 0, done = 0;
   for (int c0 = 0; c0 < C; c0 += 64 * 8) {
-    int32_t v[8];
+    uint32_t v[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int c = c0 + 64 * u + lane;
-      v[u] = c < C ? __builtin_nontemporal_load(row + c) : 0;
+      v[u] = c < C ? (uint32_t)__builtin_nontemporal_load(row + c) : 0u;
     }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const uint64_t m = __ballot(v[u] != 0);
-      if (v[u] != 0) {
-        const uint32_t cnt = (uint32_t)v[u] < XE_CNT_ESC ? (uint32_t)v[u] : XE_CNT_ESC;
-        E[xe_slot(base + (int)lane_rank(m))] = (uint32_t)(c0 + 64 * u + lane) | (cnt << 16);
-      }
-      base += (int)__popcll(m);
-    }
+    xe_emit_group(v, c0, E, ring[threadIdx.x >> 6], lane, base, done);
   }
+  xe_emit_tail(E, ring[threadIdx.x >> 6], lane, base, done);
   if (lane == 0) row_len[r] = base;
 }
 
@@ -1460,8 +1524,11 @@ static int bucket_batch(const sa_actions& A, const uint32_t* cells, int64_t n, i
 
 static int count_from_buckets(int nsets, const uint32_t* const* buckets, const int64_t* const* band_off,
                               const XbShape& S, int band0, int nbands, int64_t* shot, int64_t* goal, int64_t* move,
-                              int32_t* trans, int overwrite, hipStream_t st) {
+                              int32_t* trans, int overwrite, hipStream_t st, uint32_t* ell = nullptr,
+                              int32_t* row_len = nullptr) {
   if (nbands <= 0) return SA_OK;
+  // the compact rows come from the bins only when one launch writes the final counts
+  if (ell && (!overwrite || nsets > XB_MAX_SETS)) return fail(SA_EINVAL, "compact rows need one overwriting launch");
   const int vec = (S.C % 4 == 0) && aligned16(trans);
   const size_t lds = (size_t)S.R * S.P * 4;
   for (int s0 = 0; s0 < nsets || (s0 == 0 && nsets == 0); s0 += XB_MAX_SETS) {
@@ -1475,7 +1542,8 @@ static int count_from_buckets(int nsets, const uint32_t* const* buckets, const i
     // later launches add to what the first one wrote
     hipLaunchKernelGGL(xt_band_count_kernel, dim3((unsigned)nbands), dim3(XB_THREADS), lds, st, sets, S, band0,
                        reinterpret_cast<unsigned long long*>(shot), reinterpret_cast<unsigned long long*>(goal),
-                       reinterpret_cast<unsigned long long*>(move), trans, (overwrite && s0 == 0) ? 1 : 0, vec);
+                       reinterpret_cast<unsigned long long*>(move), trans, (overwrite && s0 == 0) ? 1 : 0, vec,
+                       ell, row_len, xe_pitch(S.C));
     int rc = check_launch("xt_band_count_kernel");
     if (rc) return rc;
     if (nsets == 0) break;
@@ -1705,6 +1773,14 @@ extern "C" int sa_xt_count_bucket(const sa_actions* a, const uint32_t* cells, in
 extern "C" int sa_xt_count_from_buckets(int32_t nsets, const uint32_t* const* buckets, const int64_t* const* band_off,
                                         int32_t l, int32_t w, int64_t* shot, int64_t* goal, int64_t* move,
                                         int32_t* trans, int32_t flags, void* stream) {
+  return sa_xt_count_from_buckets_ex(nsets, buckets, band_off, l, w, shot, goal, move, trans, flags, nullptr, nullptr,
+                                     stream);
+}
+
+extern "C" int sa_xt_count_from_buckets_ex(int32_t nsets, const uint32_t* const* buckets,
+                                           const int64_t* const* band_off, int32_t l, int32_t w, int64_t* shot,
+                                           int64_t* goal, int64_t* move, int32_t* trans, int32_t flags,
+                                           uint32_t* ell, int32_t* row_len, void* stream) {
   if (l < 1 || w < 1 || (int64_t)l * w > 46340) return fail(SA_EINVAL, "bad l or w");
   XbShape S;
   if (!xt_band_shape(l * w, &S)) return fail(SA_EINVAL, "the band-owned count does not hold %d cells", l * w);
@@ -1713,9 +1789,16 @@ extern "C" int sa_xt_count_from_buckets(int32_t nsets, const uint32_t* const* bu
     if (!band_off[k]) return fail(SA_EINVAL, "null band offsets");
   if (!shot || !goal || !move || !trans) return fail(SA_EINVAL, "null count buffer");
   if (flags & ~SA_XT_COUNT_OVERWRITE) return fail(SA_EINVAL, "unknown flags");
+  if (!ell != !row_len) return fail(SA_EINVAL, "ell and row_len come together");
+  if (ell) {
+    if (!xt_compact_ok(l * w)) return fail(SA_EINVAL, "the compact form takes 1 <= C <= %d", XE_XMAX);
+    if (!(flags & SA_XT_COUNT_OVERWRITE) || nsets > XB_MAX_SETS)
+      return fail(SA_EINVAL, "compact rows need SA_XT_COUNT_OVERWRITE and at most %d bucket sets", XB_MAX_SETS);
+    if (!aligned16(ell)) return fail(SA_EINVAL, "ell must be 16-byte aligned");
+  }
   if (nsets == 0 && !(flags & SA_XT_COUNT_OVERWRITE)) return SA_OK;
   return count_from_buckets(nsets, buckets, band_off, S, 0, S.NB, shot, goal, move, trans,
-                            (flags & SA_XT_COUNT_OVERWRITE) != 0, (hipStream_t)stream);
+                            (flags & SA_XT_COUNT_OVERWRITE) != 0, (hipStream_t)stream, ell, row_len);
 }
 
 extern "C" int sa_xt_count_band_rows(int32_t nsets, const uint32_t* const* buckets, const int64_t* const* band_off,

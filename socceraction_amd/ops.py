@@ -385,6 +385,9 @@ class XTCounts:
     move: torch.Tensor   # int64 [C]
     trans: torch.Tensor  # int32 [C*C]
     err: torch.Tensor    # int32 [1]
+    # the transition counts' compact rows (ell, row_len) as the count wrote them for the solve
+    # (xt_count_many on 1025 - 9472 cells); every op that changes the counts drops them
+    compact: Optional[Tuple[torch.Tensor, torch.Tensor]] = None
 
     @property
     def C(self) -> int:
@@ -392,6 +395,7 @@ class XTCounts:
 
     def zero_(self) -> 'XTCounts':
         """Zero every count in one fill of the backing buffer (on the current stream)."""
+        self.compact = None
         self.buf.zero_()
         return self
 
@@ -430,6 +434,7 @@ def xt_count(batch: ActionBatch, l: int, w: int, acc: Optional[XTCounts] = None,
     :func:`xt_rate_codes` of the same actions on the same grid. ``shared``: the pass runs next
     to other kernels (workgroups sized to co-reside with them)."""
     acc = acc or xt_zero_counts(l, w, batch.device)
+    acc.compact = None  # the counts change
     s = batch.struct()
     if codes is None and not shared:
         _native.check(_native.lib().sa_xt_count(ctypes.byref(s), l, w, _ptr(acc.shot),
@@ -554,16 +559,40 @@ def xt_rate_interp_codes_many(icodes: Sequence[torch.Tensor], ns: Sequence[int],
     return [t[:n] for t, n in zip(outs, ns)], err
 
 
+XB_MAX_SETS = 24  # bucket sets one band-count launch takes (sa_xt_large.hip)
+
+
+def _compact_pitch(C: int) -> int:
+    return int(_native.lib().sa_xt_compact_bytes(C, 1)) // 4
+
+
 def xt_count_buckets(parts: Sequence[XTBuckets], l: int, w: int, acc: XTCounts,
-                     overwrite: bool = False) -> XTCounts:
+                     overwrite: bool = False, compact: Optional[bool] = None) -> XTCounts:
     """The once-per-fit half of the band-owned count: every batch's buckets into ``acc`` (added;
-    ``overwrite``: written, the rows' old values never read)."""
+    ``overwrite``: written, the rows' old values never read).  ``compact`` (default: whenever it
+    can) also writes the transition counts' compact rows for the large-grid solve
+    (``sa_xt_count_from_buckets_ex``; ``acc.compact``): overwrite, <= 24 batches and
+    1025 <= C <= 9472 only."""
     k = len(parts)
+    C = l * w
+    can = (overwrite and k <= XB_MAX_SETS and _native.SA_XT_SOLVE_MAX_C < C <= _native.SA_XT_COMPACT_MAX_C)
+    if compact and not can:
+        raise ValueError('compact rows need overwrite, at most 24 batches and 1025 <= C <= 9472')
+    compact = can if compact is None else compact
+    acc.compact = None
+    ell = rl = None
+    if compact:
+        pe = _compact_pitch(C)
+        ell = torch.empty(C * pe, dtype=torch.int32, device=acc.trans.device)
+        rl = torch.empty(C, dtype=torch.int32, device=acc.trans.device)
     keys = (ctypes.c_void_p * max(k, 1))(*[p.keys.data_ptr() for p in parts])
     offs = (ctypes.c_void_p * max(k, 1))(*[p.band_off.data_ptr() for p in parts])
-    _native.check(_native.lib().sa_xt_count_from_buckets(
+    _native.check(_native.lib().sa_xt_count_from_buckets_ex(
         k, keys, offs, int(l), int(w), _ptr(acc.shot), _ptr(acc.goal), _ptr(acc.move),
-        _ptr(acc.trans), _native.SA_XT_COUNT_OVERWRITE if overwrite else 0, stream_handle()))
+        _ptr(acc.trans), _native.SA_XT_COUNT_OVERWRITE if overwrite else 0, _ptr(ell), _ptr(rl),
+        stream_handle()))
+    if compact:
+        acc.compact = (ell, rl)
     return acc
 
 
@@ -639,6 +668,7 @@ def xt_count_cells(cells: torch.Tensor, n: int, l: int, w: int, acc: Optional[XT
                    shared: bool = False) -> XTCounts:
     """The count pass of ExpectedThreat.fit from cell codes (4 B per action read)."""
     acc = acc or xt_zero_counts(l, w, cells.device)
+    acc.compact = None  # the counts change
     _native.check(_native.lib().sa_xt_count_cells(_ptr(cells), int(n), int(l), int(w),
                                                   _ptr(acc.shot), _ptr(acc.goal), _ptr(acc.move),
                                                   _ptr(acc.trans), _ptr(acc.err), int(shared),
@@ -703,10 +733,12 @@ def xt_solve(acc: XTCounts, eps: float = 1e-5, max_iter: int = 1000,
     tt = torch.empty((C, C), dtype=torch.float64, device=dev) if transition else None
     heat = torch.empty((max_iter + 1, C), dtype=torch.float64, device=dev)
     n_iter, path = ctypes.c_int32(0), ctypes.c_int32(0)
+    ell, rl = acc.compact if getattr(acc, 'compact', None) is not None else (None, None)
     _native.check(_native.lib().sa_xt_solve_ex(
         _ptr(acc.shot), _ptr(acc.goal), _ptr(acc.move), _ptr(acc.trans), acc.l, acc.w, float(eps),
         int(max_iter), _native.SA_XT_SOLVE_EXACT if exact_order else 0, _ptr(mats), _ptr(tt),
-        _ptr(heat), ctypes.byref(n_iter), ctypes.byref(path), stream_handle()))
+        _ptr(heat), ctypes.byref(n_iter), ctypes.byref(path), _ptr(ell), _ptr(rl),
+        stream_handle()))
     if n_iter.value < 0:
         raise RuntimeError(f'xT value iteration did not converge within {max_iter} iterations')
     return XTSolution(mats, tt, heat[:n_iter.value + 1], n_iter.value,

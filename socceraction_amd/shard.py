@@ -40,6 +40,7 @@ def allreduce_xt_counts(acc, group=None) -> None:
     overlapping.  No staging copy, no ``torch.cat``."""
     _check_world(group)
     _flag_count_range(acc, group)
+    acc.compact = None  # this rank's compact rows no longer describe the summed counts
     _all_reduce(acc.buf.view(torch.int32), group=group)
 
 

@@ -57,6 +57,51 @@ def test_band_count_many_batches_vs_oracle(sa, l, w):
     _same_counts(acc2, _oracle(_cat(ds), l, w), l, w)
 
 
+def _xe_slots(k):
+    return (k & ~127) | ((k & 31) << 2) | ((k >> 5) & 3)
+
+
+@pytest.mark.parametrize('l,w,hot', [(105, 68, False), (40, 30, False), (120, 68, False),
+                                     (105, 68, True)])
+def test_band_count_emits_compact_rows(sa, l, w, hot):
+    """The band count's compact rows (sa_xt_count_from_buckets_ex, written from the bins) ==
+    sa_xt_compact_rows of the dense table it wrote, entry for entry (incl. escaped counts >=
+    65535), and the solve from them == the solve that builds its own (same path, iteration
+    count and heatmaps bit for bit); an all-reduce or a further count drops them."""
+    B, ops, syn, N = sa['batch'], sa['ops'], sa['synthetic'], sa['_native']
+    C = l * w
+    ds = [syn.spadl_games(g, game_id0=31 * i + 5) for i, g in enumerate((150 if hot else 60, 45))]
+    if hot:
+        mv = np.isin(ds[0]['type_id'], (0, 1, 21))
+        ds[0]['start_x'][mv], ds[0]['start_y'][mv] = 52.2, 33.3
+        ds[0]['end_x'][mv], ds[0]['end_y'][mv] = 104.999, 0.0
+    abs_ = [B.ActionBatch.from_columns(d) for d in ds]
+    acc = ops.xt_count_many(abs_, l, w)
+    assert acc.compact is not None
+    ell, rl = acc.compact
+    pe = int(N.lib().sa_xt_compact_bytes(C, 1)) // 4
+    ref_ell = torch.empty(C * pe, dtype=torch.int32, device=ell.device)
+    ref_rl = torch.empty(C, dtype=torch.int32, device=ell.device)
+    N.check(N.lib().sa_xt_compact_rows(acc.trans.data_ptr(), C, C, ref_ell.data_ptr(),
+                                       ref_rl.data_ptr(), torch.cuda.current_stream().cuda_stream))
+    a, b = rl.cpu().numpy(), ref_rl.cpu().numpy()
+    np.testing.assert_array_equal(a, b)
+    ea, eb = ell.cpu().numpy().reshape(C, pe), ref_ell.cpu().numpy().reshape(C, pe)
+    for r in np.flatnonzero(a):
+        sl = _xe_slots(np.arange(a[r]))
+        np.testing.assert_array_equal(ea[r, sl], eb[r, sl])
+    if hot:
+        assert (ea.view(np.uint32) >> 16 == 0xFFFF).any()
+    sol = ops.xt_solve(acc, transition=False)
+    acc.compact = None
+    ref = ops.xt_solve(acc, transition=False)
+    assert sol.path == ref.path and sol.n_iter == ref.n_iter
+    assert torch.equal(sol.heatmaps, ref.heatmaps) and torch.equal(sol.mats, ref.mats)
+    acc2 = ops.xt_count_many(abs_, l, w)
+    ops.xt_count(abs_[0], l, w, acc2)
+    assert acc2.compact is None
+
+
 def test_band_count_hot_cells_and_edges(sa):
     """Adversarial key distributions: every move between two cells (one bin far above 65535
     counts, one band holding almost every key), actions on the exact pitch edges, NaN / inf
