@@ -9,9 +9,10 @@
 //    counted action becomes one 4-B key (start cell << 16 | slot):
 //      K1 xt_keys_kernel        reads the actions once, writes each workgroup's keys contiguously
 //                               (wave ballots) and the keys per band;
-//      K2 xt_band_scan_kernel   band offsets (exclusive scan);
-//      K3 xt_keys_scatter_kernel  a counting sort of each workgroup's keys by band in LDS, then
-//                               runs of keys into the band buckets;
+//      K3 xt_keys_scatter_kernel  the band offsets (every workgroup scans the band counts
+//                               itself; the first one also writes them out), a counting sort of
+//                               each workgroup's keys by band in LDS, then runs of keys into the
+//                               band buckets;
 //      K4 xt_band_count_kernel  one workgroup per band: its R rows x (C + 3) bins as u32 in LDS
 //                               (143 KB at 105 x 68), filled from the band's bucket(s), flushed
 //                               once with coalesced stores -- the shot / goal / move counts of
@@ -350,18 +351,6 @@ __device__ uint32_t block_scan(uint32_t* a, int n, uint32_t* ws) {
 }
 __device__ uint32_t block_scan_1024(uint32_t* a, int n, uint32_t* ws) { return block_scan<1024>(a, n, ws); }
 
-// K2: band_off[b] = keys of bands < b (int64, [NB + 1]); cursor[b] = band_off[b].
-__global__ __launch_bounds__(1024) void xt_band_scan_kernel(uint32_t* __restrict__ band_cnt, int NB,
-                                                            int64_t* __restrict__ band_off,
-                                                            uint32_t* __restrict__ cursor) {
-  __shared__ uint32_t ws[17];
-  const uint32_t total = block_scan_1024(band_cnt, NB, ws);
-  for (int b = threadIdx.x; b < NB; b += 1024) {
-    band_off[b] = band_cnt[b];
-    cursor[b] = band_cnt[b];
-  }
-  if (threadIdx.x == 0) band_off[NB] = total;
-}
 
 // K3: XS_SPLIT workgroups per K1 region, one per part of its keys (<= XS_PART, XS_PER per thread in registers), ranked
 // within their band by LDS atomics, each band's run gets its place in the band's bucket by ONE
@@ -369,13 +358,24 @@ __global__ __launch_bounds__(1024) void xt_band_scan_kernel(uint32_t* __restrict
 // sorted key i -- consecutive threads of a run write consecutive words.
 __global__ __launch_bounds__(XS_THREADS) void xt_keys_scatter_kernel(const uint32_t* __restrict__ keys,
                                                                      const uint32_t* __restrict__ region_cnt,
-                                                                     XbShape S, uint32_t* __restrict__ cursor,
+                                                                     XbShape S, const uint32_t* __restrict__ band_cnt,
+                                                                     int64_t* __restrict__ band_off,
+                                                                     uint32_t* __restrict__ cursor,
                                                                      uint32_t* __restrict__ buckets) {
   extern __shared__ uint32_t sm[];
   uint32_t* bh = sm;              // [NB] keys per band, then the local run offsets
-  uint32_t* bb = sm + S.NB;       // [NB] the runs' places in the buckets
+  uint32_t* bb = sm + S.NB;       // [NB] the bands' offsets, then the runs' places in the buckets
   uint32_t* sorted = sm + 2 * S.NB;  // [XS_PART]
   __shared__ uint32_t ws[17];
+  // the band offsets: every workgroup scans K1's band counts itself (5.7 KB at cfg5, from L2)
+  // instead of waiting for a one-workgroup scan launch; the first writes them out for K4
+  for (int b = threadIdx.x; b < S.NB; b += XS_THREADS) bb[b] = band_cnt[b];
+  __syncthreads();
+  const uint32_t total = block_scan_1024(bb, S.NB, ws);
+  if (blockIdx.x == 0) {
+    for (int b = threadIdx.x; b < S.NB; b += XS_THREADS) band_off[b] = bb[b];
+    if (threadIdx.x == 0) band_off[S.NB] = total;
+  }
   const int region = blockIdx.x / XS_SPLIT, part = blockIdx.x % XS_SPLIT;
   const uint32_t rc = region_cnt[region], p0 = (uint32_t)part * XS_PART;
   const uint32_t cnt = rc > p0 ? min(rc - p0, (uint32_t)XS_PART) : 0u;
@@ -398,9 +398,9 @@ __global__ __launch_bounds__(XS_THREADS) void xt_keys_scatter_kernel(const uint3
     }
   }
   __syncthreads();
-  for (int b = threadIdx.x; b < S.NB; b += XS_THREADS) {
+  for (int b = threadIdx.x; b < S.NB; b += XS_THREADS) {  // cursor: zeroed with the band counts
     const uint32_t c = bh[b];
-    bb[b] = c ? atomicAdd(&cursor[b], c) : 0u;
+    bb[b] = c ? bb[b] + atomicAdd(&cursor[b], c) : 0u;
   }
   __syncthreads();
   block_scan_1024(bh, S.NB, ws);
@@ -1480,8 +1480,8 @@ static int bucket_batch(const sa_actions& A, const uint32_t* cells, int64_t n, i
                         uint32_t* buckets, int64_t* band_off, int32_t* err, const XkRate& RO, hipStream_t st) {
   const int64_t regions = (n + XK_CHUNK - 1) / XK_CHUNK;
   // scratch: band_cnt [NB] | cursor [NB] | region_cnt [regions] | keys [regions * XK_CHUNK], each
-  // part on 256-B boundaries: the band counts' memset is ONE aligned fill (an unaligned start
-  // split it into three fill kernels, ~9 us more per batch)
+  // part on 256-B boundaries: the band counts and cursors are zeroed by ONE aligned fill (an
+  // unaligned start split it into three fill kernels, ~9 us more per batch)
   auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
   const size_t nbb = al((size_t)S.NB * 4), rcb = al((size_t)regions * 4);
   const size_t bytes = 2 * nbb + rcb + (size_t)regions * XK_CHUNK * 4;
@@ -1493,7 +1493,7 @@ static int bucket_batch(const sa_actions& A, const uint32_t* cells, int64_t n, i
   uint32_t* cursor = reinterpret_cast<uint32_t*>(base + nbb);
   uint32_t* region_cnt = reinterpret_cast<uint32_t*>(base + 2 * nbb);
   uint32_t* keys = reinterpret_cast<uint32_t*>(base + 2 * nbb + rcb);
-  rc = check_hip(hipMemsetAsync(band_cnt, 0, nbb, st), "memset band counts");
+  rc = check_hip(hipMemsetAsync(band_cnt, 0, 2 * nbb, st), "memset band counts and cursors");
   if (!rc) {
     sa_actions none;
     memset(&none, 0, sizeof(none));
@@ -1509,13 +1509,9 @@ static int bucket_batch(const sa_actions& A, const uint32_t* cells, int64_t n, i
     rc = check_launch("xt_keys_kernel");
   }
   if (!rc) {
-    hipLaunchKernelGGL(xt_band_scan_kernel, dim3(1), dim3(1024), 0, st, band_cnt, S.NB, band_off, cursor);
-    rc = check_launch("xt_band_scan_kernel");
-  }
-  if (!rc) {
     const size_t lds = ((size_t)2 * S.NB + XS_PART) * 4;
     hipLaunchKernelGGL(xt_keys_scatter_kernel, dim3((unsigned)(regions * XS_SPLIT)), dim3(XS_THREADS), lds, st, keys,
-                       region_cnt, S, cursor, buckets);
+                       region_cnt, S, band_cnt, band_off, cursor, buckets);
     rc = check_launch("xt_keys_scatter_kernel");
   }
   scratch_release(sc, st);
