@@ -247,11 +247,26 @@ def _gloo_worker(rank, world, port, q):
     # rank 0 flags an infinite shot start, rank 1 that and an infinite move start: the byte
     # lanes add up without touching each other
     acc.err.fill_(ops.XT_ERR_SHOT & 0x1 if rank == 0 else 0x101)
+    acc.compact = (torch.zeros(4, dtype=torch.int32), torch.zeros(1, dtype=torch.int32))
     shard.allreduce_xt_counts(acc)  # ONE all-reduce
+    assert acc.compact is None  # this rank's compact rows describe its own counts only
     if rank == 0:
         q.put((acc.shot.numpy().copy(), acc.goal.numpy().copy(), acc.move.numpy().copy(),
                acc.trans.numpy().copy(), int(acc.err.item())))
     dist.destroy_process_group()
+
+
+def test_xt_counts_drop_compact_rows_when_the_counts_change():
+    """XTCounts.compact (the compact rows a band count wrote for the solve) never outlives the
+    counts it describes: zeroing drops it (the all-reduce case is in the gloo test)."""
+    import torch
+
+    from socceraction_amd import ops
+    acc = ops.xt_zero_counts(105, 68, 'cpu')
+    assert acc.compact is None
+    acc.compact = (torch.zeros(4, dtype=torch.int32), torch.zeros(1, dtype=torch.int32))
+    acc.zero_()
+    assert acc.compact is None
 
 
 def test_xt_count_allreduce_gloo_world2():
