@@ -43,7 +43,7 @@ namespace sa {
 #define SA_XK_PROBE 0  // diagnostic builds (wrong counts): 1 = no band histogram, 2 = no key stores
 #endif
 #ifndef SA_XK_THREADS
-#define SA_XK_THREADS 1024  // K1 workgroup (two per CU at cfg5: 32 waves of loads in flight)
+#define SA_XK_THREADS 1024  // K1 workgroup (118 VGPRs with the rate operands: one per CU, 16 waves; 512: the same, r04ae)
 #endif
 constexpr int XK_THREADS = SA_XK_THREADS;
 #ifndef SA_XK_U
