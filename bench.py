@@ -1198,21 +1198,30 @@ def main() -> None:
     if args.rotate >= 2:  # the same step over K device copies of the batch, one per step in turn
         rotate = rotate_extra(args, dist, dev, d, ps, pc, inp, step, n, total_actions, world)
     extra_side = {}
+
+    def side(name, fn):
+        """A side entry never takes the main line down with it: an exception is reported in its
+        place (and on stderr); its parity failures still fail the run below."""
+        try:
+            extra_side[name] = fn()
+        except Exception as e:  # noqa: BLE001  (reported, not hidden)
+            import traceback
+            traceback.print_exc()
+            extra_side[name] = {'error': f'{type(e).__name__}: {e}'}
     if not args.no_side:
         # cfg3 first: its bool block wants a physically contiguous range, which cfg5's ~1e8
         # actions of device batches (allocated and freed by its entry) would fragment
-        extra_side['atomic_cfg3'] = atomic_extra(dist, rank, world, dev, args.atomic_games,
-                                                 check=check)
+        side('atomic_cfg3', lambda: atomic_extra(dist, rank, world, dev, args.atomic_games, check=check))
         torch.cuda.empty_cache()
         cfg5_sharded = args.xt_sharded or args.cfg5_solve in ('auto', 'sharded', 'sharded-rows')
-        extra_side['xt105_cfg5'] = xt105_extra(ab, dist, dev, cfg5_sharded, args.cfg5_games,
-                                               rank, world, args.games, d=d, check=check,
-                                               solve='rows' if args.cfg5_solve == 'sharded-rows'
-                                               else 'compact')
-        extra_side['convert_to_atomic'] = convert_extra(d, dist, dev)
-        extra_side['rate_on_device'] = rate_extra(ab, out, n, dev)
+        side('xt105_cfg5', lambda: xt105_extra(ab, dist, dev, cfg5_sharded, args.cfg5_games, rank, world,
+                                                args.games, d=d, check=check,
+                                                solve='rows' if args.cfg5_solve == 'sharded-rows'
+                                                else 'compact'))
+        side('convert_to_atomic', lambda: convert_extra(d, dist, dev))
+        side('rate_on_device', lambda: rate_extra(ab, out, n, dev))
         if args.e2e_games > 0 and rank == 0:
-            extra_side['end_to_end'] = e2e_extra(d, min(args.e2e_games, args.games))
+            side('end_to_end', lambda: e2e_extra(d, min(args.e2e_games, args.games)))
     side_ok = all(v.get('parity', {}).get('ok', True) for v in extra_side.values())
     if rank != 0:
         if dist:
