@@ -920,7 +920,7 @@ def main() -> None:
                          '3.24 - 3.31 ms per step, profiles/r02_step_ab.md), or on the side stream')
     ap.add_argument('--num-tile', type=int, default=128,
                     help='rows per f64/i64-block tile (0 = one tile: plain column-major)')
-    ap.add_argument('--event-every', type=int, default=4,
+    ap.add_argument('--event-every', type=int, default=10,
                     help='per-launch HIP events on every Nth timed step (1 = every step); the '
                          'kernels\' mean durations come from those steps')
     ap.add_argument('--events', default='native', choices=('native', 'torch'),
