@@ -45,7 +45,10 @@ constexpr int LANE_ACTS = 16;
 #ifndef SA_CG_COLS
 #define SA_CG_COLS 32  // bool_colgroup_kernel: target columns per wave
 #endif
-constexpr int BLOCK_WAVES = 4;
+#ifndef SA_NUM_BLOCK_WAVES
+#define SA_NUM_BLOCK_WAVES 4  // numeric-pass workgroup in waves (A/B knob; 3 waves per SIMD fit 12 per CU)
+#endif
+constexpr int BLOCK_WAVES = SA_NUM_BLOCK_WAVES;
 constexpr int NUM_PAIRS = 1;                    // 2-action pairs per lane in num_features_kernel
 constexpr int WAVE_ACTS = 128 * NUM_PAIRS;      // actions per wave in num_features_kernel
 constexpr int BLOCK_ACTS = WAVE_ACTS * BLOCK_WAVES;
@@ -1414,7 +1417,7 @@ __device__ __forceinline__ void num_features_body(const FeatArgs& args, int64_t 
 }
 
 template <bool ATOMIC, bool EXPLICIT, int KF, bool TAIL = false, bool N32 = false, bool COND = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(num_min_waves<ATOMIC, TAIL>(), 8)))
+__global__ __launch_bounds__(64 * BLOCK_WAVES) __attribute__((amdgpu_waves_per_eu(num_min_waves<ATOMIC, TAIL>(), 8)))
 void num_features_kernel(FeatArgs args) {
   const int wv = threadIdx.x / WAVE;
   const int64_t wave_base = args.row0 + (xcd_logical_block() * BLOCK_WAVES + wv) * WAVE_ACTS;
