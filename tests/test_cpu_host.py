@@ -100,6 +100,25 @@ def test_invalid_arguments_are_rejected_without_a_gpu():
     assert b'n_frames' in lib.sa_last_error()
     with pytest.raises(ValueError):
         _native.check(rc)
+    # round-5 entry points: their argument checks too come before any HIP call
+    fake = ctypes.c_void_p(256)  # never dereferenced on the host
+    none_p = ctypes.POINTER(ctypes.c_void_p)()
+    rc = lib.sa_xt_count_from_buckets_ex(0, none_p, none_p, 105, 68, fake, fake, fake, fake,
+                                         _native.SA_XT_COUNT_OVERWRITE, fake, None, None)
+    assert rc == _native.SA_EINVAL and b'together' in lib.sa_last_error()
+    rc = lib.sa_xt_count_from_buckets_ex(0, none_p, none_p, 105, 68, fake, fake, fake, fake, 0,
+                                         fake, fake, None)
+    assert rc == _native.SA_EINVAL and b'OVERWRITE' in lib.sa_last_error()
+    n_iter, path = ctypes.c_int32(0), ctypes.c_int32(0)
+    rc = lib.sa_xt_solve_ex(fake, fake, fake, fake, 16, 12, 1e-5, 100, 0, fake, fake, fake,
+                            ctypes.byref(n_iter), ctypes.byref(path), fake, fake, None)
+    assert rc == _native.SA_EINVAL and b'compact' in lib.sa_last_error()
+    rc = lib.sa_xt_solve_ex(fake, fake, fake, fake, 105, 68, 1e-5, 100, 4, fake, None, fake,
+                            ctypes.byref(n_iter), ctypes.byref(path), None, None, None)
+    assert rc == _native.SA_EINVAL and b'flags' in lib.sa_last_error()
+    rc = lib.sa_xt_rate_interp_codes_many(-1, none_p, None, fake, fake, fake, 105, 68, fake, 1050,
+                                          fake, 680, none_p, fake, None)
+    assert rc == _native.SA_EINVAL
 
 
 # ----------------------------------------------------------------------------- catalogue
