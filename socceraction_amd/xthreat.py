@@ -84,7 +84,9 @@ def _safe_divide(a, b) -> np.ndarray:
 def _fit_counts(actions: pd.DataFrame, l: int, w: int, process_group=None,
                 mask: int = ops.XT_ERR_FIT) -> ops.XTCounts:
     if len(actions):
-        acc = ops.xt_count(ActionBatch.from_frame(actions), l, w)
+        # the many-batch entry (one batch): a fresh accumulator the band-owned count writes
+        # whole, and for 1025 - 9472 cells the solve's compact rows from the same pass
+        acc = ops.xt_count_many([ActionBatch.from_frame(actions)], l, w)
     else:
         from .batch import device
         acc = ops.xt_zero_counts(l, w, device())
