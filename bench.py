@@ -109,7 +109,9 @@ def _dist():
     """One process per GPU (torch.distributed.run); backend nccl = RCCL over xGMI.
     SA_DIST_BACKEND=gloo is for rehearsing several ranks on one GPU."""
     ws = int(os.environ.get('WORLD_SIZE', '1'))
-    if ws > 1:
+    # SA_BENCH_DIST=1: the process-group path even at one rank (RCCL with world size 1), so the
+    # N-GPU code runs end to end in -m gpu on a one-GPU box (tests/test_gpu_bench.py)
+    if ws > 1 or os.environ.get('SA_BENCH_DIST') == '1':
         import torch.distributed as dist
         lr = int(os.environ.get('LOCAL_RANK', '0'))
         backend = os.environ.get('SA_DIST_BACKEND', 'nccl')

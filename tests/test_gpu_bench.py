@@ -56,6 +56,28 @@ def test_bench_gpus_2_side_entries(solve):
     assert a['parity']['ok']
 
 
+def test_bench_rccl_one_rank_every_entry():
+    """bench.py's process-group path through REAL RCCL (backend nccl) with one rank on the test
+    GPU (SA_BENCH_DIST=1 under torch.distributed.run): the step's all-reduce of the xT counts,
+    the timing barriers and max-reductions, cfg5's sharded exchange and cfg3's split -- the code
+    the driver's N-GPU runs execute -- end to end, every parity block ok, no side-entry error."""
+    env = dict(os.environ, SA_BENCH_DIST='1')
+    for k in ('WORLD_SIZE', 'RANK', 'LOCAL_RANK', 'SA_DIST_BACKEND'):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '1',
+                        '--master-addr', '127.0.0.1', '--master-port', '29533', 'bench.py', '--gpus', '1',
+                        '--games', '20', '--steps', '2', '--warmup', '1', '--no-cpu', '--cfg5-games', '45',
+                        '--atomic-games', '30', '--e2e-games', '5'], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=280)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith('{')]
+    assert p.returncode == 0 and len(lines) == 1, p.stdout[-2000:] + p.stderr[-3000:]
+    out = json.loads(lines[0])
+    assert out['n_gpus'] == 1 and out['value'] > 0 and out['parity']['ok']
+    for name in ('xt105_cfg5', 'atomic_cfg3', 'convert_to_atomic', 'rate_on_device'):
+        assert 'error' not in out[name], (name, out[name])
+    assert out['xt105_cfg5']['parity']['ok'] and out['atomic_cfg3']['parity']['ok']
+
+
 def test_device_events_order_streams_and_time():
     """socceraction_amd.events.DeviceEvent (sa_event_*, no system-scope fence): a side stream
     that waits on an event recorded after a producer kernel sees the producer's writes, and a
