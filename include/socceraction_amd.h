@@ -282,10 +282,18 @@ int sa_xt_count_codes(const sa_actions* a, int32_t l, int32_t w, int64_t* shot, 
  * Code (u32): bits 0-11 start cell, 12-23 end cell (xthreat.py:25-37 binning), 24-25 class
  * (1 = shot, type 11; 2 = move: pass / dribble / cross), 26 result == success, 27 NaN in the
  * start coordinates, 28 start not finite, 29 end not finite.  cells: [n] u32, 16-byte aligned.
- * sa_xt_count_cells accumulates exactly what sa_xt_count does on those actions (same counts,
- * same err_flags bits); sa_xt_rate_cells equals sa_xt_rate without interpolation (grid = the
- * (w, l) xT surface). */
+ * Grids of l * w <= SA_XT_CELLS16_MAX_C (202: the small-grid count; 16 x 12) take a 16-bit code
+ * instead, 2 B per action in the first half of the same buffer: s * C + e for a successful move
+ * with finite coordinates (s, e: start / end cell); C^2 + 2 s + goal for a shot with a finite
+ * start; C^2 + k C + s for a move with a finite start that is unsuccessful (k = 2), has a
+ * non-finite end and is unsuccessful (k = 3) or successful (k = 4); C^2 + 5 C + {0 shot with a
+ * NaN start, 1 shot with an infinite start, 2 / 3 move with a NaN start unsuccessful /
+ * successful, 4 / 5 move with an infinite start unsuccessful / successful}; 0xFFFF any other
+ * action.  sa_xt_count_cells accumulates exactly what sa_xt_count does on those actions (same
+ * counts, same err_flags bits); sa_xt_rate_cells equals sa_xt_rate without interpolation (grid
+ * = the (w, l) xT surface). */
 #define SA_XT_CELLS_MAX_C 4096
+#define SA_XT_CELLS16_MAX_C 202
 int sa_xt_cells(const sa_actions* a, int32_t l, int32_t w, uint32_t* cells, void* stream);
 int sa_xt_count_cells(const uint32_t* cells, int64_t n, int32_t l, int32_t w, int64_t* shot,
                       int64_t* goal, int64_t* move, int32_t* trans, int32_t* err_flags,

@@ -24,6 +24,7 @@ SA_SEG_BLOCK = 128  # rows per entry of sa_actions.seg_of_block
 SA_XT_SOLVE_MAX_C = 1024  # sa_xt_solve: larger grids may pass trans_t = NULL
 SA_XT_CELLS_MAX_C = 4096
 SA_XT_COUNT_SHARED, SA_XT_COUNT_OVERWRITE = 1, 2
+SA_XT_CELLS16_MAX_C = 202  # xT cell codes: 16 bits per action up to this many cells
 SA_XT_COMPACT_MAX_C = 9472  # sa_xt_compact_rows / sa_xt_iterate_compact
 SA_XT_SOLVE_EXACT = 1  # sa_xt_solve_ex / sa_xt_solve_compact: the reference's summation order
 # which path produced a large-grid solve (sa_xt_solve_ex's *path)

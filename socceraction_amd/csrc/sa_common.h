@@ -142,6 +142,36 @@ __device__ __forceinline__ uint32_t xt_cell_code(int t, int r, double sx, double
 }
 
 
+// Grids of C <= SA_XT_CELLS16_MAX_C cells (the small-grid count; 16 x 12) carry a 16-bit cell
+// code (include/socceraction_amd.h): s * C + e for a successful move with finite coordinates,
+// then the ranges below -- 2 B per action written by the feature pass and read by the count and
+// the rate instead of 4 (the bench step: 2.951 -> 2.935 ms, profiles/r05ap).  SA_XT_CELLS16=0
+// (A/B builds) keeps the u32 code for every grid.
+#ifndef SA_XT_CELLS16
+#define SA_XT_CELLS16 1
+#endif
+__host__ __device__ constexpr bool xt_c16(int C) { return SA_XT_CELLS16 && C <= SA_XT_CELLS16_MAX_C; }
+constexpr uint32_t XT_C16_NONE = 0xFFFFu;
+__device__ __forceinline__ uint32_t xt_cell_code16(int t, int r, double sx, double sy, double ex, double ey,
+                                                   int l, int w) {
+  const int C = l * w;
+  const bool shot = t == T_SHOT, mv = is_move(t), succ = r == R_SUCCESS;
+  if (!shot && !mv) return XT_C16_NONE;
+  const bool snan = isnan(sx) || isnan(sy), sfin = isfinite(sx) && isfinite(sy);
+  const bool efin = isfinite(ex) && isfinite(ey);
+  const uint32_t CC = (uint32_t)C * C, F = CC + 5u * C;
+  if (shot) {
+    if (snan) return F;
+    if (!sfin) return F + 1u;
+    return CC + 2u * (uint32_t)flat_index(sx, sy, l, w) + (succ ? 1u : 0u);
+  }
+  if (snan) return F + 2u + (succ ? 1u : 0u);
+  if (!sfin) return F + 4u + (succ ? 1u : 0u);
+  const uint32_t cs = (uint32_t)flat_index(sx, sy, l, w);
+  if (!efin) return CC + (succ ? 4u : 3u) * C + cs;
+  if (!succ) return CC + 2u * C + cs;
+  return cs * C + (uint32_t)flat_index(ex, ey, l, w);
+}
 // ---- shared by the xT count passes (sa_xt.hip, sa_xt_large.hip) ----
 // Rate operand of one action for a later rate() on the same (l, w) grid, written by the count
 // pass so the rate pass reads 4 B instead of the 34 B of coordinates and ids again
@@ -182,6 +212,39 @@ struct XtAct {
   bool succ, snan, sfin, efin;
   int cs, ce;              // start / end cell (valid when binned)
 };
+
+__device__ __forceinline__ XtAct decode_cell16(uint32_t c, int C) {
+  XtAct a;
+  a.cls = 0;
+  a.succ = a.snan = false;
+  a.sfin = a.efin = true;
+  a.cs = a.ce = 0;
+  const uint32_t CC = (uint32_t)C * C, F = CC + 5u * C;
+  if (c == XT_C16_NONE) return a;
+  if (c < CC) {
+    a.cls = XT_CELL_MOVE;
+    a.succ = true;
+    a.cs = (int)(c / (uint32_t)C);
+    a.ce = (int)(c - (uint32_t)a.cs * C);
+  } else if (c < CC + 2u * C) {
+    a.cls = XT_CELL_SHOT;
+    a.succ = (c - CC) & 1u;
+    a.cs = (int)((c - CC) >> 1);
+  } else if (c < F) {
+    const uint32_t k = (c - CC) / (uint32_t)C;  // 2: unsuccessful move, 3 / 4: non-finite end
+    a.cls = XT_CELL_MOVE;
+    a.cs = (int)(c - CC - k * C);
+    a.succ = k == 4;
+    a.efin = k == 2;
+  } else {
+    const uint32_t k = c - F;
+    a.cls = k < 2 ? XT_CELL_SHOT : XT_CELL_MOVE;
+    a.snan = k == 0 || k == 2 || k == 3;
+    a.sfin = false;
+    a.succ = k >= 2 && (k & 1u);
+  }
+  return a;
+}
 
 __device__ __forceinline__ XtAct decode_cell(uint32_t c) {
   XtAct a;

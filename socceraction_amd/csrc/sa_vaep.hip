@@ -1301,11 +1301,20 @@ __device__ __forceinline__ void num_features_body(const FeatArgs& args, int64_t 
       // most d0 + 1.)
       if (!ATOMIC && args.xt_cells) {  // the raw (unflipped) rows jb, jb+1: xT cell codes
         uint32_t cc[2];
+        const bool c16 = xt_c16(args.xt_l * args.xt_w);
 #pragma unroll
         for (int e = 0; e < 2; ++e)
-          cc[e] = xt_cell_code((cand[e].ids >> 8) & 0xFF, (cand[e].ids >> 16) & 0xFF, cand[e].c0,
-                               cand[e].c1, cand[e].c2, cand[e].c3, args.xt_l, args.xt_w);
-        if (jb + 2 <= n) {
+          cc[e] = c16 ? xt_cell_code16((cand[e].ids >> 8) & 0xFF, (cand[e].ids >> 16) & 0xFF, cand[e].c0,
+                                       cand[e].c1, cand[e].c2, cand[e].c3, args.xt_l, args.xt_w)
+                      : xt_cell_code((cand[e].ids >> 8) & 0xFF, (cand[e].ids >> 16) & 0xFF, cand[e].c0,
+                                     cand[e].c1, cand[e].c2, cand[e].c3, args.xt_l, args.xt_w);
+        if (c16) {
+          uint16_t* c2 = reinterpret_cast<uint16_t*>(args.xt_cells);
+          if (jb + 2 <= n)
+            *reinterpret_cast<uint32_t*>(c2 + jb) = cc[0] | (cc[1] << 16);
+          else
+            c2[jb] = (uint16_t)cc[0];
+        } else if (jb + 2 <= n) {
           *reinterpret_cast<uint2*>(args.xt_cells + jb) = make_uint2(cc[0], cc[1]);
         } else {
           args.xt_cells[jb] = cc[0];
@@ -1398,8 +1407,14 @@ __device__ __forceinline__ void num_features_body(const FeatArgs& args, int64_t 
           const int64_t r = EXPLICIT ? jr[e] : jr[e] - (dd[e] < i ? dd[e] : i);
           load_row(Fi, r, ATOMIC, w, e);
           if (!ATOMIC && !EXPLICIT && i == 0 && args.xt_cells && jb + e < n)  // raw row jb+e
-            args.xt_cells[jb + e] = xt_cell_code(w.typ[e], w.res[e], w.c0[e], w.c1[e], w.c2[e],
-                                                 w.c3[e], args.xt_l, args.xt_w);
+          {
+            if (xt_c16(args.xt_l * args.xt_w))
+              reinterpret_cast<uint16_t*>(args.xt_cells)[jb + e] = (uint16_t)xt_cell_code16(
+                  w.typ[e], w.res[e], w.c0[e], w.c1[e], w.c2[e], w.c3[e], args.xt_l, args.xt_w);
+            else
+              args.xt_cells[jb + e] = xt_cell_code(w.typ[e], w.res[e], w.c0[e], w.c1[e], w.c2[e],
+                                                   w.c3[e], args.xt_l, args.xt_w);
+          }
           if (!EXPLICIT && away[e]) flip<ATOMIC>(w, e);
           if (i == 0) {
             sx0[e] = w.c0[e];

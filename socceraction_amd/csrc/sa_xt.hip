@@ -140,14 +140,15 @@ __global__ __launch_bounds__(XT_WIDE_THREADS) void xt_count_kernel(sa_actions A,
     XtAct act[XC_U];
     if (CELLS) {
       uint32_t cv[XC_U];
+      const bool c16 = xt_c16(C);
 #pragma unroll
       for (int u = 0; u < XC_U; ++u) {
         const int64_t j = j0 + u * stride < end ? j0 + u * stride : end - 1;
-        cv[u] = cells[j];
+        cv[u] = c16 ? (uint32_t)reinterpret_cast<const uint16_t*>(cells)[j] : cells[j];
       }
 #pragma unroll
       for (int u = 0; u < XC_U; ++u) {
-        act[u] = decode_cell(cv[u]);
+        act[u] = c16 ? decode_cell16(cv[u], C) : decode_cell(cv[u]);
         if (j0 + u * stride >= end) act[u].cls = 0;
       }
     } else {
@@ -211,15 +212,21 @@ __global__ __launch_bounds__(256) void xt_cells_kernel(sa_actions A, int l, int 
   if (j0 >= A.n) return;
   const sa_frame& F = A.frames[0];
   u32x4 v = {0, 0, 0, 0};
+  const bool c16 = xt_c16(l * w);
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int64_t j = j0 + q < A.n ? j0 + q : A.n - 1;
-    v[q] = xt_cell_code(F.type_id[j], F.result_id[j], F.c0[j], F.c1[j], F.c2[j], F.c3[j], l, w);
+    v[q] = c16 ? xt_cell_code16(F.type_id[j], F.result_id[j], F.c0[j], F.c1[j], F.c2[j], F.c3[j], l, w)
+               : xt_cell_code(F.type_id[j], F.result_id[j], F.c0[j], F.c1[j], F.c2[j], F.c3[j], l, w);
   }
-  if (j0 + 4 <= A.n)
+  if (c16) {
+    uint16_t* c2 = reinterpret_cast<uint16_t*>(cells);
+    for (int q = 0; j0 + q < A.n && q < 4; ++q) c2[j0 + q] = (uint16_t)v[q];
+  } else if (j0 + 4 <= A.n) {
     *reinterpret_cast<u32x4*>(cells + j0) = v;
-  else
+  } else {
     for (int q = 0; j0 + q < A.n; ++q) cells[j0 + q] = v[q];
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -933,8 +940,9 @@ __global__ __launch_bounds__(256) void xt_rate_cells_kernel(const uint32_t* __re
   const int64_t j0 = 4 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x);
   if (j0 >= n) return;
   int32_t bad = 0;
+  const bool c16 = xt_c16(C);
   auto one = [&](uint32_t c) -> double {
-    const XtAct a = decode_cell(c);
+    const XtAct a = c16 ? decode_cell16(c, C) : decode_cell(c);
     if (a.cls != XT_CELL_MOVE || !a.succ) return __builtin_nan("");
     if (!a.sfin || !a.efin) {
       bad = 4;  // the reference's int64 cast of a non-finite coordinate raises
@@ -943,6 +951,19 @@ __global__ __launch_bounds__(256) void xt_rate_cells_kernel(const uint32_t* __re
     SA_DGUARD(a.cs < C && a.ce < C, c, return __builtin_nan(""));
     return grid[a.ce] - grid[a.cs];
   };
+  if (c16) {
+    const uint16_t* c2 = reinterpret_cast<const uint16_t*>(cells);
+    if (j0 + 4 <= n) {
+      const uint2 q = *reinterpret_cast<const uint2*>(c2 + j0);
+      const f64x2 x = {one(q.x & 0xFFFFu), one(q.x >> 16)}, y = {one(q.y & 0xFFFFu), one(q.y >> 16)};
+      __builtin_nontemporal_store(x, reinterpret_cast<f64x2*>(out + j0));
+      __builtin_nontemporal_store(y, reinterpret_cast<f64x2*>(out + j0 + 2));
+    } else {
+      for (int64_t j = j0; j < n; ++j) out[j] = one(c2[j]);
+    }
+    if (bad && err) atomicOr(err, bad);
+    return;
+  }
   if (j0 + 4 <= n) {
     const u32x4 c = *reinterpret_cast<const u32x4*>(cells + j0);
     const f64x2 x = {one(c[0]), one(c[1])}, y = {one(c[2]), one(c[3])};

@@ -655,6 +655,14 @@ def xt_cells_buffer(n: int, dev) -> torch.Tensor:
     return torch.empty(max(_ld(n), 16), dtype=torch.int32, device=dev)
 
 
+def xt_cell_codes(cells: torch.Tensor, n: int, l: int, w: int) -> torch.Tensor:
+    """The n meaningful codes of a cell-code buffer: int16 (the 16-bit codes of grids of <=
+    SA_XT_CELLS16_MAX_C cells) or int32."""
+    if l * w <= _native.SA_XT_CELLS16_MAX_C:
+        return cells.view(torch.int16)[:n]
+    return cells[:n]
+
+
 def xt_cells(batch: ActionBatch, l: int, w: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """The xT cell code of every action (``sa_xt_cells``: the count pass's binning alone)."""
     out = xt_cells_buffer(batch.n, batch.device) if out is None else out

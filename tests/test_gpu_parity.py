@@ -519,7 +519,7 @@ def test_xt_cell_codes_match_coordinate_path(sa, l, w, games):
                                       ab.device, 1024, 128)
         c2 = ops.xt_cells_buffer(ab.n, ab.device)
         ops.features_into(ab.struct(), fb, xt_cells=(l, w, c2))
-        assert torch.equal(c2[:ab.n], cells[:ab.n]), k
+        assert torch.equal(ops.xt_cell_codes(c2, ab.n, l, w), ops.xt_cell_codes(cells, ab.n, l, w)), k
     ref = ops.xt_count(ab, l, w)
     for shared in (False, True):
         acc = ops.xt_count_cells(cells, ab.n, l, w, shared=shared)
@@ -667,7 +667,8 @@ def test_step_matches_separate_launches(sa, atomic):
                         assert torch.equal(getattr(lab, c)[:n], getattr(lref, c)[:n]), (bi, nr, k, c)
                     assert torch.equal(val[:, :n], vref[:, :n]), (bi, nr, k)
                     if xt:
-                        assert torch.equal(cells[:n], cells_ref[:n])
+                        assert torch.equal(ops.xt_cell_codes(cells, n, 16, 12),
+                                           ops.xt_cell_codes(cells_ref, n, 16, 12))
                     if k == 3:  # features + labels only (no probabilities): the cfg3 step
                         out2 = ops.alloc_feature_blocks(ref.plan, n, ab.device, Rb, Rn)
                         lab2, _ = ops.labels_formula(ab, ps, pc, nr_actions=nr)
@@ -750,7 +751,7 @@ def test_chunked_step_equals_step(sa):
         cells = ops.xt_cells_buffer(n, ab.device)
         ops.step_into(ab.struct(), view, ps, pc, 10, lab, val, xt_cells=(16, 12, cells), chunk_rows=chunk,
                       prefetch=pf)
-        outs.append((blk.f64_block.clone(), blk.i64_block.clone(), cells[:n].clone(),
+        outs.append((blk.f64_block.clone(), blk.i64_block.clone(), ops.xt_cell_codes(cells, n, 16, 12).clone(),
                      [getattr(lab, c)[:n].clone() for c in ('scores', 'concedes', 'goal_from_shot')],
                      val[:, :n].clone()))
     f0, i0, c0, l0, v0 = outs[0]
