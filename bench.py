@@ -67,11 +67,13 @@ KERNEL_NAMES = {'bool_features': 'bool_colgroup_kernel', 'num_features': 'num_fe
 def step_bytes(xt_source: str) -> dict:
     """Algorithmic bytes per action of each step entry for an xT source (bench xt_step)."""
     b = dict(BYTES)
-    if xt_source == 'cells':  # the f64 pass writes 4 B of cell code; count reads 4, rate 4 + 8
-        b['num_features'] += 4
-        b['num_features_nogs'] += 4
-        b['num_step'] += 4
-        b['xt_fit_rate'] = 4 + 4 + 8
+    if xt_source == 'cells':  # the f64 pass writes the cell code; count reads it, rate it + 8
+        from socceraction_amd import _native
+        cb = 2 if 16 * 12 <= _native.SA_XT_CELLS16_MAX_C else 4  # 16-bit codes on the 16 x 12 grid
+        b['num_features'] += cb
+        b['num_features_nogs'] += cb
+        b['num_step'] += cb
+        b['xt_fit_rate'] = cb + cb + 8
     elif xt_source == 'coords':  # count 34 B, rate 34 + 8
         b['xt_fit_rate'] = 34 + 34 + 8
     return b
