@@ -283,13 +283,12 @@ int sa_xt_count_codes(const sa_actions* a, int32_t l, int32_t w, int64_t* shot, 
  * (1 = shot, type 11; 2 = move: pass / dribble / cross), 26 result == success, 27 NaN in the
  * start coordinates, 28 start not finite, 29 end not finite.  cells: [n] u32, 16-byte aligned.
  * Grids of l * w <= SA_XT_CELLS16_MAX_C (202: the small-grid count; 16 x 12) take a 16-bit code
- * instead, 2 B per action in the first half of the same buffer: s * C + e for a successful move
- * with finite coordinates (s, e: start / end cell); C^2 + 2 s + goal for a shot with a finite
- * start; C^2 + k C + s for a move with a finite start that is unsuccessful (k = 2), has a
- * non-finite end and is unsuccessful (k = 3) or successful (k = 4); C^2 + 5 C + {0 shot with a
- * NaN start, 1 shot with an infinite start, 2 / 3 move with a NaN start unsuccessful /
- * successful, 4 / 5 move with an infinite start unsuccessful / successful}; 0xFFFF any other
- * action.  sa_xt_count_cells accumulates exactly what sa_xt_count does on those actions (same
+ * instead, 2 B per action in the first half of the same buffer: s << 8 | e for a successful move
+ * with finite coordinates (s, e: start / end cell); 51712 + 2 s + goal for a shot with a finite
+ * start; for a move with a finite start 52224 + s when unsuccessful, 52480 + s / 52736 + s with a
+ * non-finite end when unsuccessful / successful; 52992 + {0 shot with a NaN start, 1 shot with an
+ * infinite start, 2 / 3 move with a NaN start unsuccessful / successful, 4 / 5 move with an
+ * infinite start unsuccessful / successful}; 0xFFFF any other action.  sa_xt_count_cells accumulates exactly what sa_xt_count does on those actions (same
  * counts, same err_flags bits); sa_xt_rate_cells equals sa_xt_rate without interpolation (grid
  * = the (w, l) xT surface). */
 #define SA_XT_CELLS_MAX_C 4096

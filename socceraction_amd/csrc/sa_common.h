@@ -152,26 +152,34 @@ __device__ __forceinline__ uint32_t xt_cell_code(int t, int r, double sx, double
 #endif
 __host__ __device__ constexpr bool xt_c16(int C) { return SA_XT_CELLS16 && C <= SA_XT_CELLS16_MAX_C; }
 constexpr uint32_t XT_C16_NONE = 0xFFFFu;
+// ranges (C <= 202 < 256, so no division decodes them): successful move with finite
+// coordinates s << 8 | e; shot with a finite start XT_C16_SHOT + 2 s + goal; a move with a finite
+// start that is unsuccessful XT_C16_MISS + s, has a non-finite end XT_C16_EEND + s (unsuccessful)
+// or XT_C16_EEND_S + s (successful); XT_C16_SPEC + {0 shot NaN start, 1 shot infinite start,
+// 2 / 3 move NaN start unsuccessful / successful, 4 / 5 move infinite start unsuccessful /
+// successful}; XT_C16_NONE any other action
+constexpr uint32_t XT_C16_SHOT = 202u << 8, XT_C16_MISS = XT_C16_SHOT + 512u, XT_C16_EEND = XT_C16_MISS + 256u,
+                   XT_C16_EEND_S = XT_C16_EEND + 256u, XT_C16_SPEC = XT_C16_EEND_S + 256u;
+static_assert(XT_C16_SPEC + 6u < XT_C16_NONE, "16-bit cell code ranges");
 __device__ __forceinline__ uint32_t xt_cell_code16(int t, int r, double sx, double sy, double ex, double ey,
                                                    int l, int w) {
-  const int C = l * w;
   const bool shot = t == T_SHOT, mv = is_move(t), succ = r == R_SUCCESS;
   if (!shot && !mv) return XT_C16_NONE;
   const bool snan = isnan(sx) || isnan(sy), sfin = isfinite(sx) && isfinite(sy);
   const bool efin = isfinite(ex) && isfinite(ey);
-  const uint32_t CC = (uint32_t)C * C, F = CC + 5u * C;
   if (shot) {
-    if (snan) return F;
-    if (!sfin) return F + 1u;
-    return CC + 2u * (uint32_t)flat_index(sx, sy, l, w) + (succ ? 1u : 0u);
+    if (snan) return XT_C16_SPEC;
+    if (!sfin) return XT_C16_SPEC + 1u;
+    return XT_C16_SHOT + 2u * (uint32_t)flat_index(sx, sy, l, w) + (succ ? 1u : 0u);
   }
-  if (snan) return F + 2u + (succ ? 1u : 0u);
-  if (!sfin) return F + 4u + (succ ? 1u : 0u);
+  if (snan) return XT_C16_SPEC + 2u + (succ ? 1u : 0u);
+  if (!sfin) return XT_C16_SPEC + 4u + (succ ? 1u : 0u);
   const uint32_t cs = (uint32_t)flat_index(sx, sy, l, w);
-  if (!efin) return CC + (succ ? 4u : 3u) * C + cs;
-  if (!succ) return CC + 2u * C + cs;
-  return cs * C + (uint32_t)flat_index(ex, ey, l, w);
+  if (!efin) return (succ ? XT_C16_EEND_S : XT_C16_EEND) + cs;
+  if (!succ) return XT_C16_MISS + cs;
+  return (cs << 8) | (uint32_t)flat_index(ex, ey, l, w);
 }
+
 // ---- shared by the xT count passes (sa_xt.hip, sa_xt_large.hip) ----
 // Rate operand of one action for a later rate() on the same (l, w) grid, written by the count
 // pass so the rate pass reads 4 B instead of the 34 B of coordinates and ids again
@@ -213,36 +221,21 @@ struct XtAct {
   int cs, ce;              // start / end cell (valid when binned)
 };
 
+// branch-free (selects only: the codes of a wave are of every kind)
 __device__ __forceinline__ XtAct decode_cell16(uint32_t c, int C) {
+  (void)C;
+  const uint32_t dB = c - XT_C16_SHOT, dR = c - XT_C16_MISS, kS = c - XT_C16_SPEC;
+  const bool A = c < XT_C16_SHOT, Bq = c >= XT_C16_SHOT && c < XT_C16_MISS;
+  const bool R = c >= XT_C16_MISS && c < XT_C16_SPEC, S = c >= XT_C16_SPEC && c != XT_C16_NONE;
+  const uint32_t kR = dR >> 8;
   XtAct a;
-  a.cls = 0;
-  a.succ = a.snan = false;
-  a.sfin = a.efin = true;
-  a.cs = a.ce = 0;
-  const uint32_t CC = (uint32_t)C * C, F = CC + 5u * C;
-  if (c == XT_C16_NONE) return a;
-  if (c < CC) {
-    a.cls = XT_CELL_MOVE;
-    a.succ = true;
-    a.cs = (int)(c / (uint32_t)C);
-    a.ce = (int)(c - (uint32_t)a.cs * C);
-  } else if (c < CC + 2u * C) {
-    a.cls = XT_CELL_SHOT;
-    a.succ = (c - CC) & 1u;
-    a.cs = (int)((c - CC) >> 1);
-  } else if (c < F) {
-    const uint32_t k = (c - CC) / (uint32_t)C;  // 2: unsuccessful move, 3 / 4: non-finite end
-    a.cls = XT_CELL_MOVE;
-    a.cs = (int)(c - CC - k * C);
-    a.succ = k == 4;
-    a.efin = k == 2;
-  } else {
-    const uint32_t k = c - F;
-    a.cls = k < 2 ? XT_CELL_SHOT : XT_CELL_MOVE;
-    a.snan = k == 0 || k == 2 || k == 3;
-    a.sfin = false;
-    a.succ = k >= 2 && (k & 1u);
-  }
+  a.cls = (A || R || (S && kS >= 2u)) ? XT_CELL_MOVE : ((Bq || (S && kS < 2u)) ? XT_CELL_SHOT : 0u);
+  a.succ = A || (Bq && (dB & 1u)) || (R && kR == 2u) || (S && kS >= 2u && (kS & 1u));
+  a.snan = S && (kS == 0u || kS == 2u || kS == 3u);
+  a.sfin = !S;
+  a.efin = !(R && kR != 0u);
+  a.cs = A ? (int)(c >> 8) : (Bq ? (int)(dB >> 1) : (R ? (int)(dR & 0xFFu) : 0));
+  a.ce = A ? (int)(c & 0xFFu) : 0;
   return a;
 }
 

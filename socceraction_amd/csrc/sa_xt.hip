@@ -140,7 +140,7 @@ __global__ __launch_bounds__(XT_WIDE_THREADS) void xt_count_kernel(sa_actions A,
     XtAct act[XC_U];
     if (CELLS) {
       uint32_t cv[XC_U];
-      const bool c16 = xt_c16(C);
+      const bool c16 = xt_c16(C);  // 16-bit codes (grids of <= SA_XT_CELLS16_MAX_C cells)
 #pragma unroll
       for (int u = 0; u < XC_U; ++u) {
         const int64_t j = j0 + u * stride < end ? j0 + u * stride : end - 1;
