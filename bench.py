@@ -423,7 +423,8 @@ def _events_ms(fn, reps: int) -> float:
     return a.elapsed_time(b) / reps
 
 
-def atomic_extra(dist, rank, world, dev, games: int, reps: int = 21, check: bool = True) -> dict:
+def atomic_extra(dist, rank, world, dev, games: int, reps: int = 21, check: bool = True,
+                 contiguous='require') -> dict:
     """BASELINE cfg3 alongside the main line: Atomic-VAEP features (k=3, default xfns, 154
     columns) + labels of cfg3's ``games`` synthetic atomic games (10,000 ≈ 4.0e7 atomic
     actions), sharded by game over the ranks (this entry scales strongly)."""
@@ -438,7 +439,7 @@ def atomic_extra(dist, rank, world, dev, games: int, reps: int = 21, check: bool
     plan = catalog.build_plan(ATOMIC_DEFAULT, 3, True)
     torch.cuda.empty_cache()  # cached blocks of earlier entries out of the way of the range
     # 'require': no silent fall-back to the caching allocator (the line says which served it)
-    out = ops.alloc_feature_blocks(plan, ab.n, dev, 1024, 128, contiguous='require')
+    out = ops.alloc_feature_blocks(plan, ab.n, dev, 1024, 128, contiguous=contiguous)
     ops.features(ab, ATOMIC_DEFAULT, 3, out=out, bool_tile=1024, num_tile=128)
     lab = ops.labels(ab)
 

@@ -1,0 +1,14 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+run() {  # tag, args...
+  t=$1; shift
+  timeout -k 10 300 python -u scripts/cfg3_time.py --times 3 "$@" > gpurun_out/r05aw_$t.json 2> gpurun_out/r05aw_$t.err || exit $?
+  cat gpurun_out/r05aw_$t.json
+}
+run req1 --contiguous require
+run all1 --contiguous all
+run pre512 --contiguous require --pre-mb 512
+run pre1536 --contiguous require --pre-mb 1536
+run req2 --contiguous require
+run all2 --contiguous all

@@ -151,6 +151,7 @@ def alloc_feature_blocks(plan: FeaturePlan, n: int, dev, bool_tile: Optional[int
                                 arena.tensor(fshape, torch.float64, al(sizes[0])),
                                 arena.tensor(ishape, torch.int64, al(sizes[0]) + al(sizes[1])))
             out._arena = arena
+            out.bool_alloc = 'contiguous-all'
             return out
     arena = None
     if contiguous and plan.n_bool:
