@@ -394,6 +394,9 @@ def _record(stream, kind: str = None):
     return e
 
 
+_LAST_TIMES: list = []
+
+
 def _events_median_ms(fn, reps: int) -> Tuple[float, float, float]:
     """(median, min, max) ms of ``reps`` back-to-back calls of ``fn``, one HIP event pair per
     call on the current stream, after one untimed call."""
@@ -407,6 +410,7 @@ def _events_median_ms(fn, reps: int) -> Tuple[float, float, float]:
         b.record()
     torch.cuda.synchronize()
     t = [a.elapsed_time(b) for a, b in ev]
+    _LAST_TIMES[:] = t  # the per-call series of the last call (scripts/cfg3_time.py)
     return float(np.median(t)), float(np.min(t)), float(np.max(t))
 
 
@@ -424,14 +428,14 @@ def _events_ms(fn, reps: int) -> float:
 
 
 def atomic_extra(dist, rank, world, dev, games: int, reps: int = 21, check: bool = True,
-                 contiguous='require') -> dict:
+                 contiguous='require', batch_contiguous: bool = False) -> dict:
     """BASELINE cfg3 alongside the main line: Atomic-VAEP features (k=3, default xfns, 154
     columns) + labels of cfg3's ``games`` synthetic atomic games (10,000 ≈ 4.0e7 atomic
     actions), sharded by game over the ranks (this entry scales strongly)."""
     mine = games // world + (1 if rank < games % world else 0)
     first = rank * (games // world) + min(rank, games % world)
     d = synthetic.atomic_games(mine, game_id0=first)
-    ab = B.ActionBatch.from_columns(d, atomic=True, dev=dev)
+    ab = B.ActionBatch.from_columns(d, atomic=True, dev=dev, contiguous=batch_contiguous)
     # the bool block in physically contiguous VRAM, as the main step's (DESIGN §2: the bool
     # pass is sensitive to its address translations; from the caching allocator its time
     # followed the allocations placed before it: 3.80 vs 3.41 - 3.43 ms per step on one box,

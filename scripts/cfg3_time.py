@@ -6,6 +6,7 @@ import json
 import os
 import sys
 
+import numpy as np
 import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -20,6 +21,10 @@ def main():
     ap.add_argument('--times', type=int, default=3)
     ap.add_argument('--after-step', action='store_true')
     ap.add_argument('--contiguous', default='require')
+    ap.add_argument('--batch-contiguous', action='store_true')
+    ap.add_argument('--reps', type=int, default=21)
+    ap.add_argument('--warm-games', type=int, default=0,
+                    help='one untimed cfg3 pass of this many games before the timed runs')
     ap.add_argument('--pre-mb', type=int, default=0,
                     help='a contiguous dummy range of this size held before the first run')
     args = ap.parse_args()
@@ -47,11 +52,18 @@ def main():
                                        contiguous=True)
         keep += [ab, out]
     res = []
-    for _ in range(args.times):
-        r = bench.atomic_extra(None, 0, 1, dev, 10000, check=False, contiguous=args.contiguous)
-        res.append((r['ms_per_step'], r['bool_block'], r['timing'], addrs[-1]))
+    if args.warm_games:
+        bench.atomic_extra(None, 0, 1, dev, args.warm_games, check=False, contiguous=args.contiguous)
         torch.cuda.empty_cache()
-    print(json.dumps({'after_step': args.after_step, 'contiguous': args.contiguous, 'pre_mb': args.pre_mb,
+    for _ in range(args.times):
+        r = bench.atomic_extra(None, 0, 1, dev, 10000, check=False, contiguous=args.contiguous,
+                               batch_contiguous=args.batch_contiguous, reps=args.reps)
+        series = [round(x, 3) for x in bench._LAST_TIMES]
+        res.append((r['ms_per_step'], r['bool_block'], r['timing'], addrs[-1],
+                    [float(np.median(series[i:i + 10])) for i in range(0, len(series), 10)]))
+        torch.cuda.empty_cache()
+    print(json.dumps({'after_step': args.after_step, 'contiguous': args.contiguous, 'pre_mb': args.pre_mb, 'warm_games': args.warm_games,
+                      'batch_contiguous': args.batch_contiguous,
                       'runs': res}), flush=True)
 
 

@@ -115,7 +115,8 @@ class ActionBatch:
     """Device-resident columns of one frame of actions (see module docstring)."""
 
     def __init__(self, cols: Dict[str, np.ndarray], seg_off: np.ndarray,
-                 home: Optional[np.ndarray], atomic: bool, dev: Optional[torch.device] = None):
+                 home: Optional[np.ndarray], atomic: bool, dev: Optional[torch.device] = None,
+                 contiguous: bool = False):
         dev = dev or device()
         self.atomic = bool(atomic)
         self.n = int(len(cols['type_id']))
@@ -135,7 +136,14 @@ class ActionBatch:
         host = np.zeros(total, dtype=np.uint8)
         for k, a in arrays.items():
             host[offsets[k]:offsets[k] + a.nbytes] = a.view(np.uint8).reshape(-1)
-        self.buffer = torch.from_numpy(host).to(dev)
+        self._dbuf = None
+        if contiguous:  # one physically contiguous range (``ops.DeviceBuffer``), raises if none
+            from .ops import DeviceBuffer
+            self._dbuf = DeviceBuffer(total, contiguous=True)
+            self.buffer = self._dbuf.tensor((total,), torch.uint8)
+            self.buffer.copy_(torch.from_numpy(host))
+        else:
+            self.buffer = torch.from_numpy(host).to(dev)
         self.cols: Dict[str, torch.Tensor] = {}
         for k, a in arrays.items():
             o = offsets[k]
@@ -182,8 +190,9 @@ class ActionBatch:
 
     @classmethod
     def from_columns(cls, d: Dict[str, np.ndarray], *, atomic: bool = False,
-                     flip: bool = True, dev=None) -> 'ActionBatch':
-        """From the flat numpy columns of :mod:`socceraction_amd.synthetic`."""
+                     flip: bool = True, dev=None, contiguous: bool = False) -> 'ActionBatch':
+        """From the flat numpy columns of :mod:`socceraction_amd.synthetic` (``contiguous``:
+        the device buffer in physically contiguous VRAM, see ``ActionBatch.__init__``)."""
         f64 = F64_COLS_ATOMIC if atomic else F64_COLS_SPADL
         cols = {f'c{i}': np.asarray(d[c], dtype=np.float64) for i, c in enumerate(f64)}
         cols['time_seconds'] = np.asarray(d['time_seconds'], dtype=np.float64)
@@ -195,7 +204,7 @@ class ActionBatch:
         team, home = encode_teams(d['team_id'], d['home_team_id'])
         cols['team'] = team
         return cls(cols, np.asarray(d['game_off'], dtype=np.int64), home if flip else None,
-                   atomic, dev)
+                   atomic, dev, contiguous)
 
     @classmethod
     def from_device(cls, cols: Dict[str, torch.Tensor], n: int, seg_off: torch.Tensor,

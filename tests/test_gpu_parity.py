@@ -721,6 +721,25 @@ def test_contiguous_bool_block_matches(sa):
     assert float(t.sum()) == 2.0 * 256 * 1024
 
 
+def test_contiguous_action_batch_matches(sa):
+    """An ActionBatch whose device buffer is one physically contiguous range holds the same
+    bytes, and the features and the whole 'all' block arena computed from it are equal."""
+    B, ops, syn = sa['batch'], sa['ops'], sa['synthetic']
+    d = syn.atomic_games(20, seed=6)
+    ref = B.ActionBatch.from_columns(d, atomic=True)
+    got = B.ActionBatch.from_columns(d, atomic=True, contiguous=True)
+    assert got._dbuf is not None and got.buffer.data_ptr() == got._dbuf.ptr
+    assert torch.equal(got.buffer, ref.buffer)
+    plan = ops.build_plan(vo.ATOMIC_DEFAULT, 3, True)
+    a = ops.alloc_feature_blocks(plan, ref.n, ref.device, 1024, 128)
+    b = ops.alloc_feature_blocks(plan, got.n, got.device, 1024, 128, contiguous='all')
+    assert b.bool_alloc in ('contiguous-all', 'caching')
+    ops.features_into(ref.struct(), a)
+    ops.features_into(got.struct(), b)
+    for x, y in zip(a.to_numpy(), b.to_numpy()):
+        np.testing.assert_array_equal(x, y)
+
+
 def test_chunked_step_equals_step(sa):
     """sa_vaep_step_f64_chunked (the numeric step pass in launches of whole 512-row blocks, each
     optionally after a pure-read pass over its inputs; bench.py's --ab probe of the pass's read /
