@@ -50,6 +50,9 @@ constexpr int XK_THREADS = SA_XK_THREADS;
 #define SA_XK_U 4  // K1 actions per thread per pass (coordinates; even)
 #endif
 static_assert(SA_XK_U >= 2 && SA_XK_U % 2 == 0 && SA_XK_U <= 16, "SA_XK_U");
+#ifndef SA_XK_BALANCE
+#define SA_XK_BALANCE 1  // K1 regions per batch rounded up to whole rounds of the CUs (shorter regions)
+#endif
 #ifndef SA_XK_NT
 #define SA_XK_NT 3  // bit 0: non-temporal coordinate / id loads in K1, bit 1: non-temporal operand stores
                     // (read once per fit; cfg5 batch 0.263 -> 0.251 ms, profiles/r04_xt_count_ab.md)
@@ -164,15 +167,16 @@ __global__ __launch_bounds__(XK_THREADS) void xt_keys_kernel(sa_actions A, const
                                                              uint32_t* __restrict__ keys,
                                                              uint32_t* __restrict__ region_cnt,
                                                              uint32_t* __restrict__ band_cnt,
-                                                             int32_t* __restrict__ err, XkRate RO, int vec) {
+                                                             int32_t* __restrict__ err, XkRate RO, int vec,
+                                                             int64_t chunk) {
   extern __shared__ uint32_t bh[];  // [NB]
   __shared__ uint32_t cursor;
   for (int b = threadIdx.x; b < S.NB; b += XK_THREADS) bh[b] = 0;
   if (threadIdx.x == 0) cursor = 0;
   __syncthreads();
-  const int64_t begin = (int64_t)blockIdx.x * XK_CHUNK;
-  const int64_t end = min(n, begin + XK_CHUNK);
-  uint32_t* out = keys + begin;
+  const int64_t begin = (int64_t)blockIdx.x * chunk;  // chunk <= XK_CHUNK, even
+  const int64_t end = min(n, begin + chunk);
+  uint32_t* out = keys + (int64_t)blockIdx.x * XK_CHUNK;
   const sa_frame& F = A.frames[0];
   const int lane = threadIdx.x & 63;
   int32_t bad = 0;
@@ -1478,7 +1482,17 @@ static bool xt_band_shape(int C, XbShape* s) {
 // K1 -> K2 -> K3 of one batch: its keys sorted into buckets[] by band, band_off[NB + 1].
 static int bucket_batch(const sa_actions& A, const uint32_t* cells, int64_t n, int l, int w, const XbShape& S,
                         uint32_t* buckets, int64_t* band_off, int32_t* err, const XkRate& RO, hipStream_t st) {
-  const int64_t regions = (n + XK_CHUNK - 1) / XK_CHUNK;
+  // K1 runs one workgroup per CU: a batch's regions in whole rounds of the CUs (16M actions:
+  // 489 regions of 32768 -> 512 of 31,488; a 4M tail: 123 -> 256), regions of >= 4096 actions
+  int64_t regions = (n + XK_CHUNK - 1) / XK_CHUNK, chunk = XK_CHUNK;
+  if (SA_XK_BALANCE && n > 0) {
+    const int64_t G = device_cus(current_device());
+    const int64_t r = (regions + G - 1) / G * G;
+    chunk = ((n + r - 1) / r + 255) & ~(int64_t)255;
+    if (chunk < 4096) chunk = 4096;
+    if (chunk > XK_CHUNK) chunk = XK_CHUNK;
+    regions = (n + chunk - 1) / chunk;
+  }
   // scratch: band_cnt [NB] | cursor [NB] | region_cnt [regions] | keys [regions * XK_CHUNK], each
   // part on 256-B boundaries: the band counts and cursors are zeroed by ONE aligned fill (an
   // unaligned start split it into three fill kernels, ~9 us more per batch)
@@ -1502,10 +1516,10 @@ static int bucket_batch(const sa_actions& A, const uint32_t* cells, int64_t n, i
                     ((uintptr_t)F.type_id & 1u) == 0 && ((uintptr_t)F.result_id & 1u) == 0;
     if (cells)
       hipLaunchKernelGGL((xt_keys_kernel<true>), dim3((unsigned)regions), dim3(XK_THREADS), (size_t)S.NB * 4, st, none,
-                         cells, n, l, w, S, keys, region_cnt, band_cnt, err, XkRate{nullptr, nullptr, 0, 0}, 0);
+                         cells, n, l, w, S, keys, region_cnt, band_cnt, err, XkRate{nullptr, nullptr, 0, 0}, 0, chunk);
     else
       hipLaunchKernelGGL((xt_keys_kernel<false>), dim3((unsigned)regions), dim3(XK_THREADS), (size_t)S.NB * 4, st, A,
-                         nullptr, n, l, w, S, keys, region_cnt, band_cnt, err, RO, vec);
+                         nullptr, n, l, w, S, keys, region_cnt, band_cnt, err, RO, vec, chunk);
     rc = check_launch("xt_keys_kernel");
   }
   if (!rc) {
