@@ -336,7 +336,11 @@ def check_xt(par: Parity, cnt: dict, acc, xT_dev, n_iter: int, l: int, w: int,
     tag = f'xT {l}x{w}'
     for k, t in (('shot', acc.shot), ('goal', acc.goal), ('move', acc.move)):
         par.exact(f'{tag} {k} counts', t.cpu().numpy(), cnt[k].reshape(-1))
-    tr = acc.trans.cpu().numpy().astype(np.int64)
+    # the counts the solve read: the compact rows when the count wrote them (cfg5 writes no
+    # dense table on one rank), else the dense table
+    idx, tc = ops.xt_transition_entries(acc)
+    tr = np.zeros(l * w * l * w, np.int64)
+    tr[idx.cpu().numpy()] = tc.cpu().numpy()
     par.exact(f'{tag} transition counts', tr, cnt['trans'].reshape(-1))
     fit = xo.solve(cnt, l, w)
     par.exact(f'{tag} iterations', n_iter + 1, len(fit['heatmaps']))
@@ -528,7 +532,9 @@ def xt105_extra(ab, dist, dev, sharded: bool = False, cfg5_games: int = 62500,
             acc = None  # each rank holds only its row block of the transition counts
             path[0] = xstats.get('solve_path', 'sequential')
         else:  # one all-reduce of the counts, replicated solve
-            acc = ops.xt_count_many(batches, l, w, interp_codes=icodes)
+            # one rank: the compact count rows alone (the solve reads nothing else; no 204 MB
+            # dense flush); replicated over ranks: the dense table the all-reduce sums
+            acc = ops.xt_count_many(batches, l, w, interp_codes=icodes, dense=dist is not None)
             mark()
             allreduce_counts(dist, acc)
             mark()

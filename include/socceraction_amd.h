@@ -354,7 +354,13 @@ int sa_xt_count_from_buckets(int32_t nsets, const uint32_t* const* buckets,
  * sa_xt_compact_rows (ell [C * sa_xt_compact_bytes(C, 1) / 4] u32, 16-byte aligned; row_len [C]),
  * straight from the bins: the large-grid solve (sa_xt_solve_ex with ell / row_len) then skips
  * its own build pass over the dense table.  Needs SA_XT_COUNT_OVERWRITE, at most 24 bucket sets
- * and 1025 <= C <= 9472; ell = row_len = NULL is sa_xt_count_from_buckets. */
+ * and 1025 <= C <= 9472; ell = row_len = NULL is sa_xt_count_from_buckets.
+ * flags | SA_XT_COUNT_COMPACT_ONLY (with ell): the dense C x C rows of `trans` are written only
+ * for the bands (sa_xt_band_shape's rows per band) that hold a transition count >= 65535 -- the
+ * only dense entries the compact solve reads; the other rows are left as they were.  shot / goal
+ * / move, ell and row_len are written in full.  (A fit that reads only the compact rows: no
+ * 4 C^2-byte flush, 204 MB at 105 x 68.) */
+#define SA_XT_COUNT_COMPACT_ONLY 4
 int sa_xt_count_from_buckets_ex(int32_t nsets, const uint32_t* const* buckets,
                                 const int64_t* const* band_off, int32_t l, int32_t w,
                                 int64_t* shot, int64_t* goal, int64_t* move, int32_t* trans,
@@ -392,6 +398,8 @@ int sa_xt_solve(const int64_t* shot, const int64_t* goal, const int64_t* move,
 #define SA_XT_PATH_REORDERED 1    /* reordered sums, every decision outside the error bound */
 #define SA_XT_PATH_INSIDE_BOUND 2 /* reordered, a decision inside the bound: re-solved in order */
 #define SA_XT_PATH_UNAVAILABLE 3  /* reordered solve not launchable here: solved in order */
+#define SA_XT_PATH_TIMEOUT 4      /* the reordered solve's grid barrier timed out (another grid held
+                                     CUs: 50 ms at the first barrier, 1 s later): solved in order */
 int sa_xt_solve_ex(const int64_t* shot, const int64_t* goal, const int64_t* move,
                    const int32_t* trans, int32_t l, int32_t w, double eps, int32_t max_iter,
                    int32_t flags, double* mats, double* trans_t, double* heatmaps, int32_t* n_iter,
@@ -703,6 +711,11 @@ int sa_event_elapsed(void* start, void* end, float* ms);
  * SA_EDATA with the source location in sa_last_error() if any check failed since the last
  * call (always SA_OK in the default build); sa_debug_enabled() tells the builds apart. */
 int sa_debug_check(void);
+/* Debug build only (SA_EINVAL otherwise): the next large-grid reordered solves have their last
+ * workgroup leave at iteration `iteration` without arriving at the grid barrier, so the others
+ * time out and the solve takes its barrier-timeout exit (SA_XT_PATH_TIMEOUT) -- the fallback a
+ * GPU shared with another persistent grid takes.  -1 switches it off. */
+int sa_debug_xt_solve_abort(int32_t iteration);
 int sa_debug_enabled(void);
 
 #ifdef __cplusplus

@@ -23,12 +23,12 @@ SA_MAX_FRAMES = 8
 SA_SEG_BLOCK = 128  # rows per entry of sa_actions.seg_of_block
 SA_XT_SOLVE_MAX_C = 1024  # sa_xt_solve: larger grids may pass trans_t = NULL
 SA_XT_CELLS_MAX_C = 4096
-SA_XT_COUNT_SHARED, SA_XT_COUNT_OVERWRITE = 1, 2
+SA_XT_COUNT_SHARED, SA_XT_COUNT_OVERWRITE, SA_XT_COUNT_COMPACT_ONLY = 1, 2, 4
 SA_XT_CELLS16_MAX_C = 202  # xT cell codes: 16 bits per action up to this many cells
 SA_XT_COMPACT_MAX_C = 9472  # sa_xt_compact_rows / sa_xt_iterate_compact
 SA_XT_SOLVE_EXACT = 1  # sa_xt_solve_ex / sa_xt_solve_compact: the reference's summation order
 # which path produced a large-grid solve (sa_xt_solve_ex's *path)
-XT_SOLVE_PATHS = ('sequential', 'reordered', 'inside-bound', 'unavailable')
+XT_SOLVE_PATHS = ('sequential', 'reordered', 'inside-bound', 'unavailable', 'timeout')
 SA_BOOL_TILE_QUANTUM = 1024
 SA_NUM_TILE_QUANTUM = 128
 SA_OK, SA_EINVAL, SA_EHIP, SA_EDATA, SA_ENOMEM = 0, -1, -2, -3, -4
@@ -244,6 +244,7 @@ _SIGNATURES = {
     'sa_build_id': (ctypes.c_char_p, []),
     'sa_debug_enabled': (ctypes.c_int, []),
     'sa_debug_check': (ctypes.c_int, []),
+    'sa_debug_xt_solve_abort': (ctypes.c_int, [ctypes.c_int32]),
     'sa_shutdown': (ctypes.c_int, []),
 }
 EXPORTED_SYMBOLS = tuple(_SIGNATURES)

@@ -80,10 +80,13 @@ __device__ __forceinline__ uint32_t ld_u8x4(const uint8_t* __restrict__ p, int64
 // -------------------------------------------------------------------------------------
 // xT binning (reference xthreat.py:25-37): numpy float64 -> int64 cast (x86 cvttsd2si: NaN /
 // out of range -> INT64_MIN), then clip; (x / 105) * l in f64, divide THEN multiply.
+// The cast + clip without the int64 conversion (gfx950 has none: ~10 f64 instructions per cast,
+// most of K1's VALU time): NaN and v >= 2^63 cast to INT64_MIN (cell 0), every other v clips to
+// [0, l - 1] before the truncation -- trunc(min(max(v, 0), l - 1)) == clip(trunc(v), 0, l - 1),
+// incl. v < -2^63 (INT64_MIN -> 0) -- so one v_cvt_i32_f64 of a value in [0, l - 1] remains.
 __device__ __forceinline__ int cell_index(double v, int l) {
-  long long c = (v >= -9.2233720368547758e18 && v < 9.2233720368547758e18) ? (long long)v
-                                                                             : (long long)INT64_MIN;
-  return c < 0 ? 0 : (c > l - 1 ? l - 1 : (int)c);
+  const bool inr = v < 9.2233720368547758e18;  // false for NaN
+  return inr ? (int)__builtin_fmin(__builtin_fmax(v, 0.0), (double)(l - 1)) : 0;
 }
 
 __device__ __forceinline__ int flat_index(double x, double y, int l, int w) {

@@ -138,6 +138,8 @@ __device__ __forceinline__ bool band_key(const XtAct& a, int C, uint32_t& key, i
   } else {
     return false;
   }
+  // only a malformed cell code fails these: never an LDS bin past the bands or a band row
+  if ((uint32_t)a.cs >= (uint32_t)C || slot > (uint32_t)C + 2u) return false;
   key = ((uint32_t)a.cs << 16) | slot;
   return true;
 }
@@ -185,14 +187,15 @@ __global__ __launch_bounds__(XK_THREADS) void xt_keys_kernel(sa_actions A, const
     XtAct act[U];
     if (CELLS) {
       uint32_t cv[U];
+      const bool c16 = xt_c16(S.C);  // 16-bit codes (grids of <= SA_XT_CELLS16_MAX_C cells), as xt_count_kernel
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int64_t j = base + u * XK_THREADS + threadIdx.x;
-        cv[u] = cells[j < end ? j : end - 1];
+        const int64_t j = base + u * XK_THREADS + threadIdx.x, jc = j < end ? j : end - 1;
+        cv[u] = c16 ? (uint32_t)reinterpret_cast<const uint16_t*>(cells)[jc] : cells[jc];
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        act[u] = decode_cell(cv[u]);
+        act[u] = c16 ? decode_cell16(cv[u], S.C) : decode_cell(cv[u]);
         if (base + u * XK_THREADS + threadIdx.x >= end) act[u].cls = 0;
       }
     } else {
@@ -477,7 +480,11 @@ __device__ __forceinline__ void xe_emit_tail(uint32_t* __restrict__ E, const uin
 
 // ell (optional, with overwrite): the band's rows also in the compact form of
 // xt_ell_build_kernel, emitted from the bins (ell + row * pe, row_len[row]) -- the solve then
-// skips its build pass and its 204 MB read of the table.
+// skips its build pass and its 204 MB read of the table.  dense = 0 (with ell): the dense rows
+// are written only for a band that holds a transition count >= 65535 (the one entry the compact
+// form escapes to its dense row); every other band's dense rows stay unwritten -- 204 MB of
+// stores a fit that reads only the compact rows does not need (sa_xt_count_from_buckets_ex
+// with SA_XT_COUNT_COMPACT_ONLY).
 __device__ __forceinline__ int xe_slot(int k);
 __global__ __launch_bounds__(XB_THREADS) void xt_band_count_kernel(XbSets sets, XbShape S, int band0,
                                                                    unsigned long long* __restrict__ shot,
@@ -485,14 +492,17 @@ __global__ __launch_bounds__(XB_THREADS) void xt_band_count_kernel(XbSets sets, 
                                                                    unsigned long long* __restrict__ move,
                                                                    int32_t* __restrict__ trans, int overwrite,
                                                                    int vec, uint32_t* __restrict__ ell,
-                                                                   int32_t* __restrict__ row_len, int pe) {
+                                                                   int32_t* __restrict__ row_len, int pe,
+                                                                   int dense) {
   extern __shared__ __attribute__((aligned(16))) uint32_t h[];  // [R][P]
   __shared__ unsigned long long msum[XB_MAX_ROWS];
+  __shared__ uint32_t esc;  // dense = 0: the band holds a transition count >= 65535
   const int lb = blockIdx.x, b = band0 + lb, C = S.C, P = S.P;
   const int r0 = b * S.R, nr = min(S.R, C - r0);
   const int orow = r0 - band0 * S.R;  // the band's first row in the outputs
   for (int e = 4 * threadIdx.x; e < nr * P; e += 4 * XB_THREADS) *reinterpret_cast<u32x4*>(h + e) = u32x4{0, 0, 0, 0};
   if (threadIdx.x < XB_MAX_ROWS) msum[threadIdx.x] = 0;
+  if (threadIdx.x == 0) esc = 0;
   // the band's keys, set after set, in tiles of XB_U keys per thread, two tiles in flight (the
   // next tile's loads are issued before the current tile's LDS atomics; one tile at a time
   // waited out a memory latency per 4 keys and per set: 148 us per cfg5 table pass).  Set
@@ -576,11 +586,24 @@ __global__ __launch_bounds__(XB_THREADS) void xt_band_count_kernel(XbSets sets, 
   const int f0 = ell ? 64 * nr : 0, fth = XB_THREADS - f0;
   if ((int)threadIdx.x >= f0) {
     const int ft = threadIdx.x - f0;
+    uint32_t big = 0;  // dense = 0: the largest transition count this thread saw
     for (int i = 0; i < nr; ++i) {
       const uint32_t* hr = h + i * P;
       int32_t* dst = trans + (int64_t)(orow + i) * C;
       unsigned long long ms = 0;
-      if (vec) {  // C % 4 == 0 and trans 16-byte aligned: every row starts 16-byte aligned
+      if (!dense) {  // the row sums (and the escape test) only: no dense stores
+        if (vec)
+          for (int c = 4 * ft; c < C; c += 4 * fth) {
+            const u32x4 v = *reinterpret_cast<const u32x4*>(hr + c);
+            ms += (unsigned long long)v[0] + v[1] + v[2] + v[3];
+            big = max(big, max(max(v[0], v[1]), max(v[2], v[3])));
+          }
+        else
+          for (int c = ft; c < C; c += fth) {
+            ms += hr[c];
+            big = max(big, hr[c]);
+          }
+      } else if (vec) {  // C % 4 == 0 and trans 16-byte aligned: every row starts 16-byte aligned
         for (int c = 4 * ft; c < C; c += 4 * fth) {
           const u32x4 v = *reinterpret_cast<const u32x4*>(hr + c);
           ms += (unsigned long long)v[0] + v[1] + v[2] + v[3];
@@ -602,6 +625,7 @@ __global__ __launch_bounds__(XB_THREADS) void xt_band_count_kernel(XbSets sets, 
       for (int d = 32; d >= 1; d >>= 1) ms += __shfl_xor(ms, d);
       if (lane == 0 && ms) atomicAdd(&msum[i], ms);
     }
+    if (big >= XE_CNT_ESC_K4) esc = 1u;  // benign race: every writer stores 1
   } else {  // ell: wave i emits row i (xe_emit_group)
     __shared__ uint32_t ring[XB_MAX_ROWS][256];
     const int i = threadIdx.x >> 6;
@@ -621,6 +645,13 @@ __global__ __launch_bounds__(XB_THREADS) void xt_band_count_kernel(XbSets sets, 
     if (lane == 0) row_len[orow + i] = base;
   }
   __syncthreads();
+  if (!dense && esc) {  // workgroup-uniform: an escaped count's dense row is read by the solve
+    for (int i = 0; i < nr; ++i) {  // (dense = 0 comes with ell, so with overwrite)
+      const uint32_t* hr = h + i * P;
+      int32_t* dst = trans + (int64_t)(orow + i) * C;
+      for (int c = threadIdx.x; c < C; c += XB_THREADS) dst[c] = (int32_t)hr[c];
+    }
+  }
   if (threadIdx.x < nr) {
     const int i = threadIdx.x, r = orow + i;
     const uint32_t* hr = h + i * P;
@@ -1216,7 +1247,8 @@ __device__ __forceinline__ double xf_group(const u32x4 (&e)[XF_G], const double*
 __global__ __launch_bounds__(XF_THREADS) void xt_solve_reordered_kernel(
     const uint32_t* __restrict__ ell, const int32_t* __restrict__ row_len, const unsigned long long* __restrict__ move,
     const double* __restrict__ gs, const double* __restrict__ pmove, int C, int hp, double eps, int max_iter,
-    int pmax, int kov, double* xb, double* __restrict__ heat, double* __restrict__ xt_out, int32_t* ctrl) {
+    int pmax, int kov, double* xb, double* __restrict__ heat, double* __restrict__ xt_out, int32_t* ctrl,
+    int force_abort) {
   // LDS: ov [XF_HALVES][kov] units | xs [C] x_t | part [pmax] unit sums | luo [pmax + 1]
   extern __shared__ __attribute__((aligned(16))) u32x4 xf_lds[];
   u32x4* ov = xf_lds;
@@ -1402,6 +1434,13 @@ __global__ __launch_bounds__(XF_THREADS) void xt_solve_reordered_kernel(
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its stores
     const int any_up = __syncthreads_or(up), any_amb = __syncthreads_or(amb);
     tick(3);
+#if SA_DEBUG
+    // sa_debug_xt_solve_abort: the last workgroup leaves without arriving (workgroup-uniform),
+    // as if it never got a CU; the others' bounded polls time out and take the abort exit
+    if (it == force_abort && g == G - 1) return;
+#else
+    (void)force_abort;
+#endif
     if (t == 0) {  // ---- grid barrier, XCD-hierarchical; one lane per workgroup
       if (any_up) __hip_atomic_fetch_or((xf_gu32*)(ctrl + XF_FLAGS + it), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (any_amb) __hip_atomic_fetch_or((xf_gu32*)(ctrl + XF_AMB), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1535,10 +1574,11 @@ static int bucket_batch(const sa_actions& A, const uint32_t* cells, int64_t n, i
 static int count_from_buckets(int nsets, const uint32_t* const* buckets, const int64_t* const* band_off,
                               const XbShape& S, int band0, int nbands, int64_t* shot, int64_t* goal, int64_t* move,
                               int32_t* trans, int overwrite, hipStream_t st, uint32_t* ell = nullptr,
-                              int32_t* row_len = nullptr) {
+                              int32_t* row_len = nullptr, int dense = 1) {
   if (nbands <= 0) return SA_OK;
   // the compact rows come from the bins only when one launch writes the final counts
   if (ell && (!overwrite || nsets > XB_MAX_SETS)) return fail(SA_EINVAL, "compact rows need one overwriting launch");
+  if (!dense && !ell) return fail(SA_EINVAL, "the dense rows may be skipped only beside the compact rows");
   const int vec = (S.C % 4 == 0) && aligned16(trans);
   const size_t lds = (size_t)S.R * S.P * 4;
   for (int s0 = 0; s0 < nsets || (s0 == 0 && nsets == 0); s0 += XB_MAX_SETS) {
@@ -1553,7 +1593,7 @@ static int count_from_buckets(int nsets, const uint32_t* const* buckets, const i
     hipLaunchKernelGGL(xt_band_count_kernel, dim3((unsigned)nbands), dim3(XB_THREADS), lds, st, sets, S, band0,
                        reinterpret_cast<unsigned long long*>(shot), reinterpret_cast<unsigned long long*>(goal),
                        reinterpret_cast<unsigned long long*>(move), trans, (overwrite && s0 == 0) ? 1 : 0, vec,
-                       ell, row_len, xe_pitch(S.C));
+                       ell, row_len, xe_pitch(S.C), dense);
     int rc = check_launch("xt_band_count_kernel");
     if (rc) return rc;
     if (nsets == 0) break;
@@ -1620,6 +1660,10 @@ static int32_t* pinned_ctrl() {
   return p;
 }
 
+// sa_debug_xt_solve_abort (debug builds): the iteration at which the reordered solve's last
+// workgroup skips the grid barrier, -1 none
+static int g_xf_force_abort = -1;
+
 static int xt_solve_reordered(const uint32_t* ell, const int32_t* row_len, const int32_t* cnt_rows,
                               const int64_t* move, const double* gs, const double* pmove, int C, double eps,
                               int max_iter, double* heat, double* xt_out, int* n_iter, int* status, hipStream_t st) {
@@ -1660,7 +1704,7 @@ static int xt_solve_reordered(const uint32_t* ell, const int32_t* row_len, const
   if (!rc) {
     hipLaunchKernelGGL(xt_solve_reordered_kernel, dim3((unsigned)G), dim3(XF_THREADS), lds, st, ell, row_len,
                        reinterpret_cast<const unsigned long long*>(move), gs, pmove, C, hp, eps, max_iter, pmax, kov,
-                       xb, heat, xt_out, ctrl);
+                       xb, heat, xt_out, ctrl, SA_DEBUG ? g_xf_force_abort : -1);
     rc = check_launch("xt_solve_reordered_kernel");
   }
   if (!rc) rc = check_hip(hipMemcpyAsync(h, ctrl, 8 * sizeof(int32_t), hipMemcpyDeviceToHost, st), "copy solve control");
@@ -1675,8 +1719,8 @@ static int xt_solve_reordered(const uint32_t* ell, const int32_t* row_len, const
 #endif
   scratch_release(sc, st);
   if (rc) return rc;
-  if (h[XF_ABORT])
-    *status = 3;
+  if (h[XF_ABORT])  // 1: a barrier timed out; 2 / 4: a bound or an escaped count (not launchable)
+    *status = h[XF_ABORT] == 1 ? 3 : 2;
   else if (h[XF_AMB])
     *status = 1;
   else {
@@ -1705,7 +1749,7 @@ int xt_compact_solve(const uint32_t* ell, const int32_t* row_len, const int32_t*
       *path = SA_XT_PATH_REORDERED;
       return SA_OK;
     }
-    *path = status == 1 ? SA_XT_PATH_INSIDE_BOUND : SA_XT_PATH_UNAVAILABLE;
+    *path = status == 1 ? SA_XT_PATH_INSIDE_BOUND : status == 3 ? SA_XT_PATH_TIMEOUT : SA_XT_PATH_UNAVAILABLE;
   }
   Scratch sc;  // convergence flags [max_iter + 1]
   int rc = scratch_acquire(sizeof(int32_t) * ((size_t)max_iter + 1), st, &sc);
@@ -1738,6 +1782,17 @@ int xt_compact_solve(const uint32_t* ell, const int32_t* row_len, const int32_t*
   return rc;
 }
 }  // namespace sa
+
+extern "C" int sa_debug_xt_solve_abort(int32_t iteration) {
+#if SA_DEBUG
+  if (iteration < -1) return fail(SA_EINVAL, "iteration must be >= -1");
+  g_xf_force_abort = iteration;
+  return SA_OK;
+#else
+  (void)iteration;
+  return fail(SA_EINVAL, "sa_debug_xt_solve_abort: debug builds only (libsocceraction_amd_debug.so)");
+#endif
+}
 
 extern "C" int sa_xt_band_shape(int32_t l, int32_t w, int32_t* rows_per_band, int32_t* n_bands) {
   if (l < 1 || w < 1 || (int64_t)l * w > 46340) return fail(SA_EINVAL, "bad l or w");
@@ -1798,8 +1853,9 @@ extern "C" int sa_xt_count_from_buckets_ex(int32_t nsets, const uint32_t* const*
   for (int k = 0; k < nsets; ++k)
     if (!band_off[k]) return fail(SA_EINVAL, "null band offsets");
   if (!shot || !goal || !move || !trans) return fail(SA_EINVAL, "null count buffer");
-  if (flags & ~SA_XT_COUNT_OVERWRITE) return fail(SA_EINVAL, "unknown flags");
+  if (flags & ~(SA_XT_COUNT_OVERWRITE | SA_XT_COUNT_COMPACT_ONLY)) return fail(SA_EINVAL, "unknown flags");
   if (!ell != !row_len) return fail(SA_EINVAL, "ell and row_len come together");
+  if ((flags & SA_XT_COUNT_COMPACT_ONLY) && !ell) return fail(SA_EINVAL, "SA_XT_COUNT_COMPACT_ONLY needs ell");
   if (ell) {
     if (!xt_compact_ok(l * w)) return fail(SA_EINVAL, "the compact form takes 1 <= C <= %d", XE_XMAX);
     if (!(flags & SA_XT_COUNT_OVERWRITE) || nsets > XB_MAX_SETS)
@@ -1808,7 +1864,8 @@ extern "C" int sa_xt_count_from_buckets_ex(int32_t nsets, const uint32_t* const*
   }
   if (nsets == 0 && !(flags & SA_XT_COUNT_OVERWRITE)) return SA_OK;
   return count_from_buckets(nsets, buckets, band_off, S, 0, S.NB, shot, goal, move, trans,
-                            (flags & SA_XT_COUNT_OVERWRITE) != 0, (hipStream_t)stream, ell, row_len);
+                            (flags & SA_XT_COUNT_OVERWRITE) != 0, (hipStream_t)stream, ell, row_len,
+                            (flags & SA_XT_COUNT_COMPACT_ONLY) ? 0 : 1);
 }
 
 extern "C" int sa_xt_count_band_rows(int32_t nsets, const uint32_t* const* buckets, const int64_t* const* band_off,

@@ -389,6 +389,9 @@ class XTCounts:
     # the transition counts' compact rows (ell, row_len) as the count wrote them for the solve
     # (xt_count_many on 1025 - 9472 cells); every op that changes the counts drops them
     compact: Optional[Tuple[torch.Tensor, torch.Tensor]] = None
+    # False: the count wrote the compact rows only (xt_count_buckets(dense=False)): ``trans``
+    # holds just the rows of bands with a count >= 65535, the compact rows are the counts
+    dense: bool = True
 
     @property
     def C(self) -> int:
@@ -397,8 +400,14 @@ class XTCounts:
     def zero_(self) -> 'XTCounts':
         """Zero every count in one fill of the backing buffer (on the current stream)."""
         self.compact = None
+        self.dense = True
         self.buf.zero_()
         return self
+
+    def require_dense(self, what: str) -> None:
+        if not self.dense:
+            raise ValueError(f'{what} reads the dense C x C transition counts, which this count '
+                             'did not write (xt_count_buckets(dense=False)); count with dense=True')
 
 
 def xt_zero_counts(l: int, w: int, dev, row_blocks: int = 1, zero_counts: bool = True) -> XTCounts:
@@ -435,6 +444,7 @@ def xt_count(batch: ActionBatch, l: int, w: int, acc: Optional[XTCounts] = None,
     :func:`xt_rate_codes` of the same actions on the same grid. ``shared``: the pass runs next
     to other kernels (workgroups sized to co-reside with them)."""
     acc = acc or xt_zero_counts(l, w, batch.device)
+    acc.require_dense('adding to a count')
     acc.compact = None  # the counts change
     s = batch.struct()
     if codes is None and not shared:
@@ -568,19 +578,25 @@ def _compact_pitch(C: int) -> int:
 
 
 def xt_count_buckets(parts: Sequence[XTBuckets], l: int, w: int, acc: XTCounts,
-                     overwrite: bool = False, compact: Optional[bool] = None) -> XTCounts:
+                     overwrite: bool = False, compact: Optional[bool] = None,
+                     dense: bool = True) -> XTCounts:
     """The once-per-fit half of the band-owned count: every batch's buckets into ``acc`` (added;
     ``overwrite``: written, the rows' old values never read).  ``compact`` (default: whenever it
     can) also writes the transition counts' compact rows for the large-grid solve
     (``sa_xt_count_from_buckets_ex``; ``acc.compact``): overwrite, <= 24 batches and
-    1025 <= C <= 9472 only."""
+    1025 <= C <= 9472 only.  ``dense=False`` (with the compact rows): the dense C x C table is
+    not written (``SA_XT_COUNT_COMPACT_ONLY``: only the rows of bands holding a count >= 65535,
+    which the compact solve reads) -- for a fit that reads the compact rows alone (the solve,
+    :func:`xt_transition_entries`); ``acc.dense`` is then False."""
     k = len(parts)
     C = l * w
     can = (overwrite and k <= XB_MAX_SETS and _native.SA_XT_SOLVE_MAX_C < C <= _native.SA_XT_COMPACT_MAX_C)
     if compact and not can:
         raise ValueError('compact rows need overwrite, at most 24 batches and 1025 <= C <= 9472')
     compact = can if compact is None else compact
+    dense = dense or not compact  # the dense rows are skipped only beside the compact rows
     acc.compact = None
+    acc.dense = True
     ell = rl = None
     if compact:
         pe = _compact_pitch(C)
@@ -588,41 +604,79 @@ def xt_count_buckets(parts: Sequence[XTBuckets], l: int, w: int, acc: XTCounts,
         rl = torch.empty(C, dtype=torch.int32, device=acc.trans.device)
     keys = (ctypes.c_void_p * max(k, 1))(*[p.keys.data_ptr() for p in parts])
     offs = (ctypes.c_void_p * max(k, 1))(*[p.band_off.data_ptr() for p in parts])
+    flags = (_native.SA_XT_COUNT_OVERWRITE if overwrite else 0) | \
+        (0 if dense else _native.SA_XT_COUNT_COMPACT_ONLY)
     _native.check(_native.lib().sa_xt_count_from_buckets_ex(
         k, keys, offs, int(l), int(w), _ptr(acc.shot), _ptr(acc.goal), _ptr(acc.move),
-        _ptr(acc.trans), _native.SA_XT_COUNT_OVERWRITE if overwrite else 0, _ptr(ell), _ptr(rl),
-        stream_handle()))
+        _ptr(acc.trans), flags, _ptr(ell), _ptr(rl), stream_handle()))
     if compact:
         acc.compact = (ell, rl)
+    acc.dense = dense
     return acc
+
+
+def xt_transition_entries(acc: XTCounts) -> Tuple[torch.Tensor, torch.Tensor]:
+    """The non-zero transition counts as ``(flat index s * C + e, count)`` int64 device tensors
+    in row-major order -- from the compact rows when the count wrote them (62.5 MB read at
+    105 x 68; counts >= 65535 from their dense rows), else from the dense table."""
+    C = acc.shot.numel()
+    if getattr(acc, 'compact', None) is None:
+        if not getattr(acc, 'dense', True):
+            acc.require_dense('xt_transition_entries without compact rows')
+        nz = torch.nonzero(acc.trans).reshape(-1)
+        return nz, acc.trans[nz].to(torch.int64)
+    ell, rl = acc.compact
+    pe = ell.numel() // C
+    k = torch.arange(pe, device=ell.device)
+    # storage slot of a row's k-th entry (sa_xt_large.hip xe_slot)
+    slot = (k & ~127) | ((k & 31) << 2) | ((k >> 5) & 3)
+    e = ell.view(C, pe)[:, slot].to(torch.int64) & 0xFFFFFFFF  # [C, pe], entry k of each row
+    used = k.unsqueeze(0) < rl.to(torch.int64).unsqueeze(1)
+    rows = torch.arange(C, device=ell.device).unsqueeze(1).expand(C, pe)[used]
+    e = e[used]
+    idx = rows * C + (e & 0xFFFF)
+    cnt = e >> 16
+    esc = cnt == 0xFFFF  # escaped: the dense row holds the count (written for its band)
+    if bool(esc.any()):
+        cnt = torch.where(esc, acc.trans[idx].to(torch.int64), cnt)
+    return idx, cnt
 
 
 def xt_count_many(batches: Sequence[ActionBatch], l: int, w: int,
                   acc: Optional[XTCounts] = None, overwrite: Optional[bool] = None,
-                  interp_codes: Optional[Sequence[torch.Tensor]] = None) -> XTCounts:
+                  interp_codes: Optional[Sequence[torch.Tensor]] = None,
+                  dense: bool = True) -> XTCounts:
     """The count pass of ONE fit over several device batches (e.g. cfg5's 1e8 actions in
     batches of <= 10k games): equal to :func:`xt_count` of every batch into one accumulator.
     Band-owned grids bucket each batch and write the C x C table once. ``overwrite`` (default:
     ``acc`` is None, a fresh accumulator): the counts are written, not added to the old ones
     (``acc``'s error flags still accumulate). ``interp_codes``: one :func:`xt_interp_codes_buffer`
-    per batch (band-owned grids only), filled for a later :func:`xt_rate_interp_codes`."""
+    per batch (band-owned grids only), filled for a later :func:`xt_rate_interp_codes`.
+    ``dense=False``: see :func:`xt_count_buckets` (band-owned grids with compact rows only;
+    ignored elsewhere)."""
     if xt_band_shape(l, w) is None or not batches:
         if interp_codes is not None:
             raise ValueError('interp_codes come from the band-owned count')
         if overwrite and acc is not None:  # the counts only: the error flags accumulate, as on
             for t in (acc.shot, acc.goal, acc.move, acc.trans):  # the band-owned path
                 t.zero_()
+            acc.compact = None  # they described the old counts
+            acc.dense = True
+        if acc is not None and not acc.dense:  # adding to rows that were never written
+            acc.require_dense('adding to a count')
         for b in batches:
             acc = xt_count(b, l, w, acc)
         return acc if acc is not None else xt_zero_counts(l, w, torch.device('cuda'))
     if overwrite is None:
         overwrite = acc is None
+    if acc is not None and not acc.dense and not overwrite:
+        acc.require_dense('adding to a count')
     # a fresh accumulator the overwriting count fills whole: only its error word zeroed (the
     # 204 MB fill of the 105 x 68 table was 27 us of cfg5's fit)
     acc = acc or xt_zero_counts(l, w, batches[0].device, zero_counts=not overwrite)
     ic = list(interp_codes) if interp_codes is not None else [None] * len(batches)
     parts = [xt_bucket(b, l, w, acc.err, interp_codes=c) for b, c in zip(batches, ic)]
-    return xt_count_buckets(parts, l, w, acc, overwrite=overwrite)
+    return xt_count_buckets(parts, l, w, acc, overwrite=overwrite, dense=dense)
 
 
 def xt_rate_codes_buffer(n: int, dev) -> torch.Tensor:
@@ -677,6 +731,7 @@ def xt_count_cells(cells: torch.Tensor, n: int, l: int, w: int, acc: Optional[XT
                    shared: bool = False) -> XTCounts:
     """The count pass of ExpectedThreat.fit from cell codes (4 B per action read)."""
     acc = acc or xt_zero_counts(l, w, cells.device)
+    acc.require_dense('adding to a count')
     acc.compact = None  # the counts change
     _native.check(_native.lib().sa_xt_count_cells(_ptr(cells), int(n), int(l), int(w),
                                                   _ptr(acc.shot), _ptr(acc.goal), _ptr(acc.move),
@@ -739,6 +794,8 @@ def xt_solve(acc: XTCounts, eps: float = 1e-5, max_iter: int = 1000,
     mats = torch.empty((4, C), dtype=torch.float64, device=dev)
     if not transition and C <= _native.SA_XT_SOLVE_MAX_C:
         transition = True  # the small-grid solve reads the transposed matrix
+    if transition or getattr(acc, 'compact', None) is None:
+        acc.require_dense('xt_solve with the transition matrix or without compact rows')
     tt = torch.empty((C, C), dtype=torch.float64, device=dev) if transition else None
     heat = torch.empty((max_iter + 1, C), dtype=torch.float64, device=dev)
     n_iter, path = ctypes.c_int32(0), ctypes.c_int32(0)
@@ -750,8 +807,18 @@ def xt_solve(acc: XTCounts, eps: float = 1e-5, max_iter: int = 1000,
         stream_handle()))
     if n_iter.value < 0:
         raise RuntimeError(f'xT value iteration did not converge within {max_iter} iterations')
-    return XTSolution(mats, tt, heat[:n_iter.value + 1], n_iter.value,
-                      _native.XT_SOLVE_PATHS[path.value])
+    p = _native.XT_SOLVE_PATHS[path.value]
+    _warn_solve_path(p)
+    return XTSolution(mats, tt, heat[:n_iter.value + 1], n_iter.value, p)
+
+
+def _warn_solve_path(path: str) -> None:
+    if path == 'timeout':
+        import warnings
+        warnings.warn('the reordered xT solve timed out at a grid barrier (another kernel held '
+                      'CUs: it needs one workgroup resident on every CU) and was redone in the '
+                      "reference's order: same result, ~50 ms - 1 s slower", RuntimeWarning,
+                      stacklevel=3)
 
 
 def xt_solve_compact(ell: torch.Tensor, row_len: torch.Tensor, cnt_rows: torch.Tensor,
@@ -766,7 +833,9 @@ def xt_solve_compact(ell: torch.Tensor, row_len: torch.Tensor, cnt_rows: torch.T
         _ptr(ell), _ptr(row_len), _ptr(cnt_rows), _ptr(move), _ptr(gs), _ptr(pmove), int(C),
         float(eps), int(max_iter), _native.SA_XT_SOLVE_EXACT if exact_order else 0, _ptr(heat),
         ctypes.byref(n_iter), ctypes.byref(path), stream_handle()))
-    return heat, n_iter.value, _native.XT_SOLVE_PATHS[path.value]
+    p = _native.XT_SOLVE_PATHS[path.value]
+    _warn_solve_path(p)
+    return heat, n_iter.value, p
 
 
 def xt_solve_async(acc: XTCounts, eps: float = 1e-5, max_iter: int = 1000) -> XTSolution:
@@ -825,6 +894,7 @@ def xt_interp_grid(xT: torch.Tensor, l: int, w: int, xs: Optional[np.ndarray] = 
 
 def xt_normalize(acc: XTCounts) -> Tuple[torch.Tensor, torch.Tensor]:
     """(mats [3, C] scoring/shot/move probabilities, trans_t [C, C]) on device."""
+    acc.require_dense('xt_normalize')
     C = acc.C
     dev = acc.shot.device
     mats = torch.empty((3, C), dtype=torch.float64, device=dev)

@@ -39,6 +39,8 @@ def allreduce_xt_counts(acc, group=None) -> None:
     flags are one byte each (``ops.XT_ERR_*``), so up to 255 ranks' flags add without
     overlapping.  No staging copy, no ``torch.cat``."""
     _check_world(group)
+    if not getattr(acc, 'dense', True):  # every rank would raise alike (the same call on each)
+        acc.require_dense('allreduce_xt_counts')
     _flag_count_range(acc, group)
     acc.compact = None  # this rank's compact rows no longer describe the summed counts
     _all_reduce(acc.buf.view(torch.int32), group=group)
@@ -453,24 +455,29 @@ def exchange_band_keys(parts, n_bands: int, group=None, dev=None, stats=None):
     per = -(-NB // W)
     dev = dev if dev is not None else (parts[0][0].device if parts else torch.device('cpu'))
     R = len(parts)
-    if R > _MAX_ROUNDS:
-        raise ValueError(f'at most {_MAX_ROUNDS} local batches per rank in one band exchange')
+    # a rank over the limit still takes part in the header exchange (its true R in the header,
+    # no split sizes), and EVERY rank raises after it: raising before the collective would leave
+    # the other ranks waiting in it
+    Rh = min(R, _MAX_ROUNDS)
     cuts = torch.tensor([q0 for q0, _ in ranges] + [NB], dtype=torch.int64, device=dev)
     # the band offsets each destination needs: its bands q0 .. q0 + per (clamped), [W, per + 1]
     want = torch.tensor([[min(NB, q0 + k) for k in range(per + 1)] for q0, _ in ranges],
                         dtype=torch.int64, device=dev)
     hdr = torch.zeros((W, 1 + _MAX_ROUNDS), dtype=torch.int64, device=dev)
     hdr[:, 0] = R
-    hc = (torch.stack([off[cuts] for _, off in parts]) if R else
-          torch.zeros((0, W + 1), dtype=torch.int64, device=dev))  # [R, W + 1] key cuts
-    if R:
-        hdr[:, 1:1 + R] = (hc[:, 1:] - hc[:, :-1]).T
+    hc = (torch.stack([off[cuts] for _, off in parts[:Rh]]) if Rh else
+          torch.zeros((0, W + 1), dtype=torch.int64, device=dev))  # [Rh, W + 1] key cuts
+    if Rh:
+        hdr[:, 1:1 + Rh] = (hc[:, 1:] - hc[:, :-1]).T
     rhdr = torch.empty_like(hdr)
     _all_to_all(rhdr.view(-1), hdr.view(-1), group=group)
     h = _to_host(torch.cat([rhdr.view(-1), hc.view(-1)]), stats)  # the exchange's one host read
     rh = h[:W * (1 + _MAX_ROUNDS)].reshape(W, 1 + _MAX_ROUNDS)
-    hcuts = h[W * (1 + _MAX_ROUNDS):].reshape(R, W + 1)
+    hcuts = h[W * (1 + _MAX_ROUNDS):].reshape(Rh, W + 1)
     rounds = int(rh[:, 0].max())
+    if rounds > _MAX_ROUNDS:  # on every rank alike (every rank read the same batch counts)
+        raise ValueError(f'at most {_MAX_ROUNDS} local batches per rank in one band exchange '
+                         f'(a rank has {rounds})')
     sets_keys, sets_off = [], []
     sent = recvd = 0
     for k in range(rounds):

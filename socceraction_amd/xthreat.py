@@ -82,11 +82,13 @@ def _safe_divide(a, b) -> np.ndarray:
 
 
 def _fit_counts(actions: pd.DataFrame, l: int, w: int, process_group=None,
-                mask: int = ops.XT_ERR_FIT) -> ops.XTCounts:
+                mask: int = ops.XT_ERR_FIT, dense: bool = True) -> ops.XTCounts:
     if len(actions):
         # the many-batch entry (one batch): a fresh accumulator the band-owned count writes
         # whole, and for 1025 - 9472 cells the solve's compact rows from the same pass
-        acc = ops.xt_count_many([ActionBatch.from_frame(actions)], l, w)
+        # (dense=False: those rows alone, no C x C table -- a fit without an all-reduce)
+        acc = ops.xt_count_many([ActionBatch.from_frame(actions)], l, w,
+                                dense=dense or process_group is not None)
     else:
         from .batch import device
         acc = ops.xt_zero_counts(l, w, device())
@@ -282,8 +284,8 @@ class ExpectedThreat:
             ops.xt_check_errors(acc)
             trans = None
         else:
-            acc = _fit_counts(actions, l, w, process_group)
             lazy = l * w > self.LAZY_TRANSITION_CELLS
+            acc = _fit_counts(actions, l, w, process_group, dense=not lazy)
             sol = ops.xt_solve(acc, self.eps, max_iter, transition=not lazy,
                                exact_order=exact_order)
             mats, heat_t, n_iter = sol.mats, sol.heatmaps, sol.n_iter
@@ -296,10 +298,11 @@ class ExpectedThreat:
         self.transition_matrix = trans
         if trans is None and not (shard_solve and process_group is not None):
             # normalised on first access from a compact HOST copy (move counts + the non-zero
-            # transition bins), so the 4*C*C-byte device count buffer is not kept alive
-            nz = torch.nonzero(acc.trans).reshape(-1)
+            # transition bins, read from the count's compact rows when it wrote them), so the
+            # 4*C*C-byte device count buffer is not kept alive
+            nz, cnt = ops.xt_transition_entries(acc)
             self._transition_counts = (acc.move.cpu().numpy(), nz.cpu().numpy(),
-                                       acc.trans[nz].cpu().numpy())
+                                       cnt.cpu().numpy())
         self.xT = m[3].reshape((w, l)).copy()
         heat = heat_t.cpu().numpy().reshape((-1, w, l))
         self.heatmaps = [h.copy() for h in heat]

@@ -400,6 +400,44 @@ def test_band_key_exchange_gloo(world):
         assert res[r][1] == 2 * world  # two rounds (rank 0's batches) x every source rank
 
 
+def _band_exchange_limit_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+
+    from socceraction_amd import shard
+    dist.init_process_group('gloo', init_method=f'tcp://127.0.0.1:{port}', rank=rank,
+                            world_size=world)
+    R, NB = 3, 11
+    nparts = shard._MAX_ROUNDS + 1 if rank == 0 else 1  # only rank 0 is over the limit
+    parts = [tuple(torch.from_numpy(a) for a in _band_keys(rank, k, R, NB)) for k in range(nparts)]
+    try:
+        shard.exchange_band_keys(parts, NB, dev=torch.device('cpu'))
+        q.put((rank, 'no error'))
+    except ValueError as e:
+        q.put((rank, 'ValueError' if 'local batches' in str(e) else repr(e)))
+    dist.destroy_process_group()
+
+
+def test_band_key_exchange_over_limit_raises_on_every_rank():
+    """A rank with more local batches than one band exchange takes: every rank
+    raises ValueError after the header all-to-all -- none is left waiting in a collective."""
+    import multiprocessing as mp
+    import socket
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_band_exchange_limit_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res == {0: 'ValueError', 1: 'ValueError'}
+
+
 def _compact_pack_worker(rank, world, port, q):
     import torch
     import torch.distributed as dist

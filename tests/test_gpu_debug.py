@@ -56,3 +56,54 @@ def test_goldens_through_the_debug_build():
 def test_debug_build_reports_a_corrupt_segment_table():
     out = _run(['-c', CORRUPT], timeout=300)
     assert out.strip().endswith('ok')
+
+
+ABORT = r"""
+import warnings
+import numpy as np, torch
+from socceraction_amd import _native, ops
+assert _native.lib().sa_debug_enabled() == 1
+rng = np.random.default_rng(11)
+C = 1500
+cnt = np.zeros((C, C), np.int32)
+nz = rng.random((C, C)) < 0.2
+cnt[nz] = rng.geometric(0.3, nz.sum())
+move = cnt.sum(axis=1, dtype=np.int64) + rng.integers(1, 50, C)
+gs, pm = rng.random(C) * 0.05, rng.random(C) * 0.95
+dev = torch.device('cuda')
+rows = torch.from_numpy(cnt).to(dev)
+lib = _native.lib()
+ell = torch.empty(int(lib.sa_xt_compact_bytes(C, C)) // 4, dtype=torch.int32, device=dev)
+slen = torch.empty(C, dtype=torch.int32, device=dev)
+from socceraction_amd.batch import stream_handle
+_native.check(lib.sa_xt_compact_rows(rows.data_ptr(), C, C, ell.data_ptr(), slen.data_ptr(), stream_handle()))
+t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+args = (ell, slen, rows, t(move), t(gs), t(pm), C, 1e-5, 1000)
+he, ne, pe = ops.xt_solve_compact(*args, exact_order=True)
+hr, nr, pr = ops.xt_solve_compact(*args)
+assert pe == 'sequential' and pr == 'reordered' and nr == ne > 3, (pe, pr, nr, ne)
+for k in (0, 3):  # the first barrier (50 ms bound) and a later one (1 s bound)
+    _native.check(lib.sa_debug_xt_solve_abort(k))
+    with warnings.catch_warnings(record=True) as wl:
+        warnings.simplefilter('always')
+        h, n, p = ops.xt_solve_compact(*args)
+    assert p == 'timeout', p
+    assert any('timed out' in str(w.message) for w in wl), [str(w.message) for w in wl]
+    # the fallback redoes the solve in the reference's order: the same count, the same bits
+    assert n == ne and torch.equal(h[:n + 1], he[:ne + 1]), (k, n, ne)
+    print('abort at', k, 'ok')
+_native.check(lib.sa_debug_xt_solve_abort(-1))
+h, n, p = ops.xt_solve_compact(*args)
+assert p == 'reordered' and n == nr and torch.equal(h[:n + 1], hr[:nr + 1])
+print('ok')
+"""
+
+
+def test_reordered_solve_barrier_timeout_exit():
+    """The persistent reordered solve's barrier-timeout exit, forced deterministically
+    (sa_debug_xt_solve_abort: the last workgroup leaves at iteration k without arriving): at the
+    first barrier and at a later one, the solve reports path 'timeout', ops warns, and the
+    reference-order fallback gives the sequential solve's iteration count and heatmaps bit for
+    bit; switched off, the reordered path runs again with its own bits."""
+    out = _run(['-c', ABORT], timeout=300)
+    assert out.strip().endswith('ok')

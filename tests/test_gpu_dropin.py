@@ -78,8 +78,8 @@ def test_compute_features_labels_rate(atomic):
                 assert v[c].dtype == ref.dtype, (c, v[c].dtype)
                 if tag == '64':
                     assert_close(v[c].to_numpy(), ref, c)
-                else:
-                    np.testing.assert_allclose(v[c].to_numpy(), ref, rtol=1e-6, atol=1e-7)
+                else:  # float32: bit-exact (the reference's f32 operations in its order)
+                    np.testing.assert_array_equal(v[c].to_numpy(), ref, err_msg=c)
 
 
 def test_rate_errors():

@@ -65,9 +65,8 @@ def test_features_labels_formula_goldens(sa, atomic):
             pc = torch.tensor(g['pc'], dtype=dt, device=ab.device)
             v = ops.formula(ab, ps, pc).cpu().numpy()[:, :n]
             for r, c in enumerate(('offensive_value', 'defensive_value', 'vaep_value')):
-                if dt == torch.float32:
-                    np.testing.assert_allclose(v[r], g[f'{c}_{tag}'], rtol=1e-6, atol=1e-7,
-                                               err_msg=f'{name} {c}')
+                if dt == torch.float32:  # a few IEEE f32 ops in the reference's order: bit-exact
+                    np.testing.assert_array_equal(v[r], g[f'{c}_{tag}'], err_msg=f'{name} {c}')
                 else:
                     assert_close(v[r], g[f'{c}_{tag}'], f'{name} {c}')
 
@@ -238,8 +237,8 @@ def test_many_small_segments_vs_oracle(sa, atomic):
             np.testing.assert_array_equal(vf.cpu().numpy()[:, :n], v)
         fo = vo.formula(cols, ps, pc, atomic=atomic, seg_off=so)
         for r, c in enumerate(('offensive_value', 'defensive_value', 'vaep_value')):
-            if dt == np.float32:
-                np.testing.assert_allclose(v[r], fo[c], rtol=1e-6, atol=1e-7, err_msg=c)
+            if dt == np.float32:  # bit-exact (the reference's f32 operations in its order)
+                np.testing.assert_array_equal(v[r], fo[c], err_msg=c)
             else:
                 assert_close(v[r], fo[c], c)
 

@@ -428,3 +428,95 @@ def test_coresident_16x12_count_full_batch_vs_oracle(sa):
     ref = ops.xt_count(ab, l, w)
     for a, b in ((acc.shot, ref.shot), (acc.goal, ref.goal), (acc.move, ref.move), (acc.trans, ref.trans)):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize('l,w,hot', [(105, 68, False), (105, 68, True), (40, 30, True)])
+def test_compact_only_count_skips_the_dense_table(sa, l, w, hot):
+    """xt_count_many(dense=False) (SA_XT_COUNT_COMPACT_ONLY): the same shot / goal / move counts
+    and compact rows as the dense count, entry for entry; the dense rows written ONLY for the
+    bands holding a count >= 65535 (the rows the compact solve reads; every other row keeps the
+    sentinel it held); the transition entries read back from the compact rows == the dense
+    table's non-zero bins; the solve == the dense count's solve bit for bit (incl. the escaped
+    case's fallback to the reference order); ops that read the dense table refuse the count."""
+    B, ops, syn = sa['batch'], sa['ops'], sa['synthetic']
+    C = l * w
+    ds = [syn.spadl_games(g, game_id0=17 * i + 3) for i, g in enumerate((150 if hot else 60, 45))]
+    if hot:  # one bin far above 65535 counts: its band's dense rows must be written
+        mv = np.isin(ds[0]['type_id'], (0, 1, 21))
+        ds[0]['start_x'][mv], ds[0]['start_y'][mv] = 52.2, 33.3
+        ds[0]['end_x'][mv], ds[0]['end_y'][mv] = 104.999, 0.0
+    abs_ = [B.ActionBatch.from_columns(d) for d in ds]
+    ref = ops.xt_count_many(abs_, l, w)
+    acc = ops.xt_zero_counts(l, w, abs_[0].device, zero_counts=False)
+    acc.trans.fill_(-7)
+    ops.xt_count_many(abs_, l, w, acc=acc, overwrite=True, dense=False)
+    assert not acc.dense and acc.compact is not None and ref.dense
+    for a, b in ((acc.shot, ref.shot), (acc.goal, ref.goal), (acc.move, ref.move), (acc.err, ref.err)):
+        assert torch.equal(a, b)
+    (ea, ra), (eb, rb) = acc.compact, ref.compact
+    assert torch.equal(ra, rb)
+    pe = ea.numel() // C
+    xa, xb = ea.cpu().numpy().reshape(C, pe), eb.cpu().numpy().reshape(C, pe)
+    lens = ra.cpu().numpy()
+    for r in np.flatnonzero(lens):
+        sl = _xe_slots(np.arange(lens[r]))
+        np.testing.assert_array_equal(xa[r, sl], xb[r, sl])
+    R, NB = ops.xt_band_shape(l, w)
+    dense_ref = ref.trans.cpu().numpy().reshape(C, C)
+    got = acc.trans.cpu().numpy().reshape(C, C)
+    esc_rows = np.flatnonzero(dense_ref.max(axis=1) >= 65535)
+    esc_bands = set((esc_rows // R).tolist())
+    assert bool(esc_bands) == hot
+    for band in range(NB):
+        rows = slice(band * R, min(C, band * R + R))
+        if band in esc_bands:
+            np.testing.assert_array_equal(got[rows], dense_ref[rows])
+        else:
+            assert (got[rows] == -7).all(), band
+    idx, cnt = ops.xt_transition_entries(acc)
+    nz = np.flatnonzero(dense_ref.reshape(-1))
+    np.testing.assert_array_equal(idx.cpu().numpy(), nz)
+    np.testing.assert_array_equal(cnt.cpu().numpy(), dense_ref.reshape(-1)[nz])
+    sol = ops.xt_solve(acc, transition=False)
+    want = ops.xt_solve(ref, transition=False)
+    assert sol.path == want.path == ('unavailable' if hot else 'reordered')
+    assert sol.n_iter == want.n_iter
+    assert torch.equal(sol.heatmaps, want.heatmaps) and torch.equal(sol.mats, want.mats)
+    for bad in (lambda: ops.xt_normalize(acc), lambda: ops.xt_solve(acc, transition=True),
+                lambda: ops.xt_count(abs_[0], l, w, acc)):
+        with pytest.raises(ValueError, match='dense'):
+            bad()
+
+
+def test_cell_code_bucket_count_small_grid(sa):
+    """sa_xt_count_bucket from 16-bit cell codes (grids of <= SA_XT_CELLS16_MAX_C cells, 16 x 12;
+    ADVICE r05): K1 loads and decodes them like the small-grid count, so the band-owned count
+    from the codes == sa_xt_count of the coordinates; 32-bit codes (40 x 30) the same."""
+    import ctypes
+
+    B, ops, syn, N = sa['batch'], sa['ops'], sa['synthetic'], sa['_native']
+    from socceraction_amd.batch import stream_handle
+    d = syn.spadl_games(30, game_id0=71)
+    ab = B.ActionBatch.from_columns(d)
+    lib = N.lib()
+    for l, w in ((16, 12), (40, 30)):
+        rr, nn = ctypes.c_int32(0), ctypes.c_int32(0)
+        N.check(lib.sa_xt_band_shape(l, w, ctypes.byref(rr), ctypes.byref(nn)))
+        cells = ops.xt_cells(ab, l, w)
+        err = torch.zeros(1, dtype=torch.int32, device=ab.device)
+        keys = torch.empty(max(ab.n, 16), dtype=torch.int32, device=ab.device)
+        off = torch.empty(nn.value + 1, dtype=torch.int64, device=ab.device)
+        N.check(lib.sa_xt_count_bucket(None, cells.data_ptr(), ab.n, l, w, keys.data_ptr(),
+                                       off.data_ptr(), err.data_ptr(), None, None, 1050, 680,
+                                       stream_handle()))
+        acc = ops.xt_zero_counts(l, w, ab.device)
+        kp = (ctypes.c_void_p * 1)(keys.data_ptr())
+        op = (ctypes.c_void_p * 1)(off.data_ptr())
+        N.check(lib.sa_xt_count_from_buckets(1, kp, op, l, w, acc.shot.data_ptr(), acc.goal.data_ptr(),
+                                             acc.move.data_ptr(), acc.trans.data_ptr(),
+                                             N.SA_XT_COUNT_OVERWRITE, stream_handle()))
+        ref = ops.xt_count(ab, l, w)
+        for a, b in ((acc.shot, ref.shot), (acc.goal, ref.goal), (acc.move, ref.move),
+                     (acc.trans, ref.trans)):
+            assert torch.equal(a, b), (l, w)
+        assert int(err.item()) == int(ref.err.item())
