@@ -15,6 +15,7 @@ N > 1 runs one rank per GPU under torch.distributed.run; each rank values its ow
 from __future__ import annotations
 
 import argparse
+import contextlib
 import copy
 import json
 import os
@@ -513,32 +514,45 @@ def xt105_extra(ab, dist, dev, sharded: bool = False, cfg5_games: int = 62500,
             gid += c
             left -= c
 
-    def once(marks=None):
+    def once(mode, marks=None, timer=None):
+        """One fit + rate in ``mode`` = (sharded, solve); ``timer`` (shard.PhaseTimes): HIP
+        events around every phase, incl. the exchange's collectives."""
+        msharded, msolve = mode
+
         def mark():  # the instrumented call only: phase boundaries (synchronised)
             if marks is not None:
                 torch.cuda.synchronize()
                 marks.append(time.perf_counter())
+
+        def phase(name):
+            return timer.phase(name) if timer is not None else contextlib.nullcontext()
         mark()
         # the count of every batch: band-owned (sa_xt_count_bucket per batch, the C x C table
         # written once by sa_xt_count_from_buckets; no global atomics), into a fresh accumulator
         # and, per action, the operand of the interpolated rate below (start / end node of the
         # 1050 x 680 grid: 8 B read by the rate instead of 34 B of coordinates and ids)
-        if sharded and dist is not None:  # band-sharded: all-to-all of the counted actions,
-            mark()                         # each rank counts its bands; row-sharded iteration
+        if msharded and dist is not None:  # band-sharded: all-to-all of the counted actions,
+            mark()                          # each rank counts its bands; row-sharded iteration
             mark()  # (count and exchange happen inside the sharded fit)
             xstats.clear()
+            if timer is not None:
+                xstats['timer'] = timer
             mats, _, n_iter, err = shard.xt_fit_bands_sharded(batches, l, w, interp_codes=icodes,
-                                                              solve=solve, stats=xstats)
+                                                              solve=msolve, stats=xstats)
+            xstats.pop('timer', None)
             acc = None  # each rank holds only its row block of the transition counts
             path[0] = xstats.get('solve_path', 'sequential')
         else:  # one all-reduce of the counts, replicated solve
             # one rank: the compact count rows alone (the solve reads nothing else; no 204 MB
             # dense flush); replicated over ranks: the dense table the all-reduce sums
-            acc = ops.xt_count_many(batches, l, w, interp_codes=icodes, dense=dist is not None)
+            with phase('count'):
+                acc = ops.xt_count_many(batches, l, w, interp_codes=icodes, dense=dist is not None)
             mark()
-            allreduce_counts(dist, acc)
+            with phase('count_all_reduce'):
+                allreduce_counts(dist, acc)
             mark()
-            sol = ops.xt_solve(acc, transition=False)  # synchronises; ExpectedThreat.fit's
+            with phase('solve'):
+                sol = ops.xt_solve(acc, transition=False)  # synchronises; ExpectedThreat.fit's
             mats, n_iter = sol.mats, sol.n_iter           # call above 1024 cells
             path[0] = sol.path
         mark()
@@ -546,8 +560,9 @@ def xt105_extra(ab, dist, dev, sharded: bool = False, cfg5_games: int = 62500,
         # the 105 x 68 surface staged in LDS (sa_xt_rate_interp_codes_many: every batch in one
         # launch), bit-identical to the 1050 x 680 grid gather
         xT = mats[3].reshape(w, l)
-        rates, _ = ops.xt_rate_interp_codes_many(icodes, [b.n for b in batches], xT, l, w, 1050,
-                                                 680, axes=axes, outs=rate_out)
+        with phase('rate'):
+            rates, _ = ops.xt_rate_interp_codes_many(icodes, [b.n for b in batches], xT, l, w,
+                                                     1050, 680, axes=axes, outs=rate_out)
         mark()
         return n_iter, acc, mats, rates
     path = ['sequential']  # the value iteration's summation path of the last call
@@ -555,72 +570,80 @@ def xt105_extra(ab, dist, dev, sharded: bool = False, cfg5_games: int = 62500,
     axes = ops.xt_interp_axes(l, w, dev)  # node positions (constants of the reference's grid)
     icodes = [ops.xt_interp_codes_buffer(b.n, dev) for b in batches]
     rate_out = [torch.empty(max(b.n, 16), dtype=torch.float64, device=dev) for b in batches]
-    once()  # warm-up (allocator, first launches)
-    torch.cuda.synchronize()
-    times = []
-    for _ in range(reps):  # each call wall-timed alone (the solve synchronises with the host)
-        if dist is not None:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        n_iter, acc, mats, rates = once()
-        torch.cuda.synchronize()
-        times.append(time.perf_counter() - t0)
-    dt = float(np.median(times))
-    marks = []
-    once(marks)  # one more call, synchronised between phases: where the time goes
-    phases = dict(zip(('count', 'exchange', 'solve', 'rate'),
-                      (round((b - a) * 1e3, 3) for a, b in zip(marks, marks[1:]))))
-    n_iter, acc, mats, rates = once()  # the checked outputs come from an untouched call
-    torch.cuda.synchronize()
-    par = Parity()
-    # reordered sums: the iteration count exact, the surface within 1e-12 relative (the error
-    # bound allows 4e-11 after 26 iterations; north_star's bar is 1e-6); in order: bit for bit
-    rtol = 0.0 if path[0] == 'sequential' else 1e-12
-    if check:  # the last call's counts, surface, iterations and the first batch's rates
-        ocnt = oracle_counts(None, l, w, dist, dev, acc=ocnt)
-        if acc is None:  # row-sharded solve: the surface is checked, the counts are not held
-            from oracle import xt_oracle as xo
-            fit = xo.solve(ocnt, l, w)
-            xT = fit['xT']
-            par.exact('xT 105x68 iterations', n_iter + 1, len(fit['heatmaps']))
-            check_surface(par, 'xT 105x68', mats[3].cpu().numpy().reshape(w, l), xT, rtol)
-        else:
-            xT = check_xt(par, ocnt, acc, mats[3], n_iter, l, w, rtol)
-        del ocnt
-        if first is not None:
-            check_xt_rate(par, first, rates[0], xT, interp=True)
-            par.games += len(sample_games(len(first['game_off']) - 1))
-        par.merge(dist, dev)
+    if check:
+        ocnt = oracle_counts(None, l, w, dist, dev, acc=ocnt)  # every rank's counts
     n = sum(b.n for b in batches)
     total = n
     if dist is not None:
-        dt = _reduce(dist, dt, dist.ReduceOp.MAX, dev)
         total = int(_reduce(dist, n, dist.ReduceOp.SUM, dev))
-    games = (f'{cfg5_games:,} synthetic games over {world} rank(s)' if cfg5_games > 0 else
-             'the step batch')
-    return {'workload': f'cfg5: xT 105x68 fit (count + all-reduce + value iteration) + '
-                        f'rate(use_interpolation=True) of {games}',
-            'actions_per_gpu': n, 'actions_total': total, 'iterations': n_iter,
-            'ms_fit_and_rate': round(dt * 1e3, 3), 'actions_per_s': round(total / dt, 1),
-            'timing': f'median of {reps} calls (wall clock around each, after a warm-up call; '
+
+    def run(mode, nreps):
+        """Time ``mode`` (median of ``nreps`` wall-clocked calls), one call with synchronised
+        phase marks, one with per-phase HIP events, then check an untouched call's outputs."""
+        once(mode)  # warm-up (allocator, first launches)
+        torch.cuda.synchronize()
+        times = []
+        for _ in range(nreps):  # each call wall-timed alone (the solve synchronises with the host)
+            if dist is not None:
+                dist.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            once(mode)
+            torch.cuda.synchronize()
+            times.append(time.perf_counter() - t0)
+        dt = float(np.median(times))
+        marks = []
+        once(mode, marks)  # one more call, synchronised between phases: where the time goes
+        phases = dict(zip(('count', 'exchange', 'solve', 'rate'),
+                          (round((b - a) * 1e3, 3) for a, b in zip(marks, marks[1:]))))
+        timer = shard.PhaseTimes(dev)
+        once(mode, timer=timer)  # and one with HIP events around each phase (no host syncs added)
+        events = timer.ms()
+        n_iter, acc, mats, rates = once(mode)  # the checked outputs come from an untouched call
+        torch.cuda.synchronize()
+        par = Parity()
+        # reordered sums: the iteration count exact, the surface within 1e-12 relative (the
+        # error bound allows 4e-11 after 26 iterations; north_star's bar is 1e-6); in order: bit
+        # for bit
+        rtol = 0.0 if path[0] == 'sequential' else 1e-12
+        if check:  # the last call's counts, surface, iterations and the first batch's rates
+            if acc is None:  # row-sharded solve: the surface is checked, the counts are not held
+                from oracle import xt_oracle as xo
+                fit = xo.solve(ocnt, l, w)
+                xT = fit['xT']
+                par.exact('xT 105x68 iterations', n_iter + 1, len(fit['heatmaps']))
+                check_surface(par, 'xT 105x68', mats[3].cpu().numpy().reshape(w, l), xT, rtol)
+            else:
+                xT = check_xt(par, ocnt, acc, mats[3], n_iter, l, w, rtol)
+            if first is not None:
+                check_xt_rate(par, first, rates[0], xT, interp=True)
+                par.games += len(sample_games(len(first['game_off']) - 1))
+            par.merge(dist, dev)
+        wall = dt
+        if dist is not None:
+            wall = _reduce(dist, dt, dist.ReduceOp.MAX, dev)
+        msharded, msolve = mode
+        return {
+            'ms_fit_and_rate': round(wall * 1e3, 3), 'actions_per_s': round(total / wall, 1),
+            'iterations': n_iter,
+            'timing': f'median of {nreps} calls (wall clock around each, after a warm-up call; '
                       f'min {min(times) * 1e3:.3f}, max {max(times) * 1e3:.3f} ms on rank {rank})'
                       + ('; max over ranks' if dist is not None else ''),
-            'scaling': 'strong' if cfg5_games > 0 else 'weak',
             'solve': (('band-sharded (all-to-all of counted actions, '
-                       + ('compact rows all-gathered once, replicated iteration)' if solve == 'compact'
+                       + ('compact rows all-gathered once, replicated iteration)' if msolve == 'compact'
                           else 'row-sharded iteration)'))
-                      if (sharded and dist is not None) else 'replicated'),
+                      if (msharded and dist is not None) else
+                      ('replicated (one all-reduce of the dense counts)' if dist is not None else
+                       'one GPU (compact count rows only, no dense table)')),
             'phases_ms': dict(phases, note='one extra call synchronised between phases (rank '
                               f'{rank}): count = band buckets + table; exchange = the counts\' '
                               'all-reduce (band-sharded: count and exchange inside solve); '
                               'solve = normalise + value '
                               'iteration incl. its host syncs; rate'),
-            'pipeline': 'band-owned count (per batch: one key per counted action, bucketed by '
-                        'start-cell band; the 7140^2 table written once, no global atomics) '
-                        'writing each action\'s 8-B interpolated-rate operand; value iteration '
-                        'over the compact count rows; rate from the operands (LDS surface)',
-            **({'exchange': dict(xstats, rank=rank)} if xstats else {}),
+            'phase_events_ms': dict(events, note=f'HIP events around each phase of one more call '
+                                    f'(rank {rank}; current stream, the collectives ordered on it)'),
+            **({'exchange': {k: v for k, v in dict(xstats, rank=rank).items() if k != 'timer'}}
+               if (msharded and dist is not None and xstats) else {}),
             'solve_path': path[0] + (' (one launch, rows summed in a fixed parallel order under '
                                      'an error bound that keeps every convergence decision)'
                                      if path[0] == 'reordered' else ''),
@@ -629,6 +652,24 @@ def xt105_extra(ab, dist, dev, sharded: bool = False, cfg5_games: int = 62500,
                                                   f'{rtol:g} relative, iteration count exact'),
                                surface_max_rel_err=float(f"{getattr(par, 'surface_rel_err', 0.0):.3e}"))}
                if check else {})}
+
+    main = run((sharded, solve), reps)
+    games = (f'{cfg5_games:,} synthetic games over {world} rank(s)' if cfg5_games > 0 else
+             'the step batch')
+    out = {'workload': f'cfg5: xT 105x68 fit (count + all-reduce + value iteration) + '
+                       f'rate(use_interpolation=True) of {games}',
+           'actions_per_gpu': n, 'actions_total': total,
+           'scaling': 'strong' if cfg5_games > 0 else 'weak',
+           'pipeline': 'band-owned count (per batch: one key per counted action, bucketed by '
+                       'start-cell band; the 7140^2 table written once, no global atomics) '
+                       'writing each action\'s 8-B interpolated-rate operand; value iteration '
+                       'over the compact count rows; rate from the operands (LDS surface)',
+           **main}
+    if dist is not None and sharded:
+        # north_star's all-reduce-only scheme beside the band-sharded default, on the same
+        # batches: the departure is judged by measurement
+        out['compare_replicated'] = run((False, 'compact'), max(5, reps // 3))
+    return out
 
 
 def rotate_extra(args, dist, dev, d, ps, pc, inp, step, n, total_actions, world) -> dict:

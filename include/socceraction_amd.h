@@ -303,10 +303,11 @@ int sa_xt_rate_cells(const uint32_t* cells, int64_t n, int32_t l, int32_t w, con
 /* Band-owned count of large grids (203 <= C <= ~12000 cells, e.g. 105 x 68; sa_xt_band_shape
  * says whether a grid takes it): the transition counts without global atomics.  sa_xt_count,
  * sa_xt_count_codes and sa_xt_count_cells use it internally for such grids; a fit over several
- * device batches calls, per batch, sa_xt_count_bucket -- one 4-B key per counted action
- * (start cell << 16 | end cell, or C / C+1 / C+2 for a shot / scored shot / move without a
- * transition), sorted by start-cell band into buckets[n] (u32) with band_off[NB + 1] (int64,
- * device) -- then ONCE sa_xt_count_from_buckets over every batch's buckets, which adds (or with
+ * device batches calls, per batch, sa_xt_count_bucket -- one key per counted action, sorted by
+ * start-cell band into buckets[n] (u16: the action's bin in its band's R x P histogram,
+ * (start cell - band * R) * P + slot, slot = the end cell of a successful move or C / C+1 / C+2
+ * for a shot / scored shot / move without a transition; R = rows per band of sa_xt_band_shape,
+ * P = C + 3 rounded up to a multiple of 4) with band_off[NB + 1] (int64, device) -- then ONCE sa_xt_count_from_buckets over every batch's buckets, which adds (or with
  * SA_XT_COUNT_OVERWRITE writes) shot / goal / move and the C x C transition counts exactly as
  * sa_xt_count over all the batches would; err_flags as sa_xt_count, set by the bucket call.
  * `cells` (C <= SA_XT_CELLS_MAX_C) replaces the coordinates of `a` when not NULL (then `a` may
@@ -316,7 +317,7 @@ int sa_xt_rate_cells(const uint32_t* cells, int64_t n, int32_t l, int32_t w, con
 #define SA_XT_COUNT_OVERWRITE 2
 int sa_xt_band_shape(int32_t l, int32_t w, int32_t* rows_per_band, int32_t* n_bands);
 int sa_xt_count_bucket(const sa_actions* a, const uint32_t* cells, int64_t n, int32_t l, int32_t w,
-                       uint32_t* buckets, int64_t* band_off, int32_t* err_flags, uint32_t* codes,
+                       uint16_t* buckets, int64_t* band_off, int32_t* err_flags, uint32_t* codes,
                        uint64_t* interp_codes, int32_t L, int32_t W, void* stream);
 /* The band-owned count of bands [band0, band0 + nbands) only (a rank's row block in the
  * row-sharded multi-GPU fit: its bands' keys gathered from every rank by an all-to-all).  Set k's
@@ -324,7 +325,7 @@ int sa_xt_count_bucket(const sa_actions* a, const uint32_t* cells, int64_t n, in
  * band_off[k] holding nbands + 1 entries; the outputs hold the rows from band0 * R on (R from
  * sa_xt_band_shape): shot / goal / move_rows [min(nbands R, C - band0 R)], trans_rows
  * [that many rows x C].  flags: SA_XT_COUNT_OVERWRITE or 0 (add). */
-int sa_xt_count_band_rows(int32_t nsets, const uint32_t* const* buckets,
+int sa_xt_count_band_rows(int32_t nsets, const uint16_t* const* buckets,
                           const int64_t* const* band_off, int32_t l, int32_t w, int32_t band0,
                           int32_t nbands, int64_t* shot_rows, int64_t* goal_rows,
                           int64_t* move_rows, int32_t* trans_rows, int32_t flags, void* stream);
@@ -346,7 +347,7 @@ int sa_xt_rate_interp_codes_many(int32_t nsets, const uint64_t* const* interp_co
                                  const double* cy, int32_t l, int32_t w, const double* xs,
                                  int32_t L, const double* ys, int32_t W, double* const* out,
                                  int32_t* err_flags, void* stream);
-int sa_xt_count_from_buckets(int32_t nsets, const uint32_t* const* buckets,
+int sa_xt_count_from_buckets(int32_t nsets, const uint16_t* const* buckets,
                              const int64_t* const* band_off, int32_t l, int32_t w, int64_t* shot,
                              int64_t* goal, int64_t* move, int32_t* trans, int32_t flags,
                              void* stream);
@@ -361,7 +362,7 @@ int sa_xt_count_from_buckets(int32_t nsets, const uint32_t* const* buckets,
  * / move, ell and row_len are written in full.  (A fit that reads only the compact rows: no
  * 4 C^2-byte flush, 204 MB at 105 x 68.) */
 #define SA_XT_COUNT_COMPACT_ONLY 4
-int sa_xt_count_from_buckets_ex(int32_t nsets, const uint32_t* const* buckets,
+int sa_xt_count_from_buckets_ex(int32_t nsets, const uint16_t* const* buckets,
                                 const int64_t* const* band_off, int32_t l, int32_t w,
                                 int64_t* shot, int64_t* goal, int64_t* move, int32_t* trans,
                                 int32_t flags, uint32_t* ell, int32_t* row_len, void* stream);

@@ -35,7 +35,7 @@ def main():
     axes = ops.xt_interp_axes(l, w, dev)
 
     def once():
-        acc = ops.xt_count_many(bs, l, w, interp_codes=ic)
+        acc = ops.xt_count_many(bs, l, w, interp_codes=ic, dense=False)
         sol = ops.xt_solve(acc, transition=False)
         xT = sol.mats[3].reshape(w, l)
         ops.xt_rate_interp_codes_many(ic, [b.n for b in bs], xT, l, w, 1050, 680, axes=axes,

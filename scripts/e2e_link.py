@@ -1,0 +1,76 @@
+"""Where bench.py's end_to_end entry (pandas in -> pandas out, 1000 games) spends its time,
+against the host link: pinned H2D / D2H GB/s measured in-process, then each stage of the
+drop-in batched calls (encode + H2D, kernels, D2H, DataFrame assembly), synchronised between
+stages.  Prints one JSON line."""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from socceraction_amd import ops, synthetic, vaep  # noqa: E402
+from socceraction_amd.batch import ActionBatch  # noqa: E402
+
+
+def link_rates(nbytes=1 << 30, reps=5):
+    dev = torch.empty(nbytes, dtype=torch.uint8, device='cuda')
+    host = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+    out = {}
+    for name, dst, src in (('d2h', host, dev), ('h2d', dev, host)):
+        t = []
+        for _ in range(reps):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            dst.copy_(src, non_blocking=True)
+            torch.cuda.synchronize()
+            t.append(time.perf_counter() - t0)
+        out[name + '_GBs'] = round(nbytes / min(t) / 1e9, 2)
+    return out
+
+
+def main():
+    games = int(sys.argv[1]) if len(sys.argv) > 1 else 1000
+    rec = link_rates()
+    d = synthetic.spadl_games(games)
+    actions = synthetic.to_frame(d)
+    gframe = synthetic.games_frame(d)
+    home_of = gframe.set_index('game_id')['home_team_id']
+    model = vaep.VAEP()
+    n = len(actions)
+    for _ in range(3):
+        stage = {}
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ab = ActionBatch.from_frame(actions, home_team_id=home_of, segments='game')
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        fb = ops.features(ab, model._split_xfns()[0], 3)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        b, f, i = fb.to_numpy()
+        t3 = time.perf_counter()
+        from socceraction_amd.catalog import assemble_frame
+        import pandas as pd
+        X = assemble_frame(fb.plan, b, f, i, n, pd.RangeIndex(n))
+        t4 = time.perf_counter()
+        t5 = time.perf_counter()
+        X2 = model.compute_features_batch(gframe, actions)
+        t6 = time.perf_counter()
+        Y = model.compute_labels_batch(gframe, actions)
+        t7 = time.perf_counter()
+        stage = {'encode_h2d_s': t1 - t0, 'kernels_s': t2 - t1, 'd2h_s': t3 - t2,
+                 'assemble_s': t4 - t3, 'features_batch_s': t6 - t5, 'labels_batch_s': t7 - t6,
+                 'd2h_bytes': int(b.nbytes + f.nbytes + i.nbytes)}
+        assert X.shape == X2.shape == (n, 568) and len(Y) == n
+    stage = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in stage.items()}
+    stage['d2h_GBs_in_path'] = round(stage['d2h_bytes'] / stage['d2h_s'] / 1e9, 2)
+    print(json.dumps({'actions': n, **rec, **stage}), flush=True)
+
+
+if __name__ == '__main__':
+    main()

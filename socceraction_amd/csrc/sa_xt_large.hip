@@ -6,7 +6,7 @@
 //    the memory side, one uncached request per lane (MI355X_MICROARCH.md "Global float atomics":
 //    64 lanes in 64 rows ~0.08 TB/s); the round-3 XC_VEC pass sat on that ceiling (0.446 ms per
 //    16M actions).  Here the start cells are cut into bands of R consecutive cells and every
-//    counted action becomes one 4-B key (start cell << 16 | slot):
+//    counted action becomes one 4-B key (start cell << 16 | slot), bucketed as a 16-bit bin:
 //      K1 xt_keys_kernel        reads the actions once, writes each workgroup's keys contiguously
 //                               (wave ballots) and the keys per band;
 //      K3 xt_keys_scatter_kernel  the band offsets (every workgroup scans the band counts
@@ -47,9 +47,12 @@ namespace sa {
 #endif
 constexpr int XK_THREADS = SA_XK_THREADS;
 #ifndef SA_XK_U
-#define SA_XK_U 4  // K1 actions per thread per pass (coordinates; even)
+#define SA_XK_U 2  // K1 actions per thread per pass (coordinates; even; 4: 146.5 vs 143.4 us per 16M, r06k2)
 #endif
 static_assert(SA_XK_U >= 2 && SA_XK_U % 2 == 0 && SA_XK_U <= 16, "SA_XK_U");
+#ifndef SA_XK_PIPE
+#define SA_XK_PIPE 0  // 1: K1's coordinate passes software-pipelined (the next pass's loads issued
+#endif                //    before this pass's arithmetic; two register buffers, alternating)
 #ifndef SA_XK_BALANCE
 #define SA_XK_BALANCE 1  // K1 regions per batch rounded up to whole rounds of the CUs (shorter regions)
 #endif
@@ -90,6 +93,13 @@ constexpr int XB_MAX_SETS = 24;     // buckets per K4 launch
 constexpr size_t XB_LDS_STATIC = 1024 + (size_t)XB_MAX_ROWS * 256 * 4;
 static_assert(XB_MAX_ROWS * 8 + XB_MAX_SETS * 24 + XB_MAX_ROWS * 256 * 4 <= XB_LDS_STATIC, "K4 static LDS");
 constexpr uint32_t XB_NONE = 0xFFFFFFFFu;
+// A bucketed key (K3's output, K4's and the band exchange's input) is 16 bits: the key's bin in
+// its band's LDS histogram, (start cell - band * R) * P + slot -- K4 adds 1 at h[key] with no
+// decode.  R * P <= (160 KB - static) / 4 < 65535 for every band shape (static_assert below), so
+// 0xFFFF never is a bin.  Half the bytes of the 4-B keys K3 wrote before round 6 (K3's stores,
+// K4's loads and the multi-GPU all-to-all).
+typedef uint16_t xb_key_t;
+static_assert((XB_LDS_MAX - XB_LDS_STATIC) / 4 < 0xFFFFu, "a band's bins fit 16-bit bucket keys");
 constexpr uint32_t XE_CNT_ESC_K4 = 0xFFFFu;  // = XE_CNT_ESC: a count >= 65535 is read from the dense row
 static_assert(XS_PER * XS_THREADS * XS_SPLIT == XK_CHUNK && XS_PER >= 1, "K3 holds one part of a K1 region");
 static_assert(XS_PART * 4 + 2 * XB_NB_MAX * 4 + 256 <= XB_LDS_MAX, "K3 LDS");
@@ -183,7 +193,124 @@ __global__ __launch_bounds__(XK_THREADS) void xt_keys_kernel(sa_actions A, const
   const int lane = threadIdx.x & 63;
   int32_t bad = 0;
   constexpr int U = CELLS ? 8 : SA_XK_U;  // actions per thread per pass, every load issued first
-  for (int64_t base = begin; base < end; base += (int64_t)U * XK_THREADS) {  // wave-uniform bound
+  // the keys of one pass's actions: ballot ranks into the region, band histogram in LDS
+  auto emit_keys = [&](const XtAct (&act)[U]) {
+    uint32_t key[U];
+    bool has[U];
+    uint64_t m[U];
+    uint32_t tot = 0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      has[u] = band_key(act[u], S.C, key[u], bad);
+      m[u] = __ballot(has[u]);
+      tot += (uint32_t)__popcll(m[u]);
+    }
+    uint32_t wbase = 0;
+    if (lane == 0 && tot) wbase = atomicAdd(&cursor, tot);
+    wbase = __shfl(wbase, 0);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (has[u]) {
+        const uint32_t pos = wbase + lane_rank(m[u]);
+        SA_DGUARD(pos < XK_CHUNK, pos, continue);
+        if (!(SA_XK_PROBE & 2)) out[pos] = key[u];
+        if (!(SA_XK_PROBE & 1)) atomicAdd(&bh[band_of(key[u], S.magic)], 1u);
+      }
+      wbase += (uint32_t)__popcll(m[u]);
+    }
+  };
+  if constexpr (!CELLS && SA_XK_PIPE) {
+    if (vec) {  // wave-uniform
+      constexpr int Q = U / 2;  // pairs per thread per pass
+      struct Raw {
+        f64x2 a[Q], b[Q], c[Q], d[Q];
+        uint32_t ty[Q], rs[Q];
+      };
+      auto load = [&](Raw& R, int64_t base) {
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+          const int64_t j = base + 2 * ((int64_t)q * XK_THREADS + threadIdx.x);
+          const int64_t jc = j + 1 < end ? j : ((end - 2) & ~(int64_t)1);  // a whole aligned pair
+          R.a[q] = xk_ld(reinterpret_cast<const f64x2*>(F.c0 + jc));
+          R.b[q] = xk_ld(reinterpret_cast<const f64x2*>(F.c1 + jc));
+          R.c[q] = xk_ld(reinterpret_cast<const f64x2*>(F.c2 + jc));
+          R.d[q] = xk_ld(reinterpret_cast<const f64x2*>(F.c3 + jc));
+          R.ty[q] = xk_ld(reinterpret_cast<const uint16_t*>(F.type_id + jc));
+          R.rs[q] = xk_ld(reinterpret_cast<const uint16_t*>(F.result_id + jc));
+        }
+      };
+      auto pass = [&](const Raw& R, int64_t base) {
+        int tt[U], rr[U];
+        double sx[U], sy[U], ex[U], ey[U];
+        int64_t jj[U];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+          const int64_t j = base + 2 * ((int64_t)q * XK_THREADS + threadIdx.x);
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const int u = 2 * q + e;
+            jj[u] = j + e;
+            sx[u] = R.a[q][e];
+            sy[u] = R.b[q][e];
+            ex[u] = R.c[q][e];
+            ey[u] = R.d[q][e];
+            tt[u] = (int)((R.ty[q] >> (8 * e)) & 0xFF);
+            rr[u] = (int)((R.rs[q] >> (8 * e)) & 0xFF);
+          }
+          if (j + 1 >= end) {  // the batch's odd last action (or none): scalar, the rest not counted
+            const int64_t k = j < end ? j : end - 1;
+            sx[2 * q] = F.c0[k];
+            sy[2 * q] = F.c1[k];
+            ex[2 * q] = F.c2[k];
+            ey[2 * q] = F.c3[k];
+            tt[2 * q] = j < end ? (int)F.type_id[k] : -1;
+            rr[2 * q] = F.result_id[k];
+            tt[2 * q + 1] = -1;
+          }
+        }
+        BinQ bq[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) bq[u] = bin_q(sx[u], sy[u], ex[u], ey[u]);
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+          const int u = 2 * q;
+          const int64_t j = jj[u];
+          if (RO.codes && tt[u] >= 0) {
+            const uint32_t c0 = rate_code_q(tt[u], rr[u], sx[u], sy[u], ex[u], ey[u], bq[u], l, w);
+            if (tt[u + 1] >= 0)
+              *reinterpret_cast<uint2*>(RO.codes + j) = make_uint2(
+                  c0, rate_code_q(tt[u + 1], rr[u + 1], sx[u + 1], sy[u + 1], ex[u + 1], ey[u + 1], bq[u + 1], l, w));
+            else
+              RO.codes[j] = c0;
+          }
+          if (RO.icodes && tt[u] >= 0) {
+            const uint64_t c0 = rate_icode_q(tt[u], rr[u], sx[u], sy[u], ex[u], ey[u], bq[u], RO.L, RO.W);
+            if (tt[u + 1] >= 0)
+              xk_st(reinterpret_cast<u64x2*>(RO.icodes + j),
+                    u64x2{c0, rate_icode_q(tt[u + 1], rr[u + 1], sx[u + 1], sy[u + 1], ex[u + 1], ey[u + 1], bq[u + 1],
+                                           RO.L, RO.W)});
+            else
+              RO.icodes[j] = c0;
+          }
+        }
+        XtAct act[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) act[u] = act_from_row_q(tt[u], rr[u], sx[u], sy[u], ex[u], ey[u], bq[u], l, w);
+        emit_keys(act);
+      };
+      const int64_t step = (int64_t)U * XK_THREADS;
+      Raw ra, rb;  // alternate: no register copy of a load in flight
+      load(ra, begin);
+      for (int64_t base = begin; base < end; base += 2 * step) {  // wave-uniform bounds
+        if (base + step < end) load(rb, base + step);
+        pass(ra, base);
+        if (base + step >= end) break;
+        if (base + 2 * step < end) load(ra, base + 2 * step);
+        pass(rb, base + step);
+      }
+    }
+  }
+  for (int64_t base = begin; base < end && !(!CELLS && SA_XK_PIPE && vec); base += (int64_t)U * XK_THREADS) {
     XtAct act[U];
     if (CELLS) {
       uint32_t cv[U];
@@ -287,29 +414,7 @@ __global__ __launch_bounds__(XK_THREADS) void xt_keys_kernel(sa_actions A, const
 #pragma unroll
       for (int u = 0; u < U; ++u) act[u] = act_from_row_q(tt[u], rr[u], sx[u], sy[u], ex[u], ey[u], bq[u], l, w);
     }
-    uint32_t key[U];
-    bool has[U];
-    uint64_t m[U];
-    uint32_t tot = 0;
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      has[u] = band_key(act[u], S.C, key[u], bad);
-      m[u] = __ballot(has[u]);
-      tot += (uint32_t)__popcll(m[u]);
-    }
-    uint32_t wbase = 0;
-    if (lane == 0 && tot) wbase = atomicAdd(&cursor, tot);
-    wbase = __shfl(wbase, 0);
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (has[u]) {
-        const uint32_t pos = wbase + lane_rank(m[u]);
-        SA_DGUARD(pos < XK_CHUNK, pos, continue);
-        if (!(SA_XK_PROBE & 2)) out[pos] = key[u];
-        if (!(SA_XK_PROBE & 1)) atomicAdd(&bh[band_of(key[u], S.magic)], 1u);
-      }
-      wbase += (uint32_t)__popcll(m[u]);
-    }
+    emit_keys(act);
   }
   if (bad) atomicOr(err, bad);
   __syncthreads();
@@ -368,7 +473,7 @@ __global__ __launch_bounds__(XS_THREADS) void xt_keys_scatter_kernel(const uint3
                                                                      XbShape S, const uint32_t* __restrict__ band_cnt,
                                                                      int64_t* __restrict__ band_off,
                                                                      uint32_t* __restrict__ cursor,
-                                                                     uint32_t* __restrict__ buckets) {
+                                                                     xb_key_t* __restrict__ buckets) {
   extern __shared__ uint32_t sm[];
   uint32_t* bh = sm;              // [NB] keys per band, then the local run offsets
   uint32_t* bb = sm + S.NB;       // [NB] the bands' offsets, then the runs' places in the buckets
@@ -423,12 +528,13 @@ __global__ __launch_bounds__(XS_THREADS) void xt_keys_scatter_kernel(const uint3
     const uint32_t key = sorted[i];
     const uint32_t b = band_of(key, S.magic);
     SA_DGUARD(b < (uint32_t)S.NB, b, continue);
-    buckets[bb[b] + (i - bh[b])] = key;
+    // the key's bin in its band's histogram (K4's LDS index): row within the band, slot
+    buckets[bb[b] + (i - bh[b])] = (xb_key_t)(((key >> 16) - b * (uint32_t)S.R) * (uint32_t)S.P + (key & 0xFFFFu));
   }
 }
 
 struct XbSets {
-  const uint32_t* keys[XB_MAX_SETS];
+  const xb_key_t* keys[XB_MAX_SETS];
   const int64_t* off[XB_MAX_SETS];
   int n;
 };
@@ -508,7 +614,7 @@ __global__ __launch_bounds__(XB_THREADS) void xt_band_count_kernel(XbSets sets, 
   // waited out a memory latency per 4 keys and per set: 148 us per cfg5 table pass).  Set
   // bounds and key pointers in LDS (global address space: no FLAT loads, whose lgkmcnt would
   // tie them to the LDS reads)
-  typedef const uint32_t __attribute__((address_space(1)))* gkeys;
+  typedef const xb_key_t __attribute__((address_space(1)))* gkeys;
   __shared__ gkeys kb[XB_MAX_SETS];
   __shared__ int64_t klo[XB_MAX_SETS], khi[XB_MAX_SETS];
   const int ns = sets.n;
@@ -543,16 +649,15 @@ __global__ __launch_bounds__(XB_THREADS) void xt_band_count_kernel(XbSets sets, 
 #pragma unroll
     for (int u = 0; u < XB_U; ++u) {
       const int64_t j = ti + u * XB_THREADS + threadIdx.x;
-      v[u] = j < hi ? kp[j] : XB_NONE;
+      v[u] = j < hi ? (uint32_t)kp[j] : XB_NONE;
     }
   };
   auto count = [&](const uint32_t (&v)[XB_U]) {
 #pragma unroll
     for (int u = 0; u < XB_U; ++u)
-      if (v[u] != XB_NONE) {
-          const int row = (int)(v[u] >> 16) - r0, slot = (int)(v[u] & 0xFFFFu);
-          SA_DGUARD(row >= 0 && row < nr && slot < C + 3, v[u], continue);
-          atomicAdd(&h[row * P + slot], 1u);
+      if (v[u] != XB_NONE) {  // the key is the bin (K3: row within the band * P + slot)
+          SA_DGUARD(v[u] < (uint32_t)(nr * P) && (int)(v[u] % (uint32_t)P) < C + 3, v[u], continue);
+          atomicAdd(&h[v[u]], 1u);
         }
   };
   int sa = 0, sb;
@@ -1520,7 +1625,7 @@ static bool xt_band_shape(int C, XbShape* s) {
 
 // K1 -> K2 -> K3 of one batch: its keys sorted into buckets[] by band, band_off[NB + 1].
 static int bucket_batch(const sa_actions& A, const uint32_t* cells, int64_t n, int l, int w, const XbShape& S,
-                        uint32_t* buckets, int64_t* band_off, int32_t* err, const XkRate& RO, hipStream_t st) {
+                        xb_key_t* buckets, int64_t* band_off, int32_t* err, const XkRate& RO, hipStream_t st) {
   // K1 runs one workgroup per CU: a batch's regions in whole rounds of the CUs (16M actions:
   // 489 regions of 32768 -> 512 of 31,488; a 4M tail: 123 -> 256), regions of >= 4096 actions
   int64_t regions = (n + XK_CHUNK - 1) / XK_CHUNK, chunk = XK_CHUNK;
@@ -1571,7 +1676,7 @@ static int bucket_batch(const sa_actions& A, const uint32_t* cells, int64_t n, i
   return rc;
 }
 
-static int count_from_buckets(int nsets, const uint32_t* const* buckets, const int64_t* const* band_off,
+static int count_from_buckets(int nsets, const xb_key_t* const* buckets, const int64_t* const* band_off,
                               const XbShape& S, int band0, int nbands, int64_t* shot, int64_t* goal, int64_t* move,
                               int32_t* trans, int overwrite, hipStream_t st, uint32_t* ell = nullptr,
                               int32_t* row_len = nullptr, int dense = 1) {
@@ -1608,14 +1713,14 @@ int xt_count_bands(const sa_actions& A, const uint32_t* cells, int64_t n, int l,
   XbShape S;
   if (!xt_band_shape(l * w, &S)) return fail(SA_EINVAL, "grid outside the band-owned count");
   Scratch sc;  // buckets [n] | band_off [NB + 1]
-  const size_t bb = ((size_t)n * 4 + 255) & ~(size_t)255;
+  const size_t bb = ((size_t)n * sizeof(xb_key_t) + 255) & ~(size_t)255;
   int rc = scratch_acquire(bb + ((size_t)S.NB + 1) * 8, st, &sc);
   if (rc) return rc;
-  uint32_t* buckets = static_cast<uint32_t*>(sc.ptr);
+  xb_key_t* buckets = static_cast<xb_key_t*>(sc.ptr);
   int64_t* band_off = reinterpret_cast<int64_t*>(static_cast<char*>(sc.ptr) + bb);
   rc = bucket_batch(A, cells, n, l, w, S, buckets, band_off, err, XkRate{codes, nullptr, 0, 0}, st);
   if (!rc) {
-    const uint32_t* bk[1] = {buckets};
+    const xb_key_t* bk[1] = {buckets};
     const int64_t* bo[1] = {band_off};
     rc = count_from_buckets(1, bk, bo, S, 0, S.NB, shot, goal, move, trans, 0, st);
   }
@@ -1804,7 +1909,7 @@ extern "C" int sa_xt_band_shape(int32_t l, int32_t w, int32_t* rows_per_band, in
 }
 
 extern "C" int sa_xt_count_bucket(const sa_actions* a, const uint32_t* cells, int64_t n, int32_t l, int32_t w,
-                                  uint32_t* buckets, int64_t* band_off, int32_t* err_flags, uint32_t* codes,
+                                  uint16_t* buckets, int64_t* band_off, int32_t* err_flags, uint32_t* codes,
                                   uint64_t* interp_codes, int32_t L, int32_t W, void* stream) {
   if (l < 1 || w < 1 || (int64_t)l * w > 46340) return fail(SA_EINVAL, "bad l or w");
   XbShape S;
@@ -1835,14 +1940,14 @@ extern "C" int sa_xt_count_bucket(const sa_actions* a, const uint32_t* cells, in
                       XkRate{codes, interp_codes, L, W}, st);
 }
 
-extern "C" int sa_xt_count_from_buckets(int32_t nsets, const uint32_t* const* buckets, const int64_t* const* band_off,
+extern "C" int sa_xt_count_from_buckets(int32_t nsets, const uint16_t* const* buckets, const int64_t* const* band_off,
                                         int32_t l, int32_t w, int64_t* shot, int64_t* goal, int64_t* move,
                                         int32_t* trans, int32_t flags, void* stream) {
   return sa_xt_count_from_buckets_ex(nsets, buckets, band_off, l, w, shot, goal, move, trans, flags, nullptr, nullptr,
                                      stream);
 }
 
-extern "C" int sa_xt_count_from_buckets_ex(int32_t nsets, const uint32_t* const* buckets,
+extern "C" int sa_xt_count_from_buckets_ex(int32_t nsets, const uint16_t* const* buckets,
                                            const int64_t* const* band_off, int32_t l, int32_t w, int64_t* shot,
                                            int64_t* goal, int64_t* move, int32_t* trans, int32_t flags,
                                            uint32_t* ell, int32_t* row_len, void* stream) {
@@ -1868,7 +1973,7 @@ extern "C" int sa_xt_count_from_buckets_ex(int32_t nsets, const uint32_t* const*
                             (flags & SA_XT_COUNT_COMPACT_ONLY) ? 0 : 1);
 }
 
-extern "C" int sa_xt_count_band_rows(int32_t nsets, const uint32_t* const* buckets, const int64_t* const* band_off,
+extern "C" int sa_xt_count_band_rows(int32_t nsets, const uint16_t* const* buckets, const int64_t* const* band_off,
                                      int32_t l, int32_t w, int32_t band0, int32_t nbands, int64_t* shot_rows,
                                      int64_t* goal_rows, int64_t* move_rows, int32_t* trans_rows, int32_t flags,
                                      void* stream) {

@@ -477,7 +477,7 @@ def xt_band_shape(l: int, w: int) -> Optional[Tuple[int, int]]:
 @dataclass
 class XTBuckets:
     """One batch's counted actions sorted by start-cell band (``sa_xt_count_bucket``)."""
-    keys: torch.Tensor      # u32 (as int32) [n]
+    keys: torch.Tensor      # u16 (as int16) [n]: each key's bin in its band's histogram
     band_off: torch.Tensor  # int64 [n_bands + 1]
 
 
@@ -504,7 +504,7 @@ def xt_bucket(batch: Optional[ActionBatch], l: int, w: int, err: torch.Tensor,
     if shape is None:
         raise ValueError(f'the band-owned count does not take a {l} x {w} grid')
     dev = err.device
-    keys = torch.empty(max(n, 16), dtype=torch.int32, device=dev)
+    keys = torch.empty(max(n, 16), dtype=torch.int16, device=dev)  # u16 bins (sa_xt_count_bucket)
     off = torch.empty(shape[1] + 1, dtype=torch.int64, device=dev)
     s = batch.struct() if cells is None else None
     _native.check(_native.lib().sa_xt_count_bucket(

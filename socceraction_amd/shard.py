@@ -9,10 +9,51 @@ solves the identical system.
 """
 from __future__ import annotations
 
+import contextlib
+import time
 from typing import List, Tuple
 
 import numpy as np
 import torch
+
+
+class PhaseTimes:
+    """Per-phase times of a multi-rank fit (its exchange steps and kernels): a HIP event pair on
+    torch's current stream around each phase on a GPU (the collectives' device work is ordered
+    on that stream: RCCL's calls make it wait for them), the wall clock on the host otherwise
+    (gloo on CPU tensors).  ``ms()`` synchronises once and sums each phase's pairs."""
+
+    def __init__(self, device=None):
+        dev = torch.device(device) if device is not None else None
+        self.cuda = dev is not None and dev.type == 'cuda'
+        self.ev = {}
+        self.wall = {}
+
+    @contextlib.contextmanager
+    def phase(self, name: str):
+        if self.cuda:
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            yield
+            b.record()
+            self.ev.setdefault(name, []).append((a, b))
+        else:
+            t0 = time.perf_counter()
+            yield
+            self.wall[name] = self.wall.get(name, 0.0) + (time.perf_counter() - t0) * 1e3
+
+    def ms(self) -> dict:
+        if self.cuda:
+            torch.cuda.synchronize()
+        out = {k: sum(a.elapsed_time(b) for a, b in v) for k, v in self.ev.items()}
+        out.update(self.wall)
+        return {k: round(v, 3) for k, v in out.items()}
+
+
+def _phase(stats, name: str):
+    """``stats['timer'].phase(name)`` when the caller passed a :class:`PhaseTimes`, else a no-op."""
+    t = stats.get('timer') if stats is not None else None
+    return t.phase(name) if t is not None else contextlib.nullcontext()
 
 
 def partition_games(game_off: np.ndarray, world: int) -> List[Tuple[int, int]]:
@@ -113,6 +154,10 @@ def _all_to_all(out: torch.Tensor, inp: torch.Tensor, out_splits=None, in_splits
     """out = the concatenation over ranks q of the part of q's ``inp`` meant for this rank
     (``in_splits`` / ``out_splits``: element counts per rank; None: equal parts)."""
     import torch.distributed as dist
+    if out.dtype == torch.int16:  # neither RCCL nor gloo takes int16: move the bytes
+        sz = lambda sp: None if sp is None else [2 * int(x) for x in sp]  # noqa: E731
+        return _all_to_all(out.view(torch.uint8), inp.contiguous().view(torch.uint8),
+                           sz(out_splits), sz(in_splits), group)
     if _on_device(group):
         dist.all_to_all_single(out, inp, out_splits, in_splits, group=group)
     else:
@@ -239,9 +284,10 @@ def xt_fit_bands_sharded(batches, l: int, w: int, eps: float = 1e-5, max_iter: i
     tables.  Rank r owns the start-cell bands [b0, b1) = ``band_ranges(NB, world)[r]``, i.e.
     the count rows [b0 R, b1 R).
 
-    1. every rank buckets its own batches (``sa_xt_count_bucket``: one 4-B key per counted
-       action, sorted by band, so each destination's keys are one contiguous range);
-    2. one all-to-all of the keys (about 3.4 B per action: ~37 MB per rank at 1e8 actions over 8
+    1. every rank buckets its own batches (``sa_xt_count_bucket``: one 16-bit key per counted
+       action -- its bin in its band's histogram -- sorted by band, so each destination's keys
+       are one contiguous range);
+    2. one all-to-all of the keys (about 1.7 B per action: ~19 MB per rank at 1e8 actions over 8
        ranks, against 204 MB x 2 (W-1) / W for the table's all-reduce) and one of the band offsets;
     3. each rank counts its own bands from every rank's keys (``sa_xt_count_band_rows``: the B x C
        rows written once from LDS, no global atomics) -- the same row block the reduce-scatter of
@@ -285,23 +331,27 @@ def xt_fit_bands_sharded(batches, l: int, w: int, eps: float = 1e-5, max_iter: i
     dev = batches[0].device if batches else torch.device('cuda', torch.cuda.current_device())
     err = torch.zeros(1, dtype=torch.int32, device=dev)
     ic = list(interp_codes) if interp_codes is not None else [None] * len(batches)
-    parts = [ops.xt_bucket(b, l, w, err, interp_codes=c) for b, c in zip(batches, ic)]
-    sets_keys, sets_off = exchange_band_keys([(p.keys, p.band_off) for p in parts], NB, group, dev,
-                                             stats)
+    with _phase(stats, 'bucket'):  # K1 - K3 of this rank's batches
+        parts = [ops.xt_bucket(b, l, w, err, interp_codes=c) for b, c in zip(batches, ic)]
+    with _phase(stats, 'key_all_to_all'):  # headers (one host read), keys, band offsets
+        sets_keys, sets_off = exchange_band_keys([(p.keys, p.band_off) for p in parts], NB, group,
+                                                 dev, stats)
     nb = b1 - b0
-    rows = torch.zeros(B * C, dtype=torch.int32, device=dev)
-    vec = torch.zeros((3, B), dtype=torch.int64, device=dev)
-    kp = (ctypes.c_void_p * len(sets_keys))(*[t.data_ptr() for t in sets_keys])
-    op = (ctypes.c_void_p * len(sets_off))(*[t.data_ptr() for t in sets_off])
-    _native.check(_native.lib().sa_xt_count_band_rows(
-        len(sets_keys), kp, op, l, w, b0, nb, vec[0].data_ptr(), vec[1].data_ptr(),
-        vec[2].data_ptr(), rows.data_ptr(), _native.SA_XT_COUNT_OVERWRITE, stream_handle()))
-    allv = torch.empty((W, 3, B), dtype=torch.int64, device=dev)
-    _all_gather(allv.reshape(-1), vec.reshape(-1), group=group)
-    full = allv.permute(1, 0, 2).reshape(3, W * B)[:, :C].contiguous()
-    # the error bytes of every rank: summed, one byte per flag, like allreduce_xt_counts (a MAX
-    # of whole words would drop one rank's lower-byte flag behind another's higher one)
-    _all_reduce(err, group=group)
+    with _phase(stats, 'band_count'):  # K4 of this rank's bands
+        rows = torch.zeros(B * C, dtype=torch.int32, device=dev)
+        vec = torch.zeros((3, B), dtype=torch.int64, device=dev)
+        kp = (ctypes.c_void_p * len(sets_keys))(*[t.data_ptr() for t in sets_keys])
+        op = (ctypes.c_void_p * len(sets_off))(*[t.data_ptr() for t in sets_off])
+        _native.check(_native.lib().sa_xt_count_band_rows(
+            len(sets_keys), kp, op, l, w, b0, nb, vec[0].data_ptr(), vec[1].data_ptr(),
+            vec[2].data_ptr(), rows.data_ptr(), _native.SA_XT_COUNT_OVERWRITE, stream_handle()))
+    with _phase(stats, 'vector_all_gather'):  # shot / goal / move of every row, the error word
+        allv = torch.empty((W, 3, B), dtype=torch.int64, device=dev)
+        _all_gather(allv.reshape(-1), vec.reshape(-1), group=group)
+        full = allv.permute(1, 0, 2).reshape(3, W * B)[:, :C].contiguous()
+        # the error bytes of every rank: summed, one byte per flag, like allreduce_xt_counts (a
+        # MAX of whole words would drop one rank's lower-byte flag behind another's higher one)
+        _all_reduce(err, group=group)
     if solve not in ('compact', 'rows'):
         raise ValueError("solve must be 'compact' or 'rows'")
     res = None
@@ -318,7 +368,9 @@ def xt_fit_bands_sharded(batches, l: int, w: int, eps: float = 1e-5, max_iter: i
             stats['solve_path'] = 'sequential'
         if stats is not None and solve == 'rows':
             stats['exchange'] = 'all-to-all of counted actions + all-gather of x per iteration'
-        res = _solve_row_block(rows, full[0], full[1], full[2], C, B, eps, max_iter, group, batch)
+        with _phase(stats, 'row_sharded_solve'):  # incl. an all-gather of x per iteration
+            res = _solve_row_block(rows, full[0], full[1], full[2], C, B, eps, max_iter, group,
+                                   batch)
     mats, heat, iters = res
     return mats, heat, iters, err
 
@@ -387,27 +439,31 @@ def _solve_compact_exchange(rows, shot, goal, move, C: int, B: int, eps: float, 
     pe = int(lib.sa_xt_compact_bytes(C, 1)) // 4  # slots per compact row
     ell = torch.empty(max(nrows, 1) * pe, dtype=torch.int32, device=dev)
     slen = torch.zeros(B + 1, dtype=torch.int32, device=dev)  # [B] row lengths | escaped flag
-    if nrows:
-        _native.check(lib.sa_xt_compact_rows(ptr(rows), C, nrows, ptr(ell), ptr(slen), stream_handle()))
-        slen[B] = (rows[:nrows * C].max() >= 65535).to(torch.int32)
-    lens = torch.empty(W * (B + 1), dtype=torch.int32, device=dev)
-    _all_gather(lens, slen, group=group)
-    lens = lens.view(W, B + 1)
-    h = _to_host(lens, stats)  # the compact exchange's one host read
+    with _phase(stats, 'compact_build'):
+        if nrows:
+            _native.check(lib.sa_xt_compact_rows(ptr(rows), C, nrows, ptr(ell), ptr(slen),
+                                                 stream_handle()))
+            slen[B] = (rows[:nrows * C].max() >= 65535).to(torch.int32)
+    with _phase(stats, 'row_length_all_gather'):  # incl. the compact exchange's one host read
+        lens = torch.empty(W * (B + 1), dtype=torch.int32, device=dev)
+        _all_gather(lens, slen, group=group)
+        lens = lens.view(W, B + 1)
+        h = _to_host(lens, stats)
     if h[:, B].any():
         return None
     nch = (lens[:, :B].reshape(-1)[:C].to(torch.int64) + 127) // 128  # chunks of every row
     nch_h = ((h[:, :B].reshape(-1)[:C].astype(np.int64) + 127) // 128)
     rank_chunks = np.array([nch_h[q * B:min(C, (q + 1) * B)].sum() for q in range(W)], np.int64)
     mx = max(int(rank_chunks.max()), 1)
-    send = torch.zeros(mx * 128, dtype=torch.int32, device=dev)
-    if nrows:
-        mine = pack_compact_rows(ell, nch[r0:r0 + nrows], pe, int(rank_chunks[r]))
-        send[:mine.numel()] = mine
-    recv = torch.empty(W * mx * 128, dtype=torch.int32, device=dev)
-    _all_gather(recv, send, group=group)
-    full = torch.empty(C * pe, dtype=torch.int32, device=dev)
-    unpack_compact_rows(recv, mx, rank_chunks, nch, B, pe, full)
+    with _phase(stats, 'compact_all_gather'):  # pack, all-gather, unpack
+        send = torch.zeros(mx * 128, dtype=torch.int32, device=dev)
+        if nrows:
+            mine = pack_compact_rows(ell, nch[r0:r0 + nrows], pe, int(rank_chunks[r]))
+            send[:mine.numel()] = mine
+        recv = torch.empty(W * mx * 128, dtype=torch.int32, device=dev)
+        _all_gather(recv, send, group=group)
+        full = torch.empty(C * pe, dtype=torch.int32, device=dev)
+        unpack_compact_rows(recv, mx, rank_chunks, nch, B, pe, full)
     lens_c = lens[:, :B].reshape(-1)[:C].contiguous()
     if stats is not None:
         stats['compact_gathered_bytes'] = W * mx * 128 * 4
@@ -421,8 +477,9 @@ def _solve_compact_exchange(rows, shot, goal, move, C: int, B: int, eps: float, 
     # single-GPU fit's own solve, so the same bits); cnt_rows is read for counts >= 65535 only,
     # which no rank has (checked above)
     from .ops import xt_solve_compact
-    heat, iters, path = xt_solve_compact(full, lens_c, rows, move, gp[0], gp[1], C, eps, max_iter,
-                                         exact_order)
+    with _phase(stats, 'solve'):  # replicated: the same iteration on every rank
+        heat, iters, path = xt_solve_compact(full, lens_c, rows, move, gp[0], gp[1], C, eps,
+                                             max_iter, exact_order)
     if stats is not None:
         stats['solve_path'] = path
     if iters < 0:
@@ -475,6 +532,9 @@ def exchange_band_keys(parts, n_bands: int, group=None, dev=None, stats=None):
     rh = h[:W * (1 + _MAX_ROUNDS)].reshape(W, 1 + _MAX_ROUNDS)
     hcuts = h[W * (1 + _MAX_ROUNDS):].reshape(Rh, W + 1)
     rounds = int(rh[:, 0].max())
+    # the keys' dtype (int16 bins of sa_xt_count_bucket; any, for the host tests): the same on
+    # every rank, so a rank without batches takes the default
+    kdt = parts[0][0].dtype if parts else torch.int16
     if rounds > _MAX_ROUNDS:  # on every rank alike (every rank read the same batch counts)
         raise ValueError(f'at most {_MAX_ROUNDS} local batches per rank in one band exchange '
                          f'(a rank has {rounds})')
@@ -489,11 +549,11 @@ def exchange_band_keys(parts, n_bands: int, group=None, dev=None, stats=None):
             offs = offs - offs[:, :1]  # relative to each destination's first band
         else:  # nothing of this round here, but every rank takes part in every exchange
             send = np.zeros(W, np.int64)
-            keys = torch.zeros(0, dtype=torch.int32, device=dev)
+            keys = torch.zeros(0, dtype=kdt, device=dev)
             offs = torch.zeros((W, per + 1), dtype=torch.int64, device=dev)
         recv_n = rh[:, 1 + k].astype(np.int64)
         total = int(recv_n.sum())
-        recv = torch.empty(max(total, 1), dtype=torch.int32, device=dev)
+        recv = torch.empty(max(total, 1), dtype=kdt, device=dev)
         _all_to_all(recv[:total], keys.contiguous(), recv_n.tolist(), send.tolist(), group=group)
         roff = torch.empty((W, per + 1), dtype=torch.int64, device=dev)
         _all_to_all(roff.reshape(-1), offs.contiguous().reshape(-1), group=group)
@@ -504,7 +564,8 @@ def exchange_band_keys(parts, n_bands: int, group=None, dev=None, stats=None):
             sets_keys.append(recv[int(starts[q]):])
             sets_off.append(roff[q])
     if stats is not None:
-        stats['keys_sent_bytes'] = stats.get('keys_sent_bytes', 0) + 4 * sent
-        stats['keys_recv_bytes'] = stats.get('keys_recv_bytes', 0) + 4 * recvd
+        ks = torch.tensor([], dtype=kdt).element_size()
+        stats['keys_sent_bytes'] = stats.get('keys_sent_bytes', 0) + ks * sent
+        stats['keys_recv_bytes'] = stats.get('keys_recv_bytes', 0) + ks * recvd
         stats['exchange_rounds'] = rounds
     return sets_keys, sets_off

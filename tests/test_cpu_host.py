@@ -324,15 +324,16 @@ def test_xt_count_allreduce_gloo_world2():
 
 
 def _band_keys(rank, part, R, NB):
-    """Synthetic bucketed keys of one local batch: start cell << 16 | slot, sorted by band."""
+    """Synthetic bucketed keys of one local batch, int16 like sa_xt_count_bucket's bins, sorted
+    by band; for the test each key also names its band (band * 1000 + bin, bin < 1000)."""
     rng = np.random.default_rng([rank, part, 5])
     n = int(rng.integers(0, 400))
     cs = rng.integers(0, NB * R - 2, n)  # the last band is partial (C = NB R - 2)
-    keys = ((cs << 16) | rng.integers(0, 50, n)).astype(np.int64)
     band = cs // R
+    keys = (band * 1000 + (cs - band * R) * 100 + rng.integers(0, 50, n)).astype(np.int64)
     order = np.argsort(band, kind='stable')
     off = np.concatenate([[0], np.cumsum(np.bincount(band, minlength=NB))])
-    return keys[order].astype(np.uint32).view(np.int32), off.astype(np.int64)
+    return keys[order].astype(np.int16), off.astype(np.int64)
 
 
 _BAND_PARTS = {2: (2, 1), 3: (2, 0, 1)}  # local batches per rank: uneven, one rank with none
@@ -355,10 +356,10 @@ def _band_exchange_worker(rank, world, port, q):
     got = []
     for k, o in zip(keys, offs):
         o = o.numpy()
-        kk = k.numpy().view(np.uint32).astype(np.int64)
+        kk = k.numpy().astype(np.int64)
         for lb in range(b1 - b0):  # every key of local band lb belongs to band b0 + lb
             seg = kk[o[lb]:o[lb + 1]]
-            assert ((seg >> 16) // R == b0 + lb).all()
+            assert (seg // 1000 == b0 + lb).all()
             got.append(seg)
     q.put((rank, np.sort(np.concatenate(got)) if got else np.zeros(0, np.int64), len(keys)))
     dist.destroy_process_group()
@@ -391,10 +392,10 @@ def test_band_key_exchange_gloo(world):
         p.join(timeout=60)
         assert p.exitcode == 0
     R, NB = 3, 11
-    every = np.concatenate([_band_keys(r, k, R, NB)[0].view(np.uint32).astype(np.int64)
+    every = np.concatenate([_band_keys(r, k, R, NB)[0].astype(np.int64)
                             for r, nparts in enumerate(_BAND_PARTS[world]) for k in range(nparts)])
     for r, (b0, b1) in enumerate(shard.band_ranges(NB, world)):
-        band = (every >> 16) // R
+        band = every // 1000
         want = np.sort(every[(band >= b0) & (band < b1)])
         np.testing.assert_array_equal(res[r][0], want)
         assert res[r][1] == 2 * world  # two rounds (rank 0's batches) x every source rank
@@ -822,3 +823,21 @@ def test_staged_layout_restates_the_walk(depth):
     got = _eval_staged_layout(lay, te.roots, te.depths(), slot_feature, X, True, False, te.base_margin)
     with np.errstate(over='ignore'):
         np.testing.assert_array_equal(got, to.predict_xgboost_json(model, X))
+
+
+def test_phase_times_on_the_host():
+    """shard.PhaseTimes (the multi-rank fit's per-phase timer): wall clock per phase on the
+    host, summed over repeats; _phase is a no-op without a timer in the stats."""
+    import time as _t
+
+    from socceraction_amd import shard
+    pt = shard.PhaseTimes('cpu')
+    for _ in range(2):
+        with shard._phase({'timer': pt}, 'a'):
+            _t.sleep(0.01)
+    with shard._phase({'timer': pt}, 'b'):
+        pass
+    with shard._phase(None, 'c'), shard._phase({}, 'd'):
+        pass
+    ms = pt.ms()
+    assert set(ms) == {'a', 'b'} and ms['a'] >= 19 and ms['b'] >= 0

@@ -51,6 +51,19 @@ def test_bench_gpus_2_side_entries(solve):
     if solve != 'replicated':
         assert ('row-sharded' in x['solve']) == (solve == 'sharded-rows')
     assert x['parity']['ok'] and x['parity']['values_checked'] > 0
+    # per-phase HIP-event times of the exchange (DESIGN §6's projection is checked against them)
+    ev = x['phase_events_ms']
+    if solve == 'replicated':
+        assert ev['count_all_reduce'] > 0 and ev['solve'] > 0 and 'compare_replicated' not in x
+    else:
+        want = ('bucket', 'key_all_to_all', 'band_count', 'vector_all_gather') + (
+            ('compact_build', 'row_length_all_gather', 'compact_all_gather', 'solve')
+            if solve == 'sharded' else ('row_sharded_solve',))
+        assert all(ev[k] > 0 for k in want), ev
+        # north_star's all-reduce-only scheme measured beside the band-sharded default
+        rep = x['compare_replicated']
+        assert rep['solve'].startswith('replicated') and rep['parity']['ok']
+        assert rep['phase_events_ms']['count_all_reduce'] > 0 and rep['ms_fit_and_rate'] > 0
     a = out['atomic_cfg3']
     assert a['atomic_actions_total'] > a['atomic_actions_per_gpu'] > 0
     assert a['parity']['ok']
