@@ -661,7 +661,8 @@ int sa_tree_predict(const void* nodes, int32_t n_nodes, const int32_t* roots, co
  * bitmaps of sa_vaep_features_bits (bool_cols index its bitmaps; bits_stride a multiple of 8).
  * f32 bit 1 (f32 = 3): the f64 / i64 blocks hold float32 values (sa_vaep_features_bits_f32);
  * xgboost arithmetic only (bit 0 set), and the same probabilities bit for bit.
- * sa_tree_staged_lds_bytes: the LDS a model needs (<= 160 KiB; n_cond = 1 + n_bool + n_num). */
+ * sa_tree_staged_lds_bytes: the LDS a model needs at most (<= 160 KiB; n_cond = 1 + n_bool +
+ * n_num; the walk also stages the roots and depths, bounded here by n_nodes trees). */
 typedef struct sa_tree_model {
   const void* nodes;
   const void* leaf;
@@ -694,6 +695,12 @@ int sa_shutdown(void);
  * (hipDeviceMallocContiguous: the largest translation fragments).  Free with sa_device_free. */
 int sa_device_alloc(int64_t bytes, int32_t flags, void** out);
 int sa_device_free(void* p);
+/* Pitched asynchronous copy (hipMemcpy2DAsync, direction from the pointers): `height` rows of
+ * `width` bytes, row r from src + r * spitch to dst + r * dpitch.  The pandas boundary's
+ * pipeline copies a chunk's [cols x rows] output block into column-major host blocks of the
+ * whole frame with one DMA per block (socceraction_amd/pipeline.py). */
+int sa_copy2d_async(void* dst, int64_t dpitch, const void* src, int64_t spitch, int64_t width,
+                    int64_t height, void* stream);
 /* Stream-ordering and timing events for device-local work: created with
  * hipEventDisableSystemFence, so recording one does not write back and invalidate the GPU's
  * caches the way a default event does (its system-scope release is what a host or peer reader

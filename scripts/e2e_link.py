@@ -72,5 +72,57 @@ def main():
     print(json.dumps({'actions': n, **rec, **stage}), flush=True)
 
 
-if __name__ == '__main__':
+if __name__ == '__main__' and not (len(sys.argv) > 2 and sys.argv[2] == 'probe'):
     main()
+
+
+def pipeline_probe(games: int = 1000):
+    """VAEP.compute_batch's pieces: the pitched D2H alone (one chunk's blocks into the frame's
+    host blocks) against a contiguous D2H of the same bytes, the host encode of one chunk, and
+    the whole call with its chunk size varied."""
+    from socceraction_amd import _native, catalog
+    d = synthetic.spadl_games(games)
+    actions = synthetic.to_frame(d)
+    gframe = synthetic.games_frame(d)
+    model = vaep.VAEP()
+    n = len(actions)
+    p = synthetic.probabilities(n)
+    out = {}
+    plan = catalog.build_plan(model._split_xfns()[0], 3, False)
+    m = 1 << 18
+    fb = ops.alloc_feature_blocks(plan, m, 'cuda')
+    hb = torch.empty((plan.n_bool, n), dtype=torch.uint8, pin_memory=True)
+    hb1 = torch.empty((plan.n_bool, m), dtype=torch.uint8, pin_memory=True)
+    src = fb.bool_block[0]
+    lib = _native.lib()
+    s = torch.cuda.current_stream()
+    for name, fn in (('pitched_d2h_GBs', lambda: _native.check(lib.sa_copy2d_async(
+                         hb.data_ptr(), n, src.data_ptr(), src.shape[-1], m, plan.n_bool, s.cuda_stream))),
+                     ('contiguous_d2h_GBs', lambda: hb1.copy_(src[:, :m], non_blocking=True))):
+        t = []
+        for _ in range(5):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            fn()
+            torch.cuda.synchronize()
+            t.append(time.perf_counter() - t0)
+        out[name] = round(plan.n_bool * m / min(t) / 1e9, 2)
+    home_of = gframe.set_index('game_id')['home_team_id']
+    t0 = time.perf_counter()
+    sub = actions.iloc[:m]
+    ab = ActionBatch.from_frame(sub, home_team_id=home_of, segments='game')
+    torch.cuda.synchronize()
+    out['encode_h2d_ms_per_256k_rows'] = round((time.perf_counter() - t0) * 1e3, 2)
+    for chunk in (1 << 17, 1 << 18, 1 << 19, 1 << 21):
+        model.compute_batch(gframe, actions, p['scores'], p['concedes'], chunk_rows=chunk)
+        t = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            model.compute_batch(gframe, actions, p['scores'], p['concedes'], chunk_rows=chunk)
+            t.append(time.perf_counter() - t0)
+        out[f'compute_batch_ms_chunk_{chunk}'] = round(min(t) * 1e3, 2)
+    print(json.dumps({'pipeline_probe': out}), flush=True)
+
+
+if __name__ == '__main__' and len(sys.argv) > 2 and sys.argv[2] == 'probe':
+    pipeline_probe(int(sys.argv[1]))

@@ -2,7 +2,7 @@
 #   bash scripts/gpu_run.sh TAG STEP [STEP ...]
 # Steps run in order, each under its own time limit; the first failing step ends the run (no
 # retries).  Outputs land in gpurun_out/TAG_*.
-#   tests[:EXPR]      python -m pytest tests -m gpu (-k EXPR)      -> TAG_gpu_tests.log
+#   tests[:A,B,..]    python -m pytest tests -m gpu (-k "A or B")    -> TAG_gpu_tests.log
 #   smoke             __graft_entry__.smoke()                      -> TAG_smoke.log
 #   bench[:ARGS]      python bench.py ARGS (commas = spaces)       -> TAG_bench.json / .err
 #   prof              scripts/profile_round.sh TAG 10 (trace + PMC) -> gpurun_out/prof_TAG_*
@@ -20,7 +20,7 @@ for step in "$@"; do
   case $kind in
     tests)
       k=()
-      [ -n "$arg" ] && k=(-k "$arg")
+      [ -n "$arg" ] && k=(-k "${arg//,/ or }")  # commas: alternatives
       timeout -k 10 1000 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread "${k[@]}" \
         > gpurun_out/${tag}_gpu_tests.log 2>&1
       rc=$?

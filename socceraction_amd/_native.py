@@ -232,6 +232,8 @@ _SIGNATURES = {
                                               ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, _p]),
     'sa_device_alloc': (ctypes.c_int, [ctypes.c_int64, ctypes.c_int32, ctypes.POINTER(ctypes.c_void_p)]),
     'sa_device_free': (ctypes.c_int, [_p]),
+    'sa_copy2d_async': (ctypes.c_int, [_p, ctypes.c_int64, _p, ctypes.c_int64, ctypes.c_int64,
+                                       ctypes.c_int64, _p]),
     'sa_event_create': (ctypes.c_int, [ctypes.c_int32, ctypes.POINTER(ctypes.c_void_p)]),
     'sa_event_destroy': (ctypes.c_int, [_p]),
     'sa_event_record': (ctypes.c_int, [_p, _p]),

@@ -172,7 +172,10 @@ class ActionBatch:
             seg_off = segment_offsets(df['game_id'].to_numpy())
             if home_team_id is None:
                 homes = []
-            elif isinstance(home_team_id, (dict, pd.Series)):
+            elif isinstance(home_team_id, pd.Series):  # one vectorised lookup (KeyError if absent)
+                gids = df['game_id'].to_numpy()[seg_off[:-1]]
+                homes = list(home_team_id.loc[gids]) if len(gids) else []
+            elif isinstance(home_team_id, dict):
                 gids = df['game_id'].to_numpy()[seg_off[:-1]]
                 homes = [home_team_id[g] for g in gids]
             else:

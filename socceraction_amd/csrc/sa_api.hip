@@ -152,6 +152,16 @@ extern "C" int sa_device_free(void* p) {
   return p ? check_hip(hipFree(p), "sa_device_free: hipFree") : SA_OK;
 }
 
+extern "C" int sa_copy2d_async(void* dst, int64_t dpitch, const void* src, int64_t spitch, int64_t width,
+                               int64_t height, void* stream) {
+  if (height == 0 || width == 0) return SA_OK;
+  if (!dst || !src || width < 0 || height < 0 || dpitch < width || spitch < width)
+    return fail(SA_EINVAL, "sa_copy2d_async: bad pitched copy");
+  return check_hip(hipMemcpy2DAsync(dst, (size_t)dpitch, src, (size_t)spitch, (size_t)width, (size_t)height,
+                                    hipMemcpyDefault, (hipStream_t)stream),
+                   "sa_copy2d_async: hipMemcpy2DAsync");
+}
+
 extern "C" int sa_event_create(int32_t timing, void** ev) {
   if (!ev) return fail(SA_EINVAL, "sa_event_create: null output");
   *ev = nullptr;

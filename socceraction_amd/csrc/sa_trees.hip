@@ -269,6 +269,25 @@ struct CondModel {  // the model's walk
 };
 
 
+// One value per lane against the thresholds of conditions [c0, c1): each condition's outcome over
+// the wave's 64 rows as one 64-bit ballot into its LDS row (lane 0 writes it at M8w).  (Loading
+// the thresholds 64 at a time and reading each back by v_readlane was slower here: 2.26 vs
+// 1.97 ms per model, profiles/r06d -- the readlane -> compare chain serialises.)
+template <typename A, bool LE>
+__device__ __forceinline__ void ballot_conditions(const CondSet<A>& P, A x, int c0, int c1, int lane,
+                                                  uint8_t* __restrict__ M8w) {
+  for (int c = c0; c < c1; ++c) {
+    const A thr = P.num_thr[c];
+    const bool right = isnan(x) ? !P.num_dl[c] : !(LE ? x <= thr : x < thr);
+    const uint64_t word = __ballot(right);
+    if (lane == 0) {
+      uint32_t* dst = reinterpret_cast<uint32_t*>(M8w + (1 + P.n_bool + c) * TS_CSTRIDE);
+      dst[0] = (uint32_t)word;
+      dst[1] = (uint32_t)(word >> 32);
+    }
+  }
+}
+
 // Condition bits of the TS_ROWS rows from R0 into M8 (TS_ROWS threads, s = 0 .. TS_ROWS-1; row
 // R0 + s belongs to thread s, whole waves).
 template <typename A, bool LE, bool N32>
@@ -349,16 +368,7 @@ __device__ __forceinline__ void stage_conditions(const CondSet<A>& P, const sa_b
         const int q = q0 + b;
         if (q >= P.n_ncol) break;
         const A x = (A)raw[b];
-        for (int c = P.col_start[q]; c < P.col_start[q + 1]; ++c) {
-          const A thr = P.num_thr[c];
-          const bool right = isnan(x) ? !P.num_dl[c] : !(LE ? x <= thr : x < thr);
-          const uint64_t word = __ballot(right);
-          if (lane == 0) {
-            uint32_t* dst = reinterpret_cast<uint32_t*>(M8 + (1 + P.n_bool + c) * TS_CSTRIDE + 8 * wv);
-            dst[0] = (uint32_t)word;
-            dst[1] = (uint32_t)(word >> 32);
-          }
-        }
+        ballot_conditions<A, LE>(P, x, P.col_start[q], P.col_start[q + 1], lane, M8 + 8 * wv);
       }
     }
     return;
@@ -378,24 +388,21 @@ __device__ __forceinline__ void stage_conditions(const CondSet<A>& P, const sa_b
       const int q = q0 + b;
       if (q >= P.n_ncol) break;
       const A x = (P.num_cols[q] >> 24) == 1 ? (A)__longlong_as_double((long long)raw[b]) : (A)(double)(int64_t)raw[b];
-      for (int c = P.col_start[q]; c < P.col_start[q + 1]; ++c) {
-        const A thr = P.num_thr[c];
-        const bool right = isnan(x) ? !P.num_dl[c] : !(LE ? x <= thr : x < thr);
-        const uint64_t word = __ballot(right);
-        if (lane == 0) {
-          uint32_t* dst = reinterpret_cast<uint32_t*>(M8 + (1 + P.n_bool + c) * TS_CSTRIDE + 8 * wv);
-          dst[0] = (uint32_t)word;
-          dst[1] = (uint32_t)(word >> 32);
-        }
-      }
+      ballot_conditions<A, LE>(P, x, P.col_start[q], P.col_start[q + 1], lane, M8 + 8 * wv);
     }
   }
 }
 
 // Row R0 + s (s = 0 .. TS_ROWS-1) through every tree from the staged conditions M8.
+// RD: the roots (RD[t]) and depths (RD[TSP + t]) staged in LDS, padded to whole groups of TG
+// (TSP = n_trees rounded up to TG): a group's roots and depths are uniform LDS reads.  Loaded
+// per tree from global memory they cost ~90 scalar instructions per group of 8 trees (address
+// arithmetic and serialised waits), the walk's whole scalar budget (SQ_INSTS_SALU 1,159 per
+// wave of 2,523 VALU, profiles/r06t).
 template <typename A>
 __device__ __forceinline__ A walk_conditions(const CondModel<A>& P, const uint32_t* __restrict__ N,
-                                             const A* __restrict__ LV, const uint8_t* __restrict__ M8, int s) {
+                                             const A* __restrict__ LV, const uint8_t* __restrict__ M8,
+                                             const int32_t* __restrict__ RD, int TSP, int s) {
   const uint8_t* Mrow = M8 + (s >> 3);  // this row's byte of every condition
   const int rbit = s & 7;
   A m = (A)P.base;
@@ -404,9 +411,8 @@ __device__ __forceinline__ A walk_conditions(const CondModel<A>& P, const uint32
     int D = 0;
 #pragma unroll
     for (int u = 0; u < TG; ++u) {
-      const int t = t0 + u < P.n_trees ? t0 + u : P.n_trees - 1;
-      k[u] = P.roots[t];
-      D = max(D, P.depth[t]);
+      k[u] = RD[t0 + u];
+      D = max(D, RD[TSP + t0 + u]);
     }
     for (int d = 0; d < D; ++d) {
       uint32_t nd[TG];
@@ -448,17 +454,24 @@ __global__ __launch_bounds__(TS_ROWS) void tree_cond_kernel(CondSet<typename std
   uint8_t* M8 = ts_lds;
   uint32_t* N = reinterpret_cast<uint32_t*>(ts_lds + moff);
   A* LV = reinterpret_cast<A*>(ts_lds + moff + (size_t)(P.n_nodes + (P.n_nodes & 1)) * 4);
+  const int TSP = (P.n_trees + TG - 1) / TG * TG;
+  int32_t* RD = reinterpret_cast<int32_t*>(ts_lds + moff + (size_t)(P.n_nodes + (P.n_nodes & 1)) * 4 +
+                                           (size_t)(P.n_nodes + (P.n_nodes & 1)) * sizeof(A));
   const int tid = threadIdx.x;
   for (int k = tid; k < P.n_nodes; k += TS_ROWS) {
     N[k] = P.nodes[k];
     LV[k] = P.leaf[k];
+  }
+  for (int t = tid; t < TSP; t += TS_ROWS) {  // padding: the last tree again, depth 0 (not summed)
+    RD[t] = P.roots[t < P.n_trees ? t : P.n_trees - 1];
+    RD[TSP + t] = t < P.n_trees ? P.depth[t] : 0;
   }
   const int64_t R0 = (int64_t)blockIdx.x * TS_ROWS;
   stage_conditions<A, LE, N32>(C, Bb, bits, bstride, Bf, Bi, n, R0, tid, M8);
   __syncthreads();
   const int64_t j = R0 + tid;
   if (j >= n) return;
-  const A m = walk_conditions<A>(P, N, LV, M8, tid);
+  const A m = walk_conditions<A>(P, N, LV, M8, RD, TSP, tid);
   if (F32)
     ((float*)P.out)[j] = 1.0f / (1.0f + expf(-(float)m));
   else
@@ -516,9 +529,16 @@ extern "C" int sa_tree_predict(const void* nodes, int32_t n_nodes, const int32_t
   return check_launch("tree_predict_kernel");
 }
 
+// The staged walk's LDS: conditions, nodes, leaf values, then the roots and depths padded to
+// whole tree groups.
+static int64_t staged_lds_bytes(int32_t n_nodes, int32_t n_cond, int32_t f32, int32_t n_trees) {
+  const int64_t np = n_nodes + (n_nodes & 1);
+  return ((int64_t)n_cond * TS_CSTRIDE + 15) / 16 * 16 + np * 4 + np * (f32 ? 4 : 8) +
+         (int64_t)(n_trees + TG - 1) / TG * TG * 8;
+}
+// (a model has at most n_nodes trees: the bound a caller without the tree count can use)
 extern "C" int64_t sa_tree_staged_lds_bytes(int32_t n_nodes, int32_t n_cond, int32_t f32) {
-  return ((int64_t)n_cond * TS_CSTRIDE + 15) / 16 * 16 + (int64_t)(n_nodes + (n_nodes & 1)) * 4 +
-         (int64_t)n_nodes * (f32 ? 4 : 8);
+  return staged_lds_bytes(n_nodes, n_cond, f32, n_nodes);
 }
 
 extern "C" int sa_tree_predict_staged(const sa_tree_model* model, const int32_t* bool_cols, int32_t n_bool,
@@ -536,7 +556,7 @@ extern "C" int sa_tree_predict_staged(const sa_tree_model* model, const int32_t*
   if (m.n_nodes < 1 || m.n_nodes > 65535 || m.n_trees < 1 || !m.nodes || !m.leaf || !m.roots || !m.tree_depth ||
       !m.p_out)
     return fail(SA_EINVAL, "bad staged tree model");
-  const int64_t lds = sa_tree_staged_lds_bytes(m.n_nodes, 1 + n_bool + n_num, f32);
+  const int64_t lds = staged_lds_bytes(m.n_nodes, 1 + n_bool + n_num, f32 & 1, m.n_trees);
   if (lds > 160 * 1024) return fail(SA_EINVAL, "staged tree model needs %lld B of LDS", (long long)lds);
   sa_block z{nullptr, 0, 0, 16};
   const sa_block Bb = bool_blk ? *bool_blk : z, Bf = f64_blk ? *f64_blk : z, Bi = i64_blk ? *i64_blk : z;

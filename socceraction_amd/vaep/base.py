@@ -140,7 +140,7 @@ class VAEP:
                                     segments='game')
         off = ab.cols['seg_off'].cpu().numpy()
         gids = actions['game_id'].to_numpy()[off[:-1]] if len(actions) else []
-        homes = [home_of[g] for g in gids]
+        homes = list(home_of.loc[gids]) if len(gids) else []  # one vectorised lookup
         return self._features_frame(ab, actions, homes, list(zip(off[:-1], off[1:])))
 
     # ---------------------------------------------------------------- labels
@@ -175,6 +175,17 @@ class VAEP:
     def compute_labels_batch(self, games: pd.DataFrame, actions: pd.DataFrame) -> pd.DataFrame:
         """Labels of many games (contiguous per game) in one launch."""
         return self._labels_frame(actions, 'game')
+
+    def compute_batch(self, games: pd.DataFrame, actions: pd.DataFrame,
+                      p_scores=None, p_concedes=None, chunk_rows: int = 1 << 18):
+        """``(compute_features_batch, compute_labels_batch, formula values)`` of the same
+        games from ONE encode of the frame, pipelined over game-aligned chunks so the host
+        encodes the next chunk while the DMA engine copies the last one out
+        (:mod:`socceraction_amd.pipeline`).  ``p_scores`` / ``p_concedes``: one probability per
+        action (e.g. a fitted model's), else the values are None.  Built-in transformers and
+        label functions only."""
+        from ..pipeline import value_frames
+        return value_frames(self, games, actions, p_scores, p_concedes, chunk_rows)
 
     # ---------------------------------------------------------------- learning (host)
     def fit(self, X: pd.DataFrame, y: pd.DataFrame, learner: str = 'xgboost',

@@ -185,6 +185,48 @@ def test_batched_api_equals_per_game(atomic):
     assert_close(v['vaep_value'].to_numpy(), np.concatenate([g['vaep_value_64'] for g in gs]), 'vaep')
 
 
+@pytest.mark.parametrize('atomic', [False, True])
+def test_pipelined_compute_batch_equals_separate_calls(atomic):
+    """VAEP.compute_batch (socceraction_amd.pipeline: one encode, game-aligned chunks, the
+    chunks' blocks copied out by pitched DMAs while the host encodes the next) == the separate
+    batched calls, frame for frame: features (names, dtypes, values), labels incl.
+    goal_from_shot, and the formula values in float64 and float32 -- with chunks small enough
+    that both device slots are reused several times, and with one chunk."""
+    import torch
+
+    from socceraction_amd import ops, synthetic
+    from socceraction_amd.batch import ActionBatch
+    if atomic:
+        from socceraction_amd.atomic.vaep import AtomicVAEP as Model
+        d = synthetic.atomic_games(40, game_id0=3)
+    else:
+        from socceraction_amd.vaep import VAEP as Model
+        d = synthetic.spadl_games(40, game_id0=3)
+    actions = synthetic.to_frame(d, atomic=atomic)
+    games = synthetic.games_frame(d)
+    model = Model()
+    model.yfns = model.yfns + [model._lab.goal_from_shot]
+    X = model.compute_features_batch(games, actions)
+    Y = model.compute_labels_batch(games, actions)
+    n = len(actions)
+    p = synthetic.probabilities(n)
+    for chunk in (5000, 1 << 20):
+        for dt in (np.float64, np.float32):
+            ps, pc = p['scores'].astype(dt), p['concedes'].astype(dt)
+            X2, Y2, V2 = model.compute_batch(games, actions, ps, pc, chunk_rows=chunk)
+            pd.testing.assert_frame_equal(X2, X)
+            pd.testing.assert_frame_equal(Y2, Y)
+            ab = ActionBatch.from_frame(actions, atomic=atomic, segments='game')
+            ref = ops.formula(ab, torch.from_numpy(ps).cuda(), torch.from_numpy(pc).cuda()).cpu().numpy()
+            for r, c in enumerate(('offensive_value', 'defensive_value', 'vaep_value')):
+                assert V2[c].dtype == dt
+                np.testing.assert_array_equal(V2[c].to_numpy(), ref[r, :n], err_msg=c)
+    X3, Y3, V3 = model.compute_batch(games, actions, chunk_rows=7000)
+    pd.testing.assert_frame_equal(X3, X)
+    pd.testing.assert_frame_equal(Y3, Y)
+    assert V3 is None
+
+
 def test_user_transformer_runs_on_host_gamestates():
     from socceraction_amd.vaep import VAEP
     from socceraction_amd.vaep import features as fs
