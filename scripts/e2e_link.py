@@ -96,9 +96,18 @@ def pipeline_probe(games: int = 1000):
     src = fb.bool_block[0]
     lib = _native.lib()
     s = torch.cuda.current_stream()
-    for name, fn in (('pitched_d2h_GBs', lambda: _native.check(lib.sa_copy2d_async(
-                         hb.data_ptr(), n, src.data_ptr(), src.shape[-1], m, plan.n_bool, s.cuda_stream))),
-                     ('contiguous_d2h_GBs', lambda: hb1.copy_(src[:, :m], non_blocking=True))):
+    def pitched(dst_off, src_off, width):
+        return lambda: _native.check(lib.sa_copy2d_async(
+            hb.data_ptr() + dst_off, n, src.data_ptr() + src_off, src.shape[-1], width, plan.n_bool,
+            s.cuda_stream))
+    cases = [('pitched_d2h_GBs', pitched(0, 0, m)),
+             ('contiguous_d2h_GBs', lambda: hb1.copy_(src[:, :m], non_blocking=True))]
+    for a in (1, 2, 4, 8, 16, 64, 256):  # dst and src offsets of a bytes (both), odd width
+        cases.append((f'pitched_d2h_off_{a}_GBs', pitched(262144 + a, a, m - 257)))
+    cases.append(('pitched_d2h_off_0_oddwidth_GBs', pitched(262144, 0, m - 257)))
+    cases.append(('pitched_d2h_dstoff_4_srcoff_0_GBs', pitched(262144 + 4, 0, m - 257)))
+    cases.append(('pitched_d2h_dstoff_0_srcoff_4_GBs', pitched(262144, 4, m - 257)))
+    for name, fn in cases:
         t = []
         for _ in range(5):
             torch.cuda.synchronize()
@@ -113,7 +122,7 @@ def pipeline_probe(games: int = 1000):
     ab = ActionBatch.from_frame(sub, home_team_id=home_of, segments='game')
     torch.cuda.synchronize()
     out['encode_h2d_ms_per_256k_rows'] = round((time.perf_counter() - t0) * 1e3, 2)
-    for chunk in (1 << 17, 1 << 18, 1 << 19, 1 << 21):
+    for chunk in (1 << 18, 1 << 21):
         model.compute_batch(gframe, actions, p['scores'], p['concedes'], chunk_rows=chunk)
         t = []
         for _ in range(3):
@@ -121,6 +130,10 @@ def pipeline_probe(games: int = 1000):
             model.compute_batch(gframe, actions, p['scores'], p['concedes'], chunk_rows=chunk)
             t.append(time.perf_counter() - t0)
         out[f'compute_batch_ms_chunk_{chunk}'] = round(min(t) * 1e3, 2)
+    from socceraction_amd.pipeline import value_frames
+    tl = []
+    value_frames(model, gframe, actions, p['scores'], p['concedes'], chunk_rows=1 << 18, timeline=tl)
+    out['timeline_chunk_262144'] = tl
     print(json.dumps({'pipeline_probe': out}), flush=True)
 
 

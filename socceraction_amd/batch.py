@@ -116,7 +116,7 @@ class ActionBatch:
 
     def __init__(self, cols: Dict[str, np.ndarray], seg_off: np.ndarray,
                  home: Optional[np.ndarray], atomic: bool, dev: Optional[torch.device] = None,
-                 contiguous: bool = False):
+                 contiguous: bool = False, pinned: bool = False):
         dev = dev or device()
         self.atomic = bool(atomic)
         self.n = int(len(cols['type_id']))
@@ -133,15 +133,24 @@ class ActionBatch:
         for k, a in arrays.items():
             offsets[k] = total
             total += _round(max(a.nbytes, 16), _ALIGN)
-        host = np.zeros(total, dtype=np.uint8)
+        # pinned: the host image in page-locked memory and the H2D asynchronous on the current
+        # stream (the image is kept with the batch) -- a pageable H2D is staged by the runtime
+        # and waits for the DMA engine behind any device-to-host copy in flight
+        # (socceraction_amd.pipeline overlaps its D2H with the next chunk's H2D)
+        hostt = torch.zeros(total, dtype=torch.uint8, pin_memory=True) if pinned else None
+        host = hostt.numpy() if pinned else np.zeros(total, dtype=np.uint8)
         for k, a in arrays.items():
             host[offsets[k]:offsets[k] + a.nbytes] = a.view(np.uint8).reshape(-1)
         self._dbuf = None
+        self._host = hostt
         if contiguous:  # one physically contiguous range (``ops.DeviceBuffer``), raises if none
             from .ops import DeviceBuffer
             self._dbuf = DeviceBuffer(total, contiguous=True)
             self.buffer = self._dbuf.tensor((total,), torch.uint8)
             self.buffer.copy_(torch.from_numpy(host))
+        elif pinned:
+            self.buffer = torch.empty(total, dtype=torch.uint8, device=dev)
+            self.buffer.copy_(hostt, non_blocking=True)
         else:
             self.buffer = torch.from_numpy(host).to(dev)
         self.cols: Dict[str, torch.Tensor] = {}
@@ -155,7 +164,8 @@ class ActionBatch:
     # ------------------------------------------------------------------ constructors
     @classmethod
     def from_frame(cls, df: pd.DataFrame, *, atomic: bool = False, home_team_id=None,
-                   segments: str = 'single', team_codes=None, dev=None) -> 'ActionBatch':
+                   segments: str = 'single', team_codes=None, dev=None,
+                   pinned: bool = False) -> 'ActionBatch':
         """Flatten a SPADL / Atomic-SPADL frame.
 
         ``segments='single'``: the whole frame is one segment (the reference's
@@ -189,7 +199,7 @@ class ActionBatch:
         else:
             cols['team'], hc = encode_teams(df['team_id'].to_numpy(), homes)
         home = hc if homes else None
-        return cls(cols, seg_off, home, atomic, dev)
+        return cls(cols, seg_off, home, atomic, dev, pinned=pinned)
 
     @classmethod
     def from_columns(cls, d: Dict[str, np.ndarray], *, atomic: bool = False,

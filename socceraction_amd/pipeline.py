@@ -33,14 +33,21 @@ def _pinned(shape, dtype) -> torch.Tensor:
     return torch.empty(shape, dtype=dtype, pin_memory=True)
 
 
-def _chunks(seg_off: np.ndarray, chunk_rows: int):
-    """Game-aligned cuts: segments [s0, s1) of about chunk_rows actions each."""
+def _chunks(seg_off: np.ndarray, chunk_rows: int, look: int = 16):
+    """Game-aligned cuts: segments [s0, s1) of about chunk_rows actions each, each cut at a game
+    boundary whose row is a multiple of 4 when one lies within ``look`` games: the DMA engine
+    moves a pitched copy at the link rate only from and to 4-byte aligned addresses (the bool
+    and label blocks are 1 byte per row: 57 vs 14 GB/s, scripts/e2e_link.py probe, r06g)."""
     cuts, s0 = [], 0
     nseg = len(seg_off) - 1
     while s0 < nseg:
         target = seg_off[s0] + chunk_rows
         s1 = int(np.searchsorted(seg_off, target, side='right')) - 1
         s1 = min(max(s1, s0 + 1), nseg)
+        if s1 < nseg and seg_off[s1] % 4:
+            near = [t for t in range(max(s0 + 1, s1 - look), min(nseg, s1 + look + 1)) if seg_off[t] % 4 == 0]
+            if near:
+                s1 = min(near, key=lambda t: abs(t - s1))
         cuts.append((s0, s1))
         s0 = s1
     return cuts
@@ -60,7 +67,8 @@ class _Slot:
 
 def value_frames(model, games: pd.DataFrame, actions: pd.DataFrame,
                  p_scores: Optional[np.ndarray] = None, p_concedes: Optional[np.ndarray] = None,
-                 chunk_rows: int = 1 << 18) -> Tuple[pd.DataFrame, pd.DataFrame, Optional[pd.DataFrame]]:
+                 chunk_rows: int = 1 << 18, timeline: Optional[list] = None
+                 ) -> Tuple[pd.DataFrame, pd.DataFrame, Optional[pd.DataFrame]]:
     """(features, labels, values) of ``actions`` (each game's rows contiguous, ``games`` maps
     game_id -> home_team_id) for a VAEP / AtomicVAEP ``model`` whose transformers are all
     known ones.  ``values`` is None without probabilities (float32 or float64; values take
@@ -95,8 +103,9 @@ def value_frames(model, games: pd.DataFrame, actions: pd.DataFrame,
         nd = np.float32 if vdt == torch.float32 else np.float64
         tps = torch.from_numpy(np.ascontiguousarray(ps, nd)).to(dev)
         tpc = torch.from_numpy(np.ascontiguousarray(pc, nd)).to(dev)
-    # the whole frame's host blocks, column-major [cols, n] (pinned: the DMA writes them)
-    ld = max(16, n)
+    # the whole frame's host blocks, column-major [cols, ld] (pinned: the DMA writes them), rows
+    # on 16-byte boundaries (aligned DMA; the frames view [:, :n])
+    ld = max(16, (n + 15) // 16 * 16)
     hb = _pinned((plan.n_bool, ld), torch.uint8)
     hf = _pinned((plan.n_f64, ld), torch.float64)
     hi = _pinned((plan.n_i64, ld), torch.int64)
@@ -117,13 +126,18 @@ def value_frames(model, games: pd.DataFrame, actions: pd.DataFrame,
         _native.check(lib.sa_copy2d_async(dst.data_ptr() + r0 * es, dst.shape[1] * es,
                                            src.data_ptr(), src.shape[-1] * es, m * es, rows,
                                            copy.cuda_stream))
+    import time
+    t_start = time.perf_counter()
+    evs = []
     for k, (s0, s1) in enumerate(cuts):
         r0, r1 = int(seg_off[s0]), int(seg_off[s1])
         m = r1 - r0
         slot = slots[k % len(slots)]
+        th0 = time.perf_counter()
         # 1. host encode + H2D of this chunk (overlaps the copy out of the previous chunk)
         ab = ActionBatch.from_frame(actions.iloc[r0:r1], atomic=atomic, home_team_id=list(homes[s0:s1]),
-                                    segments='game', dev=dev)
+                                    segments='game', dev=dev, pinned=True)
+        th1 = time.perf_counter()
         # 2. kernels, once the slot's previous copy is done
         if slot.used:
             main.wait_event(slot.done)
@@ -139,6 +153,9 @@ def value_frames(model, games: pd.DataFrame, actions: pd.DataFrame,
         ev = torch.cuda.Event()
         ev.record(main)
         copy.wait_event(ev)
+        if timeline is not None:  # diagnostics: the copy's device-side start / end
+            ea, eb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            ea.record(copy)
         d2h(hb, slot.fb.bool_block[0], r0, m, plan.n_bool)
         d2h(hf, slot.fb.f64_block[0], r0, m, plan.n_f64)
         d2h(hi, slot.fb.i64_block[0], r0, m, plan.n_i64)
@@ -146,10 +163,20 @@ def value_frames(model, games: pd.DataFrame, actions: pd.DataFrame,
         if vdt is not None:
             d2h(hv, slot.val, r0, m, 3)
         slot.done.record(copy)
+        if timeline is not None:
+            eb.record(copy)
+            evs.append((k, m, th0 - t_start, th1 - t_start, time.perf_counter() - t_start, ea, eb))
         slot.used = True
         slot.keep = ab  # the batch's device columns stay alive until the slot is reused
     copy.synchronize()
     main.synchronize()
+    if timeline is not None and evs:
+        e0 = evs[0][5]
+        for k, m, a, b, c, ea, eb in evs:  # host ms: encode start / end, launches queued; device ms
+            timeline.append({'chunk': k, 'rows': m, 'encode_ms': (round(a * 1e3, 2), round(b * 1e3, 2)),
+                             'queued_ms': round(c * 1e3, 2),
+                             'd2h_ms_from_first': (round(e0.elapsed_time(ea), 2), round(e0.elapsed_time(eb), 2))})
+        timeline.append({'host_total_ms': round((time.perf_counter() - t_start) * 1e3, 2)})
     X = catalog.assemble_frame(plan, hb.numpy(), hf.numpy(), hi.numpy(), n, pd.RangeIndex(n))
     hln = hl.numpy()  # numpy views keep their pinned tensors alive (so do the frames over them)
     ycols = {}

@@ -841,3 +841,21 @@ def test_phase_times_on_the_host():
         pass
     ms = pt.ms()
     assert set(ms) == {'a', 'b'} and ms['a'] >= 19 and ms['b'] >= 0
+
+
+def test_pipeline_chunks_cut_at_games_on_aligned_rows():
+    """socceraction_amd.pipeline._chunks: game-aligned chunks covering every game once, of about
+    the asked size, each cut at a row that is a multiple of 4 when one lies within reach (the
+    DMA's fast path), else at the plain game boundary."""
+    from socceraction_amd import pipeline
+    rng = np.random.default_rng(3)
+    sizes = rng.integers(1000, 2200, 400)
+    off = np.concatenate([[0], np.cumsum(sizes)])
+    cuts = pipeline._chunks(off, 50_000)
+    assert cuts[0][0] == 0 and cuts[-1][1] == len(sizes)
+    assert all(a[1] == b[0] for a, b in zip(cuts, cuts[1:]))
+    assert all(off[s1] % 4 == 0 for _, s1 in cuts[:-1])
+    assert all(abs((off[s1] - off[s0]) - 50_000) < 40_000 for s0, s1 in cuts[:-1])
+    odd = np.concatenate([[0], np.cumsum(np.full(50, 1001))])  # no row but 0 mod 4 every 4 games
+    cuts = pipeline._chunks(odd, 5000, look=0)
+    assert cuts[-1][1] == 50 and all(a[1] == b[0] for a, b in zip(cuts, cuts[1:]))
