@@ -462,6 +462,23 @@ def atomic_extra(dist, rank, world, dev, games: int, reps: int = 21, check: bool
         torch.cuda.synchronize()
         check_vaep(par, d, out, lab.scores, lab.concedes, None, None, atomic=True)
         par.merge(dist, dev)
+    # placement: the same step into a second, freshly allocated set of blocks, timed the same way
+    # (never the value): some allocations run every step ~10 % slower with the same bytes, TLB
+    # misses and clock (profiles/r06p_*); the line says which kind the first one was
+    placement = None
+    try:
+        out2 = ops.alloc_feature_blocks(plan, ab.n, dev, 1024, 128, contiguous=contiguous)
+        ops.features(ab, ATOMIC_DEFAULT, 3, out=out2, bool_tile=1024, num_tile=128)
+
+        def step2():
+            ops.step_into(s, out2, None, None, 10, lab, None)
+        ms2 = _events_median_ms(step2, reps)[0]
+        placement = {'realloc_ms_per_step': round(ms2, 4), 'first_over_realloc': round(ms / ms2, 4),
+                     'mode': ('slow placement (first allocation >= 4 % slower than a fresh one)'
+                              if ms > 1.04 * ms2 else 'no slow placement seen')}
+        del out2
+    except (RuntimeError, ValueError, MemoryError) as e:  # no second contiguous range: skip
+        placement = {'error': f'{type(e).__name__}: {e}'}
     n, total, wall = ab.n, ab.n, ms
     if dist is not None:
         wall = _reduce(dist, ms, dist.ReduceOp.MAX, dev)
@@ -473,6 +490,7 @@ def atomic_extra(dist, rank, world, dev, games: int, reps: int = 21, check: bool
             'atomic_actions_per_gpu': n, 'atomic_actions_total': total, 'scaling': 'strong',
             'bool_block': out.bool_alloc,
             'ms_per_step': round(wall, 4),
+            'placement': placement,
             'timing': f'median of {reps} steps (HIP events per step; min {ms_lo:.4f}, max '
                       f'{ms_hi:.4f} ms on rank {rank})',
             'atomic_actions_per_s': round(total / wall * 1e3, 1), 'bytes_per_action': bpa,

@@ -482,9 +482,11 @@ constexpr int CG_WAVES = 4;  // waves per workgroup
 constexpr int BOOL_HALO = 8;  // rows before j0 held in registers: windows i <= 8 (k <= 9)
 constexpr int WIDE_D_MAX = 1 << 30;
 
-template <bool ATOMIC, bool EXPLICIT, bool BITS, bool WIDE = false>
-__global__ __launch_bounds__(64 * CG_WAVES) void bool_colgroup_kernel(FeatArgs args, int ngroups,
-                                                                      int gcols) {
+// The pass over logical workgroup `lblock` (bool_colgroup_kernel; and the bool workgroups of the
+// SA_FUSED_STEP probe's one-launch step).
+template <bool ATOMIC, bool EXPLICIT, bool BITS, bool WIDE>
+__device__ __forceinline__ void bool_colgroup_body(const FeatArgs& args, int ngroups, int gcols,
+                                                   int64_t lblock) {
   const int lane = threadIdx.x & (WAVE - 1);
   const int wv = threadIdx.x / WAVE;
   const sa_actions& A = args.a;
@@ -492,7 +494,7 @@ __global__ __launch_bounds__(64 * CG_WAVES) void bool_colgroup_kernel(FeatArgs a
   const int64_t n = A.n;
   const int K = P.nb_prev_actions;
   const int64_t R = args.Rb;
-  const int64_t w = xcd_logical_block() * CG_WAVES + wv;
+  const int64_t w = lblock * CG_WAVES + wv;
   const int64_t tile0 = (w / ngroups) * BOOL_TILE;
   const int c_lo = (int)(w % ngroups) * gcols;
   const int c_hi = c_lo + gcols < (int)args.Cb ? c_lo + gcols : (int)args.Cb;
@@ -689,6 +691,12 @@ __global__ __launch_bounds__(64 * CG_WAVES) void bool_colgroup_kernel(FeatArgs a
       st_bool_out<BITS>(args, bb, tc, j0, m[0], m[1], m[2], m[3]);
     }
   }
+}
+
+template <bool ATOMIC, bool EXPLICIT, bool BITS, bool WIDE = false>
+__global__ __launch_bounds__(64 * CG_WAVES) void bool_colgroup_kernel(FeatArgs args, int ngroups,
+                                                                      int gcols) {
+  bool_colgroup_body<ATOMIC, EXPLICIT, BITS, WIDE>(args, ngroups, gcols, xcd_logical_block());
 }
 
 // ------------------------------------------------------------------------------ f64/i64 block
@@ -1460,6 +1468,31 @@ void num_features_kernel(FeatArgs args) {
   const int64_t wave_base = args.row0 + (xcd_logical_block() * BLOCK_WAVES + wv) * WAVE_ACTS;
   num_features_body<ATOMIC, EXPLICIT, KF, TAIL, N32, COND>(args, wave_base, args.a.frames[0], args.ps, args.pc);
 }
+
+// SA_FUSED_STEP = 1 (probe builds): the SPADL step's bool pass and numeric step pass as ONE
+// launch, their workgroups interleaved in proportion (logical workgroup L is a bool one when
+// floor((L + 1) nb / T) > floor(L nb / T)), so each CU mixes the pure-store bool tiles with the
+// read-heavy numeric tiles of the same rows, whose inputs the two then share in L2.  The A/B of
+// the headline's one bounded experiment (scripts/fused_step_ab.py).
+#ifndef SA_FUSED_STEP
+#define SA_FUSED_STEP 0
+#endif
+#if SA_FUSED_STEP
+static_assert(CG_WAVES == BLOCK_WAVES, "one workgroup shape for both passes");
+__global__ __launch_bounds__(64 * BLOCK_WAVES) void step_fused_kernel(FeatArgs args, int ngroups, int gcols,
+                                                                      int64_t nb, int64_t total) {
+  const int64_t L = xcd_logical_block();
+  if (L >= total) return;
+  const int64_t bi = L * nb / total;
+  if ((L + 1) * nb / total > bi) {
+    bool_colgroup_body<false, false, false, false>(args, ngroups, gcols, bi);
+  } else {
+    const int wv = threadIdx.x / WAVE;
+    const int64_t wave_base = args.row0 + ((L - bi) * BLOCK_WAVES + wv) * WAVE_ACTS;
+    num_features_body<false, false, 3, true, false, false>(args, wave_base, args.a.frames[0], args.ps, args.pc);
+  }
+}
+#endif
 
 // SA_NUM_STAGE = T > 0 (probe builds): the SPADL step pass with each workgroup's streamed inputs
 // -- coordinates, time and the two probabilities of T x 512 rows (56 B per row) plus the two rows
@@ -2234,6 +2267,13 @@ static int launch_features(const sa_actions* a, const sa_feature_plan* plan, con
     const int64_t waves = (a->n + BOOL_TILE - 1) / BOOL_TILE * ng;
     const dim3 cgrid(xcd_grid((waves + CG_WAVES - 1) / CG_WAVES)), cblock(WAVE * CG_WAVES);
     const bool wide = !expl && K > BOOL_HALO + 1;  // windows past the register halo
+#if SA_FUSED_STEP
+    if (!bits && !wide && !expl && !a->atomic && tail && tail->chunk == 0 && !cond && !num32) {
+      const int64_t nb = cgrid.x, nn = (a->n + BLOCK_ACTS - 1) / BLOCK_ACTS;
+      hipLaunchKernelGGL(step_fused_kernel, dim3(xcd_grid(nb + nn)), cblock, 0, st, args, ng, gc, nb, nb + nn);
+      return check_launch("step_fused_kernel");
+    }
+#endif
     if (bits) {  // the on-device VAEP.rate: SPADL or atomic, windowed, as bitmaps
       if (wide) {
         if (a->atomic)
