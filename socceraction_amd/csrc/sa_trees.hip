@@ -18,6 +18,7 @@
 // afterwards).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <type_traits>
 
@@ -37,6 +38,9 @@ struct TNode {  // 24 B
 constexpr int TR_THREADS = 1024;  // 16 waves share one LDS copy of the model
 constexpr int TR_LDS_NODES = 2048;  // 48 KB
 constexpr int TR_LDS_SLOTS = 2048;  // 8 KB
+#ifndef SA_TREE_PERSIST
+#define SA_TREE_PERSIST 0  // staged walk grid: N x the resident workgroups looping over tiles (A/B: 1.19 ms vs 1.12 per learner at N = 1, r06i; 0: one per tile)
+#endif
 #ifndef SA_TREE_TG
 #define SA_TREE_TG 8
 #endif
@@ -291,7 +295,8 @@ __device__ __forceinline__ void ballot_conditions(const CondSet<A>& P, A x, int 
 // Condition bits of the TS_ROWS rows from R0 into M8 (TS_ROWS threads, s = 0 .. TS_ROWS-1; row
 // R0 + s belongs to thread s, whole waves).
 template <typename A, bool LE, bool N32>
-__device__ __forceinline__ void stage_conditions(const CondSet<A>& P, const sa_block& Bb, const uint8_t* __restrict__ bits,
+__device__ __forceinline__ void stage_conditions(const CondSet<A>& P, const int32_t* __restrict__ BC,
+                                                 const sa_block& Bb, const uint8_t* __restrict__ bits,
                                                  int64_t bstride, const sa_block& Bf, const sa_block& Bi, int64_t n,
                                                  int64_t R0, int s, uint8_t* __restrict__ M8) {
   const int wv = s >> 6, lane = s & 63;
@@ -306,7 +311,7 @@ __device__ __forceinline__ void stage_conditions(const CondSet<A>& P, const sa_b
       for (int b = 0; b < TS_B; ++b) {
         const int it = i0 + b * TS_ROWS + s;
         const int64_t r = R0 + 64 * (it % WQ);
-        w[b] = it < nwi && r < n ? *reinterpret_cast<const uint64_t*>(bits + (int64_t)P.bool_cols[it / WQ] * bstride + r / 8)
+        w[b] = it < nwi && r < n ? *reinterpret_cast<const uint64_t*>(bits + (int64_t)BC[it / WQ] * bstride + r / 8)
                                   : 0ull;
       }
 #pragma unroll
@@ -330,7 +335,7 @@ __device__ __forceinline__ void stage_conditions(const CondSet<A>& P, const sa_b
       w[b] = u32x4{0, 0, 0, 0};
       const int64_t r = R0 + 16 * (it % TS_PIECES);
       if (it < nbi && r < n) {
-        const int64_t col = P.bool_cols[it / TS_PIECES];
+        const int64_t col = BC[it / TS_PIECES];
         SA_DCHECK(col >= 0 && col < Bb.n_cols, col);
         const int64_t t = r / Bb.tile_rows;
         w[b] = *reinterpret_cast<const u32x4*>((const uint8_t*)Bb.data + (t * Bb.n_cols + col) * Bb.tile_rows +
@@ -457,6 +462,7 @@ __global__ __launch_bounds__(TS_ROWS) void tree_cond_kernel(CondSet<typename std
   const int TSP = (P.n_trees + TG - 1) / TG * TG;
   int32_t* RD = reinterpret_cast<int32_t*>(ts_lds + moff + (size_t)(P.n_nodes + (P.n_nodes & 1)) * 4 +
                                            (size_t)(P.n_nodes + (P.n_nodes & 1)) * sizeof(A));
+  int32_t* BC = RD + 2 * TSP;  // the bool conditions' columns / bitmap rows
   const int tid = threadIdx.x;
   for (int k = tid; k < P.n_nodes; k += TS_ROWS) {
     N[k] = P.nodes[k];
@@ -466,16 +472,25 @@ __global__ __launch_bounds__(TS_ROWS) void tree_cond_kernel(CondSet<typename std
     RD[t] = P.roots[t < P.n_trees ? t : P.n_trees - 1];
     RD[TSP + t] = t < P.n_trees ? P.depth[t] : 0;
   }
-  const int64_t R0 = (int64_t)blockIdx.x * TS_ROWS;
-  stage_conditions<A, LE, N32>(C, Bb, bits, bstride, Bf, Bi, n, R0, tid, M8);
+  for (int k = tid; k < C.n_bool; k += TS_ROWS) BC[k] = C.bool_cols[k];
   __syncthreads();
-  const int64_t j = R0 + tid;
-  if (j >= n) return;
-  const A m = walk_conditions<A>(P, N, LV, M8, RD, TSP, tid);
-  if (F32)
-    ((float*)P.out)[j] = 1.0f / (1.0f + expf(-(float)m));
-  else
-    ((double*)P.out)[j] = 1.0 / (1.0 + exp(-(double)m));
+  // tiles blockIdx.x, + gridDim.x, ...: the model's tables above are staged once per workgroup
+  // (the grid is sized to the resident workgroups when SA_TREE_PERSIST, else one per tile)
+  const int64_t tiles = (n + TS_ROWS - 1) / TS_ROWS;
+  for (int64_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
+    const int64_t R0 = tile * TS_ROWS;
+    stage_conditions<A, LE, N32>(C, BC, Bb, bits, bstride, Bf, Bi, n, R0, tid, M8);
+    __syncthreads();
+    const int64_t j = R0 + tid;
+    if (j < n) {
+      const A m = walk_conditions<A>(P, N, LV, M8, RD, TSP, tid);
+      if (F32)
+        ((float*)P.out)[j] = 1.0f / (1.0f + expf(-(float)m));
+      else
+        ((double*)P.out)[j] = 1.0 / (1.0 + exp(-(double)m));
+    }
+    __syncthreads();  // every row walked before the next tile's conditions overwrite M8
+  }
 }
 
 }  // namespace sa
@@ -534,7 +549,7 @@ extern "C" int sa_tree_predict(const void* nodes, int32_t n_nodes, const int32_t
 static int64_t staged_lds_bytes(int32_t n_nodes, int32_t n_cond, int32_t f32, int32_t n_trees) {
   const int64_t np = n_nodes + (n_nodes & 1);
   return ((int64_t)n_cond * TS_CSTRIDE + 15) / 16 * 16 + np * 4 + np * (f32 ? 4 : 8) +
-         (int64_t)(n_trees + TG - 1) / TG * TG * 8;
+         (int64_t)(n_trees + TG - 1) / TG * TG * 8 + (int64_t)n_cond * 4;
 }
 // (a model has at most n_nodes trees: the bound a caller without the tree count can use)
 extern "C" int64_t sa_tree_staged_lds_bytes(int32_t n_nodes, int32_t n_cond, int32_t f32) {
@@ -563,16 +578,27 @@ extern "C" int sa_tree_predict_staged(const sa_tree_model* model, const int32_t*
   if (n_bool > 0 && !bool_bits && (Bb.tile_rows % 16 != 0 || !aligned16(Bb.data)))
     return fail(SA_EINVAL, "bool block: 16-row tiles, 16-byte aligned");
   if (n == 0) return SA_OK;
-  const dim3 grid((unsigned)((n + TS_ROWS - 1) / TS_ROWS)), block(TS_ROWS);
+  const int64_t tiles = (n + TS_ROWS - 1) / TS_ROWS;
+  const dim3 block(TS_ROWS);
   hipStream_t st = (hipStream_t)stream;
+  // SA_TREE_PERSIST: as many workgroups as are resident at once (each stages the model's tables
+  // once and loops over tiles); else one workgroup per tile
 #define SA_TS_LAUNCH(F, LEQ, A, N32)                                                                     \
   do {                                                                                                  \
     CondSet<A> C{bool_cols, num_cols, col_start, (const A*)num_thr, num_dl, n_bool, n_num > 0 ? n_ncol : 0, \
                  n_num};                                                                                \
     CondModel<A> P{(const uint32_t*)m.nodes, (const A*)m.leaf, m.roots, m.tree_depth, m.n_nodes,        \
                    m.n_trees,                m.base_margin,    m.p_out};                                \
-    hipLaunchKernelGGL((tree_cond_kernel<F, LEQ, N32>), grid, block, (size_t)lds, st, C, P, Bb, bool_bits, \
-                       bits_stride, Bf, Bi, n);                                                          \
+    int64_t g = tiles;                                                                                  \
+    if (SA_TREE_PERSIST) {                                                                              \
+      int per_cu = 0;                                                                                   \
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, tree_cond_kernel<F, LEQ, N32>, TS_ROWS, \
+                                                       (size_t)lds) != hipSuccess || per_cu < 1)        \
+        per_cu = 1;                                                                                     \
+      g = std::min<int64_t>(tiles, (int64_t)per_cu * device_cus(current_device()) * SA_TREE_PERSIST);   \
+    }                                                                                                   \
+    hipLaunchKernelGGL((tree_cond_kernel<F, LEQ, N32>), dim3((unsigned)g), block, (size_t)lds, st, C, P, Bb, \
+                       bool_bits, bits_stride, Bf, Bi, n);                                               \
   } while (0)
   const bool n32 = (f32 & 2) != 0;  // float32 numeric blocks
   if (n32 && !(f32 & 1)) return fail(SA_EINVAL, "float32 numeric blocks need float32 (xgboost) arithmetic");

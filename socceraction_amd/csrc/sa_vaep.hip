@@ -77,6 +77,7 @@ struct FeatArgs {
   const float* cond_thr;                     // per condition: float32 threshold (`x < thr` goes left)
   const int32_t* cond_dl;                    // per condition: NaN goes left
   int32_t cond_row0;                         // bitmap row of condition 0 (after the bool columns)
+  int32_t cond_n;                             // conditions (num_cond_lds_kernel stages the tables)
   // the numeric pass over rows [row0, row_end) only (row_end 0: to n); row0 a multiple of
   // BLOCK_ACTS (sa_vaep_step_f64_chunked: one launch per chunk of the batch)
   int64_t row0, row_end;
@@ -386,6 +387,9 @@ __device__ __forceinline__ void st_i64x2(float* __restrict__ base, int64_t col, 
 // label / formula stores (the stores that precede the main row loads).
 #ifndef SA_NUM_PROBE
 #define SA_NUM_PROBE 0
+#endif
+#ifndef SA_COND_FAMILY
+#define SA_COND_FAMILY 1  // the COND pass in family-major column order (0: window-major, A/B)
 #endif
 #ifndef SA_NUM_FAMILY_MAJOR
 #define SA_NUM_FAMILY_MAJOR 0  // numeric pass store order (num_features_kernel, KF = 3)
@@ -1350,7 +1354,10 @@ __device__ __forceinline__ void num_features_body(const FeatArgs& args, int64_t 
           args.xt_cells[jb] = cc[0];
         }
       }
-#if SA_NUM_FAMILY_MAJOR
+      // COND: the family-major order too -- the condition tables are numbered by column, so
+      // visiting the columns in block order moves through each 64-condition chunk once (a chunk
+      // change flushes the held bitmaps: window-major order changed chunks ~12 times per wave)
+      if constexpr (SA_NUM_FAMILY_MAJOR || (COND && SA_COND_FAMILY)) {
       // family by family, each family's windows back to back: the block columns are
       // family-major with the windows adjacent, so the wave writes its [C x 128] slab front to
       // back instead of jumping by the family width for every window.  Window i of action e
@@ -1402,7 +1409,7 @@ __device__ __forceinline__ void num_features_body(const FeatArgs& args, int64_t 
         family(FAM_TD);
         family(FAM_SD);
       }
-#else
+      } else {
 #pragma unroll 1
       for (int i = 0; i < K; ++i) {
         if (i > 0) {
@@ -1427,7 +1434,7 @@ __device__ __forceinline__ void num_features_body(const FeatArgs& args, int64_t 
         }
         emit_window<ATOMIC, FT, IT>(C, i, wf, sx0, sy0, t0, fb, ib, Rf, Ri);
       }
-#endif
+      }
     } else {
       for (int i = 0; i < K; ++i) {
         const sa_frame& Fi = EXPLICIT ? A.frames[i] : F0;
@@ -1469,11 +1476,49 @@ void num_features_kernel(FeatArgs args) {
   num_features_body<ATOMIC, EXPLICIT, KF, TAIL, N32, COND>(args, wave_base, args.a.frames[0], args.ps, args.pc);
 }
 
+// sa_vaep_features_conditions' numeric pass with the condition tables (column starts,
+// thresholds, NaN directions: 4 (Cf + Ci + 2) + 8 n_cond bytes) staged in LDS once per
+// workgroup.  Read from global memory, each column's starts and each segment's thresholds cost
+// a vmcnt(0) wait -- on gfx950 also a wait for every store the wave issued before (the bitmap
+// flushes) -- in the middle of the pass; from LDS an lgkmcnt wait on a ds_read.
+constexpr int COND_LDS_MAX = 32 * 1024;  // bytes of staged tables per workgroup (else global)
+__host__ __device__ inline int64_t cond_lds_bytes(int64_t cf, int64_t ci, int64_t n_cond) {
+  return 4 * (cf + ci + 2) + 8 * n_cond;
+}
+template <bool ATOMIC>
+__global__ __launch_bounds__(64 * BLOCK_WAVES) __attribute__((amdgpu_waves_per_eu(num_min_waves<ATOMIC, false>(), 8)))
+void num_cond_lds_kernel(FeatArgs args) {
+  extern __shared__ __attribute__((aligned(16))) int32_t ctab[];
+  const int nf = (int)args.Cf + 1, ni = (int)args.Ci + 1, nc = args.cond_n;
+  int32_t* fs = ctab;
+  int32_t* is = fs + nf;
+  float* th = reinterpret_cast<float*>(is + ni);
+  int32_t* dl = reinterpret_cast<int32_t*>(th + nc);
+  for (int i = threadIdx.x; i < nf; i += 64 * BLOCK_WAVES) fs[i] = args.cond_fstart[i];
+  for (int i = threadIdx.x; i < ni; i += 64 * BLOCK_WAVES) is[i] = args.cond_istart[i];
+  for (int i = threadIdx.x; i < nc; i += 64 * BLOCK_WAVES) {
+    th[i] = args.cond_thr[i];
+    dl[i] = args.cond_dl[i];
+  }
+  __syncthreads();
+  FeatArgs a = args;
+  a.cond_fstart = fs;
+  a.cond_istart = is;
+  a.cond_thr = th;
+  a.cond_dl = dl;
+  const int wv = threadIdx.x / WAVE;
+  const int64_t wave_base = args.row0 + (xcd_logical_block() * BLOCK_WAVES + wv) * WAVE_ACTS;
+  num_features_body<ATOMIC, false, 3, false, false, true>(a, wave_base, a.a.frames[0], a.ps, a.pc);
+}
+
 // SA_FUSED_STEP = 1 (probe builds): the SPADL step's bool pass and numeric step pass as ONE
 // launch, their workgroups interleaved in proportion (logical workgroup L is a bool one when
 // floor((L + 1) nb / T) > floor(L nb / T)), so each CU mixes the pure-store bool tiles with the
 // read-heavy numeric tiles of the same rows, whose inputs the two then share in L2.  The A/B of
 // the headline's one bounded experiment (scripts/fused_step_ab.py).
+#ifndef SA_COND_LDS
+#define SA_COND_LDS 1  // 0: the COND pass reads its condition tables from global memory (A/B)
+#endif
 #ifndef SA_FUSED_STEP
 #define SA_FUSED_STEP 0
 #endif
@@ -2111,6 +2156,7 @@ extern "C" int sa_vaep_features_conditions(const sa_actions* a, const sa_feature
   c.cond_thr = cond_thr;
   c.cond_dl = cond_dl;
   c.cond_row0 = n_bool_cols;
+  c.cond_n = n_cond;
   return launch_features(a, plan, nullptr, &fz, &iz, 0, 0, nullptr, stream, bits, bits_stride, n_bool_cols, nullptr,
                          false, &c);
 }
@@ -2259,6 +2305,7 @@ static int launch_features(const sa_actions* a, const sa_feature_plan* plan, con
                 cond ? cond->cond_thr : nullptr,
                 cond ? cond->cond_dl : nullptr,
                 cond ? cond->cond_row0 : 0};
+  args.cond_n = cond ? cond->cond_n : 0;
   const dim3 grid(xcd_grid((a->n + BLOCK_ACTS - 1) / BLOCK_ACTS)), block(BLOCK_WAVES * WAVE);
   const bool expl = a->n_frames > 1;
   if (wb) {  // one wave per (tile, group of ~32 columns), XCD-contiguous sweep order
@@ -2306,7 +2353,13 @@ static int launch_features(const sa_actions* a, const sa_feature_plan* plan, con
   const int gc = plan->i64_col[SA_XFN_GOALSCORE];
   if (wn || xt_cells || tail || (gc >= 0 && !expl)) {  // windowed mode: goalscore fused into this pass
     const bool fast = !expl && K <= 3;  // register-resident windows (KF = 3)
-    if (cond) {  // windowed, K <= 3 (checked by sa_vaep_features_conditions)
+    if (cond && SA_COND_LDS && cond_lds_bytes(args.Cf, args.Ci, args.cond_n) <= COND_LDS_MAX) {
+      const size_t lds = (size_t)cond_lds_bytes(args.Cf, args.Ci, args.cond_n);
+      if (a->atomic)
+        hipLaunchKernelGGL(num_cond_lds_kernel<true>, grid, block, lds, st, args);
+      else
+        hipLaunchKernelGGL(num_cond_lds_kernel<false>, grid, block, lds, st, args);
+    } else if (cond) {  // windowed, K <= 3 (checked by sa_vaep_features_conditions)
       if (a->atomic)
         hipLaunchKernelGGL((num_features_kernel<true, false, 3, false, false, true>), grid, block, 0, st, args);
       else
