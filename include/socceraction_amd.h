@@ -180,7 +180,8 @@ int sa_vaep_features_bits_f32(const sa_actions* a, const sa_feature_plan* plan, 
  * cond_dl[c]); the numeric columns are evaluated in the numeric pass and never written.
  * Condition c belongs to f64 column j for cond_fstart[j] <= c < cond_fstart[j+1] (j < n_f64_cols)
  * or i64 column j for cond_istart[j] <= c < cond_istart[j+1]; bits 16-byte aligned, bits_stride
- * a multiple of 16 bytes >= 16 * ceil(n / 128).  k <= 3.  The staged walk then reads every
+ * a multiple of 16 bytes >= 16 * ceil(n / 128).  k <= 3; n_f64_cols and n_i64_cols <= 63 (every
+ * k <= 3 plan: at most 47 / 15).  The staged walk then reads every
  * condition from these bitmaps (sa_tree_predict_staged with n_num = 0). */
 int sa_vaep_features_conditions(const sa_actions* a, const sa_feature_plan* plan, uint8_t* bits,
                                 int64_t bits_stride, int32_t n_bool_cols, int32_t n_f64_cols,

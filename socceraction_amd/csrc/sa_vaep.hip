@@ -97,6 +97,8 @@ struct CondAcc {
   uint64_t even, odd;  // this lane's condition (chunk + lane): ballots over even / odd rows
   uint64_t held;       // uniform: lanes holding a condition of the chunk
   int32_t chunk;       // uniform: first condition of the chunk
+  float tv;            // threshold of condition chunk + lane (loaded when the chunk changes)
+  uint64_t dlm;        // uniform: the chunk's conditions whose NaN goes left
 };
 
 // the sinks take the wave's first row (wb) and the ok / NaN masks from wave_base: one 128-row
@@ -112,7 +114,20 @@ struct CondSink {
   int32_t row0;
   int64_t wb, n;
   CondAcc* acc;
+  int32_t n_start;   // entries of start (columns + 1)
+  int32_t n_cond;
+  int32_t sv;        // start[lane] (lanes < n_start): a column's starts by v_readlane, no load
+  uint64_t ok0, ok1; // uniform: the wave's rows present (even / odd)
 };
+
+__device__ __forceinline__ CondSink cond_sink(const int32_t* start, int32_t n_start, const FeatArgs& args,
+                                              int64_t wb, int64_t n, CondAcc* acc) {
+  const int lane = threadIdx.x & 63;
+  const int64_t jb = wb + 2 * lane;
+  CondSink k{start, args.cond_thr, args.cond_dl, args.bbits, args.bstride, args.cond_row0, wb, n, acc,
+             n_start, args.cond_n, lane < n_start ? start[lane] : 0, __ballot(jb < n), __ballot(jb + 1 < n)};
+  return k;
+}
 
 __device__ __forceinline__ uint64_t spread32(uint32_t v) {  // bit i -> bit 2i
   uint64_t x = v;
@@ -150,31 +165,36 @@ __device__ __forceinline__ uint64_t writelane64(uint64_t old, uint64_t v, int k)
 __device__ __forceinline__ void cond_store(const CondSink* s, int64_t col, float x0, float x1) {
   CondAcc* a = s->acc;
   const int lane = threadIdx.x & 63;
-  const int64_t jb = s->wb + 2 * lane;
-  // per column: the rows present and the NaN rows as wave masks; per condition two compares,
-  // the rest is scalar (`!(x < thr)` is true for NaN: right unless NaN goes left)
-  const uint64_t ok0 = __ballot(jb < s->n), ok1 = __ballot(jb + 1 < s->n);
+  // per column: the NaN rows as wave masks (the rows present: per wave, in the sink); per
+  // condition two compares, the rest is scalar (`!(x < thr)` is true for NaN: right unless NaN
+  // goes left)
+  const uint64_t ok0 = s->ok0, ok1 = s->ok1;
   const uint64_t nan0 = __ballot(isnan(x0)), nan1 = __ballot(isnan(x1));
-  const int c0 = s->start[col], c1 = s->start[col + 1];
-  // the column's conditions in segments inside one 64-condition chunk: a segment's thresholds
-  // come in one vector load (one per lane) and are read back by v_readlane, and the chunk test
-  // runs once per segment, not per condition (the COND pass cost 0.9 ms over the plain
-  // numeric pass at cfg2 with a load and a chunk test per condition, r06t / r06d)
+  // the column's first / end condition from the lane-resident starts (n_start <= 64: checked by
+  // sa_vaep_features_conditions; k <= 3 plans have at most 47 f64 / 15 i64 columns)
+  SA_DCHECK(col + 1 < s->n_start, col);
+  const int c0 = __builtin_amdgcn_readlane(s->sv, (int)col);
+  const int c1 = __builtin_amdgcn_readlane(s->sv, (int)col + 1);
+  // the column's conditions in segments inside one 64-condition chunk; a chunk's thresholds and
+  // NaN directions are loaded (one per lane) when the wave enters it and read back by
+  // v_readlane, so a segment costs no load and no wait (the COND pass with a threshold load and
+  // chunk test per condition cost 0.9 ms over the plain numeric pass, with a load per segment
+  // 0.8, r06t / r06i)
   for (int cb = c0; cb < c1;) {  // wave-uniform
     const int chunk = cb & ~63;
     if (chunk != a->chunk) {
       if (a->held) cond_flush(s);
       a->chunk = chunk;
+      const int cl = chunk + lane;
+      a->tv = cl < s->n_cond ? s->thr[cl] : 0.0f;
+      a->dlm = __ballot(cl < s->n_cond && s->dl[cl] != 0);  // NaN goes left, per condition
     }
     const int ce = c1 < chunk + 64 ? c1 : chunk + 64;
-    const int cl = cb + lane;
-    const float tv = cl < ce ? s->thr[cl] : 0.0f;
-    const uint64_t dlm = __ballot(cl < ce && s->dl[cl] != 0);  // NaN goes left, per condition
     for (int c = cb; c < ce; ++c) {
-      const int q = c - cb;
-      const float thr = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(tv), q));
+      const int q = c & 63;
+      const float thr = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(a->tv), q));
       uint64_t m0 = __ballot(!(x0 < thr)) & ok0, m1 = __ballot(!(x1 < thr)) & ok1;
-      if ((dlm >> q) & 1ull) {
+      if ((a->dlm >> q) & 1ull) {
         m0 &= ~nan0;
         m1 &= ~nan1;
       }
@@ -1198,11 +1218,12 @@ __device__ __forceinline__ void num_features_body(const FeatArgs& args, int64_t 
   const int64_t Rf = args.Rf, Ri = args.Ri;
   // whole wave past the end (uniform: the goalscore ballots need every lane)
   if (wave_base >= n || (args.row_end > 0 && wave_base >= args.row_end)) return;
-  CondAcc acc{0, 0, 0, -64};
-  CondSink sink_f{args.cond_fstart, args.cond_thr, args.cond_dl, args.bbits, args.bstride, args.cond_row0,
-                  wave_base, n, &acc};
-  CondSink sink_i{args.cond_istart, args.cond_thr, args.cond_dl, args.bbits, args.bstride, args.cond_row0,
-                  wave_base, n, &acc};
+  CondAcc acc{0, 0, 0, -64, 0.0f, 0};
+  CondSink sink_f, sink_i;
+  if constexpr (COND) {
+    sink_f = cond_sink(args.cond_fstart, (int)args.Cf + 1, args, wave_base, n, &acc);
+    sink_i = cond_sink(args.cond_istart, (int)args.Ci + 1, args, wave_base, n, &acc);
+  }
   auto fblock = [&](int64_t j) -> FT* {
     if constexpr (COND) return &sink_f;
     else return reinterpret_cast<FT*>(args.fout) + tile_off(j, 0, args.Cf, Rf);
@@ -2148,6 +2169,8 @@ extern "C" int sa_vaep_features_conditions(const sa_actions* a, const sa_feature
     return fail(SA_EINVAL, "condition bitmaps: 16-byte aligned rows of at least ceil(n/128)*16 bytes");
   if (!cond_fstart || !cond_istart || (n_cond > 0 && (!cond_thr || !cond_dl)))
     return fail(SA_EINVAL, "null condition table");
+  if (n_f64_cols >= WAVE || n_i64_cols >= WAVE)  // the starts are held one per lane
+    return fail(SA_EINVAL, "condition bitmaps: at most %d f64 and %d i64 columns", WAVE - 1, WAVE - 1);
   // stand-in descriptors: the numeric pass writes no block in this mode, only the bitmaps
   const sa_block fz{bits, n_f64_cols, 0, 128}, iz{bits, n_i64_cols, 0, 128};
   FeatArgs c{};
