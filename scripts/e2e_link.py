@@ -131,6 +131,13 @@ def pipeline_probe(games: int = 1000):
             t.append(time.perf_counter() - t0)
         out[f'compute_batch_ms_chunk_{chunk}'] = round(min(t) * 1e3, 2)
     from socceraction_amd.pipeline import value_frames
+    for ramp in ((4, 2), (), (8, 4, 2)):  # the first chunks' sizes: chunk_rows / ramp[i]
+        t = []
+        for _ in range(4):
+            t0 = time.perf_counter()
+            value_frames(model, gframe, actions, p['scores'], p['concedes'], chunk_rows=1 << 18, ramp=ramp)
+            t.append(time.perf_counter() - t0)
+        out[f'value_frames_ms_ramp_{"_".join(map(str, ramp)) or "none"}'] = round(min(t[1:]) * 1e3, 2)
     tl = []
     value_frames(model, gframe, actions, p['scores'], p['concedes'], chunk_rows=1 << 18, timeline=tl)
     out['timeline_chunk_262144'] = tl

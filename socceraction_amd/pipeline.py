@@ -19,6 +19,7 @@ games (one segment per game; ``tests/test_gpu_dropin.py``).
 """
 from __future__ import annotations
 
+import time
 from typing import Optional, Tuple
 
 import numpy as np
@@ -33,15 +34,18 @@ def _pinned(shape, dtype) -> torch.Tensor:
     return torch.empty(shape, dtype=dtype, pin_memory=True)
 
 
-def _chunks(seg_off: np.ndarray, chunk_rows: int, look: int = 16):
+def _chunks(seg_off: np.ndarray, chunk_rows: int, look: int = 16, ramp=(4, 2)):
     """Game-aligned cuts: segments [s0, s1) of about chunk_rows actions each, each cut at a game
     boundary whose row is a multiple of 4 when one lies within ``look`` games: the DMA engine
     moves a pitched copy at the link rate only from and to 4-byte aligned addresses (the bool
-    and label blocks are 1 byte per row: 57 vs 14 GB/s, scripts/e2e_link.py probe, r06g)."""
+    and label blocks are 1 byte per row: 57 vs 14 GB/s, scripts/e2e_link.py probe, r06g).
+    The first chunks are chunk_rows / ramp[i]: the link idles until the first chunk is encoded
+    and valued, so a small first chunk starts the copies sooner."""
     cuts, s0 = [], 0
     nseg = len(seg_off) - 1
     while s0 < nseg:
-        target = seg_off[s0] + chunk_rows
+        k = len(cuts)
+        target = seg_off[s0] + (max(1, chunk_rows // ramp[k]) if k < len(ramp) else chunk_rows)
         s1 = int(np.searchsorted(seg_off, target, side='right')) - 1
         s1 = min(max(s1, s0 + 1), nseg)
         if s1 < nseg and seg_off[s1] % 4:
@@ -67,12 +71,13 @@ class _Slot:
 
 def value_frames(model, games: pd.DataFrame, actions: pd.DataFrame,
                  p_scores: Optional[np.ndarray] = None, p_concedes: Optional[np.ndarray] = None,
-                 chunk_rows: int = 1 << 18, timeline: Optional[list] = None
+                 chunk_rows: int = 1 << 18, timeline: Optional[list] = None, ramp=(4, 2)
                  ) -> Tuple[pd.DataFrame, pd.DataFrame, Optional[pd.DataFrame]]:
     """(features, labels, values) of ``actions`` (each game's rows contiguous, ``games`` maps
     game_id -> home_team_id) for a VAEP / AtomicVAEP ``model`` whose transformers are all
     known ones.  ``values`` is None without probabilities (float32 or float64; values take
     their dtype, the reference's rule)."""
+    t_call = time.perf_counter()
     known, unknown = model._split_xfns()
     if unknown:
         raise ValueError('the pipelined batch path takes the built-in transformers only')
@@ -101,8 +106,10 @@ def value_frames(model, games: pd.DataFrame, actions: pd.DataFrame,
             raise ValueError('one probability per action is required')
         vdt = torch.float32 if (ps.dtype == np.float32 and pc.dtype == np.float32) else torch.float64
         nd = np.float32 if vdt == torch.float32 else np.float64
-        tps = torch.from_numpy(np.ascontiguousarray(ps, nd)).to(dev)
-        tpc = torch.from_numpy(np.ascontiguousarray(pc, nd)).to(dev)
+        # the probabilities go up chunk by chunk with the chunk's columns (below), while the host
+        # would otherwise wait for the copies out: not as one blocking copy before the first chunk
+        ps = np.ascontiguousarray(ps, nd)
+        pc = np.ascontiguousarray(pc, nd)
     # the whole frame's host blocks, column-major [cols, ld] (pinned: the DMA writes them), rows
     # on 16-byte boundaries (aligned DMA; the frames view [:, :n])
     ld = max(16, (n + 15) // 16 * 16)
@@ -111,7 +118,7 @@ def value_frames(model, games: pd.DataFrame, actions: pd.DataFrame,
     hi = _pinned((plan.n_i64, ld), torch.int64)
     hl = _pinned((3, ld), torch.uint8)
     hv = _pinned((3, ld), vdt) if vdt is not None else None
-    cuts = _chunks(seg_off, chunk_rows) if n else []
+    cuts = _chunks(seg_off, chunk_rows, ramp=ramp) if n else []
     rmax = max((int(seg_off[s1] - seg_off[s0]) for s0, s1 in cuts), default=16)
     slots = [_Slot(plan, rmax, dev, vdt) for _ in range(min(2, max(1, len(cuts))))]
     main = torch.cuda.current_stream()
@@ -126,8 +133,9 @@ def value_frames(model, games: pd.DataFrame, actions: pd.DataFrame,
         _native.check(lib.sa_copy2d_async(dst.data_ptr() + r0 * es, dst.shape[1] * es,
                                            src.data_ptr(), src.shape[-1] * es, m * es, rows,
                                            copy.cuda_stream))
-    import time
     t_start = time.perf_counter()
+    if timeline is not None:
+        timeline.append({'setup_ms': round((t_start - t_call) * 1e3, 2)})
     evs = []
     for k, (s0, s1) in enumerate(cuts):
         r0, r1 = int(seg_off[s0]), int(seg_off[s1])
@@ -146,7 +154,9 @@ def value_frames(model, games: pd.DataFrame, actions: pd.DataFrame,
         ops.features_into(ab.struct(), fb)
         lb = ops.LabelBlocks(m, slot.lab[0], slot.lab[1], slot.lab[2])
         if vdt is not None:
-            ops.labels_formula(ab, tps[r0:r1], tpc[r0:r1], labels_out=lb, values_out=slot.val)
+            tps = torch.from_numpy(ps[r0:r1]).to(dev, non_blocking=True)
+            tpc = torch.from_numpy(pc[r0:r1]).to(dev, non_blocking=True)
+            ops.labels_formula(ab, tps, tpc, labels_out=lb, values_out=slot.val)
         else:
             ops.labels(ab, out=lb)
         # 3. pitched copies into the frame's host blocks, on the copy stream
@@ -167,7 +177,7 @@ def value_frames(model, games: pd.DataFrame, actions: pd.DataFrame,
             eb.record(copy)
             evs.append((k, m, th0 - t_start, th1 - t_start, time.perf_counter() - t_start, ea, eb))
         slot.used = True
-        slot.keep = ab  # the batch's device columns stay alive until the slot is reused
+        slot.keep = (ab, tps, tpc) if vdt is not None else ab  # alive until the slot is reused
     copy.synchronize()
     main.synchronize()
     if timeline is not None and evs:
@@ -177,16 +187,19 @@ def value_frames(model, games: pd.DataFrame, actions: pd.DataFrame,
                              'queued_ms': round(c * 1e3, 2),
                              'd2h_ms_from_first': (round(e0.elapsed_time(ea), 2), round(e0.elapsed_time(eb), 2))})
         timeline.append({'host_total_ms': round((time.perf_counter() - t_start) * 1e3, 2)})
+    t_frames = time.perf_counter()
     X = catalog.assemble_frame(plan, hb.numpy(), hf.numpy(), hi.numpy(), n, pd.RangeIndex(n))
     hln = hl.numpy()  # numpy views keep their pinned tensors alive (so do the frames over them)
     ycols = {}
     for f in model.yfns:  # compute_labels' columns (atomic: goal_from_shot is named 'goal')
         key = names[f]
         ycols['goal' if (atomic and key == 'goal_from_shot') else key] = hln[lrow[key], :n].view(bool)
-    Y = pd.DataFrame(ycols, index=pd.RangeIndex(n))
+    Y = pd.DataFrame(ycols, index=pd.RangeIndex(n), copy=False)  # views, as X (a copy: 5 ms)
     V = None
     if vdt is not None:
         hvn = hv.numpy()
         V = pd.DataFrame({'offensive_value': hvn[0, :n], 'defensive_value': hvn[1, :n],
-                          'vaep_value': hvn[2, :n]})
+                          'vaep_value': hvn[2, :n]}, copy=False)
+    if timeline is not None:
+        timeline.append({'frames_ms': round((time.perf_counter() - t_frames) * 1e3, 2)})
     return X, Y, V

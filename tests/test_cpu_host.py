@@ -855,7 +855,10 @@ def test_pipeline_chunks_cut_at_games_on_aligned_rows():
     assert cuts[0][0] == 0 and cuts[-1][1] == len(sizes)
     assert all(a[1] == b[0] for a, b in zip(cuts, cuts[1:]))
     assert all(off[s1] % 4 == 0 for _, s1 in cuts[:-1])
-    assert all(abs((off[s1] - off[s0]) - 50_000) < 40_000 for s0, s1 in cuts[:-1])
+    want = [12_500, 25_000] + [50_000] * len(cuts)  # the ramp: chunk_rows / 4, / 2, then chunk_rows
+    assert all(abs((off[s1] - off[s0]) - w) < 10_000 for (s0, s1), w in zip(cuts[:-1], want))
+    flat = pipeline._chunks(off, 50_000, ramp=())
+    assert all(abs((off[s1] - off[s0]) - 50_000) < 10_000 for s0, s1 in flat[:-1])
     odd = np.concatenate([[0], np.cumsum(np.full(50, 1001))])  # no row but 0 mod 4 every 4 games
     cuts = pipeline._chunks(odd, 5000, look=0)
     assert cuts[-1][1] == 50 and all(a[1] == b[0] for a, b in zip(cuts, cuts[1:]))
