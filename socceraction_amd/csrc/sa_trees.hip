@@ -38,6 +38,9 @@ struct TNode {  // 24 B
 constexpr int TR_THREADS = 1024;  // 16 waves share one LDS copy of the model
 constexpr int TR_LDS_NODES = 2048;  // 48 KB
 constexpr int TR_LDS_SLOTS = 2048;  // 8 KB
+#ifndef SA_TREE_SCALED
+#define SA_TREE_SCALED 1  // staged walk: condition byte offsets in the staged nodes (0: indices)
+#endif
 #ifndef SA_TREE_PERSIST
 #define SA_TREE_PERSIST 0  // staged walk grid: N x the resident workgroups looping over tiles (A/B: 1.19 ms vs 1.12 per learner at N = 1, r06i; 0: one per tile)
 #endif
@@ -404,7 +407,10 @@ __device__ __forceinline__ void stage_conditions(const CondSet<A>& P, const int3
 // per tree from global memory they cost ~90 scalar instructions per group of 8 trees (address
 // arithmetic and serialised waits), the walk's whole scalar budget (SQ_INSTS_SALU 1,159 per
 // wave of 2,523 VALU, profiles/r06t).
-template <typename A>
+// SCALED: the nodes' condition halves hold the condition's byte offset in M8 (condition x
+// TS_CSTRIDE, staged so when it fits 16 bits): the bit's address is then one add of the node's
+// low half, not a mask and a multiply-add (the walk is bound by VALU issue: 5 -> 4 per level).
+template <typename A, bool SCALED = false>
 __device__ __forceinline__ A walk_conditions(const CondModel<A>& P, const uint32_t* __restrict__ N,
                                              const A* __restrict__ LV, const uint8_t* __restrict__ M8,
                                              const int32_t* __restrict__ RD, int TSP, int s) {
@@ -425,7 +431,7 @@ __device__ __forceinline__ A walk_conditions(const CondModel<A>& P, const uint32
       for (int u = 0; u < TG; ++u) nd[u] = N[k[u]];
 #pragma unroll
       for (int u = 0; u < TG; ++u) {
-        const uint32_t bit = (Mrow[(nd[u] & 0xFFFFu) * TS_CSTRIDE] >> rbit) & 1u;
+        const uint32_t bit = (Mrow[SCALED ? (nd[u] & 0xFFFFu) : (nd[u] & 0xFFFFu) * TS_CSTRIDE] >> rbit) & 1u;
         k[u] = (int)(nd[u] >> 16) + (int)bit;
       }
     }
@@ -464,8 +470,10 @@ __global__ __launch_bounds__(TS_ROWS) void tree_cond_kernel(CondSet<typename std
                                            (size_t)(P.n_nodes + (P.n_nodes & 1)) * sizeof(A));
   int32_t* BC = RD + 2 * TSP;  // the bool conditions' columns / bitmap rows
   const int tid = threadIdx.x;
+  const bool scaled = SA_TREE_SCALED && (int64_t)n_cond * TS_CSTRIDE <= 0x10000;  // uniform
   for (int k = tid; k < P.n_nodes; k += TS_ROWS) {
-    N[k] = P.nodes[k];
+    const uint32_t nd = P.nodes[k];
+    N[k] = scaled ? (nd & 0xFFFF0000u) | ((nd & 0xFFFFu) * TS_CSTRIDE) : nd;
     LV[k] = P.leaf[k];
   }
   for (int t = tid; t < TSP; t += TS_ROWS) {  // padding: the last tree again, depth 0 (not summed)
@@ -483,7 +491,8 @@ __global__ __launch_bounds__(TS_ROWS) void tree_cond_kernel(CondSet<typename std
     __syncthreads();
     const int64_t j = R0 + tid;
     if (j < n) {
-      const A m = walk_conditions<A>(P, N, LV, M8, RD, TSP, tid);
+      const A m = scaled ? walk_conditions<A, true>(P, N, LV, M8, RD, TSP, tid)
+                         : walk_conditions<A, false>(P, N, LV, M8, RD, TSP, tid);
       if (F32)
         ((float*)P.out)[j] = 1.0f / (1.0f + expf(-(float)m));
       else
