@@ -195,8 +195,8 @@ def test_staged_walk_equals_gather_walk(sa, kind):
     np.testing.assert_array_equal(te.predict_blocks(fb).cpu().numpy(), ref)  # the default path
 
 
-@pytest.mark.parametrize('atomic', [False, True])
-def test_bool_bitmap_features_and_trees(sa, atomic):
+@pytest.mark.parametrize('atomic,k', [(False, 3), (True, 3), (False, 1), (False, 2), (True, 2)])
+def test_bool_bitmap_features_and_trees(sa, atomic, k):
     """sa_vaep_features_bits: the bool features as bitmaps equal the bool block bit for bit
     (rows >= n clear), the f64 / i64 blocks are unchanged, host export of the bitmap form equals
     the block form, and the staged walk reading the bitmaps equals the walk reading the block
@@ -213,17 +213,17 @@ def test_bool_bitmap_features_and_trees(sa, atomic):
         d = synthetic.spadl_games(150, seed=6)
         xfns = vo.SPADL_DEFAULT
     ab = B.ActionBatch.from_columns(d, atomic=atomic)
-    ref = ops.features(ab, xfns, 3, bool_tile=1024, num_tile=128)
-    got = ops.features(ab, xfns, 3, num_tile=128, bool_bits=True)
+    ref = ops.features(ab, xfns, k, bool_tile=1024, num_tile=128)
+    got = ops.features(ab, xfns, k, num_tile=128, bool_bits=True)
     assert got.bool_block is None and ref.n % 64 != 0
     rb = ref.block('b').cpu().numpy()
     bits = got.bool_bits.cpu().numpy().view(np.uint8)
     unpacked = np.unpackbits(bits, axis=1, bitorder='little')
     np.testing.assert_array_equal(unpacked[:, :ref.n], rb)
     assert not unpacked[:, ref.n:].any()
-    for k in 'fi':
-        np.testing.assert_array_equal(got.block(k).cpu().numpy(), ref.block(k).cpu().numpy())
-    if atomic:
+    for kb in 'fi':
+        np.testing.assert_array_equal(got.block(kb).cpu().numpy(), ref.block(kb).cpu().numpy())
+    if atomic or k != 3:
         return
     kinds = [k for _, k, _ in ref.plan.order]
     xg = trees.TreeEnsemble.from_model(trees.synthetic_xgboost_json(
