@@ -474,8 +474,10 @@ def atomic_extra(dist, rank, world, dev, games: int, reps: int = 21, check: bool
             ops.step_into(s, out2, None, None, 10, lab, None)
         ms2 = _events_median_ms(step2, reps)[0]
         placement = {'realloc_ms_per_step': round(ms2, 4), 'first_over_realloc': round(ms / ms2, 4),
-                     'mode': ('slow placement (first allocation >= 4 % slower than a fresh one)'
-                              if ms > 1.04 * ms2 else 'no slow placement seen')}
+                     'mode': ('slow placement: the first (timed) allocation >= 4 % slower than a fresh one'
+                              if ms > 1.04 * ms2 else
+                              'the fresh allocation got the slow placement (>= 4 % slower); the timed one did not'
+                              if ms2 > 1.04 * ms else 'no slow placement seen')}
         del out2
     except (RuntimeError, ValueError, MemoryError) as e:  # no second contiguous range: skip
         placement = {'error': f'{type(e).__name__}: {e}'}
