@@ -571,6 +571,12 @@ def xt105_extra(ab, dist, dev, sharded: bool = False, cfg5_games: int = 62500,
             with phase('count_all_reduce'):
                 allreduce_counts(dist, acc)
             mark()
+            if marks is None and timer is None:  # the timed calls: solve + rate in one call, the
+                # rate queued behind the solve before its host round trip (sa_xt_fit_rate_interp_codes)
+                sol, rates, _ = ops.xt_fit_rate_interp_codes(acc, icodes, [b.n for b in batches],
+                                                             axes=axes, outs=rate_out)
+                path[0] = sol.path
+                return sol.n_iter, acc, sol.mats, rates
             with phase('solve'):
                 sol = ops.xt_solve(acc, transition=False)  # synchronises; ExpectedThreat.fit's
             mats, n_iter = sol.mats, sol.n_iter           # call above 1024 cells
@@ -659,7 +665,9 @@ def xt105_extra(ab, dist, dev, sharded: bool = False, cfg5_games: int = 62500,
                               f'{rank}): count = band buckets + table; exchange = the counts\' '
                               'all-reduce (band-sharded: count and exchange inside solve); '
                               'solve = normalise + value '
-                              'iteration incl. its host syncs; rate'),
+                              'iteration incl. its host syncs; rate (the timed calls with one GPU '
+                              'or the replicated solve run solve + rate as one call, the rate '
+                              'queued behind the solve before its host round trip)'),
             'phase_events_ms': dict(events, note=f'HIP events around each phase of one more call '
                                     f'(rank {rank}; current stream, the collectives ordered on it)'),
             **({'exchange': {k: v for k, v in dict(xstats, rank=rank).items() if k != 'timer'}}

@@ -348,6 +348,21 @@ int sa_xt_rate_interp_codes_many(int32_t nsets, const uint64_t* const* interp_co
                                  const double* cy, int32_t l, int32_t w, const double* xs,
                                  int32_t L, const double* ys, int32_t W, double* const* out,
                                  int32_t* err_flags, void* stream);
+/* ExpectedThreat.fit + rate(use_interpolation=True) of the same actions (xthreat.py:322-345,
+ * 408-465) in one call, for grids above the small-grid limit: sa_xt_solve_ex (no transposed
+ * matrix; ell / row_len the count's compact rows or NULL) then sa_xt_rate_interp_codes_many over
+ * the surface mats[3 * C ..] -- the rate queued right behind the one-launch reordered solve,
+ * before the host waits for the solve's status, and run again when the status sends the solve to
+ * the reference's order.  The same outputs as the two calls. */
+int sa_xt_fit_rate_interp_codes(const int64_t* shot, const int64_t* goal, const int64_t* move,
+                                const int32_t* trans, int32_t l, int32_t w, double eps,
+                                int32_t max_iter, int32_t flags, double* mats, double* heatmaps,
+                                int32_t* n_iter, int32_t* path, const uint32_t* ell,
+                                const int32_t* row_len, int32_t nsets,
+                                const uint64_t* const* interp_codes, const int64_t* n,
+                                const double* cx, const double* cy, const double* xs, int32_t L,
+                                const double* ys, int32_t W, double* const* out,
+                                int32_t* err_flags, void* stream);
 int sa_xt_count_from_buckets(int32_t nsets, const uint16_t* const* buckets,
                              const int64_t* const* band_off, int32_t l, int32_t w, int64_t* shot,
                              int64_t* goal, int64_t* move, int32_t* trans, int32_t flags,

@@ -178,6 +178,13 @@ _SIGNATURES = {
                                                     ctypes.POINTER(ctypes.c_int64), _p, _p, _p,
                                                     ctypes.c_int32, ctypes.c_int32, _p, ctypes.c_int32,
                                                     _p, ctypes.c_int32, ctypes.POINTER(_p), _p, _p]),
+    'sa_xt_fit_rate_interp_codes': (ctypes.c_int, [_p, _p, _p, _p, ctypes.c_int32, ctypes.c_int32,
+                                                   ctypes.c_double, ctypes.c_int32, ctypes.c_int32, _p, _p,
+                                                   ctypes.POINTER(ctypes.c_int32),
+                                                   ctypes.POINTER(ctypes.c_int32), _p, _p, ctypes.c_int32,
+                                                   ctypes.POINTER(_p), ctypes.POINTER(ctypes.c_int64), _p, _p,
+                                                   _p, ctypes.c_int32, _p, ctypes.c_int32, ctypes.POINTER(_p),
+                                                   _p, _p]),
     'sa_xt_count_from_buckets_ex': (ctypes.c_int, [ctypes.c_int32, ctypes.POINTER(_p), ctypes.POINTER(_p),
                                                    ctypes.c_int32, ctypes.c_int32, _p, _p, _p, _p,
                                                    ctypes.c_int32, _p, _p, _p]),

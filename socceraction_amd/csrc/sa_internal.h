@@ -48,7 +48,16 @@ int xt_compact_iterate(const uint32_t* ell, const int32_t* row_len, const int32_
 // reordered sums under an error bound, or the reference's order (SA_XT_SOLVE_EXACT, or when the
 // bound cannot decide); *path = SA_XT_PATH_*.  xt_out (optional): the reordered path also
 // writes the final iterate there (the surface).  Synchronises the stream.
+// hook (optional): work enqueued right after the one-launch reordered solve, before the host
+// waits for its status (sa_xt_fit_rate_interp_codes: the rate of the surface the solve writes);
+// hook->ran says whether it was.
+struct SolveHook {
+  int (*fn)(void* ctx);
+  void* ctx;
+  bool ran;
+};
 int xt_compact_solve(const uint32_t* ell, const int32_t* row_len, const int32_t* cnt_rows, const int64_t* move,
                      const double* gs, const double* pmove, int C, double eps, int max_iter, int flags,
-                     double* heat, int* n_iter, int* path, hipStream_t st, double* xt_out = nullptr);
+                     double* heat, int* n_iter, int* path, hipStream_t st, double* xt_out = nullptr,
+                     SolveHook* hook = nullptr);
 }  // namespace sa

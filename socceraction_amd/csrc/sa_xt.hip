@@ -1123,10 +1123,23 @@ extern "C" int sa_xt_solve(const int64_t* shot, const int64_t* goal, const int64
                         nullptr, nullptr, stream);
 }
 
+static int solve_ex(const int64_t* shot, const int64_t* goal, const int64_t* move, const int32_t* trans, int32_t l,
+                    int32_t w, double eps, int32_t max_iter, int32_t flags, double* mats, double* trans_t,
+                    double* heatmaps, int32_t* n_iter, int32_t* path, const uint32_t* ell_in,
+                    const int32_t* row_len_in, void* stream, SolveHook* hook);
+
 extern "C" int sa_xt_solve_ex(const int64_t* shot, const int64_t* goal, const int64_t* move,
                               const int32_t* trans, int32_t l, int32_t w, double eps, int32_t max_iter,
                               int32_t flags, double* mats, double* trans_t, double* heatmaps, int32_t* n_iter,
                               int32_t* path, const uint32_t* ell_in, const int32_t* row_len_in, void* stream) {
+  return solve_ex(shot, goal, move, trans, l, w, eps, max_iter, flags, mats, trans_t, heatmaps, n_iter, path, ell_in,
+                  row_len_in, stream, nullptr);
+}
+
+static int solve_ex(const int64_t* shot, const int64_t* goal, const int64_t* move, const int32_t* trans, int32_t l,
+                    int32_t w, double eps, int32_t max_iter, int32_t flags, double* mats, double* trans_t,
+                    double* heatmaps, int32_t* n_iter, int32_t* path, const uint32_t* ell_in,
+                    const int32_t* row_len_in, void* stream, SolveHook* hook) {
   if (l < 1 || w < 1 || max_iter < 0) return fail(SA_EINVAL, "bad l, w or max_iter");
   const int C = l * w;
   if (!shot || !goal || !move || !trans || !mats || (!trans_t && C <= XT_SOLVE_MAX_C) || !heatmaps || !n_iter)
@@ -1193,7 +1206,7 @@ extern "C" int sa_xt_solve_ex(const int64_t* shot, const int64_t* goal, const in
     if (compact && !rc) {  // reordered under the error bound, or the reference's order
       int p = SA_XT_PATH_SEQUENTIAL;
       rc = xt_compact_solve(ell, slen, trans, move, gs, pm, C, eps, max_iter, flags, heatmaps, &iters, &p, st,
-                            mats + 3 * C);
+                            mats + 3 * C, hook);
       if (path) *path = p;
       surface_done = p == SA_XT_PATH_REORDERED;
     }
@@ -1366,6 +1379,44 @@ extern "C" int sa_xt_rate_interp_codes_many(int32_t nsets, const uint64_t* const
     rc = check_launch("xt_rate_icodes_lds_kernel");
   }
   scratch_release(sc, st);
+  return rc;
+}
+
+// ExpectedThreat.fit + rate(use_interpolation=True) of the same actions in one call: sa_xt_solve_ex
+// (no transposed matrix) then sa_xt_rate_interp_codes_many over the surface it wrote.  Above the
+// small-grid limit the rate is queued right behind the one-launch reordered solve, before the
+// host waits for the solve's status -- no host round trip between the two; when the status
+// sends the solve to another path (the reference's order: a decision inside the bound, a
+// barrier timeout, an escaped count) the surface is rewritten and the rate runs again.
+extern "C" int sa_xt_fit_rate_interp_codes(const int64_t* shot, const int64_t* goal, const int64_t* move,
+                                           const int32_t* trans, int32_t l, int32_t w, double eps, int32_t max_iter,
+                                           int32_t flags, double* mats, double* heatmaps, int32_t* n_iter,
+                                           int32_t* path, const uint32_t* ell, const int32_t* row_len, int32_t nsets,
+                                           const uint64_t* const* interp_codes, const int64_t* n, const double* cx,
+                                           const double* cy, const double* xs, int32_t L, const double* ys,
+                                           int32_t W, double* const* out, int32_t* err_flags, void* stream) {
+  if (l < 1 || w < 1 || !mats || !path) return fail(SA_EINVAL, "bad l, w or null mats / path");
+  if (l * w <= XT_SOLVE_MAX_C) return fail(SA_EINVAL, "the fused fit + rate is for grids above %d cells", XT_SOLVE_MAX_C);
+  struct Rate {
+    int32_t nsets;
+    const uint64_t* const* codes;
+    const int64_t* n;
+    const double *xT, *cx, *cy, *xs, *ys;
+    int32_t l, w, L, W;
+    double* const* out;
+    int32_t* err;
+    void* stream;
+  } r{nsets, interp_codes, n, mats + 3 * (int64_t)(l * w), cx, cy, xs, ys, l, w, L, W, out, err_flags, stream};
+  auto rate = [](void* p) -> int {
+    const Rate& q = *static_cast<const Rate*>(p);
+    return sa_xt_rate_interp_codes_many(q.nsets, q.codes, q.n, q.xT, q.cx, q.cy, q.l, q.w, q.xs, q.L, q.ys, q.W,
+                                        q.out, q.err, q.stream);
+  };
+  SolveHook hook{rate, &r, false};
+  int rc = solve_ex(shot, goal, move, trans, l, w, eps, max_iter, flags, mats, nullptr, heatmaps, n_iter, path, ell,
+                    row_len, stream, &hook);
+  if (rc) return rc;
+  if (!hook.ran || *path != SA_XT_PATH_REORDERED) rc = rate(&r);  // the surface the solve returned
   return rc;
 }
 

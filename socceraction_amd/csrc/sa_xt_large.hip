@@ -1771,7 +1771,8 @@ static int g_xf_force_abort = -1;
 
 static int xt_solve_reordered(const uint32_t* ell, const int32_t* row_len, const int32_t* cnt_rows,
                               const int64_t* move, const double* gs, const double* pmove, int C, double eps,
-                              int max_iter, double* heat, double* xt_out, int* n_iter, int* status, hipStream_t st) {
+                              int max_iter, double* heat, double* xt_out, int* n_iter, int* status, hipStream_t st,
+                              SolveHook* hook) {
   *status = 2;
   *n_iter = -1;
   if (!xt_compact_ok(C) || max_iter < 1) return SA_OK;
@@ -1813,6 +1814,10 @@ static int xt_solve_reordered(const uint32_t* ell, const int32_t* row_len, const
     rc = check_launch("xt_solve_reordered_kernel");
   }
   if (!rc) rc = check_hip(hipMemcpyAsync(h, ctrl, 8 * sizeof(int32_t), hipMemcpyDeviceToHost, st), "copy solve control");
+  if (!rc && hook) {  // queued behind the solve: no host round trip between the two
+    rc = hook->fn(hook->ctx);
+    hook->ran = true;
+  }
   if (!rc) rc = check_hip(hipStreamSynchronize(st), "hipStreamSynchronize");
 #if SA_XF_PROBE
   int32_t pro[4] = {0, 0, 0, 0};
@@ -1841,13 +1846,13 @@ static int xt_solve_reordered(const uint32_t* ell, const int32_t* row_len, const
 // cannot decide.  *path: SA_XT_PATH_*.  Synchronises the stream.
 int xt_compact_solve(const uint32_t* ell, const int32_t* row_len, const int32_t* cnt_rows, const int64_t* move,
                      const double* gs, const double* pmove, int C, double eps, int max_iter, int flags,
-                     double* heat, int* n_iter, int* path, hipStream_t st, double* xt_out) {
+                     double* heat, int* n_iter, int* path, hipStream_t st, double* xt_out, SolveHook* hook) {
   *n_iter = -1;
   *path = SA_XT_PATH_SEQUENTIAL;
   if (!(flags & SA_XT_SOLVE_EXACT)) {
     int status = 2, it = -1;
     int rc = xt_solve_reordered(ell, row_len, cnt_rows, move, gs, pmove, C, eps, max_iter, heat, xt_out, &it,
-                                &status, st);
+                                &status, st, xt_out ? hook : nullptr);
     if (rc) return rc;
     if (status == 0) {
       *n_iter = it;

@@ -570,6 +570,58 @@ def xt_rate_interp_codes_many(icodes: Sequence[torch.Tensor], ns: Sequence[int],
     return [t[:n] for t, n in zip(outs, ns)], err
 
 
+def xt_fit_rate_interp_codes(acc: XTCounts, icodes: Sequence[torch.Tensor], ns: Sequence[int],
+                             L: int = 1050, W: int = 680, axes: Optional[torch.Tensor] = None,
+                             outs: Optional[Sequence[torch.Tensor]] = None, eps: float = 1e-5,
+                             max_iter: int = 1000, exact_order: bool = False
+                             ) -> Tuple[XTSolution, List[torch.Tensor], torch.Tensor]:
+    """:func:`xt_solve` (``transition=False``) then :func:`xt_rate_interp_codes_many` over the
+    surface, in one call (``sa_xt_fit_rate_interp_codes``, grids above ``SA_XT_SOLVE_MAX_C``
+    cells): the rate is queued right behind the one-launch solve instead of after its host
+    round trip.  The same outputs as the two calls."""
+    C, l, w = acc.C, acc.l, acc.w
+    if C <= _native.SA_XT_SOLVE_MAX_C:
+        raise ValueError('the fused fit + rate is for grids above SA_XT_SOLVE_MAX_C cells')
+    if len(icodes) != len(ns) or (outs is not None and len(outs) != len(ns)):
+        raise ValueError('one operand buffer, count (and out) per batch')
+    if getattr(acc, 'compact', None) is None:
+        acc.require_dense('xt_fit_rate_interp_codes without compact rows')
+    dev = acc.shot.device
+    axes = xt_interp_axes(l, w, dev, L, W) if axes is None else axes
+    if axes.numel() != l + w + L + W:
+        raise ValueError('axes must hold l + w + L + W node positions')
+    ns = [int(n) for n in ns]
+    for c, n in zip(icodes, ns):
+        if n < 0 or c.numel() * c.element_size() < 8 * n:
+            raise ValueError('an operand buffer holds fewer than n codes')
+    outs = [torch.empty(max(_ld(n), 16), dtype=torch.float64, device=dev) for n in ns] \
+        if outs is None else list(outs)
+    for o, n in zip(outs, ns):
+        if o.dtype != torch.float64 or o.numel() < n:
+            raise ValueError('out must be float64 with room for n values')
+    mats = torch.empty((4, C), dtype=torch.float64, device=dev)
+    heat = torch.empty((max_iter + 1, C), dtype=torch.float64, device=dev)
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    k = len(ns)
+    cp = (ctypes.c_void_p * max(k, 1))(*[c.data_ptr() for c in icodes])
+    op = (ctypes.c_void_p * max(k, 1))(*[o.data_ptr() for o in outs])
+    nn = (ctypes.c_int64 * max(k, 1))(*ns)
+    n_iter, path = ctypes.c_int32(0), ctypes.c_int32(0)
+    ell, rl = acc.compact if getattr(acc, 'compact', None) is not None else (None, None)
+    o = l + w
+    _native.check(_native.lib().sa_xt_fit_rate_interp_codes(
+        _ptr(acc.shot), _ptr(acc.goal), _ptr(acc.move), _ptr(acc.trans), l, w, float(eps),
+        int(max_iter), _native.SA_XT_SOLVE_EXACT if exact_order else 0, _ptr(mats), _ptr(heat),
+        ctypes.byref(n_iter), ctypes.byref(path), _ptr(ell), _ptr(rl), k, cp, nn, _ptr(axes[:l]),
+        _ptr(axes[l:o]), _ptr(axes[o:o + L]), L, _ptr(axes[o + L:]), W, op, _ptr(err), stream_handle()))
+    if n_iter.value < 0:
+        raise RuntimeError(f'xT value iteration did not converge within {max_iter} iterations')
+    p = _native.XT_SOLVE_PATHS[path.value]
+    _warn_solve_path(p)
+    sol = XTSolution(mats, None, heat[:n_iter.value + 1], n_iter.value, p)
+    return sol, [t[:n] for t, n in zip(outs, ns)], err
+
+
 XB_MAX_SETS = 24  # bucket sets one band-count launch takes (sa_xt_large.hip)
 
 

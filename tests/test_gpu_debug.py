@@ -107,3 +107,35 @@ def test_reordered_solve_barrier_timeout_exit():
     bit; switched off, the reordered path runs again with its own bits."""
     out = _run(['-c', ABORT], timeout=300)
     assert out.strip().endswith('ok')
+
+
+ABORT_FUSED = r"""
+import warnings
+import torch
+from socceraction_amd import _native, ops, synthetic, batch as B
+lib = _native.lib()
+assert lib.sa_debug_enabled() == 1
+ab = B.ActionBatch.from_columns(synthetic.spadl_games(60, game_id0=5))
+ic = [ops.xt_interp_codes_buffer(ab.n, ab.device)]
+acc = ops.xt_count_many([ab], 105, 68, interp_codes=ic, dense=False)
+sol = ops.xt_solve(acc, transition=False, exact_order=True)
+ref, _ = ops.xt_rate_interp_codes_many(ic, [ab.n], sol.mats[3].reshape(68, 105), 105, 68)
+_native.check(lib.sa_debug_xt_solve_abort(2))
+with warnings.catch_warnings(record=True) as wl:
+    warnings.simplefilter('always')
+    sol2, got, _ = ops.xt_fit_rate_interp_codes(acc, ic, [ab.n])
+_native.check(lib.sa_debug_xt_solve_abort(-1))
+assert sol2.path == 'timeout', sol2.path
+assert any('timed out' in str(w.message) for w in wl)
+assert sol2.n_iter == sol.n_iter > 3 and torch.equal(sol2.heatmaps, sol.heatmaps)
+assert torch.equal(got[0].view(torch.int64), ref[0].view(torch.int64))
+print('ok')
+"""
+
+
+def test_fused_fit_rate_after_a_barrier_timeout():
+    """sa_xt_fit_rate_interp_codes when the reordered solve aborts (forced at iteration 2): the
+    rate queued behind it ran over a half-written surface, the solve is redone in the
+    reference's order and the rate again -- rates and heatmaps equal the exact-order solve's."""
+    out = _run(['-c', ABORT_FUSED], timeout=300)
+    assert out.strip().endswith('ok')

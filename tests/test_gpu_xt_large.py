@@ -520,3 +520,33 @@ def test_cell_code_bucket_count_small_grid(sa):
                      (acc.trans, ref.trans)):
             assert torch.equal(a, b), (l, w)
         assert int(err.item()) == int(ref.err.item())
+
+
+@pytest.mark.parametrize('hot', [False, True])
+def test_fused_fit_rate_equals_solve_then_rate(sa, hot):
+    """sa_xt_fit_rate_interp_codes (the rate queued behind the one-launch solve, before its host
+    round trip) == xt_solve(transition=False) then xt_rate_interp_codes_many: iteration count,
+    path, matrices, heatmaps and every rate bit for bit; with an escaped count (hot) the solve
+    takes the reference's order after the speculative rate ran, and the rate is redone over the
+    rewritten surface."""
+    B, ops, syn = sa['batch'], sa['ops'], sa['synthetic']
+    ds = [syn.spadl_games(g, game_id0=41 * i + 7) for i, g in enumerate((120 if hot else 90, 37))]
+    if hot:  # one bin far above 65535 counts: the compact solve cannot take it
+        mv = np.isin(ds[0]['type_id'], (0, 1, 21))
+        ds[0]['start_x'][mv], ds[0]['start_y'][mv] = 52.2, 33.3
+        ds[0]['end_x'][mv], ds[0]['end_y'][mv] = 104.999, 0.0
+    bs = [B.ActionBatch.from_columns(d) for d in ds]
+    ns = [b.n for b in bs]
+    ic = [ops.xt_interp_codes_buffer(b.n, b.device) for b in bs]
+    acc = ops.xt_count_many(bs, 105, 68, interp_codes=ic, dense=hot)
+    sol = ops.xt_solve(acc, transition=False)
+    ref, ref_err = ops.xt_rate_interp_codes_many(ic, ns, sol.mats[3].reshape(68, 105), 105, 68)
+    sol2, got, err = ops.xt_fit_rate_interp_codes(acc, ic, ns)
+    assert sol2.path == sol.path == ('unavailable' if hot else 'reordered')
+    assert sol2.n_iter == sol.n_iter
+    assert torch.equal(sol2.mats, sol.mats) and torch.equal(sol2.heatmaps, sol.heatmaps)
+    for g, r in zip(got, ref):
+        assert torch.equal(g.view(torch.int64), r.view(torch.int64))  # NaN patterns included
+    assert int(err.item()) == int(ref_err.item())
+    with pytest.raises(ValueError):
+        ops.xt_fit_rate_interp_codes(ops.xt_count_many(bs, 16, 12), ic, ns)
