@@ -1397,6 +1397,14 @@ extern "C" int sa_xt_fit_rate_interp_codes(const int64_t* shot, const int64_t* g
                                            int32_t W, double* const* out, int32_t* err_flags, void* stream) {
   if (l < 1 || w < 1 || !mats || !path) return fail(SA_EINVAL, "bad l, w or null mats / path");
   if (l * w <= XT_SOLVE_MAX_C) return fail(SA_EINVAL, "the fused fit + rate is for grids above %d cells", XT_SOLVE_MAX_C);
+  // the rate's arguments checked before anything is launched (sa_xt_rate_interp_codes_many's own
+  // checks would first run behind the solve)
+  if (nsets < 0 || (nsets > 0 && (!interp_codes || !n || !out)) || !cx || !cy || !xs || !ys || L < 1 || W < 1 ||
+      l < 2 || w < 2 || (int64_t)L * W > INT32_MAX)
+    return fail(SA_EINVAL, "bad rate arguments");
+  for (int q = 0; q < nsets; ++q)
+    if (n[q] < 0 || (n[q] > 0 && (!interp_codes[q] || !out[q] || !aligned16(interp_codes[q]) || !aligned16(out[q]))))
+      return fail(SA_EINVAL, "set %d: bad count, codes or out", q);
   struct Rate {
     int32_t nsets;
     const uint64_t* const* codes;

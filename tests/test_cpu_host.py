@@ -119,6 +119,14 @@ def test_invalid_arguments_are_rejected_without_a_gpu():
     rc = lib.sa_xt_rate_interp_codes_many(-1, none_p, None, fake, fake, fake, 105, 68, fake, 1050,
                                           fake, 680, none_p, fake, None)
     assert rc == _native.SA_EINVAL
+    # round 6: the fused fit + rate checks its grid and the rate's arguments before launching
+    fit_rate = lambda l, w, nsets, L: lib.sa_xt_fit_rate_interp_codes(  # noqa: E731
+        fake, fake, fake, fake, l, w, 1e-5, 100, 0, fake, fake, ctypes.byref(n_iter),
+        ctypes.byref(path), fake, fake, nsets, none_p, None, fake, fake, fake, L, fake, 680, none_p,
+        fake, None)
+    assert fit_rate(16, 12, 0, 1050) == _native.SA_EINVAL and b'above' in lib.sa_last_error()
+    assert fit_rate(105, 68, -1, 1050) == _native.SA_EINVAL and b'rate' in lib.sa_last_error()
+    assert fit_rate(105, 68, 0, 0) == _native.SA_EINVAL and b'rate' in lib.sa_last_error()
 
 
 # ----------------------------------------------------------------------------- catalogue
