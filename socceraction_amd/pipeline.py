@@ -71,12 +71,14 @@ class _Slot:
 
 def value_frames(model, games: pd.DataFrame, actions: pd.DataFrame,
                  p_scores: Optional[np.ndarray] = None, p_concedes: Optional[np.ndarray] = None,
-                 chunk_rows: int = 1 << 18, timeline: Optional[list] = None, ramp=(4, 2)
-                 ) -> Tuple[pd.DataFrame, pd.DataFrame, Optional[pd.DataFrame]]:
+                 chunk_rows: int = 1 << 18, timeline: Optional[list] = None, ramp=(4, 2),
+                 labels: bool = True
+                 ) -> Tuple[pd.DataFrame, Optional[pd.DataFrame], Optional[pd.DataFrame]]:
     """(features, labels, values) of ``actions`` (each game's rows contiguous, ``games`` maps
     game_id -> home_team_id) for a VAEP / AtomicVAEP ``model`` whose transformers are all
     known ones.  ``values`` is None without probabilities (float32 or float64; values take
-    their dtype, the reference's rule)."""
+    their dtype, the reference's rule); ``labels=False``: features only (labels None; the
+    pipelined ``compute_features_batch``)."""
     t_call = time.perf_counter()
     known, unknown = model._split_xfns()
     if unknown:
@@ -95,10 +97,12 @@ def value_frames(model, games: pd.DataFrame, actions: pd.DataFrame,
     homes = home_map.reindex(seg_gid).to_numpy()
     lab = model._lab
     names = {lab.scores: 'scores', lab.concedes: 'concedes', lab.goal_from_shot: 'goal_from_shot'}
-    if not all(f in names for f in model.yfns):
+    if labels and not all(f in names for f in model.yfns):
         raise ValueError('the pipelined batch path takes the built-in label functions only')
     lrow = {'scores': 0, 'concedes': 1, 'goal_from_shot': 2}
     vdt = None
+    if p_scores is not None and not labels:
+        raise ValueError('values come with the labels pass (labels=True)')
     if p_scores is not None:
         ps = np.asarray(p_scores)
         pc = np.asarray(p_concedes)
@@ -116,7 +120,7 @@ def value_frames(model, games: pd.DataFrame, actions: pd.DataFrame,
     hb = _pinned((plan.n_bool, ld), torch.uint8)
     hf = _pinned((plan.n_f64, ld), torch.float64)
     hi = _pinned((plan.n_i64, ld), torch.int64)
-    hl = _pinned((3, ld), torch.uint8)
+    hl = _pinned((3, ld), torch.uint8) if labels else None
     hv = _pinned((3, ld), vdt) if vdt is not None else None
     cuts = _chunks(seg_off, chunk_rows, ramp=ramp) if n else []
     rmax = max((int(seg_off[s1] - seg_off[s0]) for s0, s1 in cuts), default=16)
@@ -153,11 +157,11 @@ def value_frames(model, games: pd.DataFrame, actions: pd.DataFrame,
                                slot.fb.i64_block)
         ops.features_into(ab.struct(), fb)
         lb = ops.LabelBlocks(m, slot.lab[0], slot.lab[1], slot.lab[2])
-        if vdt is not None:
+        if labels and vdt is not None:
             tps = torch.from_numpy(ps[r0:r1]).to(dev, non_blocking=True)
             tpc = torch.from_numpy(pc[r0:r1]).to(dev, non_blocking=True)
             ops.labels_formula(ab, tps, tpc, labels_out=lb, values_out=slot.val)
-        else:
+        elif labels:
             ops.labels(ab, out=lb)
         # 3. pitched copies into the frame's host blocks, on the copy stream
         ev = torch.cuda.Event()
@@ -169,7 +173,8 @@ def value_frames(model, games: pd.DataFrame, actions: pd.DataFrame,
         d2h(hb, slot.fb.bool_block[0], r0, m, plan.n_bool)
         d2h(hf, slot.fb.f64_block[0], r0, m, plan.n_f64)
         d2h(hi, slot.fb.i64_block[0], r0, m, plan.n_i64)
-        d2h(hl, slot.lab, r0, m, 3)
+        if labels:
+            d2h(hl, slot.lab, r0, m, 3)
         if vdt is not None:
             d2h(hv, slot.val, r0, m, 3)
         slot.done.record(copy)
@@ -189,12 +194,14 @@ def value_frames(model, games: pd.DataFrame, actions: pd.DataFrame,
         timeline.append({'host_total_ms': round((time.perf_counter() - t_start) * 1e3, 2)})
     t_frames = time.perf_counter()
     X = catalog.assemble_frame(plan, hb.numpy(), hf.numpy(), hi.numpy(), n, pd.RangeIndex(n))
-    hln = hl.numpy()  # numpy views keep their pinned tensors alive (so do the frames over them)
-    ycols = {}
-    for f in model.yfns:  # compute_labels' columns (atomic: goal_from_shot is named 'goal')
-        key = names[f]
-        ycols['goal' if (atomic and key == 'goal_from_shot') else key] = hln[lrow[key], :n].view(bool)
-    Y = pd.DataFrame(ycols, index=pd.RangeIndex(n), copy=False)  # views, as X (a copy: 5 ms)
+    Y = None
+    if labels:
+        hln = hl.numpy()  # numpy views keep their pinned tensors alive (so do the frames over them)
+        ycols = {}
+        for f in model.yfns:  # compute_labels' columns (atomic: goal_from_shot is named 'goal')
+            key = names[f]
+            ycols['goal' if (atomic and key == 'goal_from_shot') else key] = hln[lrow[key], :n].view(bool)
+        Y = pd.DataFrame(ycols, index=pd.RangeIndex(n), copy=False)  # views, as X (a copy: 5 ms)
     V = None
     if vdt is not None:
         hvn = hv.numpy()

@@ -129,12 +129,19 @@ class VAEP:
         return self._features_frame(ab, game_actions, [home], [(0, len(game_actions))])
 
     def compute_features_batch(self, games: pd.DataFrame, actions: pd.DataFrame) -> pd.DataFrame:
-        """Features of many games at once (one kernel launch).
+        """Features of many games at once.
 
         ``actions`` holds the games' actions with each game's rows contiguous;
         ``games`` maps ``game_id -> home_team_id``. Equals ``pd.concat`` of the per-game
-        :meth:`compute_features` outputs with ``ignore_index=True``.
+        :meth:`compute_features` outputs with ``ignore_index=True``.  With built-in
+        transformers only, the pipelined path of :meth:`compute_batch` (features only); with a
+        user transformer, one launch for the known ones and the host for the rest.
         """
+        if len(actions) and not self._split_xfns()[1]:
+            # every transformer a known one: the pipelined path (game-aligned chunks, copies out
+            # overlapping the next chunk's encode; socceraction_amd.pipeline), the same frame
+            from ..pipeline import value_frames
+            return value_frames(self, games, actions, labels=False)[0]
         home_of = games.set_index('game_id')['home_team_id']
         ab = ActionBatch.from_frame(actions, atomic=self._atomic, home_team_id=home_of,
                                     segments='game')

@@ -206,7 +206,11 @@ def test_pipelined_compute_batch_equals_separate_calls(atomic):
     games = synthetic.games_frame(d)
     model = Model()
     model.yfns = model.yfns + [model._lab.goal_from_shot]
-    X = model.compute_features_batch(games, actions)
+    # the reference frame from the per-game calls (compute_features_batch itself now takes the
+    # pipelined path, features only: it must equal them too)
+    X = pd.concat([model.compute_features(g, actions[actions['game_id'] == g.game_id].reset_index(drop=True))
+                   for g in games.itertuples()], ignore_index=True)
+    pd.testing.assert_frame_equal(model.compute_features_batch(games, actions), X)
     Y = model.compute_labels_batch(games, actions)
     n = len(actions)
     p = synthetic.probabilities(n)
